@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST DDP training samples/sec on MI355X.
+
+Metric/config from BASELINE.json: the reference's MNIST DDP workload
+(jiaqianjing/pytorch-operator examples/mnist/mnist.py -- Net, batch 64 per rank,
+SGD(lr=0.01, momentum=0.5), fp32, every rank iterating its own data, gradients
+averaged by DDP all-reduce) on 1/2/4/8 MI355X, one process per GPU over RCCL.
+
+Each timed step is a complete training step: batch gather + normalisation,
+forward, NLL loss, backward, gradient all-reduce (world > 1) and the SGD update.
+Data is synthetic (a learnable MNIST-shaped dataset resident in HBM), weights are
+random-init (torch.manual_seed + the reference's default init).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--kernels hip|torch]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+
+Rank 0 prints ONE JSON line.  ``value`` is the whole-job samples/s (sum over
+ranks), timed as the MAX over ranks of K steps bracketed by barrier+synchronize.
+``vs_baseline`` divides by 210 samples/s/rank x N: the reference's derived
+per-rank throughput (>= 210 samples/s/rank, 420 aggregate at 2 ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_PER_RANK = 210.0
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--kernels", choices=["hip", "torch"], default="hip")
+    p.add_argument("--mode", choices=["eager", "graph", "graph-comm"], default="graph")
+    p.add_argument("--steps-per-graph", type=int, default=0,
+                   help="whole steps per hipGraph replay (world 1 only; 0 = auto)")
+    p.add_argument("--dataset-size", type=int, default=60000)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pytorch_operator_amd.parallel.dist import init_from_env
+
+    env = init_from_env("nccl", use_gpu=True)
+    world, rank, dev = env.world_size, env.rank, env.device
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
+                  file=sys.stderr)
+    B = args.batch_size
+
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    ds = make_synthetic_mnist(args.dataset_size, seed=1 + rank, device=dev)
+
+    if args.kernels == "hip":
+        from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+        from pytorch_operator_amd.ops import mnist as K
+        from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
+        from pytorch_operator_amd.parallel.graphed_step import GraphedStep
+        cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
+        sync = FlatGradAllReduce() if world > 1 else None
+        tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
+                               seed=1, grad_sync=sync)
+        if world > 1:  # DDP constructor semantics: start from rank 0's parameters
+            dist.broadcast(tr.flat_params, 0)
+        spg = args.steps_per_graph
+        if spg <= 0:
+            spg = 1
+            if world == 1 or args.mode == "graph-comm":
+                for cand in (10, 8, 5, 4, 2):
+                    if args.steps % cand == 0 and args.warmup % cand == 0:
+                        spg = cand
+                        break
+        if world > 1 and args.mode == "graph":
+            spg = 1
+        eager_w = min(args.warmup, 3)
+        for _ in range(eager_w):
+            tr.train_step()  # eager warmup: loads the library, initialises momentum
+        runner = GraphedStep(tr, mode=args.mode, steps_per_graph=spg)
+        rest = max(0, args.warmup - eager_w - runner.internal_steps)
+        rest -= rest % runner.steps_per_graph
+        runner.run(rest)
+
+        def run(n):
+            runner.run(n)
+        steps = args.steps - args.steps % runner.steps_per_graph
+        mode_desc = f"{args.mode}(spg={runner.steps_per_graph})"
+    else:
+        from pytorch_operator_amd.models.mnist import Net
+        import torch.nn.functional as F
+        torch.manual_seed(1)
+        model = Net().to(dev)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+        opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.5)
+        xf = ds.float_images()
+        lab = ds.labels.long()
+        state = {"i": 0}
+
+        def run(n):
+            for _ in range(n):
+                i = state["i"]
+                idx = ds.perm[(i * B) % ds.n: (i * B) % ds.n + B].long()
+                state["i"] = i + 1
+                opt.zero_grad(set_to_none=True)
+                loss = F.nll_loss(model(xf[idx]), lab[idx])
+                loss.backward()
+                opt.step()
+        run(args.warmup)
+        steps = args.steps
+        mode_desc = "torch-eager"
+
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    samples = steps * B * world
+    value = samples / dt
+    result = {
+        "metric": "mnist_ddp_train_samples_per_sec",
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (BASELINE_PER_RANK * world), 1),
+        "dtype": "fp32",
+        "data": "synthetic (learnable MNIST-shaped uint8 images in HBM), random-init weights",
+        "config": {
+            "model": "mnist-cnn (reference examples/mnist/mnist.py Net: conv20-conv50-fc500-fc10)",
+            "global_batch": B * world,
+            "per_rank_batch": B,
+            "seq_len": None,
+            "parallelism": f"dp{world}",
+            "optimizer": "SGD(lr=0.01, momentum=0.5)",
+            "kernels": args.kernels,
+            "exec": mode_desc,
+            "backend": "rccl" if world > 1 else "none",
+        },
+    }
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

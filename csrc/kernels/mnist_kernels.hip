@@ -1,0 +1,764 @@
+// Hand-written CDNA4 (gfx950) kernels for the MNIST DDP training step of the
+// reference workload (jiaqianjing/pytorch-operator examples/mnist/mnist.py:17-43):
+//
+//   conv1(1->20,k5) -> ReLU -> maxpool2 -> conv2(20->50,k5) -> ReLU -> maxpool2
+//   -> fc1(800->500) -> ReLU -> fc2(500->10) -> log_softmax -> nll_loss(mean)
+//
+// The whole step is 6 launches (+1 fused SGD launch, +RCCL all-reduce when
+// world_size > 1).  The step is launch/latency bound (~0.84 GFLOP at B=64), so
+// the design goal is few, fused, fully-occupied launches that a hipGraph can
+// replay back to back:
+//
+//   A conv1_fwd_pool   uint8 gather + Normalize + conv1 + bias + ReLU + pool(argmax)
+//                      (+ zero-fill of the atomically-accumulated grad segment)
+//   B conv2_fwd_pool   implicit GEMM on v_mfma_f32_16x16x4_f32, LDS-staged im2col,
+//                      bias + ReLU + 2x2 max-pool fused in the accumulator epilogue
+//   C fc1_fwd          MFMA GEMM, K split over the 8 waves of a workgroup, LDS
+//                      reduction, bias + ReLU epilogue
+//   D head             fc2 + log_softmax + NLL + d(logits) + fc2^T GEMV + ReLU mask
+//   E fc1_bwd          dW_fc1 / db_fc1 (MFMA), dX_fc1 (MFMA) with un-pool + ReLU
+//                      mask epilogue, dW_fc2 / db_fc2
+//   F conv_bwd         per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
+//                      dW_conv2 (MFMA, im2col from LDS), col2im + un-pool + ReLU
+//                      mask -> dz1 (LDS), dW_conv1 (MFMA), db_conv1/db_conv2
+//   H sgd_momentum     multi-tensor SGD(momentum) over the flat parameter buffer
+//
+// All arithmetic is fp32 (the reference's dtype); matrix work uses the exact-fp32
+// MFMA (one rounding per product, same as an fmaf chain).
+#include "pto_common.h"
+
+using namespace pto;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// A: conv1 forward (+bias, ReLU, 2x2 max-pool with argmax).  One thread per
+// pooled output (B*20*144 threads); a 256-thread block spans at most two
+// samples, whose normalised images are staged in LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
+    BatchSrc src, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ a1, uint8_t* __restrict__ idx1, int B,
+    float* __restrict__ zero_ptr, int zero_n) {
+  __shared__ float img[2][784];
+  __shared__ float ws[500];
+  __shared__ float bs[20];
+  const int tid = threadIdx.x;
+  if (zero_ptr != nullptr) {
+    for (int i = blockIdx.x * 256 + tid; i < zero_n; i += gridDim.x * 256) zero_ptr[i] = 0.f;
+  }
+  const int item0 = blockIdx.x * 256;
+  const int total = B * 2880;
+  const int b0 = item0 / 2880;
+  const int b1 = min((item0 + 255) / 2880, B - 1);
+  const int nb = b1 - b0 + 1;
+  for (int e = tid; e < nb * 784; e += 256) {
+    const int s = e / 784, p = e - s * 784;
+    img[s][p] = load_px(src, batch_row(src, b0 + s, B), p);
+  }
+  for (int e = tid; e < 500; e += 256) ws[e] = w[e];
+  if (tid < 20) bs[tid] = bias[tid];
+  __syncthreads();
+
+  const int item = item0 + tid;
+  if (item >= total) return;
+  const int b = item / 2880;
+  const int rem = item - b * 2880;
+  const int c = rem / 144;
+  const int p = rem - c * 144;
+  const int ph = p / 12, pw = p - ph * 12;
+  const float* im = &img[b - b0][(2 * ph) * 28 + 2 * pw];
+  float patch[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) patch[r][q] = im[r * 28 + q];
+  const float* wc = ws + c * 25;
+  float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const float wv = wc[kh * 5 + kw];
+      o00 = fmaf(patch[kh][kw], wv, o00);
+      o01 = fmaf(patch[kh][kw + 1], wv, o01);
+      o10 = fmaf(patch[kh + 1][kw], wv, o10);
+      o11 = fmaf(patch[kh + 1][kw + 1], wv, o11);
+    }
+  const float bc = bs[c];
+  o00 += bc; o01 += bc; o10 += bc; o11 += bc;
+  // torch max_pool2d scans (0,0),(0,1),(1,0),(1,1) and keeps the first maximum.
+  float m = o00; int am = 0;
+  if (o01 > m) { m = o01; am = 1; }
+  if (o10 > m) { m = o10; am = 2; }
+  if (o11 > m) { m = o11; am = 3; }
+  a1[item] = fmaxf(m, 0.f);
+  idx1[item] = (uint8_t)am;
+}
+
+// ---------------------------------------------------------------------------
+// B: conv2 forward as an implicit GEMM on fp32 MFMA.
+//   grid = (4 output-channel groups of 16, B samples), 4 waves per block.
+//   wave w owns conv rows {2w, 2w+1} x 8 cols = 16 positions (M) x 16 channels (N);
+//   K = 500 = (20 in-ch x 25 taps) is walked as 125 MFMA steps.  Lane group
+//   g = lane>>4 owns input channels {g, g+4, .., g+16}, which makes every LDS
+//   offset of the unrolled loop a compile-time immediate.
+//   LDS row strides are chosen for conflict-free ds_read_b32:
+//     image: row stride 16, channel stride 200 (== 8 mod 32)
+//     weights: row stride 514 (== 2 mod 32, lane groups differ by 25 -> odd banks)
+//   The 2x2 pool window = 2 registers of this lane x 2 registers of lane^32.
+// ---------------------------------------------------------------------------
+constexpr int C2_RS = 16;
+constexpr int C2_CS = 200;
+constexpr int C2_WS = 514;
+
+__global__ __launch_bounds__(256) void conv2_fwd_pool_kernel(
+    const float* __restrict__ a1, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B) {
+  __shared__ float in_s[20 * C2_CS];
+  __shared__ float w_s[16 * C2_WS];
+  const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const float* src = a1 + (size_t)b * 2880;
+  for (int e = tid; e < 2880; e += 256) {
+    const int c = e / 144, p = e - c * 144;
+    const int y = p / 12, x = p - y * 12;
+    in_s[c * C2_CS + y * C2_RS + x] = src[e];
+  }
+  for (int e = tid; e < 16 * 125; e += 256) {
+    const int j = e / 125, q = e - j * 125;
+    const int co = cg * 16 + j;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (co < 50) v = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
+    float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
+    d[0] = make_float2(v.x, v.y);
+    d[1] = make_float2(v.z, v.w);
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int oh = 2 * wv + (i >> 3), ow = i & 7;
+  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
+  const float* Bb = w_s + i * C2_WS + g * 25;
+  f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int cj = 0; cj < 5; ++cj)
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const float av = Ab[cj * 4 * C2_CS + kh * C2_RS + kw];
+        const float bv = Bb[cj * 100 + kh * 5 + kw];
+        if (((cj * 25 + kh * 5 + kw) & 1) == 0) acc0 = mfma16x16x4(av, bv, acc0);
+        else acc1 = mfma16x16x4(av, bv, acc1);
+      }
+  const f32x4 acc = acc0 + acc1;
+  const int co = cg * 16 + i;
+  const float bco = (co < 50) ? bias[co] : 0.f;
+  // reg r of this lane = conv position (oh = 2wv + (g>>1), ow = 4(g&1) + r)
+  const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
+  float mA = v0; int aA = 0;
+  if (v1 > mA) { mA = v1; aA = 1; }
+  float mB = v2; int aB = 0;
+  if (v3 > mB) { mB = v3; aB = 1; }
+  const float pA = __shfl_xor(mA, 32, 64);
+  const int paA = __shfl_xor(aA, 32, 64);
+  const float pB = __shfl_xor(mB, 32, 64);
+  const int paB = __shfl_xor(aB, 32, 64);
+  if (g < 2 && co < 50) {  // top row of the window; partner lane holds the bottom row
+    if (pA > mA) { mA = pA; aA = 2 + paA; }
+    if (pB > mB) { mB = pB; aB = 2 + paB; }
+    const size_t o = (size_t)b * 800 + co * 16 + wv * 4 + 2 * (g & 1);
+    a2[o] = fmaxf(mA, 0.f);
+    a2[o + 1] = fmaxf(mB, 0.f);
+    idx2[o] = (uint8_t)aA;
+    idx2[o + 1] = (uint8_t)aB;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C: fc1 forward: h = relu(x[B,800] . W[500,800]^T + b).
+//   grid = (32 N-tiles, ceil(B/16) M-tiles), 8 waves; wave w reduces K range
+//   [100w, 100w+100) (lane group g owns k = 100w + 25g + s), partial tiles are
+//   summed through LDS and the bias+ReLU epilogue is applied once.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void fc1_fwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ h, int B) {
+  __shared__ f32x4 red[8][64];
+  const int nt = blockIdx.x, mt = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int row = mt * 16 + i, col = nt * 16 + i;
+  const bool rv = row < B, cv = col < 500;
+  const int k0 = wv * 100 + g * 25;
+  const float* xa = x + (size_t)(rv ? row : B - 1) * 800 + k0;
+  const float* wb = w + (size_t)(cv ? col : 499) * 800 + k0;
+  float av[25], bv[25];
+#pragma unroll
+  for (int s = 0; s < 25; ++s) { av[s] = xa[s]; bv[s] = wb[s]; }
+  f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+  for (int s = 0; s < 25; ++s) {
+    const float a = rv ? av[s] : 0.f;
+    const float bb = cv ? bv[s] : 0.f;
+    if (s & 1) c1 = mfma16x16x4(a, bb, c1);
+    else c0 = mfma16x16x4(a, bb, c0);
+  }
+  red[wv][lane] = c0 + c1;
+  __syncthreads();
+  if (tid < 256) {
+    const int l = tid >> 2, r = tid & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[q][l][r];
+    const int orow = mt * 16 + (l >> 4) * 4 + r, ocol = nt * 16 + (l & 15);
+    if (orow < B && ocol < 500) h[(size_t)orow * 500 + ocol] = fmaxf(s + bias[ocol], 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// D: head.  One wave per sample: logits = h.W2^T + b2, log_softmax, NLL,
+// d(logits) = (softmax - onehot) * grad_scale, dh = (d(logits).W2) * (h > 0).
+// stats[0] += loss * loss_scale, stats[1] += (argmax == target).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void head_kernel(
+    const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
+    BatchSrc src, int B, float grad_scale, float loss_scale,
+    float* __restrict__ dlogits, float* __restrict__ dh, float* __restrict__ logp_out,
+    float* __restrict__ stats) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int b = blockIdx.x * 4 + (tid >> 6);
+  if (b >= B) return;  // whole wave exits together; the kernel has no barrier
+  float hv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = lane + 64 * q;
+    hv[q] = (k < 500) ? h[(size_t)b * 500 + k] : 0.f;
+  }
+  float logit[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    float p = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = lane + 64 * q;
+      if (k < 500) p = fmaf(hv[q], w2[j * 500 + k], p);
+    }
+    logit[j] = wave_sum(p) + b2[j];
+  }
+  float m = logit[0];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) m = fmaxf(m, logit[j]);
+  float se = 0.f;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) se += __expf(logit[j] - m);
+  const float lse = m + __logf(se);
+  const int t = src.labels[batch_row(src, b, B)];
+  float lt = 0.f;
+  int pred = 0;
+  float best = logit[0];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    if (j == t) lt = logit[j];
+    if (logit[j] > best) { best = logit[j]; pred = j; }
+  }
+  if (lane == 0 && stats != nullptr) {
+    atomicAdd(&stats[0], (lse - lt) * loss_scale);
+    atomicAdd(&stats[1], pred == t ? 1.f : 0.f);
+  }
+  if (logp_out != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (lane == j) logp_out[(size_t)b * 10 + j] = logit[j] - lse;
+  }
+  if (dh == nullptr) return;
+  float dl[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) dl[j] = (__expf(logit[j] - lse) - (j == t ? 1.f : 0.f)) * grad_scale;
+  if (dlogits != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (lane == j) dlogits[(size_t)b * 10 + j] = dl[j];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = lane + 64 * q;
+    if (k < 500) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) s = fmaf(dl[j], w2[j * 500 + k], s);
+      dh[(size_t)b * 500 + k] = hv[q] > 0.f ? s : 0.f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// E: fc1 backward, three independent jobs in one launch (blockDim 256):
+//   job 1 (400 blocks x 4 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B),
+//          db_fc1 from the kt==0 tiles.  Written, not accumulated: no zeroing needed.
+//   job 2 (ceil(B/16)*50 blocks): da2[B,800] = dh . W_fc1 (K = 500 split over 4
+//          waves + LDS reduce), epilogue un-pools through idx2 and applies the
+//          ReLU mask, writing the full dz2[B,50,8,8] (pre-pool conv2 grad).
+//   job 3 (20 blocks): dW_fc2[10,500] = dlogits^T . h, db_fc2.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fc1_bwd_kernel(
+    const float* __restrict__ dh, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
+    const float* __restrict__ w1, const float* __restrict__ dlog, const float* __restrict__ h,
+    float* __restrict__ gw1, float* __restrict__ gb1, float* __restrict__ gw2,
+    float* __restrict__ gb2, float* __restrict__ dz2, int B) {
+  __shared__ f32x4 red[4][64];
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  constexpr int nJ1 = 400;
+  const int nJ2 = ((B + 15) / 16) * 50;
+  if (blk < nJ1) {
+    const int tile = blk * 4 + wv;
+    const int nt = tile / 50, kt = tile - nt * 50;
+    const int n = nt * 16 + i, f = kt * 16 + i;
+    const bool nv = n < 500;
+    const int nc = nv ? n : 499;
+    f32x4 c0 = zero4(), c1 = zero4();
+    const int nsteps = (B + 3) / 4;
+    for (int s = 0; s < nsteps; s += 2) {
+      {
+        const int bb = 4 * s + g;
+        const bool bv = bb < B;
+        const int bc = bv ? bb : B - 1;
+        const float av = dh[(size_t)bc * 500 + nc];
+        const float fv = a2[(size_t)bc * 800 + f];
+        c0 = mfma16x16x4((bv && nv) ? av : 0.f, bv ? fv : 0.f, c0);
+      }
+      if (s + 1 < nsteps) {
+        const int bb = 4 * (s + 1) + g;
+        const bool bv = bb < B;
+        const int bc = bv ? bb : B - 1;
+        const float av = dh[(size_t)bc * 500 + nc];
+        const float fv = a2[(size_t)bc * 800 + f];
+        c1 = mfma16x16x4((bv && nv) ? av : 0.f, bv ? fv : 0.f, c1);
+      }
+    }
+    const f32x4 c = c0 + c1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int nn = nt * 16 + g * 4 + r;
+      if (nn < 500) gw1[(size_t)nn * 800 + kt * 16 + i] = c[r];
+    }
+    if (kt == 0) {
+      float s = 0.f;
+      for (int bb = g; bb < B; bb += 4) s += dh[(size_t)bb * 500 + nc];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (g == 0 && nv) gb1[n] = s;
+    }
+  } else if (blk < nJ1 + nJ2) {
+    const int t2 = blk - nJ1;
+    const int mt = t2 / 50, kt = t2 - mt * 50;
+    const int row = mt * 16 + i;
+    const bool rv = row < B;
+    const int rc = rv ? row : B - 1;
+    const int f = kt * 16 + i;
+    const int s0 = wv * 32, s1 = min(125, s0 + 32);
+    f32x4 c0 = zero4(), c1 = zero4();
+    for (int s = s0; s < s1; s += 2) {
+      {
+        const int k = 4 * s + g;
+        const float av = dh[(size_t)rc * 500 + k];
+        const float bv = w1[(size_t)k * 800 + f];
+        c0 = mfma16x16x4(rv ? av : 0.f, bv, c0);
+      }
+      if (s + 1 < s1) {
+        const int k = 4 * (s + 1) + g;
+        const float av = dh[(size_t)rc * 500 + k];
+        const float bv = w1[(size_t)k * 800 + f];
+        c1 = mfma16x16x4(rv ? av : 0.f, bv, c1);
+      }
+    }
+    red[wv][lane] = c0 + c1;
+    __syncthreads();
+    const int l = tid >> 2, r = tid & 3;
+    const float v = red[0][l][r] + red[1][l][r] + red[2][l][r] + red[3][l][r];
+    const int bs = mt * 16 + (l >> 4) * 4 + r;
+    const int ff = kt * 16 + (l & 15);
+    if (bs < B) {
+      const size_t o = (size_t)bs * 800 + ff;
+      const float d = a2[o] > 0.f ? v : 0.f;
+      const int p = idx2[o];
+      const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
+      float* z = dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+      z[0] = p == 0 ? d : 0.f;
+      z[1] = p == 1 ? d : 0.f;
+      z[8] = p == 2 ? d : 0.f;
+      z[9] = p == 3 ? d : 0.f;
+    }
+  } else {
+    const int blk3 = blk - nJ1 - nJ2;
+    const int e = blk3 * 256 + tid;
+    if (e < 5000) {
+      const int j = e / 500, k = e - j * 500;
+      float s = 0.f;
+      for (int bb = 0; bb < B; ++bb) s = fmaf(dlog[(size_t)bb * 10 + j], h[(size_t)bb * 500 + k], s);
+      gw2[e] = s;
+    }
+    if (blk3 == 0 && tid < 10) {
+      float s = 0.f;
+      for (int bb = 0; bb < B; ++bb) s += dlog[(size_t)bb * 10 + tid];
+      gb2[tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// F: conv backward.  grid = (4 input-channel groups of 5, B samples), 8 waves.
+//   phase 2a  dcol[64 pos, 125 (ci,kh,kw)] = dz2[b]^T . W2[:, group]   (MFMA, K = 50)
+//   phase 2b  dW_conv2[50, group] += dz2[b] . im2col(a1[b])             (MFMA, K = 64)
+//   phase 3   da1 = col2im(dcol); un-pool via idx1 + ReLU mask -> dz1 (LDS)
+//   phase 4   dW_conv1[group, 25] += dz1 . im2col(x[b])                 (MFMA, K = 576)
+//   conv grads are accumulated with fp32 atomics into a segment that launch A zeroed.
+// ---------------------------------------------------------------------------
+constexpr int F_DS = 66;    // dz_s  [64 co][66]   (== 2 mod 32)
+constexpr int F_DT = 66;    // dzT_s [64 pos][66]
+constexpr int F_WS = 144;   // w_s   [52 co][144]  (== 16 mod 32)
+constexpr int F_DC = 132;   // dcol  [64 pos][132] (4*132 == 16 mod 32)
+constexpr int F_Z1 = 580;   // dz1_s [5][580]      (== 4 mod 32)
+constexpr int F_OFF_DZ = 0;
+constexpr int F_OFF_DZT = F_OFF_DZ + 64 * F_DS;
+constexpr int F_OFF_W = F_OFF_DZT + 64 * F_DT;
+constexpr int F_OFF_DCOL = F_OFF_W + 52 * F_WS;
+constexpr int F_OFF_A1 = F_OFF_DCOL + 64 * F_DC;
+constexpr int F_OFF_X = F_OFF_A1 + 5 * 144;
+constexpr int F_LDS = F_OFF_X + 784;
+// aliases of the (dead after phase 2a) weight region:
+constexpr int F_OFF_DZ1 = F_OFF_W;
+constexpr int F_OFF_RED = F_OFF_W + 5 * F_Z1;
+static_assert(5 * F_Z1 + 8 * 256 <= 52 * F_WS, "alias region too small");
+
+__global__ __launch_bounds__(512) void conv_bwd_kernel(
+    const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, BatchSrc src, float* __restrict__ gw2,
+    float* __restrict__ gb2, float* __restrict__ gw1, float* __restrict__ gb1,
+    float* __restrict__ dz1_out, int B) {
+  extern __shared__ float lds[];
+  float* dz_s = lds + F_OFF_DZ;
+  float* dzT_s = lds + F_OFF_DZT;
+  float* w_s = lds + F_OFF_W;
+  float* dcol_s = lds + F_OFF_DCOL;
+  float* a1_s = lds + F_OFF_A1;
+  float* x_s = lds + F_OFF_X;
+  float* dz1_s = lds + F_OFF_DZ1;
+  float* red = lds + F_OFF_RED;
+
+  const int cig = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+
+  // ---- phase 1: stage
+  const float* dzb = dz2 + (size_t)b * 3200;
+  for (int e = tid; e < 64 * 64; e += 512) {
+    const int co = e >> 6, pos = e & 63;
+    const float v = co < 50 ? dzb[e] : 0.f;
+    dz_s[co * F_DS + pos] = v;
+    dzT_s[pos * F_DT + co] = v;
+  }
+  for (int e = tid; e < 52 * 128; e += 512) {
+    const int co = e >> 7, j = e & 127;
+    w_s[co * F_WS + j] = (co < 50 && j < 125) ? w2[(size_t)co * 500 + cig * 125 + j] : 0.f;
+  }
+  for (int e = tid; e < 720; e += 512) a1_s[e] = a1[(size_t)b * 2880 + cig * 720 + e];
+  {
+    const int row = batch_row(src, b, B);
+    for (int e = tid; e < 784; e += 512) x_s[e] = load_px(src, row, e);
+  }
+  __syncthreads();
+
+  // ---- phase 2a: dcol = dz2^T . W2 slice   (M = 64 pos, N = 128, K = 52)
+  {
+    const int mt = wv & 3, nt0 = (wv >> 2) * 4;
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      const float av = dzT_s[(mt * 16 + i) * F_DT + 4 * s + g];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const float bv = w_s[(4 * s + g) * F_WS + (nt0 + n) * 16 + i];
+        acc[n] = mfma16x16x4(av, bv, acc[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dcol_s[(mt * 16 + g * 4 + r) * F_DC + (nt0 + n) * 16 + i] = acc[n][r];
+  }
+  // ---- phase 2b: dW_conv2 partial  (M = 64 co, N = 128 (ci,kh,kw), K = 64 pos)
+  {
+    const int mt = wv & 3, nt0 = (wv >> 2) * 4;
+    int boff[4];
+    bool jv[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int j = (nt0 + n) * 16 + i;
+      jv[n] = j < 125;
+      const int jc = jv[n] ? j : 124;
+      const int ci = jc / 25, t = jc - ci * 25;
+      boff[n] = ci * 144 + (t / 5) * 12 + (t % 5);
+    }
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float av = dz_s[(mt * 16 + i) * F_DS + 4 * s + g];
+      const int poff = (s >> 1) * 12 + 4 * (s & 1) + g;  // pos = 4s+g -> (oh, ow)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const float bv = jv[n] ? a1_s[boff[n] + poff] : 0.f;
+        acc[n] = mfma16x16x4(av, bv, acc[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int j = (nt0 + n) * 16 + i;
+      if (j < 125) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = mt * 16 + g * 4 + r;
+          if (co < 50) atomicAdd(&gw2[(size_t)co * 500 + cig * 125 + j], acc[n][r]);
+        }
+      }
+    }
+  }
+  if (cig == 0 && tid < 50) {
+    float s = 0.f;
+    for (int p = 0; p < 64; ++p) s += dz_s[tid * F_DS + p];
+    atomicAdd(&gb2[tid], s);
+  }
+  __syncthreads();
+
+  // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]
+  for (int e = tid; e < 720; e += 512) {
+    const int c = e / 144, p = e - c * 144;
+    const int y = p / 12, x = p - y * 12;
+    float da = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      const int oy = y - kh;
+      if (oy < 0 || oy > 7) continue;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const int ox = x - kw;
+        if (ox < 0 || ox > 7) continue;
+        da += dcol_s[(oy * 8 + ox) * F_DC + c * 25 + kh * 5 + kw];
+      }
+    }
+    const float d = a1_s[e] > 0.f ? da : 0.f;
+    const int pidx = idx1[(size_t)b * 2880 + cig * 720 + e];
+    float* z = dz1_s + c * F_Z1 + (2 * y) * 24 + 2 * x;
+    z[0] = pidx == 0 ? d : 0.f;
+    z[1] = pidx == 1 ? d : 0.f;
+    z[24] = pidx == 2 ? d : 0.f;
+    z[25] = pidx == 3 ? d : 0.f;
+    if (dz1_out != nullptr) {
+      float* zo = dz1_out + (size_t)b * 11520 + (cig * 5 + c) * 576 + (2 * y) * 24 + 2 * x;
+      zo[0] = z[0]; zo[1] = z[1]; zo[24] = z[24]; zo[25] = z[25];
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 4: dW_conv1 partial (M = 16 (5 valid ch), N = 32 (25 taps), K = 576)
+  {
+    const int nt = wv & 1, kq = wv >> 1;
+    const int t = nt * 16 + i;
+    const bool tv = t < 25;
+    const int tc = tv ? t : 24;
+    const int xoff = (tc / 5) * 28 + (tc % 5);
+    const bool cv = i < 5;
+    const float* arow = dz1_s + (cv ? i : 4) * F_Z1;
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy) {
+      const int y = kq * 6 + yy;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int x = 4 * q + g;
+        const float av = cv ? arow[y * 24 + x] : 0.f;
+        const float bv = tv ? x_s[y * 28 + x + xoff] : 0.f;
+        if (q & 1) c1 = mfma16x16x4(av, bv, c1);
+        else c0 = mfma16x16x4(av, bv, c0);
+      }
+    }
+    reinterpret_cast<f32x4*>(red)[wv * 64 + lane] = c0 + c1;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    // lane l of ntile nt, reg r: channel row = (l>>4)*4 + r, tap col = nt*16 + (l&15)
+    const int nt = tid >> 6, l = tid & 63;
+    const f32x4* rv4 = reinterpret_cast<const f32x4*>(red);
+    const f32x4 s = rv4[(0 * 2 + nt) * 64 + l] + rv4[(1 * 2 + nt) * 64 + l] +
+                    rv4[(2 * 2 + nt) * 64 + l] + rv4[(3 * 2 + nt) * 64 + l];
+    const int tt = nt * 16 + (l & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = (l >> 4) * 4 + r;
+      if (c < 5 && tt < 25) atomicAdd(&gw1[(cig * 5 + c) * 25 + tt], s[r]);
+    }
+  } else if (tid >= 128 && tid < 128 + 5 * 64) {
+    const int c = (tid - 128) >> 6, l = tid & 63;
+    float s = 0.f;
+    for (int p = l; p < 576; p += 64) s += dz1_s[c * F_Z1 + p];
+    s = wave_sum(s);
+    if (l == 0) atomicAdd(&gb1[cig * 5 + c], s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// H: SGD with momentum over a flat fp32 buffer (torch.optim.SGD semantics:
+// buf = momentum*buf + (1-dampening)*g (buf = g on the first step),
+// p -= lr * (nesterov ? g + momentum*buf : buf)); grad_scale folds the DDP 1/world.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgd_momentum_kernel(
+    float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ buf, long n,
+    float lr, float momentum, float dampening, float wd, float grad_scale, int nesterov,
+    int first_step, int* __restrict__ step_counter) {
+  const long n4 = n >> 2;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < n4 + 4; v += stride) {
+    // vector body + scalar tail (the last 4 "virtual" slots cover n % 4 elements)
+    long lo, hi;
+    if (v < n4) { lo = v * 4; hi = lo + 4; }
+    else { lo = n4 * 4 + (v - n4); hi = lo + 1; if (lo >= n) continue; }
+    if (hi - lo == 4) {
+      float4 pp = reinterpret_cast<float4*>(p)[v];
+      const float4 gg = reinterpret_cast<const float4*>(gr)[v];
+      float4 bb = reinterpret_cast<float4*>(buf)[v];
+      float* pe = &pp.x; const float* ge = &gg.x; float* be = &bb.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float d = ge[e] * grad_scale + wd * pe[e];
+        if (momentum != 0.f) {
+          be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
+          d = nesterov ? d + momentum * be[e] : be[e];
+        }
+        pe[e] -= lr * d;
+      }
+      reinterpret_cast<float4*>(p)[v] = pp;
+      reinterpret_cast<float4*>(buf)[v] = bb;
+    } else {
+      float d = gr[lo] * grad_scale + wd * p[lo];
+      if (momentum != 0.f) {
+        buf[lo] = first_step ? d : momentum * buf[lo] + (1.f - dampening) * d;
+        d = nesterov ? d + momentum * buf[lo] : buf[lo];
+      }
+      p[lo] -= lr * d;
+    }
+  }
+  if (step_counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(step_counter, 1);
+}
+
+inline BatchSrc make_src(const void* x, int is_u8, const int* labels, const int* perm,
+                         const int* cursor, int host_offset, int n_total, float scale,
+                         float shift) {
+  BatchSrc s;
+  s.x = x; s.labels = labels; s.perm = perm; s.cursor = cursor; s.host_offset = host_offset;
+  s.n_total = n_total; s.is_u8 = is_u8; s.scale = scale; s.shift = shift;
+  return s;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI (loaded with ctypes by pytorch_operator_amd/ops/_native.py).  Every
+// launcher validates the shapes its grid assumes before touching the GPU.
+// Returns hipSuccess (0) or a hipError_t / -1 for a host-side shape error.
+// ===========================================================================
+#define PTO_CHECK_B(B) do { if ((B) <= 0 || (B) > (1 << 20)) return -1; } while (0)
+
+extern "C" {
+
+int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* perm, const int* cursor,
+                        int host_offset, int n_total, float scale, float shift,
+                        const float* w, const float* bias, float* a1, uint8_t* idx1, int B,
+                        float* zero_ptr, int zero_n, void* stream) {
+  PTO_CHECK_B(B);
+  if (perm != nullptr && n_total <= 0) return -1;
+  const BatchSrc src = make_src(x, is_u8, nullptr, perm, cursor, host_offset, n_total, scale, shift);
+  const int blocks = (B * 2880 + 255) / 256;
+  hipLaunchKernelGGL(conv1_fwd_pool_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     src, w, bias, a1, idx1, B, zero_ptr, zero_n);
+  return (int)hipGetLastError();
+}
+
+int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, float* a2,
+                        uint8_t* idx2, int B, void* stream) {
+  PTO_CHECK_B(B);
+  hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(256), 0, (hipStream_t)stream,
+                     a1, w, bias, a2, idx2, B);
+  return (int)hipGetLastError();
+}
+
+int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* h, int B,
+                      void* stream) {
+  PTO_CHECK_B(B);
+  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(32, (B + 15) / 16), dim3(512), 0,
+                     (hipStream_t)stream, x, w, bias, h, B);
+  return (int)hipGetLastError();
+}
+
+int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* labels,
+                   const int* perm, const int* cursor, int host_offset, int n_total, int B,
+                   float grad_scale, float loss_scale, float* dlogits, float* dh, float* logp,
+                   float* stats, void* stream) {
+  PTO_CHECK_B(B);
+  if (labels == nullptr) return -1;
+  const BatchSrc src = make_src(nullptr, 0, labels, perm, cursor, host_offset, n_total, 1.f, 0.f);
+  hipLaunchKernelGGL(head_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, w2,
+                     b2, src, B, grad_scale, loss_scale, dlogits, dh, logp, stats);
+  return (int)hipGetLastError();
+}
+
+int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
+                      const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
+                      float* gb2, float* dz2, int B, void* stream) {
+  PTO_CHECK_B(B);
+  const int blocks = 400 + ((B + 15) / 16) * 50 + 20;
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, a2,
+                     idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, B);
+  return (int)hipGetLastError();
+}
+
+int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                       const void* x, int is_u8, const int* perm, const int* cursor,
+                       int host_offset, int n_total, float scale, float shift, float* gw2,
+                       float* gb2, float* gw1, float* gb1, float* dz1_out, int B, void* stream) {
+  PTO_CHECK_B(B);
+  if (perm != nullptr && n_total <= 0) return -1;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             F_LDS * (int)sizeof(float));
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const BatchSrc src = make_src(x, is_u8, nullptr, perm, cursor, host_offset, n_total, scale, shift);
+  hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(512), F_LDS * sizeof(float),
+                     (hipStream_t)stream, dz2, w2, a1, idx1, src, gw2, gb2, gw1, gb1, dz1_out, B);
+  return (int)hipGetLastError();
+}
+
+int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, float momentum,
+                     float dampening, float wd, float grad_scale, int nesterov, int first_step,
+                     int* step_counter, void* stream) {
+  if (n <= 0) return -1;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) & 15) return -2;  // float4 path
+  long v = (n >> 2) + 4;
+  int blocks = (int)((v + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(sgd_momentum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g,
+                     buf, n, lr, momentum, dampening, wd, grad_scale, nesterov, first_step,
+                     step_counter);
+  return (int)hipGetLastError();
+}
+
+int pto_conv_bwd_lds_bytes() { return F_LDS * (int)sizeof(float); }
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Build + load the hand-written gfx950 HIP kernel library (``libpto_hip.so``).
+
+The kernels live in ``csrc/kernels/*.hip`` and are compiled in-tree with
+``hipcc --offload-arch=gfx950`` into ``pytorch_operator_amd/_lib/libpto_hip.so``
+(so the built object travels with a ``gpurun`` snapshot and is the one the
+driver sees loaded).  The library exports a plain C ABI and is bound with
+``ctypes``; every launcher validates shapes on the host before launching.
+
+The library is linked against the HIP runtime by soname (``libamdhip64.so.7``);
+``torch`` is always imported first so the process shares torch's already-loaded
+HIP runtime (one runtime -> stream handles from ``torch.cuda`` are valid here).
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import shutil
+import subprocess
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded before the HIP library, see module doc)
+
+_PKG = Path(__file__).resolve().parent.parent
+_ROOT = _PKG.parent
+_SRC_DIR = _ROOT / "csrc" / "kernels"
+_LIB_DIR = _PKG / "_lib"
+_LIB_PATH = _LIB_DIR / "libpto_hip.so"
+_STAMP = _LIB_DIR / "libpto_hip.stamp"
+_ARCH = os.environ.get("PTO_OFFLOAD_ARCH", "gfx950")
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    """Raised when the HIP kernel library cannot be built or loaded."""
+
+
+def _sources():
+    return sorted(_SRC_DIR.glob("*.hip")) + sorted(_SRC_DIR.glob("*.h"))
+
+
+def _source_digest() -> str:
+    h = hashlib.sha256()
+    h.update(_ARCH.encode())
+    for p in _sources():
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def hipcc_path() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise NativeLibraryError("hipcc not found (need ROCm: /opt/rocm/bin/hipcc)")
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every ``csrc/kernels/*.hip`` for gfx950 into one shared library.
+
+    Rebuilds only when the sources (or the target arch) changed.
+    """
+    digest = _source_digest()
+    if not force and _LIB_PATH.exists() and _STAMP.exists() and _STAMP.read_text() == digest:
+        return _LIB_PATH
+    _LIB_DIR.mkdir(parents=True, exist_ok=True)
+    hip_srcs = [str(p) for p in sorted(_SRC_DIR.glob("*.hip"))]
+    tmp = _LIB_PATH.with_suffix(f".so.tmp{os.getpid()}")
+    cmd = [
+        hipcc_path(), f"--offload-arch={_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        "-munsafe-fp-atomics", "-I", str(_SRC_DIR), "-o", str(tmp), *hip_srcs,
+    ]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise NativeLibraryError(f"hipcc failed ({res.returncode}):\n{res.stderr[-8000:]}")
+    os.replace(tmp, _LIB_PATH)
+    _STAMP.write_text(digest)
+    return _LIB_PATH
+
+
+_VP = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_L = ctypes.c_long
+
+_SIGNATURES = {
+    "pto_mnist_conv1_fwd": [_VP, _I, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _I, _VP, _I, _VP],
+    "pto_mnist_conv2_fwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP],
+    "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
+    "pto_mnist_head": [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP],
+    "pto_mnist_conv_bwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP,
+                           _VP, _VP, _I, _VP],
+    "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
+    "pto_conv_bwd_lds_bytes": [],
+}
+
+
+def load(build_if_missing: bool = True):
+    """Return the loaded ``ctypes.CDLL`` (building it first if needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if build_if_missing:
+            build()
+        if not _LIB_PATH.exists():
+            raise NativeLibraryError(f"{_LIB_PATH} missing; run pytorch_operator_amd.ops.build()")
+        lib = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise NativeLibraryError(f"{what} failed with code {rc}")

@@ -1,0 +1,260 @@
+"""Python bindings for the fused MNIST kernels (csrc/kernels/mnist_kernels.hip).
+
+Each function validates shapes/dtypes/devices on the host (the kernels' grids
+assume them) and launches on the current torch stream, so calls compose with
+``torch.cuda`` streams, events and graph capture.
+
+Reference op sequence (jiaqianjing/pytorch-operator examples/mnist/mnist.py:25-33,
+37-43): conv1 -> relu -> pool -> conv2 -> relu -> pool -> fc1 -> relu -> fc2 ->
+log_softmax -> nll_loss -> backward -> SGD.step.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native
+
+MNIST_MEAN = 0.1307
+MNIST_STD = 0.3081
+U8_SCALE = 1.0 / (255.0 * MNIST_STD)
+U8_SHIFT = -MNIST_MEAN / MNIST_STD
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _req(t: torch.Tensor, shape, dtype, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class BatchSource:
+    """Where a batch's pixels/labels come from (mirrors ``pto::BatchSrc``).
+
+    ``x``: [N,784] (or [N,1,28,28]) uint8 raw pixels or fp32 values.
+    ``perm``: optional int32 [N] order; the batch is ``perm[offset : offset+B]``
+    (wrapping), with ``offset = cursor[0]*B % N`` when a device ``cursor`` is given
+    (graph replay) or ``host_offset`` otherwise.  Without ``perm`` the batch is
+    rows ``0..B-1`` of ``x``.
+    """
+
+    def __init__(self, x: torch.Tensor, labels: Optional[torch.Tensor] = None,
+                 perm: Optional[torch.Tensor] = None, cursor: Optional[torch.Tensor] = None,
+                 host_offset: int = 0, normalize: Optional[bool] = None):
+        if not x.is_cuda or not x.is_contiguous():
+            raise ValueError("x must be a contiguous CUDA tensor")
+        if x.numel() % 784 != 0:
+            raise ValueError("x must hold 28x28 images")
+        self.x = x
+        self.n_total = x.numel() // 784
+        self.is_u8 = x.dtype == torch.uint8
+        if not self.is_u8 and x.dtype != torch.float32:
+            raise ValueError("x must be uint8 or float32")
+        if normalize is None:
+            normalize = self.is_u8
+        if self.is_u8 and normalize:
+            self.scale, self.shift = U8_SCALE, U8_SHIFT
+        elif normalize:
+            self.scale, self.shift = 1.0 / MNIST_STD, -MNIST_MEAN / MNIST_STD
+        else:
+            self.scale, self.shift = 1.0, 0.0
+        if labels is not None:
+            if labels.dtype != torch.int32 or not labels.is_cuda or labels.numel() != self.n_total:
+                raise ValueError("labels must be int32 CUDA [N]")
+        self.labels = labels
+        if perm is not None:
+            if perm.dtype != torch.int32 or perm.numel() != self.n_total or not perm.is_cuda:
+                raise ValueError("perm must be int32 CUDA [N]")
+        self.perm = perm
+        if cursor is not None and (cursor.dtype != torch.int32 or not cursor.is_cuda):
+            raise ValueError("cursor must be an int32 CUDA tensor")
+        self.cursor = cursor
+        self.host_offset = int(host_offset)
+
+    def check_batch(self, B: int) -> None:
+        if self.perm is None and B > self.n_total:
+            raise ValueError(f"batch {B} larger than dataset {self.n_total}")
+
+
+def conv1_fwd(src: BatchSource, w: torch.Tensor, b: torch.Tensor, B: int,
+              out: Optional[torch.Tensor] = None, idx: Optional[torch.Tensor] = None,
+              zero: Optional[torch.Tensor] = None):
+    """relu(maxpool2(conv1(normalize(x)))) -> (a1 [B,20,12,12] f32, idx1 uint8 argmax)."""
+    lib = _native.load()
+    src.check_batch(B)
+    _req(w, (20, 1, 5, 5), torch.float32, "conv1.weight")
+    _req(b, (20,), torch.float32, "conv1.bias")
+    dev = w.device
+    out = torch.empty((B, 20, 12, 12), device=dev) if out is None else out
+    idx = torch.empty((B, 20, 12, 12), device=dev, dtype=torch.uint8) if idx is None else idx
+    _req(out, (B, 20, 12, 12), torch.float32, "a1")
+    _req(idx, (B, 20, 12, 12), torch.uint8, "idx1")
+    zn = 0
+    if zero is not None:
+        if zero.dtype != torch.float32 or not zero.is_contiguous():
+            raise ValueError("zero must be contiguous fp32")
+        zn = zero.numel()
+    rc = lib.pto_mnist_conv1_fwd(
+        src.x.data_ptr(), int(src.is_u8), _ptr(src.perm), _ptr(src.cursor), src.host_offset,
+        src.n_total, src.scale, src.shift, w.data_ptr(), b.data_ptr(), out.data_ptr(),
+        idx.data_ptr(), B, _ptr(zero), zn, _stream())
+    _native.check(rc, "conv1_fwd")
+    return out, idx
+
+
+def conv2_fwd(a1: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+              out: Optional[torch.Tensor] = None, idx: Optional[torch.Tensor] = None):
+    """relu(maxpool2(conv2(a1))) flattened -> (a2 [B,800], idx2 uint8 [B,800])."""
+    lib = _native.load()
+    B = a1.shape[0]
+    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
+    _req(w, (50, 20, 5, 5), torch.float32, "conv2.weight")
+    _req(b, (50,), torch.float32, "conv2.bias")
+    if w.data_ptr() % 16:
+        raise ValueError("conv2.weight must be 16-byte aligned")
+    out = torch.empty((B, 800), device=a1.device) if out is None else out
+    idx = torch.empty((B, 800), device=a1.device, dtype=torch.uint8) if idx is None else idx
+    _req(out, (B, 800), torch.float32, "a2")
+    _req(idx, (B, 800), torch.uint8, "idx2")
+    rc = lib.pto_mnist_conv2_fwd(a1.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                 idx.data_ptr(), B, _stream())
+    _native.check(rc, "conv2_fwd")
+    return out, idx
+
+
+def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """relu(x @ w.T + b) for x [B,800], w [500,800]."""
+    lib = _native.load()
+    B = x.shape[0]
+    _req(x, (B, 800), torch.float32, "x")
+    _req(w, (500, 800), torch.float32, "fc1.weight")
+    _req(b, (500,), torch.float32, "fc1.bias")
+    out = torch.empty((B, 500), device=x.device) if out is None else out
+    _req(out, (B, 500), torch.float32, "h1")
+    rc = lib.pto_mnist_fc1_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), B,
+                               _stream())
+    _native.check(rc, "fc1_fwd")
+    return out
+
+
+def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, src: BatchSource, *,
+         grad_scale: float = 0.0, loss_scale: float = 1.0, want_grad: bool = True,
+         want_logp: bool = False, stats: Optional[torch.Tensor] = None,
+         dlogits: Optional[torch.Tensor] = None, dh: Optional[torch.Tensor] = None,
+         logp: Optional[torch.Tensor] = None):
+    """fc2 + log_softmax + nll (+ d(logits), dh with the fc1 ReLU mask).
+
+    ``stats`` (fp32 [>=2]) accumulates ``loss*loss_scale`` and the correct count.
+    """
+    lib = _native.load()
+    B = h.shape[0]
+    _req(h, (B, 500), torch.float32, "h1")
+    _req(w, (10, 500), torch.float32, "fc2.weight")
+    _req(b, (10,), torch.float32, "fc2.bias")
+    if src.labels is None:
+        raise ValueError("BatchSource has no labels")
+    src.check_batch(B)
+    dev = h.device
+    if want_grad:
+        dlogits = torch.empty((B, 10), device=dev) if dlogits is None else dlogits
+        dh = torch.empty((B, 500), device=dev) if dh is None else dh
+        _req(dlogits, (B, 10), torch.float32, "dlogits")
+        _req(dh, (B, 500), torch.float32, "dh")
+    else:
+        dlogits = dh = None
+    if want_logp:
+        logp = torch.empty((B, 10), device=dev) if logp is None else logp
+        _req(logp, (B, 10), torch.float32, "logp")
+    else:
+        logp = None
+    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
+        raise ValueError("stats must be fp32 with >= 2 elements")
+    rc = lib.pto_mnist_head(h.data_ptr(), w.data_ptr(), b.data_ptr(), src.labels.data_ptr(),
+                            _ptr(src.perm), _ptr(src.cursor), src.host_offset, src.n_total, B,
+                            float(grad_scale), float(loss_scale), _ptr(dlogits), _ptr(dh),
+                            _ptr(logp), _ptr(stats), _stream())
+    _native.check(rc, "head")
+    return dlogits, dh, logp
+
+
+def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None):
+    """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked)."""
+    lib = _native.load()
+    B = dh.shape[0]
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
+    _req(w1, (500, 800), torch.float32, "fc1.weight")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h1")
+    _req(gw1, (500, 800), torch.float32, "grad fc1.weight")
+    _req(gb1, (500,), torch.float32, "grad fc1.bias")
+    _req(gw2, (10, 500), torch.float32, "grad fc2.weight")
+    _req(gb2, (10,), torch.float32, "grad fc2.bias")
+    dz2 = torch.empty((B, 50, 8, 8), device=dh.device) if dz2 is None else dz2
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
+                               dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),
+                               gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), B, _stream())
+    _native.check(rc, "fc1_bwd")
+    return dz2
+
+
+def conv_bwd(dz2, w2, a1, idx1, src: BatchSource, gw2, gb2, gw1, gb1, want_dz1=False):
+    """conv2 weight/bias grads, dz1 (internal), conv1 weight/bias grads.
+
+    The conv grads are ACCUMULATED (fp32 atomics): zero them first (the fused step
+    zeroes them inside conv1_fwd via ``zero=``).
+    """
+    lib = _native.load()
+    B = dz2.shape[0]
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    _req(w2, (50, 20, 5, 5), torch.float32, "conv2.weight")
+    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
+    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(gw2, (50, 20, 5, 5), torch.float32, "grad conv2.weight")
+    _req(gb2, (50,), torch.float32, "grad conv2.bias")
+    _req(gw1, (20, 1, 5, 5), torch.float32, "grad conv1.weight")
+    _req(gb1, (20,), torch.float32, "grad conv1.bias")
+    src.check_batch(B)
+    dz1 = torch.empty((B, 20, 24, 24), device=dz2.device) if want_dz1 else None
+    rc = lib.pto_mnist_conv_bwd(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(),
+                                src.x.data_ptr(), int(src.is_u8), _ptr(src.perm),
+                                _ptr(src.cursor), src.host_offset, src.n_total, src.scale,
+                                src.shift, gw2.data_ptr(), gb2.data_ptr(), gw1.data_ptr(),
+                                gb1.data_ptr(), _ptr(dz1), B, _stream())
+    _native.check(rc, "conv_bwd")
+    return dz1
+
+
+def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, *, lr: float,
+                  momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                  nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
+                  step_counter: Optional[torch.Tensor] = None) -> None:
+    """In-place fused SGD(momentum) over flat fp32 buffers (torch.optim.SGD math)."""
+    lib = _native.load()
+    n = params.numel()
+    for t, nm in ((params, "params"), (grads, "grads"), (buf, "momentum_buffer")):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
+    if step_counter is not None and (step_counter.dtype != torch.int32 or not step_counter.is_cuda):
+        raise ValueError("step_counter must be int32 CUDA")
+    rc = lib.pto_sgd_momentum(params.data_ptr(), grads.data_ptr(), buf.data_ptr(), n, float(lr),
+                              float(momentum), float(dampening), float(weight_decay),
+                              float(grad_scale), int(nesterov), int(first_step),
+                              _ptr(step_counter), _stream())
+    _native.check(rc, "sgd_momentum")

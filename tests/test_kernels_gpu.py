@@ -1,0 +1,188 @@
+"""Numerics of the hand-written gfx950 MNIST kernels vs a plain PyTorch fp32 reference.
+
+Every fused kernel is compared against the same op computed by torch on the CPU in
+fp32 (the reference's dtype): activations, argmax pooling, log-probs, every
+parameter gradient, and the SGD(momentum) update.  Tolerances are relative to the
+tensor's max magnitude (different summation orders, exact-fp32 MFMA).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+def _data(B, seed=0, n_total=None):
+    g = torch.Generator().manual_seed(seed)
+    n = n_total or B
+    x = torch.randint(0, 256, (n, 784), generator=g, dtype=torch.uint8)
+    y = torch.randint(0, 10, (n,), generator=g, dtype=torch.int32)
+    return x, y
+
+
+def _norm(x_u8):
+    return ((x_u8.float() / 255.0 - 0.1307) / 0.3081).view(-1, 1, 28, 28)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pytorch_operator_amd.ops import _native
+    return _native.load()
+
+
+@pytest.mark.parametrize("B", [64, 37, 1])
+def test_forward_kernels_match_torch(lib, B):
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    sd = reference_init(3)
+    dev = torch.device("cuda")
+    p = {k: v.to(dev).contiguous() for k, v in sd.items()}
+    x, y = _data(B, seed=B)
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    a1, idx1 = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    a2, idx2 = K.conv2_fwd(a1, p["conv2.weight"], p["conv2.bias"])
+    h1 = K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"])
+    stats = torch.zeros(16, device=dev)
+    _, _, logp = K.head(h1, p["fc2.weight"], p["fc2.bias"], src, want_grad=False, want_logp=True,
+                        stats=stats, loss_scale=1.0 / B)
+    torch.cuda.synchronize()
+
+    xn = _norm(x)
+    z1 = F.conv2d(xn, sd["conv1.weight"], sd["conv1.bias"])
+    r1, ri1 = F.max_pool2d(F.relu(z1), 2, 2, return_indices=True)
+    assert _rel(a1, r1) < 1e-5
+    z2 = F.conv2d(r1, sd["conv2.weight"], sd["conv2.bias"])
+    r2 = F.max_pool2d(F.relu(z2), 2, 2).reshape(B, 800)
+    assert _rel(a2, r2) < 1e-5
+    rh = F.relu(r2 @ sd["fc1.weight"].T + sd["fc1.bias"])
+    assert _rel(h1, rh) < 1e-5
+    rl = F.log_softmax(rh @ sd["fc2.weight"].T + sd["fc2.bias"], dim=1)
+    assert _rel(logp, rl) < 1e-5
+    loss = F.nll_loss(rl, y.long())
+    assert abs(float(stats[0]) - float(loss)) < 1e-4 * max(1.0, abs(float(loss)))
+    assert int(stats[1]) == int((rl.argmax(1) == y.long()).sum())
+
+
+@pytest.mark.parametrize("B", [64, 50])
+def test_fused_step_gradients_and_sgd_match_torch(lib, B):
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer, Net, reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    x, y = _data(B, seed=100 + B)
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, seed=5)
+    tr.forward_backward()
+    torch.cuda.synchronize()
+
+    net = Net()
+    net.load_state_dict(reference_init(5))
+    out = net(_norm(x))
+    loss = F.nll_loss(out, y.long())
+    loss.backward()
+    assert abs(tr.loss() - float(loss)) < 1e-4
+    for name, prm in net.named_parameters():
+        err = _rel(tr.grads[name], prm.grad)
+        assert err < 2e-4, (name, err)
+
+    # two SGD(momentum) steps on the same batch vs torch.optim.SGD
+    opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.5)
+    opt.step()
+    tr.optimizer_step(advance_cursor=False)
+    opt.zero_grad()
+    F.nll_loss(net(_norm(x)), y.long()).backward()
+    opt.step()
+    tr.train_step(advance_cursor=False)
+    torch.cuda.synchronize()
+    for name, prm in net.named_parameters():
+        err = _rel(tr.params[name], prm.data)
+        assert err < 1e-4, (name, err)
+
+
+def test_conv_bwd_dz1_matches_autograd(lib):
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    B = 16
+    dev = torch.device("cuda")
+    sd = reference_init(7)
+    x, y = _data(B, seed=11)
+    xn = _norm(x).requires_grad_(False)
+    c1w = sd["conv1.weight"].clone().requires_grad_(True)
+    z1 = F.conv2d(xn, c1w, sd["conv1.bias"])
+    r1 = F.max_pool2d(F.relu(z1), 2, 2)
+    r1.retain_grad()
+    z2 = F.conv2d(r1, sd["conv2.weight"], sd["conv2.bias"])
+    z2.retain_grad()
+    out = F.max_pool2d(F.relu(z2), 2, 2)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    # feed torch's dz2 into the kernel and compare dz1 / conv grads
+    p = {k: v.to(dev).contiguous() for k, v in sd.items()}
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    a1, idx1 = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    gw2 = torch.zeros(50, 20, 5, 5, device=dev)
+    gb2 = torch.zeros(50, device=dev)
+    gw1 = torch.zeros(20, 1, 5, 5, device=dev)
+    gb1 = torch.zeros(20, device=dev)
+    dz2 = z2.grad.contiguous().to(dev)
+    dz1 = K.conv_bwd(dz2, p["conv2.weight"], a1, idx1, src, gw2, gb2, gw1, gb1, want_dz1=True)
+    torch.cuda.synchronize()
+    # dz1 = grad wrt conv1 pre-activation output z1
+    z1b = F.conv2d(xn, sd["conv1.weight"], sd["conv1.bias"]).requires_grad_(True)
+    r1b = F.max_pool2d(F.relu(z1b), 2, 2)
+    (r1b * r1.grad).sum().backward()
+    assert _rel(dz1, z1b.grad) < 1e-4
+    assert _rel(gw1, c1w.grad) < 2e-4
+    ref_gw2 = torch.nn.grad.conv2d_weight(r1.detach(), (50, 20, 5, 5), z2.grad)
+    assert _rel(gw2, ref_gw2) < 1e-4
+    assert _rel(gb2, z2.grad.sum((0, 2, 3))) < 1e-4
+
+
+def test_graph_replay_matches_eager(lib):
+    """A captured step replays on successive batches exactly like eager steps."""
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    n = 640
+    x, y = _data(n, seed=42, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(0)).to(torch.int32)
+
+    def make():
+        cur = torch.zeros(1, dtype=torch.int32, device=dev)
+        src = K.BatchSource(x.to(dev), y.to(dev), perm=perm.to(dev), cursor=cur)
+        return FusedMnistTrainer(batch_size=64, source=src, seed=9)
+
+    eager = make()
+    for _ in range(6):
+        eager.train_step()
+    graphed = make()
+    graphed.train_step()  # first step eager (initialises momentum)
+    g = graphed.capture(steps_per_graph=1)
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(graphed.cursor.item()) == 6
+    assert _rel(graphed.flat_params, eager.flat_params) < 1e-5
+
+
+def test_training_reduces_loss_on_learnable_synthetic_data(lib):
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    ds = make_synthetic_mnist(6400, seed=1, device=dev)
+    cur = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cur)
+    tr = FusedMnistTrainer(batch_size=64, source=src, seed=1)
+    losses = []
+    for i in range(100):
+        tr.train_step()
+        losses.append(tr.loss())
+    assert sum(losses[-10:]) / 10 < 0.5 * sum(losses[:10]) / 10
+    _, acc = tr.evaluate(K.BatchSource(ds.images, ds.labels), n=2000)
+    assert acc > 0.9
