@@ -5,19 +5,23 @@
 //   -> fc1(800->500) -> ReLU -> fc2(500->10) -> log_softmax -> nll_loss(mean)
 //
 // The whole step is 6 launches (+1 fused SGD launch, +RCCL all-reduce when
-// world_size > 1).  The step is launch/latency bound (~0.84 GFLOP at B=64), so
-// the design goal is few, fused, fully-occupied launches that a hipGraph can
-// replay back to back:
+// world_size > 1).  At B=64 the step is ~0.84 GFLOP: it is launch- and
+// latency-bound, so every kernel is shaped to (a) issue all of its global loads
+// up front (no load -> use -> load chains), (b) keep its MFMA chains short by
+// splitting K across the waves of a workgroup, and (c) keep the launch count low
+// so a hipGraph can replay the step back to back:
 //
-//   A conv1_fwd_pool   uint8 gather + Normalize + conv1 + bias + ReLU + pool(argmax)
-//                      (+ zero-fill of the atomically-accumulated grad segment)
+//   A conv1_fwd_pool   uint8 gather + Normalize + conv1 + bias + ReLU + pool(argmax);
+//                      also emits the normalised batch + gathered labels for the
+//                      later launches, and zero-fills the atomically-accumulated
+//                      grad segment (conv grads + loss stats)
 //   B conv2_fwd_pool   implicit GEMM on v_mfma_f32_16x16x4_f32, LDS-staged im2col,
-//                      bias + ReLU + 2x2 max-pool fused in the accumulator epilogue
-//   C fc1_fwd          MFMA GEMM, K split over the 8 waves of a workgroup, LDS
-//                      reduction, bias + ReLU epilogue
+//                      K split over two wave groups, bias + ReLU + 2x2 max-pool
+//                      fused in the accumulator epilogue
+//   C fc1_fwd          MFMA GEMM, K split over 10 waves, LDS reduction, bias+ReLU
 //   D head             fc2 + log_softmax + NLL + d(logits) + fc2^T GEMV + ReLU mask
 //   E fc1_bwd          dW_fc1 / db_fc1 (MFMA), dX_fc1 (MFMA) with un-pool + ReLU
-//                      mask epilogue, dW_fc2 / db_fc2
+//                      mask epilogue, dW_fc2 / db_fc2, loss statistics
 //   F conv_bwd         per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
 //                      dW_conv2 (MFMA, im2col from LDS), col2im + un-pool + ReLU
 //                      mask -> dz1 (LDS), dW_conv1 (MFMA), db_conv1/db_conv2
@@ -25,40 +29,71 @@
 //
 // All arithmetic is fp32 (the reference's dtype); matrix work uses the exact-fp32
 // MFMA (one rounding per product, same as an fmaf chain).
+//
+// Every kernel takes an optional `dbg` pointer: when non-null, thread 0 of each
+// block records wall_clock64() (100 MHz) at phase boundaries into
+// dbg[block * 16 + phase] (used by tools/phase_profile.py; null in production).
 #include "pto_common.h"
 
 using namespace pto;
 
 namespace {
 
+typedef unsigned long long u64;
+
+__device__ __forceinline__ void stamp(u64* dbg, int phase) {
+  if (dbg != nullptr && threadIdx.x == 0) {
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    dbg[blk * 16 + phase] = (u64)wall_clock64();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // A: conv1 forward (+bias, ReLU, 2x2 max-pool with argmax).  One thread per
 // pooled output (B*20*144 threads); a 256-thread block spans at most two
-// samples, whose normalised images are staged in LDS.
+// samples, whose normalised images are staged in LDS.  The block that owns a
+// sample's first output also publishes xn[b] (normalised image) and lab[b].
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
     BatchSrc src, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ a1, uint8_t* __restrict__ idx1, int B,
-    float* __restrict__ zero_ptr, int zero_n) {
+    float* __restrict__ zero_ptr, int zero_n, float* __restrict__ xn_out,
+    int* __restrict__ lab_out, u64* dbg) {
   __shared__ float img[2][784];
   __shared__ float ws[500];
   __shared__ float bs[20];
   const int tid = threadIdx.x;
-  if (zero_ptr != nullptr) {
-    for (int i = blockIdx.x * 256 + tid; i < zero_n; i += gridDim.x * 256) zero_ptr[i] = 0.f;
-  }
+  stamp(dbg, 0);
   const int item0 = blockIdx.x * 256;
   const int total = B * 2880;
   const int b0 = item0 / 2880;
   const int b1 = min((item0 + 255) / 2880, B - 1);
   const int nb = b1 - b0 + 1;
-  for (int e = tid; e < nb * 784; e += 256) {
-    const int s = e / 784, p = e - s * 784;
-    img[s][p] = load_px(src, batch_row(src, b0 + s, B), p);
+  const int row0 = batch_row(src, b0, B);
+  const int row1 = batch_row(src, b1, B);
+  if (zero_ptr != nullptr) {
+    for (int i = blockIdx.x * 256 + tid; i < zero_n; i += gridDim.x * 256) zero_ptr[i] = 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int e = tid + k * 256;
+    if (e < nb * 784) {
+      const int s = e >= 784 ? 1 : 0;
+      const int p = e - s * 784;
+      const float v = load_px(src, s ? row1 : row0, p);
+      img[s][p] = v;
+      const int bb = b0 + s;
+      if (xn_out != nullptr && bb * 2880 >= item0) xn_out[(size_t)bb * 784 + p] = v;
+    }
+  }
+  if (lab_out != nullptr && src.labels != nullptr && tid < nb) {
+    const int bb = b0 + tid;
+    if (bb * 2880 >= item0) lab_out[bb] = src.labels[tid ? row1 : row0];
   }
   for (int e = tid; e < 500; e += 256) ws[e] = w[e];
   if (tid < 20) bs[tid] = bias[tid];
   __syncthreads();
+  stamp(dbg, 1);
 
   const int item = item0 + tid;
   if (item >= total) return;
@@ -98,64 +133,89 @@ __global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
 
 // ---------------------------------------------------------------------------
 // B: conv2 forward as an implicit GEMM on fp32 MFMA.
-//   grid = (4 output-channel groups of 16, B samples), 4 waves per block.
-//   wave w owns conv rows {2w, 2w+1} x 8 cols = 16 positions (M) x 16 channels (N);
-//   K = 500 = (20 in-ch x 25 taps) is walked as 125 MFMA steps.  Lane group
-//   g = lane>>4 owns input channels {g, g+4, .., g+16}, which makes every LDS
-//   offset of the unrolled loop a compile-time immediate.
-//   LDS row strides are chosen for conflict-free ds_read_b32:
+//   grid = (4 output-channel groups of 16, B samples), 8 waves per block.
+//   wave w: position tile pt = w & 3 (conv rows {2pt, 2pt+1} x 8 cols = 16
+//   positions, M) x 16 channels (N); K half kh2 = w >> 2 walks (cj,kh) pairs
+//   [0,13) or [13,25) x 5 kw = 65 / 60 MFMA steps.  Lane group g = lane>>4 owns
+//   input channels {g, g+4, .., g+16}, so every LDS offset of the unrolled loop
+//   is a compile-time immediate.  LDS strides give conflict-free ds_read_b32:
 //     image: row stride 16, channel stride 200 (== 8 mod 32)
 //     weights: row stride 514 (== 2 mod 32, lane groups differ by 25 -> odd banks)
-//   The 2x2 pool window = 2 registers of this lane x 2 registers of lane^32.
+//   The two K halves meet in LDS; the 2x2 pool window = 2 registers of this
+//   lane x 2 registers of lane^32.
 // ---------------------------------------------------------------------------
 constexpr int C2_RS = 16;
 constexpr int C2_CS = 200;
 constexpr int C2_WS = 514;
 
-__global__ __launch_bounds__(256) void conv2_fwd_pool_kernel(
-    const float* __restrict__ a1, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B) {
-  __shared__ float in_s[20 * C2_CS];
-  __shared__ float w_s[16 * C2_WS];
-  const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const float* src = a1 + (size_t)b * 2880;
-  for (int e = tid; e < 2880; e += 256) {
-    const int c = e / 144, p = e - c * 144;
-    const int y = p / 12, x = p - y * 12;
-    in_s[c * C2_CS + y * C2_RS + x] = src[e];
-  }
-  for (int e = tid; e < 16 * 125; e += 256) {
-    const int j = e / 125, q = e - j * 125;
-    const int co = cg * 16 + j;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (co < 50) v = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
-    float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
-    d[0] = make_float2(v.x, v.y);
-    d[1] = make_float2(v.z, v.w);
-  }
-  __syncthreads();
-
-  const int lane = tid & 63, wv = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int oh = 2 * wv + (i >> 3), ow = i & 7;
-  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
-  const float* Bb = w_s + i * C2_WS + g * 25;
+template <int Q0, int Q1>
+__device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb) {
   f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-  for (int cj = 0; cj < 5; ++cj)
+  for (int q = Q0; q < Q1; ++q) {
+    const int cj = q / 5, kh = q % 5;
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
+    for (int kw = 0; kw < 5; ++kw) {
+      const float av = Ab[cj * 4 * C2_CS + kh * C2_RS + kw];
+      const float bv = Bb[cj * 100 + kh * 5 + kw];
+      if (kw & 1) acc1 = mfma16x16x4(av, bv, acc1);
+      else acc0 = mfma16x16x4(av, bv, acc0);
+    }
+  }
+  return acc0 + acc1;
+}
+
+__global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
+    const float* __restrict__ a1, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
+  __shared__ float in_s[20 * C2_CS];
+  __shared__ float w_s[16 * C2_WS];
+  __shared__ f32x4 red[4][64];
+  const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  stamp(dbg, 0);
+  const float* src = a1 + (size_t)b * 2880;
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const float av = Ab[cj * 4 * C2_CS + kh * C2_RS + kw];
-        const float bv = Bb[cj * 100 + kh * 5 + kw];
-        if (((cj * 25 + kh * 5 + kw) & 1) == 0) acc0 = mfma16x16x4(av, bv, acc0);
-        else acc1 = mfma16x16x4(av, bv, acc1);
-      }
-  const f32x4 acc = acc0 + acc1;
+  for (int k = 0; k < 6; ++k) {
+    const int e = tid + k * 512;
+    if (e < 2880) {
+      const int c = e / 144, p = e - c * 144;
+      const int y = p / 12, x = p - y * 12;
+      in_s[c * C2_CS + y * C2_RS + x] = src[e];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = tid + k * 512;
+    if (e < 16 * 125) {
+      const int j = e / 125, q = e - j * 125;
+      const int co = cg * 16 + j;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (co < 50) v = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
+      float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
+      d[0] = make_float2(v.x, v.y);
+      d[1] = make_float2(v.z, v.w);
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 1);
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int pt = wv & 3, khalf = wv >> 2;
+  const int i = lane & 15, g = lane >> 4;
+  const int oh = 2 * pt + (i >> 3), ow = i & 7;
+  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
+  const float* Bb = w_s + i * C2_WS + g * 25;
+  f32x4 acc;
+  if (khalf == 0) acc = conv2_k_range<0, 13>(Ab, Bb);
+  else acc = conv2_k_range<13, 25>(Ab, Bb);
+  if (khalf == 1) red[pt][lane] = acc;
+  __syncthreads();
+  stamp(dbg, 2);
+  if (khalf == 1) return;
+  acc += red[pt][lane];
   const int co = cg * 16 + i;
   const float bco = (co < 50) ? bias[co] : 0.f;
-  // reg r of this lane = conv position (oh = 2wv + (g>>1), ow = 4(g&1) + r)
+  // reg r of this lane = conv position (oh = 2pt + (g>>1), ow = 4(g&1) + r)
   const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
   float mA = v0; int aA = 0;
   if (v1 > mA) { mA = v1; aA = 1; }
@@ -168,7 +228,7 @@ __global__ __launch_bounds__(256) void conv2_fwd_pool_kernel(
   if (g < 2 && co < 50) {  // top row of the window; partner lane holds the bottom row
     if (pA > mA) { mA = pA; aA = 2 + paA; }
     if (pB > mB) { mB = pB; aB = 2 + paB; }
-    const size_t o = (size_t)b * 800 + co * 16 + wv * 4 + 2 * (g & 1);
+    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);
     a2[o] = fmaxf(mA, 0.f);
     a2[o + 1] = fmaxf(mB, 0.f);
     idx2[o] = (uint8_t)aA;
@@ -178,40 +238,48 @@ __global__ __launch_bounds__(256) void conv2_fwd_pool_kernel(
 
 // ---------------------------------------------------------------------------
 // C: fc1 forward: h = relu(x[B,800] . W[500,800]^T + b).
-//   grid = (32 N-tiles, ceil(B/16) M-tiles), 8 waves; wave w reduces K range
-//   [100w, 100w+100) (lane group g owns k = 100w + 25g + s), partial tiles are
-//   summed through LDS and the bias+ReLU epilogue is applied once.
+//   grid = (32 N-tiles, ceil(B/16) M-tiles), 10 waves; wave w reduces K range
+//   [80w, 80w+80), lane group g owns k = 80w + 20g + [0,20) (5 float4 loads per
+//   operand, all issued before the first MFMA); the ten partial tiles are summed
+//   through LDS and the bias+ReLU epilogue is applied once.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void fc1_fwd_kernel(
+__global__ __launch_bounds__(640) void fc1_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ h, int B) {
-  __shared__ f32x4 red[8][64];
+    float* __restrict__ h, int B, u64* dbg) {
+  __shared__ f32x4 red[10][64];
   const int nt = blockIdx.x, mt = blockIdx.y, tid = threadIdx.x;
+  stamp(dbg, 0);
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int row = mt * 16 + i, col = nt * 16 + i;
   const bool rv = row < B, cv = col < 500;
-  const int k0 = wv * 100 + g * 25;
-  const float* xa = x + (size_t)(rv ? row : B - 1) * 800 + k0;
-  const float* wb = w + (size_t)(cv ? col : 499) * 800 + k0;
-  float av[25], bv[25];
+  const int k0 = wv * 80 + g * 20;
+  const float4* xa = reinterpret_cast<const float4*>(x + (size_t)(rv ? row : B - 1) * 800 + k0);
+  const float4* wb = reinterpret_cast<const float4*>(w + (size_t)(cv ? col : 499) * 800 + k0);
+  float4 av[5], bv[5];
 #pragma unroll
-  for (int s = 0; s < 25; ++s) { av[s] = xa[s]; bv[s] = wb[s]; }
+  for (int s = 0; s < 5; ++s) { av[s] = xa[s]; bv[s] = wb[s]; }
   f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
-  for (int s = 0; s < 25; ++s) {
-    const float a = rv ? av[s] : 0.f;
-    const float bb = cv ? bv[s] : 0.f;
-    if (s & 1) c1 = mfma16x16x4(a, bb, c1);
-    else c0 = mfma16x16x4(a, bb, c0);
+  for (int s = 0; s < 5; ++s) {
+    const float* ae = &av[s].x;
+    const float* be = &bv[s].x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = rv ? ae[e] : 0.f;
+      const float bb = cv ? be[e] : 0.f;
+      if (e & 1) c1 = mfma16x16x4(a, bb, c1);
+      else c0 = mfma16x16x4(a, bb, c0);
+    }
   }
   red[wv][lane] = c0 + c1;
   __syncthreads();
+  stamp(dbg, 1);
   if (tid < 256) {
     const int l = tid >> 2, r = tid & 3;
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += red[q][l][r];
+    for (int q = 0; q < 10; ++q) s += red[q][l][r];
     const int orow = mt * 16 + (l >> 4) * 4 + r, ocol = nt * 16 + (l & 15);
     if (orow < B && ocol < 500) h[(size_t)orow * 500 + ocol] = fmaxf(s + bias[ocol], 0.f);
   }
@@ -220,33 +288,49 @@ __global__ __launch_bounds__(512) void fc1_fwd_kernel(
 // ---------------------------------------------------------------------------
 // D: head.  One wave per sample: logits = h.W2^T + b2, log_softmax, NLL,
 // d(logits) = (softmax - onehot) * grad_scale, dh = (d(logits).W2) * (h > 0).
-// stats[0] += loss * loss_scale, stats[1] += (argmax == target).
+// All loads (label, h row, the 10x500 W2 slice this lane needs) are issued
+// first.  Per-sample (loss, correct) go to per_sample[b] (reduced later by
+// fc1_bwd, deterministic); eval callers may instead accumulate into `stats`
+// (one atomic per block after an LDS reduction).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void head_kernel(
     const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
-    BatchSrc src, int B, float grad_scale, float loss_scale,
+    const int* __restrict__ lab, int B, float grad_scale, float loss_scale,
     float* __restrict__ dlogits, float* __restrict__ dh, float* __restrict__ logp_out,
-    float* __restrict__ stats) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int b = blockIdx.x * 4 + (tid >> 6);
-  if (b >= B) return;  // whole wave exits together; the kernel has no barrier
-  float hv[8];
+    float* __restrict__ per_sample, float* __restrict__ stats, u64* dbg) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wq = tid >> 6;
+  stamp(dbg, 0);
+  const int b = blockIdx.x * 4 + wq;
+  const bool bvalid = b < B;
+  const int bc = bvalid ? b : B - 1;
+  const int t = lab[bc];
+  float hv[8], wv[10][8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const int k = lane + 64 * q;
-    hv[q] = (k < 500) ? h[(size_t)b * 500 + k] : 0.f;
+    const int k = min(lane + 64 * q, 499);
+    hv[q] = h[(size_t)bc * 500 + k];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) wv[j][q] = w2[j * 500 + k];
   }
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (lane + 64 * q >= 500) hv[q] = 0.f;
   float logit[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) {
     float p = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = lane + 64 * q;
-      if (k < 500) p = fmaf(hv[q], w2[j * 500 + k], p);
-    }
-    logit[j] = wave_sum(p) + b2[j];
+    for (int q = 0; q < 8; ++q) p = fmaf(hv[q], wv[j][q], p);
+    logit[j] = p;
   }
+  // 10 independent butterfly reductions, interleaved
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) logit[j] += __shfl_xor(logit[j], o, 64);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) logit[j] += b2[j];
   float m = logit[0];
 #pragma unroll
   for (int j = 1; j < 10; ++j) m = fmaxf(m, logit[j]);
@@ -254,7 +338,6 @@ __global__ __launch_bounds__(256) void head_kernel(
 #pragma unroll
   for (int j = 0; j < 10; ++j) se += __expf(logit[j] - m);
   const float lse = m + __logf(se);
-  const int t = src.labels[batch_row(src, b, B)];
   float lt = 0.f;
   int pred = 0;
   float best = logit[0];
@@ -263,10 +346,24 @@ __global__ __launch_bounds__(256) void head_kernel(
     if (j == t) lt = logit[j];
     if (logit[j] > best) { best = logit[j]; pred = j; }
   }
-  if (lane == 0 && stats != nullptr) {
-    atomicAdd(&stats[0], (lse - lt) * loss_scale);
-    atomicAdd(&stats[1], pred == t ? 1.f : 0.f);
+  const float lossb = lse - lt;
+  const float corr = pred == t ? 1.f : 0.f;
+  if (bvalid && lane == 0 && per_sample != nullptr) {
+    per_sample[2 * b] = lossb;
+    per_sample[2 * b + 1] = corr;
   }
+  if (stats != nullptr) {
+    if (lane == 0) {
+      red[0][wq] = bvalid ? lossb * loss_scale : 0.f;
+      red[1][wq] = bvalid ? corr : 0.f;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      atomicAdd(&stats[0], red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+      atomicAdd(&stats[1], red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    }
+  }
+  if (!bvalid) return;
   if (logp_out != nullptr) {
 #pragma unroll
     for (int j = 0; j < 10; ++j)
@@ -287,32 +384,37 @@ __global__ __launch_bounds__(256) void head_kernel(
     if (k < 500) {
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) s = fmaf(dl[j], w2[j * 500 + k], s);
+      for (int j = 0; j < 10; ++j) s = fmaf(dl[j], wv[j][q], s);
       dh[(size_t)b * 500 + k] = hv[q] > 0.f ? s : 0.f;
     }
   }
+  stamp(dbg, 1);
 }
 
 // ---------------------------------------------------------------------------
 // E: fc1 backward, three independent jobs in one launch (blockDim 256):
-//   job 1 (400 blocks x 4 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B),
-//          db_fc1 from the kt==0 tiles.  Written, not accumulated: no zeroing needed.
+//   job 1 (400 blocks x 4 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B,
+//          64 samples per register-preloaded chunk), db_fc1 from the kt==0 tiles.
+//          Written, not accumulated: no zeroing needed.
 //   job 2 (ceil(B/16)*50 blocks): da2[B,800] = dh . W_fc1 (K = 500 split over 4
-//          waves + LDS reduce), epilogue un-pools through idx2 and applies the
-//          ReLU mask, writing the full dz2[B,50,8,8] (pre-pool conv2 grad).
-//   job 3 (20 blocks): dW_fc2[10,500] = dlogits^T . h, db_fc2.
+//          waves, operands preloaded, LDS reduce); the epilogue un-pools through
+//          idx2 and applies the ReLU mask, writing the full dz2[B,50,8,8].
+//   job 3 (8 blocks): dW_fc2[10,500] = dlogits^T . h (MFMA, K = B), db_fc2, and
+//          the step's loss statistics from the head's per-sample values.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ dh, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ w1, const float* __restrict__ dlog, const float* __restrict__ h,
     float* __restrict__ gw1, float* __restrict__ gb1, float* __restrict__ gw2,
-    float* __restrict__ gb2, float* __restrict__ dz2, int B) {
+    float* __restrict__ gb2, float* __restrict__ dz2, const float* __restrict__ per_sample,
+    float* __restrict__ stats, float loss_scale, int B, u64* dbg) {
   __shared__ f32x4 red[4][64];
   const int blk = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   constexpr int nJ1 = 400;
   const int nJ2 = ((B + 15) / 16) * 50;
+  stamp(dbg, 0);
   if (blk < nJ1) {
     const int tile = blk * 4 + wv;
     const int nt = tile / 50, kt = tile - nt * 50;
@@ -320,23 +422,23 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const bool nv = n < 500;
     const int nc = nv ? n : 499;
     f32x4 c0 = zero4(), c1 = zero4();
-    const int nsteps = (B + 3) / 4;
-    for (int s = 0; s < nsteps; s += 2) {
-      {
-        const int bb = 4 * s + g;
-        const bool bv = bb < B;
-        const int bc = bv ? bb : B - 1;
-        const float av = dh[(size_t)bc * 500 + nc];
-        const float fv = a2[(size_t)bc * 800 + f];
-        c0 = mfma16x16x4((bv && nv) ? av : 0.f, bv ? fv : 0.f, c0);
+    float dbsum = 0.f;
+    for (int base = 0; base < B; base += 64) {
+      float av[16], fv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int bb = min(base + 4 * s + g, B - 1);
+        av[s] = dh[(size_t)bb * 500 + nc];
+        fv[s] = a2[(size_t)bb * 800 + f];
       }
-      if (s + 1 < nsteps) {
-        const int bb = 4 * (s + 1) + g;
-        const bool bv = bb < B;
-        const int bc = bv ? bb : B - 1;
-        const float av = dh[(size_t)bc * 500 + nc];
-        const float fv = a2[(size_t)bc * 800 + f];
-        c1 = mfma16x16x4((bv && nv) ? av : 0.f, bv ? fv : 0.f, c1);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const bool bv = base + 4 * s + g < B;
+        const float a = (bv && nv) ? av[s] : 0.f;
+        dbsum += a;
+        const float fb = bv ? fv[s] : 0.f;
+        if (s & 1) c1 = mfma16x16x4(a, fb, c1);
+        else c0 = mfma16x16x4(a, fb, c0);
       }
     }
     const f32x4 c = c0 + c1;
@@ -346,11 +448,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       if (nn < 500) gw1[(size_t)nn * 800 + kt * 16 + i] = c[r];
     }
     if (kt == 0) {
-      float s = 0.f;
-      for (int bb = g; bb < B; bb += 4) s += dh[(size_t)bb * 500 + nc];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (g == 0 && nv) gb1[n] = s;
+      dbsum += __shfl_xor(dbsum, 16, 64);
+      dbsum += __shfl_xor(dbsum, 32, 64);
+      if (g == 0 && nv) gb1[n] = dbsum;
     }
   } else if (blk < nJ1 + nJ2) {
     const int t2 = blk - nJ1;
@@ -359,21 +459,21 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const bool rv = row < B;
     const int rc = rv ? row : B - 1;
     const int f = kt * 16 + i;
-    const int s0 = wv * 32, s1 = min(125, s0 + 32);
+    const int s0 = wv * 32;  // steps [s0, s0+32) of 125 (wave 3: 29 valid)
+    float av[32], bv[32];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const int k = min(4 * (s0 + s) + g, 499);
+      av[s] = dh[(size_t)rc * 500 + k];
+      bv[s] = w1[(size_t)k * 800 + f];
+    }
     f32x4 c0 = zero4(), c1 = zero4();
-    for (int s = s0; s < s1; s += 2) {
-      {
-        const int k = 4 * s + g;
-        const float av = dh[(size_t)rc * 500 + k];
-        const float bv = w1[(size_t)k * 800 + f];
-        c0 = mfma16x16x4(rv ? av : 0.f, bv, c0);
-      }
-      if (s + 1 < s1) {
-        const int k = 4 * (s + 1) + g;
-        const float av = dh[(size_t)rc * 500 + k];
-        const float bv = w1[(size_t)k * 800 + f];
-        c1 = mfma16x16x4(rv ? av : 0.f, bv, c1);
-      }
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const bool kv = (s0 + s) < 125;
+      const float a = (rv && kv) ? av[s] : 0.f;
+      if (s & 1) c1 = mfma16x16x4(a, bv[s], c1);
+      else c0 = mfma16x16x4(a, bv[s], c0);
     }
     red[wv][lane] = c0 + c1;
     __syncthreads();
@@ -393,29 +493,64 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       z[9] = p == 3 ? d : 0.f;
     }
   } else {
-    const int blk3 = blk - nJ1 - nJ2;
-    const int e = blk3 * 256 + tid;
-    if (e < 5000) {
-      const int j = e / 500, k = e - j * 500;
-      float s = 0.f;
-      for (int bb = 0; bb < B; ++bb) s = fmaf(dlog[(size_t)bb * 10 + j], h[(size_t)bb * 500 + k], s);
-      gw2[e] = s;
+    // dW_fc2[10,500] = dlogits^T . h : M = 10 (16), N = 500 (32 tiles), K = B
+    const int nt = (blk - nJ1 - nJ2) * 4 + wv;  // 0..31
+    const int jc = min(i, 9);
+    const int n = nt * 16 + i;
+    const int ncl = min(n, 499);
+    f32x4 c0 = zero4(), c1 = zero4();
+    float dbsum = 0.f;
+    for (int base = 0; base < B; base += 64) {
+      float av[16], hv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int bb = min(base + 4 * s + g, B - 1);
+        av[s] = dlog[(size_t)bb * 10 + jc];
+        hv[s] = h[(size_t)bb * 500 + ncl];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const bool bv = base + 4 * s + g < B;
+        const float a = (bv && i < 10) ? av[s] : 0.f;
+        dbsum += a;
+        const float hb = bv ? hv[s] : 0.f;
+        if (s & 1) c1 = mfma16x16x4(a, hb, c1);
+        else c0 = mfma16x16x4(a, hb, c0);
+      }
     }
-    if (blk3 == 0 && tid < 10) {
-      float s = 0.f;
-      for (int bb = 0; bb < B; ++bb) s += dlog[(size_t)bb * 10 + tid];
-      gb2[tid] = s;
+    const f32x4 c = c0 + c1;
+    if (n < 500) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = g * 4 + r;
+        if (j < 10) gw2[j * 500 + n] = c[r];
+      }
+    }
+    if (nt == 0) {
+      dbsum += __shfl_xor(dbsum, 16, 64);
+      dbsum += __shfl_xor(dbsum, 32, 64);
+      if (g == 0 && i < 10) gb2[i] = dbsum;
+    }
+    if (nt == 1 && per_sample != nullptr && stats != nullptr) {
+      float ls = 0.f, cs = 0.f;
+      for (int bb = lane; bb < B; bb += 64) { ls += per_sample[2 * bb]; cs += per_sample[2 * bb + 1]; }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if (lane == 0) { stats[0] = ls * loss_scale; stats[1] = cs; }
     }
   }
+  stamp(dbg, 1);
 }
 
 // ---------------------------------------------------------------------------
 // F: conv backward.  grid = (4 input-channel groups of 5, B samples), 8 waves.
+//   phase 1   stage dz2[b] (two layouts), the W2 column slice, a1 slice, xn[b], idx1 slice
 //   phase 2a  dcol[64 pos, 125 (ci,kh,kw)] = dz2[b]^T . W2[:, group]   (MFMA, K = 50)
-//   phase 2b  dW_conv2[50, group] += dz2[b] . im2col(a1[b])             (MFMA, K = 64)
+//   phase 2b  dW_conv2[50, group] partial = dz2[b] . im2col(a1[b])      (MFMA, K = 64)
 //   phase 3   da1 = col2im(dcol); un-pool via idx1 + ReLU mask -> dz1 (LDS)
-//   phase 4   dW_conv1[group, 25] += dz1 . im2col(x[b])                 (MFMA, K = 576)
-//   conv grads are accumulated with fp32 atomics into a segment that launch A zeroed.
+//   phase 4   dW_conv1[group, 25] partial = dz1 . im2col(xn[b])         (MFMA, K = 576)
+//   The partial conv grads are added with fp32 atomics at the very end (so no
+//   barrier waits for them) into a segment that launch A zeroed.
 // ---------------------------------------------------------------------------
 constexpr int F_DS = 66;    // dz_s  [64 co][66]   (== 2 mod 32)
 constexpr int F_DT = 66;    // dzT_s [64 pos][66]
@@ -428,7 +563,8 @@ constexpr int F_OFF_W = F_OFF_DZT + 64 * F_DT;
 constexpr int F_OFF_DCOL = F_OFF_W + 52 * F_WS;
 constexpr int F_OFF_A1 = F_OFF_DCOL + 64 * F_DC;
 constexpr int F_OFF_X = F_OFF_A1 + 5 * 144;
-constexpr int F_LDS = F_OFF_X + 784;
+constexpr int F_OFF_IDX = F_OFF_X + 784;        // 720 uint8 (180 floats)
+constexpr int F_LDS = F_OFF_IDX + 180;
 // aliases of the (dead after phase 2a) weight region:
 constexpr int F_OFF_DZ1 = F_OFF_W;
 constexpr int F_OFF_RED = F_OFF_W + 5 * F_Z1;
@@ -436,9 +572,9 @@ static_assert(5 * F_Z1 + 8 * 256 <= 52 * F_WS, "alias region too small");
 
 __global__ __launch_bounds__(512) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
-    const uint8_t* __restrict__ idx1, BatchSrc src, float* __restrict__ gw2,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ gw1, float* __restrict__ gb1,
-    float* __restrict__ dz1_out, int B) {
+    float* __restrict__ dz1_out, int slab_stride, int B, u64* dbg) {
   extern __shared__ float lds[];
   float* dz_s = lds + F_OFF_DZ;
   float* dzT_s = lds + F_OFF_DZT;
@@ -446,35 +582,72 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
   float* dcol_s = lds + F_OFF_DCOL;
   float* a1_s = lds + F_OFF_A1;
   float* x_s = lds + F_OFF_X;
+  uint8_t* idx_s = reinterpret_cast<uint8_t*>(lds + F_OFF_IDX);
   float* dz1_s = lds + F_OFF_DZ1;
   float* red = lds + F_OFF_RED;
 
   const int cig = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
+  stamp(dbg, 0);
 
-  // ---- phase 1: stage
-  const float* dzb = dz2 + (size_t)b * 3200;
-  for (int e = tid; e < 64 * 64; e += 512) {
-    const int co = e >> 6, pos = e & 63;
-    const float v = co < 50 ? dzb[e] : 0.f;
-    dz_s[co * F_DS + pos] = v;
-    dzT_s[pos * F_DT + co] = v;
-  }
-  for (int e = tid; e < 52 * 128; e += 512) {
-    const int co = e >> 7, j = e & 127;
-    w_s[co * F_WS + j] = (co < 50 && j < 125) ? w2[(size_t)co * 500 + cig * 125 + j] : 0.f;
-  }
-  for (int e = tid; e < 720; e += 512) a1_s[e] = a1[(size_t)b * 2880 + cig * 720 + e];
+  // ---- phase 1: stage (all loads of a thread are independent and unrolled)
   {
-    const int row = batch_row(src, b, B);
-    for (int e = tid; e < 784; e += 512) x_s[e] = load_px(src, row, e);
+    const float* dzb = dz2 + (size_t)b * 3200;
+    // clamped addresses + register selects: no load is predicated (a predicated
+    // load makes hipcc wait vmcnt(0) per element)
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = dzb[min(tid + k * 512, 3199)];
+    float wv_[13];
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int e = tid + k * 512;  // < 6656 = 52*128
+      const int co = min(e >> 7, 49), j = min(e & 127, 124);
+      wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
+    }
+    float av[2], xv[2];
+    uint8_t iv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + k * 512;
+      av[k] = a1[(size_t)b * 2880 + cig * 720 + min(e, 719)];
+      iv[k] = idx1[(size_t)b * 2880 + cig * 720 + min(e, 719)];
+      xv[k] = xn[(size_t)b * 784 + min(e, 783)];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (tid + k * 512 >= 3200) v[k] = 0.f;  // co >= 50
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int e = tid + k * 512;
+      if ((e >> 7) >= 50 || (e & 127) >= 125) wv_[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e = tid + k * 512;
+      const int co = e >> 6, pos = e & 63;
+      dz_s[co * F_DS + pos] = v[k];
+      dzT_s[pos * F_DT + co] = v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int e = tid + k * 512;
+      w_s[(e >> 7) * F_WS + (e & 127)] = wv_[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + k * 512;
+      if (e < 720) { a1_s[e] = av[k]; idx_s[e] = iv[k]; }
+      if (e < 784) x_s[e] = xv[k];
+    }
   }
   __syncthreads();
+  stamp(dbg, 1);
 
+  const int mt = wv & 3, nt0 = (wv >> 2) * 4;
   // ---- phase 2a: dcol = dz2^T . W2 slice   (M = 64 pos, N = 128, K = 52)
   {
-    const int mt = wv & 3, nt0 = (wv >> 2) * 4;
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < 13; ++s) {
@@ -492,8 +665,8 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
         dcol_s[(mt * 16 + g * 4 + r) * F_DC + (nt0 + n) * 16 + i] = acc[n][r];
   }
   // ---- phase 2b: dW_conv2 partial  (M = 64 co, N = 128 (ci,kh,kw), K = 64 pos)
+  f32x4 gacc[4] = {zero4(), zero4(), zero4(), zero4()};
   {
-    const int mt = wv & 3, nt0 = (wv >> 2) * 4;
     int boff[4];
     bool jv[4];
 #pragma unroll
@@ -504,7 +677,6 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
       const int ci = jc / 25, t = jc - ci * 25;
       boff[n] = ci * 144 + (t / 5) * 12 + (t % 5);
     }
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const float av = dz_s[(mt * 16 + i) * F_DS + 4 * s + g];
@@ -512,57 +684,53 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const float bv = jv[n] ? a1_s[boff[n] + poff] : 0.f;
-        acc[n] = mfma16x16x4(av, bv, acc[n]);
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int j = (nt0 + n) * 16 + i;
-      if (j < 125) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = mt * 16 + g * 4 + r;
-          if (co < 50) atomicAdd(&gw2[(size_t)co * 500 + cig * 125 + j], acc[n][r]);
-        }
+        gacc[n] = mfma16x16x4(av, bv, gacc[n]);
       }
     }
   }
+  float b2sum = 0.f;
   if (cig == 0 && tid < 50) {
-    float s = 0.f;
-    for (int p = 0; p < 64; ++p) s += dz_s[tid * F_DS + p];
-    atomicAdd(&gb2[tid], s);
+#pragma unroll 8
+    for (int p = 0; p < 64; ++p) b2sum += dz_s[tid * F_DS + p];
   }
   __syncthreads();
+  stamp(dbg, 2);
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]
-  for (int e = tid; e < 720; e += 512) {
-    const int c = e / 144, p = e - c * 144;
-    const int y = p / 12, x = p - y * 12;
-    float da = 0.f;
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      const int oy = y - kh;
-      if (oy < 0 || oy > 7) continue;
+  for (int k = 0; k < 2; ++k) {
+    const int e = tid + k * 512;
+    if (e < 720) {
+      const int c = e / 144, p = e - c * 144;
+      const int y = p / 12, x = p - y * 12;
+      float da = 0.f;
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const int ox = x - kw;
-        if (ox < 0 || ox > 7) continue;
-        da += dcol_s[(oy * 8 + ox) * F_DC + c * 25 + kh * 5 + kw];
+      for (int kh = 0; kh < 5; ++kh) {
+        const int oy = y - kh;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const int ox = x - kw;
+          const bool ok = (oy >= 0) & (oy <= 7) & (ox >= 0) & (ox <= 7);
+          const int addr = ok ? (oy * 8 + ox) * F_DC + c * 25 + kh * 5 + kw : 0;
+          const float v = dcol_s[addr];
+          da += ok ? v : 0.f;
+        }
       }
-    }
-    const float d = a1_s[e] > 0.f ? da : 0.f;
-    const int pidx = idx1[(size_t)b * 2880 + cig * 720 + e];
-    float* z = dz1_s + c * F_Z1 + (2 * y) * 24 + 2 * x;
-    z[0] = pidx == 0 ? d : 0.f;
-    z[1] = pidx == 1 ? d : 0.f;
-    z[24] = pidx == 2 ? d : 0.f;
-    z[25] = pidx == 3 ? d : 0.f;
-    if (dz1_out != nullptr) {
-      float* zo = dz1_out + (size_t)b * 11520 + (cig * 5 + c) * 576 + (2 * y) * 24 + 2 * x;
-      zo[0] = z[0]; zo[1] = z[1]; zo[24] = z[24]; zo[25] = z[25];
+      const float d = a1_s[e] > 0.f ? da : 0.f;
+      const int pidx = idx_s[e];
+      float* z = dz1_s + c * F_Z1 + (2 * y) * 24 + 2 * x;
+      z[0] = pidx == 0 ? d : 0.f;
+      z[1] = pidx == 1 ? d : 0.f;
+      z[24] = pidx == 2 ? d : 0.f;
+      z[25] = pidx == 3 ? d : 0.f;
+      if (dz1_out != nullptr) {
+        float* zo = dz1_out + (size_t)b * 11520 + (cig * 5 + c) * 576 + (2 * y) * 24 + 2 * x;
+        zo[0] = z[0]; zo[1] = z[1]; zo[24] = z[24]; zo[25] = z[25];
+      }
     }
   }
   __syncthreads();
+  stamp(dbg, 3);
 
   // ---- phase 4: dW_conv1 partial (M = 16 (5 valid ch), N = 32 (25 taps), K = 576)
   {
@@ -588,7 +756,39 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
     }
     reinterpret_cast<f32x4*>(red)[wv * 64 + lane] = c0 + c1;
   }
+  float b1sum = 0.f;
+  if (tid >= 128 && tid < 128 + 5 * 64) {
+    const int c = (tid - 128) >> 6;
+    for (int p = lane; p < 576; p += 64) b1sum += dz1_s[c * F_Z1 + p];
+    b1sum = wave_sum(b1sum);
+  }
   __syncthreads();
+  stamp(dbg, 4);
+
+  // ---- epilogue.  slab_stride > 0: plain stores of this block's partial grads into
+  // the per-sample slab (reduced deterministically by conv_grad_reduce_kernel);
+  // slab_stride == 0: fp32 atomics straight into the grads (standalone use).
+  const bool slab = slab_stride > 0;
+  const size_t so = slab ? (size_t)b * slab_stride : 0;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int j = (nt0 + n) * 16 + i;
+    if (j < 125) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = mt * 16 + g * 4 + r;
+        if (co < 50) {
+          float* dst = gw2 + so + (size_t)co * 500 + cig * 125 + j;
+          if (slab) *dst = gacc[n][r];
+          else atomicAdd(dst, gacc[n][r]);
+        }
+      }
+    }
+  }
+  if (cig == 0 && tid < 50) {
+    if (slab) gb2[so + tid] = b2sum;
+    else atomicAdd(&gb2[tid], b2sum);
+  }
   if (tid < 128) {
     // lane l of ntile nt, reg r: channel row = (l>>4)*4 + r, tap col = nt*16 + (l&15)
     const int nt = tid >> 6, l = tid & 63;
@@ -599,15 +799,56 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = (l >> 4) * 4 + r;
-      if (c < 5 && tt < 25) atomicAdd(&gw1[(cig * 5 + c) * 25 + tt], s[r]);
+      if (c < 5 && tt < 25) {
+        float* dst = gw1 + so + (cig * 5 + c) * 25 + tt;
+        if (slab) *dst = s[r];
+        else atomicAdd(dst, s[r]);
+      }
     }
-  } else if (tid >= 128 && tid < 128 + 5 * 64) {
-    const int c = (tid - 128) >> 6, l = tid & 63;
-    float s = 0.f;
-    for (int p = l; p < 576; p += 64) s += dz1_s[c * F_Z1 + p];
-    s = wave_sum(s);
-    if (l == 0) atomicAdd(&gb1[cig * 5 + c], s);
+  } else if (tid < 128 + 5 * 64 && lane == 0) {
+    float* dst = gb1 + so + cig * 5 + ((tid - 128) >> 6);
+    if (slab) *dst = b1sum;
+    else atomicAdd(dst, b1sum);
   }
+  stamp(dbg, 5);
+}
+
+// ---------------------------------------------------------------------------
+// G: deterministic reduction of the per-sample conv-grad slabs:
+//   out[o] = sum_b P[b * stride + o],  o < n   (n, stride multiples of 4).
+//   256 threads = 64 float4 columns x 4 sample slices; each thread preloads up to
+//   16 samples (one latency round), slices meet in LDS.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void slab_reduce_kernel(
+    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ out, u64* dbg) {
+  __shared__ float4 red[4][64];
+  stamp(dbg, 0);
+  const int tid = threadIdx.x;
+  const int col = blockIdx.x * 64 + (tid & 63);
+  const int slice = tid >> 6;
+  const int n4 = n >> 2, s4 = stride >> 2;
+  const int cc = min(col, n4 - 1);
+  const float4* P4 = reinterpret_cast<const float4*>(P);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int per = (B + 3) / 4;  // samples per slice
+  const int b0 = slice * per, b1 = min(B, b0 + per);
+  for (int base = b0; base < b1; base += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+  }
+  red[slice][tid & 63] = acc;
+  __syncthreads();
+  if (tid < 64 && col < n4) {
+    float4 r = red[0][tid];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) { r.x += red[q][tid].x; r.y += red[q][tid].y; r.z += red[q][tid].z; r.w += red[q][tid].w; }
+    reinterpret_cast<float4*>(out)[col] = r;
+  }
+  stamp(dbg, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -663,6 +904,8 @@ inline BatchSrc make_src(const void* x, int is_u8, const int* labels, const int*
   return s;
 }
 
+u64* g_dbg = nullptr;  // phase-timestamp buffer (tools/phase_profile.py); null in production
+
 }  // namespace
 
 // ===========================================================================
@@ -674,63 +917,68 @@ inline BatchSrc make_src(const void* x, int is_u8, const int* labels, const int*
 
 extern "C" {
 
-int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* perm, const int* cursor,
-                        int host_offset, int n_total, float scale, float shift,
-                        const float* w, const float* bias, float* a1, uint8_t* idx1, int B,
-                        float* zero_ptr, int zero_n, void* stream) {
+void pto_set_debug_buffer(void* p) { g_dbg = reinterpret_cast<u64*>(p); }
+
+int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* labels, const int* perm,
+                        const int* cursor, int host_offset, int n_total, float scale,
+                        float shift, const float* w, const float* bias, float* a1, uint8_t* idx1,
+                        int B, float* zero_ptr, int zero_n, float* xn_out, int* lab_out,
+                        void* stream) {
   PTO_CHECK_B(B);
   if (perm != nullptr && n_total <= 0) return -1;
-  const BatchSrc src = make_src(x, is_u8, nullptr, perm, cursor, host_offset, n_total, scale, shift);
+  if (lab_out != nullptr && labels == nullptr) return -1;
+  const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
   const int blocks = (B * 2880 + 255) / 256;
   hipLaunchKernelGGL(conv1_fwd_pool_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     src, w, bias, a1, idx1, B, zero_ptr, zero_n);
+                     src, w, bias, a1, idx1, B, zero_ptr, zero_n, xn_out, lab_out, g_dbg);
   return (int)hipGetLastError();
 }
 
 int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, float* a2,
                         uint8_t* idx2, int B, void* stream) {
   PTO_CHECK_B(B);
-  hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(256), 0, (hipStream_t)stream,
-                     a1, w, bias, a2, idx2, B);
+  hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(512), 0, (hipStream_t)stream,
+                     a1, w, bias, a2, idx2, B, g_dbg);
   return (int)hipGetLastError();
 }
 
 int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* h, int B,
                       void* stream) {
   PTO_CHECK_B(B);
-  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(32, (B + 15) / 16), dim3(512), 0,
-                     (hipStream_t)stream, x, w, bias, h, B);
+  if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return -2;  // float4 loads
+  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(32, (B + 15) / 16), dim3(640), 0,
+                     (hipStream_t)stream, x, w, bias, h, B, g_dbg);
   return (int)hipGetLastError();
 }
 
-int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* labels,
-                   const int* perm, const int* cursor, int host_offset, int n_total, int B,
+int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* lab, int B,
                    float grad_scale, float loss_scale, float* dlogits, float* dh, float* logp,
-                   float* stats, void* stream) {
+                   float* per_sample, float* stats, void* stream) {
   PTO_CHECK_B(B);
-  if (labels == nullptr) return -1;
-  const BatchSrc src = make_src(nullptr, 0, labels, perm, cursor, host_offset, n_total, 1.f, 0.f);
+  if (lab == nullptr) return -1;
   hipLaunchKernelGGL(head_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, w2,
-                     b2, src, B, grad_scale, loss_scale, dlogits, dh, logp, stats);
+                     b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats,
+                     g_dbg);
   return (int)hipGetLastError();
 }
 
 int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                       const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
-                      float* gb2, float* dz2, int B, void* stream) {
+                      float* gb2, float* dz2, const float* per_sample, float* stats,
+                      float loss_scale, int B, void* stream) {
   PTO_CHECK_B(B);
-  const int blocks = 400 + ((B + 15) / 16) * 50 + 20;
+  const int blocks = 400 + ((B + 15) / 16) * 50 + 8;
   hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, a2,
-                     idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, B);
+                     idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, per_sample, stats, loss_scale,
+                     B, g_dbg);
   return (int)hipGetLastError();
 }
 
 int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                       const void* x, int is_u8, const int* perm, const int* cursor,
-                       int host_offset, int n_total, float scale, float shift, float* gw2,
-                       float* gb2, float* gw1, float* gb1, float* dz1_out, int B, void* stream) {
+                       const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
+                       float* dz1_out, int slab_stride, int B, void* stream) {
   PTO_CHECK_B(B);
-  if (perm != nullptr && n_total <= 0) return -1;
+  if (slab_stride < 0) return -1;
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel,
@@ -739,9 +987,19 @@ int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  const BatchSrc src = make_src(x, is_u8, nullptr, perm, cursor, host_offset, n_total, scale, shift);
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(512), F_LDS * sizeof(float),
-                     (hipStream_t)stream, dz2, w2, a1, idx1, src, gw2, gb2, gw1, gb1, dz1_out, B);
+                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
+                     slab_stride, B, g_dbg);
+  return (int)hipGetLastError();
+}
+
+int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)out)) & 15) return -2;
+  const int blocks = (n / 4 + 63) / 64;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P, B, n,
+                     stride, out, g_dbg);
   return (int)hipGetLastError();
 }
 

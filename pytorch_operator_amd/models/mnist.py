@@ -116,11 +116,10 @@ class FusedMnistTrainer:
         L = self.layout.total
         dev = self.device
         self.flat_params = torch.zeros(L, device=dev)
-        # [stats(16) | grads(L)]: conv1_fwd zeroes stats + the conv grad segment each step
-        self._grad_arena = torch.zeros(16 + L, device=dev)
-        self.stats = self._grad_arena[:16]
-        self.flat_grads = self._grad_arena[16:]
-        self._zero_range = self._grad_arena[:16 + self.layout.conv_end]
+        # grads are fully overwritten every step (no zeroing): fc grads by fc1_bwd, conv
+        # grads by the deterministic slab reduction; stats = (loss, #correct) of the step
+        self.flat_grads = torch.zeros(L, device=dev)
+        self.stats = torch.zeros(16, device=dev)
         self.flat_momentum = torch.zeros(L, device=dev)
         self.params = _views(self.flat_params, self.layout)
         self.grads = _views(self.flat_grads, self.layout)
@@ -145,6 +144,15 @@ class FusedMnistTrainer:
         self.dlogits = torch.empty((B, 10), device=dev)
         self.dh = torch.empty((B, 500), device=dev)
         self.dz2 = torch.empty((B, 50, 8, 8), device=dev)
+        self.xn = torch.empty((B, 784), device=dev)
+        self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
+        self.per_sample = torch.empty((B, 2), device=dev)
+        # per-sample conv-grad slabs in the flat conv-segment layout (pads stay 0)
+        self.conv_slab = torch.zeros((B, self.layout.conv_end), device=dev)
+        self.slab_views = {
+            k: self.conv_slab[0][self.layout.offsets[k]:self.layout.offsets[k] +
+                                 int(torch.Size(shape).numel())].view(shape)
+            for k, shape in PARAM_SPECS if self.layout.offsets[k] < self.layout.conv_end}
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return {k: v.detach().clone() for k, v in self.params.items()}
@@ -168,25 +176,27 @@ class FusedMnistTrainer:
         K, p, g = self.K, self.params, self.grads
         src = source or self.source
         B = self.B if B is None else B
-        a1, idx1 = self.a1[:B], self.idx1[:B]
+        a1, idx1, xn, lab = self.a1[:B], self.idx1[:B], self.xn[:B], self.lab[:B]
         a2, idx2, h1 = self.a2[:B], self.idx2[:B], self.h1[:B]
-        dlog, dh, dz2 = self.dlogits[:B], self.dh[:B], self.dz2[:B]
-        K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=a1, idx=idx1,
-                    zero=self._zero_range)
+        dlog, dh, dz2, ps = self.dlogits[:B], self.dh[:B], self.dz2[:B], self.per_sample[:B]
+        K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=a1, idx=idx1, xn=xn, lab=lab)
         K.conv2_fwd(a1, p["conv2.weight"], p["conv2.bias"], out=a2, idx=idx2)
         K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"], out=h1)
-        K.head(h1, p["fc2.weight"], p["fc2.bias"], src, grad_scale=1.0 / B, loss_scale=1.0 / B,
-               stats=self.stats, dlogits=dlog, dh=dh)
+        K.head(h1, p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B, per_sample=ps,
+               dlogits=dlog, dh=dh)
         K.fc1_bwd(dh, a2, idx2, p["fc1.weight"], dlog, h1, g["fc1.weight"], g["fc1.bias"],
-                  g["fc2.weight"], g["fc2.bias"], dz2=dz2)
+                  g["fc2.weight"], g["fc2.bias"], dz2=dz2, per_sample=ps, stats=self.stats,
+                  loss_scale=1.0 / B)
 
     def backward_conv(self, source=None, B: Optional[int] = None) -> None:
         """Launch F: conv2/conv1 grads (the conv bucket is complete after this)."""
         K, p, g = self.K, self.params, self.grads
-        src = source or self.source
         B = self.B if B is None else B
-        K.conv_bwd(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], src,
-                   g["conv2.weight"], g["conv2.bias"], g["conv1.weight"], g["conv1.bias"])
+        sv = self.slab_views
+        K.conv_bwd(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
+                   sv["conv2.weight"], sv["conv2.bias"], sv["conv1.weight"], sv["conv1.bias"],
+                   slab=self.conv_slab)
+        K.slab_reduce(self.conv_slab, B, self.conv_bucket())
 
     def forward_backward(self, source=None, B: Optional[int] = None) -> None:
         """Launch the 6 fused fwd/bwd kernels for one batch (grads land in flat_grads)."""
@@ -251,6 +261,8 @@ class FusedMnistTrainer:
         a2 = torch.empty((batch_size, 800), device=dev)
         idx2 = torch.empty((batch_size, 800), device=dev, dtype=torch.uint8)
         h1 = torch.empty((batch_size, 500), device=dev)
+        xn = torch.empty((batch_size, 784), device=dev)
+        lab = torch.empty((batch_size,), device=dev, dtype=torch.int32)
         stats = torch.zeros(16, device=dev)
         from ..ops.mnist import BatchSource
         ident = torch.arange(source.n_total, device=dev, dtype=torch.int32) \
@@ -260,10 +272,11 @@ class FusedMnistTrainer:
             sub = BatchSource(source.x, source.labels, perm=ident, host_offset=off,
                               normalize=None)
             sub.scale, sub.shift = source.scale, source.shift
-            K.conv1_fwd(sub, p["conv1.weight"], p["conv1.bias"], B, out=a1[:B], idx=idx1[:B])
+            K.conv1_fwd(sub, p["conv1.weight"], p["conv1.bias"], B, out=a1[:B], idx=idx1[:B],
+                        xn=xn[:B], lab=lab[:B])
             K.conv2_fwd(a1[:B], p["conv2.weight"], p["conv2.bias"], out=a2[:B], idx=idx2[:B])
             K.fc1_fwd(a2[:B], p["fc1.weight"], p["fc1.bias"], out=h1[:B])
-            K.head(h1[:B], p["fc2.weight"], p["fc2.bias"], sub, loss_scale=1.0, want_grad=False,
-                   stats=stats)
+            K.head(h1[:B], p["fc2.weight"], p["fc2.bias"], lab[:B], loss_scale=1.0,
+                   want_grad=False, stats=stats)
         s = stats.cpu()
         return float(s[0]) / n, float(s[1]) / n

@@ -89,16 +89,18 @@ _F = ctypes.c_float
 _L = ctypes.c_long
 
 _SIGNATURES = {
-    "pto_mnist_conv1_fwd": [_VP, _I, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _I, _VP, _I, _VP],
+    "pto_mnist_conv1_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _I, _VP,
+                            _I, _VP, _VP, _VP],
     "pto_mnist_conv2_fwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_head": [_VP, _VP, _VP, _VP, _VP, _VP, _I, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _VP],
-    "pto_mnist_fc1_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_conv_bwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP,
-                           _VP, _VP, _I, _VP],
+    "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _VP],
+    "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
+    "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     "pto_conv_bwd_lds_bytes": [],
 }
+_VOID_FNS = {"pto_set_debug_buffer": [_VP]}
 
 
 def load(build_if_missing: bool = True):
@@ -118,6 +120,10 @@ def load(build_if_missing: bool = True):
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
+        for name, argtypes in _VOID_FNS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = None
         _lib = lib
         return lib
 

@@ -91,8 +91,14 @@ class BatchSource:
 
 def conv1_fwd(src: BatchSource, w: torch.Tensor, b: torch.Tensor, B: int,
               out: Optional[torch.Tensor] = None, idx: Optional[torch.Tensor] = None,
-              zero: Optional[torch.Tensor] = None):
-    """relu(maxpool2(conv1(normalize(x)))) -> (a1 [B,20,12,12] f32, idx1 uint8 argmax)."""
+              zero: Optional[torch.Tensor] = None, xn: Optional[torch.Tensor] = None,
+              lab: Optional[torch.Tensor] = None):
+    """relu(maxpool2(conv1(normalize(x)))).
+
+    Returns ``(a1 [B,20,12,12] f32, idx1 uint8 argmax, xn [B,784] normalised batch,
+    lab [B] int32 gathered labels or None)``.  ``zero`` (optional) is zero-filled by
+    the same launch.
+    """
     lib = _native.load()
     src.check_batch(B)
     _req(w, (20, 1, 5, 5), torch.float32, "conv1.weight")
@@ -100,19 +106,27 @@ def conv1_fwd(src: BatchSource, w: torch.Tensor, b: torch.Tensor, B: int,
     dev = w.device
     out = torch.empty((B, 20, 12, 12), device=dev) if out is None else out
     idx = torch.empty((B, 20, 12, 12), device=dev, dtype=torch.uint8) if idx is None else idx
+    xn = torch.empty((B, 784), device=dev) if xn is None else xn
+    if src.labels is not None and lab is None:
+        lab = torch.empty((B,), device=dev, dtype=torch.int32)
     _req(out, (B, 20, 12, 12), torch.float32, "a1")
     _req(idx, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(xn, (B, 784), torch.float32, "xn")
+    if lab is not None:
+        if src.labels is None:
+            raise ValueError("lab output requested but BatchSource has no labels")
+        _req(lab, (B,), torch.int32, "lab")
     zn = 0
     if zero is not None:
         if zero.dtype != torch.float32 or not zero.is_contiguous():
             raise ValueError("zero must be contiguous fp32")
         zn = zero.numel()
     rc = lib.pto_mnist_conv1_fwd(
-        src.x.data_ptr(), int(src.is_u8), _ptr(src.perm), _ptr(src.cursor), src.host_offset,
-        src.n_total, src.scale, src.shift, w.data_ptr(), b.data_ptr(), out.data_ptr(),
-        idx.data_ptr(), B, _ptr(zero), zn, _stream())
+        src.x.data_ptr(), int(src.is_u8), _ptr(src.labels), _ptr(src.perm), _ptr(src.cursor),
+        src.host_offset, src.n_total, src.scale, src.shift, w.data_ptr(), b.data_ptr(),
+        out.data_ptr(), idx.data_ptr(), B, _ptr(zero), zn, xn.data_ptr(), _ptr(lab), _stream())
     _native.check(rc, "conv1_fwd")
-    return out, idx
+    return out, idx, xn, lab
 
 
 def conv2_fwd(a1: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
@@ -151,23 +165,23 @@ def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out
 
 
-def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, src: BatchSource, *,
+def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *,
          grad_scale: float = 0.0, loss_scale: float = 1.0, want_grad: bool = True,
          want_logp: bool = False, stats: Optional[torch.Tensor] = None,
-         dlogits: Optional[torch.Tensor] = None, dh: Optional[torch.Tensor] = None,
-         logp: Optional[torch.Tensor] = None):
+         per_sample: Optional[torch.Tensor] = None, dlogits: Optional[torch.Tensor] = None,
+         dh: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None):
     """fc2 + log_softmax + nll (+ d(logits), dh with the fc1 ReLU mask).
 
-    ``stats`` (fp32 [>=2]) accumulates ``loss*loss_scale`` and the correct count.
+    ``lab``: int32 [B] targets (``conv1_fwd`` gathers them).  ``per_sample`` (fp32
+    [B,2]) receives (loss, correct) per sample; ``stats`` (fp32 [>=2]) accumulates
+    ``sum(loss)*loss_scale`` and the correct count atomically.
     """
     lib = _native.load()
     B = h.shape[0]
     _req(h, (B, 500), torch.float32, "h1")
     _req(w, (10, 500), torch.float32, "fc2.weight")
     _req(b, (10,), torch.float32, "fc2.bias")
-    if src.labels is None:
-        raise ValueError("BatchSource has no labels")
-    src.check_batch(B)
+    _req(lab, (B,), torch.int32, "lab")
     dev = h.device
     if want_grad:
         dlogits = torch.empty((B, 10), device=dev) if dlogits is None else dlogits
@@ -181,18 +195,24 @@ def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, src: BatchSource, *,
         _req(logp, (B, 10), torch.float32, "logp")
     else:
         logp = None
+    if per_sample is not None:
+        _req(per_sample, (B, 2), torch.float32, "per_sample")
     if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
         raise ValueError("stats must be fp32 with >= 2 elements")
-    rc = lib.pto_mnist_head(h.data_ptr(), w.data_ptr(), b.data_ptr(), src.labels.data_ptr(),
-                            _ptr(src.perm), _ptr(src.cursor), src.host_offset, src.n_total, B,
+    rc = lib.pto_mnist_head(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), B,
                             float(grad_scale), float(loss_scale), _ptr(dlogits), _ptr(dh),
-                            _ptr(logp), _ptr(stats), _stream())
+                            _ptr(logp), _ptr(per_sample), _ptr(stats), _stream())
     _native.check(rc, "head")
     return dlogits, dh, logp
 
 
-def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None):
-    """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked)."""
+def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_sample=None,
+            stats=None, loss_scale: float = 1.0):
+    """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked).
+
+    With ``per_sample`` (head output) and ``stats``, also writes
+    ``stats[0] = sum(loss)*loss_scale`` and ``stats[1] = #correct``.
+    """
     lib = _native.load()
     B = dh.shape[0]
     _req(dh, (B, 500), torch.float32, "dh")
@@ -207,18 +227,25 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None):
     _req(gb2, (10,), torch.float32, "grad fc2.bias")
     dz2 = torch.empty((B, 50, 8, 8), device=dh.device) if dz2 is None else dz2
     _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    if per_sample is not None:
+        _req(per_sample, (B, 2), torch.float32, "per_sample")
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),
-                               gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), B, _stream())
+                               gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
+                               _ptr(stats), float(loss_scale), B, _stream())
     _native.check(rc, "fc1_bwd")
     return dz2
 
 
-def conv_bwd(dz2, w2, a1, idx1, src: BatchSource, gw2, gb2, gw1, gb1, want_dz1=False):
+def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
+             slab: Optional[torch.Tensor] = None):
     """conv2 weight/bias grads, dz1 (internal), conv1 weight/bias grads.
 
-    The conv grads are ACCUMULATED (fp32 atomics): zero them first (the fused step
-    zeroes them inside conv1_fwd via ``zero=``).
+    ``xn`` is the normalised batch [B,784] (``conv1_fwd`` output).
+    Without ``slab`` the conv grads are ACCUMULATED with fp32 atomics (zero them
+    first).  With ``slab`` ([B, S] fp32, and gw2/gb2/gw1/gb1 being views into
+    ``slab[0]``), every sample writes its partial grads into its own slab row
+    (plain stores); ``slab_reduce`` then sums the rows deterministically.
     """
     lib = _native.load()
     B = dz2.shape[0]
@@ -226,19 +253,47 @@ def conv_bwd(dz2, w2, a1, idx1, src: BatchSource, gw2, gb2, gw1, gb1, want_dz1=F
     _req(w2, (50, 20, 5, 5), torch.float32, "conv2.weight")
     _req(a1, (B, 20, 12, 12), torch.float32, "a1")
     _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(xn, (B, 784), torch.float32, "xn")
     _req(gw2, (50, 20, 5, 5), torch.float32, "grad conv2.weight")
     _req(gb2, (50,), torch.float32, "grad conv2.bias")
     _req(gw1, (20, 1, 5, 5), torch.float32, "grad conv1.weight")
     _req(gb1, (20,), torch.float32, "grad conv1.bias")
-    src.check_batch(B)
+    stride = 0
+    if slab is not None:
+        if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or \
+                slab.dtype != torch.float32:
+            raise ValueError("slab must be contiguous fp32 [>=B, S]")
+        stride = slab.shape[1]
+        lo, hi = slab.data_ptr(), slab.data_ptr() + stride * 4
+        for t in (gw2, gb2, gw1, gb1):
+            if not (lo <= t.data_ptr() and t.data_ptr() + t.numel() * 4 <= hi):
+                raise ValueError("with slab=, grad views must lie inside slab[0]")
     dz1 = torch.empty((B, 20, 24, 24), device=dz2.device) if want_dz1 else None
     rc = lib.pto_mnist_conv_bwd(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(),
-                                src.x.data_ptr(), int(src.is_u8), _ptr(src.perm),
-                                _ptr(src.cursor), src.host_offset, src.n_total, src.scale,
-                                src.shift, gw2.data_ptr(), gb2.data_ptr(), gw1.data_ptr(),
-                                gb1.data_ptr(), _ptr(dz1), B, _stream())
+                                xn.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), gw1.data_ptr(),
+                                gb1.data_ptr(), _ptr(dz1), stride, B, _stream())
     _native.check(rc, "conv_bwd")
     return dz1
+
+
+def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor) -> torch.Tensor:
+    """out[o] = sum_{b<B} slab[b, o] for o < out.numel() (deterministic order)."""
+    lib = _native.load()
+    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2:
+        raise ValueError("slab must be contiguous fp32 [rows, S]")
+    if B > slab.shape[0]:
+        raise ValueError("B exceeds slab rows")
+    n = out.numel()
+    if out.dtype != torch.float32 or not out.is_contiguous() or n > slab.shape[1]:
+        raise ValueError("out must be contiguous fp32 with <= S elements")
+    rc = lib.pto_slab_reduce(slab.data_ptr(), B, n, slab.shape[1], out.data_ptr(), _stream())
+    _native.check(rc, "slab_reduce")
+    return out
+
+
+def set_debug_buffer(buf: Optional[torch.Tensor]) -> None:
+    """Route per-phase wall_clock64 stamps of every kernel into ``buf`` (int64, or None)."""
+    _native.load().pto_set_debug_buffer(_ptr(buf))
 
 
 def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, *, lr: float,

@@ -45,15 +45,18 @@ def test_forward_kernels_match_torch(lib, B):
     p = {k: v.to(dev).contiguous() for k, v in sd.items()}
     x, y = _data(B, seed=B)
     src = K.BatchSource(x.to(dev), y.to(dev))
-    a1, idx1 = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    a1, idx1, xn, lab = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
     a2, idx2 = K.conv2_fwd(a1, p["conv2.weight"], p["conv2.bias"])
     h1 = K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"])
     stats = torch.zeros(16, device=dev)
-    _, _, logp = K.head(h1, p["fc2.weight"], p["fc2.bias"], src, want_grad=False, want_logp=True,
+    _, _, logp = K.head(h1, p["fc2.weight"], p["fc2.bias"], lab, want_grad=False, want_logp=True,
                         stats=stats, loss_scale=1.0 / B)
     torch.cuda.synchronize()
 
-    xn = _norm(x)
+    assert torch.equal(lab.cpu(), y)
+    xn_ref = _norm(x)
+    assert _rel(xn, xn_ref.view(B, 784)) < 1e-6
+    xn = xn_ref
     z1 = F.conv2d(xn, sd["conv1.weight"], sd["conv1.bias"])
     r1, ri1 = F.max_pool2d(F.relu(z1), 2, 2, return_indices=True)
     assert _rel(a1, r1) < 1e-5
@@ -124,13 +127,13 @@ def test_conv_bwd_dz1_matches_autograd(lib):
     # feed torch's dz2 into the kernel and compare dz1 / conv grads
     p = {k: v.to(dev).contiguous() for k, v in sd.items()}
     src = K.BatchSource(x.to(dev), y.to(dev))
-    a1, idx1 = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    a1, idx1, xnk, _ = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
     gw2 = torch.zeros(50, 20, 5, 5, device=dev)
     gb2 = torch.zeros(50, device=dev)
     gw1 = torch.zeros(20, 1, 5, 5, device=dev)
     gb1 = torch.zeros(20, device=dev)
     dz2 = z2.grad.contiguous().to(dev)
-    dz1 = K.conv_bwd(dz2, p["conv2.weight"], a1, idx1, src, gw2, gb2, gw1, gb1, want_dz1=True)
+    dz1 = K.conv_bwd(dz2, p["conv2.weight"], a1, idx1, xnk, gw2, gb2, gw1, gb1, want_dz1=True)
     torch.cuda.synchronize()
     # dz1 = grad wrt conv1 pre-activation output z1
     z1b = F.conv2d(xn, sd["conv1.weight"], sd["conv1.bias"]).requires_grad_(True)

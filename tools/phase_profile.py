@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-phase timing of the fused MNIST kernels from in-kernel wall_clock64 stamps.
+
+Each kernel, when given a debug buffer, has thread 0 of every block record the
+100 MHz wall clock at its phase boundaries.  For each kernel this prints the
+kernel span (first block start -> last stamp), and per phase the mean / max
+block time, which tells whether a kernel is load-latency-, compute- or
+tail-bound.  Run on the GPU box:  python tools/phase_profile.py
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from pytorch_operator_amd.data.synthetic import make_synthetic_mnist  # noqa: E402
+from pytorch_operator_amd.models.mnist import FusedMnistTrainer  # noqa: E402
+from pytorch_operator_amd.ops import mnist as K  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda")
+    ds = make_synthetic_mnist(6400, device=dev)
+    cur = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cur)
+    B = int(os.environ.get("B", "64"))
+    tr = FusedMnistTrainer(batch_size=B, source=src)
+    for _ in range(20):
+        tr.train_step()
+    torch.cuda.synchronize()
+    dbg = torch.zeros(1 << 16, dtype=torch.int64, device=dev)
+    p, g = tr.params, tr.grads
+    launches = [
+        ("conv1_fwd", lambda: K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=tr.a1,
+                                          idx=tr.idx1, xn=tr.xn, lab=tr.lab)),
+        ("conv2_fwd", lambda: K.conv2_fwd(tr.a1, p["conv2.weight"], p["conv2.bias"], out=tr.a2,
+                                          idx=tr.idx2)),
+        ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
+        ("head", lambda: K.head(tr.h1, p["fc2.weight"], p["fc2.bias"], tr.lab, grad_scale=1.0 / B,
+                                per_sample=tr.per_sample, dlogits=tr.dlogits, dh=tr.dh)),
+        ("fc1_bwd", lambda: K.fc1_bwd(tr.dh, tr.a2, tr.idx2, p["fc1.weight"], tr.dlogits, tr.h1,
+                                      g["fc1.weight"], g["fc1.bias"], g["fc2.weight"],
+                                      g["fc2.bias"], dz2=tr.dz2, per_sample=tr.per_sample,
+                                      stats=tr.stats, loss_scale=1.0 / B)),
+        ("conv_bwd", lambda: K.conv_bwd(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn,
+                                        tr.slab_views["conv2.weight"], tr.slab_views["conv2.bias"],
+                                        tr.slab_views["conv1.weight"], tr.slab_views["conv1.bias"],
+                                        slab=tr.conv_slab)),
+        ("slab_reduce", lambda: K.slab_reduce(tr.conv_slab, B, tr.conv_bucket())),
+    ]
+    reps = 20
+    for name, fn in launches:
+        spans, phase_means, phase_maxs = [], None, None
+        for _ in range(reps):
+            dbg.zero_()
+            K.set_debug_buffer(dbg)
+            fn()
+            torch.cuda.synchronize()
+            K.set_debug_buffer(None)
+            d = dbg.view(-1, 16).cpu()
+            used = d[:, 0] > 0
+            d = d[used].double()
+            nph = int((d > 0).sum(1).max())
+            t0 = d[:, 0].min()
+            last = d[:, :nph].max()
+            spans.append(float(last - t0) / 100.0)  # 100 MHz -> us
+            deltas = (d[:, 1:nph] - d[:, 0:nph - 1]) / 100.0
+            m = deltas.mean(0)
+            mx = deltas.max(0).values
+            phase_means = m if phase_means is None else phase_means + m
+            phase_maxs = mx if phase_maxs is None else torch.maximum(phase_maxs, mx)
+            starts = (d[:, 0] - t0) / 100.0
+        spans.sort()
+        pm = (phase_means / reps).tolist()
+        print(f"{name:10s} blocks={int(used.sum()):5d} span med={spans[len(spans)//2]:7.2f}us "
+              f"start-skew max={float(starts.max()):6.2f}us  phases(mean/max us): " +
+              "  ".join(f"p{i}->{i+1} {a:.2f}/{b:.2f}" for i, (a, b) in
+                        enumerate(zip(pm, phase_maxs.tolist()))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
