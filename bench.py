@@ -41,6 +41,8 @@ def parse_args(argv=None):
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per hipGraph replay (world 1 only; 0 = auto)")
     p.add_argument("--dataset-size", type=int, default=60000)
+    p.add_argument("--overlap", type=int, default=1, help="side-stream overlap in the step (1/0)")
+    p.add_argument("--fuse-conv12", type=int, default=0)
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -74,6 +76,8 @@ def main(argv=None):
         sync = FlatGradAllReduce() if world > 1 else None
         tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
                                seed=1, grad_sync=sync)
+        tr.overlap = bool(args.overlap)
+        tr.fuse_conv12 = bool(args.fuse_conv12)
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph
@@ -97,7 +101,7 @@ def main(argv=None):
         def run(n):
             runner.run(n)
         steps = args.steps - args.steps % runner.steps_per_graph
-        mode_desc = f"{args.mode}(spg={runner.steps_per_graph})"
+        mode_desc = f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap})"
     else:
         from pytorch_operator_amd.models.mnist import Net
         import torch.nn.functional as F

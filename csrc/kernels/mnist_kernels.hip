@@ -237,6 +237,143 @@ __global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// AB: conv1 + conv2 forward fused (the training path).  grid = (4 conv2 output
+//   channel groups, B samples), 8 waves.  Every block recomputes conv1 + ReLU +
+//   pool for its sample on the VALU straight into the conv2 im2col image in LDS
+//   (4x redundant, ~1 us, cheaper than a launch boundary + an HBM round trip);
+//   the cg == 0 block publishes a1/idx1 (for the backward), xn and lab.
+//   conv2 then runs exactly as conv2_fwd_pool_kernel.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void conv12_fwd_kernel(
+    BatchSrc src, const float* __restrict__ w1, const float* __restrict__ b1,
+    const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
+    uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
+    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
+  __shared__ float img[784];
+  __shared__ float w1s[520];
+  __shared__ float in_s[20 * C2_CS];
+  __shared__ float w_s[16 * C2_WS];
+  __shared__ f32x4 red[4][64];
+  const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  stamp(dbg, 0);
+  const int row = batch_row(src, b, B);
+  const bool pub = cg == 0;
+  {
+    const float x0 = load_px(src, row, tid);
+    const float x1 = load_px(src, row, min(tid + 512, 783));
+    const float wv = w1[min(tid, 499)];
+    const float bv1 = b1[min(tid, 19)];
+    float4 wq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = min(tid + k * 512, 16 * 125 - 1);
+      const int j = e / 125, q = e - j * 125;
+      const int co = min(cg * 16 + j, 49);
+      wq[k] = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
+    }
+    img[tid] = x0;
+    if (tid + 512 < 784) img[tid + 512] = x1;
+    if (tid < 500) w1s[tid] = wv;
+    if (tid < 20) w1s[500 + tid] = bv1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * 512;
+      if (e < 16 * 125) {
+        const int j = e / 125, q = e - j * 125;
+        float4 v = wq[k];
+        if (cg * 16 + j >= 50) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
+        d[0] = make_float2(v.x, v.y);
+        d[1] = make_float2(v.z, v.w);
+      }
+    }
+    if (pub) {
+      xn_out[(size_t)b * 784 + tid] = x0;
+      if (tid + 512 < 784) xn_out[(size_t)b * 784 + tid + 512] = x1;
+      if (tid == 0 && lab_out != nullptr) lab_out[b] = src.labels[row];
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 1);
+  // conv1 + bias + ReLU + 2x2 max-pool (VALU), 2880 outputs over 512 threads
+#pragma unroll 1
+  for (int k = 0; k < 6; ++k) {
+    const int e = tid + k * 512;
+    if (e < 2880) {
+      const int c = e / 144, p = e - c * 144;
+      const int ph = p / 12, pw = p - ph * 12;
+      const float* im = img + (2 * ph) * 28 + 2 * pw;
+      float patch[6][6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) patch[r][q] = im[r * 28 + q];
+      const float* wc = w1s + c * 25;
+      float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float wv = wc[kh * 5 + kw];
+          o00 = fmaf(patch[kh][kw], wv, o00);
+          o01 = fmaf(patch[kh][kw + 1], wv, o01);
+          o10 = fmaf(patch[kh + 1][kw], wv, o10);
+          o11 = fmaf(patch[kh + 1][kw + 1], wv, o11);
+        }
+      const float bc = w1s[500 + c];
+      o00 += bc; o01 += bc; o10 += bc; o11 += bc;
+      float m = o00; int am = 0;
+      if (o01 > m) { m = o01; am = 1; }
+      if (o10 > m) { m = o10; am = 2; }
+      if (o11 > m) { m = o11; am = 3; }
+      const float v = fmaxf(m, 0.f);
+      in_s[c * C2_CS + ph * C2_RS + pw] = v;
+      if (pub) {
+        a1[(size_t)b * 2880 + e] = v;
+        idx1[(size_t)b * 2880 + e] = (uint8_t)am;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 2);
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int pt = wv & 3, khalf = wv >> 2;
+  const int i = lane & 15, g = lane >> 4;
+  const int oh = 2 * pt + (i >> 3), ow = i & 7;
+  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
+  const float* Bb = w_s + i * C2_WS + g * 25;
+  f32x4 acc;
+  if (khalf == 0) acc = conv2_k_range<0, 13>(Ab, Bb);
+  else acc = conv2_k_range<13, 25>(Ab, Bb);
+  if (khalf == 1) red[pt][lane] = acc;
+  __syncthreads();
+  stamp(dbg, 3);
+  if (khalf == 1) return;
+  acc += red[pt][lane];
+  const int co = cg * 16 + i;
+  const float bco = (co < 50) ? bias[co] : 0.f;
+  const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
+  float mA = v0; int aA = 0;
+  if (v1 > mA) { mA = v1; aA = 1; }
+  float mB = v2; int aB = 0;
+  if (v3 > mB) { mB = v3; aB = 1; }
+  const float pA = __shfl_xor(mA, 32, 64);
+  const int paA = __shfl_xor(aA, 32, 64);
+  const float pB = __shfl_xor(mB, 32, 64);
+  const int paB = __shfl_xor(aB, 32, 64);
+  if (g < 2 && co < 50) {
+    if (pA > mA) { mA = pA; aA = 2 + paA; }
+    if (pB > mB) { mB = pB; aB = 2 + paB; }
+    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);
+    a2[o] = fmaxf(mA, 0.f);
+    a2[o + 1] = fmaxf(mB, 0.f);
+    idx2[o] = (uint8_t)aA;
+    idx2[o + 1] = (uint8_t)aB;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // C: fc1 forward: h = relu(x[B,800] . W[500,800]^T + b).
 //   grid = (32 N-tiles, ceil(B/16) M-tiles), 10 waves; wave w reduces K range
 //   [80w, 80w+80), lane group g owns k = 80w + 20g + [0,20) (5 float4 loads per
@@ -407,13 +544,16 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ dlog, const float* __restrict__ h,
     float* __restrict__ gw1, float* __restrict__ gb1, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ dz2, const float* __restrict__ per_sample,
-    float* __restrict__ stats, float loss_scale, int B, u64* dbg) {
+    float* __restrict__ stats, float loss_scale, int jobs, int B, u64* dbg) {
   __shared__ f32x4 red[4][64];
-  const int blk = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  constexpr int nJ1 = 400;
-  const int nJ2 = ((B + 15) / 16) * 50;
+  // jobs bit0: dW_fc1/db_fc1, bit1: dz2, bit2: dW_fc2/db_fc2/stats.  Block ids are
+  // laid out job1 | job2 | job3 with absent jobs taking no blocks.
+  const int nJ1 = (jobs & 1) ? 400 : 0;
+  const int nJ2 = (jobs & 2) ? ((B + 15) / 16) * 50 : 0;
+  const int blk = blockIdx.x;
   stamp(dbg, 0);
   if (blk < nJ1) {
     const int tile = blk * 4 + wv;
@@ -852,6 +992,65 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// G+H: slab reduction fused with the SGD(momentum) update of the same elements
+//   (single-process path: the conv grads never make a round trip before the
+//   update).  Also writes the reduced grads (inspection / grad-norm logging) and
+//   advances the device batch cursor.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
+    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ gout,
+    float* __restrict__ p, float* __restrict__ buf, float lr, float momentum, float dampening,
+    float wd, float grad_scale, int nesterov, int first_step, int* __restrict__ step_counter,
+    u64* dbg) {
+  __shared__ float4 red[4][64];
+  stamp(dbg, 0);
+  const int tid = threadIdx.x;
+  const int col = blockIdx.x * 64 + (tid & 63);
+  const int slice = tid >> 6;
+  const int n4 = n >> 2, s4 = stride >> 2;
+  const int cc = min(col, n4 - 1);
+  const float4* P4 = reinterpret_cast<const float4*>(P);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int per = (B + 3) / 4;
+  const int b0 = slice * per, b1 = min(B, b0 + per);
+  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bb = pp;
+  if (tid < 64) {  // prefetch the parameters + momentum this column updates
+    pp = reinterpret_cast<const float4*>(p)[cc];
+    bb = reinterpret_cast<const float4*>(buf)[cc];
+  }
+  for (int base = b0; base < b1; base += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+  }
+  red[slice][tid & 63] = acc;
+  __syncthreads();
+  if (tid < 64 && col < n4) {
+    float4 r = red[0][tid];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) { r.x += red[q][tid].x; r.y += red[q][tid].y; r.z += red[q][tid].z; r.w += red[q][tid].w; }
+    if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
+    float* pe = &pp.x; float* be = &bb.x; const float* ge = &r.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = ge[e] * grad_scale + wd * pe[e];
+      if (momentum != 0.f) {
+        be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
+        d = nesterov ? d + momentum * be[e] : be[e];
+      }
+      pe[e] -= lr * d;
+    }
+    reinterpret_cast<float4*>(p)[col] = pp;
+    reinterpret_cast<float4*>(buf)[col] = bb;
+  }
+  if (step_counter != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(step_counter, 1);
+  stamp(dbg, 1);
+}
+
+// ---------------------------------------------------------------------------
 // H: SGD with momentum over a flat fp32 buffer (torch.optim.SGD semantics:
 // buf = momentum*buf + (1-dampening)*g (buf = g on the first step),
 // p -= lr * (nesterov ? g + momentum*buf : buf)); grad_scale folds the DDP 1/world.
@@ -942,6 +1141,21 @@ int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, floa
   return (int)hipGetLastError();
 }
 
+int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int* perm,
+                         const int* cursor, int host_offset, int n_total, float scale,
+                         float shift, const float* w1, const float* b1, const float* w2,
+                         const float* b2, float* a1, uint8_t* idx1, float* xn_out, int* lab_out,
+                         float* a2, uint8_t* idx2, int B, void* stream) {
+  PTO_CHECK_B(B);
+  if (perm != nullptr && n_total <= 0) return -1;
+  if (lab_out != nullptr && labels == nullptr) return -1;
+  if (((uintptr_t)w2) & 15) return -2;
+  const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
+  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(512), 0, (hipStream_t)stream, src, w1,
+                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, g_dbg);
+  return (int)hipGetLastError();
+}
+
 int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* h, int B,
                       void* stream) {
   PTO_CHECK_B(B);
@@ -965,12 +1179,14 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
 int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                       const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                       float* gb2, float* dz2, const float* per_sample, float* stats,
-                      float loss_scale, int B, void* stream) {
+                      float loss_scale, int jobs, int B, void* stream) {
   PTO_CHECK_B(B);
-  const int blocks = 400 + ((B + 15) / 16) * 50 + 8;
+  if (jobs <= 0 || jobs > 7) return -1;
+  const int blocks = ((jobs & 1) ? 400 : 0) + ((jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
+                     ((jobs & 4) ? 8 : 0);
   hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, a2,
                      idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, per_sample, stats, loss_scale,
-                     B, g_dbg);
+                     jobs, B, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -1014,6 +1230,20 @@ int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, flo
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g,
                      buf, n, lr, momentum, dampening, wd, grad_scale, nesterov, first_step,
                      step_counter);
+  return (int)hipGetLastError();
+}
+
+int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, float* p,
+                        float* buf, float lr, float momentum, float dampening, float wd,
+                        float grad_scale, int nesterov, int first_step, int* step_counter,
+                        void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf)) & 15) return -2;
+  const int blocks = (n / 4 + 63) / 64;
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
+                     B, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
+                     nesterov, first_step, step_counter, g_dbg);
   return (int)hipGetLastError();
 }
 

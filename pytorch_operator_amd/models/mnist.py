@@ -132,6 +132,10 @@ class FusedMnistTrainer:
         self.source = source
         self._alloc(self.B)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # schedule knobs (measured on MI355X, see profiles/): conv1+conv2 as one launch
+        # recomputes conv1 4x per sample and loses to two launches; side-stream overlap
+        self.fuse_conv12 = False
+        self.overlap = True
 
     # ---------------------------------------------------------------- state
     def _alloc(self, B: int):
@@ -171,35 +175,75 @@ class FusedMnistTrainer:
         return self.flat_grads[:self.layout.conv_end]
 
     # ---------------------------------------------------------------- step
-    def forward_backward_fc(self, source=None, B: Optional[int] = None) -> None:
-        """Launches A-E: forward, loss, fc1/fc2 grads (the fc bucket is complete after this)."""
-        K, p, g = self.K, self.params, self.grads
+    #
+    # Launch schedule of one step (main = current stream, side = self._side):
+    #
+    #   main: conv12_fwd -> fc1_fwd -> head -+-> fc1_bwd[dgrad] -+-> conv_bwd -> tail(conv)
+    #   side:                                +-> fc1_bwd[wgrad+fc2] ------+-> tail(fc) -+
+    #                                                          (waits dgrad)            join
+    #
+    # fc1_bwd's weight-gradient half and the fc-parameter update run beside the
+    # input-gradient / conv-backward chain, which is the critical path.  tail() is the
+    # SGD update (single process) or the bucket all-reduce + SGD (DDP, grad_sync).
+    def _side_stream(self) -> torch.cuda.Stream:
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def forward(self, source=None, B: Optional[int] = None) -> None:
+        """Launches conv12_fwd, fc1_fwd, head (loss, d(logits), dh)."""
+        K, p = self.K, self.params
         src = source or self.source
         B = self.B if B is None else B
-        a1, idx1, xn, lab = self.a1[:B], self.idx1[:B], self.xn[:B], self.lab[:B]
-        a2, idx2, h1 = self.a2[:B], self.idx2[:B], self.h1[:B]
-        dlog, dh, dz2, ps = self.dlogits[:B], self.dh[:B], self.dz2[:B], self.per_sample[:B]
-        K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=a1, idx=idx1, xn=xn, lab=lab)
-        K.conv2_fwd(a1, p["conv2.weight"], p["conv2.bias"], out=a2, idx=idx2)
-        K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"], out=h1)
-        K.head(h1, p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B, per_sample=ps,
-               dlogits=dlog, dh=dh)
-        K.fc1_bwd(dh, a2, idx2, p["fc1.weight"], dlog, h1, g["fc1.weight"], g["fc1.bias"],
-                  g["fc2.weight"], g["fc2.bias"], dz2=dz2, per_sample=ps, stats=self.stats,
-                  loss_scale=1.0 / B)
+        if self.fuse_conv12:
+            K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
+                         p["conv2.bias"], B, a1=self.a1[:B], idx1=self.idx1[:B], xn=self.xn[:B],
+                         lab=self.lab[:B], a2=self.a2[:B], idx2=self.idx2[:B])
+        else:
+            K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=self.a1[:B],
+                        idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
+            K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
+                        idx=self.idx2[:B])
+        K.fc1_fwd(self.a2[:B], p["fc1.weight"], p["fc1.bias"], out=self.h1[:B])
+        K.head(self.h1[:B], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
+               per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B])
 
-    def backward_conv(self, source=None, B: Optional[int] = None) -> None:
-        """Launch F: conv2/conv1 grads (the conv bucket is complete after this)."""
+    def _fc1_bwd(self, B: int, jobs: int) -> None:
         K, p, g = self.K, self.params, self.grads
-        B = self.B if B is None else B
+        K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
+                  self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
+                  dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
+                  loss_scale=1.0 / B, jobs=jobs)
+
+    def _conv_bwd(self, B: int) -> None:
+        K, p = self.K, self.params
         sv = self.slab_views
         K.conv_bwd(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
                    sv["conv2.weight"], sv["conv2.bias"], sv["conv1.weight"], sv["conv1.bias"],
                    slab=self.conv_slab)
-        K.slab_reduce(self.conv_slab, B, self.conv_bucket())
+
+    def _sgd(self, lo: int, hi: int, grad_scale: float, advance_cursor: bool) -> None:
+        self.K.sgd_momentum_(self.flat_params[lo:hi], self.flat_grads[lo:hi],
+                             self.flat_momentum[lo:hi], lr=self.lr, momentum=self.momentum,
+                             dampening=self.dampening, weight_decay=self.weight_decay,
+                             nesterov=self.nesterov, grad_scale=grad_scale,
+                             first_step=self._first_step,
+                             step_counter=self.cursor if advance_cursor else None)
+
+    def forward_backward_fc(self, source=None, B: Optional[int] = None) -> None:
+        """Forward + loss + fc backward (the fc bucket and dz2 are complete after this)."""
+        B = self.B if B is None else B
+        self.forward(source, B)
+        self._fc1_bwd(B, self.K.FC1_BWD_ALL)
+
+    def backward_conv(self, source=None, B: Optional[int] = None) -> None:
+        """conv backward + deterministic slab reduction into the conv bucket."""
+        B = self.B if B is None else B
+        self._conv_bwd(B)
+        self.K.slab_reduce(self.conv_slab, B, self.conv_bucket())
 
     def forward_backward(self, source=None, B: Optional[int] = None) -> None:
-        """Launch the 6 fused fwd/bwd kernels for one batch (grads land in flat_grads)."""
+        """All fwd/bwd launches for one batch; grads land in flat_grads (DDP hooks fire)."""
         self.forward_backward_fc(source, B)
         if self.grad_sync is not None:
             self.grad_sync.fc_ready(self.fc_bucket())
@@ -210,16 +254,56 @@ class FusedMnistTrainer:
     def optimizer_step(self, advance_cursor: bool = True, grad_scale: Optional[float] = None) -> None:
         if grad_scale is None:
             grad_scale = self.grad_sync.finish() if self.grad_sync is not None else 1.0
-        self.K.sgd_momentum_(self.flat_params, self.flat_grads, self.flat_momentum, lr=self.lr,
-                             momentum=self.momentum, dampening=self.dampening,
-                             weight_decay=self.weight_decay, nesterov=self.nesterov,
-                             grad_scale=grad_scale, first_step=self._first_step,
-                             step_counter=self.cursor if advance_cursor else None)
+        self._sgd(0, self.layout.total, grad_scale, advance_cursor)
         self._first_step = False
 
-    def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True):
-        self.forward_backward(source, B)
-        self.optimizer_step(advance_cursor)
+    def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True,
+                   overlap: Optional[bool] = None):
+        """One full training step (forward, backward, [all-reduce], SGD)."""
+        overlap = self.overlap if overlap is None else overlap
+        if self.grad_sync is not None:
+            self.forward_backward(source, B)
+            self.optimizer_step(advance_cursor)
+            return
+        if not overlap:
+            K = self.K
+            B = self.B if B is None else B
+            ce = self.layout.conv_end
+            self.forward(source, B)
+            self._fc1_bwd(B, K.FC1_BWD_ALL)
+            self._sgd(ce, self.layout.total, 1.0, False)
+            self._conv_bwd(B)
+            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
+                               self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+                               dampening=self.dampening, weight_decay=self.weight_decay,
+                               nesterov=self.nesterov, first_step=self._first_step,
+                               step_counter=self.cursor if advance_cursor else None)
+            self._first_step = False
+            return
+            self.forward_backward(source, B)
+            self.optimizer_step(advance_cursor)
+            return
+        K = self.K
+        B = self.B if B is None else B
+        ce = self.layout.conv_end
+        main = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        self.forward(source, B)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)
+        self._fc1_bwd(B, K.FC1_BWD_DGRAD)
+        side.wait_stream(main)  # fc1.weight is read by the dgrad launch: update after it
+        with torch.cuda.stream(side):
+            self._sgd(ce, self.layout.total, 1.0, False)
+        self._conv_bwd(B)
+        K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
+                           self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+                           dampening=self.dampening, weight_decay=self.weight_decay,
+                           nesterov=self.nesterov, first_step=self._first_step,
+                           step_counter=self.cursor if advance_cursor else None)
+        main.wait_stream(side)
+        self._first_step = False
 
     def loss(self) -> float:
         return float(self.stats[0].item())
@@ -272,9 +356,9 @@ class FusedMnistTrainer:
             sub = BatchSource(source.x, source.labels, perm=ident, host_offset=off,
                               normalize=None)
             sub.scale, sub.shift = source.scale, source.shift
-            K.conv1_fwd(sub, p["conv1.weight"], p["conv1.bias"], B, out=a1[:B], idx=idx1[:B],
-                        xn=xn[:B], lab=lab[:B])
-            K.conv2_fwd(a1[:B], p["conv2.weight"], p["conv2.bias"], out=a2[:B], idx=idx2[:B])
+            K.conv12_fwd(sub, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
+                         p["conv2.bias"], B, a1=a1[:B], idx1=idx1[:B], xn=xn[:B], lab=lab[:B],
+                         a2=a2[:B], idx2=idx2[:B])
             K.fc1_fwd(a2[:B], p["fc1.weight"], p["fc1.bias"], out=h1[:B])
             K.head(h1[:B], p["fc2.weight"], p["fc2.bias"], lab[:B], loss_scale=1.0,
                    want_grad=False, stats=stats)

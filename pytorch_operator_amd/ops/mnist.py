@@ -149,6 +149,42 @@ def conv2_fwd(a1: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out, idx
 
 
+def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
+               b2: torch.Tensor, B: int, a1=None, idx1=None, xn=None, lab=None, a2=None,
+               idx2=None):
+    """conv1+pool+conv2+pool fused (one launch): returns (a1, idx1, xn, lab, a2, idx2)."""
+    lib = _native.load()
+    src.check_batch(B)
+    _req(w1, (20, 1, 5, 5), torch.float32, "conv1.weight")
+    _req(b1, (20,), torch.float32, "conv1.bias")
+    _req(w2, (50, 20, 5, 5), torch.float32, "conv2.weight")
+    _req(b2, (50,), torch.float32, "conv2.bias")
+    dev = w1.device
+    a1 = torch.empty((B, 20, 12, 12), device=dev) if a1 is None else a1
+    idx1 = torch.empty((B, 20, 12, 12), device=dev, dtype=torch.uint8) if idx1 is None else idx1
+    xn = torch.empty((B, 784), device=dev) if xn is None else xn
+    if src.labels is not None and lab is None:
+        lab = torch.empty((B,), device=dev, dtype=torch.int32)
+    a2 = torch.empty((B, 800), device=dev) if a2 is None else a2
+    idx2 = torch.empty((B, 800), device=dev, dtype=torch.uint8) if idx2 is None else idx2
+    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
+    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(xn, (B, 784), torch.float32, "xn")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
+    if lab is not None:
+        if src.labels is None:
+            raise ValueError("lab output requested but BatchSource has no labels")
+        _req(lab, (B,), torch.int32, "lab")
+    rc = lib.pto_mnist_conv12_fwd(
+        src.x.data_ptr(), int(src.is_u8), _ptr(src.labels), _ptr(src.perm), _ptr(src.cursor),
+        src.host_offset, src.n_total, src.scale, src.shift, w1.data_ptr(), b1.data_ptr(),
+        w2.data_ptr(), b2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(), _ptr(lab),
+        a2.data_ptr(), idx2.data_ptr(), B, _stream())
+    _native.check(rc, "conv12_fwd")
+    return a1, idx1, xn, lab, a2, idx2
+
+
 def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
             out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """relu(x @ w.T + b) for x [B,800], w [500,800]."""
@@ -206,11 +242,19 @@ def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *
     return dlogits, dh, logp
 
 
+FC1_BWD_WGRAD = 1   # dW_fc1, db_fc1
+FC1_BWD_DGRAD = 2   # dz2 (input grad, un-pooled + ReLU-masked)
+FC1_BWD_FC2 = 4     # dW_fc2, db_fc2, loss statistics
+FC1_BWD_ALL = 7
+
+
 def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_sample=None,
-            stats=None, loss_scale: float = 1.0):
+            stats=None, loss_scale: float = 1.0, jobs: int = FC1_BWD_ALL):
     """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked).
 
-    With ``per_sample`` (head output) and ``stats``, also writes
+    ``jobs`` selects which of the three independent parts to launch (so the weight
+    gradients can run on a side stream concurrently with the input gradient).
+    With ``per_sample`` (head output) and ``stats``, job FC2 also writes
     ``stats[0] = sum(loss)*loss_scale`` and ``stats[1] = #correct``.
     """
     lib = _native.load()
@@ -232,7 +276,7 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),
                                gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
-                               _ptr(stats), float(loss_scale), B, _stream())
+                               _ptr(stats), float(loss_scale), int(jobs), B, _stream())
     _native.check(rc, "fc1_bwd")
     return dz2
 
@@ -289,6 +333,27 @@ def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor) -> torch.Tensor:
     rc = lib.pto_slab_reduce(slab.data_ptr(), B, n, slab.shape[1], out.data_ptr(), _stream())
     _native.check(rc, "slab_reduce")
     return out
+
+
+def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: torch.Tensor,
+                     buf: torch.Tensor, *, lr: float, momentum: float = 0.0,
+                     dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                     grad_scale: float = 1.0, first_step: bool = False,
+                     step_counter: Optional[torch.Tensor] = None) -> None:
+    """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch)."""
+    lib = _native.load()
+    n = params.numel()
+    for t, nm in ((grads, "grads"), (params, "params"), (buf, "momentum_buffer")):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
+    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
+            slab.shape[1] < n or slab.shape[0] < B:
+        raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
+    rc = lib.pto_slab_reduce_sgd(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
+                                 params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
+                                 float(dampening), float(weight_decay), float(grad_scale),
+                                 int(nesterov), int(first_step), _ptr(step_counter), _stream())
+    _native.check(rc, "slab_reduce_sgd")
 
 
 def set_debug_buffer(buf: Optional[torch.Tensor]) -> None:

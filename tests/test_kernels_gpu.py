@@ -189,3 +189,25 @@ def test_training_reduces_loss_on_learnable_synthetic_data(lib):
     assert sum(losses[-10:]) / 10 < 0.5 * sum(losses[:10]) / 10
     _, acc = tr.evaluate(K.BatchSource(ds.images, ds.labels), n=2000)
     assert acc > 0.9
+
+
+@pytest.mark.parametrize("B", [64, 13])
+def test_conv12_fused_matches_separate_kernels(lib, B):
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    sd = reference_init(4)
+    p = {k: v.to(dev).contiguous() for k, v in sd.items()}
+    n = 300
+    x, y = _data(n, seed=5, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(1)).to(torch.int32).to(dev)
+    src = K.BatchSource(x.to(dev), y.to(dev), perm=perm, host_offset=250)
+    a1, idx1, xn, lab = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    a2, idx2 = K.conv2_fwd(a1, p["conv2.weight"], p["conv2.bias"])
+    f = K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"], p["conv2.bias"], B)
+    torch.cuda.synchronize()
+    assert torch.equal(f[0], a1) and torch.equal(f[1], idx1)
+    assert torch.equal(f[2], xn) and torch.equal(f[3], lab)
+    assert torch.equal(f[4], a2) and torch.equal(f[5], idx2)
+    rows = perm.cpu()[(torch.arange(B) + 250) % n].long()
+    assert torch.equal(lab.cpu(), y[rows])

@@ -32,22 +32,20 @@ def main():
     dbg = torch.zeros(1 << 16, dtype=torch.int64, device=dev)
     p, g = tr.params, tr.grads
     launches = [
-        ("conv1_fwd", lambda: K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=tr.a1,
-                                          idx=tr.idx1, xn=tr.xn, lab=tr.lab)),
-        ("conv2_fwd", lambda: K.conv2_fwd(tr.a1, p["conv2.weight"], p["conv2.bias"], out=tr.a2,
-                                          idx=tr.idx2)),
+        ("conv12_fwd", lambda: K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"],
+                                            p["conv2.weight"], p["conv2.bias"], B, a1=tr.a1,
+                                            idx1=tr.idx1, xn=tr.xn, lab=tr.lab, a2=tr.a2,
+                                            idx2=tr.idx2)),
         ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
         ("head", lambda: K.head(tr.h1, p["fc2.weight"], p["fc2.bias"], tr.lab, grad_scale=1.0 / B,
                                 per_sample=tr.per_sample, dlogits=tr.dlogits, dh=tr.dh)),
-        ("fc1_bwd", lambda: K.fc1_bwd(tr.dh, tr.a2, tr.idx2, p["fc1.weight"], tr.dlogits, tr.h1,
-                                      g["fc1.weight"], g["fc1.bias"], g["fc2.weight"],
-                                      g["fc2.bias"], dz2=tr.dz2, per_sample=tr.per_sample,
-                                      stats=tr.stats, loss_scale=1.0 / B)),
-        ("conv_bwd", lambda: K.conv_bwd(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn,
-                                        tr.slab_views["conv2.weight"], tr.slab_views["conv2.bias"],
-                                        tr.slab_views["conv1.weight"], tr.slab_views["conv1.bias"],
-                                        slab=tr.conv_slab)),
-        ("slab_reduce", lambda: K.slab_reduce(tr.conv_slab, B, tr.conv_bucket())),
+        ("fc1_bwd_w", lambda: tr._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)),
+        ("fc1_bwd_d", lambda: tr._fc1_bwd(B, K.FC1_BWD_DGRAD)),
+        ("conv_bwd", lambda: tr._conv_bwd(B)),
+        ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(),
+                                                    tr.flat_params[:tr.layout.conv_end],
+                                                    tr.flat_momentum[:tr.layout.conv_end],
+                                                    lr=0.0, momentum=0.5)),
     ]
     reps = 20
     for name, fn in launches:
