@@ -41,8 +41,8 @@ def parse_args(argv=None):
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per hipGraph replay (world 1 only; 0 = auto)")
     p.add_argument("--dataset-size", type=int, default=60000)
-    p.add_argument("--overlap", type=int, default=1, help="side-stream overlap in the step (1/0)")
-    p.add_argument("--fuse-conv12", type=int, default=0)
+    p.add_argument("--overlap", type=int, default=0, help="side-stream overlap in the step (1/0)")
+    p.add_argument("--fuse-conv12", type=int, default=1)
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 

@@ -45,6 +45,7 @@ __device__ __forceinline__ void stamp(u64* dbg, int phase) {
   if (dbg != nullptr && threadIdx.x == 0) {
     const int blk = blockIdx.y * gridDim.x + blockIdx.x;
     dbg[blk * 16 + phase] = (u64)wall_clock64();
+    dbg[blk * 16 + 8 + phase] = (u64)clock64();  // shader clock -> effective GHz per phase
   }
 }
 
@@ -295,42 +296,81 @@ __global__ __launch_bounds__(512) void conv12_fwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 1);
-  // conv1 + bias + ReLU + 2x2 max-pool (VALU), 2880 outputs over 512 threads
+  // conv1 + bias + ReLU + 2x2 max-pool as an implicit GEMM on MFMA: 36 position
+  // tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 2 channel tiles (0-15, 16-19)
+  // x 7 K-steps (25 taps, zero-padded to 28 through the weight fragments).  The
+  // pool epilogue is the same register/lane^32 pairing as conv2's.
+  {
+    const int lane = tid & 63, wv = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    int toff[7];
+    float bw[2][7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int tap = 4 * s + g;
+      const int tc = tap < 25 ? tap : 24;
+      toff[s] = (tc / 5) * 28 + (tc % 5);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = nt * 16 + i;
+        const float wv_ = w1s[min(c, 19) * 25 + tc];
+        bw[nt][s] = (c < 20 && tap < 25) ? wv_ : 0.f;
+      }
+    }
+    // 72 tasks = 36 position tiles x 2 channel tiles; wave w takes tasks w, w+8, ..
+    // (9 each) as three independent accumulator chains per iteration (MFMA latency
+    // 40 cycles > 32-cycle issue: one chain alone would idle the matrix pipe).
 #pragma unroll 1
-  for (int k = 0; k < 6; ++k) {
-    const int e = tid + k * 512;
-    if (e < 2880) {
-      const int c = e / 144, p = e - c * 144;
-      const int ph = p / 12, pw = p - ph * 12;
-      const float* im = img + (2 * ph) * 28 + 2 * pw;
-      float patch[6][6];
+    for (int t0 = wv; t0 < 72; t0 += 24) {
+      f32x4 acc[3];
+      const float* ibs[3];
+      int nts[3];
 #pragma unroll
-      for (int r = 0; r < 6; ++r)
+      for (int u = 0; u < 3; ++u) {
+        const int t = t0 + 8 * u;
+        const int pt1 = t >> 1;
+        nts[u] = t & 1;
+        const int py = pt1 / 3, px = pt1 - py * 3;
+        ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
+        acc[u] = zero4();
+      }
 #pragma unroll
-        for (int q = 0; q < 6; ++q) patch[r][q] = im[r * 28 + q];
-      const float* wc = w1s + c * 25;
-      float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+      for (int s = 0; s < 7; ++s)
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
+        for (int u = 0; u < 3; ++u)
+          acc[u] = mfma16x16x4(ibs[u][toff[s]], nts[u] ? bw[1][s] : bw[0][s], acc[u]);
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) {
-          const float wv = wc[kh * 5 + kw];
-          o00 = fmaf(patch[kh][kw], wv, o00);
-          o01 = fmaf(patch[kh][kw + 1], wv, o01);
-          o10 = fmaf(patch[kh + 1][kw], wv, o10);
-          o11 = fmaf(patch[kh + 1][kw + 1], wv, o11);
+      for (int u = 0; u < 3; ++u) {
+        const int t = t0 + 8 * u;
+        const int pt1 = t >> 1, nt = t & 1;
+        const int py = pt1 / 3, px = pt1 - py * 3;
+        const int c = nt * 16 + i;
+        const float bc = w1s[500 + min(c, 19)];
+        const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc,
+                    v3 = acc[u][3] + bc;
+        float mA = v0; int aA = 0;
+        if (v1 > mA) { mA = v1; aA = 1; }
+        float mB = v2; int aB = 0;
+        if (v3 > mB) { mB = v3; aB = 1; }
+        const float pA = __shfl_xor(mA, 32, 64);
+        const int paA = __shfl_xor(aA, 32, 64);
+        const float pB = __shfl_xor(mB, 32, 64);
+        const int paB = __shfl_xor(aB, 32, 64);
+        if (g < 2 && c < 20) {
+          if (pA > mA) { mA = pA; aA = 2 + paA; }
+          if (pB > mB) { mB = pB; aB = 2 + paB; }
+          const int pw = 4 * px + 2 * (g & 1);
+          const float va = fmaxf(mA, 0.f), vb = fmaxf(mB, 0.f);
+          in_s[c * C2_CS + py * C2_RS + pw] = va;
+          in_s[c * C2_CS + py * C2_RS + pw + 1] = vb;
+          if (pub) {
+            const size_t o = (size_t)b * 2880 + c * 144 + py * 12 + pw;
+            a1[o] = va;
+            a1[o + 1] = vb;
+            idx1[o] = (uint8_t)aA;
+            idx1[o + 1] = (uint8_t)aB;
+          }
         }
-      const float bc = w1s[500 + c];
-      o00 += bc; o01 += bc; o10 += bc; o11 += bc;
-      float m = o00; int am = 0;
-      if (o01 > m) { m = o01; am = 1; }
-      if (o10 > m) { m = o10; am = 2; }
-      if (o11 > m) { m = o11; am = 3; }
-      const float v = fmaxf(m, 0.f);
-      in_s[c * C2_CS + ph * C2_RS + pw] = v;
-      if (pub) {
-        a1[(size_t)b * 2880 + e] = v;
-        idx1[(size_t)b * 2880 + e] = (uint8_t)am;
       }
     }
   }
@@ -692,16 +732,18 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 //   The partial conv grads are added with fp32 atomics at the very end (so no
 //   barrier waits for them) into a segment that launch A zeroed.
 // ---------------------------------------------------------------------------
-constexpr int F_DS = 66;    // dz_s  [64 co][66]   (== 2 mod 32)
-constexpr int F_DT = 66;    // dzT_s [64 pos][66]
-constexpr int F_WS = 144;   // w_s   [52 co][144]  (== 16 mod 32)
-constexpr int F_DC = 132;   // dcol  [64 pos][132] (4*132 == 16 mod 32)
+// LDS row strides (ds_read_b32/ds_write_b32 banks = word % 32, 32-lane groups):
+constexpr int F_DS = 66;    // dz_s   [64 co][66]    A of 2b: lanes = co rows  (== 2 mod 32)
+constexpr int F_D8 = 80;    // dz80_s [52 co][80]    B of 2a: lanes = pos cols, +row per g (== 16 mod 32)
+constexpr int F_WS = 144;   // w_s    [52 co][144]   A of 2a: lanes = j cols, +row per g (== 16 mod 32)
+constexpr int F_DC = 68;    // dcolT  [128 j][68]    2a C writes (4*68 == 16 mod 32); col2im reads
+                            //                       walk pos with lanes -> conflict-free
 constexpr int F_Z1 = 580;   // dz1_s [5][580]      (== 4 mod 32)
 constexpr int F_OFF_DZ = 0;
-constexpr int F_OFF_DZT = F_OFF_DZ + 64 * F_DS;
-constexpr int F_OFF_W = F_OFF_DZT + 64 * F_DT;
+constexpr int F_OFF_D8 = F_OFF_DZ + 64 * F_DS;
+constexpr int F_OFF_W = F_OFF_D8 + 52 * F_D8;
 constexpr int F_OFF_DCOL = F_OFF_W + 52 * F_WS;
-constexpr int F_OFF_A1 = F_OFF_DCOL + 64 * F_DC;
+constexpr int F_OFF_A1 = F_OFF_DCOL + 128 * F_DC;
 constexpr int F_OFF_X = F_OFF_A1 + 5 * 144;
 constexpr int F_OFF_IDX = F_OFF_X + 784;        // 720 uint8 (180 floats)
 constexpr int F_LDS = F_OFF_IDX + 180;
@@ -717,7 +759,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
     float* __restrict__ dz1_out, int slab_stride, int B, u64* dbg) {
   extern __shared__ float lds[];
   float* dz_s = lds + F_OFF_DZ;
-  float* dzT_s = lds + F_OFF_DZT;
+  float* dz80_s = lds + F_OFF_D8;
   float* w_s = lds + F_OFF_W;
   float* dcol_s = lds + F_OFF_DCOL;
   float* a1_s = lds + F_OFF_A1;
@@ -768,7 +810,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
       const int e = tid + k * 512;
       const int co = e >> 6, pos = e & 63;
       dz_s[co * F_DS + pos] = v[k];
-      dzT_s[pos * F_DT + co] = v[k];
+      if (co < 52) dz80_s[co * F_D8 + pos] = v[k];
     }
 #pragma unroll
     for (int k = 0; k < 13; ++k) {
@@ -786,15 +828,16 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
   stamp(dbg, 1);
 
   const int mt = wv & 3, nt0 = (wv >> 2) * 4;
-  // ---- phase 2a: dcol = dz2^T . W2 slice   (M = 64 pos, N = 128, K = 52)
+  // ---- phase 2a: dcolT[j][pos] = W2 slice^T . dz2   (M = 128 j, N = 64 pos, K = 52)
   {
+    const int pt = wv & 3, jt0 = (wv >> 2) * 4;
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < 13; ++s) {
-      const float av = dzT_s[(mt * 16 + i) * F_DT + 4 * s + g];
+      const float bv = dz80_s[(4 * s + g) * F_D8 + pt * 16 + i];
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const float bv = w_s[(4 * s + g) * F_WS + (nt0 + n) * 16 + i];
+        const float av = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
         acc[n] = mfma16x16x4(av, bv, acc[n]);
       }
     }
@@ -802,7 +845,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
     for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        dcol_s[(mt * 16 + g * 4 + r) * F_DC + (nt0 + n) * 16 + i] = acc[n][r];
+        dcol_s[((jt0 + n) * 16 + g * 4 + r) * F_DC + pt * 16 + i] = acc[n][r];
   }
   // ---- phase 2b: dW_conv2 partial  (M = 64 co, N = 128 (ci,kh,kw), K = 64 pos)
   f32x4 gacc[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -851,7 +894,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
         for (int kw = 0; kw < 5; ++kw) {
           const int ox = x - kw;
           const bool ok = (oy >= 0) & (oy <= 7) & (ox >= 0) & (ox <= 7);
-          const int addr = ok ? (oy * 8 + ox) * F_DC + c * 25 + kh * 5 + kw : 0;
+          const int addr = ok ? (c * 25 + kh * 5 + kw) * F_DC + oy * 8 + ox : 0;
           const float v = dcol_s[addr];
           da += ok ? v : 0.f;
         }
@@ -1001,10 +1044,33 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     const float* __restrict__ P, int B, int n, int stride, float* __restrict__ gout,
     float* __restrict__ p, float* __restrict__ buf, float lr, float momentum, float dampening,
     float wd, float grad_scale, int nesterov, int first_step, int* __restrict__ step_counter,
-    u64* dbg) {
+    float* __restrict__ p2, const float* __restrict__ g2, float* __restrict__ buf2, int n2,
+    int red_blocks, u64* dbg) {
   __shared__ float4 red[4][64];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= red_blocks) {
+    // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
+    const int v = (blockIdx.x - red_blocks) * 256 + tid;
+    if (v < (n2 >> 2)) {
+      float4 pp = reinterpret_cast<float4*>(p2)[v];
+      const float4 gg = reinterpret_cast<const float4*>(g2)[v];
+      float4 bb = reinterpret_cast<float4*>(buf2)[v];
+      float* pe = &pp.x; const float* ge = &gg.x; float* be = &bb.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float d = ge[e] * grad_scale + wd * pe[e];
+        if (momentum != 0.f) {
+          be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
+          d = nesterov ? d + momentum * be[e] : be[e];
+        }
+        pe[e] -= lr * d;
+      }
+      reinterpret_cast<float4*>(p2)[v] = pp;
+      reinterpret_cast<float4*>(buf2)[v] = bb;
+    }
+    return;
+  }
   const int col = blockIdx.x * 64 + (tid & 63);
   const int slice = tid >> 6;
   const int n4 = n >> 2, s4 = stride >> 2;
@@ -1236,14 +1302,19 @@ int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, flo
 int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, float* p,
                         float* buf, float lr, float momentum, float dampening, float wd,
                         float grad_scale, int nesterov, int first_step, int* step_counter,
-                        void* stream) {
+                        float* p2, const float* g2, float* buf2, int n2, void* stream) {
   PTO_CHECK_B(B);
   if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
-  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf)) & 15) return -2;
-  const int blocks = (n / 4 + 63) / 64;
+  if (n2 < 0 || (n2 & 3) || (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)))
+    return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) |
+       ((uintptr_t)p2) | ((uintptr_t)g2) | ((uintptr_t)buf2)) & 15)
+    return -2;
+  const int red_blocks = (n / 4 + 63) / 64;
+  const int blocks = red_blocks + (n2 / 4 + 255) / 256;
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
                      B, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
-                     nesterov, first_step, step_counter, g_dbg);
+                     nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks, g_dbg);
   return (int)hipGetLastError();
 }
 

@@ -134,8 +134,8 @@ class FusedMnistTrainer:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         # schedule knobs (measured on MI355X, see profiles/): conv1+conv2 as one launch
         # recomputes conv1 4x per sample and loses to two launches; side-stream overlap
-        self.fuse_conv12 = False
-        self.overlap = True
+        self.fuse_conv12 = True
+        self.overlap = False
 
     # ---------------------------------------------------------------- state
     def _alloc(self, B: int):
@@ -271,13 +271,15 @@ class FusedMnistTrainer:
             ce = self.layout.conv_end
             self.forward(source, B)
             self._fc1_bwd(B, K.FC1_BWD_ALL)
-            self._sgd(ce, self.layout.total, 1.0, False)
             self._conv_bwd(B)
+            # one tail launch: reduce conv slabs + SGD(conv) | SGD(fc), advance cursor
             K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
                                self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
                                dampening=self.dampening, weight_decay=self.weight_decay,
                                nesterov=self.nesterov, first_step=self._first_step,
-                               step_counter=self.cursor if advance_cursor else None)
+                               step_counter=self.cursor if advance_cursor else None,
+                               extra=(self.flat_params[ce:], self.flat_grads[ce:],
+                                      self.flat_momentum[ce:]))
             self._first_step = False
             return
             self.forward_backward(source, B)

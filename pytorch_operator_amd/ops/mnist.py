@@ -339,8 +339,13 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                      buf: torch.Tensor, *, lr: float, momentum: float = 0.0,
                      dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                      grad_scale: float = 1.0, first_step: bool = False,
-                     step_counter: Optional[torch.Tensor] = None) -> None:
-    """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch)."""
+                     step_counter: Optional[torch.Tensor] = None,
+                     extra: Optional[tuple] = None) -> None:
+    """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch).
+
+    ``extra=(params2, grads2, buf2)``: also apply the same SGD to a second,
+    already-reduced range in the same launch (e.g. the fc parameters).
+    """
     lib = _native.load()
     n = params.numel()
     for t, nm in ((grads, "grads"), (params, "params"), (buf, "momentum_buffer")):
@@ -349,10 +354,19 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
     if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
             slab.shape[1] < n or slab.shape[0] < B:
         raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
+    p2 = g2 = b2 = None
+    n2 = 0
+    if extra is not None:
+        p2, g2, b2 = extra
+        n2 = p2.numel()
+        for t, nm in ((p2, "params2"), (g2, "grads2"), (b2, "buf2")):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n2:
+                raise ValueError(f"{nm} must be contiguous fp32 with {n2} elements")
     rc = lib.pto_slab_reduce_sgd(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
                                  params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
                                  float(dampening), float(weight_decay), float(grad_scale),
-                                 int(nesterov), int(first_step), _ptr(step_counter), _stream())
+                                 int(nesterov), int(first_step), _ptr(step_counter), _ptr(p2),
+                                 _ptr(g2), _ptr(b2), n2, _stream())
     _native.check(rc, "slab_reduce_sgd")
 
 

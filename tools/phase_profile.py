@@ -56,14 +56,16 @@ def main():
             fn()
             torch.cuda.synchronize()
             K.set_debug_buffer(None)
-            d = dbg.view(-1, 16).cpu()
-            used = d[:, 0] > 0
-            d = d[used].double()
+            dfull = dbg.view(-1, 16).cpu()
+            used = dfull[:, 0] > 0
+            d = dfull[used][:, :8].double()
+            dc = dfull[used][:, 8:].double()
             nph = int((d > 0).sum(1).max())
             t0 = d[:, 0].min()
             last = d[:, :nph].max()
             spans.append(float(last - t0) / 100.0)  # 100 MHz -> us
             deltas = (d[:, 1:nph] - d[:, 0:nph - 1]) / 100.0
+            ghz = float(((dc[:, nph - 1] - dc[:, 0]) / ((d[:, nph - 1] - d[:, 0]) * 10.0)).mean())
             m = deltas.mean(0)
             mx = deltas.max(0).values
             phase_means = m if phase_means is None else phase_means + m
@@ -71,7 +73,7 @@ def main():
             starts = (d[:, 0] - t0) / 100.0
         spans.sort()
         pm = (phase_means / reps).tolist()
-        print(f"{name:10s} blocks={int(used.sum()):5d} span med={spans[len(spans)//2]:7.2f}us "
+        print(f"{name:10s} blocks={int(used.sum()):5d} clk={ghz:4.2f}GHz span med={spans[len(spans)//2]:7.2f}us "
               f"start-skew max={float(starts.max()):6.2f}us  phases(mean/max us): " +
               "  ".join(f"p{i}->{i+1} {a:.2f}/{b:.2f}" for i, (a, b) in
                         enumerate(zip(pm, phase_maxs.tolist()))), flush=True)
