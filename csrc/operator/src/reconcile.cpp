@@ -1,0 +1,618 @@
+#include "pto/reconcile.hpp"
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "pto/yaml_lite.hpp"
+
+namespace pto {
+
+// pkg/common/config/config.go:9-20 (same YAML, same fields)
+const char* const kDefaultInitContainerTemplate = R"(
+- name: init-pytorch
+  image: {{.InitContainerImage}}
+  imagePullPolicy: IfNotPresent
+  resources:
+    limits:
+      cpu: 100m
+      memory: 20Mi
+    requests:
+      cpu: 50m
+      memory: 10Mi
+  command: ['sh', '-c', 'until nslookup {{.MasterAddr}}; do echo waiting for master; sleep 2; done;'])";
+
+namespace {
+
+std::string fmt(const char* f, const std::string& a) {
+  char buf[512];
+  std::snprintf(buf, sizeof buf, f, a.c_str());
+  return buf;
+}
+
+Json* ensure_obj(Json& parent, const char* key) {
+  Json& v = parent[key];
+  if (!v.is_object()) v = Json::object();
+  return &v;
+}
+
+int label_index(const Json& obj, bool* ok) {
+  const Json* v = obj.path({"metadata", "labels", kLabelReplicaIndex});
+  *ok = false;
+  if (!v || !v->is_string()) return -1;
+  const std::string& s = v->as_string();
+  if (s.empty()) return -1;
+  char* end = nullptr;
+  long x = std::strtol(s.c_str(), &end, 10);
+  if (!end || *end != '\0') return -1;
+  *ok = true;
+  return (int)x;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ helpers
+std::vector<Json> filter_by_replica_type(const std::vector<Json>& objs, const std::string& rt) {
+  std::vector<Json> out;
+  for (const auto& o : objs) {
+    const Json* v = o.path({"metadata", "labels", kLabelReplicaType});
+    if (v && v->is_string() && v->as_string() == rt) out.push_back(o);
+  }
+  return out;
+}
+
+std::vector<std::vector<Json>> slices_by_index(const std::vector<Json>& objs, int replicas) {
+  std::vector<std::vector<Json>> out((size_t)std::max(replicas, 0));
+  for (const auto& o : objs) {
+    bool ok = false;
+    int idx = label_index(o, &ok);
+    if (!ok) continue;  // missing / malformed index label: ignored (reference logs a warning)
+    if (idx < 0 || idx >= replicas) continue;
+    out[(size_t)idx].push_back(o);
+  }
+  return out;
+}
+
+std::vector<Json> init_containers(const ControllerConfig& cfg, const std::string& master_addr,
+                                  std::string* error) {
+  std::vector<Json> out;
+  try {
+    std::string text = render_template(
+        cfg.init_container_template,
+        {{"MasterAddr", master_addr}, {"InitContainerImage", cfg.init_container_image}});
+    Json parsed = yaml_parse(text);
+    if (!parsed.is_array()) {
+      *error = "init container template must be a YAML list of containers";
+      return out;
+    }
+    for (const auto& c : parsed.as_array()) out.push_back(c);
+  } catch (const std::exception& e) {
+    *error = e.what();
+  }
+  return out;
+}
+
+std::string set_cluster_spec(Json& tmpl, const Json& job, int32_t total, int index,
+                             const std::string& rtype) {
+  int rank = index;
+  auto port = port_of(job, kReplicaMaster);
+  if (!port) return "failed to found the port";
+  std::string master_addr = gen_general_name(job_name(job), "master", "0");
+  if (rtype == kReplicaMaster) {
+    if (rank != 0) return "invalid config: There should be only a single master with index=0";
+    master_addr = "localhost";
+  } else {
+    rank = rank + 1;
+  }
+  Json* containers = tmpl.path({"spec", "containers"});
+  if (!containers || !containers->is_array()) return "";
+  for (auto& c : containers->as_array()) {
+    Json& env = c["env"];
+    if (!env.is_array()) env = Json::array();
+    auto add = [&](const char* k, const std::string& v) {
+      Json e = Json::object();
+      e["name"] = k;
+      e["value"] = v;
+      env.push_back(e);
+    };
+    add("MASTER_PORT", std::to_string(*port));
+    add("MASTER_ADDR", master_addr);
+    add("WORLD_SIZE", std::to_string(total));
+    add("RANK", std::to_string(rank));
+    add("PYTHONUNBUFFERED", "0");
+  }
+  return "";
+}
+
+static void inject_rccl_env(Json& tmpl, const ControllerConfig& cfg) {
+  Json* containers = tmpl.path({"spec", "containers"});
+  if (!containers || !containers->is_array()) return;
+  for (auto& c : containers->as_array()) {
+    if (c.str_or("name") != kDefaultContainerName) continue;
+    Json& env = c["env"];
+    if (!env.is_array()) env = Json::array();
+    auto has = [&](const std::string& k) {
+      for (const auto& e : env.as_array())
+        if (e.str_or("name") == k) return true;
+      return false;
+    };
+    auto add = [&](const std::string& k, const std::string& v) {
+      if (has(k)) return;
+      Json e = Json::object();
+      e["name"] = k;
+      e["value"] = v;
+      env.push_back(e);
+    };
+    add("LOCAL_RANK", "0");  // one amd.com/gpu per pod: the pod sees its GPU as device 0
+    for (const auto& kv : cfg.rccl_env) add(kv.first, kv.second);
+  }
+}
+
+Json build_pod(const Json& job, const std::string& rtype, int index, const ControllerConfig& cfg,
+               std::vector<Event>* events, std::string* error) {
+  const std::string rt = to_lower(rtype);
+  const std::string name = job_name(job);
+  const bool master_role = rtype == kReplicaMaster;
+  Json labels = gen_labels(name);
+  labels[kLabelReplicaType] = rt;
+  labels[kLabelReplicaIndex] = std::to_string(index);
+  if (master_role) labels[kLabelJobRole] = "master";
+
+  const Json* spec = replica_spec(job, rtype);
+  Json tmpl = spec && spec->get("template") ? *spec->get("template") : Json::object();
+  if (!tmpl.is_object()) tmpl = Json::object();
+  Json* md = ensure_obj(tmpl, "metadata");
+  (*md)["name"] = gen_general_name(name, rt, std::to_string(index));
+  Json* lbl = ensure_obj(*md, "labels");
+  for (const auto& kv : labels.as_object()) (*lbl)[kv.first] = kv.second;
+
+  std::string err = set_cluster_spec(tmpl, job, total_replicas(job), index, rtype);
+  if (!err.empty()) {
+    *error = err;
+    return Json();
+  }
+  Json* pspec = ensure_obj(tmpl, "spec");
+  if (!pspec->str_or("restartPolicy").empty()) {
+    events->push_back({"Warning", kReasonPodTemplateRestartPolicy,
+                       "Restart policy in pod template will be overwritten by restart policy in replica spec",
+                       kKind, name});
+  }
+  std::string rp = spec ? spec->str_or("restartPolicy") : "";
+  (*pspec)["restartPolicy"] = rp == kRestartExitCode ? std::string(kRestartNever) : rp;
+
+  if (!master_role) {
+    auto inits = init_containers(cfg, gen_general_name(name, "master", "0"), error);
+    if (!error->empty()) return Json();
+    Json& ic = (*pspec)["initContainers"];
+    if (!ic.is_array()) ic = Json::array();
+    for (auto& c : inits) ic.push_back(c);
+  }
+  if (cfg.enable_gang_scheduling) {
+    bool non_gang = false;
+    for (const auto& t : replica_types(job)) {
+      const Json* s = replica_spec(job, t);
+      const Json* sn = s ? s->path({"template", "spec", "schedulerName"}) : nullptr;
+      if (sn && sn->is_string() && !sn->as_string().empty() && sn->as_string() != cfg.gang_scheduler_name)
+        non_gang = true;
+    }
+    if (non_gang) {
+      events->push_back({"Warning", kReasonPodTemplateSchedulerName,
+                         "Another scheduler is specified when gang-scheduling is enabled and it will not be overwritten",
+                         kKind, name});
+    } else {
+      (*pspec)["schedulerName"] = cfg.gang_scheduler_name;
+    }
+    Json* ann = ensure_obj(*md, "annotations");
+    (*ann)[kGangPodGroupAnnotation] = gen_pod_group_name(name);
+  }
+  if (cfg.inject_rccl_env) inject_rccl_env(tmpl, cfg);
+
+  // RealPodControl.GetPodFromTemplate: labels, annotations, finalizers, name, ownerRef, spec
+  Json pod = Json::object();
+  pod["apiVersion"] = "v1";
+  pod["kind"] = "Pod";
+  Json pmd = Json::object();
+  pmd["name"] = md->str_or("name");
+  pmd["namespace"] = job_namespace(job);
+  pmd["labels"] = *lbl;
+  if (const Json* a = md->get("annotations"); a && a->is_object()) pmd["annotations"] = *a;
+  if (const Json* f = md->get("finalizers"); f && f->is_array()) pmd["finalizers"] = *f;
+  Json owners = Json::array();
+  owners.push_back(gen_owner_reference(job));
+  pmd["ownerReferences"] = owners;
+  pod["metadata"] = pmd;
+  pod["spec"] = *pspec;
+  return pod;
+}
+
+Json build_service(const Json& job, const std::string& rtype, int index, std::string* error) {
+  const std::string rt = to_lower(rtype);
+  Json labels = gen_labels(job_name(job));
+  labels[kLabelReplicaType] = rt;
+  labels[kLabelReplicaIndex] = std::to_string(index);
+  auto port = port_of(job, rtype);
+  if (!port) {
+    *error = "failed to found the port";
+    return Json();
+  }
+  Json svc = Json::object();
+  svc["apiVersion"] = "v1";
+  svc["kind"] = "Service";
+  Json md = Json::object();
+  md["name"] = gen_general_name(job_name(job), rt, std::to_string(index));
+  md["namespace"] = job_namespace(job);
+  md["labels"] = labels;
+  Json owners = Json::array();
+  owners.push_back(gen_owner_reference(job));
+  md["ownerReferences"] = owners;
+  svc["metadata"] = md;
+  Json spec = Json::object();
+  spec["clusterIP"] = "None";
+  spec["selector"] = labels;
+  Json p = Json::object();
+  p["name"] = kDefaultPortName;
+  p["port"] = *port;
+  Json ports = Json::array();
+  ports.push_back(p);
+  spec["ports"] = ports;
+  svc["spec"] = spec;
+  return svc;
+}
+
+bool past_backoff_limit(const Json& job, const std::vector<Json>& pods) {
+  const Json* bl = job.path({"spec", "backoffLimit"});
+  if (!bl || !bl->is_number()) return false;
+  int64_t limit = bl->as_int();
+  int64_t result = 0;
+  for (const auto& rtype : replica_types(job)) {
+    std::string rp = restart_policy_of(job, rtype);
+    if (rp != kRestartOnFailure && rp != kRestartAlways) continue;  // not counted
+    for (const auto& po : filter_by_replica_type(pods, to_lower(rtype))) {
+      std::string ph = pod_phase(po);
+      if (ph != "Running" && ph != "Pending") continue;
+      for (const char* key : {"initContainerStatuses", "containerStatuses"}) {
+        const Json* st = po.path({"status", key});
+        if (!st || !st->is_array()) continue;
+        for (const auto& cs : st->as_array()) result += cs.int_or("restartCount", 0);
+      }
+    }
+  }
+  if (limit == 0) return result > 0;
+  return result >= limit;
+}
+
+bool past_active_deadline(const Json& job, int64_t now) {
+  const Json* ads = job.path({"spec", "activeDeadlineSeconds"});
+  const Json* st = job.path({"status", "startTime"});
+  if (!ads || !ads->is_number() || !st || !st->is_string()) return false;
+  auto start = parse_time(st->as_string());
+  if (!start) return false;
+  return now - *start >= ads->as_int() * 1000;
+}
+
+// ------------------------------------------------------------------ reconcile
+namespace {
+
+struct Ctx {
+  const ReconcileInput& in;
+  const ControllerConfig& cfg;
+  Json job;
+  JobStatus status;
+  ReconcileResult res;
+  std::string name, key;
+};
+
+void delete_pods_and_services(Ctx& c) {
+  if (c.in.pods.empty()) return;  // (Q2) services are not deleted once the pods are gone
+  const Json* pol = c.job.path({"spec", "cleanPodPolicy"});
+  std::string policy = pol && pol->is_string() ? pol->as_string() : kCleanPodPolicyNone;
+  // (Q1) None and Running both delete nothing -- kept for behavioural parity.
+  if (policy == kCleanPodPolicyNone || policy == kCleanPodPolicyRunning) return;
+  for (const auto& p : c.in.pods)
+    c.res.delete_pods.push_back({p.path({"metadata", "namespace"}) ? p.path({"metadata", "namespace"})->as_string()
+                                                                   : job_namespace(c.job),
+                                 p.path({"metadata", "name"})->as_string()});
+  for (const auto& s : filter_by_replica_type(c.in.services, "master")) {
+    const Json* ns = s.path({"metadata", "namespace"});
+    c.res.delete_services.push_back({ns && ns->is_string() ? ns->as_string() : job_namespace(c.job),
+                                     s.path({"metadata", "name"})->as_string()});
+  }
+}
+
+void cleanup_job(Ctx& c) {
+  const Json* ttl = c.job.path({"spec", "ttlSecondsAfterFinished"});
+  if (!ttl || !ttl->is_number()) return;
+  if (!c.status.completion_time) return;  // (Q4) reference dereferences nil here; we wait
+  auto done = parse_time(*c.status.completion_time);
+  if (!done) return;
+  int64_t deadline = *done + ttl->as_int() * 1000;
+  if (c.in.now > deadline) {
+    c.res.delete_job = true;
+  } else {
+    // reference: AddRateLimited(key); requeue exactly when the TTL expires instead
+    c.res.requeue_after_s.push_back((double)(deadline - c.in.now) / 1000.0 + 0.001);
+  }
+}
+
+void set_cond(Ctx& c, const char* type, const char* reason, const std::string& msg) {
+  set_condition(c.status, new_condition(type, reason, msg, c.in.now));
+}
+
+void update_status_single(Ctx& c, const std::string& rtype, int replicas, bool restart) {
+  ReplicaStatus& rs = c.status.ensure_replica(rtype);
+  int expected = replicas - rs.succeeded;
+  int running = rs.active;
+  int failed = rs.failed;
+  if (!c.status.start_time) {
+    c.status.start_time = format_time(c.in.now);
+    const Json* ads = c.job.path({"spec", "activeDeadlineSeconds"});
+    if (ads && ads->is_number()) c.res.requeue_after_s.push_back((double)ads->as_int());
+  }
+  if (contains_master_spec(c.job)) {
+    if (rtype == kReplicaMaster) {
+      if (running > 0) set_cond(c, kJobRunning, kReasonRunning, fmt("PyTorchJob %s is running.", c.name));
+      if (expected == 0) {
+        std::string msg = fmt("PyTorchJob %s is successfully completed.", c.name);
+        c.res.events.push_back({"Normal", kReasonSucceeded, msg, kKind, c.name});
+        if (!c.status.completion_time) c.status.completion_time = format_time(c.in.now);
+        set_cond(c, kJobSucceeded, kReasonSucceeded, msg);
+        c.res.metrics.successful++;
+      }
+    }
+  } else {
+    c.res.error = "invalid config: Job must contain master replica spec";
+    return;
+  }
+  if (failed > 0) {
+    char buf[512];
+    if (restart) {
+      std::snprintf(buf, sizeof buf, "PyTorchJob %s is restarting because %d %s replica(s) failed.",
+                    c.name.c_str(), failed, rtype.c_str());
+      c.res.events.push_back({"Warning", kReasonRestarting, buf, kKind, c.name});
+      set_cond(c, kJobRestarting, kReasonRestarting, buf);
+      c.res.metrics.failed++;
+      c.res.metrics.restarted++;
+    } else {
+      std::snprintf(buf, sizeof buf, "PyTorchJob %s is failed because %d %s replica(s) failed.",
+                    c.name.c_str(), failed, rtype.c_str());
+      c.res.events.push_back({"Normal", kReasonFailed, buf, kKind, c.name});
+      if (!c.status.completion_time) c.status.completion_time = format_time(c.in.now);
+      set_cond(c, kJobFailed, kReasonFailed, buf);
+      c.res.metrics.failed++;
+    }
+  }
+}
+
+void reconcile_pods(Ctx& c, const std::string& rtype) {
+  const std::string rt = to_lower(rtype);
+  auto pods = filter_by_replica_type(c.in.pods, rt);
+  const int replicas = replicas_of(c.job, rtype);
+  bool restart = false;
+  c.status.ensure_replica(rtype) = ReplicaStatus{};  // initializePyTorchReplicaStatuses
+  const std::string rp = restart_policy_of(c.job, rtype);
+  auto slices = slices_by_index(pods, replicas);
+  for (size_t index = 0; index < slices.size(); ++index) {
+    auto& slice = slices[index];
+    if (slice.size() > 1) continue;  // (Q7) too many pods for one index: warning only
+    if (slice.empty()) {
+      std::string err;
+      Json pod = build_pod(c.job, rtype, (int)index, c.cfg, &c.res.events, &err);
+      if (!err.empty()) {
+        c.res.error = err;
+        return;
+      }
+      c.res.create_pods.push_back(pod);
+      c.res.create_pod_expectation_keys.push_back(gen_expectation_pods_key(c.key, rt));
+      continue;
+    }
+    const Json& pod = slice[0];
+    const std::string pns = pod.path({"metadata", "namespace"}) ? pod.path({"metadata", "namespace"})->as_string()
+                                                                 : job_namespace(c.job);
+    const std::string pname = pod.path({"metadata", "name"})->as_string();
+    if (rp == kRestartExitCode) {
+      int32_t exit_code = 0;
+      const Json* css = pod.path({"status", "containerStatuses"});
+      if (css && css->is_array()) {
+        for (const auto& cs : css->as_array()) {
+          const Json* term = cs.path({"state", "terminated"});
+          if (cs.str_or("name") == kDefaultContainerName && term && term->is_object()) {
+            exit_code = (int32_t)term->int_or("exitCode", 0);
+            c.res.events.push_back({"Normal", kReasonExitedWithCode,
+                                    "Pod: " + pns + "." + pname + " exited with code " + std::to_string(exit_code),
+                                    kKind, c.name});
+          }
+        }
+      }
+      if (pod_phase(pod) == "Failed" && is_retryable_exit_code(exit_code)) {
+        c.res.delete_pods.push_back({pns, pname});
+        restart = true;
+      }
+    }
+    ReplicaStatus& rs = c.status.ensure_replica(rtype);
+    const std::string ph = pod_phase(pod);
+    if (ph == "Running") rs.active++;
+    else if (ph == "Succeeded") rs.succeeded++;
+    else if (ph == "Failed") rs.failed++;
+  }
+  update_status_single(c, rtype, replicas, restart);
+}
+
+void reconcile_services(Ctx& c, const std::string& rtype) {
+  const std::string rt = to_lower(rtype);
+  const int replicas = replicas_of(c.job, rtype);
+  auto slices = slices_by_index(filter_by_replica_type(c.in.services, rt), replicas);
+  for (size_t index = 0; index < slices.size(); ++index) {
+    if (!slices[index].empty()) continue;
+    std::string err;
+    Json svc = build_service(c.job, rtype, (int)index, &err);
+    if (!err.empty()) {
+      c.res.error = err;
+      return;
+    }
+    c.res.create_services.push_back(svc);
+    c.res.create_service_expectation_keys.push_back(gen_expectation_services_key(c.key, rt));
+  }
+}
+
+}  // namespace
+
+ReconcileResult reconcile(const ReconcileInput& in, const ControllerConfig& cfg) {
+  Ctx c{in, cfg, in.job, {}, {}, {}, {}};
+  c.name = job_name(c.job);
+  c.key = job_key(c.job);
+  const Json* st = c.job.get("status");
+  c.status = JobStatus::from_json(st ? *st : Json());
+  const JobStatus old = c.status;
+  auto finish = [&]() {
+    Json sj = c.status.to_json();
+    c.res.status_changed = !(c.status == old);
+    c.res.status = sj;
+    return std::move(c.res);
+  };
+
+  if (is_succeeded(c.status) || is_failed(c.status)) {
+    delete_pods_and_services(c);
+    cleanup_job(c);
+    if (cfg.enable_gang_scheduling) c.res.delete_podgroup = true;
+    if (is_succeeded(c.status)) {
+      for (auto& kv : c.status.replica_statuses) {
+        kv.second.succeeded += kv.second.active;
+        kv.second.active = 0;
+      }
+    }
+    return finish();
+  }
+
+  int32_t active = 0, failed = 0;
+  for (const auto& p : in.pods) {
+    if (is_pod_active(p)) active++;
+    if (pod_phase(p) == "Failed") failed++;
+  }
+  const int32_t total = total_replicas(c.job);
+  int32_t prev_failed = 0;
+  for (const auto& kv : c.status.replica_statuses) prev_failed += kv.second.failed;
+
+  bool exceeds_backoff = false, past_backoff = false;
+  const Json* bl = c.job.path({"spec", "backoffLimit"});
+  if (bl && bl->is_number()) {
+    bool new_failure = failed > prev_failed;
+    exceeds_backoff = new_failure && active != total && (int64_t)in.requeues + 1 > bl->as_int();
+    past_backoff = past_backoff_limit(c.job, in.pods);
+  }
+  std::string failure_message;
+  bool exceeds_limit = false;
+  if (exceeds_backoff || past_backoff) {
+    exceeds_limit = true;
+    failure_message = fmt("PyTorchJob %s has failed because it has reached the specified backoff limit", c.name);
+  } else if (past_active_deadline(c.job, in.now)) {
+    exceeds_limit = true;
+    failure_message = fmt("PyTorchJob %s has failed because it was active longer than specified deadline", c.name);
+  }
+
+  if (exceeds_limit) {
+    delete_pods_and_services(c);
+    cleanup_job(c);
+    if (cfg.enable_gang_scheduling) c.res.delete_podgroup = true;
+    c.res.events.push_back({"Normal", kReasonFailed, failure_message, kKind, c.name});
+    if (!c.status.completion_time) c.status.completion_time = format_time(in.now);
+    set_cond(c, kJobFailed, kReasonFailed, failure_message);
+    // (parity) the reference increments no failure counter on this path
+  } else {
+    if (cfg.enable_gang_scheduling && !in.podgroup_exists) {
+      Json pg = Json::object();
+      pg["apiVersion"] = "scheduling.incubator.k8s.io/v1alpha1";
+      pg["kind"] = "PodGroup";
+      Json md = Json::object();
+      md["name"] = gen_pod_group_name(c.name);
+      md["namespace"] = job_namespace(c.job);
+      Json owners = Json::array();
+      owners.push_back(gen_owner_reference(c.job));
+      md["ownerReferences"] = owners;
+      pg["metadata"] = md;
+      Json spec = Json::object();
+      spec["minMember"] = total;
+      pg["spec"] = spec;
+      c.res.create_podgroup = pg;
+    }
+    for (const auto& rtype : replica_types(c.job)) {
+      reconcile_pods(c, rtype);
+      if (!c.res.error.empty()) return finish();
+      if (rtype != kReplicaMaster) continue;  // services only for the Master
+      reconcile_services(c, rtype);
+      if (!c.res.error.empty()) return finish();
+    }
+  }
+  return finish();
+}
+
+JobAddedResult on_job_added(const Json& job_in, int64_t now) {
+  JobAddedResult r;
+  const Json* spec = job_in.get("spec");
+  std::string err = spec && spec->is_object() ? validate_spec(*spec) : "PyTorchJobSpec is not valid";
+  const std::string name = job_name(job_in);
+  if (!err.empty()) {
+    r.valid = false;
+    r.error = err;
+    std::string msg = "Failed to unmarshal the object to PyTorchJob: Spec is invalid " + err;
+    r.events.push_back({"Warning", kReasonInvalidSpec, msg, kKind, name});
+    JobStatus s;
+    JobCondition c = new_condition(kJobFailed, kReasonInvalidSpec, msg, now);
+    s.conditions.push_back(c);
+    r.status = s.to_json();
+    return r;
+  }
+  Json job = job_in;
+  set_defaults(job);
+  const Json* st = job.get("status");
+  JobStatus s = JobStatus::from_json(st ? *st : Json());
+  set_condition(s, new_condition(kJobCreated, kReasonCreated, "PyTorchJob " + name + " is created.", now));
+  r.status = s.to_json();
+  r.metrics.created = 1;
+  return r;
+}
+
+double deadline_requeue_on_update(const Json& old_job, const Json& cur_job, int64_t now) {
+  const Json* st = cur_job.path({"status", "startTime"});
+  if (!st || !st->is_string()) return -1;
+  const Json* cur = cur_job.path({"spec", "activeDeadlineSeconds"});
+  if (!cur || !cur->is_number()) return -1;
+  const Json* old = old_job.path({"spec", "activeDeadlineSeconds"});
+  if (old && old->is_number() && old->as_int() == cur->as_int()) return -1;
+  auto start = parse_time(st->as_string());
+  if (!start) return -1;
+  double passed = (double)(now - *start) / 1000.0;
+  double total = (double)cur->as_int();
+  return std::max(0.0, total - passed);  // AddAfter handles total < passed as "now"
+}
+
+}  // namespace pto
+
+namespace pto {
+// updateStatusSingle on a job whose .status already carries replica counts
+// (status_test.go drives it this way).
+Json update_status_single_json(const Json& job, const std::string& rtype, int replicas, bool restart,
+                               int64_t now) {
+  ReconcileInput in;
+  in.job = job;
+  in.now = now;
+  ControllerConfig cfg;
+  Ctx c{in, cfg, job, {}, {}, {}, {}};
+  c.name = job_name(job);
+  c.key = job_key(job);
+  const Json* st = job.get("status");
+  c.status = JobStatus::from_json(st ? *st : Json());
+  update_status_single(c, rtype, replicas, restart);
+  Json out = Json::object();
+  out["status"] = c.status.to_json();
+  out["error"] = c.res.error;
+  Json evs = Json::array();
+  for (const auto& e : c.res.events) {
+    Json o = Json::object();
+    o["type"] = e.type;
+    o["reason"] = e.reason;
+    o["message"] = e.message;
+    evs.push_back(o);
+  }
+  out["events"] = evs;
+  return out;
+}
+}  // namespace pto
