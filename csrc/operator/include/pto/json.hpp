@@ -111,6 +111,8 @@ class Json {
   // Array access.
   Json& operator[](size_t i);
   const Json& operator[](size_t i) const;
+  Json& operator[](int i) { return (*this)[(size_t)i]; }  // literal 0 must not mean (const char*)0
+  const Json& operator[](int i) const { return (*this)[(size_t)i]; }
   void push_back(Json v);
   size_t size() const;
 

@@ -1,0 +1,239 @@
+#include "pto/kube.hpp"
+
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <thread>
+
+#include "pto/log.hpp"
+#include "pto/yaml_lite.hpp"
+
+namespace pto {
+
+const Resource kPods{"", "v1", "pods"};
+const Resource kServices{"", "v1", "services"};
+const Resource kEvents{"", "v1", "events"};
+const Resource kEndpoints{"", "v1", "endpoints"};
+const Resource kLeases{"coordination.k8s.io", "v1", "leases"};
+const Resource kPyTorchJobs{"kubeflow.org", "v1", "pytorchjobs"};
+const Resource kPodGroups{"scheduling.incubator.k8s.io", "v1alpha1", "podgroups"};
+const Resource kCRDs{"apiextensions.k8s.io", "v1", "customresourcedefinitions", false};
+
+std::string Resource::path(const std::string& ns, const std::string& name, const std::string& sub) const {
+  std::string p = group.empty() ? "/api/" + version : "/apis/" + group + "/" + version;
+  if (namespaced && !ns.empty()) p += "/namespaces/" + ns;
+  p += "/" + plural;
+  if (!name.empty()) p += "/" + name;
+  if (!sub.empty()) p += "/" + sub;
+  return p;
+}
+
+static std::string read_file(const std::string& path, bool* ok) {
+  std::ifstream f(path, std::ios::binary);
+  *ok = (bool)f;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+static const Json* named(const Json& list, const std::string& name) {
+  if (!list.is_array()) return nullptr;
+  for (const auto& e : list.as_array())
+    if (e.str_or("name") == name) return &e;
+  return nullptr;
+}
+
+std::optional<KubeConfig> load_kube_config(const std::string& master_url, const std::string& kubeconfig,
+                                           std::string* error) {
+  KubeConfig kc;
+  if (!kubeconfig.empty()) {
+    bool ok = false;
+    std::string text = read_file(kubeconfig, &ok);
+    if (!ok) {
+      *error = "cannot read kubeconfig " + kubeconfig;
+      return std::nullopt;
+    }
+    Json doc;
+    try {
+      doc = text.find_first_not_of(" \t\r\n") != std::string::npos && text[text.find_first_not_of(" \t\r\n")] == '{'
+                ? Json::parse(text)
+                : yaml_parse(text);
+    } catch (const std::exception& e) {
+      *error = std::string("kubeconfig parse error: ") + e.what();
+      return std::nullopt;
+    }
+    std::string ctx_name = doc.str_or("current-context");
+    const Json* ctx = named(doc.get("contexts") ? *doc.get("contexts") : Json(), ctx_name);
+    const Json* ctxv = ctx ? ctx->get("context") : nullptr;
+    std::string cluster_name = ctxv ? ctxv->str_or("cluster") : "";
+    std::string user_name = ctxv ? ctxv->str_or("user") : "";
+    if (ctxv && !ctxv->str_or("namespace").empty()) kc.ns = ctxv->str_or("namespace");
+    const Json* cl = named(doc.get("clusters") ? *doc.get("clusters") : Json(), cluster_name);
+    if (!cl && doc.get("clusters") && doc.get("clusters")->size() > 0) cl = &doc.get("clusters")->as_array()[0];
+    const Json* clv = cl ? cl->get("cluster") : nullptr;
+    if (clv) {
+      kc.server = clv->str_or("server");
+      kc.tls.ca_file = clv->str_or("certificate-authority");
+      if (!clv->str_or("certificate-authority-data").empty())
+        kc.tls.ca_data = base64_decode(clv->str_or("certificate-authority-data"));
+      kc.tls.insecure_skip_verify = clv->bool_or("insecure-skip-tls-verify", false);
+    }
+    const Json* us = named(doc.get("users") ? *doc.get("users") : Json(), user_name);
+    const Json* usv = us ? us->get("user") : nullptr;
+    if (usv) {
+      kc.token = usv->str_or("token");
+      if (!usv->str_or("tokenFile").empty()) {
+        bool tok_ok;
+        kc.token = read_file(usv->str_or("tokenFile"), &tok_ok);
+      }
+      kc.tls.cert_file = usv->str_or("client-certificate");
+      kc.tls.key_file = usv->str_or("client-key");
+      if (!usv->str_or("client-certificate-data").empty())
+        kc.tls.cert_data = base64_decode(usv->str_or("client-certificate-data"));
+      if (!usv->str_or("client-key-data").empty())
+        kc.tls.key_data = base64_decode(usv->str_or("client-key-data"));
+    }
+  } else if (master_url.empty()) {
+    // in-cluster config
+    const char* host = std::getenv("KUBERNETES_SERVICE_HOST");
+    const char* port = std::getenv("KUBERNETES_SERVICE_PORT");
+    if (!host || !port) {
+      *error = "no --kubeconfig/--master given and not running in a cluster";
+      return std::nullopt;
+    }
+    kc.server = std::string("https://") + host + ":" + port;
+    bool ok;
+    kc.token = read_file("/var/run/secrets/kubernetes.io/serviceaccount/token", &ok);
+    kc.tls.ca_file = "/var/run/secrets/kubernetes.io/serviceaccount/ca.crt";
+    std::string ns = read_file("/var/run/secrets/kubernetes.io/serviceaccount/namespace", &ok);
+    if (ok && !ns.empty()) kc.ns = ns;
+  }
+  if (!master_url.empty()) kc.server = master_url;
+  while (!kc.token.empty() && (kc.token.back() == '\n' || kc.token.back() == '\r')) kc.token.pop_back();
+  if (kc.server.empty()) {
+    *error = "no API server address";
+    return std::nullopt;
+  }
+  return kc;
+}
+
+KubeClient::KubeClient(const KubeConfig& cfg, double qps, int burst)
+    : cfg_(cfg), qps_(qps), burst_(burst), tokens_(burst), last_(std::chrono::steady_clock::now()) {
+  if (!Url::parse(cfg.server, &url_)) url_ = Url{};
+  http_ = std::make_unique<HttpClient>(url_, cfg.tls, cfg.token, 30.0);
+}
+
+void KubeClient::throttle() {
+  if (qps_ <= 0) return;
+  double wait = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto now = std::chrono::steady_clock::now();
+    double el = std::chrono::duration<double>(now - last_).count();
+    last_ = now;
+    tokens_ = std::min<double>(burst_, tokens_ + el * qps_);
+    tokens_ -= 1.0;
+    if (tokens_ < 0) wait = -tokens_ / qps_;
+  }
+  if (wait > 0) std::this_thread::sleep_for(std::chrono::duration<double>(wait));
+}
+
+std::optional<Json> KubeClient::call(const std::string& method, const std::string& path,
+                                     const std::string& body, ApiError* err, const std::string& ctype) {
+  throttle();
+  HttpResponse r = http_->request(method, path, body, ctype);
+  if (r.status == 0) {
+    if (err) *err = ApiError{0, r.error};
+    return std::nullopt;
+  }
+  if (r.status < 200 || r.status >= 300) {
+    std::string msg = r.body;
+    try {
+      Json j = Json::parse(r.body);
+      msg = j.str_or("message", r.body);
+    } catch (...) {
+    }
+    if (err) *err = ApiError{r.status, msg};
+    return std::nullopt;
+  }
+  if (r.body.empty()) return Json::object();
+  try {
+    return Json::parse(r.body);
+  } catch (const std::exception& e) {
+    if (err) *err = ApiError{r.status, std::string("bad JSON from server: ") + e.what()};
+    return std::nullopt;
+  }
+}
+
+std::optional<Json> KubeClient::get(const Resource& r, const std::string& ns, const std::string& name,
+                                    ApiError* err) {
+  return call("GET", r.path(ns, name), "", err);
+}
+
+std::optional<Json> KubeClient::list(const Resource& r, const std::string& ns, const std::string& sel,
+                                     ApiError* err) {
+  std::string p = r.path(ns);
+  if (!sel.empty()) p += "?labelSelector=" + url_encode(sel);
+  return call("GET", p, "", err);
+}
+
+std::optional<Json> KubeClient::create(const Resource& r, const std::string& ns, const Json& obj, ApiError* err) {
+  return call("POST", r.path(ns), obj.dump(), err);
+}
+
+std::optional<Json> KubeClient::update(const Resource& r, const std::string& ns, const Json& obj, ApiError* err) {
+  const Json* md = obj.get("metadata");
+  return call("PUT", r.path(ns, md ? md->str_or("name") : ""), obj.dump(), err);
+}
+
+std::optional<Json> KubeClient::update_status(const Resource& r, const std::string& ns, const Json& obj,
+                                              ApiError* err) {
+  const Json* md = obj.get("metadata");
+  return call("PUT", r.path(ns, md ? md->str_or("name") : "", "status"), obj.dump(), err);
+}
+
+std::optional<Json> KubeClient::patch_merge(const Resource& r, const std::string& ns, const std::string& name,
+                                            const Json& patch, ApiError* err) {
+  return call("PATCH", r.path(ns, name), patch.dump(), err, "application/merge-patch+json");
+}
+
+bool KubeClient::del(const Resource& r, const std::string& ns, const std::string& name, ApiError* err) {
+  Json opts = Json::object();
+  opts["kind"] = "DeleteOptions";
+  opts["apiVersion"] = "v1";
+  opts["propagationPolicy"] = "Background";
+  return call("DELETE", r.path(ns, name), opts.dump(), err).has_value();
+}
+
+void KubeClient::watch(const Resource& r, const std::string& ns, const std::string& sel,
+                       const std::string& rv, const std::function<bool(const std::string&, const Json&)>& on_event,
+                       const std::atomic<bool>* stop, double timeout_s, ApiError* err) {
+  std::string p = r.path(ns) + "?watch=true&allowWatchBookmarks=true&timeoutSeconds=" +
+                  std::to_string((int)timeout_s);
+  if (!rv.empty()) p += "&resourceVersion=" + url_encode(rv);
+  if (!sel.empty()) p += "&labelSelector=" + url_encode(sel);
+  std::string transport_err;
+  int code = http_->stream_lines(
+      p,
+      [&](const std::string& line) {
+        Json ev;
+        try {
+          ev = Json::parse(line);
+        } catch (...) {
+          return true;
+        }
+        std::string type = ev.str_or("type");
+        const Json* obj = ev.get("object");
+        if (type == "ERROR") {
+          int c = obj ? (int)obj->int_or("code", 500) : 500;
+          if (err) *err = ApiError{c, obj ? obj->str_or("message") : "watch error"};
+          return false;
+        }
+        return on_event(type, obj ? *obj : Json());
+      },
+      stop, timeout_s + 30.0, &transport_err);
+  if (code == 0 && err && err->code == 0) *err = ApiError{0, transport_err};
+  else if (code != 200 && code != 0 && err && err->code == 0) *err = ApiError{code, "watch failed"};
+}
+
+}  // namespace pto

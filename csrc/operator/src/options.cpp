@@ -1,0 +1,153 @@
+#include "pto/options.hpp"
+
+#include <cstdlib>
+#include <functional>
+#include <map>
+
+namespace pto {
+
+bool parse_duration(const std::string& s, double* seconds) {
+  if (s.empty()) return false;
+  double total = 0;
+  size_t i = 0;
+  bool any = false;
+  while (i < s.size()) {
+    size_t j = i;
+    while (j < s.size() && (std::isdigit((unsigned char)s[j]) || s[j] == '.')) ++j;
+    if (j == i) return false;
+    double v = std::atof(s.substr(i, j - i).c_str());
+    size_t k = j;
+    while (k < s.size() && std::isalpha((unsigned char)s[k])) ++k;
+    std::string unit = s.substr(j, k - j);
+    double mul;
+    if (unit == "h") mul = 3600;
+    else if (unit == "m") mul = 60;
+    else if (unit == "s") mul = 1;
+    else if (unit == "ms") mul = 1e-3;
+    else if (unit == "us" || unit == "µs") mul = 1e-6;
+    else if (unit == "ns") mul = 1e-9;
+    else if (unit.empty() && v == 0) mul = 0;
+    else return false;
+    total += v * mul;
+    any = true;
+    i = k;
+  }
+  *seconds = total;
+  return any;
+}
+
+namespace {
+bool parse_bool(const std::string& v, bool* out) {
+  if (v == "1" || v == "t" || v == "T" || v == "true" || v == "TRUE" || v == "True") return *out = true, true;
+  if (v == "0" || v == "f" || v == "F" || v == "false" || v == "FALSE" || v == "False") return *out = false, true;
+  return false;
+}
+}  // namespace
+
+std::string usage() {
+  return "Usage of pytorch-operator:\n"
+         "  -kubeconfig string        The path of kubeconfig file\n"
+         "  -master string            The url of the Kubernetes API server, will overrides any value in kubeconfig\n"
+         "  -namespace string         The namespace to monitor pytorch jobs (default: all namespaces)\n"
+         "  -threadiness int          How many threads to process the main logic (default 1)\n"
+         "  -version                  Show version and quit\n"
+         "  -json-log-format          Set true to use json style log format (default true)\n"
+         "  -enable-gang-scheduling   Set true to enable gang scheduling\n"
+         "  -gang-scheduler-name      The scheduler to gang-schedule jobs (default \"volcano\")\n"
+         "  -monitoring-port int      Endpoint port for displaying monitoring metrics (default 8443)\n"
+         "  -resyc-period duration    Resync interval of the operator (default 12h0m0s)\n"
+         "  -init-container-image     The image of the injected init container (default \"alpine:3.10\")\n"
+         "  -qps int                  Maximum QPS to the master from this client (default 5)\n"
+         "  -burst int                Maximum burst for throttle (default 10)\n"
+         "  -leader-elect             Run leader election on a Lease (default true)\n"
+         "  -inject-rccl-env          Inject LOCAL_RANK and RCCL tuning env into pytorch containers\n"
+         "  -init-container-template-file  (default /etc/config/initContainer.yaml)\n"
+         "  -log-level string         debug|info|warning|error (default info)\n";
+}
+
+std::string parse_flags(int argc, char** argv, ServerOption* o) {
+  using Setter = std::function<std::string(const std::string&)>;
+  struct Flag {
+    bool is_bool;
+    Setter set;
+  };
+  auto str = [](std::string* dst) { return Flag{false, [dst](const std::string& v) { *dst = v; return std::string(); }}; };
+  auto integer = [](int* dst) {
+    return Flag{false, [dst](const std::string& v) {
+                  char* e = nullptr;
+                  long x = std::strtol(v.c_str(), &e, 10);
+                  if (!e || *e) return std::string("invalid integer value \"") + v + "\"";
+                  *dst = (int)x;
+                  return std::string();
+                }};
+  };
+  auto boolean = [](bool* dst) {
+    return Flag{true, [dst](const std::string& v) {
+                  if (!parse_bool(v, dst)) return std::string("invalid boolean value \"") + v + "\"";
+                  return std::string();
+                }};
+  };
+  auto ignore_bool = Flag{true, [](const std::string&) { return std::string(); }};
+  auto ignore_val = Flag{false, [](const std::string&) { return std::string(); }};
+  std::map<std::string, Flag> flags = {
+      {"kubeconfig", str(&o->kubeconfig)},
+      {"master", str(&o->master_url)},
+      {"namespace", str(&o->namespace_)},
+      {"threadiness", integer(&o->threadiness)},
+      {"version", boolean(&o->print_version)},
+      {"json-log-format", boolean(&o->json_log_format)},
+      {"enable-gang-scheduling", boolean(&o->enable_gang_scheduling)},
+      {"gang-scheduler-name", str(&o->gang_scheduler_name)},
+      {"monitoring-port", integer(&o->monitoring_port)},
+      {"resyc-period", Flag{false, [o](const std::string& v) {
+         if (!parse_duration(v, &o->resync_period_s)) return std::string("invalid duration \"") + v + "\"";
+         return std::string();
+       }}},
+      {"init-container-image", str(&o->init_container_image)},
+      {"qps", integer(&o->qps)},
+      {"burst", integer(&o->burst)},
+      {"leader-elect", boolean(&o->leader_elect)},
+      {"inject-rccl-env", boolean(&o->inject_rccl_env)},
+      {"init-container-template-file", str(&o->init_container_template_file)},
+      {"log-level", str(&o->log_level)},
+      // glog flags accepted for compatibility with the reference Deployment
+      {"alsologtostderr", ignore_bool},
+      {"logtostderr", ignore_bool},
+      {"v", ignore_val},
+      {"stderrthreshold", ignore_val},
+      {"log_dir", ignore_val},
+      {"vmodule", ignore_val},
+      {"log_backtrace_at", ignore_val},
+  };
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--") break;
+    if (a.size() < 2 || a[0] != '-') return "unexpected argument: " + a;
+    std::string body = a.substr(a[1] == '-' ? 2 : 1);
+    if (body == "h" || body == "help") return "help";
+    std::string name = body, value;
+    bool has_value = false;
+    auto eq = body.find('=');
+    if (eq != std::string::npos) {
+      name = body.substr(0, eq);
+      value = body.substr(eq + 1);
+      has_value = true;
+    }
+    auto it = flags.find(name);
+    if (it == flags.end()) return "flag provided but not defined: -" + name;
+    if (it->second.is_bool) {
+      std::string err = it->second.set(has_value ? value : "true");
+      if (!err.empty()) return err + " for -" + name;
+      continue;
+    }
+    if (!has_value) {
+      if (i + 1 >= argc) return "flag needs an argument: -" + name;
+      value = argv[++i];
+    }
+    std::string err = it->second.set(value);
+    if (!err.empty()) return err + " for -" + name;
+  }
+  return "";
+}
+
+}  // namespace pto
