@@ -1,0 +1,297 @@
+"""The PyTorchJob MNIST DDP worker (the container entrypoint of the example jobs).
+
+Behavioural parity with the reference worker examples/mnist/mnist.py:
+
+* same CLI (``--batch-size 64 --test-batch-size 1000 --epochs 1 --lr 0.01
+  --momentum 0.5 --no-cuda --seed 1 --log-interval 10 --save-model --dir logs
+  --backend``), same model (``models.mnist.Net``), SGD(lr, momentum), NLL loss;
+* process group from the operator's env contract (MASTER_ADDR/MASTER_PORT/WORLD_SIZE/
+  RANK, mnist.py:82-116) when WORLD_SIZE > 1;
+* the same stdout lines (``Train Epoch: e [n/N (p%)]\\tloss=x`` every log interval,
+  ``accuracy=x`` after each epoch's test pass) and TensorBoard scalars ``loss`` /
+  ``accuracy`` under ``--dir``.
+
+MI355X-native differences:
+
+* ``--backend rccl`` (alias of nccl: RCCL over xGMI); ``mpi`` fails clearly;
+* on a GPU the step runs the fused gfx950 kernels (``--kernels hip``, default) on an
+  HBM-resident uint8 dataset, replayed as hipGraphs; DDP is two flat-bucket RCCL
+  all-reduces overlapped with the conv backward.  ``--kernels torch`` is the plain
+  PyTorch path (also used on CPU with gloo);
+* data: real MNIST IDX files from ``--data-dir`` if present, else the synthetic set
+  (no network);  ``--shard`` (default) gives each rank a disjoint slice like a
+  ``DistributedSampler``; ``--no-shard`` reproduces the reference, where every rank
+  iterates the full dataset;
+* one machine-readable JSON line per milestone (``first_step``, ``train_done``) so the
+  operator benchmarks can measure create-to-first-step latency and throughput.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="PyTorch MNIST Example (MI355X-native worker)")
+    p.add_argument("--batch-size", type=int, default=64, metavar="N")
+    p.add_argument("--test-batch-size", type=int, default=1000, metavar="N")
+    p.add_argument("--epochs", type=int, default=1, metavar="N")
+    p.add_argument("--lr", type=float, default=0.01, metavar="LR")
+    p.add_argument("--momentum", type=float, default=0.5, metavar="M")
+    p.add_argument("--no-cuda", action="store_true", default=False)
+    p.add_argument("--seed", type=int, default=1, metavar="S")
+    p.add_argument("--log-interval", type=int, default=10, metavar="N")
+    p.add_argument("--save-model", action="store_true", default=False)
+    p.add_argument("--dir", default="logs", metavar="L", help="TensorBoard summary directory")
+    p.add_argument("--backend", type=str, default="gloo", choices=["gloo", "nccl", "rccl", "mpi"])
+    # MI355X-native extensions
+    p.add_argument("--kernels", choices=["auto", "hip", "torch"], default="auto")
+    p.add_argument("--data-dir", default="../data", help="directory holding MNIST IDX files")
+    p.add_argument("--synthetic", action="store_true", help="force the synthetic dataset")
+    p.add_argument("--dataset-size", type=int, default=60000, help="synthetic train set size")
+    p.add_argument("--test-size", type=int, default=10000, help="synthetic test set size")
+    p.add_argument("--shard", dest="shard", action="store_true", default=True)
+    p.add_argument("--no-shard", dest="shard", action="store_false")
+    p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
+    p.add_argument("--no-graph", action="store_true", help="HIP path: eager launches, no hipGraphs")
+    p.add_argument("--model-path", default="mnist_cnn.pt")
+    p.add_argument("--metrics-file", default=None, help="append the JSON milestone lines here too")
+    return p.parse_args(argv)
+
+
+class _Emitter:
+    def __init__(self, rank: int, path):
+        self.rank, self.path = rank, path
+
+    def __call__(self, event: str, **kw):
+        rec = {"event": event, "rank": self.rank, "unix_ns": time.time_ns(), **kw}
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if self.path:
+            with open(self.path, "a") as f:
+                f.write(line + "\n")
+
+
+def _datasets(args, rank: int, world: int, device):
+    import torch
+    from ..data.mnist_idx import load_mnist
+    from ..data.synthetic import make_synthetic_mnist
+    train = test = None
+    if not args.synthetic:
+        train = load_mnist(args.data_dir, "train")
+        test = load_mnist(args.data_dir, "test")
+    source = "mnist-idx"
+    if train is None or test is None:
+        source = "synthetic"
+        tr = make_synthetic_mnist(args.dataset_size, seed=args.seed)
+        te = make_synthetic_mnist(args.test_size, seed=args.seed + 7919)
+        train, test = (tr.images, tr.labels), (te.images, te.labels)
+    xtr, ytr = train
+    if args.shard and world > 1:
+        xtr, ytr = xtr[rank::world].contiguous(), ytr[rank::world].contiguous()
+    return (xtr.to(device), ytr.to(device)), (test[0].to(device), test[1].to(device)), source
+
+
+def _epoch_perm(n: int, seed: int, epoch: int, rank: int, shard: bool, device):
+    import torch
+    # reference: DataLoader(shuffle=True) under torch.manual_seed(seed) -- identical order
+    # on every rank.  Sharded runs shuffle their own slice.
+    g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + epoch * 7 + (rank if shard else 0))
+    return torch.randperm(n, generator=g).to(torch.int32).to(device)
+
+
+def run(args) -> dict:
+    import torch
+    import torch.nn.functional as F
+    from ..parallel.dist import init_from_env
+
+    use_cuda = not args.no_cuda and torch.cuda.is_available()
+    if use_cuda:
+        print("Using CUDA")  # reference wording; the device is an MI355X over HIP
+    torch.manual_seed(args.seed)
+    env = init_from_env(args.backend, use_gpu=use_cuda)
+    rank, world, device = env.rank, env.world_size, env.device
+    emit = _Emitter(rank, args.metrics_file)
+    if world > 1:
+        print(f"Using distributed PyTorch with {args.backend} backend")
+    kernels = args.kernels
+    if kernels == "auto":
+        kernels = "hip" if use_cuda else "torch"
+    if kernels == "hip" and not use_cuda:
+        raise SystemExit("--kernels hip needs a GPU (drop --no-cuda or use --kernels torch)")
+
+    from ..utils.tb_writer import SummaryWriter
+    writer = SummaryWriter(args.dir)
+    (xtr, ytr), (xte, yte), data_source = _datasets(args, rank, world, device)
+    n = xtr.shape[0]
+    B = args.batch_size
+    steps_per_epoch = math.ceil(n / B)
+    if args.max_steps:
+        steps_per_epoch = min(steps_per_epoch, args.max_steps)
+    emit("start", world_size=world, backend=env.backend, kernels=kernels, data=data_source,
+         n_train=int(n), steps_per_epoch=steps_per_epoch)
+
+    if kernels == "hip":
+        result = _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch)
+    else:
+        result = _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch)
+    writer.close()
+    emit("train_done", **result)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss, writer):
+    print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
+        epoch, batch_idx * B, n, 100.0 * batch_idx / steps_per_epoch, loss), flush=True)
+    writer.add_scalar("loss", loss, epoch * steps_per_epoch + batch_idx)
+
+
+def _log_test(acc, epoch, writer):
+    print("\naccuracy={:.4f}\n".format(acc), flush=True)
+    writer.add_scalar("accuracy", acc, epoch)
+    writer.flush()
+
+
+def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> dict:
+    import torch
+    import torch.distributed as dist
+    from ..models.mnist import FusedMnistTrainer
+    from ..ops import mnist as K
+    from ..parallel.ddp import FlatGradAllReduce
+    from ..parallel.graphed_step import GraphedStep
+
+    dev, world, rank = env.device, env.world_size, env.rank
+    B, n = args.batch_size, xtr.shape[0]
+    perm = _epoch_perm(n, args.seed, 1, rank, args.shard, dev)
+    cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(xtr, ytr, perm=perm, cursor=cursor)
+    sync = FlatGradAllReduce() if world > 1 else None
+    tr = FusedMnistTrainer(batch_size=B, source=src, lr=args.lr, momentum=args.momentum,
+                           device=dev, seed=args.seed, grad_sync=sync)
+    if world > 1:
+        dist.broadcast(tr.flat_params, 0)  # DDP constructor semantics
+    log_iv = max(1, args.log_interval)
+    runner = None
+    t_train = 0.0
+    steps_done = 0
+    for epoch in range(1, args.epochs + 1):
+        if epoch > 1:
+            perm.copy_(_epoch_perm(n, args.seed, epoch, rank, args.shard, dev))
+        cursor.zero_()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        # batch 0: eager (initialises momentum on the first epoch), logged
+        tr.train_step()
+        if epoch == 1 and steps_done == 0:
+            torch.cuda.synchronize(dev)
+            emit("first_step")
+        _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer)
+        if runner is None and not args.no_graph:
+            # capturing runs warm-up steps: snapshot the state, capture, restore, so the
+            # trajectory is exactly the eager one (a log block = one graph replay)
+            saved = (tr.flat_params.clone(), tr.flat_momentum.clone())
+            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if world == 1 else 1)
+            tr.flat_params.copy_(saved[0])
+            tr.flat_momentum.copy_(saved[1])
+            cursor.fill_(1)
+        # blocks of log_iv steps ending on a logged batch (batches 1..L, L+1..2L, ...)
+        b = 1
+        while b < steps_per_epoch:
+            chunk = min(log_iv, steps_per_epoch - b)
+            if runner is not None and chunk % runner.steps_per_graph == 0:
+                runner.run(chunk)
+            else:
+                for _ in range(chunk):
+                    tr.train_step()
+            b += chunk
+            if (b - 1) % log_iv == 0:
+                _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer)
+        torch.cuda.synchronize(dev)
+        t_train += time.perf_counter() - t0
+        steps_done += steps_per_epoch
+        loss, acc = _evaluate_hip(tr, K, xte, yte, args.test_batch_size)
+        _log_test(acc, epoch, writer)
+    if args.save_model and rank == 0:
+        torch.save({k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}, args.model_path)
+    return {"steps": steps_done, "train_seconds": round(t_train, 4),
+            "samples_per_sec": round(steps_done * B * world / t_train, 1) if t_train else None,
+            "test_loss": round(loss, 5), "accuracy": round(acc, 5)}
+
+
+def _evaluate_hip(tr, K, xte, yte, batch_size):
+    src = K.BatchSource(xte, yte)
+    return tr.evaluate(src, batch_size=min(batch_size, xte.shape[0]))
+
+
+def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> dict:
+    import torch
+    import torch.nn.functional as F
+    from ..models.mnist import Net
+
+    dev, world, rank = env.device, env.world_size, env.rank
+    B, n = args.batch_size, xtr.shape[0]
+    torch.manual_seed(args.seed)
+    model = Net().to(dev)
+    if world > 1:
+        kw = {"device_ids": [dev.index]} if dev.type == "cuda" else {}
+        model = torch.nn.parallel.DistributedDataParallel(model, **kw)
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum)
+
+    def norm(x):
+        return ((x.float() / 255.0 - 0.1307) / 0.3081).view(-1, 1, 28, 28)
+
+    t_train, steps_done = 0.0, 0
+    for epoch in range(1, args.epochs + 1):
+        model.train()
+        perm = _epoch_perm(n, args.seed, epoch, rank, args.shard, dev).long()
+        t0 = time.perf_counter()
+        for batch_idx in range(steps_per_epoch):
+            idx = perm[batch_idx * B:(batch_idx + 1) * B]
+            data, target = norm(xtr[idx]), ytr[idx].long()
+            opt.zero_grad()
+            loss = F.nll_loss(model(data), target)
+            loss.backward()
+            opt.step()
+            if epoch == 1 and batch_idx == 0:
+                emit("first_step")
+            if batch_idx % args.log_interval == 0:
+                _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss.item(), writer)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t_train += time.perf_counter() - t0
+        steps_done += steps_per_epoch
+        model.eval()
+        test_loss, correct = 0.0, 0
+        with torch.no_grad():
+            for s in range(0, xte.shape[0], args.test_batch_size):
+                data, target = norm(xte[s:s + args.test_batch_size]), yte[s:s + args.test_batch_size].long()
+                out = model(data)
+                test_loss += F.nll_loss(out, target, reduction="sum").item()
+                correct += out.argmax(1).eq(target).sum().item()
+        acc = correct / xte.shape[0]
+        test_loss /= xte.shape[0]
+        _log_test(acc, epoch, writer)
+    if args.save_model and rank == 0:
+        m = model.module if hasattr(model, "module") else model
+        torch.save(m.state_dict(), args.model_path)
+    return {"steps": steps_done, "train_seconds": round(t_train, 4),
+            "samples_per_sec": round(steps_done * B * world / t_train, 1) if t_train else None,
+            "test_loss": round(test_loss, 5), "accuracy": round(acc, 5)}
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    run(args)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
