@@ -56,7 +56,10 @@ class EventSink {
 
 class PyTorchController {
  public:
-  PyTorchController(KubeClient* client, ControllerOptions opts);
+  // `core` serves pods/services/events/podgroups, `jobs` the PyTorchJob resource: two
+  // clients with independent rate limiters, like the reference's kubeClientSet and
+  // pytorchJobClientSet (app/server.go:createClientSets).  jobs may equal core.
+  PyTorchController(KubeClient* core, KubeClient* jobs, ControllerOptions opts);
   ~PyTorchController();
 
   void start_informers();
@@ -85,6 +88,7 @@ class PyTorchController {
   std::string write_status(Json& job, const Json& status);
 
   KubeClient* client_;
+  KubeClient* jclient_;
   ControllerOptions o_;
   Expectations exp_;
   RateLimitedQueue queue_;

@@ -25,6 +25,8 @@ struct ServerOption {
   int burst = 10;
   // extensions
   bool leader_elect = true;
+  // leader-election timings (client-go LeaderElectionConfig; reference hardcodes 15s/5s/3s)
+  double lease_duration_s = 15.0, renew_deadline_s = 5.0, retry_period_s = 3.0;
   bool inject_rccl_env = false;
   std::string init_container_template_file = "/etc/config/initContainer.yaml";
   std::string log_level = "info";

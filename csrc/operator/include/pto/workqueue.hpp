@@ -93,7 +93,13 @@ class RateLimitedQueue {
       if (wake == clock::time_point::max()) {
         cv_.wait(lk);
       } else {
-        if (cv_.wait_until(lk, wake) == std::cv_status::timeout && clock::now() >= deadline) {
+        // Sleep on a system_clock deadline: libstdc++ maps steady_clock waits to
+        // pthread_cond_clockwait, which ThreadSanitizer (gcc 11) does not intercept and
+        // misreports as a double lock.  Every wake re-checks the steady-clock state.
+        auto sys_wake = std::chrono::system_clock::now() +
+                        std::chrono::duration_cast<std::chrono::system_clock::duration>(wake - clock::now());
+        cv_.wait_until(lk, sys_wake);
+        if (clock::now() >= deadline) {
           promote_due_locked();
           if (queue_.empty()) return false;
           break;

@@ -132,12 +132,12 @@ void EventSink::loop() {
 }
 
 // ------------------------------------------------------------------ controller
-PyTorchController::PyTorchController(KubeClient* client, ControllerOptions opts)
-    : client_(client), o_(std::move(opts)), events_(client) {
+PyTorchController::PyTorchController(KubeClient* core, KubeClient* jobs, ControllerOptions opts)
+    : client_(core), jclient_(jobs ? jobs : core), o_(std::move(opts)), events_(core) {
   Informer::Handlers jh{[this](const Json& o) { add_job(o); },
                         [this](const Json& a, const Json& b) { update_job(a, b); },
                         [this](const Json& o) { delete_job(o); }};
-  jobs_ = std::make_unique<Informer>(client_, kPyTorchJobs, o_.watch_namespace, "", o_.job_resync_s, jh);
+  jobs_ = std::make_unique<Informer>(jclient_, kPyTorchJobs, o_.watch_namespace, "", o_.job_resync_s, jh);
   Informer::Handlers ph{[this](const Json& o) { add_pod(o); },
                         [this](const Json& a, const Json& b) { update_pod(a, b); },
                         [this](const Json& o) { delete_pod(o); }};
@@ -183,7 +183,7 @@ void PyTorchController::add_job(const Json& obj) {
       Json job = obj;
       job["status"] = r.status;
       ApiError err;
-      if (auto out = client_->update_status(kPyTorchJobs, job_namespace(obj), job, &err)) jobs_->update_cache(*out);
+      if (auto out = jclient_->update_status(kPyTorchJobs, job_namespace(obj), job, &err)) jobs_->update_cache(*out);
       else LOG_ERROR("Could not update the PyTorchJob: %s", err.message.c_str());
     }
     return;
@@ -304,7 +304,7 @@ std::vector<Json> PyTorchController::claim(const Json& job, Informer* inf, const
     // orphan with matching labels: adopt after re-checking the job is not being deleted
     if (!can_adopt_checked) {
       ApiError err;
-      auto fresh = client_->get(kPyTorchJobs, ns, job_name(job), &err);
+      auto fresh = jclient_->get(kPyTorchJobs, ns, job_name(job), &err);
       can_adopt = fresh && job_uid(*fresh) == uid && !being_deleted(*fresh);
       can_adopt_checked = true;
     }
@@ -336,7 +336,7 @@ std::string PyTorchController::write_status(Json& job, const Json& status) {
   Json upd = job;
   upd["status"] = status;
   ApiError err;
-  auto out = client_->update_status(kPyTorchJobs, job_namespace(job), upd, &err);
+  auto out = jclient_->update_status(kPyTorchJobs, job_namespace(job), upd, &err);
   if (!out) return "update status: " + err.message;
   jobs_->update_cache(*out);
   job = *out;
@@ -413,7 +413,7 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
   if (!r.error.empty()) return r.error;
   if (r.delete_job) {
     ApiError e2;
-    if (!client_->del(kPyTorchJobs, ns, job_name(job), &e2) && !e2.not_found())
+    if (!jclient_->del(kPyTorchJobs, ns, job_name(job), &e2) && !e2.not_found())
       return "Cleanup PyTorchJob error: " + e2.message;
   }
   if (r.status_changed && !r.delete_job) {

@@ -36,9 +36,11 @@ static std::string read_file(const std::string& path, bool* ok) {
   return ss.str();
 }
 
-static const Json* named(const Json& list, const std::string& name) {
-  if (!list.is_array()) return nullptr;
-  for (const auto& e : list.as_array())
+// Entry `name` of a kubeconfig list (doc[key]); a pointer into doc, never a temporary.
+static const Json* named(const Json& doc, const char* key, const std::string& name) {
+  const Json* list = doc.get(key);
+  if (!list || !list->is_array()) return nullptr;
+  for (const auto& e : list->as_array())
     if (e.str_or("name") == name) return &e;
   return nullptr;
 }
@@ -63,12 +65,12 @@ std::optional<KubeConfig> load_kube_config(const std::string& master_url, const 
       return std::nullopt;
     }
     std::string ctx_name = doc.str_or("current-context");
-    const Json* ctx = named(doc.get("contexts") ? *doc.get("contexts") : Json(), ctx_name);
+    const Json* ctx = named(doc, "contexts", ctx_name);
     const Json* ctxv = ctx ? ctx->get("context") : nullptr;
     std::string cluster_name = ctxv ? ctxv->str_or("cluster") : "";
     std::string user_name = ctxv ? ctxv->str_or("user") : "";
     if (ctxv && !ctxv->str_or("namespace").empty()) kc.ns = ctxv->str_or("namespace");
-    const Json* cl = named(doc.get("clusters") ? *doc.get("clusters") : Json(), cluster_name);
+    const Json* cl = named(doc, "clusters", cluster_name);
     if (!cl && doc.get("clusters") && doc.get("clusters")->size() > 0) cl = &doc.get("clusters")->as_array()[0];
     const Json* clv = cl ? cl->get("cluster") : nullptr;
     if (clv) {
@@ -78,7 +80,7 @@ std::optional<KubeConfig> load_kube_config(const std::string& master_url, const 
         kc.tls.ca_data = base64_decode(clv->str_or("certificate-authority-data"));
       kc.tls.insecure_skip_verify = clv->bool_or("insecure-skip-tls-verify", false);
     }
-    const Json* us = named(doc.get("users") ? *doc.get("users") : Json(), user_name);
+    const Json* us = named(doc, "users", user_name);
     const Json* usv = us ? us->get("user") : nullptr;
     if (usv) {
       kc.token = usv->str_or("token");

@@ -103,12 +103,14 @@ int main(int argc, char** argv) {
     LOG_ERROR("Error building kubeconfig: %s", cerr.c_str());
     return 1;
   }
-  KubeClient client(*kcfg, opt.qps, opt.burst);
+  KubeClient client(*kcfg, opt.qps, opt.burst);       // pods / services / events / podgroups
+  KubeClient job_client(*kcfg, opt.qps, opt.burst);   // pytorchjobs (own rate limiter)
+  KubeClient lease_client(*kcfg, opt.qps, opt.burst); // leader election
 
   // checkCRDExists (server.go:201-213): a NotFound on LIST means the CRD is missing.
   {
     ApiError err;
-    if (!client.list(kPyTorchJobs, opt.namespace_, "", &err)) {
+    if (!job_client.list(kPyTorchJobs, opt.namespace_, "", &err)) {
       LOG_ERROR("list pytorchjobs: %s", err.message.c_str());
       if (err.not_found()) {
         LOG_INFO("CRD doesn't exist. Exiting");
@@ -136,14 +138,17 @@ int main(int argc, char** argv) {
       LOG_INFO("Using default init container template");
     }
   }
-  PyTorchController tc(&client, co);
+  PyTorchController tc(&client, &job_client, co);
   tc.start_informers();
 
   auto run = [&] { tc.run(&g_stop); };
   if (opt.leader_elect) {
     LeaderElectionConfig lc;
     lc.ns = lock_ns;
-    LeaderElector le(&client, lc);
+    lc.lease_s = opt.lease_duration_s;
+    lc.renew_deadline_s = opt.renew_deadline_s;
+    lc.retry_s = opt.retry_period_s;
+    LeaderElector le(&lease_client, lc);
     le.run(run, [] {
       LOG_ERROR("leader election lost");
       std::fflush(stderr);

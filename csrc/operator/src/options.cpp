@@ -60,6 +60,9 @@ std::string usage() {
          "  -qps int                  Maximum QPS to the master from this client (default 5)\n"
          "  -burst int                Maximum burst for throttle (default 10)\n"
          "  -leader-elect             Run leader election on a Lease (default true)\n"
+         "  -leader-elect-lease-duration duration   (default 15s)\n"
+         "  -leader-elect-renew-deadline duration   (default 5s)\n"
+         "  -leader-elect-retry-period duration     (default 3s)\n"
          "  -inject-rccl-env          Inject LOCAL_RANK and RCCL tuning env into pytorch containers\n"
          "  -init-container-template-file  (default /etc/config/initContainer.yaml)\n"
          "  -log-level string         debug|info|warning|error (default info)\n";
@@ -87,6 +90,12 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
                   return std::string();
                 }};
   };
+  auto duration = [](double* dst) {
+    return Flag{false, [dst](const std::string& v) {
+                  if (!parse_duration(v, dst)) return std::string("invalid duration \"") + v + "\"";
+                  return std::string();
+                }};
+  };
   auto ignore_bool = Flag{true, [](const std::string&) { return std::string(); }};
   auto ignore_val = Flag{false, [](const std::string&) { return std::string(); }};
   std::map<std::string, Flag> flags = {
@@ -107,6 +116,9 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
       {"qps", integer(&o->qps)},
       {"burst", integer(&o->burst)},
       {"leader-elect", boolean(&o->leader_elect)},
+      {"leader-elect-lease-duration", duration(&o->lease_duration_s)},
+      {"leader-elect-renew-deadline", duration(&o->renew_deadline_s)},
+      {"leader-elect-retry-period", duration(&o->retry_period_s)},
       {"inject-rccl-env", boolean(&o->inject_rccl_env)},
       {"init-container-template-file", str(&o->init_container_template_file)},
       {"log-level", str(&o->log_level)},

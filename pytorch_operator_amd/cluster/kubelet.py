@@ -64,14 +64,45 @@ SCRIPT_MAP = {
 }
 
 
+_POD_SCOPED_ENV = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                   "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID", "KUBECONFIG", "PYTHONPATH"}
+
+
 def _now() -> str:
     return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
 
 
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+def _ephemeral_range():
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo, hi = (int(x) for x in f.read().split())
+        return lo, hi
+    except (OSError, ValueError):
+        return 32768, 60999
+
+
+def _free_port(taken=()) -> int:
+    """A free port *below* the kernel's ephemeral range.
+
+    Rendezvous ports are connected to before anyone listens (workers race the master's
+    TCPStore); a port inside the ephemeral range can then be handed out as the client's own
+    source port, and the TCP simultaneous-open rule connects the socket to itself -- a
+    silent hang in init_process_group.  Ports below the range never collide that way.
+    """
+    import random
+    lo, _ = _ephemeral_range()
+    base = max(1024, lo - 12000)
+    for _ in range(1000):
+        port = random.randrange(base, lo)
+        if port in taken:
+            continue
+        with socket.socket() as s:
+            try:
+                s.bind(("0.0.0.0", port))
+            except OSError:
+                continue
+            return port
+    raise RuntimeError("no free rendezvous port")
 
 
 class _Container:
@@ -221,13 +252,13 @@ class PodRunner(threading.Thread):
         return cmd + args
 
     def _env(self, spec: dict) -> Dict[str, str]:
-        base = {k: v for k, v in os.environ.items()
-                if k in ("PATH", "HOME", "LANG", "LC_ALL", "TMPDIR", "HSA_ENABLE_IPC_MODE_LEGACY",
-                         "LD_LIBRARY_PATH", "ROCM_PATH", "OMP_NUM_THREADS")}
+        # the node's environment minus anything a container must get from its pod spec
+        base = {k: v for k, v in os.environ.items() if k not in _POD_SCOPED_ENV}
         base["PYTHONPATH"] = os.pathsep.join([self.k.repo_root] + [p for p in
                                             os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
         base["HOSTNAME"] = self.name
         base["PYTHONUNBUFFERED"] = "1"
+        base.setdefault("PYTHONFAULTHANDLER", "1")  # SIGABRT/SIGSEGV dump Python stacks into the pod log
         base.setdefault("OMP_NUM_THREADS", "1")
         md = self.pod["metadata"]
         for e in spec.get("env") or []:
@@ -245,12 +276,16 @@ class PodRunner(threading.Thread):
             # the master itself gets MASTER_ADDR=localhost (pod.go:246-251): its Service
             # carries the pod's name, so map it to the same per-Service port as the workers
             svc = self.name if addr in ("localhost", "127.0.0.1") else addr.split(".")[0]
-            port = self.k._service_port(self.ns, svc, base.get("MASTER_PORT"))
+            port = self.k._service_port(self.ns, svc, base.get("MASTER_PORT"),
+                                        known=addr in ("localhost", "127.0.0.1"))
             if port is not None:
                 base["MASTER_ADDR"] = "127.0.0.1"
                 base["MASTER_PORT"] = str(port)
         if self.gpus:
-            base["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in self.gpus)
+            # node-relative ids -> the node's own visible set (never widen visibility)
+            node = [d for d in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if d.strip()]
+            ids = [node[g] if node else str(g) for g in self.gpus]
+            base["HIP_VISIBLE_DEVICES"] = ",".join(ids)
         elif self.k.hide_gpus_without_request:
             base["HIP_VISIBLE_DEVICES"] = ""
         base.update(self.k.extra_env)
@@ -386,17 +421,22 @@ class LocalKubelet:
             r.gpus = []
             self.finished_pods.append(f"{r.ns}/{r.name}")
 
-    def _service_port(self, ns: str, svc: str, port: Optional[str]) -> Optional[int]:
+    def _service_port(self, ns: str, svc: str, port: Optional[str], known: bool = False) -> Optional[int]:
+        """Host port standing in for ``svc:port``.  ``known``: the caller is the pod behind
+        the Service (the master, which may start before its Service is created)."""
         with self.lock:
             key = (ns, svc, port)
             if key in self.ports:
                 return self.ports[key]
-        try:
-            self.rest.get(SERVICES, svc, ns)
-        except ApiException:
-            return None
+        if not known:
+            try:
+                self.rest.get(SERVICES, svc, ns)
+            except ApiException:
+                return None
         with self.lock:
-            return self.ports.setdefault(key, _free_port())
+            if key not in self.ports:
+                self.ports[key] = _free_port(set(self.ports.values()))
+            return self.ports[key]
 
     # ---------------------------------------------------------------- watch loop
     def _mine(self, pod: dict) -> bool:

@@ -34,7 +34,7 @@ def operator_binary() -> str:
     return p
 
 
-def _free_port() -> int:
+def free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -60,7 +60,7 @@ class LocalCluster:
         self.kubelet_env = kubelet_env
         self.verbose = verbose
         self.operator: Optional[subprocess.Popen] = None
-        self.monitoring_port = _free_port()
+        self.monitoring_port = free_port()
         self.operator_log = os.path.join(workdir, "operator.log")
         self.kubelet: Optional[LocalKubelet] = None
         self.rest: Optional[KubeRest] = None
@@ -77,14 +77,19 @@ class LocalCluster:
             self.start_operator_process()
         return self
 
-    def start_operator_process(self, extra_args: Optional[List[str]] = None) -> subprocess.Popen:
+    def spawn_operator(self, monitoring_port: int, log_path: str,
+                       extra_args: Optional[List[str]] = None) -> subprocess.Popen:
+        """Start one operator replica (several may run: leader election picks one)."""
         args = [operator_binary(), "--kubeconfig", self.kubeconfig,
-                f"--monitoring-port={self.monitoring_port}", "--json-log-format=false",
+                f"--monitoring-port={monitoring_port}", "--json-log-format=false",
                 *self.operator_args, *(extra_args or [])]
         env = dict(os.environ, KUBEFLOW_NAMESPACE="kubeflow", **self.operator_env)
         env.pop("KUBECONFIG", None)
-        self.operator = subprocess.Popen(args, env=env, stdout=open(self.operator_log, "ab"),
-                                         stderr=subprocess.STDOUT, start_new_session=True)
+        with open(log_path, "ab") as log:
+            return subprocess.Popen(args, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+
+    def start_operator_process(self, extra_args: Optional[List[str]] = None) -> subprocess.Popen:
+        self.operator = self.spawn_operator(self.monitoring_port, self.operator_log, extra_args)
         return self.operator
 
     def stop_operator(self, timeout: float = 15.0):

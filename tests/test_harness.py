@@ -1,0 +1,155 @@
+"""Worker entrypoints on CPU: the MNIST DDP worker and the smoke send/recv test.
+
+The reference has no tests for examples/; these pin its observable contract (CLI,
+log lines, TensorBoard scalars, DDP over the env rendezvous) for the MI355X worker.
+Multi-process cases use gloo with world_size 2 on 127.0.0.1.
+"""
+import glob
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from pytorch_operator_amd.data.mnist_idx import load_mnist, read_idx, write_idx
+from pytorch_operator_amd.utils.tb_writer import SummaryWriter, crc32c, read_events
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(module, args, world, cwd, timeout=240):
+    port = _port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(r),
+                   PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, "-m", module, *args], cwd=cwd, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=timeout)
+        outs.append((p.returncode, out))
+    return outs
+
+
+def _events(out):
+    return [json.loads(x) for x in out.splitlines() if x.startswith('{"event"')]
+
+
+def test_crc32c_known_vector():
+    assert crc32c(b"123456789") == 0xE3069283
+
+
+def test_tensorboard_writer_roundtrip(tmp_path):
+    with SummaryWriter(str(tmp_path)) as w:
+        w.add_scalar("loss", 2.5, 0)
+        w.add_scalar("loss", 1.25, 10)
+        w.add_scalar("accuracy", 0.5, 1)
+    ev = read_events(glob.glob(str(tmp_path / "events.out.tfevents.*"))[0])
+    assert ev[1:] == [(0, {"loss": 2.5}), (10, {"loss": 1.25}), (1, {"accuracy": 0.5})]
+    lines = [json.loads(x) for x in open(tmp_path / "scalars.jsonl")]
+    assert [x["tag"] for x in lines] == ["loss", "loss", "accuracy"]
+
+
+def test_idx_reader_roundtrip(tmp_path):
+    x = np.random.default_rng(0).integers(0, 256, (7, 28, 28), dtype=np.uint8)
+    y = np.arange(7, dtype=np.uint8)
+    raw = tmp_path / "MNIST" / "raw"
+    raw.mkdir(parents=True)
+    write_idx(str(raw / "train-images-idx3-ubyte.gz"), x)
+    write_idx(str(raw / "train-labels-idx1-ubyte"), y)
+    assert (read_idx(str(raw / "train-images-idx3-ubyte.gz")) == x).all()
+    xi, yi = load_mnist(str(tmp_path), "train")
+    assert xi.shape == (7, 784) and xi.dtype == torch.uint8 and yi.dtype == torch.int32
+    assert (xi.numpy().reshape(7, 28, 28) == x).all() and (yi.numpy() == y).all()
+    assert load_mnist(str(tmp_path), "test") is None
+
+
+def test_mnist_worker_single_process_reference_output(tmp_path):
+    (rc, out), = _launch("pytorch_operator_amd.harness.mnist",
+                         ["--dataset-size", "1280", "--test-size", "400", "--log-interval", "5", "--save-model",
+                          "--dir", str(tmp_path / "tb")], 1, tmp_path)
+    assert rc == 0, out
+    assert "Train Epoch: 1 [0/1280 (0%)]\tloss=" in out
+    assert "Train Epoch: 1 [320/1280 (25%)]\tloss=" in out
+    assert "\naccuracy=" in out
+    ev = _events(out)
+    assert [e["event"] for e in ev] == ["start", "first_step", "train_done"]
+    assert ev[0]["kernels"] == "torch" and ev[-1]["steps"] == 20
+    sd = torch.load(tmp_path / "mnist_cnn.pt", weights_only=True)
+    assert sd["fc1.weight"].shape == (500, 800)
+    scal = [json.loads(x) for x in open(tmp_path / "tb" / "scalars.jsonl")]
+    assert [s["step"] for s in scal if s["tag"] == "loss"] == [20, 25, 30, 35]  # epoch*len + batch_idx
+
+
+def test_mnist_worker_learns_on_real_idx_files(tmp_path):
+    """IDX files present -> used instead of synthetic data (content from the synthetic generator)."""
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    d = tmp_path / "data"
+    d.mkdir()
+    tr, te = make_synthetic_mnist(3000, seed=3), make_synthetic_mnist(500, seed=4)
+    write_idx(str(d / "train-images-idx3-ubyte"), tr.images.numpy().reshape(-1, 28, 28))
+    write_idx(str(d / "train-labels-idx1-ubyte"), tr.labels.numpy().astype(np.uint8))
+    write_idx(str(d / "t10k-images-idx3-ubyte"), te.images.numpy().reshape(-1, 28, 28))
+    write_idx(str(d / "t10k-labels-idx1-ubyte"), te.labels.numpy().astype(np.uint8))
+    (rc, out), = _launch("pytorch_operator_amd.harness.mnist", ["--data-dir", str(d), "--epochs", "2",
+                                                                "--dir", str(tmp_path / "tb")], 1, tmp_path)
+    assert rc == 0, out
+    ev = _events(out)
+    assert ev[0]["data"] == "mnist-idx" and ev[0]["n_train"] == 3000
+    assert out.count("accuracy=") == 2
+    assert ev[-1]["accuracy"] > 0.5
+
+
+def test_mnist_worker_ddp_gloo_two_ranks(tmp_path):
+    outs = _launch("pytorch_operator_amd.harness.mnist",
+                   ["--backend", "gloo", "--dataset-size", "1280", "--test-size", "256", "--dir",
+                    str(tmp_path / "tb")], 2, tmp_path)
+    for rc, out in outs:
+        assert rc == 0, out
+        assert "Using distributed PyTorch with gloo backend" in out
+    ev0, ev1 = _events(outs[0][1]), _events(outs[1][1])
+    # sharded: 640 samples per rank -> 10 steps each; DDP keeps the replicas identical
+    assert ev0[-1]["steps"] == 10 and ev1[-1]["steps"] == 10
+    assert ev0[-1]["test_loss"] == ev1[-1]["test_loss"]
+
+
+def test_mnist_worker_no_shard_matches_reference_semantics(tmp_path):
+    outs = _launch("pytorch_operator_amd.harness.mnist",
+                   ["--backend", "gloo", "--dataset-size", "640", "--test-size", "128", "--no-shard",
+                    "--dir", str(tmp_path / "tb")], 2, tmp_path)
+    for rc, out in outs:
+        assert rc == 0, out
+    assert _events(outs[0][1])[-1]["steps"] == 10  # every rank walks the whole set
+
+
+def test_backend_aliases():
+    from pytorch_operator_amd.parallel.dist import backend_for
+    assert backend_for("rccl", True) == "nccl"
+    assert backend_for("GLOO", False) == "gloo"
+    assert backend_for(None, False) == "gloo" and backend_for(None, True) == "nccl"
+    with pytest.raises(ValueError):
+        backend_for("ucc", False)
+    with pytest.raises(RuntimeError):
+        backend_for("mpi", False)
+
+
+def test_dist_sendrecv_three_ranks(tmp_path):
+    outs = _launch("pytorch_operator_amd.harness.dist_sendrecv", [], 3, tmp_path, timeout=120)
+    for rc, out in outs:
+        assert rc == 0, out
+    master = outs[0][1]
+    assert "Result from worker 1" in master and "Result from worker 2" in master
+    assert "all_reduce ok (6.0)" in master
+    assert "MASTER_ADDR: 127.0.0.1" in master and "WORLD_SIZE: 3" in master
