@@ -26,6 +26,11 @@ What it emulates
   with ``state.terminated.exitCode`` -- the field the ExitCode restart policy reads
   (reference pkg/controller.v1/pytorch/pod.go:116-135);
 * deletion: SIGTERM to the container's process group, SIGKILL after the grace period;
+* fault injection (the SURVEY 5.3 injector): pod annotations
+  ``fault.pto.amd.com/exit-code`` (exit code to report), ``fault.pto.amd.com/after-seconds``
+  (delay after container start, default 0) and ``fault.pto.amd.com/times`` (how many runs of
+  that pod *name* to hit, default 1; counted across pod recreations) kill the container and
+  report the given code -- e.g. 137 to exercise the ExitCode restart policy with a real job;
 * logs: stdout/stderr of every container go to ``<log_dir>/<ns>_<pod>.log``, served by the
   fake API server's ``pods/{name}/log`` endpoint.
 """
@@ -323,9 +328,19 @@ class PodRunner(threading.Thread):
             if not init:
                 self._push("Running", [{"type": "PodScheduled", "status": "True"},
                                        {"type": "Ready", "status": "True", "lastTransitionTime": started}])
+            injected = None if init else self.k._fault_for(self)
+            if injected is not None:
+                code_fault, after = injected
+                timer = threading.Timer(after, self._inject, args=(c.proc,))
+                timer.daemon = True
+                timer.start()
             code = c.proc.wait()
             if code < 0:  # killed by signal -> 128+N like a container runtime
                 code = 128 - code
+            if injected is not None:
+                timer.cancel()
+                if code == 128 + signal.SIGKILL and self._alive():
+                    code = code_fault
             if not self._alive():
                 return
             term = {"exitCode": code, "reason": "Completed" if code == 0 else "Error",
@@ -342,6 +357,13 @@ class PodRunner(threading.Thread):
             c.exit_code = code
             c.state = {"terminated": term}
             return
+
+    @staticmethod
+    def _inject(proc: subprocess.Popen):
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except (ProcessLookupError, PermissionError):
+            pass
 
     def kill(self, grace_s: float = 2.0):
         self.stopping.set()
@@ -386,6 +408,7 @@ class LocalKubelet:
         self.verbose = verbose
         self.runners: Dict[str, PodRunner] = {}
         self.ports: Dict[tuple, int] = {}
+        self.faults_done: Dict[tuple, int] = {}
         self.lock = threading.RLock()
         self.stopped = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="kubelet")
@@ -420,6 +443,19 @@ class LocalKubelet:
             self.free_gpus = sorted(self.free_gpus + r.gpus)
             r.gpus = []
             self.finished_pods.append(f"{r.ns}/{r.name}")
+
+    def _fault_for(self, r: PodRunner):
+        """(exit_code, after_s) when this run of the pod should be killed, else None."""
+        ann = r.pod["metadata"].get("annotations") or {}
+        if "fault.pto.amd.com/exit-code" not in ann:
+            return None
+        key = (r.ns, r.name)
+        with self.lock:
+            n = self.faults_done.get(key, 0)
+            if n >= int(ann.get("fault.pto.amd.com/times", "1")):
+                return None
+            self.faults_done[key] = n + 1
+        return int(ann["fault.pto.amd.com/exit-code"]), float(ann.get("fault.pto.amd.com/after-seconds", "0"))
 
     def _service_port(self, ns: str, svc: str, port: Optional[str], known: bool = False) -> Optional[int]:
         """Host port standing in for ``svc:port``.  ``known``: the caller is the pod behind

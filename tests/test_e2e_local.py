@@ -286,3 +286,36 @@ def test_leader_failover(tmp_path):
         finally:
             standby.terminate()
             standby.wait(15)
+
+
+def test_injected_worker_fault_is_retried_under_exit_code_policy(cluster):
+    """Kubelet fault injection: the worker is SIGKILLed once (137, retryable),
+    the operator recreates it and the real gloo rendezvous still completes."""
+    c = cluster
+    worker = replica(1, policy="ExitCode")
+    worker["template"]["metadata"] = {"annotations": {"fault.pto.amd.com/exit-code": "137",
+                                                      "fault.pto.amd.com/after-seconds": "0.1"}}
+    c.rest.create(PYTORCHJOBS, make_job("e2e-fault", replica(1, policy="ExitCode"), worker), NS)
+    types, job = wait_finished(c, "e2e-fault", timeout=120)
+    assert types[-1] == "Succeeded", job["status"]
+    assert "all_reduce ok (3.0)" in c.rest.pod_log("e2e-fault-master-0", NS)
+    evs = [e for e in c.rest.list(EVENTS, NS)["items"] if e.get("reason") == "ExitedWithCode"
+           and "e2e-fault-worker-0" in e.get("message", "")]
+    assert evs, "operator should record the retryable exit"
+
+
+def test_many_concurrent_jobs_with_threadiness(tmp_path):
+    """Multi-worker reconcile stress: 4 sync threads, 12 concurrent jobs."""
+    with LocalCluster(workdir=str(tmp_path / "s"), operator_args=["--threadiness=4", "--qps=50",
+                                                                  "--burst=100"]) as c:
+        c.wait_operator_ready()
+        names = [f"stress-{i}" for i in range(12)]
+        for n in names:
+            c.rest.create(PYTORCHJOBS, make_job(n, replica(1, "busybox", command=py("pass")),
+                                                replica(2, "busybox", command=py("pass"))), NS)
+        for n in names:
+            types, job = wait_finished(c, n, timeout=120)
+            assert types[-1] == "Succeeded", (n, job["status"])
+            # (the master's success ends the job: workers may not have started yet)
+            assert len(pod_names(c, n)) == 3  # expectations: no duplicate pods under concurrency
+        assert c.metric_value("pytorch_operator_jobs_successful_total") == 12
