@@ -43,6 +43,8 @@ def parse_args(argv=None):
     p.add_argument("--dataset-size", type=int, default=60000)
     p.add_argument("--overlap", type=int, default=0, help="side-stream overlap in the step (1/0)")
     p.add_argument("--fuse-conv12", type=int, default=1)
+    p.add_argument("--backend", default="nccl", choices=["nccl", "rccl", "gloo"],
+                   help="collective backend (gloo only to rehearse the multi-rank path on one GPU)")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -55,7 +57,7 @@ def main(argv=None):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_operator_amd.parallel.dist import init_from_env
 
-    env = init_from_env("nccl", use_gpu=True)
+    env = init_from_env(args.backend, use_gpu=True)
     world, rank, dev = env.world_size, env.rank, env.device
     if world != args.gpus:
         if rank == 0:
@@ -143,6 +145,17 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    in_sync = None
+    if world > 1:
+        # DDP invariant (checked after the timed region): every replica holds rank 0's weights
+        flat = tr.flat_params if args.kernels == "hip" else torch.cat(
+            [q.detach().reshape(-1) for q in model.parameters()])
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        diff = (flat - ref).abs().max().reshape(1)
+        dist.all_reduce(diff, op=dist.ReduceOp.MAX)
+        in_sync = bool(float(diff.item()) == 0.0)
+
     samples = steps * B * world
     value = samples / dt
     result = {
@@ -156,6 +169,7 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (BASELINE_PER_RANK * world), 1),
+        "replicas_in_sync": in_sync,
         "dtype": "fp32",
         "data": "synthetic (learnable MNIST-shaped uint8 images in HBM), random-init weights",
         "config": {
@@ -167,7 +181,7 @@ def main(argv=None):
             "optimizer": "SGD(lr=0.01, momentum=0.5)",
             "kernels": args.kernels,
             "exec": mode_desc,
-            "backend": "rccl" if world > 1 else "none",
+            "backend": ("rccl" if env.backend == "nccl" else env.backend) if world > 1 else "none",
         },
     }
     if rank == 0:

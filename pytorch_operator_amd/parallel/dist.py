@@ -72,8 +72,14 @@ def init_from_env(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank % ngpu if ngpu else 0)))
     b = backend_for(backend, use_gpu)
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        dev_index = local_rank
+        if ngpu and local_rank >= ngpu:
+            if b == "nccl":
+                raise RuntimeError(f"LOCAL_RANK {local_rank} but only {ngpu} visible GPU(s); RCCL needs one GPU per rank")
+            # gloo rehearsal of a multi-rank job on fewer GPUs (ranks share a device)
+            dev_index = local_rank % ngpu
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
