@@ -45,6 +45,9 @@ def parse_args(argv=None):
     p.add_argument("--fuse-conv12", type=int, default=1)
     p.add_argument("--backend", default="nccl", choices=["nccl", "rccl", "gloo"],
                    help="collective backend (gloo only to rehearse the multi-rank path on one GPU)")
+    p.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
+                   help="DDP gradient path for world>1: xGMI peer-memory kernel fused with SGD "
+                        "(self-tested at start-up, RCCL fallback) or RCCL all-reduce")
     p.add_argument("--json-out", default=None)
     return p.parse_args(argv)
 
@@ -71,11 +74,18 @@ def main(argv=None):
     if args.kernels == "hip":
         from pytorch_operator_amd.models.mnist import FusedMnistTrainer
         from pytorch_operator_amd.ops import mnist as K
-        from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
         from pytorch_operator_amd.parallel.graphed_step import GraphedStep
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
-        sync = FlatGradAllReduce() if world > 1 else None
+        sync, xg, ar_path = None, None, "none"
+        if world > 1:
+            from pytorch_operator_amd.models.mnist import flat_layout
+            from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
+            from pytorch_operator_amd.parallel.xgmi import try_xgmi
+            sync, ar_path = FlatGradAllReduce(), "rccl"
+            if args.allreduce != "rccl":
+                xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
+                              log=lambda m: print(m, file=sys.stderr) if rank == 0 else None)
         tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
                                seed=1, grad_sync=sync)
         tr.overlap = bool(args.overlap)
@@ -83,27 +93,32 @@ def main(argv=None):
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph
-        if spg <= 0:
-            spg = 1
-            if world == 1 or args.mode == "graph-comm":
-                for cand in (10, 8, 5, 4, 2):
-                    if args.steps % cand == 0 and args.warmup % cand == 0:
-                        spg = cand
-                        break
-        if world > 1 and args.mode == "graph":
-            spg = 1
+        if spg <= 0:  # whole steps per graph replay: any divisor of both steps and warmup
+            spg = next((c for c in (10, 8, 5, 4, 2) if args.steps % c == 0 and args.warmup % c == 0), 1)
         eager_w = min(args.warmup, 3)
         for _ in range(eager_w):
             tr.train_step()  # eager warmup: loads the library, initialises momentum
-        runner = GraphedStep(tr, mode=args.mode, steps_per_graph=spg)
-        rest = max(0, args.warmup - eager_w - runner.internal_steps)
+        done_w = eager_w
+        tune = None
+        if xg is not None and args.allreduce == "auto" and args.mode != "eager":
+            # measured choice between RCCL and the xGMI kernel (both trials are warm-up steps)
+            from pytorch_operator_amd.parallel.autotune import choose_grad_sync
+            runner, ar_path, tune = choose_grad_sync(tr, sync, xg, mode=args.mode, spg=spg, trial_steps=40)
+            done_w += 2 * max(spg, 40 - 40 % spg) + 4
+        elif xg is not None:
+            tr.grad_sync, ar_path = xg, "xgmi"
+            runner = GraphedStep(tr, mode="graph" if args.mode != "eager" else "eager", steps_per_graph=spg)
+        else:
+            runner = GraphedStep(tr, mode=args.mode,
+                                 steps_per_graph=1 if (world > 1 and args.mode == "graph") else spg)
+        rest = max(0, args.warmup - done_w - runner.internal_steps)
         rest -= rest % runner.steps_per_graph
         runner.run(rest)
 
         def run(n):
             runner.run(n)
         steps = args.steps - args.steps % runner.steps_per_graph
-        mode_desc = f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap})"
+        mode_desc = f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap},allreduce={ar_path})"
     else:
         from pytorch_operator_amd.models.mnist import Net
         import torch.nn.functional as F
@@ -128,6 +143,7 @@ def main(argv=None):
         run(args.warmup)
         steps = args.steps
         mode_desc = "torch-eager"
+        ar_path, tune = "ddp", None
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -182,6 +198,8 @@ def main(argv=None):
             "kernels": args.kernels,
             "exec": mode_desc,
             "backend": ("rccl" if env.backend == "nccl" else env.backend) if world > 1 else "none",
+            "grad_allreduce": ar_path,
+            "allreduce_trial": tune,
         },
     }
     if rank == 0:

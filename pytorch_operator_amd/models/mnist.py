@@ -261,6 +261,17 @@ class FusedMnistTrainer:
                    overlap: Optional[bool] = None):
         """One full training step (forward, backward, [all-reduce], SGD)."""
         overlap = self.overlap if overlap is None else overlap
+        if getattr(self.grad_sync, "fused_sgd", False):
+            # xGMI path: one kernel does the cross-GPU reduce-scatter, SGD on this rank's
+            # shard and the all-gather of updated parameters (parallel/xgmi.py)
+            self.forward_backward(source, B)
+            self.grad_sync.xar.allreduce_sgd_(
+                self.flat_grads, self.flat_params, self.flat_momentum, lr=self.lr,
+                momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
+                nesterov=self.nesterov, first_step=self._first_step,
+                step_counter=self.cursor if advance_cursor else None)
+            self._first_step = False
+            return
         if self.grad_sync is not None:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
@@ -281,9 +292,6 @@ class FusedMnistTrainer:
                                extra=(self.flat_params[ce:], self.flat_grads[ce:],
                                       self.flat_momentum[ce:]))
             self._first_step = False
-            return
-            self.forward_backward(source, B)
-            self.optimizer_step(advance_cursor)
             return
         K = self.K
         B = self.B if B is None else B

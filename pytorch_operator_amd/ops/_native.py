@@ -102,7 +102,16 @@ _SIGNATURES = {
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     "pto_conv_bwd_lds_bytes": [],
+    # xgmi_allreduce.hip
+    "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],
+    "pto_xar_open": [_VP, _VP],
+    "pto_xar_error": [_VP],
+    "pto_xar_alloc_kind": [_VP],
+    "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],
+    "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
+    "pto_xar_destroy": [_VP],
 }
+_LONG_FNS = {"pto_xar_npad": [_VP]}
 _VOID_FNS = {"pto_set_debug_buffer": [_VP]}
 
 
@@ -123,6 +132,10 @@ def load(build_if_missing: bool = True):
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
+        for name, argtypes in _LONG_FNS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_long
         for name, argtypes in _VOID_FNS.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes

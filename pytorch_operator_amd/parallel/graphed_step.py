@@ -15,6 +15,10 @@ Modes
                 overlaps G2 on RCCL's own stream; G3 waits for both).
 ``graph-comm``  the all-reduces are captured too: one graph per step (RCCL
                 collectives support stream capture).  Fewest host calls.
+
+With the xGMI peer-memory all-reduce (``parallel.xgmi``, ``grad_sync.fused_sgd``) the
+exchange is an ordinary kernel, so ``graph`` captures ``steps_per_graph`` whole DDP
+steps exactly like the single-GPU case.
 """
 from __future__ import annotations
 
@@ -37,6 +41,7 @@ class GraphedStep:
         if mode not in ("eager", "graph", "graph-comm"):
             raise ValueError(f"unknown mode {mode}")
         self.tr = trainer
+        self.sync = trainer.grad_sync  # the gradient path these graphs were built for
         self.mode = mode
         self.steps_per_graph = steps_per_graph if mode != "eager" else 1
         self.world = trainer.grad_sync.world if trainer.grad_sync is not None else 1
@@ -57,7 +62,7 @@ class GraphedStep:
         self.internal_steps += 1
         torch.cuda.current_stream(tr.device).wait_stream(s)
         torch.cuda.synchronize(tr.device)
-        if self.world == 1 or mode == "graph-comm":
+        if self.world == 1 or mode == "graph-comm" or getattr(tr.grad_sync, "fused_sgd", False):
             def whole():
                 for _ in range(self.steps_per_graph):
                     tr.train_step()
@@ -72,6 +77,7 @@ class GraphedStep:
     def run(self, n_steps: int) -> None:
         """Execute ``n_steps`` training steps (must be a multiple of steps_per_graph in graph modes)."""
         tr = self.tr
+        tr.grad_sync = self.sync
         if self.mode == "eager":
             for _ in range(n_steps):
                 tr.train_step()

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Rehearse the xGMI peer-memory all-reduce with W ranks on the GPUs this box has.
+
+    torchrun --nproc-per-node 2 tools/xgmi_check.py [--backend gloo]
+
+On a 1-GPU box the ranks share GPU 0 (gloo for the reference collectives), which still
+exercises the whole protocol -- IPC export/import, counters, parity buffers, bounded
+waits, fused SGD, graph capture -- everything except the cross-GPU fabric itself.
+Prints one JSON line per rank; exit 0 iff every check passed on every rank.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--steps", type=int, default=8)
+    a = ap.parse_args(argv)
+    import torch
+    import torch.distributed as dist
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer, flat_layout
+    from pytorch_operator_amd.ops import mnist as K
+    from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
+    from pytorch_operator_amd.parallel.dist import init_from_env
+    from pytorch_operator_amd.parallel.graphed_step import GraphedStep
+    from pytorch_operator_amd.parallel.xgmi import XgmiAllReduce, XgmiGradSync
+
+    env = init_from_env(a.backend, use_gpu=True)
+    rank, world, dev = env.rank, env.world_size, env.device
+    res = {"rank": rank, "world": world}
+    L = flat_layout().total
+    xar = XgmiAllReduce(L, device=dev)
+    res["alloc_kind"] = xar.alloc_kind
+    res["self_test"] = xar.self_test()
+    res["self_test_report"] = xar.last_report[:4]
+
+    ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
+
+    def trainer(sync):
+        cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
+        tr = FusedMnistTrainer(batch_size=64, source=src, lr=0.01, momentum=0.5, device=dev, seed=1,
+                               grad_sync=sync)
+        dist.broadcast(tr.flat_params, 0)
+        return tr
+
+    ta = trainer(XgmiGradSync(xar))
+    tb = trainer(FlatGradAllReduce())
+    for _ in range(a.steps):
+        ta.train_step()
+        tb.train_step()
+    torch.cuda.synchronize(dev)
+    res["max_diff_vs_rccl_path"] = float((ta.flat_params - tb.flat_params).abs().max())
+    res["eager_match"] = res["max_diff_vs_rccl_path"] < 1e-4
+
+    runner = GraphedStep(ta, mode="graph", steps_per_graph=4)
+    runner.run(8)
+    torch.cuda.synchronize(dev)
+    ref = ta.flat_params.clone()
+    dist.broadcast(ref, 0)
+    res["graph_in_sync"] = bool(torch.equal(ref, ta.flat_params))
+    res["finite"] = bool(torch.isfinite(ta.flat_params).all())
+    # autotune hand-over in both directions keeps the replicas identical
+    from pytorch_operator_amd.parallel.autotune import choose_grad_sync
+    for force in ("rccl", "xgmi"):
+        runner, path, times = choose_grad_sync(ta, FlatGradAllReduce(), XgmiGradSync(xar), spg=4,
+                                               trial_steps=8, force=force)
+        runner.run(8)
+        torch.cuda.synchronize(dev)
+        ref = ta.flat_params.clone()
+        dist.broadcast(ref, 0)
+        mref = ta.flat_momentum.clone()
+        dist.broadcast(mref, 0)
+        res[f"handover_{force}_in_sync"] = bool(torch.equal(ref, ta.flat_params)) and (
+            force == "xgmi" or bool(torch.equal(mref, ta.flat_momentum)))
+        res[f"handover_{force}_times"] = times
+    res["kernel_error"] = xar.error()
+    ok = res["self_test"] and res["eager_match"] and res["graph_in_sync"] and res["finite"] \
+        and res["kernel_error"] == 0 and res["handover_rccl_in_sync"] and res["handover_xgmi_in_sync"]
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    res["all_ok"] = bool(flag.item())
+    print(json.dumps(res), flush=True)
+    dist.barrier()
+    xar.close()
+    dist.destroy_process_group()
+    return 0 if res["all_ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
