@@ -188,15 +188,18 @@ def test_ttl_seconds_after_finished_deletes_job(cluster):
     c = cluster
     c.rest.create(PYTORCHJOBS, make_job("e2e-ttl", replica(1, "busybox", command=py("pass")),
                                         ttlSecondsAfterFinished=1), NS)
-    wait_finished(c, "e2e-ttl")
+    seen = set()
 
     def gone():
         try:
-            c.rest.get(PYTORCHJOBS, "e2e-ttl", NS)
+            seen.update(conditions(c, "e2e-ttl")[0])
             return False
         except ApiException as e:
             return e.status == 404
-    wait_until(gone, 30, what="TTL deletion")
+    wait_until(gone, 60, interval=0.05, what="TTL deletion")
+    # the job can finish and expire between two polls; it is only ever deleted once finished
+    assert "Failed" not in seen
+    assert c.metric_value("pytorch_operator_jobs_successful_total") >= 1
 
 
 def test_unschedulable_gpu_request_stays_pending(cluster):
