@@ -89,7 +89,7 @@ def main(argv=None):
     p.add_argument("--json-out", default=None)
     a = p.parse_args(argv)
     gpu = bool(a.gpus)
-    args = ["--backend", a.backend, "--dataset-size", str(a.dataset_size), "--no-shard"]
+    args = ["--backend", a.backend, "--dataset-size", str(a.dataset_size)]
     if not gpu:
         args.append("--no-cuda")
     if a.max_steps:

@@ -15,13 +15,14 @@ MI355X-native differences:
 
 * ``--backend rccl`` (alias of nccl: RCCL over xGMI); ``mpi`` fails clearly;
 * on a GPU the step runs the fused gfx950 kernels (``--kernels hip``, default) on an
-  HBM-resident uint8 dataset, replayed as hipGraphs; DDP is two flat-bucket RCCL
-  all-reduces overlapped with the conv backward.  ``--kernels torch`` is the plain
+  HBM-resident uint8 dataset, replayed as hipGraphs; DDP gradients go through the
+  xGMI peer-memory all-reduce fused with SGD when its start-up self-test passes
+  (``parallel/xgmi.py``), else two flat-bucket RCCL all-reduces.  ``--kernels torch`` is the plain
   PyTorch path (also used on CPU with gloo);
 * data: real MNIST IDX files from ``--data-dir`` if present, else the synthetic set
-  (no network);  ``--shard`` (default) gives each rank a disjoint slice like a
-  ``DistributedSampler``; ``--no-shard`` reproduces the reference, where every rank
-  iterates the full dataset;
+  (no network); by default every rank iterates the full dataset like the reference
+  (quirk Q8: no DistributedSampler); ``--shard`` gives each rank a disjoint slice like a
+  ``DistributedSampler``;
 * one machine-readable JSON line per milestone (``first_step``, ``train_done``) so the
   operator benchmarks can measure create-to-first-step latency and throughput.
 """
@@ -54,10 +55,15 @@ def parse_args(argv=None):
     p.add_argument("--synthetic", action="store_true", help="force the synthetic dataset")
     p.add_argument("--dataset-size", type=int, default=60000, help="synthetic train set size")
     p.add_argument("--test-size", type=int, default=10000, help="synthetic test set size")
-    p.add_argument("--shard", dest="shard", action="store_true", default=True)
+    # reference semantics (quirk Q8): no DistributedSampler, every rank walks the full set
+    p.add_argument("--shard", dest="shard", action="store_true", default=False,
+                   help="give each rank a disjoint 1/W slice (DistributedSampler semantics)")
     p.add_argument("--no-shard", dest="shard", action="store_false")
     p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
     p.add_argument("--no-graph", action="store_true", help="HIP path: eager launches, no hipGraphs")
+    p.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"], default="auto",
+                   help="HIP path, world>1: xGMI peer-memory all-reduce fused with SGD (self-tested, "
+                        "RCCL fallback) or RCCL bucket all-reduce")
     p.add_argument("--model-path", default="mnist_cnn.pt")
     p.add_argument("--metrics-file", default=None, help="append the JSON milestone lines here too")
     return p.parse_args(argv)
@@ -173,7 +179,14 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
     perm = _epoch_perm(n, args.seed, 1, rank, args.shard, dev)
     cursor = torch.zeros(1, dtype=torch.int32, device=dev)
     src = K.BatchSource(xtr, ytr, perm=perm, cursor=cursor)
-    sync = FlatGradAllReduce() if world > 1 else None
+    sync = None
+    if world > 1:
+        from ..models.mnist import flat_layout
+        from ..parallel.xgmi import try_xgmi
+        sync = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi") \
+            if args.allreduce != "rccl" else None
+        sync = sync or FlatGradAllReduce()
+        emit("grad_allreduce", path="xgmi" if getattr(sync, "fused_sgd", False) else "rccl")
     tr = FusedMnistTrainer(batch_size=B, source=src, lr=args.lr, momentum=args.momentum,
                            device=dev, seed=args.seed, grad_sync=sync)
     if world > 1:
@@ -198,7 +211,8 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
             # capturing runs warm-up steps: snapshot the state, capture, restore, so the
             # trajectory is exactly the eager one (a log block = one graph replay)
             saved = (tr.flat_params.clone(), tr.flat_momentum.clone())
-            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if world == 1 else 1)
+            whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
+            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1)
             tr.flat_params.copy_(saved[0])
             tr.flat_momentum.copy_(saved[1])
             cursor.fill_(1)

@@ -136,9 +136,9 @@ def test_mnist_gloo_ddp_job(cluster):
     log = c.rest.pod_log("e2e-mnist-master-0", NS)
     assert types[-1] == "Succeeded", log[-2000:]
     assert "Using distributed PyTorch with gloo backend" in log
-    assert "Train Epoch: 1 [0/1000 (0%)]" in log and "accuracy=" in log
+    assert "Train Epoch: 1 [0/2000 (0%)]" in log and "accuracy=" in log
     done = [json.loads(x) for x in log.splitlines() if x.startswith('{"event": "train_done"')]
-    assert done and done[0]["steps"] == 16
+    assert done and done[0]["steps"] == 20  # full 2000-sample set per rank, capped by --max-steps
 
 
 def test_exit_code_policy_restarts_retryable_failure(cluster, tmp_path):

@@ -114,7 +114,7 @@ def test_mnist_worker_learns_on_real_idx_files(tmp_path):
 
 def test_mnist_worker_ddp_gloo_two_ranks(tmp_path):
     outs = _launch("pytorch_operator_amd.harness.mnist",
-                   ["--backend", "gloo", "--dataset-size", "1280", "--test-size", "256", "--dir",
+                   ["--backend", "gloo", "--dataset-size", "1280", "--test-size", "256", "--shard", "--dir",
                     str(tmp_path / "tb")], 2, tmp_path)
     for rc, out in outs:
         assert rc == 0, out
@@ -125,9 +125,9 @@ def test_mnist_worker_ddp_gloo_two_ranks(tmp_path):
     assert ev0[-1]["test_loss"] == ev1[-1]["test_loss"]
 
 
-def test_mnist_worker_no_shard_matches_reference_semantics(tmp_path):
+def test_mnist_worker_default_matches_reference_semantics(tmp_path):
     outs = _launch("pytorch_operator_amd.harness.mnist",
-                   ["--backend", "gloo", "--dataset-size", "640", "--test-size", "128", "--no-shard",
+                   ["--backend", "gloo", "--dataset-size", "640", "--test-size", "128",
                     "--dir", str(tmp_path / "tb")], 2, tmp_path)
     for rc, out in outs:
         assert rc == 0, out
