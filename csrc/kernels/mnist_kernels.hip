@@ -728,9 +728,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 //   phase 2a  dcol[64 pos, 125 (ci,kh,kw)] = dz2[b]^T . W2[:, group]   (MFMA, K = 50)
 //   phase 2b  dW_conv2[50, group] partial = dz2[b] . im2col(a1[b])      (MFMA, K = 64)
 //   phase 3   da1 = col2im(dcol); un-pool via idx1 + ReLU mask -> dz1 (LDS)
-//   phase 4   dW_conv1[group, 25] partial = dz1 . im2col(xn[b])         (MFMA, K = 576)
-//   The partial conv grads are added with fp32 atomics at the very end (so no
-//   barrier waits for them) into a segment that launch A zeroed.
+//   phase 4   dW_conv1[group, 25] + db_conv1 partials = dz1 . im2col(xn[b]) (VALU)
+//   The block's partial conv grads go to its sample's slab row (slab_stride > 0,
+//   reduced deterministically later) or are added with fp32 atomics.
 // ---------------------------------------------------------------------------
 // LDS row strides (ds_read_b32/ds_write_b32 banks = word % 32, 32-lane groups):
 constexpr int F_DS = 66;    // dz_s   [64 co][66]    A of 2b: lanes = co rows  (== 2 mod 32)
@@ -750,7 +750,8 @@ constexpr int F_LDS = F_OFF_IDX + 180;
 // aliases of the (dead after phase 2a) weight region:
 constexpr int F_OFF_DZ1 = F_OFF_W;
 constexpr int F_OFF_RED = F_OFF_W + 5 * F_Z1;
-static_assert(5 * F_Z1 + 8 * 256 <= 52 * F_WS, "alias region too small");
+constexpr int F_RED1 = 132;  // phase-4 partial row: 125 dW_conv1 taps + 5 bias sums
+static_assert(5 * F_Z1 + 16 * F_RED1 <= 52 * F_WS, "alias region too small");
 
 __global__ __launch_bounds__(512) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
@@ -915,37 +916,44 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
   __syncthreads();
   stamp(dbg, 3);
 
-  // ---- phase 4: dW_conv1 partial (M = 16 (5 valid ch), N = 32 (25 taps), K = 576)
-  {
-    const int nt = wv & 1, kq = wv >> 1;
-    const int t = nt * 16 + i;
-    const bool tv = t < 25;
-    const int tc = tv ? t : 24;
-    const int xoff = (tc / 5) * 28 + (tc % 5);
-    const bool cv = i < 5;
-    const float* arow = dz1_s + (cv ? i : 4) * F_Z1;
-    f32x4 c0 = zero4(), c1 = zero4();
+  // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU.  As an MFMA GEMM this is
+  // M = 5 channels padded to 16 (3/4 of every MFMA wasted, ~3 us); here 400 threads =
+  // (channel c, kernel row kh, 8 row-groups x 2 column-halves) each slide a 16-wide
+  // register window of the input row across 12 output columns: 5 FMAs per 2 LDS reads.
+  // The kh == 0 threads also sum dz1 for the bias gradient.  16 partials meet in LDS.
+  if (tid < 400) {
+    const int c = tid / 80, rem = tid - c * 80;
+    const int kh = rem >> 4, part = rem & 15;
+    const int ry = part >> 1, cx = (part & 1) * 12;
+    const float* zr = dz1_s + c * F_Z1;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float bs = 0.f;
 #pragma unroll
-    for (int yy = 0; yy < 6; ++yy) {
-      const int y = kq * 6 + yy;
+    for (int yy = 0; yy < 3; ++yy) {
+      const int y = ry * 3 + yy;
+      const float* xr = x_s + (y + kh) * 28 + cx;
+      float xw[16];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int x = 4 * q + g;
-        const float av = cv ? arow[y * 24 + x] : 0.f;
-        const float bv = tv ? x_s[y * 28 + x + xoff] : 0.f;
-        if (q & 1) c1 = mfma16x16x4(av, bv, c1);
-        else c0 = mfma16x16x4(av, bv, c0);
+      for (int q = 0; q < 16; ++q) xw[q] = xr[q];
+#pragma unroll
+      for (int x = 0; x < 12; ++x) {
+        const float a = zr[y * 24 + cx + x];
+        bs += a;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
       }
     }
-    reinterpret_cast<f32x4*>(red)[wv * 64 + lane] = c0 + c1;
-  }
-  float b1sum = 0.f;
-  if (tid >= 128 && tid < 128 + 5 * 64) {
-    const int c = (tid - 128) >> 6;
-    for (int p = lane; p < 576; p += 64) b1sum += dz1_s[c * F_Z1 + p];
-    b1sum = wave_sum(b1sum);
+    float* pr = red + part * F_RED1;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
+    if (kh == 0) pr[125 + c] = bs;
   }
   __syncthreads();
+  float w1sum = 0.f;
+  if (tid < 130) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w1sum += red[q * F_RED1 + tid];
+  }
   stamp(dbg, 4);
 
   // ---- epilogue.  slab_stride > 0: plain stores of this block's partial grads into
@@ -972,26 +980,14 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
     if (slab) gb2[so + tid] = b2sum;
     else atomicAdd(&gb2[tid], b2sum);
   }
-  if (tid < 128) {
-    // lane l of ntile nt, reg r: channel row = (l>>4)*4 + r, tap col = nt*16 + (l&15)
-    const int nt = tid >> 6, l = tid & 63;
-    const f32x4* rv4 = reinterpret_cast<const f32x4*>(red);
-    const f32x4 s = rv4[(0 * 2 + nt) * 64 + l] + rv4[(1 * 2 + nt) * 64 + l] +
-                    rv4[(2 * 2 + nt) * 64 + l] + rv4[(3 * 2 + nt) * 64 + l];
-    const int tt = nt * 16 + (l & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = (l >> 4) * 4 + r;
-      if (c < 5 && tt < 25) {
-        float* dst = gw1 + so + (cig * 5 + c) * 25 + tt;
-        if (slab) *dst = s[r];
-        else atomicAdd(dst, s[r]);
-      }
-    }
-  } else if (tid < 128 + 5 * 64 && lane == 0) {
-    float* dst = gb1 + so + cig * 5 + ((tid - 128) >> 6);
-    if (slab) *dst = b1sum;
-    else atomicAdd(dst, b1sum);
+  if (tid < 125) {  // tid = c * 25 + kh * 5 + kw
+    float* dst = gw1 + so + cig * 125 + tid;
+    if (slab) *dst = w1sum;
+    else atomicAdd(dst, w1sum);
+  } else if (tid < 130) {
+    float* dst = gb1 + so + cig * 5 + (tid - 125);
+    if (slab) *dst = w1sum;
+    else atomicAdd(dst, w1sum);
   }
   stamp(dbg, 5);
 }
