@@ -48,6 +48,11 @@ struct XarArgs {
   float lr, momentum, dampening, wd, scale;
   int nesterov, first_step;
   int* step_counter;     // optional: advanced once per launch (the trainer's batch cursor)
+  // optional fused slab reduction: the first conv4 float4s of the published gradient are
+  // sum_{r < slab_rows} slab[r * slab_stride + .] (the conv backward's per-sample partials)
+  const float* slab;
+  int slab_rows;
+  long slab_stride, conv4;
   int* err;
   long long timeout_ticks;  // wall_clock64 ticks (100 MHz)
 };
@@ -112,12 +117,40 @@ __global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) {
   const long long deadline = (long long)wall_clock64() + a.timeout_ticks;
   const long n4 = a.n >> 2;  // n is a multiple of 4 (host-checked)
 
-  // ---- phase 1: publish my gradients (padding published as zeros)
+  // ---- phase 1: publish my gradients (padding published as zeros).  With a slab, the
+  // conv segment is reduced here over the per-sample rows (fixed row order), spread over
+  // all blocks; the rest is copied from `in`.
   {
-    const long per = a.npad / a.nblk;  // multiple of 4
-    const long lo4 = (long)b * (per >> 2), hi4 = lo4 + (per >> 2);
     float4* dst = reinterpret_cast<float4*>(data_buf(mine, a.npad, par));
     const float4* src = reinterpret_cast<const float4*>(a.in);
+    const long c4 = a.slab != nullptr ? a.conv4 : 0;
+    if (c4 > 0) {
+      __shared__ float4 part[kThreads];
+      const long per_c = (c4 + a.nblk - 1) / a.nblk;  // <= kThreads / 2 (host-checked)
+      const long col = (long)b * per_c + (tid % per_c);
+      const int half = tid / (int)per_c;              // 0 / 1: rows [0, R/2) / [R/2, R)
+      const int rh = (a.slab_rows + 1) / 2;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (half < 2 && col < c4 && (long)tid < 2 * per_c) {
+        const float4* sp = reinterpret_cast<const float4*>(a.slab) + col;
+        const long s4 = a.slab_stride >> 2;
+        const int r0 = half * rh, r1 = min(a.slab_rows, r0 + rh);
+#pragma unroll 8
+        for (int r = r0; r < r1; ++r) {
+          const float4 x = sp[(long)r * s4];
+          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+        }
+      }
+      part[tid] = acc;
+      __syncthreads();
+      if ((long)tid < per_c && col < c4) {
+        const float4 o = part[tid + per_c];
+        dst[col] = make_float4(acc.x + o.x, acc.y + o.y, acc.z + o.z, acc.w + o.w);
+      }
+    }
+    const long rest = a.npad / 4 - c4;
+    const long per = (rest + a.nblk - 1) / a.nblk;
+    const long lo4 = c4 + (long)b * per, hi4 = min(lo4 + per, a.npad / 4);
     for (long v = lo4 + tid; v < hi4; v += kThreads)
       dst[v] = v < n4 ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
     __threadfence_system();
@@ -130,8 +163,9 @@ __global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) {
     if (tid == 0) {
       const unsigned long long target = (unsigned long long)a.nblk * s;
       int ok = s_ok;
-      for (int q = 0; q < a.world && ok; ++q)
-        if (q != a.rank) ok = wait_ge(pub_ctr(a.base[q]), target, deadline, a.err);
+      // every rank's publish, this one's included: the chunk this block reduces was
+      // published by whichever local block owned it in phase 1
+      for (int q = 0; q < a.world && ok; ++q) ok = wait_ge(pub_ctr(a.base[q]), target, deadline, a.err);
       s_ok = ok;
     }
     __syncthreads();
@@ -144,13 +178,11 @@ __global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       if (ok) {
         for (int q = 0; q < a.world; ++q) {  // fixed rank order: deterministic sums
-          const float4 x = q == a.rank ? (v < n4 ? reinterpret_cast<const float4*>(a.in)[v]
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f))
-                                       : reinterpret_cast<const float4*>(data_buf(a.base[q], a.npad, par))[v];
+          const float4 x = reinterpret_cast<const float4*>(data_buf(a.base[q], a.npad, par))[v];
           acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
         }
-      } else if (v < n4) {
-        acc = reinterpret_cast<const float4*>(a.in)[v];  // degraded: local gradient only
+      } else {
+        acc = reinterpret_cast<const float4*>(data_buf(mine, a.npad, par))[v];  // degraded: local only
       }
       float4 res;
       if (a.mode == 0) {
@@ -313,7 +345,8 @@ int pto_xar_allreduce(void* ctx, const float* in, float* out, float scale, void*
 // p, mbuf <- SGD(p, mean over ranks of grads) -- each rank updates its shard, then all gather.
 int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
                           float dampening, float wd, float scale, int nesterov, int first_step,
-                          int* step_counter, void* stream) {
+                          int* step_counter, const float* slab, int slab_rows, long slab_stride,
+                          long conv_n, void* stream) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
   XarArgs a{};
   a.mode = 1;
@@ -328,6 +361,16 @@ int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, 
   a.nesterov = nesterov;
   a.first_step = first_step;
   a.step_counter = step_counter;
+  if (slab != nullptr) {
+    if (slab_rows <= 0 || (conv_n & 3) || (slab_stride & 3) || slab_stride < conv_n || conv_n > c->n ||
+        ((uintptr_t)slab & 15))
+      return -1;
+    a.slab = slab;
+    a.slab_rows = slab_rows;
+    a.slab_stride = slab_stride;
+    a.conv4 = conv_n >> 2;
+    if ((a.conv4 + c->nblk - 1) / c->nblk > kThreads / 2) return -1;  // one column pair per thread
+  }
   return launch(c, a, stream);
 }
 

@@ -262,14 +262,18 @@ class FusedMnistTrainer:
         """One full training step (forward, backward, [all-reduce], SGD)."""
         overlap = self.overlap if overlap is None else overlap
         if getattr(self.grad_sync, "fused_sgd", False):
-            # xGMI path: one kernel does the cross-GPU reduce-scatter, SGD on this rank's
-            # shard and the all-gather of updated parameters (parallel/xgmi.py)
-            self.forward_backward(source, B)
+            # xGMI path: one kernel reduces the per-sample conv-grad slabs, does the
+            # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
+            # updated parameters (parallel/xgmi.py).  flat_grads[:conv_end] is not written.
+            B_ = self.B if B is None else B
+            self.forward_backward_fc(source, B_)
+            self._conv_bwd(B_)
             self.grad_sync.xar.allreduce_sgd_(
                 self.flat_grads, self.flat_params, self.flat_momentum, lr=self.lr,
                 momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
                 nesterov=self.nesterov, first_step=self._first_step,
-                step_counter=self.cursor if advance_cursor else None)
+                step_counter=self.cursor if advance_cursor else None,
+                slab=self.conv_slab, slab_rows=B_, conv_n=self.layout.conv_end)
             self._first_step = False
             return
         if self.grad_sync is not None:

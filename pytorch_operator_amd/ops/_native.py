@@ -108,7 +108,7 @@ _SIGNATURES = {
     "pto_xar_error": [_VP],
     "pto_xar_alloc_kind": [_VP],
     "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],
-    "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
+    "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _I, _L, _L, _VP],
     "pto_xar_destroy": [_VP],
 }
 _LONG_FNS = {"pto_xar_npad": [_VP]}

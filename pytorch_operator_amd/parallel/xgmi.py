@@ -81,14 +81,25 @@ class XgmiAllReduce:
     def allreduce_sgd_(self, grads: torch.Tensor, params: torch.Tensor, momentum_buf: torch.Tensor, *,
                        lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
                        nesterov: bool = False, first_step: bool = False,
-                       step_counter: Optional[torch.Tensor] = None) -> None:
+                       step_counter: Optional[torch.Tensor] = None,
+                       slab: Optional[torch.Tensor] = None, slab_rows: int = 0, conv_n: int = 0) -> None:
+        """SGD with the mean gradient over ranks.  With ``slab`` ([rows, stride] fp32), the
+        first ``conv_n`` gradient entries are the sum of its first ``slab_rows`` rows
+        (fused deterministic reduction of the per-sample conv partials); ``grads`` then
+        only needs to hold the entries after ``conv_n``."""
         for t in (grads, params, momentum_buf):
             self._check(t)
         sc = step_counter.data_ptr() if step_counter is not None else None
+        sp, stride = None, 0
+        if slab is not None:
+            if not (slab.is_cuda and slab.dtype == torch.float32 and slab.is_contiguous() and slab.dim() == 2
+                    and slab_rows <= slab.shape[0] and conv_n <= slab.shape[1]):
+                raise ValueError("slab must be a contiguous fp32 CUDA [rows, stride] tensor")
+            sp, stride = slab.data_ptr(), slab.shape[1]
         _native.check(self.lib.pto_xar_allreduce_sgd(
             self._ctx, grads.data_ptr(), params.data_ptr(), momentum_buf.data_ptr(), lr, momentum,
             dampening, weight_decay, 1.0 / self.world, int(nesterov), int(first_step), sc,
-            self._stream()), "pto_xar_allreduce_sgd")
+            sp, int(slab_rows), int(stride), int(conv_n), self._stream()), "pto_xar_allreduce_sgd")
 
     def gather_sharded_(self, t: torch.Tensor) -> None:
         """Reassemble a tensor each rank only kept for its own shard (e.g. the momentum
@@ -111,7 +122,7 @@ class XgmiAllReduce:
             raise ValueError("tensor must be 16-byte aligned")
 
     # ------------------------------------------------------------------ validation
-    def self_test(self, steps: int = 6, seed: int = 1234) -> bool:
+    def self_test(self, steps: int = 12, seed: int = 1234) -> bool:
         """Kernel vs ``dist.all_reduce`` on random data (mean and fused SGD); all ranks agree."""
         ok = True
         report = []
