@@ -65,6 +65,11 @@ def parse_args(argv=None):
                    help="HIP path, world>1: xGMI peer-memory all-reduce fused with SGD (self-tested, "
                         "RCCL fallback) or RCCL bucket all-reduce")
     p.add_argument("--model-path", default="mnist_cnn.pt")
+    p.add_argument("--checkpoint-dir", default=None,
+                   help="write an end-of-epoch checkpoint (weights + optimizer state) here")
+    p.add_argument("--resume", action="store_true",
+                   help="continue from --checkpoint-dir if a checkpoint exists (e.g. after an ExitCode restart)")
+    p.add_argument("--trace", action="store_true", help="roctx ranges around epochs, step blocks and eval")
     p.add_argument("--metrics-file", default=None, help="append the JSON milestone lines here too")
     return p.parse_args(argv)
 
@@ -154,6 +159,77 @@ def run(args) -> dict:
     return result
 
 
+class _Trace:
+    """roctx ranges (torch.cuda.nvtx maps to roctx on ROCm builds) when --trace is given."""
+
+    def __init__(self, on: bool):
+        self.on = False
+        if on:
+            try:
+                import torch.cuda.nvtx as nvtx
+                nvtx.range_push("probe")
+                nvtx.range_pop()
+                self.nvtx, self.on = nvtx, True
+            except Exception:  # noqa: BLE001 -- tracing is best effort
+                self.on = False
+
+    def __call__(self, name):
+        import contextlib
+        if not self.on:
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def rng():
+            self.nvtx.range_push(name)
+            try:
+                yield
+            finally:
+                self.nvtx.range_pop()
+        return rng()
+
+
+def _ckpt_path(args):
+    return os.path.join(args.checkpoint_dir, "ckpt.pt") if args.checkpoint_dir else None
+
+
+def _save_ckpt(args, rank, state: dict) -> None:
+    """Rank 0 writes atomically (tmp + rename) so a crash never leaves a torn file."""
+    import torch
+    path = _ckpt_path(args)
+    if not path or rank != 0:
+        return
+    os.makedirs(args.checkpoint_dir, exist_ok=True)
+    tmp = path + f".tmp{os.getpid()}"
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+
+
+def _maybe_fault(epoch: int, resumed: bool) -> None:
+    """Fault-injection hook for recovery tests: PTO_FAULT_EXIT_AFTER_EPOCH=N makes a
+    fresh (non-resumed) run exit with 137 -- a retryable SIGKILL code -- right after it
+    checkpointed epoch N."""
+    n = os.environ.get("PTO_FAULT_EXIT_AFTER_EPOCH")
+    if n and not resumed and epoch == int(n):
+        print(f"fault injection: exiting with 137 after epoch {epoch}", flush=True)
+        os._exit(137)
+
+
+def _load_ckpt(args):
+    import torch
+    path = _ckpt_path(args)
+    if not (args.resume and path and os.path.exists(path)):
+        return None
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def _percentiles(samples_ms):
+    if not samples_ms:
+        return None
+    xs = sorted(samples_ms)
+    pick = lambda q: round(xs[min(len(xs) - 1, int(q * (len(xs) - 1) + 0.5))], 5)  # noqa: E731
+    return {"p50": pick(0.5), "p90": pick(0.9), "p99": pick(0.99), "n": len(xs)}
+
+
 def _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss, writer):
     print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
         epoch, batch_idx * B, n, 100.0 * batch_idx / steps_per_epoch, loss), flush=True)
@@ -189,13 +265,33 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         emit("grad_allreduce", path="xgmi" if getattr(sync, "fused_sgd", False) else "rccl")
     tr = FusedMnistTrainer(batch_size=B, source=src, lr=args.lr, momentum=args.momentum,
                            device=dev, seed=args.seed, grad_sync=sync)
+    trace = _Trace(args.trace)
+    start_epoch = 1
+    ck = _load_ckpt(args) if rank == 0 else None
+    if world > 1:
+        flag = [ck["epoch"] if ck is not None else 0]
+        dist.broadcast_object_list(flag, 0)
+        resumed_epoch = flag[0]
+    else:
+        resumed_epoch = ck["epoch"] if ck is not None else 0
+    if ck is not None:
+        tr.load_state_dict({k: v.to(dev) for k, v in ck["params"].items()})
+        tr.flat_momentum.copy_(ck["momentum"].to(dev))
+    if resumed_epoch:
+        if world > 1:
+            dist.broadcast(tr.flat_momentum, 0)
+        tr._first_step = False
+        start_epoch = resumed_epoch + 1
+        emit("resumed", epoch=resumed_epoch)
     if world > 1:
         dist.broadcast(tr.flat_params, 0)  # DDP constructor semantics
     log_iv = max(1, args.log_interval)
     runner = None
     t_train = 0.0
     steps_done = 0
-    for epoch in range(1, args.epochs + 1):
+    step_ms = []
+    loss = acc = float("nan")
+    for epoch in range(start_epoch, args.epochs + 1):
         if epoch > 1:
             perm.copy_(_epoch_perm(n, args.seed, epoch, rank, args.shard, dev))
         cursor.zero_()
@@ -203,7 +299,7 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         t0 = time.perf_counter()
         # batch 0: eager (initialises momentum on the first epoch), logged
         tr.train_step()
-        if epoch == 1 and steps_done == 0:
+        if steps_done == 0:
             torch.cuda.synchronize(dev)
             emit("first_step")
         _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer)
@@ -218,25 +314,41 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
             cursor.fill_(1)
         # blocks of log_iv steps ending on a logged batch (batches 1..L, L+1..2L, ...)
         b = 1
-        while b < steps_per_epoch:
-            chunk = min(log_iv, steps_per_epoch - b)
-            if runner is not None and chunk % runner.steps_per_graph == 0:
-                runner.run(chunk)
-            else:
-                for _ in range(chunk):
-                    tr.train_step()
-            b += chunk
-            if (b - 1) % log_iv == 0:
-                _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer)
+        events = []
+        with trace(f"epoch{epoch}"):
+            while b < steps_per_epoch:
+                chunk = min(log_iv, steps_per_epoch - b)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                with trace("steps"):
+                    if runner is not None and chunk % runner.steps_per_graph == 0:
+                        runner.run(chunk)
+                    else:
+                        for _ in range(chunk):
+                            tr.train_step()
+                e1.record()
+                events.append((e0, e1, chunk))
+                b += chunk
+                if (b - 1) % log_iv == 0:
+                    _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer)
         torch.cuda.synchronize(dev)
         t_train += time.perf_counter() - t0
+        step_ms += [e0.elapsed_time(e1) / c for e0, e1, c in events]
         steps_done += steps_per_epoch
-        loss, acc = _evaluate_hip(tr, K, xte, yte, args.test_batch_size)
+        with trace("eval"):
+            loss, acc = _evaluate_hip(tr, K, xte, yte, args.test_batch_size)
         _log_test(acc, epoch, writer)
+        if args.checkpoint_dir:
+            if getattr(sync, "fused_sgd", False):
+                sync.xar.gather_sharded_(tr.flat_momentum)  # xGMI keeps only this rank's shard
+            _save_ckpt(args, rank, {"epoch": epoch, "momentum": tr.flat_momentum.detach().cpu().clone(),
+                                    "params": {k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}})
+        _maybe_fault(epoch, resumed_epoch > 0)
     if args.save_model and rank == 0:
         torch.save({k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}, args.model_path)
     return {"steps": steps_done, "train_seconds": round(t_train, 4),
             "samples_per_sec": round(steps_done * B * world / t_train, 1) if t_train else None,
+            "step_ms": _percentiles(step_ms),
             "test_loss": round(loss, 5), "accuracy": round(acc, 5)}
 
 
@@ -258,12 +370,21 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -
         kw = {"device_ids": [dev.index]} if dev.type == "cuda" else {}
         model = torch.nn.parallel.DistributedDataParallel(model, **kw)
     opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum)
+    core = model.module if hasattr(model, "module") else model
+    start_epoch = 1
+    ck = _load_ckpt(args)
+    if ck is not None:  # every rank loads (CPU jobs share the checkpoint directory)
+        core.load_state_dict(ck["model"])
+        opt.load_state_dict(ck["optim"])
+        start_epoch = ck["epoch"] + 1
+        emit("resumed", epoch=ck["epoch"])
 
     def norm(x):
         return ((x.float() / 255.0 - 0.1307) / 0.3081).view(-1, 1, 28, 28)
 
     t_train, steps_done = 0.0, 0
-    for epoch in range(1, args.epochs + 1):
+    test_loss = acc = float("nan")
+    for epoch in range(start_epoch, args.epochs + 1):
         model.train()
         perm = _epoch_perm(n, args.seed, epoch, rank, args.shard, dev).long()
         t0 = time.perf_counter()
@@ -274,7 +395,7 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -
             loss = F.nll_loss(model(data), target)
             loss.backward()
             opt.step()
-            if epoch == 1 and batch_idx == 0:
+            if steps_done == 0 and batch_idx == 0:
                 emit("first_step")
             if batch_idx % args.log_interval == 0:
                 _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss.item(), writer)
@@ -293,9 +414,10 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -
         acc = correct / xte.shape[0]
         test_loss /= xte.shape[0]
         _log_test(acc, epoch, writer)
+        _save_ckpt(args, rank, {"epoch": epoch, "model": core.state_dict(), "optim": opt.state_dict()})
+        _maybe_fault(epoch, start_epoch > 1)
     if args.save_model and rank == 0:
-        m = model.module if hasattr(model, "module") else model
-        torch.save(m.state_dict(), args.model_path)
+        torch.save(core.state_dict(), args.model_path)
     return {"steps": steps_done, "train_seconds": round(t_train, 4),
             "samples_per_sec": round(steps_done * B * world / t_train, 1) if t_train else None,
             "test_loss": round(test_loss, 5), "accuracy": round(acc, 5)}

@@ -153,3 +153,34 @@ def test_dist_sendrecv_three_ranks(tmp_path):
     assert "Result from worker 1" in master and "Result from worker 2" in master
     assert "all_reduce ok (6.0)" in master
     assert "MASTER_ADDR: 127.0.0.1" in master and "WORLD_SIZE: 3" in master
+
+
+def test_checkpoint_resume_continues_at_next_epoch(tmp_path):
+    ck = tmp_path / "ck"
+    common = ["--dataset-size", "640", "--test-size", "128", "--checkpoint-dir", str(ck), "--dir", str(tmp_path / "tb")]
+    (rc, out), = _launch("pytorch_operator_amd.harness.mnist", ["--epochs", "1", *common], 1, tmp_path)
+    assert rc == 0, out
+    assert (ck / "ckpt.pt").exists()
+    (rc, out), = _launch("pytorch_operator_amd.harness.mnist", ["--epochs", "2", "--resume", *common], 1, tmp_path)
+    assert rc == 0, out
+    ev = _events(out)
+    assert any(e["event"] == "resumed" and e["epoch"] == 1 for e in ev)
+    assert "Train Epoch: 2 [0/640" in out and "Train Epoch: 1 " not in out
+    assert ev[-1]["steps"] == 10  # only epoch 2 ran
+    sd = torch.load(ck / "ckpt.pt", weights_only=True)
+    assert sd["epoch"] == 2 and "optim" in sd
+
+
+def test_fault_injection_hook_exits_137_after_checkpoint(tmp_path):
+    ck = tmp_path / "ck"
+    env_args = ["--dataset-size", "640", "--test-size", "128", "--epochs", "2", "--checkpoint-dir", str(ck),
+                "--resume", "--dir", str(tmp_path / "tb")]
+    os.environ["PTO_FAULT_EXIT_AFTER_EPOCH"] = "1"
+    try:
+        (rc, out), = _launch("pytorch_operator_amd.harness.mnist", env_args, 1, tmp_path)
+        assert rc == 137 and (ck / "ckpt.pt").exists()
+        (rc, out), = _launch("pytorch_operator_amd.harness.mnist", env_args, 1, tmp_path)
+        assert rc == 0, out  # resumed runs are never faulted
+        assert any(e["event"] == "resumed" for e in _events(out))
+    finally:
+        del os.environ["PTO_FAULT_EXIT_AFTER_EPOCH"]
