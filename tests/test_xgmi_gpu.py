@@ -23,13 +23,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_xgmi_allreduce_two_ranks():
+def test_xgmi_allreduce_two_ranks(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
-           "--backend", "gloo"]
+           "--backend", "gloo", "--out", str(tmp_path)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=dict(os.environ, PYTHONPATH=str(ROOT)))
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert r.returncode == 0 and len(lines) == 2, r.stdout[-3000:] + r.stderr[-3000:]
-    for res in lines:
+    results = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(2)
+               if (tmp_path / f"rank{k}.json").exists()]
+    assert r.returncode == 0 and len(results) == 2, r.stdout[-3000:] + r.stderr[-3000:]
+    for res in results:
         assert res["all_ok"], res

@@ -22,6 +22,7 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--out", default=None, help="also write <out>/rank<r>.json")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -89,6 +90,10 @@ def main(argv=None) -> int:
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     res["all_ok"] = bool(flag.item())
     print(json.dumps(res), flush=True)
+    if a.out:
+        os.makedirs(a.out, exist_ok=True)
+        with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
     dist.barrier()
     xar.close()
     dist.destroy_process_group()
