@@ -1,0 +1,189 @@
+// Fused RMSNorm forward/backward for the Llama path (fp32 or bf16 activations, fp32
+// weight, fp32 statistics).  y = x * rsqrt(mean(x^2) + eps) * w.
+//
+// Forward: one workgroup per row, D/256 elements per lane held in registers, sum of
+// squares reduced wave-then-LDS, rstd saved for the backward.
+// Backward: a workgroup owns R consecutive rows; per row it recomputes the row dot
+// product sum_j dy_j w_j x_j, writes dx, and accumulates dw_j += dy_j x_j rstd for its
+// columns in registers; the per-workgroup dw partials are reduced column-wise by a
+// second tiny launch in fixed order (deterministic, no atomics).
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kMaxPer = 32;  // D <= kT * kMaxPer = 8192
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long i);
+template <>
+__device__ __forceinline__ float ld<float>(const float* p, long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p, long i) {
+  return __bfloat162float(p[i]);
+}
+template <typename T>
+__device__ __forceinline__ void st(T* p, long i, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, long i, float v) { p[i] = v; }
+template <>
+__device__ __forceinline__ void st<__hip_bfloat16>(__hip_bfloat16* p, long i, float v) {
+  p[i] = __float2bfloat16(v);
+}
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < kT / 64; ++k) t += sh[k];
+  return t;
+}
+
+template <typename T, int PER>
+__global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                         T* __restrict__ y, float* __restrict__ rstd, int D,
+                                                         float eps) {
+  __shared__ float sh[kT / 64];
+  const long row = blockIdx.x;
+  const T* xr = x + row * D;
+  float v[PER];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int j = threadIdx.x + k * kT;
+    v[k] = j < D ? ld(xr, j) : 0.f;
+    ss += v[k] * v[k];
+  }
+  const float r = rsqrtf(block_sum(ss, sh) / (float)D + eps);
+  if (threadIdx.x == 0) rstd[row] = r;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int j = threadIdx.x + k * kT;
+    if (j < D) st(y + row * D, j, v[k] * r * w[j]);
+  }
+}
+
+template <typename T, int PER>
+__global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ rstd, T* __restrict__ dx,
+                                                         float* __restrict__ dw_part, long rows, int D,
+                                                         int rows_per_block) {
+  __shared__ float sh[kT / 64];
+  float wv[PER], dwa[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int j = threadIdx.x + k * kT;
+    wv[k] = j < D ? w[j] : 0.f;
+    dwa[k] = 0.f;
+  }
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  for (long row = r0; row < min(rows, r0 + rows_per_block); ++row) {
+    float xv[PER], gv[PER];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int j = threadIdx.x + k * kT;
+      const bool ok = j < D;
+      xv[k] = ok ? ld(x + row * D, j) : 0.f;
+      gv[k] = ok ? ld(dy + row * D, j) : 0.f;
+      dot += gv[k] * wv[k] * xv[k];
+    }
+    const float r = rstd[row];
+    const float c = block_sum(dot, sh) * r * r * r / (float)D;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int j = threadIdx.x + k * kT;
+      if (j < D) {
+        st(dx + row * D, j, r * wv[k] * gv[k] - xv[k] * c);
+        dwa[k] += gv[k] * xv[k] * r;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int j = threadIdx.x + k * kT;
+    if (j < D) dw_part[(long)blockIdx.x * D + j] = dwa[k];
+  }
+}
+
+__global__ __launch_bounds__(kT) void colsum_kernel(const float* __restrict__ part, int nparts, int D,
+                                                    float* __restrict__ out) {
+  const int j = blockIdx.x * kT + threadIdx.x;
+  if (j >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * D + j];
+  out[j] = s;
+}
+
+template <typename T, int PER>
+void fwd_launch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, PER>), dim3(rows), dim3(kT), 0, (hipStream_t)stream, (const T*)x, w,
+                     (T*)y, rstd, D, eps);
+}
+
+template <typename T>
+int fwd_dispatch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
+  const int per = (D + kT - 1) / kT;
+  if (per <= 1) fwd_launch<T, 1>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 2) fwd_launch<T, 2>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 4) fwd_launch<T, 4>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 8) fwd_launch<T, 8>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 16) fwd_launch<T, 16>(x, w, y, rstd, rows, D, eps, stream);
+  else fwd_launch<T, 32>(x, w, y, rstd, rows, D, eps, stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T, int PER>
+void bwd_launch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
+                long rows, int D, int rpb, long nb, void* stream) {
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, PER>), dim3(nb), dim3(kT), 0, (hipStream_t)stream, (const T*)dy,
+                     (const T*)x, w, rstd, (T*)dx, dw_part, rows, D, rpb);
+}
+
+template <typename T>
+void bwd_dispatch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
+                  long rows, int D, int rpb, long nb, void* stream) {
+  const int per = (D + kT - 1) / kT;
+  if (per <= 1) bwd_launch<T, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 2) bwd_launch<T, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 4) bwd_launch<T, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 8) bwd_launch<T, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 16) bwd_launch<T, 16>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else bwd_launch<T, 32>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+// dtype: 0 = fp32, 1 = bf16
+int pto_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, int dtype,
+                    void* stream) {
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0) return -1;
+  return dtype == 0 ? fwd_dispatch<float>(x, w, y, rstd, rows, D, eps, stream)
+                    : fwd_dispatch<__hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream);
+}
+
+// Number of workgroups (= rows of dw_part) the backward uses for `rows` rows.
+long pto_rmsnorm_bwd_parts(long rows, int rows_per_block) { return (rows + rows_per_block - 1) / rows_per_block; }
+
+int pto_rmsnorm_bwd(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw,
+                    float* dw_part, long rows, int D, int rows_per_block, int dtype, void* stream) {
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || rows_per_block <= 0) return -1;
+  const long nb = (rows + rows_per_block - 1) / rows_per_block;
+  if (dtype == 0) bwd_dispatch<float>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  else bwd_dispatch<__hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + kT - 1) / kT), dim3(kT), 0, (hipStream_t)stream, dw_part, (int)nb,
+                     D, dw);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

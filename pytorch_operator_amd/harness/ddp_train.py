@@ -1,0 +1,178 @@
+"""DDP training worker for the BASELINE's large-model job shapes (ResNet-50 / Llama-3 bf16).
+
+The reference only ships the MNIST worker; BASELINE.json additionally names
+"ResNet-50 DDP bf16" and "Llama-3 8B DDP bf16" (Master=1 Worker=7 on 8x MI355X).  This
+entrypoint runs either shape under the same operator contract (env rendezvous, one
+``amd.com/gpu`` per pod, ``--backend rccl``) with synthetic data and random-init
+weights, and reports throughput as one JSON line (rank 0):
+
+    python -m pytorch_operator_amd.harness.ddp_train --model resnet50 --batch-size 256
+    python -m pytorch_operator_amd.harness.ddp_train --model llama3-8b --seq-len 2048 --batch-size 1
+
+MI355X specifics: bf16 autocast (MFMA bf16 through hipBLASLt/MIOpen), fused RMSNorm HIP
+kernel in the Llama blocks, DDP with flat gradient buckets sized for xGMI
+(``--bucket-mb``, default 64: few, large RCCL collectives), ``gradient_as_bucket_view``
+(no gradient copy), optional bf16 gradient compression (``--allreduce-dtype bf16``), and
+the 288 GB HBM budget that lets Llama-3 8B train with plain DDP (whole fp32 model, grads
+and AdamW state per GPU -- no sharding).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+MODELS = ("resnet50", "resnet-tiny", "llama3-8b", "llama3-1b", "llama-tiny")
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="DDP training worker (ResNet-50 / Llama-3, synthetic data)")
+    p.add_argument("--model", choices=MODELS, default="resnet50")
+    p.add_argument("--batch-size", type=int, default=None, help="per-rank batch (default 256 / 1)")
+    p.add_argument("--seq-len", type=int, default=2048)
+    p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--backend", default=None, choices=["gloo", "nccl", "rccl"])
+    p.add_argument("--no-cuda", action="store_true")
+    p.add_argument("--bucket-mb", type=float, default=64.0)
+    p.add_argument("--allreduce-dtype", choices=["fp32", "bf16"], default="fp32")
+    p.add_argument("--grad-checkpoint", action="store_true", help="Llama: recompute blocks in backward")
+    p.add_argument("--lr", type=float, default=None)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args(argv)
+
+
+def build(args, device):
+    import torch
+    if args.model.startswith("resnet"):
+        from ..models.resnet import resnet50, resnet_tiny
+        model = resnet50() if args.model == "resnet50" else resnet_tiny()
+        model = model.to(device=device, memory_format=torch.channels_last)
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr or 0.1, momentum=0.9, weight_decay=1e-4)
+        return model, opt
+    from ..models.llama import CONFIGS, Llama
+    with torch.device(device):
+        model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
+    kw = {"fused": True} if device.type == "cuda" else {}
+    try:
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1, **kw)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1)
+    return model, opt
+
+
+def train_flops_per_sample(args) -> float:
+    if args.model.startswith("resnet"):
+        scale = (args.image_size / 224.0) ** 2
+        return 3 * 4.09e9 * scale if args.model == "resnet50" else 0.0
+    from ..models.llama import CONFIGS
+    c = CONFIGS[args.model]
+    n = c.num_params() - c.vocab_size * c.dim  # embedding lookup is not a matmul
+    attn = 12 * c.n_layers * c.dim * args.seq_len  # causal attention, fwd+bwd, per token (x1/2 causal, x2)
+    return (6 * n + attn) * args.seq_len  # per sequence
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    from ..parallel.dist import init_from_env
+
+    use_gpu = not args.no_cuda and torch.cuda.is_available()
+    env = init_from_env(args.backend, use_gpu=use_gpu)
+    dev, world, rank = env.device, env.world_size, env.rank
+    torch.manual_seed(args.seed)
+    is_llama = args.model.startswith("llama")
+    B = args.batch_size or (1 if is_llama else (256 if use_gpu else 2))
+    model, opt = build(args, dev)
+    n_params = sum(p.numel() for p in model.parameters())
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        model = DDP(model, device_ids=[dev.index] if use_gpu else None, bucket_cap_mb=args.bucket_mb,
+                    gradient_as_bucket_view=True, static_graph=True)
+        if args.allreduce_dtype == "bf16":
+            from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+            model.register_comm_hook(None, default_hooks.bf16_compress_hook)
+    g = torch.Generator(device="cpu").manual_seed(args.seed + rank)
+    if is_llama:
+        from ..models.llama import CONFIGS
+        V = CONFIGS[args.model].vocab_size
+        data = torch.randint(0, V, (B, args.seq_len + 1), generator=g).to(dev)
+        x, y = data[:, :-1].contiguous(), data[:, 1:].contiguous()
+    else:
+        H = args.image_size if args.model == "resnet50" else 32
+        x = torch.randn(B, 3, H, H, generator=g).to(dev).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000 if args.model == "resnet50" else 10, (B,), generator=g).to(dev)
+    amp = torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=args.dtype == "bf16")
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with amp:
+            if is_llama:
+                loss = model(x, y)
+            else:
+                loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(dev)
+
+    t_start = time.time_ns()
+    loss = step()
+    sync()
+    if rank == 0:
+        print(json.dumps({"event": "first_step", "rank": rank, "unix_ns": time.time_ns(),
+                          "first_step_s": round((time.time_ns() - t_start) / 1e9, 3),
+                          "loss": float(loss)}), flush=True)
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    samples = args.steps * B * world
+    per_sample = train_flops_per_sample(args)
+    unit_tokens = is_llama
+    value = samples * (args.seq_len if unit_tokens else 1) / dt
+    res = {"metric": f"{args.model.replace('-', '_')}_ddp_train_{'tokens' if unit_tokens else 'images'}_per_sec",
+           "value": round(value, 1), "unit": "tokens/s" if unit_tokens else "images/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "dtype": args.dtype, "data": "synthetic", "params": n_params, "per_rank_batch": B,
+           "seq_len": args.seq_len if is_llama else None, "loss": float(loss),
+           "tflops_per_gpu": round(per_sample * samples / dt / world / 1e12, 1) if per_sample else None,
+           "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
+           "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(json.dumps(res) + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

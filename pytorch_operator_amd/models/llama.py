@@ -1,0 +1,161 @@
+"""Llama-3 decoder for the BASELINE "Llama-3 8B DDP bf16" PyTorchJob config.
+
+Not part of the reference (MNIST only); BASELINE.json names it as the large-model job
+shape: Master=1 Worker=7, 288 GB HBM sizing, OnFailure restarts + gang scheduling.
+Plain DDP fits on MI355X: 8.0 B parameters in fp32 (32 GB) + fp32 grads (32 GB) + AdamW
+moments (64 GB) + bf16 activations for a 2 k-token sequence stay well inside 288 GB, so
+no sharding is needed -- every rank keeps the whole model and only gradients cross xGMI.
+
+Architecture (Meta's reference layout): token embedding, ``n_layers`` x [RMSNorm ->
+GQA attention with RoPE (theta 500 000) -> residual, RMSNorm -> SwiGLU FFN -> residual],
+final RMSNorm, untied output projection.  Matmuls run in bf16 under autocast
+(hipBLASLt); attention uses ``scaled_dot_product_attention`` (ROCm flash attention);
+RMSNorm uses the fused HIP kernel from ``ops.norm`` when it is built (fp32 statistics).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass
+class LlamaConfig:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    vocab_size: int = 128256
+    ffn_hidden: int = 14336
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+    def num_params(self) -> int:
+        d, f, v, L = self.dim, self.ffn_hidden, self.vocab_size, self.n_layers
+        kv = self.n_kv_heads * self.head_dim
+        per_layer = d * d * 2 + d * kv * 2 + 3 * d * f + 2 * d
+        return L * per_layer + 2 * v * d + d
+
+
+CONFIGS = {
+    "llama3-8b": LlamaConfig(),
+    "llama3-1b": LlamaConfig(dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, ffn_hidden=8192),
+    "llama-tiny": LlamaConfig(dim=64, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=256, ffn_hidden=128,
+                              max_seq_len=256),
+}
+
+
+def rope_tables(head_dim: int, seq_len: int, theta: float, device=None):
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, device=device, dtype=torch.float32) / head_dim))
+    t = torch.arange(seq_len, device=device, dtype=torch.float32)
+    ang = torch.outer(t, inv)  # [S, D/2]
+    return torch.cos(ang), torch.sin(ang)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x [B, S, H, D]; rotates adjacent pairs (x0, x1) like Meta's complex formulation."""
+    xf = x.float().reshape(*x.shape[:-1], -1, 2)
+    x0, x1 = xf[..., 0], xf[..., 1]
+    c = cos[None, :, None, :]
+    s = sin[None, :, None, :]
+    out = torch.stack((x0 * c - x1 * s, x0 * s + x1 * c), dim=-1)
+    return out.flatten(-2).type_as(x)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, dim: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops.norm import rms_norm
+        return rms_norm(x, self.weight, self.eps)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.nh, self.nkv, self.hd = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        self.wq = nn.Linear(cfg.dim, self.nh * self.hd, bias=False)
+        self.wk = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
+        self.wv = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
+        self.wo = nn.Linear(self.nh * self.hd, cfg.dim, bias=False)
+
+    def forward(self, x, cos, sin):
+        B, S, _ = x.shape
+        q = apply_rope(self.wq(x).view(B, S, self.nh, self.hd), cos, sin)
+        k = apply_rope(self.wk(x).view(B, S, self.nkv, self.hd), cos, sin)
+        v = self.wv(x).view(B, S, self.nkv, self.hd)
+        q, k, v = (t.transpose(1, 2) for t in (q, k, v))  # [B, H, S, D]
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.nkv != self.nh)
+        return self.wo(o.transpose(1, 2).reshape(B, S, self.nh * self.hd))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.w1 = nn.Linear(cfg.dim, cfg.ffn_hidden, bias=False)
+        self.w3 = nn.Linear(cfg.dim, cfg.ffn_hidden, bias=False)
+        self.w2 = nn.Linear(cfg.ffn_hidden, cfg.dim, bias=False)
+
+    def forward(self, x):
+        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.attention_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.attention = Attention(cfg)
+        self.ffn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.feed_forward = FeedForward(cfg)
+
+    def forward(self, x, cos, sin):
+        x = x + self.attention(self.attention_norm(x), cos, sin)
+        return x + self.feed_forward(self.ffn_norm(x))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig, checkpoint_layers: bool = False):
+        super().__init__()
+        self.cfg = cfg
+        self.checkpoint_layers = checkpoint_layers
+        self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
+        self.layers = nn.ModuleList(Block(cfg) for _ in range(cfg.n_layers))
+        self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
+        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self, std: float = 0.02):
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=std)
+        # scaled init of the residual projections (GPT-2 / Llama practice)
+        for blk in self.layers:
+            nn.init.normal_(blk.attention.wo.weight, std=std / math.sqrt(2 * self.cfg.n_layers))
+            nn.init.normal_(blk.feed_forward.w2.weight, std=std / math.sqrt(2 * self.cfg.n_layers))
+
+    def forward(self, tokens: torch.Tensor, targets: Optional[torch.Tensor] = None):
+        B, S = tokens.shape
+        cos, sin = rope_tables(self.cfg.head_dim, S, self.cfg.rope_theta, tokens.device)
+        h = self.tok_embeddings(tokens)
+        for blk in self.layers:
+            if self.checkpoint_layers and self.training:
+                h = torch.utils.checkpoint.checkpoint(blk, h, cos, sin, use_reentrant=False)
+            else:
+                h = blk(h, cos, sin)
+        logits = self.output(self.norm(h))
+        if targets is None:
+            return logits
+        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.view(-1))
