@@ -184,3 +184,33 @@ def test_fault_injection_hook_exits_137_after_checkpoint(tmp_path):
         assert any(e["event"] == "resumed" for e in _events(out))
     finally:
         del os.environ["PTO_FAULT_EXIT_AFTER_EPOCH"]
+
+
+def test_ddp_train_worker_llama_tiny_two_ranks(tmp_path):
+    outs = _launch("pytorch_operator_amd.harness.ddp_train",
+                   ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--steps", "2", "--warmup", "1",
+                    "--backend", "gloo", "--allreduce-dtype", "bf16"], 2, tmp_path)
+    for rc, out in outs:
+        assert rc == 0, out
+    res = json.loads([ln for ln in outs[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    assert res["metric"] == "llama_tiny_ddp_train_tokens_per_sec" and res["n_gpus"] == 2
+
+
+def test_ddp_train_worker_resnet_tiny(tmp_path):
+    (rc, out), = _launch("pytorch_operator_amd.harness.ddp_train",
+                         ["--model", "resnet-tiny", "--batch-size", "2", "--steps", "2", "--warmup", "1"], 1, tmp_path)
+    assert rc == 0, out
+    assert '"resnet_tiny_ddp_train_images_per_sec"' in out
+
+
+def test_example_yamls_are_valid_jobs():
+    import yaml
+    from opfixtures import opcore
+    for path in sorted((ROOT / "examples").rglob("*.yaml")):
+        job = yaml.safe_load(path.read_text())
+        assert job["kind"] == "PyTorchJob", path
+        err = opcore().validate_spec(json.dumps(job["spec"]))
+        assert not err, (path, err)
+        for spec in job["spec"]["pytorchReplicaSpecs"].values():
+            for c in spec["template"]["spec"]["containers"]:
+                assert "nvidia.com/gpu" not in json.dumps(c), path  # MI355X-only resources
