@@ -149,3 +149,13 @@ def test_watch_prints_table_until_finished(client, cluster):
 def test_client_configuration_object(cluster):
     c = PyTorchJobClient(client_configuration=Configuration(host=cluster.api.url))
     assert "items" in c.get(namespace=NS)
+
+
+def test_generated_schema_is_up_to_date():
+    """The reference's verify-codegen step: docs/pytorchjob.schema.json matches the models."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    r = subprocess.run([sys.executable, str(root / "tools" / "gen_schema.py"), "--check"], capture_output=True)
+    assert r.returncode == 0, "run `make schema`"
