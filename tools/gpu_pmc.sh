@@ -11,3 +11,4 @@ for ctrs in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA 
   cd $R && timeout -k 10 240 rocprofv3 --kernel-trace --pmc $ctrs -d $R/gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps 200 --warmup 10 --mode eager > $R/gpurun_out/pmc/log$i.txt 2>&1 || { tail -5 $R/gpurun_out/pmc/log$i.txt; exit 1; }
 done
 find $R/gpurun_out/pmc -name "*.csv" | head -20
+python3 tools/pmc_summary.py $(find $R/gpurun_out/pmc -name "*counter_collection.csv") > $R/gpurun_out/pmc/summary.txt && head -5 $R/gpurun_out/pmc/summary.txt
