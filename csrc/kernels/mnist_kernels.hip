@@ -738,20 +738,28 @@ constexpr int F_D8 = 80;    // dz80_s [52 co][80]    B of 2a: lanes = pos cols, 
 constexpr int F_WS = 144;   // w_s    [52 co][144]   A of 2a: lanes = j cols, +row per g (== 16 mod 32)
 constexpr int F_DC = 68;    // dcolT  [128 j][68]    2a C writes (4*68 == 16 mod 32); col2im reads
                             //                       walk pos with lanes -> conflict-free
-constexpr int F_Z1 = 580;   // dz1_s [5][580]      (== 4 mod 32)
+constexpr int F_Z1 = 628;   // dz1_s [5][24 rows x F_Z1R] (+4 pad)
+// strides picked with an LDS bank-conflict model so that the phase-2b im2col gathers,
+// the phase-3 reads/stores and the phase-4 sliding windows are (nearly) conflict-free:
+constexpr int F_Z1R = 26;   // dz1 row stride
+constexpr int F_A1R = 13;   // a1 row stride
+constexpr int F_A1C = 160;  // a1 channel stride (>= 12 rows x F_A1R)
+constexpr int F_XR = 29;    // xn row stride
 constexpr int F_OFF_DZ = 0;
 constexpr int F_OFF_D8 = F_OFF_DZ + 64 * F_DS;
 constexpr int F_OFF_W = F_OFF_D8 + 52 * F_D8;
 constexpr int F_OFF_DCOL = F_OFF_W + 52 * F_WS;
 constexpr int F_OFF_A1 = F_OFF_DCOL + 128 * F_DC;
-constexpr int F_OFF_X = F_OFF_A1 + 5 * 144;
-constexpr int F_OFF_IDX = F_OFF_X + 784;        // 720 uint8 (180 floats)
+constexpr int F_OFF_X = F_OFF_A1 + 4 * F_A1C + 12 * F_A1R;  // last channel ends at 12 rows
+constexpr int F_OFF_IDX = F_OFF_X + 28 * F_XR;  // 720 uint8 (180 floats)
 constexpr int F_LDS = F_OFF_IDX + 180;
 // aliases of the (dead after phase 2a) weight region:
 constexpr int F_OFF_DZ1 = F_OFF_W;
 constexpr int F_OFF_RED = F_OFF_W + 5 * F_Z1;
 constexpr int F_RED1 = 132;  // phase-4 partial row: 125 dW_conv1 taps + 5 bias sums
 static_assert(5 * F_Z1 + 16 * F_RED1 <= 52 * F_WS, "alias region too small");
+static_assert(F_A1C >= 12 * F_A1R && F_Z1 >= 24 * F_Z1R && F_Z1R >= 24 && F_A1R >= 12 && F_XR >= 28,
+              "padded LDS rows/channels must not overlap");
 
 __global__ __launch_bounds__(512) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
@@ -821,8 +829,12 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = tid + k * 512;
-      if (e < 720) { a1_s[e] = av[k]; idx_s[e] = iv[k]; }
-      if (e < 784) x_s[e] = xv[k];
+      if (e < 720) {
+        const int c = e / 144, pp = e - c * 144, yy = pp / 12;
+        a1_s[c * F_A1C + yy * F_A1R + (pp - yy * 12)] = av[k];
+        idx_s[e] = iv[k];
+      }
+      if (e < 784) x_s[(e / 28) * F_XR + e % 28] = xv[k];
     }
   }
   __syncthreads();
@@ -859,12 +871,12 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
       jv[n] = j < 125;
       const int jc = jv[n] ? j : 124;
       const int ci = jc / 25, t = jc - ci * 25;
-      boff[n] = ci * 144 + (t / 5) * 12 + (t % 5);
+      boff[n] = ci * F_A1C + (t / 5) * F_A1R + (t % 5);
     }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const float av = dz_s[(mt * 16 + i) * F_DS + 4 * s + g];
-      const int poff = (s >> 1) * 12 + 4 * (s & 1) + g;  // pos = 4s+g -> (oh, ow)
+      const int poff = (s >> 1) * F_A1R + 4 * (s & 1) + g;  // pos = 4s+g -> (oh, ow)
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const float bv = jv[n] ? a1_s[boff[n] + poff] : 0.f;
@@ -900,16 +912,16 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
           da += ok ? v : 0.f;
         }
       }
-      const float d = a1_s[e] > 0.f ? da : 0.f;
+      const float d = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
       const int pidx = idx_s[e];
-      float* z = dz1_s + c * F_Z1 + (2 * y) * 24 + 2 * x;
+      float* z = dz1_s + c * F_Z1 + (2 * y) * F_Z1R + 2 * x;
       z[0] = pidx == 0 ? d : 0.f;
       z[1] = pidx == 1 ? d : 0.f;
-      z[24] = pidx == 2 ? d : 0.f;
-      z[25] = pidx == 3 ? d : 0.f;
+      z[F_Z1R] = pidx == 2 ? d : 0.f;
+      z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
       if (dz1_out != nullptr) {
         float* zo = dz1_out + (size_t)b * 11520 + (cig * 5 + c) * 576 + (2 * y) * 24 + 2 * x;
-        zo[0] = z[0]; zo[1] = z[1]; zo[24] = z[24]; zo[25] = z[25];
+        zo[0] = z[0]; zo[1] = z[1]; zo[24] = z[F_Z1R]; zo[25] = z[F_Z1R + 1];
       }
     }
   }
@@ -918,26 +930,26 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
 
   // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU.  As an MFMA GEMM this is
   // M = 5 channels padded to 16 (3/4 of every MFMA wasted, ~3 us); here 400 threads =
-  // (channel c, kernel row kh, 8 row-groups x 2 column-halves) each slide a 16-wide
+  // (channel c, 8 row-groups x 2 column-halves, kernel row kh) each slide a 16-wide
   // register window of the input row across 12 output columns: 5 FMAs per 2 LDS reads.
   // The kh == 0 threads also sum dz1 for the bias gradient.  16 partials meet in LDS.
   if (tid < 400) {
     const int c = tid / 80, rem = tid - c * 80;
-    const int kh = rem >> 4, part = rem & 15;
-    const int ry = part >> 1, cx = (part & 1) * 12;
+    const int part = rem / 5, kh = rem - part * 5;
+    const int ry = part & 7, cx = (part >> 3) * 12;
     const float* zr = dz1_s + c * F_Z1;
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float bs = 0.f;
 #pragma unroll
     for (int yy = 0; yy < 3; ++yy) {
       const int y = ry * 3 + yy;
-      const float* xr = x_s + (y + kh) * 28 + cx;
+      const float* xr = x_s + (y + kh) * F_XR + cx;
       float xw[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) xw[q] = xr[q];
 #pragma unroll
       for (int x = 0; x < 12; ++x) {
-        const float a = zr[y * 24 + cx + x];
+        const float a = zr[y * F_Z1R + cx + x];
         bs += a;
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
