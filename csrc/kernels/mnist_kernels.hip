@@ -723,7 +723,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// F: conv backward.  grid = (4 input-channel groups of 5, B samples), 8 waves.
+// F: conv backward.  grid = (4 input-channel groups of 5, B samples), F_NT/64 waves.
 //   phase 1   stage dz2[b] (two layouts), the W2 column slice, a1 slice, xn[b], idx1 slice
 //   phase 2a  dcol[64 pos, 125 (ci,kh,kw)] = dz2[b]^T . W2[:, group]   (MFMA, K = 50)
 //   phase 2b  dW_conv2[50, group] partial = dz2[b] . im2col(a1[b])      (MFMA, K = 64)
@@ -761,7 +761,14 @@ static_assert(5 * F_Z1 + 16 * F_RED1 <= 52 * F_WS, "alias region too small");
 static_assert(F_A1C >= 12 * F_A1R && F_Z1 >= 24 * F_Z1R && F_Z1R >= 24 && F_A1R >= 12 && F_XR >= 28,
               "padded LDS rows/channels must not overlap");
 
-__global__ __launch_bounds__(512) void conv_bwd_kernel(
+constexpr int F_NT = 1024;          // 16 waves: 4 per SIMD hide the LDS latency of phase 2
+constexpr int F_NW = F_NT / 64;
+constexpr int F_TPW = 32 / F_NW;     // 16x16 tiles per wave in each of 2a / 2b (32 tiles each)
+constexpr int F_NDZ = 4096 / F_NT;   // dz2 staging: 64 co (50 real) x 64 pos
+constexpr int F_NW2 = (6656 + F_NT - 1) / F_NT;  // W2 slice staging: 52 co x 128 j
+static_assert(F_NT >= 784 && 4096 % F_NT == 0 && 32 % F_NW == 0, "conv_bwd thread mapping");
+
+__global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ gw1, float* __restrict__ gb1,
@@ -787,86 +794,81 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
     const float* dzb = dz2 + (size_t)b * 3200;
     // clamped addresses + register selects: no load is predicated (a predicated
     // load makes hipcc wait vmcnt(0) per element)
-    float v[8];
+    float v[F_NDZ];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = dzb[min(tid + k * 512, 3199)];
-    float wv_[13];
+    for (int k = 0; k < F_NDZ; ++k) v[k] = dzb[min(tid + k * F_NT, 3199)];
+    float wv_[F_NW2];
 #pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      const int e = tid + k * 512;  // < 6656 = 52*128
+    for (int k = 0; k < F_NW2; ++k) {
+      const int e = tid + k * F_NT;
       const int co = min(e >> 7, 49), j = min(e & 127, 124);
       wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
     }
-    float av[2], xv[2];
-    uint8_t iv[2];
+    const int ec = min(tid, 719);
+    const float av = a1[(size_t)b * 2880 + cig * 720 + ec];
+    const uint8_t iv = idx1[(size_t)b * 2880 + cig * 720 + ec];
+    const float xv = xn[(size_t)b * 784 + min(tid, 783)];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + k * 512;
-      av[k] = a1[(size_t)b * 2880 + cig * 720 + min(e, 719)];
-      iv[k] = idx1[(size_t)b * 2880 + cig * 720 + min(e, 719)];
-      xv[k] = xn[(size_t)b * 784 + min(e, 783)];
-    }
+    for (int k = 0; k < F_NDZ; ++k)
+      if (tid + k * F_NT >= 3200) v[k] = 0.f;  // co >= 50
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (tid + k * 512 >= 3200) v[k] = 0.f;  // co >= 50
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < F_NW2; ++k) {
+      const int e = tid + k * F_NT;
       if ((e >> 7) >= 50 || (e & 127) >= 125) wv_[k] = 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < F_NDZ; ++k) {
+      const int e = tid + k * F_NT;
       const int co = e >> 6, pos = e & 63;
       dz_s[co * F_DS + pos] = v[k];
       if (co < 52) dz80_s[co * F_D8 + pos] = v[k];
     }
 #pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      const int e = tid + k * 512;
-      w_s[(e >> 7) * F_WS + (e & 127)] = wv_[k];
+    for (int k = 0; k < F_NW2; ++k) {
+      const int e = tid + k * F_NT;
+      if (e < 6656) w_s[(e >> 7) * F_WS + (e & 127)] = wv_[k];
     }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + k * 512;
-      if (e < 720) {
-        const int c = e / 144, pp = e - c * 144, yy = pp / 12;
-        a1_s[c * F_A1C + yy * F_A1R + (pp - yy * 12)] = av[k];
-        idx_s[e] = iv[k];
-      }
-      if (e < 784) x_s[(e / 28) * F_XR + e % 28] = xv[k];
+    if (tid < 720) {
+      const int c = tid / 144, pp = tid - c * 144, yy = pp / 12;
+      a1_s[c * F_A1C + yy * F_A1R + (pp - yy * 12)] = av;
+      idx_s[tid] = iv;
     }
+    if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv;
   }
   __syncthreads();
   stamp(dbg, 1);
 
-  const int mt = wv & 3, nt0 = (wv >> 2) * 4;
+  const int mt = wv & 3, nt0 = (wv >> 2) * F_TPW;
   // ---- phase 2a: dcolT[j][pos] = W2 slice^T . dz2   (M = 128 j, N = 64 pos, K = 52)
   {
-    const int pt = wv & 3, jt0 = (wv >> 2) * 4;
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+    const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
+    f32x4 acc[F_TPW];
+#pragma unroll
+    for (int n = 0; n < F_TPW; ++n) acc[n] = zero4();
 #pragma unroll
     for (int s = 0; s < 13; ++s) {
       const float bv = dz80_s[(4 * s + g) * F_D8 + pt * 16 + i];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < F_TPW; ++n) {
         const float av = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
         acc[n] = mfma16x16x4(av, bv, acc[n]);
       }
     }
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < F_TPW; ++n)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         dcol_s[((jt0 + n) * 16 + g * 4 + r) * F_DC + pt * 16 + i] = acc[n][r];
   }
   // ---- phase 2b: dW_conv2 partial  (M = 64 co, N = 128 (ci,kh,kw), K = 64 pos)
-  f32x4 gacc[4] = {zero4(), zero4(), zero4(), zero4()};
-  {
-    int boff[4];
-    bool jv[4];
+  f32x4 gacc[F_TPW];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+  for (int n = 0; n < F_TPW; ++n) gacc[n] = zero4();
+  {
+    int boff[F_TPW];
+    bool jv[F_TPW];
+#pragma unroll
+    for (int n = 0; n < F_TPW; ++n) {
       const int j = (nt0 + n) * 16 + i;
       jv[n] = j < 125;
       const int jc = jv[n] ? j : 124;
@@ -878,7 +880,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
       const float av = dz_s[(mt * 16 + i) * F_DS + 4 * s + g];
       const int poff = (s >> 1) * F_A1R + 4 * (s & 1) + g;  // pos = 4s+g -> (oh, ow)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < F_TPW; ++n) {
         const float bv = jv[n] ? a1_s[boff[n] + poff] : 0.f;
         gacc[n] = mfma16x16x4(av, bv, gacc[n]);
       }
@@ -894,8 +896,8 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int e = tid + k * 512;
+  for (int k = 0; k < (720 + F_NT - 1) / F_NT; ++k) {
+    const int e = tid + k * F_NT;
     if (e < 720) {
       const int c = e / 144, p = e - c * 144;
       const int y = p / 12, x = p - y * 12;
@@ -974,7 +976,7 @@ __global__ __launch_bounds__(512) void conv_bwd_kernel(
   const bool slab = slab_stride > 0;
   const size_t so = slab ? (size_t)b * slab_stride : 0;
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
+  for (int n = 0; n < F_TPW; ++n) {
     const int j = (nt0 + n) * 16 + i;
     if (j < 125) {
 #pragma unroll
@@ -1277,7 +1279,7 @@ int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(512), F_LDS * sizeof(float),
+  hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float),
                      (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
                      slab_stride, B, g_dbg);
   return (int)hipGetLastError();
