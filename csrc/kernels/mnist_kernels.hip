@@ -166,18 +166,42 @@ __device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb)
   return acc0 + acc1;
 }
 
-__global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
+constexpr int AB_NT = 1024;  // conv forward blocks: 16 waves, 4 per SIMD keep the matrix pipe fed
+
+// conv2 implicit GEMM of one block: 4 position tiles x 4 K quarters (the 25
+// (ci-group, kh) rows split 6/7/6/6) over 16 waves; the quarters meet in LDS in a fixed
+// order (the standalone and the fused kernel produce bit-identical a2).  Returns the
+// full sum in the kq == 0 waves.
+__device__ __forceinline__ f32x4 conv2_block(const float* in_s, const float* w_s, f32x4 (*red)[4][64],
+                                             int wv, int lane) {
+  const int pt = wv & 3, kq = wv >> 2;
+  const int i = lane & 15, g = lane >> 4;
+  const int oh = 2 * pt + (i >> 3), ow = i & 7;
+  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
+  const float* Bb = w_s + i * C2_WS + g * 25;
+  f32x4 acc;
+  if (kq == 0) acc = conv2_k_range<0, 6>(Ab, Bb);
+  else if (kq == 1) acc = conv2_k_range<6, 13>(Ab, Bb);
+  else if (kq == 2) acc = conv2_k_range<13, 19>(Ab, Bb);
+  else acc = conv2_k_range<19, 25>(Ab, Bb);
+  if (kq > 0) red[kq - 1][pt][lane] = acc;
+  __syncthreads();
+  if (kq == 0) acc += red[0][pt][lane] + red[1][pt][lane] + red[2][pt][lane];
+  return acc;
+}
+
+__global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
     const float* __restrict__ a1, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
   __shared__ float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
-  __shared__ f32x4 red[4][64];
+  __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   stamp(dbg, 0);
   const float* src = a1 + (size_t)b * 2880;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const int e = tid + k * 512;
+  for (int k = 0; k < (2880 + AB_NT - 1) / AB_NT; ++k) {
+    const int e = tid + k * AB_NT;
     if (e < 2880) {
       const int c = e / 144, p = e - c * 144;
       const int y = p / 12, x = p - y * 12;
@@ -185,8 +209,8 @@ __global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
     }
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int e = tid + k * 512;
+  for (int k = 0; k < (2000 + AB_NT - 1) / AB_NT; ++k) {
+    const int e = tid + k * AB_NT;
     if (e < 16 * 125) {
       const int j = e / 125, q = e - j * 125;
       const int co = cg * 16 + j;
@@ -201,19 +225,10 @@ __global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
   stamp(dbg, 1);
 
   const int lane = tid & 63, wv = tid >> 6;
-  const int pt = wv & 3, khalf = wv >> 2;
-  const int i = lane & 15, g = lane >> 4;
-  const int oh = 2 * pt + (i >> 3), ow = i & 7;
-  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
-  const float* Bb = w_s + i * C2_WS + g * 25;
-  f32x4 acc;
-  if (khalf == 0) acc = conv2_k_range<0, 13>(Ab, Bb);
-  else acc = conv2_k_range<13, 25>(Ab, Bb);
-  if (khalf == 1) red[pt][lane] = acc;
-  __syncthreads();
+  const int pt = wv & 3, i = lane & 15, g = lane >> 4;
+  f32x4 acc = conv2_block(in_s, w_s, red, wv, lane);
   stamp(dbg, 2);
-  if (khalf == 1) return;
-  acc += red[pt][lane];
+  if (wv >= 4) return;
   const int co = cg * 16 + i;
   const float bco = (co < 50) ? bias[co] : 0.f;
   // reg r of this lane = conv position (oh = 2pt + (g>>1), ow = 4(g&1) + r)
@@ -239,13 +254,70 @@ __global__ __launch_bounds__(512) void conv2_fwd_pool_kernel(
 
 // ---------------------------------------------------------------------------
 // AB: conv1 + conv2 forward fused (the training path).  grid = (4 conv2 output
-//   channel groups, B samples), 8 waves.  Every block recomputes conv1 + ReLU +
-//   pool for its sample on the VALU straight into the conv2 im2col image in LDS
+//   channel groups, B samples), 16 waves.  Every block recomputes conv1 + ReLU +
+//   pool for its sample on MFMA straight into the conv2 im2col image in LDS
 //   (4x redundant, ~1 us, cheaper than a launch boundary + an HBM round trip);
 //   the cg == 0 block publishes a1/idx1 (for the backward), xn and lab.
 //   conv2 then runs exactly as conv2_fwd_pool_kernel.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void conv12_fwd_kernel(
+// conv1 tasks t0, t0 + 16, .. (NU of them) as NU independent MFMA accumulator chains,
+// then bias + ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1 if pub).
+template <int NU>
+__device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int (&toff)[7],
+                                            const float (&bw)[2][7], const float* w1s, float* in_s,
+                                            bool pub, float* a1, uint8_t* idx1, int b, int i, int g) {
+  f32x4 acc[NU];
+  const float* ibs[NU];
+  int nts[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int t = t0 + 16 * u;
+    const int pt1 = t >> 1;
+    nts[u] = t & 1;
+    const int py = pt1 / 3, px = pt1 - py * 3;
+    ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
+    acc[u] = zero4();
+  }
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      acc[u] = mfma16x16x4(ibs[u][toff[s]], nts[u] ? bw[1][s] : bw[0][s], acc[u]);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int t = t0 + 16 * u;
+    const int pt1 = t >> 1, nt = t & 1;
+    const int py = pt1 / 3, px = pt1 - py * 3;
+    const int c = nt * 16 + i;
+    const float bc = w1s[500 + min(c, 19)];
+    const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc, v3 = acc[u][3] + bc;
+    float mA = v0; int aA = 0;
+    if (v1 > mA) { mA = v1; aA = 1; }
+    float mB = v2; int aB = 0;
+    if (v3 > mB) { mB = v3; aB = 1; }
+    const float pA = __shfl_xor(mA, 32, 64);
+    const int paA = __shfl_xor(aA, 32, 64);
+    const float pB = __shfl_xor(mB, 32, 64);
+    const int paB = __shfl_xor(aB, 32, 64);
+    if (g < 2 && c < 20) {
+      if (pA > mA) { mA = pA; aA = 2 + paA; }
+      if (pB > mB) { mB = pB; aB = 2 + paB; }
+      const int pw = 4 * px + 2 * (g & 1);
+      const float va = fmaxf(mA, 0.f), vb = fmaxf(mB, 0.f);
+      in_s[c * C2_CS + py * C2_RS + pw] = va;
+      in_s[c * C2_CS + py * C2_RS + pw + 1] = vb;
+      if (pub) {
+        const size_t o = (size_t)b * 2880 + c * 144 + py * 12 + pw;
+        a1[o] = va;
+        a1[o + 1] = vb;
+        idx1[o] = (uint8_t)aA;
+        idx1[o + 1] = (uint8_t)aB;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     BatchSrc src, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
     uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
@@ -254,31 +326,29 @@ __global__ __launch_bounds__(512) void conv12_fwd_kernel(
   __shared__ float w1s[520];
   __shared__ float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
-  __shared__ f32x4 red[4][64];
+  __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   stamp(dbg, 0);
   const int row = batch_row(src, b, B);
   const bool pub = cg == 0;
   {
-    const float x0 = load_px(src, row, tid);
-    const float x1 = load_px(src, row, min(tid + 512, 783));
+    const float x0 = load_px(src, row, min(tid, 783));
     const float wv = w1[min(tid, 499)];
     const float bv1 = b1[min(tid, 19)];
-    float4 wq[4];
+    float4 wq[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = min(tid + k * 512, 16 * 125 - 1);
+    for (int k = 0; k < 2; ++k) {
+      const int e = min(tid + k * AB_NT, 16 * 125 - 1);
       const int j = e / 125, q = e - j * 125;
       const int co = min(cg * 16 + j, 49);
       wq[k] = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
     }
-    img[tid] = x0;
-    if (tid + 512 < 784) img[tid + 512] = x1;
+    if (tid < 784) img[tid] = x0;
     if (tid < 500) w1s[tid] = wv;
     if (tid < 20) w1s[500 + tid] = bv1;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = tid + k * 512;
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + k * AB_NT;
       if (e < 16 * 125) {
         const int j = e / 125, q = e - j * 125;
         float4 v = wq[k];
@@ -288,9 +358,8 @@ __global__ __launch_bounds__(512) void conv12_fwd_kernel(
         d[1] = make_float2(v.z, v.w);
       }
     }
-    if (pub) {
+    if (pub && tid < 784) {
       xn_out[(size_t)b * 784 + tid] = x0;
-      if (tid + 512 < 784) xn_out[(size_t)b * 784 + tid + 512] = x1;
       if (tid == 0 && lab_out != nullptr) lab_out[b] = src.labels[row];
     }
   }
@@ -317,80 +386,21 @@ __global__ __launch_bounds__(512) void conv12_fwd_kernel(
         bw[nt][s] = (c < 20 && tap < 25) ? wv_ : 0.f;
       }
     }
-    // 72 tasks = 36 position tiles x 2 channel tiles; wave w takes tasks w, w+8, ..
-    // (9 each) as three independent accumulator chains per iteration (MFMA latency
-    // 40 cycles > 32-cycle issue: one chain alone would idle the matrix pipe).
-#pragma unroll 1
-    for (int t0 = wv; t0 < 72; t0 += 24) {
-      f32x4 acc[3];
-      const float* ibs[3];
-      int nts[3];
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int t = t0 + 8 * u;
-        const int pt1 = t >> 1;
-        nts[u] = t & 1;
-        const int py = pt1 / 3, px = pt1 - py * 3;
-        ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
-        acc[u] = zero4();
-      }
-#pragma unroll
-      for (int s = 0; s < 7; ++s)
-#pragma unroll
-        for (int u = 0; u < 3; ++u)
-          acc[u] = mfma16x16x4(ibs[u][toff[s]], nts[u] ? bw[1][s] : bw[0][s], acc[u]);
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int t = t0 + 8 * u;
-        const int pt1 = t >> 1, nt = t & 1;
-        const int py = pt1 / 3, px = pt1 - py * 3;
-        const int c = nt * 16 + i;
-        const float bc = w1s[500 + min(c, 19)];
-        const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc,
-                    v3 = acc[u][3] + bc;
-        float mA = v0; int aA = 0;
-        if (v1 > mA) { mA = v1; aA = 1; }
-        float mB = v2; int aB = 0;
-        if (v3 > mB) { mB = v3; aB = 1; }
-        const float pA = __shfl_xor(mA, 32, 64);
-        const int paA = __shfl_xor(aA, 32, 64);
-        const float pB = __shfl_xor(mB, 32, 64);
-        const int paB = __shfl_xor(aB, 32, 64);
-        if (g < 2 && c < 20) {
-          if (pA > mA) { mA = pA; aA = 2 + paA; }
-          if (pB > mB) { mB = pB; aB = 2 + paB; }
-          const int pw = 4 * px + 2 * (g & 1);
-          const float va = fmaxf(mA, 0.f), vb = fmaxf(mB, 0.f);
-          in_s[c * C2_CS + py * C2_RS + pw] = va;
-          in_s[c * C2_CS + py * C2_RS + pw + 1] = vb;
-          if (pub) {
-            const size_t o = (size_t)b * 2880 + c * 144 + py * 12 + pw;
-            a1[o] = va;
-            a1[o + 1] = vb;
-            idx1[o] = (uint8_t)aA;
-            idx1[o + 1] = (uint8_t)aB;
-          }
-        }
-      }
-    }
+    // 72 tasks = 36 position tiles x 2 channel tiles; wave w takes tasks w, w+16, ..
+    // (5 for w < 8, 4 otherwise: 18 per SIMD) as independent accumulator chains
+    // (MFMA latency > issue interval: one chain alone would idle the matrix pipe).
+    conv1_tasks<3>(wv, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
+    if (wv < 8) conv1_tasks<2>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
+    else conv1_tasks<1>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
   }
   __syncthreads();
   stamp(dbg, 2);
 
   const int lane = tid & 63, wv = tid >> 6;
-  const int pt = wv & 3, khalf = wv >> 2;
-  const int i = lane & 15, g = lane >> 4;
-  const int oh = 2 * pt + (i >> 3), ow = i & 7;
-  const float* Ab = in_s + g * C2_CS + oh * C2_RS + ow;
-  const float* Bb = w_s + i * C2_WS + g * 25;
-  f32x4 acc;
-  if (khalf == 0) acc = conv2_k_range<0, 13>(Ab, Bb);
-  else acc = conv2_k_range<13, 25>(Ab, Bb);
-  if (khalf == 1) red[pt][lane] = acc;
-  __syncthreads();
+  const int pt = wv & 3, i = lane & 15, g = lane >> 4;
+  f32x4 acc = conv2_block(in_s, w_s, red, wv, lane);
   stamp(dbg, 3);
-  if (khalf == 1) return;
-  acc += red[pt][lane];
+  if (wv >= 4) return;
   const int co = cg * 16 + i;
   const float bco = (co < 50) ? bias[co] : 0.f;
   const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
@@ -1212,7 +1222,7 @@ int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* labels, const int* 
 int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, float* a2,
                         uint8_t* idx2, int B, void* stream) {
   PTO_CHECK_B(B);
-  hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(512), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream,
                      a1, w, bias, a2, idx2, B, g_dbg);
   return (int)hipGetLastError();
 }
@@ -1227,7 +1237,7 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
   if (lab_out != nullptr && labels == nullptr) return -1;
   if (((uintptr_t)w2) & 15) return -2;
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
-  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(512), 0, (hipStream_t)stream, src, w1,
+  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
                      b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, g_dbg);
   return (int)hipGetLastError();
 }
