@@ -3,29 +3,44 @@
 // Why: at B=64 the MNIST step is ~50 us of GPU time and the DDP gradient all-reduce is
 // 1.7 MB (431k fp32).  RCCL launched from the host between graph replays adds its own
 // launch/proxy latency and keeps the step out of a single hipGraph.  Every GPU of an
-// 8x MI355X node has a direct xGMI link to every other, so a two-shot all-reduce done by
-// ordinary loads from peer memory (IPC-mapped) moves only 2 x 1.7 MB / W per link and can
-// be captured in the step's hipGraph like any other kernel.
+// 8x MI355X node has a direct xGMI link to every other, so a two-shot all-reduce done
+// with ordinary stores into peer memory (IPC-mapped) moves only 2 x 1.7 MB x (W-1)/W per
+// GPU, spread over all W-1 links, and is captured in the step's hipGraph like any other
+// kernel.
 //
-// Protocol (one launch per step, `nblk` workgroups per rank, all co-resident):
+// PUSH protocol (one launch per step, `nblk` workgroups per rank, all co-resident).
+// Remote traffic is only posted stores (no remote loads, no remote polling: a remote load
+// is a full xGMI round trip, a store is fire-and-forget); every wait polls LOCAL memory
+// with one lane per flag, so W flags cost one local round trip, not W remote ones.
+//
 //   buffer (per rank, uncached device memory, IPC-exported):
-//     [pub counter | red counter | data[2][npad] | red[2][npad]]
-//   step s = pub/nblk + 1 read at kernel start (only this rank's own blocks add to pub);
-//   parity p = s & 1 double-buffers data/red, which makes reuse safe: a rank can only
-//   write parity p again at step s+2 after it has seen every peer's step s+1 counters,
-//   and a peer reaches step s+1 only after finishing its step-s reads.
-//   phase 1  publish: copy my gradients into data[p]; fence; pub += 1 (per block)
-//   phase 2  reduce-scatter: block b of rank r sums chunk b of shard r over all ranks in
-//            rank order (deterministic), scales by 1/W, then either stores the mean
-//            (mode 0) or applies SGD to that chunk of the parameters (mode 1, ZeRO-1
-//            style: each parameter is updated by exactly one rank); writes the result into
-//            red[p]; fence; red += 1
-//   phase 3  all-gather: copy every other rank's red[p] chunks into the local output
-//            (mean gradients, or the updated parameters).
-// Every wait is bounded (wall clock): on timeout the kernel sets an error word and
-// drains instead of hanging; later launches see the error and skip the exchange.  The
-// Python side self-tests the path against torch.distributed.all_reduce at start-up and
-// falls back to RCCL when anything disagrees (parallel/xgmi.py).
+//     [flag1[W][nblk] | flag2[W][nblk] | stepc[nblk] | pad | recv[W][shard] | gath[npad]]
+//   shard = npad / W (rank q owns flat elements [q*shard, (q+1)*shard)),
+//   chunk = shard / nblk (block b of every rank handles chunk b of each shard).
+//   step s = ++stepc[b] (per block, local): flags hold step numbers, compared with >= s.
+//
+//   phase 1  produce + push: block b computes its balanced slice of the flat gradient
+//            (the conv segment reduced from the per-sample slabs in fixed row order, the
+//            rest copied) and stores every element into its OWNER's recv[my rank][.];
+//            fence; flag1[my rank][b] := s on every rank.
+//   phase 2  (owner) wait until flag1[*][*] >= s (local, lanes in parallel); chunk b of
+//            my shard = sum over senders in rank order (deterministic), scale 1/W; SGD on
+//            it (mode 1, ZeRO-1: each parameter is updated by exactly one rank) or the mean
+//            (mode 0); store the result locally and into every peer's gath[.]; fence;
+//            flag2[my rank][b] := s on every rank.
+//   phase 3  wait flag2[q][b] >= s for every q != me (local, one lane per owner), copy
+//            chunk b of every other shard from gath into the output / parameters.
+//
+// Single buffering is safe: a rank writes step s+1 data into a peer only after its whole
+// step-s launch finished, and that launch waited (phase 3) for every owner's flag2 of step
+// s, which each owner raises only after it finished reading its step-s recv chunk; gath
+// of step s+1 is written only after the owner saw flag1 of step s+1 from the receiver.
+//
+// Every wait is bounded (wall clock): on timeout the kernel sets an error word and goes
+// on without waiting; later launches see the error and fall back to a rank-local SGD
+// step (no remote traffic) instead of hanging.  The Python side self-tests the path
+// against torch.distributed.all_reduce at start-up and falls back to RCCL when anything
+// disagrees (parallel/xgmi.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,14 +48,19 @@
 
 namespace {
 
+// clang vector type: element-wise arithmetic stays in VGPRs (HIP's f4 wrapper makes
+// SROA give up on member references and spill to scratch)
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 constexpr int kMaxWorld = 8;
 constexpr int kThreads = 256;
-constexpr size_t kCtrBytes = 256;  // two counters on separate 128-B lines
+constexpr int kMaxBlocks = 256;
+constexpr size_t kHdrBytes = 64 * 1024;  // flag1 + flag2 + stepc (<= 2*8*256*4 + 1 KB)
 
 struct XarArgs {
   char* base[kMaxWorld];  // every rank's buffer (IPC-mapped; base[rank] is local)
   int rank, world, nblk, mode;
-  long n, npad, shard, chunk;
+  long n4, npad4, shard4, chunk4;
   const float* in;
   float* out;            // mode 0
   float* p;              // mode 1: parameters (updated in place)
@@ -48,35 +68,69 @@ struct XarArgs {
   float lr, momentum, dampening, wd, scale;
   int nesterov, first_step;
   int* step_counter;     // optional: advanced once per launch (the trainer's batch cursor)
-  // optional fused slab reduction: the first conv4 float4s of the published gradient are
+  // optional fused slab reduction: the first conv4 f4s of the gradient are
   // sum_{r < slab_rows} slab[r * slab_stride + .] (the conv backward's per-sample partials)
   const float* slab;
   int slab_rows;
   long slab_stride, conv4;
   int* err;
   long long timeout_ticks;  // wall_clock64 ticks (100 MHz)
+  unsigned long long* stamps;  // optional: 4 wall_clock64 stamps per (rank, block)
+  int light_fence;  // exchange buffers are uncached: no L2 writeback / invalidate needed
 };
 
-__device__ __forceinline__ unsigned long long* pub_ctr(char* b) {
-  return reinterpret_cast<unsigned long long*>(b);
+// Release before raising a flag / acquire after seeing one.  The exchange buffers are
+// allocated uncached (MTYPE UC), so their data never sits in any L2: draining this wave's
+// outstanding memory operations (s_waitcnt) orders them.  A system-scope fence would also
+// write back (buffer_wbl2) / invalidate (buffer_inv) the whole L2 of this XCD -- 10s of
+// us when the step's tensors are dirty in it -- and is kept only for cached fallbacks.
+__device__ __forceinline__ void release_fence(const XarArgs& a) {
+  if (a.light_fence) {
+    __builtin_amdgcn_s_waitcnt(0);  // every store of this wave acknowledged
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  } else {
+    __threadfence_system();
+  }
 }
-__device__ __forceinline__ unsigned long long* red_ctr(char* b) {
-  return reinterpret_cast<unsigned long long*>(b + 128);
-}
-__device__ __forceinline__ float* data_buf(char* b, long npad, int par) {
-  return reinterpret_cast<float*>(b + kCtrBytes) + (long)par * npad;
-}
-__device__ __forceinline__ float* red_buf(char* b, long npad, int par) {
-  return reinterpret_cast<float*>(b + kCtrBytes) + (long)(2 + par) * npad;
+__device__ __forceinline__ void acquire_fence(const XarArgs& a) {
+  if (a.light_fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  else __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
-__device__ __forceinline__ unsigned long long load_sys(const unsigned long long* p) {
+__device__ __forceinline__ unsigned* flag1(char* b, int nblk, int q, int blk) {
+  return reinterpret_cast<unsigned*>(b) + q * nblk + blk;
+}
+__device__ __forceinline__ unsigned* flag2(char* b, int nblk, int q, int blk) {
+  return reinterpret_cast<unsigned*>(b) + (kMaxWorld + q) * nblk + blk;
+}
+__device__ __forceinline__ unsigned* stepc(char* b, int nblk, int blk) {
+  return reinterpret_cast<unsigned*>(b) + 2 * kMaxWorld * nblk + blk;
+}
+__device__ __forceinline__ f4* recv_buf(char* b) {
+  return reinterpret_cast<f4*>(b + kHdrBytes);
+}
+__device__ __forceinline__ f4* gath_buf(char* b, long npad4) {
+  return reinterpret_cast<f4*>(b + kHdrBytes) + npad4;
+}
+
+// Buffer of rank q: a select chain over the kernel arguments (SGPR selects when q is
+// uniform) -- keeps the pointer in the global address space and `a` out of scratch.
+__device__ __forceinline__ char* peer(const XarArgs& a, int q) {
+  char* r = a.base[0];
+#pragma unroll
+  for (int k = 1; k < kMaxWorld; ++k) r = q == k ? a.base[k] : r;
+  return r;
+}
+
+__device__ __forceinline__ unsigned load_sys(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void store_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
-// Poll *p >= target; one lane.  Returns false (and flags the error) on timeout.
-__device__ bool wait_ge(const unsigned long long* p, unsigned long long target, long long deadline,
-                        int* err) {
+// Poll one local flag until >= target; false (error flagged) on timeout.
+__device__ bool wait_flag(const unsigned* p, unsigned target, long long deadline, int* err) {
   while (load_sys(p) < target) {
     if ((long long)wall_clock64() > deadline) {
       atomicOr(err, 1);
@@ -87,148 +141,234 @@ __device__ bool wait_ge(const unsigned long long* p, unsigned long long target, 
   return true;
 }
 
-__device__ __forceinline__ void sgd4(float4& pp, float4 g, float4& bb, const XarArgs& a) {
-  float* pe = &pp.x;
-  const float* ge = &g.x;
-  float* be = &bb.x;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float d = ge[e] * a.scale + a.wd * pe[e];
-    if (a.momentum != 0.f) {
-      be[e] = a.first_step ? d : a.momentum * be[e] + (1.f - a.dampening) * d;
-      d = a.nesterov ? d + a.momentum * be[e] : be[e];
+// torch.optim.SGD (momentum, dampening, weight decay, nesterov) on four elements
+__device__ __forceinline__ void sgd4(f4& p, f4 g, f4& m, const XarArgs& a, float scale) {
+  f4 d = g * scale + a.wd * p;
+  if (a.momentum != 0.f) {
+    m = a.first_step ? d : a.momentum * m + (1.f - a.dampening) * d;
+    d = a.nesterov ? d + a.momentum * m : m;
+  }
+  p -= a.lr * d;
+}
+
+// Element v (float4 units, v < npad4) of this rank's flat gradient outside the slab-reduced
+// conv segment.  Padding reads as zero.
+__device__ __forceinline__ f4 grad4(const XarArgs& a, long v) {
+  return v < a.n4 ? reinterpret_cast<const f4*>(a.in)[v] : f4{0.f, 0.f, 0.f, 0.f};
+}
+
+
+// Deposit gradient element v with the rank that owns it (or apply a local SGD step when
+// the exchange is degraded).
+__device__ __forceinline__ void deposit(const XarArgs& a, long v, f4 g, bool degraded) {
+  if (degraded) {
+    if (v >= a.n4) return;
+    if (a.mode == 0) {
+      reinterpret_cast<f4*>(a.out)[v] = g;
+    } else {
+      f4 pp = reinterpret_cast<f4*>(a.p)[v];
+      f4 bb = reinterpret_cast<f4*>(a.mbuf)[v];
+      sgd4(pp, g, bb, a, 1.f);
+      reinterpret_cast<f4*>(a.p)[v] = pp;
+      reinterpret_cast<f4*>(a.mbuf)[v] = bb;
     }
-    pe[e] -= a.lr * d;
+    return;
+  }
+  const int q = (int)((unsigned)v / (unsigned)a.shard4);  // npad4 < 2^31 (host-checked)
+  const long pos = v - (long)q * a.shard4;
+  recv_buf(peer(a, q))[(long)a.rank * a.shard4 + pos] = g;
+}
+
+// Wait until every flag in `f[idx]` (idx = tid, tid + kThreads, ... < nf) is >= target.
+// All of a thread's flags are loaded back to back (one local round trip per poll), the
+// block leaves together.  False (error flagged) on timeout.
+__device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long deadline, int* err) {
+  for (;;) {
+    int pending = 0;
+    for (int i = threadIdx.x; i < nf; i += kThreads) pending |= load_sys(f + i) < target;
+    if (!__syncthreads_or(pending)) return true;
+    if ((long long)wall_clock64() > deadline) {
+      if (threadIdx.x == 0) atomicOr(err, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 
-__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) {
-  __shared__ unsigned long long s_step;
-  __shared__ int s_ok;
-  const int tid = threadIdx.x, b = blockIdx.x;
-  char* mine = a.base[a.rank];
+constexpr int kP2 = 2;  // phase-2 elements per thread per batch
+constexpr int kP3 = 4;  // phase-3 float4s per thread per batch
+
+__device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
+  __shared__ unsigned s_step;
+  __shared__ int s_degraded;
+  __shared__ f4 part[kThreads];
+  const int tid = threadIdx.x;
+  char* mine = peer(a, a.rank);
   if (tid == 0) {
-    s_step = load_sys(pub_ctr(mine)) / (unsigned long long)a.nblk + 1ull;
-    s_ok = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    s_step = load_sys(stepc(mine, a.nblk, b)) + 1u;
+    s_degraded = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   }
   __syncthreads();
-  const unsigned long long s = s_step;
-  const int par = (int)(s & 1ull);
+  const unsigned s = s_step;
+  const bool degraded = s_degraded;
   const long long deadline = (long long)wall_clock64() + a.timeout_ticks;
-  const long n4 = a.n >> 2;  // n is a multiple of 4 (host-checked)
+  unsigned long long* st = a.stamps != nullptr ? a.stamps + ((long)a.rank * a.nblk + b) * 4 : nullptr;
+  if (st != nullptr && tid == 0) st[0] = wall_clock64();
+  const f4 zero4 = f4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- phase 1: publish my gradients (padding published as zeros).  With a slab, the
-  // conv segment is reduced here over the per-sample rows (fixed row order), spread over
-  // all blocks; the rest is copied from `in`.
+  // ---- phase 1: produce my gradient slice and push it to the owners
   {
-    float4* dst = reinterpret_cast<float4*>(data_buf(mine, a.npad, par));
-    const float4* src = reinterpret_cast<const float4*>(a.in);
     const long c4 = a.slab != nullptr ? a.conv4 : 0;
+    const long rest = a.npad4 - c4;
+    const long per = (rest + a.nblk - 1) / a.nblk;
+    const long lo4 = c4 + (long)b * per, hi4 = min(lo4 + per, a.npad4);
+    // first batch of the copied segment: loads in flight while the slab rows are summed
+    f4 g0, g1, g2, g3;
+    auto load_batch = [&](long v0) {
+      g0 = v0 < hi4 ? grad4(a, v0) : zero4;
+      g1 = v0 + kThreads < hi4 ? grad4(a, v0 + kThreads) : zero4;
+      g2 = v0 + 2 * kThreads < hi4 ? grad4(a, v0 + 2 * kThreads) : zero4;
+      g3 = v0 + 3 * kThreads < hi4 ? grad4(a, v0 + 3 * kThreads) : zero4;
+    };
+    load_batch(lo4 + tid);
     if (c4 > 0) {
-      __shared__ float4 part[kThreads];
-      const long per_c = (c4 + a.nblk - 1) / a.nblk;  // <= kThreads / 2 (host-checked)
-      const long col = (long)b * per_c + (tid % per_c);
-      const int half = tid / (int)per_c;              // 0 / 1: rows [0, R/2) / [R/2, R)
-      const int rh = (a.slab_rows + 1) / 2;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (half < 2 && col < c4 && (long)tid < 2 * per_c) {
-        const float4* sp = reinterpret_cast<const float4*>(a.slab) + col;
+      // conv segment: columns [b*per_c, (b+1)*per_c) reduced over the slab rows, split in
+      // nsplit row groups (fixed order -> deterministic)
+      const int per_c = (int)((c4 + a.nblk - 1) / a.nblk);  // <= kThreads (host-checked)
+      int nsplit = kThreads / per_c;
+      nsplit = nsplit < 1 ? 1 : (nsplit > 8 ? 8 : nsplit);
+      const int grp = tid / per_c, ci = tid - grp * per_c;
+      const long col = (long)b * per_c + ci;
+      const int rows_per = (a.slab_rows + nsplit - 1) / nsplit;
+      f4 acc = zero4;
+      if (grp < nsplit && col < c4) {
+        const f4* sp = reinterpret_cast<const f4*>(a.slab) + col;
         const long s4 = a.slab_stride >> 2;
-        const int r0 = half * rh, r1 = min(a.slab_rows, r0 + rh);
+        const int r0 = grp * rows_per, r1 = min(a.slab_rows, r0 + rows_per);
 #pragma unroll 8
-        for (int r = r0; r < r1; ++r) {
-          const float4 x = sp[(long)r * s4];
-          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
-        }
+        for (int r = r0; r < r1; ++r) acc += sp[(long)r * s4];
       }
       part[tid] = acc;
       __syncthreads();
-      if ((long)tid < per_c && col < c4) {
-        const float4 o = part[tid + per_c];
-        dst[col] = make_float4(acc.x + o.x, acc.y + o.y, acc.z + o.z, acc.w + o.w);
+      if (tid < per_c && col < c4) {
+        f4 gs = part[tid];
+        for (int k = 1; k < nsplit; ++k) gs += part[k * per_c + tid];
+        deposit(a, col, gs, degraded);
       }
     }
-    const long rest = a.npad / 4 - c4;
-    const long per = (rest + a.nblk - 1) / a.nblk;
-    const long lo4 = c4 + (long)b * per, hi4 = min(lo4 + per, a.npad / 4);
-    for (long v = lo4 + tid; v < hi4; v += kThreads)
-      dst[v] = v < n4 ? src[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-    __threadfence_system();
+    for (long v0 = lo4 + tid; v0 < hi4; v0 += 4 * kThreads) {
+      if (v0 != lo4 + tid) load_batch(v0);
+      deposit(a, v0, g0, degraded);
+      if (v0 + kThreads < hi4) deposit(a, v0 + kThreads, g1, degraded);
+      if (v0 + 2 * kThreads < hi4) deposit(a, v0 + 2 * kThreads, g2, degraded);
+      if (v0 + 3 * kThreads < hi4) deposit(a, v0 + 3 * kThreads, g3, degraded);
+    }
+    if (degraded) {
+      if (a.step_counter != nullptr && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
+      if (tid == 0) store_sys(stepc(mine, a.nblk, b), s);
+      return;
+    }
+    release_fence(a);
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(pub_ctr(mine), 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < a.world) store_sys(flag1(peer(a, tid), a.nblk, a.rank, b), s);
+    if (st != nullptr && tid == 0) st[1] = wall_clock64();
   }
 
-  // ---- phase 2: reduce-scatter (+ SGD) of chunk b of my shard
+  // ---- phase 2: reduce chunk b of my shard (+ SGD), push the result to every rank
   {
-    if (tid == 0) {
-      const unsigned long long target = (unsigned long long)a.nblk * s;
-      int ok = s_ok;
-      // every rank's publish, this one's included: the chunk this block reduces was
-      // published by whichever local block owned it in phase 1
-      for (int q = 0; q < a.world && ok; ++q) ok = wait_ge(pub_ctr(a.base[q]), target, deadline, a.err);
-      s_ok = ok;
-    }
-    __syncthreads();
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    const bool ok = s_ok;
-    const long lo4 = ((long)a.rank * a.shard + (long)b * a.chunk) >> 2;
-    const long hi4 = lo4 + (a.chunk >> 2);
-    float4* red = reinterpret_cast<float4*>(red_buf(mine, a.npad, par));
-    for (long v = lo4 + tid; v < hi4; v += kThreads) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
-        for (int q = 0; q < a.world; ++q) {  // fixed rank order: deterministic sums
-          const float4 x = reinterpret_cast<const float4*>(data_buf(a.base[q], a.npad, par))[v];
-          acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
-        }
-      } else {
-        acc = reinterpret_cast<const float4*>(data_buf(mine, a.npad, par))[v];  // degraded: local only
+    const long base4 = (long)a.rank * a.shard4 + (long)b * a.chunk4;
+    const f4* rv = recv_buf(mine) + (long)b * a.chunk4;
+    f4 pp[kP2], bb[kP2];
+    auto load_pb = [&](long i0) {  // parameters / momentum: independent of the peers
+#pragma unroll
+      for (int k = 0; k < kP2; ++k) {
+        const long i = i0 + (long)k * kThreads, v = base4 + i;
+        const bool in = a.mode == 1 && i < a.chunk4 && v < a.n4;
+        pp[k] = in ? reinterpret_cast<const f4*>(a.p)[v] : zero4;
+        bb[k] = in ? reinterpret_cast<const f4*>(a.mbuf)[v] : zero4;
       }
-      float4 res;
-      if (a.mode == 0) {
-        res = make_float4(acc.x * a.scale, acc.y * a.scale, acc.z * a.scale, acc.w * a.scale);
-        if (v < n4) reinterpret_cast<float4*>(a.out)[v] = res;
-      } else {
-        if (v < n4) {
-          float4 pp = reinterpret_cast<float4*>(a.p)[v];
-          float4 bb = reinterpret_cast<float4*>(a.mbuf)[v];
-          sgd4(pp, acc, bb, a);
-          reinterpret_cast<float4*>(a.p)[v] = pp;
-          reinterpret_cast<float4*>(a.mbuf)[v] = bb;
-          res = pp;
+    };
+    load_pb(tid);  // in flight while waiting
+    // every sender block's flag (or timed out: go on, the error is set); block-uniform
+    wait_flags(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err);
+    acquire_fence(a);
+    for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
+      f4 acc[kP2];
+#pragma unroll
+      for (int k = 0; k < kP2; ++k) {
+        const long i = i0 + (long)k * kThreads;
+        acc[k] = zero4;
+        if (i < a.chunk4)
+          for (int q = 0; q < a.world; ++q) acc[k] += rv[(long)q * a.shard4 + i];  // rank order
+      }
+#pragma unroll
+      for (int k = 0; k < kP2; ++k) {
+        const long i = i0 + (long)k * kThreads, v = base4 + i;
+        if (i >= a.chunk4) continue;
+        f4 res;
+        if (a.mode == 0) {
+          res = acc[k] * a.scale;
+          if (v < a.n4) reinterpret_cast<f4*>(a.out)[v] = res;
+        } else if (v < a.n4) {
+          sgd4(pp[k], acc[k], bb[k], a, a.scale);
+          reinterpret_cast<f4*>(a.p)[v] = pp[k];
+          reinterpret_cast<f4*>(a.mbuf)[v] = bb[k];
+          res = pp[k];
         } else {
-          res = make_float4(0.f, 0.f, 0.f, 0.f);
+          res = zero4;
+        }
+        for (int j = 1; j < a.world; ++j) {
+          const int q = a.rank + j < a.world ? a.rank + j : a.rank + j - a.world;
+          gath_buf(peer(a, q), a.npad4)[v] = res;
         }
       }
-      red[v] = res;
+      i0 += (long)kP2 * kThreads;
+      if (i0 >= a.chunk4) break;
+      load_pb(i0);
     }
-    __threadfence_system();
+    release_fence(a);
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(red_ctr(mine), 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < a.world && tid != a.rank) store_sys(flag2(peer(a, tid), a.nblk, a.rank, b), s);
+    if (st != nullptr && tid == 0) st[2] = wall_clock64();
   }
 
-  // ---- phase 3: all-gather chunk b of every other rank's shard
-  float* dst = a.mode == 0 ? a.out : a.p;
-  for (int k = 1; k < a.world; ++k) {
-    const int q = (a.rank + k) % a.world;
-    if (tid == 0) {
-      int ok = s_ok;
-      if (ok) ok = wait_ge(red_ctr(a.base[q]), (unsigned long long)a.nblk * s, deadline, a.err);
-      s_ok = ok;
+  // ---- phase 3: collect chunk b of every other shard
+  {
+    int ok = 1;
+    if (tid < a.world && tid != a.rank) ok = wait_flag(flag2(mine, a.nblk, tid, b), s, deadline, a.err);
+    (void)__syncthreads_and(ok);
+    acquire_fence(a);
+    f4* dst = reinterpret_cast<f4*>(a.mode == 0 ? a.out : a.p);
+    const f4* gb = gath_buf(mine, a.npad4);
+    const long tot = (long)(a.world - 1) * a.chunk4;
+    for (long j0 = tid; j0 < tot; j0 += (long)kP3 * kThreads) {
+      f4 x[kP3];
+      long vv[kP3];
+#pragma unroll
+      for (int k = 0; k < kP3; ++k) {
+        const long j = j0 + (long)k * kThreads;
+        const long kk = j / a.chunk4, i = j - kk * a.chunk4;
+        const int q = a.rank + 1 + (int)kk < a.world ? a.rank + 1 + (int)kk : a.rank + 1 + (int)kk - a.world;
+        vv[k] = j < tot ? (long)q * a.shard4 + (long)b * a.chunk4 + i : a.n4;
+        x[k] = vv[k] < a.n4 ? gb[vv[k]] : zero4;
+      }
+#pragma unroll
+      for (int k = 0; k < kP3; ++k)
+        if (vv[k] < a.n4) dst[vv[k]] = x[k];
     }
-    __syncthreads();
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    if (!s_ok) {
-      __syncthreads();
-      continue;
-    }
-    const long lo4 = ((long)q * a.shard + (long)b * a.chunk) >> 2;
-    const long hi4 = min(lo4 + (a.chunk >> 2), n4);
-    const float4* src = reinterpret_cast<const float4*>(red_buf(a.base[q], a.npad, par));
-    for (long v = lo4 + tid; v < hi4; v += kThreads) reinterpret_cast<float4*>(dst)[v] = src[v];
-    __syncthreads();  // s_ok is rewritten by lane 0 in the next round
   }
   if (a.step_counter != nullptr && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
+  if (tid == 0) store_sys(stepc(mine, a.nblk, b), s);
+  if (st != nullptr && tid == 0) st[3] = wall_clock64();
+}
+
+__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body(a, blockIdx.x); }
+
+// Emulation of `world` ranks on ONE device in one launch (blockIdx.y = rank): all blocks
+// of all ranks are co-resident, so the protocol (and its latency floor over local HBM)
+// can be tested at any world size on a single GPU.
+__global__ __launch_bounds__(kThreads) void xar_kernel_emu(const XarArgs* __restrict__ all) {
+  xar_body(all[blockIdx.y], blockIdx.x);
 }
 
 struct XarCtx {
@@ -250,7 +390,7 @@ extern "C" {
 int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void** ctx_out,
                    void* handle_out) {
   if (world < 2 || world > kMaxWorld || rank < 0 || rank >= world || n <= 0 || (n & 3) ||
-      nblk < 1 || nblk > 1024)
+      nblk < 1 || nblk > kMaxBlocks || n > (1L << 32))
     return -1;
   XarCtx* c = new XarCtx{};
   c->rank = rank;
@@ -259,7 +399,7 @@ int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void
   c->n = n;
   c->npad = round_up(n, (long)world * nblk * 4);
   hipGetDevice(&c->device);
-  const size_t bytes = kCtrBytes + (size_t)4 * c->npad * sizeof(float);
+  const size_t bytes = kHdrBytes + (size_t)2 * c->npad * sizeof(float);
   void* p = nullptr;
   const unsigned kinds[] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
   for (unsigned k : kinds) {
@@ -320,12 +460,13 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.rank = c->rank;
   a.world = c->world;
   a.nblk = c->nblk;
-  a.n = c->n;
-  a.npad = c->npad;
-  a.shard = c->npad / c->world;
-  a.chunk = a.shard / c->nblk;
+  a.n4 = c->n >> 2;
+  a.npad4 = c->npad >> 2;
+  a.shard4 = a.npad4 / c->world;
+  a.chunk4 = a.shard4 / c->nblk;
   a.err = c->err;
   a.timeout_ticks = c->timeout_ticks;
+  a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
   hipLaunchKernelGGL(xar_kernel, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
@@ -369,9 +510,135 @@ int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, 
     a.slab_rows = slab_rows;
     a.slab_stride = slab_stride;
     a.conv4 = conv_n >> 2;
-    if ((a.conv4 + c->nblk - 1) / c->nblk > kThreads / 2) return -1;  // one column pair per thread
+    if ((a.conv4 + c->nblk - 1) / c->nblk > kThreads) return -1;  // one column per thread
   }
   return launch(c, a, stream);
+}
+
+// ---- single-device emulation of `world` ranks (tests / latency floor) -------------------
+struct XarEmu {
+  int world, nblk;
+  long n, npad;
+  char* base[kMaxWorld];
+  int* err;         // one word per emulated rank
+  XarArgs* d_args;  // device copy of the per-rank arguments
+  long long timeout_ticks;
+  unsigned long long* stamps;
+  int light_fence;
+};
+
+// alloc_kind: 0 = uncached (as the multi-process path), 1 = fine-grained, 2 = hipMalloc.
+// fence: -1 = light iff uncached (as the multi-process path), 0 = system, 1 = light.
+int pto_xar_emu_create(int world, long n, int nblk, double timeout_s, int alloc_kind, int fence,
+                       void** ctx_out) {
+  if (world < 2 || world > kMaxWorld || n <= 0 || (n & 3) || nblk < 1 || nblk > kMaxBlocks ||
+      n > (1L << 32))
+    return -1;
+  XarEmu* e = new XarEmu{};
+  e->world = world;
+  e->nblk = nblk;
+  e->n = n;
+  e->npad = round_up(n, (long)world * nblk * 4);
+  const size_t bytes = kHdrBytes + (size_t)2 * e->npad * sizeof(float);
+  for (int q = 0; q < world; ++q) {
+    void* p = nullptr;
+    const hipError_t r = alloc_kind == 2 ? hipMalloc(&p, bytes)
+                         : hipExtMallocWithFlags(&p, bytes, alloc_kind == 1 ? hipDeviceMallocFinegrained
+                                                                            : hipDeviceMallocUncached);
+    if (r != hipSuccess) return -2;
+    if (hipMemset(p, 0, bytes) != hipSuccess) return -2;
+    e->base[q] = static_cast<char*>(p);
+  }
+  if (hipMalloc(&e->err, kMaxWorld * sizeof(int)) != hipSuccess) return -2;
+  if (hipMemset(e->err, 0, kMaxWorld * sizeof(int)) != hipSuccess) return -2;
+  if (hipMalloc(&e->d_args, kMaxWorld * sizeof(XarArgs)) != hipSuccess) return -2;
+  e->timeout_ticks = (long long)(timeout_s * 1e8);
+  e->light_fence = fence < 0 ? alloc_kind == 0 : fence;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  *ctx_out = e;
+  return 0;
+}
+
+long pto_xar_emu_npad(void* ctx) { return static_cast<XarEmu*>(ctx)->npad; }
+
+// Phase stamps (world x nblk x 4 uint64, wall_clock64 at 100 MHz) for the next emu_set.
+void pto_xar_emu_stamps(void* ctx, unsigned long long* buf) { static_cast<XarEmu*>(ctx)->stamps = buf; }
+
+// Per-rank tensors as arrays of `world` device addresses.  mode 0: dst = out (mean);
+// mode 1: dst = parameters, mbuf = momentum (SGD).  slab may be null.
+int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* dst, const long long* mbuf,
+                    const long long* slab, int slab_rows, long slab_stride, long conv_n, float lr,
+                    float momentum, float dampening, float wd, int nesterov, int first_step) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  XarArgs h[kMaxWorld];
+  for (int r = 0; r < e->world; ++r) {
+    XarArgs a{};
+    for (int q = 0; q < kMaxWorld; ++q) a.base[q] = q < e->world ? e->base[q] : nullptr;
+    a.rank = r;
+    a.world = e->world;
+    a.nblk = e->nblk;
+    a.mode = mode;
+    a.n4 = e->n >> 2;
+    a.npad4 = e->npad >> 2;
+    a.shard4 = a.npad4 / e->world;
+    a.chunk4 = a.shard4 / e->nblk;
+    a.in = reinterpret_cast<const float*>(in[r]);
+    if (mode == 0) {
+      a.out = reinterpret_cast<float*>(dst[r]);
+    } else {
+      a.p = reinterpret_cast<float*>(dst[r]);
+      a.mbuf = reinterpret_cast<float*>(mbuf[r]);
+    }
+    a.lr = lr;
+    a.momentum = momentum;
+    a.dampening = dampening;
+    a.wd = wd;
+    a.scale = 1.f / (float)e->world;
+    a.nesterov = nesterov;
+    a.first_step = first_step;
+    if (slab != nullptr) {
+      if (slab_rows <= 0 || (conv_n & 3) || (slab_stride & 3) || slab_stride < conv_n || conv_n > e->n)
+        return -1;
+      a.slab = reinterpret_cast<const float*>(slab[r]);
+      a.slab_rows = slab_rows;
+      a.slab_stride = slab_stride;
+      a.conv4 = conv_n >> 2;
+      if ((a.conv4 + e->nblk - 1) / e->nblk > kThreads) return -1;
+    }
+    a.err = e->err + r;
+    a.timeout_ticks = e->timeout_ticks;
+    a.stamps = e->stamps;
+    a.light_fence = e->light_fence;
+    h[r] = a;
+  }
+  if (hipMemcpy(e->d_args, h, e->world * sizeof(XarArgs), hipMemcpyHostToDevice) != hipSuccess) return -2;
+  return 0;
+}
+
+int pto_xar_emu_launch(void* ctx, void* stream) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  hipLaunchKernelGGL(xar_kernel_emu, dim3(e->nblk, e->world), dim3(kThreads), 0, (hipStream_t)stream,
+                     e->d_args);
+  return (int)hipGetLastError();
+}
+
+int pto_xar_emu_error(void* ctx) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  int v[kMaxWorld] = {};
+  if (hipMemcpy(v, e->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  int acc = 0;
+  for (int q = 0; q < e->world; ++q) acc |= v[q];
+  return acc;
+}
+
+int pto_xar_emu_destroy(void* ctx) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  (void)hipDeviceSynchronize();
+  for (int q = 0; q < e->world; ++q) (void)hipFree(e->base[q]);
+  (void)hipFree(e->err);
+  (void)hipFree(e->d_args);
+  delete e;
+  return 0;
 }
 
 int pto_xar_destroy(void* ctx) {

@@ -110,12 +110,17 @@ _SIGNATURES = {
     "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],
     "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _I, _L, _L, _VP],
     "pto_xar_destroy": [_VP],
+    "pto_xar_emu_create": [_I, _L, _I, ctypes.c_double, _I, _I, ctypes.POINTER(_VP)],
+    "pto_xar_emu_set": [_VP, _I, _VP, _VP, _VP, _VP, _I, _L, _L, _F, _F, _F, _F, _I, _I],
+    "pto_xar_emu_launch": [_VP, _VP],
+    "pto_xar_emu_error": [_VP],
+    "pto_xar_emu_destroy": [_VP],
     # rmsnorm.hip
     "pto_rmsnorm_fwd": [_VP, _VP, _VP, _VP, _L, _I, _F, _I, _VP],
     "pto_rmsnorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _L, _I, _I, _I, _VP],
 }
-_LONG_FNS = {"pto_xar_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I]}
-_VOID_FNS = {"pto_set_debug_buffer": [_VP]}
+_LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I]}
+_VOID_FNS = {"pto_set_debug_buffer": [_VP], "pto_xar_emu_stamps": [_VP, _VP]}
 
 
 def load(build_if_missing: bool = True):

@@ -4,10 +4,13 @@
 uncached device buffer through a HIP IPC handle, the handles are exchanged once over the
 process group, and each training step then runs ONE kernel per rank that
 
-1. publishes the rank's flat gradients into its buffer,
-2. reduces shard ``rank`` across all ranks (fixed rank order) and applies SGD to it,
-3. gathers every other shard's updated parameters from its owner.
+1. pushes every gradient element into the buffer of the rank that owns it (posted
+   stores over xGMI, then a step-numbered flag per sender block),
+2. reduces shard ``rank`` across all senders (fixed rank order) and applies SGD to it,
+   then pushes the updated parameters into every peer's buffer (+ a flag per chunk),
+3. copies the other shards' parameters from its own buffer once their flags arrive.
 
+Remote traffic is stores only and every wait polls local memory, one lane per flag.
 No host involvement per step, so the whole DDP step (forward, backward, all-reduce,
 optimizer) is one hipGraph.  This replaces the reference's implicit DDP all-reduce
 (examples/mnist/mnist.py:136-138 -> NCCL ring) with the direct two-shot exchange that
@@ -36,7 +39,7 @@ class XgmiUnavailable(RuntimeError):
 class XgmiAllReduce:
     """Rank-local handle on the shared exchange buffers (world 2..8, one GPU per rank)."""
 
-    def __init__(self, n: int, group=None, nblk: int = 64, timeout_s: float = 5.0,
+    def __init__(self, n: int, group=None, nblk: int = 128, timeout_s: float = 5.0,
                  device: Optional[torch.device] = None):
         if not dist.is_initialized():
             raise XgmiUnavailable("needs an initialised process group")
@@ -170,6 +173,74 @@ class XgmiAllReduce:
     def close(self) -> None:
         if self._ctx:
             self.lib.pto_xar_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class XgmiEmulation:
+    """``world`` ranks of the same kernel on ONE device in one launch (grid.y = rank).
+
+    Every block of every emulated rank is co-resident, so the protocol runs exactly as on
+    a node (flags, pushes, step counters, bounded waits) with local HBM in place of the
+    xGMI links: a world-8 correctness test and the protocol's latency floor on a 1-GPU box.
+    """
+
+    def __init__(self, world: int, n: int, nblk: int = 128, timeout_s: float = 2.0, alloc_kind: int = 0,
+                 fence: int = -1):
+        self.lib = _native.load()
+        self.world, self.n = int(world), int(n)
+        self._ctx = ctypes.c_void_p()
+        rc = self.lib.pto_xar_emu_create(self.world, self.n, nblk, timeout_s, alloc_kind, fence,
+                                         ctypes.byref(self._ctx))
+        if rc != 0:
+            self._ctx = None
+            raise XgmiUnavailable(f"pto_xar_emu_create failed ({rc})")
+        self.npad = int(self.lib.pto_xar_emu_npad(self._ctx))
+        self.nblk = nblk
+        self.stamps = None
+
+    def enable_stamps(self) -> torch.Tensor:
+        """Per (rank, block): wall_clock64 at start / flags1 sent / flags2 sent / end (call
+        before ``configure``)."""
+        self.stamps = torch.zeros(self.world * self.nblk * 4, dtype=torch.int64, device="cuda")
+        self.lib.pto_xar_emu_stamps(self._ctx, ctypes.c_void_p(self.stamps.data_ptr()))
+        return self.stamps
+
+    def _ptrs(self, ts):
+        if ts is None:
+            return None
+        assert len(ts) == self.world
+        return (ctypes.c_longlong * self.world)(*[t.data_ptr() for t in ts])
+
+    def configure(self, mode: int, inputs, dst, mbuf=None, slab=None, slab_rows: int = 0, conv_n: int = 0,
+                  lr: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                  nesterov: bool = False, first_step: bool = False) -> None:
+        for t in list(inputs) + list(dst) + list(mbuf or []):
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == self.n
+                    and t.data_ptr() % 16 == 0):
+                raise ValueError(f"expected aligned contiguous fp32 CUDA tensors of {self.n} elements")
+        stride = slab[0].shape[1] if slab is not None else 0
+        self._keep = (inputs, dst, mbuf, slab)  # the kernel holds raw pointers
+        _native.check(self.lib.pto_xar_emu_set(
+            self._ctx, int(mode), self._ptrs(inputs), self._ptrs(dst), self._ptrs(mbuf), self._ptrs(slab),
+            int(slab_rows), int(stride), int(conv_n), lr, momentum, dampening, weight_decay,
+            int(nesterov), int(first_step)), "pto_xar_emu_set")
+
+    def launch(self) -> None:
+        _native.check(self.lib.pto_xar_emu_launch(
+            self._ctx, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "pto_xar_emu_launch")
+
+    def error(self) -> int:
+        return int(self.lib.pto_xar_emu_error(self._ctx))
+
+    def close(self) -> None:
+        if self._ctx:
+            self.lib.pto_xar_emu_destroy(self._ctx)
             self._ctx = None
 
     def __del__(self):

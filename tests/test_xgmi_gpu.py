@@ -1,6 +1,6 @@
 """xGMI peer-memory all-reduce + fused SGD (csrc/kernels/xgmi_allreduce.hip).
 
-Two ranks on the box's GPU(s) run tools/xgmi_check.py: the kernel must agree with
+2 and 4 ranks on the box's GPU(s) run tools/xgmi_check.py: the kernel must agree with
 torch.distributed.all_reduce, the fused-SGD DDP step must match the RCCL/gloo path, and
 graph-captured steps must keep the replicas bit-identical.
 """
@@ -23,14 +23,15 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_xgmi_allreduce_two_ranks(tmp_path):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_ranks(tmp_path, world):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
            "--backend", "gloo", "--out", str(tmp_path)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=dict(os.environ, PYTHONPATH=str(ROOT)))
-    results = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(2)
+    results = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(world)
                if (tmp_path / f"rank{k}.json").exists()]
-    assert r.returncode == 0 and len(results) == 2, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0 and len(results) == world, r.stdout[-3000:] + r.stderr[-3000:]
     for res in results:
         assert res["all_ok"], res

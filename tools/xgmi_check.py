@@ -18,11 +18,44 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _bench_exchange(xar, tr, dev, launches: int = 50, reps: int = 5) -> dict:
+    """us per fused exchange launch (slab reduce + push + reduce-scatter/SGD + all-gather),
+    back-to-back in one graph, MAX over ranks; on a shared GPU this bounds the protocol's
+    latency floor, not the xGMI fabric's."""
+    import time
+    import torch
+    import torch.distributed as dist
+    p, m, g = tr.flat_params.clone(), tr.flat_momentum.clone(), tr.flat_grads.clone()
+    slab, B, ce = tr.conv_slab, tr.B, tr.layout.conv_end
+
+    def body():
+        for _ in range(launches):
+            xar.allreduce_sgd_(g, p, m, lr=0.0, momentum=0.5, slab=slab, slab_rows=B, conv_n=ce)
+    body()
+    torch.cuda.synchronize(dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        body()
+    best = float("inf")
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        best = min(best, float(t.item()))
+    return {"per_launch_us": round(best / launches * 1e6, 2), "launches": launches}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--out", default=None, help="also write <out>/rank<r>.json")
+    ap.add_argument("--bench", action="store_true",
+                    help="time the fused exchange alone (graph of back-to-back launches)")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -83,6 +116,8 @@ def main(argv=None) -> int:
         res[f"handover_{force}_in_sync"] = bool(torch.equal(ref, ta.flat_params)) and (
             force == "xgmi" or bool(torch.equal(mref, ta.flat_momentum)))
         res[f"handover_{force}_times"] = times
+    if a.bench:
+        res["exchange_us"] = _bench_exchange(xar, ta, dev)
     res["kernel_error"] = xar.error()
     ok = res["self_test"] and res["eager_match"] and res["graph_in_sync"] and res["finite"] \
         and res["kernel_error"] == 0 and res["handover_rccl_in_sync"] and res["handover_xgmi_in_sync"]

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Latency anatomy of the xGMI push all-reduce, emulated on one GPU (grid.y = rank).
+
+For each buffer allocation kind and world size: us per fused launch (graph of 50
+back-to-back launches) and, for one stamped launch, the mean/max per-block phase times
+(produce+push | wait flags1 + reduce/SGD + push | wait flags2 + gather) and the span.
+Prints one JSON line per configuration.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> int:
+    import torch
+    from pytorch_operator_amd.models.mnist import flat_layout
+    from pytorch_operator_amd.parallel.xgmi import XgmiEmulation
+
+    dev = torch.device("cuda", 0)
+    L, ce, B = flat_layout().total, flat_layout().conv_end, 64
+    kinds = [int(k) for k in os.environ.get("XAR_KINDS", "0,1,2").split(",")]
+    worlds = [int(w) for w in os.environ.get("XAR_WORLDS", "2,8").split(",")]
+    nblks = [int(b) for b in os.environ.get("XAR_NBLK", "128").split(",")]
+    fences = [int(f) for f in os.environ.get("XAR_FENCE", "-1").split(",")]
+    for kind, fence in [(k, f) for k in kinds for f in fences]:
+        for world in worlds:
+            for nblk in nblks:
+                emu = XgmiEmulation(world, L, nblk=nblk, alloc_kind=kind, fence=fence)
+                ps = [torch.zeros(L, device=dev) for _ in range(world)]
+                ms = [torch.zeros(L, device=dev) for _ in range(world)]
+                grads = [torch.randn(L, device=dev) for _ in range(world)]
+                slabs = [torch.randn(B, ce, device=dev) for _ in range(world)]
+                cfg = dict(slab=slabs, slab_rows=B, conv_n=ce, lr=0.0, momentum=0.5)
+                emu.configure(1, grads, ps, ms, **cfg)
+                emu.launch()
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    for _ in range(50):
+                        emu.launch()
+                best = float("inf")
+                for _ in range(5):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    graph.replay()
+                    torch.cuda.synchronize()
+                    best = min(best, time.perf_counter() - t0)
+                st = emu.enable_stamps()
+                emu.configure(1, grads, ps, ms, **cfg)
+                for _ in range(3):
+                    emu.launch()
+                torch.cuda.synchronize()
+                s = st.view(world, nblk, 4).double().cpu() / 100.0  # us (100 MHz)
+                t0 = s[..., 0].min()
+                ph = s[..., 1:] - s[..., :-1]
+                res = {"alloc_kind": kind, "fence": fence, "world": world, "nblk": nblk,
+                       "us_per_launch": round(best / 50 * 1e6, 2),
+                       "span_us": round(float(s[..., 3].max() - t0), 2),
+                       "start_skew_us": round(float(s[..., 0].max() - t0), 2),
+                       "phase_mean_us": [round(float(x), 2) for x in ph.mean((0, 1))],
+                       "phase_max_us": [round(float(x), 2) for x in ph.amax((0, 1))],
+                       "error": emu.error()}
+                print(json.dumps(res), flush=True)
+                emu.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
