@@ -122,6 +122,15 @@ __device__ __forceinline__ char* peer(const XarArgs& a, int q) {
   return r;
 }
 
+// Posted store into a peer's buffer, written through to memory (sc0 sc1 = system scope)
+// whatever MTYPE the importing GPU's page tables give the IPC mapping of a REMOTE device's
+// buffer: the light fence below (s_waitcnt only) is then enough on every fabric, not just
+// for the uncached local allocation the 1-GPU tests exercise.  A 16-B write-through store
+// costs about what a plain one does (MI355X_MICROARCH.md, hand-off price list).
+__device__ __forceinline__ void push4(f4* p, f4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
 __device__ __forceinline__ unsigned load_sys(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -176,7 +185,7 @@ __device__ __forceinline__ void deposit(const XarArgs& a, long v, f4 g, bool deg
   }
   const int q = (int)((unsigned)v / (unsigned)a.shard4);  // npad4 < 2^31 (host-checked)
   const long pos = v - (long)q * a.shard4;
-  recv_buf(peer(a, q))[(long)a.rank * a.shard4 + pos] = g;
+  push4(recv_buf(peer(a, q)) + (long)a.rank * a.shard4 + pos, g);
 }
 
 // Wait until every flag in `f[idx]` (idx = tid, tid + kThreads, ... < nf) is >= target.
@@ -319,7 +328,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
         }
         for (int j = 1; j < a.world; ++j) {
           const int q = a.rank + j < a.world ? a.rank + j : a.rank + j - a.world;
-          gath_buf(peer(a, q), a.npad4)[v] = res;
+          push4(gath_buf(peer(a, q), a.npad4) + v, res);
         }
       }
       i0 += (long)kP2 * kThreads;
@@ -398,7 +407,10 @@ int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void
   c->nblk = nblk;
   c->n = n;
   c->npad = round_up(n, (long)world * nblk * 4);
-  hipGetDevice(&c->device);
+  if (hipGetDevice(&c->device) != hipSuccess) {
+    delete c;
+    return -2;
+  }
   const size_t bytes = kHdrBytes + (size_t)2 * c->npad * sizeof(float);
   void* p = nullptr;
   const unsigned kinds[] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
@@ -417,15 +429,24 @@ int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void
     }
     c->alloc_kind = 0;
   }
-  hipMemset(p, 0, bytes);
   c->base[rank] = static_cast<char*>(p);
-  if (hipMalloc(&c->err, sizeof(int)) != hipSuccess) return -2;
-  hipMemset(c->err, 0, sizeof(int));
-  c->timeout_ticks = (long long)(timeout_s * 1e8);  // wall_clock64 runs at 100 MHz
   hipIpcMemHandle_t h;
-  if (hipIpcGetMemHandle(&h, p) != hipSuccess) return -3;
+  int rc = 0;
+  if (hipMemset(p, 0, bytes) != hipSuccess || hipMalloc(&c->err, sizeof(int)) != hipSuccess ||
+      hipMemset(c->err, 0, sizeof(int)) != hipSuccess)
+    rc = -2;
+  else if (hipIpcGetMemHandle(&h, p) != hipSuccess)
+    rc = -3;
+  else if (hipDeviceSynchronize() != hipSuccess)
+    rc = -2;
+  if (rc != 0) {
+    (void)hipFree(c->err);
+    (void)hipFree(p);
+    delete c;
+    return rc;
+  }
+  c->timeout_ticks = (long long)(timeout_s * 1e8);  // wall_clock64 runs at 100 MHz
   memcpy(handle_out, &h, sizeof(h));
-  hipDeviceSynchronize();
   *ctx_out = c;
   return 0;
 }
@@ -451,7 +472,7 @@ int pto_xar_open(void* ctx, const void* handles) {
 int pto_xar_error(void* ctx) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
   int v = 0;
-  hipMemcpy(&v, c->err, sizeof(int), hipMemcpyDeviceToHost);
+  if (hipMemcpy(&v, c->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return v;
 }
 
@@ -643,13 +664,13 @@ int pto_xar_emu_destroy(void* ctx) {
 
 int pto_xar_destroy(void* ctx) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
-  hipDeviceSynchronize();
+  (void)hipDeviceSynchronize();
   for (int q = 0; q < c->world; ++q) {
     if (q == c->rank || c->base[q] == nullptr) continue;
-    hipIpcCloseMemHandle(c->base[q]);
+    (void)hipIpcCloseMemHandle(c->base[q]);
   }
-  hipFree(c->base[c->rank]);
-  hipFree(c->err);
+  (void)hipFree(c->base[c->rank]);
+  (void)hipFree(c->err);
   delete c;
   return 0;
 }
