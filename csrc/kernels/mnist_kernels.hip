@@ -199,6 +199,9 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   stamp(dbg, 0);
   const float* src = a1 + (size_t)b * 2880;
+  // epilogue bias, loaded now so the tail after the last barrier has no memory round trip
+  const int co_pre = cg * 16 + (tid & 15);
+  const float bco = co_pre < 50 ? bias[co_pre] : 0.f;
 #pragma unroll
   for (int k = 0; k < (2880 + AB_NT - 1) / AB_NT; ++k) {
     const int e = tid + k * AB_NT;
@@ -230,7 +233,6 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
   stamp(dbg, 2);
   if (wv >= 4) return;
   const int co = cg * 16 + i;
-  const float bco = (co < 50) ? bias[co] : 0.f;
   // reg r of this lane = conv position (oh = 2pt + (g>>1), ow = 4(g&1) + r)
   const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
   float mA = v0; int aA = 0;
@@ -331,6 +333,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   stamp(dbg, 0);
   const int row = batch_row(src, b, B);
   const bool pub = cg == 0;
+  // conv2 epilogue bias, loaded with the staging loads (no round trip after the last barrier)
+  const int co_pre = cg * 16 + (tid & 15);
+  const float bco = co_pre < 50 ? bias[co_pre] : 0.f;
   {
     const float x0 = load_px(src, row, min(tid, 783));
     const float wv = w1[min(tid, 499)];
@@ -389,9 +394,15 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     // 72 tasks = 36 position tiles x 2 channel tiles; wave w takes tasks w, w+16, ..
     // (5 for w < 8, 4 otherwise: 18 per SIMD) as independent accumulator chains
     // (MFMA latency > issue interval: one chain alone would idle the matrix pipe).
+#ifdef PTO_EXP_NO_TILE1  // experiment: channel tile 1 (odd waves) skipped
+    if (!(wv & 1)) {
+#endif
     conv1_tasks<3>(wv, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
     if (wv < 8) conv1_tasks<2>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
     else conv1_tasks<1>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
+#ifdef PTO_EXP_NO_TILE1
+    }
+#endif
   }
   __syncthreads();
   stamp(dbg, 2);
@@ -402,7 +413,6 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   stamp(dbg, 3);
   if (wv >= 4) return;
   const int co = cg * 16 + i;
-  const float bco = (co < 50) ? bias[co] : 0.f;
   const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
   float mA = v0; int aA = 0;
   if (v1 > mA) { mA = v1; aA = 1; }
@@ -446,6 +456,10 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
   float4 av[5], bv[5];
 #pragma unroll
   for (int s = 0; s < 5; ++s) { av[s] = xa[s]; bv[s] = wb[s]; }
+  // epilogue operands of thread tid < 256, in flight with the GEMM loads
+  const int l_e = tid >> 2, r_e = tid & 3;
+  const int orow = mt * 16 + (l_e >> 4) * 4 + r_e, ocol = nt * 16 + (l_e & 15);
+  const float bo = (tid < 256 && ocol < 500) ? bias[ocol] : 0.f;
   f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
   for (int s = 0; s < 5; ++s) {
@@ -463,12 +477,10 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
   __syncthreads();
   stamp(dbg, 1);
   if (tid < 256) {
-    const int l = tid >> 2, r = tid & 3;
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < 10; ++q) s += red[q][l][r];
-    const int orow = mt * 16 + (l >> 4) * 4 + r, ocol = nt * 16 + (l & 15);
-    if (orow < B && ocol < 500) h[(size_t)orow * 500 + ocol] = fmaxf(s + bias[ocol], 0.f);
+    for (int q = 0; q < 10; ++q) s += red[q][l_e][r_e];
+    if (orow < B && ocol < 500) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
   }
 }
 
@@ -479,16 +491,20 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
 // first.  Per-sample (loss, correct) go to per_sample[b] (reduced later by
 // fc1_bwd, deterministic); eval callers may instead accumulate into `stats`
 // (one atomic per block after an LDS reduction).
+// WPB waves per block: the training path (B = 64) runs one wave per block so the
+// 20 KB W2 stream of each sample lands on its own CU (4 waves per block put 80 KB of
+// L2 traffic on each of 16 CUs); the eval path (B = 1000) keeps 4 to cut the atomics.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void head_kernel(
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void head_kernel(
     const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
     const int* __restrict__ lab, int B, float grad_scale, float loss_scale,
     float* __restrict__ dlogits, float* __restrict__ dh, float* __restrict__ logp_out,
     float* __restrict__ per_sample, float* __restrict__ stats, u64* dbg) {
-  __shared__ float red[2][4];
+  __shared__ float red[2][WPB];
   const int tid = threadIdx.x, lane = tid & 63, wq = tid >> 6;
   stamp(dbg, 0);
-  const int b = blockIdx.x * 4 + wq;
+  const int b = blockIdx.x * WPB + wq;
   const bool bvalid = b < B;
   const int bc = bvalid ? b : B - 1;
   const int t = lab[bc];
@@ -546,8 +562,11 @@ __global__ __launch_bounds__(256) void head_kernel(
     }
     __syncthreads();
     if (tid == 0) {
-      atomicAdd(&stats[0], red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-      atomicAdd(&stats[1], red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+      float sl = 0.f, sc = 0.f;
+#pragma unroll
+      for (int q = 0; q < WPB; ++q) { sl += red[0][q]; sc += red[1][q]; }
+      atomicAdd(&stats[0], sl);
+      atomicAdd(&stats[1], sc);
     }
   }
   if (!bvalid) return;
@@ -579,34 +598,41 @@ __global__ __launch_bounds__(256) void head_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// E: fc1 backward, three independent jobs in one launch (blockDim 256):
-//   job 1 (400 blocks x 4 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B,
+// E: fc1 backward, three independent jobs in one launch (blockDim 512 = 8 waves):
+//   job 1 (200 blocks x 8 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B,
 //          64 samples per register-preloaded chunk), db_fc1 from the kt==0 tiles.
 //          Written, not accumulated: no zeroing needed.
-//   job 2 (ceil(B/16)*50 blocks): da2[B,800] = dh . W_fc1 (K = 500 split over 4
-//          waves, operands preloaded, LDS reduce); the epilogue un-pools through
-//          idx2 and applies the ReLU mask, writing the full dz2[B,50,8,8].
-//   job 3 (8 blocks): dW_fc2[10,500] = dlogits^T . h (MFMA, K = B), db_fc2, and
+//   job 2 (ceil(B/16)*50 blocks): da2[B,800] = dh . W_fc1 (K = 500 split over 8
+//          waves, 16 steps = 32 loads per lane: within the 63 outstanding loads vmcnt
+//          can track, so every load is in flight at once; LDS reduce); the epilogue
+//          un-pools through idx2 and applies the ReLU mask, writing dz2[B,50,8,8].
+//          This job is the critical path into the conv backward.
+//   job 3 (4 blocks): dW_fc2[10,500] = dlogits^T . h (MFMA, K = B), db_fc2, and
 //          the step's loss statistics from the head's per-sample values.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fc1_bwd_kernel(
+constexpr int E_NT = 512;
+constexpr int E_NW = E_NT / 64;
+constexpr int E_NJ1 = 1600 / E_NW;  // job-1 blocks
+constexpr int E_NJ3 = 32 / E_NW;    // job-3 blocks
+
+__global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
     const float* __restrict__ dh, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
     const float* __restrict__ w1, const float* __restrict__ dlog, const float* __restrict__ h,
     float* __restrict__ gw1, float* __restrict__ gb1, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ dz2, const float* __restrict__ per_sample,
     float* __restrict__ stats, float loss_scale, int jobs, int B, u64* dbg) {
-  __shared__ f32x4 red[4][64];
+  __shared__ f32x4 red[E_NW][64];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   // jobs bit0: dW_fc1/db_fc1, bit1: dz2, bit2: dW_fc2/db_fc2/stats.  Block ids are
   // laid out job1 | job2 | job3 with absent jobs taking no blocks.
-  const int nJ1 = (jobs & 1) ? 400 : 0;
+  const int nJ1 = (jobs & 1) ? E_NJ1 : 0;
   const int nJ2 = (jobs & 2) ? ((B + 15) / 16) * 50 : 0;
   const int blk = blockIdx.x;
   stamp(dbg, 0);
   if (blk < nJ1) {
-    const int tile = blk * 4 + wv;
+    const int tile = blk * E_NW + wv;
     const int nt = tile / 50, kt = tile - nt * 50;
     const int n = nt * 16 + i, f = kt * 16 + i;
     const bool nv = n < 500;
@@ -649,32 +675,38 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const bool rv = row < B;
     const int rc = rv ? row : B - 1;
     const int f = kt * 16 + i;
-    const int s0 = wv * 32;  // steps [s0, s0+32) of 125 (wave 3: 29 valid)
-    float av[32], bv[32];
+    const int s0 = wv * 16;  // steps [s0, s0+16) of 125 (wave 7: 13 valid)
+    float av[16], bv[16];
 #pragma unroll
-    for (int s = 0; s < 32; ++s) {
+    for (int s = 0; s < 16; ++s) {
       const int k = min(4 * (s0 + s) + g, 499);
       av[s] = dh[(size_t)rc * 500 + k];
       bv[s] = w1[(size_t)k * 800 + f];
     }
+    // epilogue operands of threads tid < 256 (ReLU mask + pool argmax), in flight with
+    // the GEMM loads
+    const int l = (tid & 255) >> 2, r = tid & 3;
+    const int bs = mt * 16 + (l >> 4) * 4 + r;
+    const int ff = kt * 16 + (l & 15);
+    const size_t o = (size_t)min(bs, B - 1) * 800 + ff;
+    float a2o = a2[o];
+    int p = idx2[o];
     f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
-    for (int s = 0; s < 32; ++s) {
+    for (int s = 0; s < 16; ++s) {
       const bool kv = (s0 + s) < 125;
       const float a = (rv && kv) ? av[s] : 0.f;
       if (s & 1) c1 = mfma16x16x4(a, bv[s], c1);
       else c0 = mfma16x16x4(a, bv[s], c0);
     }
+    asm volatile("" : "+v"(a2o), "+v"(p));  // keep the epilogue loads above the barrier
     red[wv][lane] = c0 + c1;
     __syncthreads();
-    const int l = tid >> 2, r = tid & 3;
-    const float v = red[0][l][r] + red[1][l][r] + red[2][l][r] + red[3][l][r];
-    const int bs = mt * 16 + (l >> 4) * 4 + r;
-    const int ff = kt * 16 + (l & 15);
-    if (bs < B) {
-      const size_t o = (size_t)bs * 800 + ff;
-      const float d = a2[o] > 0.f ? v : 0.f;
-      const int p = idx2[o];
+    float v = red[0][l][r];
+#pragma unroll
+    for (int q = 1; q < E_NW; ++q) v += red[q][l][r];
+    if (tid < 256 && bs < B) {
+      const float d = a2o > 0.f ? v : 0.f;
       const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
       float* z = dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
       z[0] = p == 0 ? d : 0.f;
@@ -684,10 +716,14 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     }
   } else {
     // dW_fc2[10,500] = dlogits^T . h : M = 10 (16), N = 500 (32 tiles), K = B
-    const int nt = (blk - nJ1 - nJ2) * 4 + wv;  // 0..31
+    const int nt = (blk - nJ1 - nJ2) * E_NW + wv;  // 0..31
     const int jc = min(i, 9);
     const int n = nt * 16 + i;
     const int ncl = min(n, 499);
+    // loss statistics (wave nt == 1): the first 64 samples' values, in flight with the GEMM loads
+    const bool do_stats = nt == 1 && per_sample != nullptr && stats != nullptr;
+    float ls = 0.f, cs = 0.f;
+    if (do_stats && lane < B) { ls = per_sample[2 * lane]; cs = per_sample[2 * lane + 1]; }
     f32x4 c0 = zero4(), c1 = zero4();
     float dbsum = 0.f;
     for (int base = 0; base < B; base += 64) {
@@ -721,9 +757,8 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
       dbsum += __shfl_xor(dbsum, 32, 64);
       if (g == 0 && i < 10) gb2[i] = dbsum;
     }
-    if (nt == 1 && per_sample != nullptr && stats != nullptr) {
-      float ls = 0.f, cs = 0.f;
-      for (int bb = lane; bb < B; bb += 64) { ls += per_sample[2 * bb]; cs += per_sample[2 * bb + 1]; }
+    if (do_stats) {
+      for (int bb = lane + 64; bb < B; bb += 64) { ls += per_sample[2 * bb]; cs += per_sample[2 * bb + 1]; }
       ls = wave_sum(ls);
       cs = wave_sum(cs);
       if (lane == 0) { stats[0] = ls * loss_scale; stats[1] = cs; }
@@ -1256,9 +1291,13 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
                    float* per_sample, float* stats, void* stream) {
   PTO_CHECK_B(B);
   if (lab == nullptr) return -1;
-  hipLaunchKernelGGL(head_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, w2,
-                     b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats,
-                     g_dbg);
+  if (stats == nullptr)
+    hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(64), 0, (hipStream_t)stream, h, w2, b2, lab,
+                       B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, g_dbg);
+  else
+    hipLaunchKernelGGL(head_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h,
+                       w2, b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample,
+                       stats, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -1268,9 +1307,9 @@ int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, con
                       float loss_scale, int jobs, int B, void* stream) {
   PTO_CHECK_B(B);
   if (jobs <= 0 || jobs > 7) return -1;
-  const int blocks = ((jobs & 1) ? 400 : 0) + ((jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
-                     ((jobs & 4) ? 8 : 0);
-  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dh, a2,
+  const int blocks = ((jobs & 1) ? E_NJ1 : 0) + ((jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
+                     ((jobs & 4) ? E_NJ3 : 0);
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, dh, a2,
                      idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, per_sample, stats, loss_scale,
                      jobs, B, g_dbg);
   return (int)hipGetLastError();

@@ -131,11 +131,13 @@ def load(build_if_missing: bool = True):
     with _lock:
         if _lib is not None:
             return _lib
-        if build_if_missing:
+        # PTO_HIP_LIB: load a prebuilt variant instead (kernel A/B experiments, tools/exp_*.sh)
+        path = Path(os.environ["PTO_HIP_LIB"]) if os.environ.get("PTO_HIP_LIB") else _LIB_PATH
+        if build_if_missing and path == _LIB_PATH:
             build()
-        if not _LIB_PATH.exists():
-            raise NativeLibraryError(f"{_LIB_PATH} missing; run pytorch_operator_amd.ops.build()")
-        lib = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        if not path.exists():
+            raise NativeLibraryError(f"{path} missing; run pytorch_operator_amd.ops.build()")
+        lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         for name, argtypes in _SIGNATURES.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes
@@ -153,7 +155,7 @@ def load(build_if_missing: bool = True):
 
 
 def library_path() -> Path:
-    return _LIB_PATH
+    return Path(os.environ["PTO_HIP_LIB"]) if os.environ.get("PTO_HIP_LIB") else _LIB_PATH
 
 
 def check(rc: int, what: str) -> None:
