@@ -436,8 +436,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
 // ---------------------------------------------------------------------------
 // C: fc1 forward: h = relu(x[B,800] . W[500,800]^T + b).
 //   grid = (32 N-tiles, ceil(B/16) M-tiles), 10 waves; wave w reduces K range
-//   [80w, 80w+80), lane group g owns k = 80w + 20g + [0,20) (5 float4 loads per
-//   operand, all issued before the first MFMA); the ten partial tiles are summed
+//   [80w, 80w+80); lane group g owns k = 80w + 16s + 4g + [0,4), s < 5 (5 float4
+//   loads per operand, all issued before the first MFMA; the four lane groups of a
+//   row read one contiguous 64 B segment per load); the ten partial tiles are summed
 //   through LDS and the bias+ReLU epilogue is applied once.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(640) void fc1_fwd_kernel(
@@ -450,12 +451,12 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
   const int i = lane & 15, g = lane >> 4;
   const int row = mt * 16 + i, col = nt * 16 + i;
   const bool rv = row < B, cv = col < 500;
-  const int k0 = wv * 80 + g * 20;
+  const int k0 = wv * 80 + g * 4;
   const float4* xa = reinterpret_cast<const float4*>(x + (size_t)(rv ? row : B - 1) * 800 + k0);
   const float4* wb = reinterpret_cast<const float4*>(w + (size_t)(cv ? col : 499) * 800 + k0);
   float4 av[5], bv[5];
 #pragma unroll
-  for (int s = 0; s < 5; ++s) { av[s] = xa[s]; bv[s] = wb[s]; }
+  for (int s = 0; s < 5; ++s) { av[s] = xa[4 * s]; bv[s] = wb[4 * s]; }
   // epilogue operands of thread tid < 256, in flight with the GEMM loads
   const int l_e = tid >> 2, r_e = tid & 3;
   const int orow = mt * 16 + (l_e >> 4) * 4 + r_e, ocol = nt * 16 + (l_e & 15);
@@ -508,17 +509,29 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
   const bool bvalid = b < B;
   const int bc = bvalid ? b : B - 1;
   const int t = lab[bc];
+  // lane owns k = 8 lane + [0, 8): two float4 per row (h, every W2 row), 22 loads per
+  // lane, all in flight at once (lane 62 has half a chunk, lane 63 none)
+  const int k0 = 8 * lane;
+  const bool v0 = k0 < 500, v1 = k0 + 4 < 500;
+  const int o0 = v0 ? k0 : 496, o1 = v1 ? k0 + 4 : 496;
   float hv[8], wv[10][8];
+  {
+    const float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
+    const float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
+    float4 w0[10], w1v[10];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int k = min(lane + 64 * q, 499);
-    hv[q] = h[(size_t)bc * 500 + k];
+    for (int j = 0; j < 10; ++j) {
+      w0[j] = *reinterpret_cast<const float4*>(w2 + j * 500 + o0);
+      w1v[j] = *reinterpret_cast<const float4*>(w2 + j * 500 + o1);
+    }
+    hv[0] = v0 ? h0.x : 0.f; hv[1] = v0 ? h0.y : 0.f; hv[2] = v0 ? h0.z : 0.f; hv[3] = v0 ? h0.w : 0.f;
+    hv[4] = v1 ? h1.x : 0.f; hv[5] = v1 ? h1.y : 0.f; hv[6] = v1 ? h1.z : 0.f; hv[7] = v1 ? h1.w : 0.f;
 #pragma unroll
-    for (int j = 0; j < 10; ++j) wv[j][q] = w2[j * 500 + k];
+    for (int j = 0; j < 10; ++j) {
+      wv[j][0] = w0[j].x; wv[j][1] = w0[j].y; wv[j][2] = w0[j].z; wv[j][3] = w0[j].w;
+      wv[j][4] = w1v[j].x; wv[j][5] = w1v[j].y; wv[j][6] = w1v[j].z; wv[j][7] = w1v[j].w;
+    }
   }
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-    if (lane + 64 * q >= 500) hv[q] = 0.f;
   float logit[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) {
@@ -584,16 +597,17 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     for (int j = 0; j < 10; ++j)
       if (lane == j) dlogits[(size_t)b * 10 + j] = dl[j];
   }
+  float dv[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const int k = lane + 64 * q;
-    if (k < 500) {
-      float s = 0.f;
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) s = fmaf(dl[j], wv[j][q], s);
-      dh[(size_t)b * 500 + k] = hv[q] > 0.f ? s : 0.f;
-    }
+    for (int j = 0; j < 10; ++j) s = fmaf(dl[j], wv[j][q], s);
+    dv[q] = hv[q] > 0.f ? s : 0.f;
   }
+  float4* dr = reinterpret_cast<float4*>(dh + (size_t)b * 500 + k0);
+  if (v0) dr[0] = make_float4(dv[0], dv[1], dv[2], dv[3]);
+  if (v1) dr[1] = make_float4(dv[4], dv[5], dv[6], dv[7]);
   stamp(dbg, 1);
 }
 
@@ -675,14 +689,22 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
     const bool rv = row < B;
     const int rc = rv ? row : B - 1;
     const int f = kt * 16 + i;
-    const int s0 = wv * 16;  // steps [s0, s0+16) of 125 (wave 7: 13 valid)
+    // K order: step s of wave wv, lane group g covers k = 64 wv + 16 g + s, so a lane's
+    // 16 dh values are contiguous (4 float4 loads); k >= 500 (wave 7, g = 3, s >= 4) is 0
+    const int kb = 64 * wv + 16 * g;
     float av[16], bv[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = min(4 * (s0 + s) + g, 499);
-      av[s] = dh[(size_t)rc * 500 + k];
-      bv[s] = w1[(size_t)k * 800 + f];
+    for (int q = 0; q < 4; ++q) {
+      const int kq = kb + 4 * q;
+      const float4 d4 = *reinterpret_cast<const float4*>(dh + (size_t)rc * 500 + min(kq, 496));
+      const bool ok = rv && kq < 500;
+      av[4 * q] = ok ? d4.x : 0.f;
+      av[4 * q + 1] = ok ? d4.y : 0.f;
+      av[4 * q + 2] = ok ? d4.z : 0.f;
+      av[4 * q + 3] = ok ? d4.w : 0.f;
     }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) bv[s] = w1[(size_t)min(kb + s, 499) * 800 + f];
     // epilogue operands of threads tid < 256 (ReLU mask + pool argmax), in flight with
     // the GEMM loads
     const int l = (tid & 255) >> 2, r = tid & 3;
@@ -694,10 +716,8 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
     f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const bool kv = (s0 + s) < 125;
-      const float a = (rv && kv) ? av[s] : 0.f;
-      if (s & 1) c1 = mfma16x16x4(a, bv[s], c1);
-      else c0 = mfma16x16x4(a, bv[s], c0);
+      if (s & 1) c1 = mfma16x16x4(av[s], bv[s], c1);
+      else c0 = mfma16x16x4(av[s], bv[s], c0);
     }
     asm volatile("" : "+v"(a2o), "+v"(p));  // keep the epilogue loads above the barrier
     red[wv][lane] = c0 + c1;
@@ -1291,6 +1311,7 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
                    float* per_sample, float* stats, void* stream) {
   PTO_CHECK_B(B);
   if (lab == nullptr) return -1;
+  if ((((uintptr_t)h) | ((uintptr_t)w2) | ((uintptr_t)dh)) & 15) return -2;  // float4 rows
   if (stats == nullptr)
     hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(64), 0, (hipStream_t)stream, h, w2, b2, lab,
                        B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, g_dbg);
@@ -1307,6 +1328,7 @@ int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, con
                       float loss_scale, int jobs, int B, void* stream) {
   PTO_CHECK_B(B);
   if (jobs <= 0 || jobs > 7) return -1;
+  if (((uintptr_t)dh) & 15) return -2;  // float4 dh rows (job 2)
   const int blocks = ((jobs & 1) ? E_NJ1 : 0) + ((jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
                      ((jobs & 4) ? E_NJ3 : 0);
   hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, dh, a2,
