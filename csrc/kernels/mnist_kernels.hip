@@ -262,20 +262,19 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
 //   the cg == 0 block publishes a1/idx1 (for the backward), xn and lab.
 //   conv2 then runs exactly as conv2_fwd_pool_kernel.
 // ---------------------------------------------------------------------------
-// conv1 tasks t0, t0 + 16, .. (NU of them) as NU independent MFMA accumulator chains,
-// then bias + ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1 if pub).
+// conv1 channels 0-15 on MFMA: position tiles t0, t0 + 16, .. (NU of them; tile = conv
+// rows {2py, 2py+1} x cols 8px..8px+7) as NU independent accumulator chains, then bias +
+// ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1 if pub).  Channels 16-19
+// would fill only a quarter of a second 16-wide channel tile: conv1_valu_window does them.
 template <int NU>
 __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int (&toff)[7],
-                                            const float (&bw)[2][7], const float* w1s, float* in_s,
+                                            const float (&bw)[7], float bc, float* in_s,
                                             bool pub, float* a1, uint8_t* idx1, int b, int i, int g) {
   f32x4 acc[NU];
   const float* ibs[NU];
-  int nts[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int t = t0 + 16 * u;
-    const int pt1 = t >> 1;
-    nts[u] = t & 1;
+    const int pt1 = t0 + 16 * u;
     const int py = pt1 / 3, px = pt1 - py * 3;
     ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
     acc[u] = zero4();
@@ -283,15 +282,12 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
 #pragma unroll
   for (int s = 0; s < 7; ++s)
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
-      acc[u] = mfma16x16x4(ibs[u][toff[s]], nts[u] ? bw[1][s] : bw[0][s], acc[u]);
+    for (int u = 0; u < NU; ++u) acc[u] = mfma16x16x4(ibs[u][toff[s]], bw[s], acc[u]);
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int t = t0 + 16 * u;
-    const int pt1 = t >> 1, nt = t & 1;
+    const int pt1 = t0 + 16 * u;
     const int py = pt1 / 3, px = pt1 - py * 3;
-    const int c = nt * 16 + i;
-    const float bc = w1s[500 + min(c, 19)];
+    const int c = i;
     const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc, v3 = acc[u][3] + bc;
     float mA = v0; int aA = 0;
     if (v1 > mA) { mA = v1; aA = 1; }
@@ -301,7 +297,7 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     const int paA = __shfl_xor(aA, 32, 64);
     const float pB = __shfl_xor(mB, 32, 64);
     const int paB = __shfl_xor(aB, 32, 64);
-    if (g < 2 && c < 20) {
+    if (g < 2) {
       if (pA > mA) { mA = pA; aA = 2 + paA; }
       if (pB > mB) { mB = pB; aB = 2 + paB; }
       const int pw = 4 * px + 2 * (g & 1);
@@ -316,6 +312,47 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
         idx1[o + 1] = (uint8_t)aB;
       }
     }
+  }
+}
+
+// conv1 channels 16-19 on the VALU (f32 FMA runs at the f32 MFMA rate): one pooled output
+// per thread, item = (c - 16) * 144 + pooled position.  Same tap order as the MFMA chain
+// and the standalone conv1 kernel (bit-identical results).
+__device__ __forceinline__ void conv1_valu_window(int item, const float* img, const float* w1s,
+                                                  float* in_s, bool pub, float* a1, uint8_t* idx1,
+                                                  int b) {
+  const int c = 16 + item / 144, p = item - (c - 16) * 144;
+  const int ph = p / 12, pw = p - ph * 12;
+  const float* im = img + (2 * ph) * 28 + 2 * pw;
+  const float* wc = w1s + c * 25;
+  float patch[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) patch[r][q] = im[r * 28 + q];
+  float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const float wv = wc[kh * 5 + kw];
+      o00 = fmaf(patch[kh][kw], wv, o00);
+      o01 = fmaf(patch[kh][kw + 1], wv, o01);
+      o10 = fmaf(patch[kh + 1][kw], wv, o10);
+      o11 = fmaf(patch[kh + 1][kw + 1], wv, o11);
+    }
+  const float bc = w1s[500 + c];
+  o00 += bc; o01 += bc; o10 += bc; o11 += bc;
+  float m = o00; int am = 0;
+  if (o01 > m) { m = o01; am = 1; }
+  if (o10 > m) { m = o10; am = 2; }
+  if (o11 > m) { m = o11; am = 3; }
+  const float v = fmaxf(m, 0.f);
+  in_s[c * C2_CS + ph * C2_RS + pw] = v;
+  if (pub) {
+    const size_t o = (size_t)b * 2880 + c * 144 + p;
+    a1[o] = v;
+    idx1[o] = (uint8_t)am;
   }
 }
 
@@ -370,39 +407,28 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 1);
-  // conv1 + bias + ReLU + 2x2 max-pool as an implicit GEMM on MFMA: 36 position
-  // tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 2 channel tiles (0-15, 16-19)
-  // x 7 K-steps (25 taps, zero-padded to 28 through the weight fragments).  The
-  // pool epilogue is the same register/lane^32 pairing as conv2's.
+  // conv1 + bias + ReLU + 2x2 max-pool.  Channels 0-15: implicit GEMM on MFMA, 36
+  // position tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 7 K-steps (25 taps,
+  // zero-padded to 28 through the weight fragments); wave w takes tiles w, w+16 (+ w+32
+  // for w < 4): 9 tiles per SIMD.  The pool epilogue is the same register/lane^32
+  // pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
   {
     const int lane = tid & 63, wv = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     int toff[7];
-    float bw[2][7];
+    float bw[7];
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
       const int tap = 4 * s + g;
       const int tc = tap < 25 ? tap : 24;
       toff[s] = (tc / 5) * 28 + (tc % 5);
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int c = nt * 16 + i;
-        const float wv_ = w1s[min(c, 19) * 25 + tc];
-        bw[nt][s] = (c < 20 && tap < 25) ? wv_ : 0.f;
-      }
+      const float wv_ = w1s[i * 25 + tc];
+      bw[s] = tap < 25 ? wv_ : 0.f;
     }
-    // 72 tasks = 36 position tiles x 2 channel tiles; wave w takes tasks w, w+16, ..
-    // (5 for w < 8, 4 otherwise: 18 per SIMD) as independent accumulator chains
-    // (MFMA latency > issue interval: one chain alone would idle the matrix pipe).
-#ifdef PTO_EXP_NO_TILE1  // experiment: channel tile 1 (odd waves) skipped
-    if (!(wv & 1)) {
-#endif
-    conv1_tasks<3>(wv, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
-    if (wv < 8) conv1_tasks<2>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
-    else conv1_tasks<1>(wv + 48, img, toff, bw, w1s, in_s, pub, a1, idx1, b, i, g);
-#ifdef PTO_EXP_NO_TILE1
-    }
-#endif
+    const float bc = w1s[500 + i];
+    conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+    if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+    if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
   }
   __syncthreads();
   stamp(dbg, 2);
