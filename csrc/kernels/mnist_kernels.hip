@@ -145,6 +145,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
 //   The two K halves meet in LDS; the 2x2 pool window = 2 registers of this
 //   lane x 2 registers of lane^32.
 // ---------------------------------------------------------------------------
+// Value of lane l + 32 for lanes l < 32 (v_permlane32_swap: one VALU op; __shfl_xor(v, 32)
+// lowers to an LDS ds_bpermute round trip).  Lanes >= 32 get an unspecified value.
+__device__ __forceinline__ float from_upper_half(float v) {
+  return __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false)[1]);
+}
+__device__ __forceinline__ int from_upper_half(int v) {
+  return (int)__builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false)[1];
+}
+
 constexpr int C2_RS = 16;
 constexpr int C2_CS = 200;
 constexpr int C2_WS = 514;
@@ -239,10 +248,10 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
   if (v1 > mA) { mA = v1; aA = 1; }
   float mB = v2; int aB = 0;
   if (v3 > mB) { mB = v3; aB = 1; }
-  const float pA = __shfl_xor(mA, 32, 64);
-  const int paA = __shfl_xor(aA, 32, 64);
-  const float pB = __shfl_xor(mB, 32, 64);
-  const int paB = __shfl_xor(aB, 32, 64);
+  const float pA = from_upper_half(mA);
+  const int paA = from_upper_half(aA);
+  const float pB = from_upper_half(mB);
+  const int paB = from_upper_half(aB);
   if (g < 2 && co < 50) {  // top row of the window; partner lane holds the bottom row
     if (pA > mA) { mA = pA; aA = 2 + paA; }
     if (pB > mB) { mB = pB; aB = 2 + paB; }
@@ -279,10 +288,18 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
     acc[u] = zero4();
   }
+  // every LDS operand read is issued before the first MFMA (the scheduler would otherwise
+  // interleave them and stall each MFMA on its own read)
+  float av[NU][7];
 #pragma unroll
   for (int s = 0; s < 7; ++s)
 #pragma unroll
-    for (int u = 0; u < NU; ++u) acc[u] = mfma16x16x4(ibs[u][toff[s]], bw[s], acc[u]);
+    for (int u = 0; u < NU; ++u) av[u][s] = ibs[u][toff[s]];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < 7; ++s)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc[u] = mfma16x16x4(av[u][s], bw[s], acc[u]);
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int pt1 = t0 + 16 * u;
@@ -293,10 +310,10 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     if (v1 > mA) { mA = v1; aA = 1; }
     float mB = v2; int aB = 0;
     if (v3 > mB) { mB = v3; aB = 1; }
-    const float pA = __shfl_xor(mA, 32, 64);
-    const int paA = __shfl_xor(aA, 32, 64);
-    const float pB = __shfl_xor(mB, 32, 64);
-    const int paB = __shfl_xor(aB, 32, 64);
+    const float pA = from_upper_half(mA);
+    const int paA = from_upper_half(aA);
+    const float pB = from_upper_half(mB);
+    const int paB = from_upper_half(aB);
     if (g < 2) {
       if (pA > mA) { mA = pA; aA = 2 + paA; }
       if (pB > mB) { mB = pB; aB = 2 + paB; }
@@ -426,6 +443,7 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
       bw[s] = tap < 25 ? wv_ : 0.f;
     }
     const float bc = w1s[500 + i];
+    __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
     conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
@@ -444,10 +462,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   if (v1 > mA) { mA = v1; aA = 1; }
   float mB = v2; int aB = 0;
   if (v3 > mB) { mB = v3; aB = 1; }
-  const float pA = __shfl_xor(mA, 32, 64);
-  const int paA = __shfl_xor(aA, 32, 64);
-  const float pB = __shfl_xor(mB, 32, 64);
-  const int paB = __shfl_xor(aB, 32, 64);
+  const float pA = from_upper_half(mA);
+  const int paA = from_upper_half(aA);
+  const float pB = from_upper_half(mB);
+  const int paB = from_upper_half(aB);
   if (g < 2 && co < 50) {
     if (pA > mA) { mA = pA; aA = 2 + paA; }
     if (pB > mB) { mB = pB; aB = 2 + paB; }
@@ -929,7 +947,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   __syncthreads();
   stamp(dbg, 1);
 
-  const int mt = wv & 3, nt0 = (wv >> 2) * F_TPW;
   // ---- phase 2a: dcolT[j][pos] = W2 slice^T . dz2   (M = 128 j, N = 64 pos, K = 52)
   {
     const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
@@ -951,30 +968,61 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
       for (int r = 0; r < 4; ++r)
         dcol_s[((jt0 + n) * 16 + g * 4 + r) * F_DC + pt * 16 + i] = acc[n][r];
   }
-  // ---- phase 2b: dW_conv2 partial  (M = 64 co, N = 128 (ci,kh,kw), K = 64 pos)
-  f32x4 gacc[F_TPW];
-#pragma unroll
-  for (int n = 0; n < F_TPW; ++n) gacc[n] = zero4();
+  // ---- phase 2b: dW_conv2 partial  (M = 48 co, N = 128 (ci,kh,kw), K = 64 pos)
+  // MFMA tiles (mt, nt) for co 0..47: waves 0-3 take mt 0, nt {2w, 2w+1}; waves 4-7 mt 1,
+  // nt {2w-8, 2w-7}; waves 8-15 mt 2, nt w-8 -- 6 tiles per SIMD, and one A fragment per
+  // K-step for both tiles of a wave.  co 48 and 49 (a fourth 16-row tile would be 7/8
+  // padding) are 250 VALU dot products in waves 8-11, one per SIMD, same pos order as the
+  // MFMA chain.
+  const int mt = wv < 4 ? 0 : (wv < 8 ? 1 : 2);
+  const int ntw = wv < 8 ? 2 * (wv & 3) : wv - 8;
+  const int nt2 = wv < 8 ? 2 : 1;  // tiles of this wave
+  f32x4 gacc[2] = {zero4(), zero4()};
+  float grow = 0.f;  // VALU rows: co 48 + item / 125, j = item % 125
+  const int item = tid - 512;
   {
-    int boff[F_TPW];
-    bool jv[F_TPW];
+    // B columns j >= 125 read a clamped (valid, finite) address: they only feed output
+    // columns the epilogue never stores, so no select/branch sits between load and MFMA
+    int boff[2];
 #pragma unroll
-    for (int n = 0; n < F_TPW; ++n) {
-      const int j = (nt0 + n) * 16 + i;
-      jv[n] = j < 125;
-      const int jc = jv[n] ? j : 124;
+    for (int n = 0; n < 2; ++n) {
+      const int jc = min((ntw + n) * 16 + i, 124);
       const int ci = jc / 25, t = jc - ci * 25;
       boff[n] = ci * F_A1C + (t / 5) * F_A1R + (t % 5);
     }
+    const float* arow = dz_s + (mt * 16 + i) * F_DS + g;
+    if (wv < 8) {
+      float av[16], b0[16], b1[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float av = dz_s[(mt * 16 + i) * F_DS + 4 * s + g];
-      const int poff = (s >> 1) * F_A1R + 4 * (s & 1) + g;  // pos = 4s+g -> (oh, ow)
-#pragma unroll
-      for (int n = 0; n < F_TPW; ++n) {
-        const float bv = jv[n] ? a1_s[boff[n] + poff] : 0.f;
-        gacc[n] = mfma16x16x4(av, bv, gacc[n]);
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int poff = (s2 >> 1) * F_A1R + 4 * (s2 & 1) + g;  // pos = 4s+g -> (oh, ow)
+        av[s2] = arow[4 * s2];
+        b0[s2] = a1_s[boff[0] + poff];
+        b1[s2] = a1_s[boff[1] + poff];
       }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        gacc[0] = mfma16x16x4(av[s2], b0[s2], gacc[0]);
+        gacc[1] = mfma16x16x4(av[s2], b1[s2], gacc[1]);
+      }
+    } else {
+      float av[16], b0[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int poff = (s2 >> 1) * F_A1R + 4 * (s2 & 1) + g;
+        av[s2] = arow[4 * s2];
+        b0[s2] = a1_s[boff[0] + poff];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) gacc[0] = mfma16x16x4(av[s2], b0[s2], gacc[0]);
+    }
+    if (item >= 0 && item < 250) {
+      const int co = 48 + item / 125, j = item % 125;
+      const int ci = j / 25, t = j - ci * 25;
+      const float* ar = a1_s + ci * F_A1C + (t / 5) * F_A1R + (t % 5);
+      const float* dr = dz_s + co * F_DS;
+#pragma unroll 16
+      for (int pos = 0; pos < 64; ++pos) grow = fmaf(dr[pos], ar[(pos >> 3) * F_A1R + (pos & 7)], grow);
     }
   }
   float b2sum = 0.f;
@@ -1067,19 +1115,22 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   const bool slab = slab_stride > 0;
   const size_t so = slab ? (size_t)b * slab_stride : 0;
 #pragma unroll
-  for (int n = 0; n < F_TPW; ++n) {
-    const int j = (nt0 + n) * 16 + i;
-    if (j < 125) {
+  for (int n = 0; n < 2; ++n) {
+    const int j = (ntw + n) * 16 + i;
+    if (n < nt2 && j < 125) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = mt * 16 + g * 4 + r;
-        if (co < 50) {
-          float* dst = gw2 + so + (size_t)co * 500 + cig * 125 + j;
-          if (slab) *dst = gacc[n][r];
-          else atomicAdd(dst, gacc[n][r]);
-        }
+        float* dst = gw2 + so + (size_t)co * 500 + cig * 125 + j;
+        if (slab) *dst = gacc[n][r];
+        else atomicAdd(dst, gacc[n][r]);
       }
     }
+  }
+  if (item >= 0 && item < 250) {
+    float* dst = gw2 + so + (size_t)(48 + item / 125) * 500 + cig * 125 + item % 125;
+    if (slab) *dst = grow;
+    else atomicAdd(dst, grow);
   }
   if (cig == 0 && tid < 50) {
     if (slab) gb2[so + tid] = b2sum;
