@@ -953,15 +953,19 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
     f32x4 acc[F_TPW];
 #pragma unroll
     for (int n = 0; n < F_TPW; ++n) acc[n] = zero4();
+    // all 39 LDS operands of the wave first, then the MFMA chains
+    float bv[13], av[F_TPW][13];
 #pragma unroll
     for (int s = 0; s < 13; ++s) {
-      const float bv = dz80_s[(4 * s + g) * F_D8 + pt * 16 + i];
+      bv[s] = dz80_s[(4 * s + g) * F_D8 + pt * 16 + i];
 #pragma unroll
-      for (int n = 0; n < F_TPW; ++n) {
-        const float av = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
-        acc[n] = mfma16x16x4(av, bv, acc[n]);
-      }
+      for (int n = 0; n < F_TPW; ++n) av[n][s] = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 13; ++s)
+#pragma unroll
+      for (int n = 0; n < F_TPW; ++n) acc[n] = mfma16x16x4(av[n][s], bv[s], acc[n]);
 #pragma unroll
     for (int n = 0; n < F_TPW; ++n)
 #pragma unroll
