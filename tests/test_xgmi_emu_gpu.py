@@ -14,9 +14,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _emu(world, n):
+def _emu(world, n, nblk=128):
     from pytorch_operator_amd.parallel.xgmi import XgmiEmulation
-    return XgmiEmulation(world, n)
+    return XgmiEmulation(world, n, nblk=nblk)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -43,15 +43,15 @@ def test_mean_allreduce(world, n):
         emu.close()
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_fused_sgd_with_slab(world):
+@pytest.mark.parametrize("world,nblk", [(2, 128), (4, 128), (8, 128), (2, 256)])
+def test_fused_sgd_with_slab(world, nblk):
     from pytorch_operator_amd.models.mnist import flat_layout
     dev = torch.device("cuda", 0)
     L = flat_layout().total
     ce = flat_layout().conv_end
     B, lr, mom = 64, 0.01, 0.5
     g = torch.Generator(device="cpu").manual_seed(100 + world)
-    emu = _emu(world, L)
+    emu = _emu(world, L, nblk)  # nblk 256: the one-GPU-per-rank default (parallel/xgmi.py)
     try:
         p0 = torch.randn(L, generator=g).to(dev)
         ps = [p0.clone() for _ in range(world)]
