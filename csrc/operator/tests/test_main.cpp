@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 
+#include "pto/util.hpp"
 #include "pto/api.hpp"
 #include "pto/expectations.hpp"
 #include "pto/http.hpp"
@@ -182,7 +183,23 @@ static void test_reconcile_smoke() {
   CHECK(r.status.path({"startTime"}) != nullptr);
 }
 
+// pkg/util/util_test.go:5-11 (TestRandString) + Pformat
+static void test_util() {
+  CHECK(rand_string(4).size() == 4);
+  CHECK(rand_string(0).empty());
+  const std::string r = rand_string(64);
+  bool ok = true;
+  for (char c : r) ok = ok && ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z'));
+  CHECK(ok);
+  CHECK(rand_string(16) != rand_string(16));
+  CHECK(pformat(Json("plain")) == "plain");
+  const Json o = Json::parse(R"({"a":1,"b":[true,null]})");
+  CHECK(pformat(o) == o.dump(2));
+  CHECK(Json::parse(pformat(o)).dump() == o.dump());
+}
+
 int main() {
+  test_util();
   test_json();
   test_yaml();
   test_options();

@@ -17,6 +17,7 @@ import pytest
 
 from pytorch_operator_amd.cluster.local import LocalCluster
 from pytorch_operator_amd.cluster.rest import EVENTS, PODGROUPS, PODS, PYTORCHJOBS, SERVICES, ApiException
+from pytorch_operator_amd.utils import pformat, rand_string
 
 NS = "default"
 
@@ -312,13 +313,14 @@ def test_many_concurrent_jobs_with_threadiness(tmp_path):
     with LocalCluster(workdir=str(tmp_path / "s"), operator_args=["--threadiness=4", "--qps=50",
                                                                   "--burst=100"]) as c:
         c.wait_operator_ready()
-        names = [f"stress-{i}" for i in range(12)]
+        # random suffixes like the reference e2e (test/e2e/v1/default/defaults.go + util.RandString)
+        names = [f"stress-{i}-{rand_string(4)}" for i in range(12)]
         for n in names:
             c.rest.create(PYTORCHJOBS, make_job(n, replica(1, "busybox", command=py("pass")),
                                                 replica(2, "busybox", command=py("pass"))), NS)
         for n in names:
             types, job = wait_finished(c, n, timeout=120)
-            assert types[-1] == "Succeeded", (n, job["status"])
+            assert types[-1] == "Succeeded", pformat(job["status"])
             # (the master's success ends the job: workers may not have started yet)
             assert len(pod_names(c, n)) == 3  # expectations: no duplicate pods under concurrency
         assert c.metric_value("pytorch_operator_jobs_successful_total") == 12

@@ -214,3 +214,16 @@ def test_example_yamls_are_valid_jobs():
         for spec in job["spec"]["pytorchReplicaSpecs"].values():
             for c in spec["template"]["spec"]["containers"]:
                 assert "nvidia.com/gpu" not in json.dumps(c), path  # MI355X-only resources
+
+
+def test_util_pformat_and_rand_string():
+    """pkg/util/util_test.go:5-11 (TestRandString) plus Pformat's string pass-through."""
+    import json
+    from pytorch_operator_amd.utils import pformat, rand_string
+    assert len(rand_string(4)) == 4 and rand_string(0) == ""
+    s = rand_string(64)
+    assert set(s) <= set("0123456789abcdefghijklmnopqrstuvwxyz")
+    assert rand_string(16) != rand_string(16)
+    assert pformat("as-is") == "as-is"
+    obj = {"status": {"conditions": [{"type": "Running", "status": "True"}]}}
+    assert json.loads(pformat(obj)) == obj and "\n  " in pformat(obj)
