@@ -33,6 +33,8 @@
 // Every kernel takes an optional `dbg` pointer: when non-null, thread 0 of each
 // block records wall_clock64() (100 MHz) at phase boundaries into
 // dbg[block * 16 + phase] (used by tools/phase_profile.py; null in production).
+#include <atomic>
+
 #include "pto_common.h"
 
 using namespace pto;
@@ -1423,13 +1425,17 @@ int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const
                        float* dz1_out, int slab_stride, int B, void* stream) {
   PTO_CHECK_B(B);
   if (slab_stride < 0) return -1;
-  static bool attr_set = false;
-  if (!attr_set) {
+  // > 64 KB of dynamic LDS must be opted into once per device (thread-safe: several
+  // host threads may drive different GPUs through this library)
+  static std::atomic<unsigned> attr_set{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
+  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
     const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              F_LDS * (int)sizeof(float));
     if (e != hipSuccess) return (int)e;
-    attr_set = true;
+    attr_set.fetch_or(1u << dev, std::memory_order_release);
   }
   hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float),
                      (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
