@@ -487,17 +487,22 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
 //   row read one contiguous 64 B segment per load); the ten partial tiles are summed
 //   through LDS and the bias+ReLU epilogue is applied once.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(640) void fc1_fwd_kernel(
+// KS = 2 (training path): K split over two blocks (blockIdx.z) of 5 waves each, 256
+// blocks on the 256 CUs with half the operand bytes per CU; each writes its pre-activation
+// partial to h + z * B * 500 and head_kernel adds the halves, bias and ReLU.
+template <int KS>
+__global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ h, int B, u64* dbg) {
-  __shared__ f32x4 red[10][64];
-  const int nt = blockIdx.x, mt = blockIdx.y, tid = threadIdx.x;
+  constexpr int NW = 10 / KS;
+  __shared__ f32x4 red[NW][64];
+  const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, tid = threadIdx.x;
   stamp(dbg, 0);
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int row = mt * 16 + i, col = nt * 16 + i;
   const bool rv = row < B, cv = col < 500;
-  const int k0 = wv * 80 + g * 4;
+  const int k0 = (kz * NW + wv) * 80 + g * 4;
   const float4* xa = reinterpret_cast<const float4*>(x + (size_t)(rv ? row : B - 1) * 800 + k0);
   const float4* wb = reinterpret_cast<const float4*>(w + (size_t)(cv ? col : 499) * 800 + k0);
   float4 av[5], bv[5];
@@ -526,8 +531,11 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
   if (tid < 256) {
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < 10; ++q) s += red[q][l_e][r_e];
-    if (orow < B && ocol < 500) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
+    for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
+    if (orow < B && ocol < 500) {
+      if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
+      else h[((size_t)kz * B + orow) * 500 + ocol] = s;
+    }
   }
 }
 
@@ -542,12 +550,15 @@ __global__ __launch_bounds__(640) void fc1_fwd_kernel(
 // 20 KB W2 stream of each sample lands on its own CU (4 waves per block put 80 KB of
 // L2 traffic on each of 16 CUs); the eval path (B = 1000) keeps 4 to cut the atomics.
 // ---------------------------------------------------------------------------
+// With hp2 (the split-K fc1 path): h = relu(h + hp2 + b1) is formed here and written to
+// h_out for the backward.
 template <int WPB>
 __global__ __launch_bounds__(64 * WPB) void head_kernel(
     const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
     const int* __restrict__ lab, int B, float grad_scale, float loss_scale,
     float* __restrict__ dlogits, float* __restrict__ dh, float* __restrict__ logp_out,
-    float* __restrict__ per_sample, float* __restrict__ stats, u64* dbg) {
+    float* __restrict__ per_sample, float* __restrict__ stats, const float* __restrict__ hp2,
+    const float* __restrict__ b1, float* __restrict__ h_out, u64* dbg) {
   __shared__ float red[2][WPB];
   const int tid = threadIdx.x, lane = tid & 63, wq = tid >> 6;
   stamp(dbg, 0);
@@ -562,8 +573,23 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
   const int o0 = v0 ? k0 : 496, o1 = v1 ? k0 + 4 : 496;
   float hv[8], wv[10][8];
   {
-    const float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
-    const float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
+    float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
+    float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
+    if (hp2 != nullptr) {
+      const float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
+      const float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
+      const float4 c0 = *reinterpret_cast<const float4*>(b1 + o0);
+      const float4 c1 = *reinterpret_cast<const float4*>(b1 + o1);
+      h0 = make_float4(fmaxf(h0.x + q0.x + c0.x, 0.f), fmaxf(h0.y + q0.y + c0.y, 0.f),
+                       fmaxf(h0.z + q0.z + c0.z, 0.f), fmaxf(h0.w + q0.w + c0.w, 0.f));
+      h1 = make_float4(fmaxf(h1.x + q1.x + c1.x, 0.f), fmaxf(h1.y + q1.y + c1.y, 0.f),
+                       fmaxf(h1.z + q1.z + c1.z, 0.f), fmaxf(h1.w + q1.w + c1.w, 0.f));
+      if (bvalid) {
+        float4* ho = reinterpret_cast<float4*>(h_out + (size_t)b * 500);
+        if (v0) ho[k0 >> 2] = h0;
+        if (v1) ho[(k0 >> 2) + 1] = h1;
+      }
+    }
     float4 w0[10], w1v[10];
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
@@ -1390,24 +1416,38 @@ int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* 
                       void* stream) {
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return -2;  // float4 loads
-  hipLaunchKernelGGL(fc1_fwd_kernel, dim3(32, (B + 15) / 16), dim3(640), 0,
+  hipLaunchKernelGGL(fc1_fwd_kernel<1>, dim3(32, (B + 15) / 16), dim3(640), 0,
                      (hipStream_t)stream, x, w, bias, h, B, g_dbg);
+  return (int)hipGetLastError();
+}
+
+// Split-K fc1: pre-activation halves to parts[2][B][500] (head_kernel finishes h).
+int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, void* stream) {
+  PTO_CHECK_B(B);
+  if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)parts)) & 15) return -2;
+  hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3(32, (B + 15) / 16, 2), dim3(320), 0,
+                     (hipStream_t)stream, x, w, nullptr, parts, B, g_dbg);
   return (int)hipGetLastError();
 }
 
 int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* lab, int B,
                    float grad_scale, float loss_scale, float* dlogits, float* dh, float* logp,
-                   float* per_sample, float* stats, void* stream) {
+                   float* per_sample, float* stats, const float* hp2, const float* b1, float* h_out,
+                   void* stream) {
   PTO_CHECK_B(B);
   if (lab == nullptr) return -1;
-  if ((((uintptr_t)h) | ((uintptr_t)w2) | ((uintptr_t)dh)) & 15) return -2;  // float4 rows
+  if (hp2 != nullptr && (b1 == nullptr || h_out == nullptr)) return -1;
+  if ((((uintptr_t)h) | ((uintptr_t)w2) | ((uintptr_t)dh) | ((uintptr_t)hp2) | ((uintptr_t)b1) |
+       ((uintptr_t)h_out)) & 15)
+    return -2;  // float4 rows
   if (stats == nullptr)
     hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(64), 0, (hipStream_t)stream, h, w2, b2, lab,
-                       B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, g_dbg);
+                       B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, hp2, b1,
+                       h_out, g_dbg);
   else
     hipLaunchKernelGGL(head_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h,
                        w2, b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample,
-                       stats, g_dbg);
+                       stats, hp2, b1, h_out, g_dbg);
   return (int)hipGetLastError();
 }
 

@@ -151,6 +151,7 @@ class FusedMnistTrainer:
         self.xn = torch.empty((B, 784), device=dev)
         self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
         self.per_sample = torch.empty((B, 2), device=dev)
+        self.h_parts = torch.empty(2 * B * 500, device=dev)  # split-K fc1 pre-activations
         # per-sample conv-grad slabs in the flat conv-segment layout (pads stay 0)
         self.conv_slab = torch.zeros((B, self.layout.conv_end), device=dev)
         self.slab_views = {
@@ -204,9 +205,11 @@ class FusedMnistTrainer:
                         idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
-        K.fc1_fwd(self.a2[:B], p["fc1.weight"], p["fc1.bias"], out=self.h1[:B])
-        K.head(self.h1[:B], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
-               per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B])
+        # split-K fc1 (256 workgroups); the head adds the halves + bias, applies ReLU, writes h1
+        hp = K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500))
+        K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
+               per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
+               h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
     def _fc1_bwd(self, B: int, jobs: int) -> None:
         K, p, g = self.K, self.params, self.grads

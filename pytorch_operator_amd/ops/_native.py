@@ -96,7 +96,8 @@ _SIGNATURES = {
     "pto_slab_reduce_sgd": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                             _VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _VP],

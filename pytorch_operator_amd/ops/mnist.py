@@ -201,20 +201,46 @@ def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out
 
 
+def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Split-K fc1 forward: the two pre-activation halves ``out[z] = x[:, Kz] @ w[:, Kz].T``
+    (K halves of 400) as fp32 [2, B, 500]; ``head(..., h_second=out[1], fc1_bias=b,
+    h_out=h)`` finishes ``h = relu(out[0] + out[1] + b)``.  256 workgroups instead of 128:
+    half the operand bytes per CU on the latency-bound load phase."""
+    lib = _native.load()
+    B = x.shape[0]
+    _req(x, (B, 800), torch.float32, "x")
+    _req(w, (500, 800), torch.float32, "fc1.weight")
+    out = torch.empty((2, B, 500), device=x.device) if out is None else out
+    _req(out, (2, B, 500), torch.float32, "fc1 partials")
+    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _stream())
+    _native.check(rc, "fc1_fwd_parts")
+    return out
+
+
 def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *,
          grad_scale: float = 0.0, loss_scale: float = 1.0, want_grad: bool = True,
          want_logp: bool = False, stats: Optional[torch.Tensor] = None,
          per_sample: Optional[torch.Tensor] = None, dlogits: Optional[torch.Tensor] = None,
-         dh: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None):
+         dh: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None,
+         h_second: Optional[torch.Tensor] = None, fc1_bias: Optional[torch.Tensor] = None,
+         h_out: Optional[torch.Tensor] = None):
     """fc2 + log_softmax + nll (+ d(logits), dh with the fc1 ReLU mask).
 
     ``lab``: int32 [B] targets (``conv1_fwd`` gathers them).  ``per_sample`` (fp32
     [B,2]) receives (loss, correct) per sample; ``stats`` (fp32 [>=2]) accumulates
-    ``sum(loss)*loss_scale`` and the correct count atomically.
+    ``sum(loss)*loss_scale`` and the correct count atomically.  With ``h_second``
+    (``fc1_fwd_parts``), ``h`` is the first split-K half: the kernel forms
+    ``relu(h + h_second + fc1_bias)`` and writes it to ``h_out``.
     """
     lib = _native.load()
     B = h.shape[0]
     _req(h, (B, 500), torch.float32, "h1")
+    if h_second is not None:
+        _req(h_second, (B, 500), torch.float32, "h_second")
+        if fc1_bias is None or h_out is None:
+            raise ValueError("h_second needs fc1_bias and h_out")
+        _req(fc1_bias, (500,), torch.float32, "fc1.bias")
+        _req(h_out, (B, 500), torch.float32, "h_out")
     _req(w, (10, 500), torch.float32, "fc2.weight")
     _req(b, (10,), torch.float32, "fc2.bias")
     _req(lab, (B,), torch.int32, "lab")
@@ -237,7 +263,8 @@ def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *
         raise ValueError("stats must be fp32 with >= 2 elements")
     rc = lib.pto_mnist_head(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), B,
                             float(grad_scale), float(loss_scale), _ptr(dlogits), _ptr(dh),
-                            _ptr(logp), _ptr(per_sample), _ptr(stats), _stream())
+                            _ptr(logp), _ptr(per_sample), _ptr(stats), _ptr(h_second),
+                            _ptr(fc1_bias), _ptr(h_out), _stream())
     _native.check(rc, "head")
     return dlogits, dh, logp
 

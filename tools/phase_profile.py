@@ -39,6 +39,13 @@ def main():
         ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
         ("head", lambda: K.head(tr.h1, p["fc2.weight"], p["fc2.bias"], tr.lab, grad_scale=1.0 / B,
                                 per_sample=tr.per_sample, dlogits=tr.dlogits, dh=tr.dh)),
+        ("fc1_parts", lambda: K.fc1_fwd_parts(tr.a2, p["fc1.weight"],
+                                              out=tr.h_parts[:2 * B * 500].view(2, B, 500))),
+        ("head_parts", lambda: K.head(tr.h_parts[:B * 500].view(B, 500), p["fc2.weight"], p["fc2.bias"],
+                                      tr.lab, grad_scale=1.0 / B, per_sample=tr.per_sample,
+                                      dlogits=tr.dlogits, dh=tr.dh,
+                                      h_second=tr.h_parts[B * 500:2 * B * 500].view(B, 500),
+                                      fc1_bias=p["fc1.bias"], h_out=tr.h1)),
         ("fc1_bwd_w", lambda: tr._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)),
         ("fc1_bwd_d", lambda: tr._fc1_bwd(B, K.FC1_BWD_DGRAD)),
         ("conv_bwd", lambda: tr._conv_bwd(B)),
