@@ -233,11 +233,19 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     const long lo4 = c4 + (long)b * per, hi4 = min(lo4 + per, a.npad4);
     // first batch of the copied segment: loads in flight while the slab rows are summed
     f4 g0, g1, g2, g3;
+    // unconditional loads from clamped addresses, then selects (a predicated load becomes
+    // a branch + a wait per element)
+    const f4* gin = reinterpret_cast<const f4*>(a.in);
+    const long vmax = a.n4 - 1;
+    auto ld = [&](long v) {
+      const f4 x = gin[v < vmax ? v : vmax];
+      return (v < hi4 && v < a.n4) ? x : zero4;
+    };
     auto load_batch = [&](long v0) {
-      g0 = v0 < hi4 ? grad4(a, v0) : zero4;
-      g1 = v0 + kThreads < hi4 ? grad4(a, v0 + kThreads) : zero4;
-      g2 = v0 + 2 * kThreads < hi4 ? grad4(a, v0 + 2 * kThreads) : zero4;
-      g3 = v0 + 3 * kThreads < hi4 ? grad4(a, v0 + 3 * kThreads) : zero4;
+      g0 = ld(v0);
+      g1 = ld(v0 + kThreads);
+      g2 = ld(v0 + 2 * kThreads);
+      g3 = ld(v0 + 3 * kThreads);
     };
     load_batch(lo4 + tid);
     if (c4 > 0) {
@@ -302,13 +310,22 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     wait_flags(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err);
     acquire_fence(a);
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
+      // every sender's contribution in flight at once (clamped addresses, no predicated
+      // load: a runtime-bounded loop here waited a full memory round trip per sender)
+      f4 rq[kP2][kMaxWorld];
+#pragma unroll
+      for (int k = 0; k < kP2; ++k) {
+        const long i = min(i0 + (long)k * kThreads, a.chunk4 - 1);
+#pragma unroll
+        for (int q = 0; q < kMaxWorld; ++q) rq[k][q] = rv[(long)min(q, a.world - 1) * a.shard4 + i];
+      }
       f4 acc[kP2];
 #pragma unroll
       for (int k = 0; k < kP2; ++k) {
-        const long i = i0 + (long)k * kThreads;
-        acc[k] = zero4;
-        if (i < a.chunk4)
-          for (int q = 0; q < a.world; ++q) acc[k] += rv[(long)q * a.shard4 + i];  // rank order
+        acc[k] = rq[k][0];
+#pragma unroll
+        for (int q = 1; q < kMaxWorld; ++q)
+          if (q < a.world) acc[k] += rq[k][q];  // rank order (deterministic)
       }
 #pragma unroll
       for (int k = 0; k < kP2; ++k) {
@@ -326,7 +343,9 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
         } else {
           res = zero4;
         }
-        for (int j = 1; j < a.world; ++j) {
+#pragma unroll
+        for (int j = 1; j < kMaxWorld; ++j) {
+          if (j >= a.world) break;
           const int q = a.rank + j < a.world ? a.rank + j : a.rank + j - a.world;
           push4(gath_buf(peer(a, q), a.npad4) + v, res);
         }
@@ -359,7 +378,8 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
         const long kk = j / a.chunk4, i = j - kk * a.chunk4;
         const int q = a.rank + 1 + (int)kk < a.world ? a.rank + 1 + (int)kk : a.rank + 1 + (int)kk - a.world;
         vv[k] = j < tot ? (long)q * a.shard4 + (long)b * a.chunk4 + i : a.n4;
-        x[k] = vv[k] < a.n4 ? gb[vv[k]] : zero4;
+        const f4 xg = gb[vv[k] < a.npad4 ? vv[k] : a.npad4 - 1];  // unconditional load
+        x[k] = vv[k] < a.n4 ? xg : zero4;
       }
 #pragma unroll
       for (int k = 0; k < kP3; ++k)
