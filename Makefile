@@ -7,7 +7,7 @@ GPURUN ?= /usr/local/graft/bin/gpurun
 build:            ## HIP kernels (gfx950), operator binary, _opcore, C++ tests
 	$(PY) -c "import __graft_entry__ as g; g.build()"
 
-test: test-cpu    ## CPU suite (what CI runs without a GPU)
+test: test-cpu    ## CPU suite (what CI runs without a GPU; tools/ci.sh cpu = build + verify + this)
 
 test-cpu: build
 	$(PY) -m pytest tests -m "not gpu" -q
