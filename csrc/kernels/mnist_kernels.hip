@@ -4,28 +4,28 @@
 //   conv1(1->20,k5) -> ReLU -> maxpool2 -> conv2(20->50,k5) -> ReLU -> maxpool2
 //   -> fc1(800->500) -> ReLU -> fc2(500->10) -> log_softmax -> nll_loss(mean)
 //
-// The whole step is 6 launches (+1 fused SGD launch, +RCCL all-reduce when
-// world_size > 1).  At B=64 the step is ~0.84 GFLOP: it is launch- and
-// latency-bound, so every kernel is shaped to (a) issue all of its global loads
-// up front (no load -> use -> load chains), (b) keep its MFMA chains short by
-// splitting K across the waves of a workgroup, and (c) keep the launch count low
-// so a hipGraph can replay the step back to back:
+// The training step is 6 launches (world_size > 1: the tail launch is the xGMI
+// exchange of xgmi_allreduce.hip, or RCCL buckets).  At B=64 the step is ~0.84
+// GFLOP: it is latency-bound, so every kernel is shaped to (a) issue all of its
+// global loads up front (no load -> use -> load chains, no predicated loads, at most
+// the 63 loads vmcnt can track), (b) keep its MFMA chains short by splitting K
+// across the waves of a workgroup, and (c) keep the launch count low so a hipGraph
+// replays the step back to back (docs/kernels.md has the measured design log):
 //
-//   A conv1_fwd_pool   uint8 gather + Normalize + conv1 + bias + ReLU + pool(argmax);
-//                      also emits the normalised batch + gathered labels for the
-//                      later launches, and zero-fills the atomically-accumulated
-//                      grad segment (conv grads + loss stats)
-//   B conv2_fwd_pool   implicit GEMM on v_mfma_f32_16x16x4_f32, LDS-staged im2col,
-//                      K split over two wave groups, bias + ReLU + 2x2 max-pool
-//                      fused in the accumulator epilogue
-//   C fc1_fwd          MFMA GEMM, K split over 10 waves, LDS reduction, bias+ReLU
-//   D head             fc2 + log_softmax + NLL + d(logits) + fc2^T GEMV + ReLU mask
-//   E fc1_bwd          dW_fc1 / db_fc1 (MFMA), dX_fc1 (MFMA) with un-pool + ReLU
+//   AB conv12_fwd      uint8 gather + Normalize; conv1 channels 0-15 on MFMA, 16-19 on
+//                      the VALU; bias + ReLU + 2x2 max-pool (argmax) into an LDS
+//                      im2col image; conv2 as an implicit GEMM on
+//                      v_mfma_f32_16x16x4_f32, bias + ReLU + pool in the epilogue
+//   C  fc1_fwd<2>      split-K MFMA GEMM (256 workgroups), pre-activation halves
+//   D  head            relu(half0 + half1 + b1), fc2 + log_softmax + NLL +
+//                      d(logits) + fc2^T GEMV + ReLU mask
+//   E  fc1_bwd         dW_fc1 / db_fc1 (MFMA), dX_fc1 (MFMA) with un-pool + ReLU
 //                      mask epilogue, dW_fc2 / db_fc2, loss statistics
-//   F conv_bwd         per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
-//                      dW_conv2 (MFMA, im2col from LDS), col2im + un-pool + ReLU
-//                      mask -> dz1 (LDS), dW_conv1 (MFMA), db_conv1/db_conv2
-//   H sgd_momentum     multi-tensor SGD(momentum) over the flat parameter buffer
+//   F  conv_bwd        per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
+//                      dW_conv2 (MFMA + VALU rows), col2im + un-pool + ReLU mask ->
+//                      dz1 (LDS), dW_conv1 (VALU), per-sample slab rows
+//   G  slab_reduce_sgd deterministic slab reduction + SGD(momentum) on every parameter
+// (A conv1_fwd_pool, B conv2_fwd_pool, sgd_momentum: the unfused / eval building blocks.)
 //
 // All arithmetic is fp32 (the reference's dtype); matrix work uses the exact-fp32
 // MFMA (one rounding per product, same as an fmaf chain).
