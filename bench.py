@@ -94,7 +94,7 @@ def main(argv=None):
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph
         if spg <= 0:  # whole steps per graph replay: any divisor of both steps and warmup
-            spg = next((c for c in (10, 8, 5, 4, 2) if args.steps % c == 0 and args.warmup % c == 0), 1)
+            spg = next((c for c in (50, 25, 20, 10, 8, 5, 4, 2) if args.steps % c == 0 and args.warmup % c == 0), 1)
         eager_w = min(args.warmup, 3)
         for _ in range(eager_w):
             tr.train_step()  # eager warmup: loads the library, initialises momentum
