@@ -30,6 +30,12 @@ import time
 BASELINE_PER_RANK = 210.0
 
 
+def pick_steps_per_graph(steps: int, warmup: int) -> int:
+    """Whole training steps per hipGraph replay: the largest of 50, 25, 20, 10, 8, 5, 4, 2
+    dividing both ``steps`` and ``warmup`` (so exactly ``steps`` steps are timed), else 1."""
+    return next((c for c in (50, 25, 20, 10, 8, 5, 4, 2) if steps % c == 0 and warmup % c == 0), 1)
+
+
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
@@ -92,9 +98,7 @@ def main(argv=None):
         tr.fuse_conv12 = bool(args.fuse_conv12)
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
-        spg = args.steps_per_graph
-        if spg <= 0:  # whole steps per graph replay: any divisor of both steps and warmup
-            spg = next((c for c in (50, 25, 20, 10, 8, 5, 4, 2) if args.steps % c == 0 and args.warmup % c == 0), 1)
+        spg = args.steps_per_graph if args.steps_per_graph > 0 else pick_steps_per_graph(args.steps, args.warmup)
         eager_w = min(args.warmup, 3)
         for _ in range(eager_w):
             tr.train_step()  # eager warmup: loads the library, initialises momentum

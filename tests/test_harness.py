@@ -227,3 +227,21 @@ def test_util_pformat_and_rand_string():
     assert pformat("as-is") == "as-is"
     obj = {"status": {"conditions": [{"type": "Running", "status": "True"}]}}
     assert json.loads(pformat(obj)) == obj and "\n  " in pformat(obj)
+
+
+def test_bench_contract_cli_and_graph_chunking():
+    """bench.py (driver contract): defaults are N=1 with a K/W that finish in seconds, and the
+    steps-per-graph choice always divides K and W so exactly K steps are timed."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = bench.parse_args([])
+    assert a.gpus == 1 and a.steps > 0 and a.warmup >= 0
+    for k, w in [(2000, 50), (4000, 100), (100, 10), (7, 3), (5, 1), (30, 0), (1, 1)]:
+        spg = bench.pick_steps_per_graph(k, w)
+        assert k % spg == 0 and w % spg == 0 and spg >= 1
+    assert bench.pick_steps_per_graph(2000, 50) == 50
+    assert bench.pick_steps_per_graph(7, 3) == 1
