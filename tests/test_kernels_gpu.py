@@ -72,7 +72,7 @@ def test_forward_kernels_match_torch(lib, B):
     assert int(stats[1]) == int((rl.argmax(1) == y.long()).sum())
 
 
-@pytest.mark.parametrize("B", [64, 50])
+@pytest.mark.parametrize("B", [64, 50, 128, 130])
 def test_fused_step_gradients_and_sgd_match_torch(lib, B):
     from pytorch_operator_amd.models.mnist import FusedMnistTrainer, Net, reference_init
     from pytorch_operator_amd.ops import mnist as K
