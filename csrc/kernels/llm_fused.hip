@@ -1,0 +1,203 @@
+// Fused elementwise kernels for the Llama DDP worker (BASELINE "Llama-3 8B DDP bf16").
+//
+// The eager PyTorch forms of these ops each expand into a chain of fp32 elementwise
+// kernels over [tokens, hidden] tensors (RoPE: bf16->fp32 copy, 4 muls, add, sub, stack,
+// fp32->bf16 copy; SwiGLU backward: silu_backward + 2 muls + the saved silu), which the
+// rocprofv3 trace of the 8B step showed as ~15% of step time (profiles/
+// r1_llama3_8b_kernel_stats.md).  Here each op is one pass over HBM: 16-byte vector
+// loads/stores (8 bf16 or 2x4 fp32 per lane), fp32 math in registers.
+//
+//   rope:    x [rows = B*S*H, D] (adjacent pairs rotated, Meta's complex layout), position
+//            of a row = (row / H) % S, tables cos/sin [S, D/2] fp32.  sign = +1 forward,
+//            -1 backward (the adjoint of a rotation is the rotation by -theta).
+//   swiglu:  y = silu(a) * b ; backward da = dy*b*sig(a)*(1 + a*(1-sig(a))), db = dy*silu(a)
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kT = 256;
+
+struct V8 {
+  float v[8];
+};
+
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (inputs are finite)
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <typename T>
+struct Vec;
+
+template <>
+struct Vec<float> {
+  static __device__ __forceinline__ V8 load(const float* p) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    return V8{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w}};
+  }
+  static __device__ __forceinline__ void store(float* p, const V8& r) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(r.v[4], r.v[5], r.v[6], r.v[7]);
+  }
+  static __device__ __forceinline__ float load1(const float* p) { return *p; }
+  static __device__ __forceinline__ void store1(float* p, float v) { *p = v; }
+};
+
+template <>
+struct Vec<uint16_t> {  // bf16 bits
+  static __device__ __forceinline__ V8 load(const uint16_t* p) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    V8 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r.v[2 * i] = __uint_as_float(w[i] << 16);
+      r.v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+    return r;
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const V8& r) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(r.v[2 * i]) | ((uint32_t)f2bf(r.v[2 * i + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  static __device__ __forceinline__ float load1(const uint16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void store1(uint16_t* p, float v) { *p = f2bf(v); }
+};
+
+// ---------------------------------------------------------------------------------- rope
+template <typename T>
+__global__ __launch_bounds__(kT) void rope_kernel(const T* __restrict__ x, const float* __restrict__ cosb,
+                                                  const float* __restrict__ sinb, T* __restrict__ y, long groups,
+                                                  int H, int S, int D, float sign) {
+  const int gpr = D / 8;  // 8-element groups per row (D % 8 == 0 checked on the host)
+  for (long g = (long)blockIdx.x * kT + threadIdx.x; g < groups; g += (long)gridDim.x * kT) {
+    const long row = g / gpr;
+    const int c8 = (int)(g - row * gpr) * 8;
+    const int s = (int)((row / H) % S);
+    const V8 in = Vec<T>::load(x + row * D + c8);
+    const float4 cv = *reinterpret_cast<const float4*>(cosb + (long)s * (D / 2) + c8 / 2);
+    const float4 sv = *reinterpret_cast<const float4*>(sinb + (long)s * (D / 2) + c8 / 2);
+    const float cs[4] = {cv.x, cv.y, cv.z, cv.w}, sn[4] = {sign * sv.x, sign * sv.y, sign * sv.z, sign * sv.w};
+    V8 out;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float x0 = in.v[2 * i], x1 = in.v[2 * i + 1];
+      out.v[2 * i] = x0 * cs[i] - x1 * sn[i];
+      out.v[2 * i + 1] = x0 * sn[i] + x1 * cs[i];
+    }
+    Vec<T>::store(y + row * D + c8, out);
+  }
+}
+
+// -------------------------------------------------------------------------------- swiglu
+__device__ __forceinline__ float sigmoid(float a) { return 1.f / (1.f + __expf(-a)); }
+
+template <typename T>
+__global__ __launch_bounds__(kT) void swiglu_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                        T* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long g = (long)blockIdx.x * kT + threadIdx.x; g <= n8; g += (long)gridDim.x * kT) {
+    if (g < n8) {
+      const V8 av = Vec<T>::load(a + g * 8), bv = Vec<T>::load(b + g * 8);
+      V8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o.v[i] = av.v[i] * sigmoid(av.v[i]) * bv.v[i];
+      Vec<T>::store(y + g * 8, o);
+    } else {
+      for (long i = n8 * 8; i < n; ++i) {
+        const float av = Vec<T>::load1(a + i);
+        Vec<T>::store1(y + i, av * sigmoid(av) * Vec<T>::load1(b + i));
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kT) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ a,
+                                                        const T* __restrict__ b, T* __restrict__ da,
+                                                        T* __restrict__ db, long n) {
+  const long n8 = n / 8;
+  for (long g = (long)blockIdx.x * kT + threadIdx.x; g <= n8; g += (long)gridDim.x * kT) {
+    if (g < n8) {
+      const V8 gv = Vec<T>::load(dy + g * 8), av = Vec<T>::load(a + g * 8), bv = Vec<T>::load(b + g * 8);
+      V8 oa, ob;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float sg = sigmoid(av.v[i]);
+        oa.v[i] = gv.v[i] * bv.v[i] * sg * (1.f + av.v[i] * (1.f - sg));
+        ob.v[i] = gv.v[i] * av.v[i] * sg;
+      }
+      Vec<T>::store(da + g * 8, oa);
+      Vec<T>::store(db + g * 8, ob);
+    } else {
+      for (long i = n8 * 8; i < n; ++i) {
+        const float gv = Vec<T>::load1(dy + i), av = Vec<T>::load1(a + i), bv = Vec<T>::load1(b + i);
+        const float sg = sigmoid(av);
+        Vec<T>::store1(da + i, gv * bv * sg * (1.f + av * (1.f - sg)));
+        Vec<T>::store1(db + i, gv * av * sg);
+      }
+    }
+  }
+}
+
+// Enough workgroups to fill 256 CUs several times over; grid-stride beyond that.
+unsigned grid_for(long work) {
+  const long b = (work + kT - 1) / kT;
+  return (unsigned)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+// dtype: 0 = fp32, 1 = bf16.  All pointers 16-byte aligned, tensors contiguous.
+int pto_rope(const void* x, const float* cosb, const float* sinb, void* y, long rows, int H, int S, int D,
+             float sign, int dtype, void* stream) {
+  if (rows <= 0 || H <= 0 || S <= 0 || D <= 0 || D % 8 || (rows % H) || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(cosb) || !aligned16(sinb)) return -2;
+  const long groups = rows * (D / 8);
+  if (dtype == 0)
+    hipLaunchKernelGGL(rope_kernel<float>, dim3(grid_for(groups)), dim3(kT), 0, (hipStream_t)stream,
+                       (const float*)x, cosb, sinb, (float*)y, groups, H, S, D, sign);
+  else
+    hipLaunchKernelGGL(rope_kernel<uint16_t>, dim3(grid_for(groups)), dim3(kT), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, cosb, sinb, (uint16_t*)y, groups, H, S, D, sign);
+  return (int)hipGetLastError();
+}
+
+int pto_swiglu_fwd(const void* a, const void* b, void* y, long n, int dtype, void* stream) {
+  if (n <= 0 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(a) || !aligned16(b) || !aligned16(y)) return -2;
+  const unsigned grid = grid_for(n / 8 + 1);
+  if (dtype == 0)
+    hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(grid), dim3(kT), 0, (hipStream_t)stream, (const float*)a,
+                       (const float*)b, (float*)y, n);
+  else
+    hipLaunchKernelGGL(swiglu_fwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)y, n);
+  return (int)hipGetLastError();
+}
+
+int pto_swiglu_bwd(const void* dy, const void* a, const void* b, void* da, void* db, long n, int dtype,
+                   void* stream) {
+  if (n <= 0 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(dy) || !aligned16(a) || !aligned16(b) || !aligned16(da) || !aligned16(db)) return -2;
+  const unsigned grid = grid_for(n / 8 + 1);
+  if (dtype == 0)
+    hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(grid), dim3(kT), 0, (hipStream_t)stream, (const float*)dy,
+                       (const float*)a, (const float*)b, (float*)da, (float*)db, n);
+  else
+    hipLaunchKernelGGL(swiglu_bwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const uint16_t*)dy, (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)da,
+                       (uint16_t*)db, n);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

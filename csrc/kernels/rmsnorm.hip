@@ -46,13 +46,16 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return t;
 }
 
-template <typename T, int PER>
-__global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                         T* __restrict__ y, float* __restrict__ rstd, int D,
+// TX: activation dtype of x / dx (the residual stream, fp32 or bf16).  TY: dtype of y / dy
+// (bf16 when the norm feeds autocast bf16 matmuls: writing bf16 here removes the separate
+// fp32->bf16 cast kernel in the forward and the bf16->fp32 dy cast in the backward).
+template <typename TX, typename TY, int PER>
+__global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w,
+                                                         TY* __restrict__ y, float* __restrict__ rstd, int D,
                                                          float eps) {
   __shared__ float sh[kT / 64];
   const long row = blockIdx.x;
-  const T* xr = x + row * D;
+  const TX* xr = x + row * D;
   float v[PER];
   float ss = 0.f;
 #pragma unroll
@@ -70,10 +73,10 @@ __global__ __launch_bounds__(kT) void rmsnorm_fwd_kernel(const T* __restrict__ x
   }
 }
 
-template <typename T, int PER>
-__global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename TX, typename TY, int PER>
+__global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const TY* __restrict__ dy, const TX* __restrict__ x,
                                                          const float* __restrict__ w,
-                                                         const float* __restrict__ rstd, T* __restrict__ dx,
+                                                         const float* __restrict__ rstd, TX* __restrict__ dx,
                                                          float* __restrict__ dw_part, long rows, int D,
                                                          int rows_per_block) {
   __shared__ float sh[kT / 64];
@@ -114,62 +117,103 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const T* __restrict__ d
   }
 }
 
+// Column sums of dw_part [nparts, D] in a fixed order (deterministic).  A workgroup owns
+// kColsPerWg columns: kCLanes lanes per row slice read them as float4 and kSlices slices
+// walk disjoint row ranges with all loads of a slice issued back to back, then the slices
+// are added in slice order through LDS.  D=4096, 512 parts: 128 workgroups x 256 lanes
+// with 32 float4 loads in flight each, instead of 16 workgroups each walking 512 rows one
+// dependent load at a time (123 us -> a few us, see docs/kernels.md).
+constexpr int kCLanes = 8;                   // float4 lanes per slice -> 32 columns
+constexpr int kColsPerWg = kCLanes * 4;
+constexpr int kSlices = kT / kCLanes;        // 32 row slices
 __global__ __launch_bounds__(kT) void colsum_kernel(const float* __restrict__ part, int nparts, int D,
                                                     float* __restrict__ out) {
-  const int j = blockIdx.x * kT + threadIdx.x;
-  if (j >= D) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * D + j];
-  out[j] = s;
+  __shared__ float4 sh[kSlices][kCLanes];
+  const int lane = threadIdx.x % kCLanes, slice = threadIdx.x / kCLanes;
+  const int j = blockIdx.x * kColsPerWg + lane * 4;
+  const int per = (nparts + kSlices - 1) / kSlices;
+  const int p0 = slice * per, p1 = min(nparts, p0 + per);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j + 3 < D && (D & 3) == 0) {
+#pragma unroll 8
+    for (int p = p0; p < p1; ++p) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)p * D + j);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  } else {
+    for (int p = p0; p < p1; ++p) {
+      const float* r = part + (long)p * D;
+      if (j < D) s.x += r[j];
+      if (j + 1 < D) s.y += r[j + 1];
+      if (j + 2 < D) s.z += r[j + 2];
+      if (j + 3 < D) s.w += r[j + 3];
+    }
+  }
+  sh[slice][lane] = s;
+  __syncthreads();
+  if (slice == 0) {
+    float4 t = sh[0][lane];
+    for (int k = 1; k < kSlices; ++k) {
+      const float4 v = sh[k][lane];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    if (j < D) out[j] = t.x;
+    if (j + 1 < D) out[j + 1] = t.y;
+    if (j + 2 < D) out[j + 2] = t.z;
+    if (j + 3 < D) out[j + 3] = t.w;
+  }
 }
 
-template <typename T, int PER>
+template <typename TX, typename TY, int PER>
 void fwd_launch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
-  hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, PER>), dim3(rows), dim3(kT), 0, (hipStream_t)stream, (const T*)x, w,
-                     (T*)y, rstd, D, eps);
+  hipLaunchKernelGGL((rmsnorm_fwd_kernel<TX, TY, PER>), dim3(rows), dim3(kT), 0, (hipStream_t)stream,
+                     (const TX*)x, w, (TY*)y, rstd, D, eps);
 }
 
-template <typename T>
+template <typename TX, typename TY>
 int fwd_dispatch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
   const int per = (D + kT - 1) / kT;
-  if (per <= 1) fwd_launch<T, 1>(x, w, y, rstd, rows, D, eps, stream);
-  else if (per <= 2) fwd_launch<T, 2>(x, w, y, rstd, rows, D, eps, stream);
-  else if (per <= 4) fwd_launch<T, 4>(x, w, y, rstd, rows, D, eps, stream);
-  else if (per <= 8) fwd_launch<T, 8>(x, w, y, rstd, rows, D, eps, stream);
-  else if (per <= 16) fwd_launch<T, 16>(x, w, y, rstd, rows, D, eps, stream);
-  else fwd_launch<T, 32>(x, w, y, rstd, rows, D, eps, stream);
+  if (per <= 1) fwd_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 2) fwd_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 4) fwd_launch<TX, TY, 4>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 8) fwd_launch<TX, TY, 8>(x, w, y, rstd, rows, D, eps, stream);
+  else if (per <= 16) fwd_launch<TX, TY, 16>(x, w, y, rstd, rows, D, eps, stream);
+  else fwd_launch<TX, TY, 32>(x, w, y, rstd, rows, D, eps, stream);
   return (int)hipGetLastError();
 }
 
-template <typename T, int PER>
+template <typename TX, typename TY, int PER>
 void bwd_launch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
                 long rows, int D, int rpb, long nb, void* stream) {
-  hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, PER>), dim3(nb), dim3(kT), 0, (hipStream_t)stream, (const T*)dy,
-                     (const T*)x, w, rstd, (T*)dx, dw_part, rows, D, rpb);
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<TX, TY, PER>), dim3(nb), dim3(kT), 0, (hipStream_t)stream,
+                     (const TY*)dy, (const TX*)x, w, rstd, (TX*)dx, dw_part, rows, D, rpb);
 }
 
-template <typename T>
+template <typename TX, typename TY>
 void bwd_dispatch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
                   long rows, int D, int rpb, long nb, void* stream) {
   const int per = (D + kT - 1) / kT;
-  if (per <= 1) bwd_launch<T, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-  else if (per <= 2) bwd_launch<T, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-  else if (per <= 4) bwd_launch<T, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-  else if (per <= 8) bwd_launch<T, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-  else if (per <= 16) bwd_launch<T, 16>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-  else bwd_launch<T, 32>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  if (per <= 1) bwd_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 2) bwd_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 4) bwd_launch<TX, TY, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 8) bwd_launch<TX, TY, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else if (per <= 16) bwd_launch<TX, TY, 16>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  else bwd_launch<TX, TY, 32>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
 }
+
+// dtype pair code: 0 = (x fp32, y fp32), 1 = (bf16, bf16), 2 = (x fp32, y bf16)
+bool valid_pair(int code) { return code >= 0 && code <= 2; }
 
 }  // namespace
 
 extern "C" {
 
-// dtype: 0 = fp32, 1 = bf16
 int pto_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, int dtype,
                     void* stream) {
-  if (D <= 0 || D > kT * kMaxPer || rows <= 0) return -1;
-  return dtype == 0 ? fwd_dispatch<float>(x, w, y, rstd, rows, D, eps, stream)
-                    : fwd_dispatch<__hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream);
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || !valid_pair(dtype)) return -1;
+  if (dtype == 0) return fwd_dispatch<float, float>(x, w, y, rstd, rows, D, eps, stream);
+  if (dtype == 1) return fwd_dispatch<__hip_bfloat16, __hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream);
+  return fwd_dispatch<float, __hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream);
 }
 
 // Number of workgroups (= rows of dw_part) the backward uses for `rows` rows.
@@ -177,12 +221,15 @@ long pto_rmsnorm_bwd_parts(long rows, int rows_per_block) { return (rows + rows_
 
 int pto_rmsnorm_bwd(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw,
                     float* dw_part, long rows, int D, int rows_per_block, int dtype, void* stream) {
-  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || rows_per_block <= 0) return -1;
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || rows_per_block <= 0 || !valid_pair(dtype)) return -1;
   const long nb = (rows + rows_per_block - 1) / rows_per_block;
-  if (dtype == 0) bwd_dispatch<float>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
-  else bwd_dispatch<__hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
-  hipLaunchKernelGGL(colsum_kernel, dim3((D + kT - 1) / kT), dim3(kT), 0, (hipStream_t)stream, dw_part, (int)nb,
-                     D, dw);
+  if (nb > (1L << 30)) return -1;
+  if (dtype == 0) bwd_dispatch<float, float>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  else if (dtype == 1)
+    bwd_dispatch<__hip_bfloat16, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  else bwd_dispatch<float, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  hipLaunchKernelGGL(colsum_kernel, dim3((D + kColsPerWg - 1) / kColsPerWg), dim3(kT), 0, (hipStream_t)stream,
+                     dw_part, (int)nb, D, dw);
   return (int)hipGetLastError();
 }
 

@@ -9,8 +9,11 @@ no sharding is needed -- every rank keeps the whole model and only gradients cro
 Architecture (Meta's reference layout): token embedding, ``n_layers`` x [RMSNorm ->
 GQA attention with RoPE (theta 500 000) -> residual, RMSNorm -> SwiGLU FFN -> residual],
 final RMSNorm, untied output projection.  Matmuls run in bf16 under autocast
-(hipBLASLt); attention uses ``scaled_dot_product_attention`` (ROCm flash attention);
-RMSNorm uses the fused HIP kernel from ``ops.norm`` when it is built (fp32 statistics).
+(hipBLASLt); attention uses ``scaled_dot_product_attention`` (ROCm flash attention).
+The elementwise work between the matmuls runs as hand-written HIP kernels on a GPU:
+RMSNorm (``ops.norm``, fp32 statistics over the fp32 residual stream, bf16 output under
+autocast so the next matmul reads it directly), RoPE and SwiGLU (``ops.llm``, one HBM pass
+each, fwd and bwd).  On CPU the same math runs in PyTorch.
 """
 from __future__ import annotations
 
@@ -63,12 +66,8 @@ def rope_tables(head_dim: int, seq_len: int, theta: float, device=None):
 
 def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     """x [B, S, H, D]; rotates adjacent pairs (x0, x1) like Meta's complex formulation."""
-    xf = x.float().reshape(*x.shape[:-1], -1, 2)
-    x0, x1 = xf[..., 0], xf[..., 1]
-    c = cos[None, :, None, :]
-    s = sin[None, :, None, :]
-    out = torch.stack((x0 * c - x1 * s, x0 * s + x1 * c), dim=-1)
-    return out.flatten(-2).type_as(x)
+    from ..ops.llm import rope
+    return rope(x, cos, sin)
 
 
 class RMSNorm(nn.Module):
@@ -79,7 +78,10 @@ class RMSNorm(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         from ..ops.norm import rms_norm
-        return rms_norm(x, self.weight, self.eps)
+        out_dtype = None
+        if x.is_cuda and x.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):
+            out_dtype = torch.get_autocast_dtype("cuda")  # consumed by a bf16 matmul next
+        return rms_norm(x, self.weight, self.eps, out_dtype)
 
 
 class Attention(nn.Module):
@@ -109,7 +111,8 @@ class FeedForward(nn.Module):
         self.w2 = nn.Linear(cfg.ffn_hidden, cfg.dim, bias=False)
 
     def forward(self, x):
-        return self.w2(F.silu(self.w1(x)) * self.w3(x))
+        from ..ops.llm import swiglu
+        return self.w2(swiglu(self.w1(x), self.w3(x)))
 
 
 class Block(nn.Module):
@@ -158,4 +161,4 @@ class Llama(nn.Module):
         logits = self.output(self.norm(h))
         if targets is None:
             return logits
-        return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.view(-1))
+        return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), targets.reshape(-1))

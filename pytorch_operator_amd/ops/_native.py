@@ -119,6 +119,10 @@ _SIGNATURES = {
     # rmsnorm.hip
     "pto_rmsnorm_fwd": [_VP, _VP, _VP, _VP, _L, _I, _F, _I, _VP],
     "pto_rmsnorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _L, _I, _I, _I, _VP],
+    # llm_fused.hip
+    "pto_rope": [_VP, _VP, _VP, _VP, _L, _I, _I, _I, _F, _I, _VP],
+    "pto_swiglu_fwd": [_VP, _VP, _VP, _L, _I, _VP],
+    "pto_swiglu_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _VP],
 }
 _LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I]}
 _VOID_FNS = {"pto_set_debug_buffer": [_VP], "pto_xar_emu_stamps": [_VP, _VP]}

@@ -1,0 +1,99 @@
+"""Fused RoPE and SwiGLU (``csrc/kernels/llm_fused.hip``) as autograd ops for the Llama worker.
+
+``rope(x, cos, sin)``: ``x`` [B, S, H, D] (fp32 or bf16, contiguous), tables [S, D/2] fp32;
+rotates adjacent pairs like Meta's complex formulation.  The backward is the same kernel
+with the rotation negated.  ``swiglu(a, b)`` = ``silu(a) * b`` with a one-pass backward.
+
+On a GPU the HIP kernels run (a missing library is an error, never a silent fallback); on
+CPU the same math runs in PyTorch (CPU tests and the gloo plumbing config).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+# ------------------------------------------------------------------------------------ rope
+def rope_reference(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    xf = x.float().reshape(*x.shape[:-1], -1, 2)
+    x0, x1 = xf[..., 0], xf[..., 1]
+    c = cos[None, :, None, :]
+    s = sin[None, :, None, :]
+    out = torch.stack((x0 * c - x1 * s, x0 * s + x1 * c), dim=-1)
+    return out.flatten(-2).type_as(x)
+
+
+def _rope_launch(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, sign: float) -> torch.Tensor:
+    B, S, H, D = x.shape
+    y = torch.empty_like(x)
+    _native.check(_native.load().pto_rope(x.data_ptr(), cos.data_ptr(), sin.data_ptr(), y.data_ptr(), B * S * H, H,
+                                          S, D, sign, _DT[x.dtype], _stream(x)), "rope")
+    return y
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        ctx.save_for_backward(cos, sin)
+        return _rope_launch(x, cos, sin, 1.0)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        return _rope_launch(_aligned(dy), cos, sin, -1.0), None, None
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    if not x.is_cuda:
+        return rope_reference(x, cos, sin)
+    if x.dim() != 4 or x.dtype not in _DT or x.shape[-1] % 8 or cos.shape != (x.shape[1], x.shape[3] // 2):
+        raise ValueError(f"rope: x [B,S,H,D] fp32/bf16 with D % 8 == 0 and tables [S, D/2]; got {tuple(x.shape)}")
+    return _Rope.apply(_aligned(x), _aligned(cos.float()), _aligned(sin.float()))
+
+
+# ---------------------------------------------------------------------------------- swiglu
+def swiglu_reference(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return F.silu(a) * b
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        y = torch.empty_like(a)
+        _native.check(_native.load().pto_swiglu_fwd(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(),
+                                                    _DT[a.dtype], _stream(a)), "swiglu_fwd")
+        ctx.save_for_backward(a, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, b = ctx.saved_tensors
+        dy = _aligned(dy.to(a.dtype))
+        da, db = torch.empty_like(a), torch.empty_like(b)
+        _native.check(_native.load().pto_swiglu_bwd(dy.data_ptr(), a.data_ptr(), b.data_ptr(), da.data_ptr(),
+                                                    db.data_ptr(), a.numel(), _DT[a.dtype], _stream(a)),
+                      "swiglu_bwd")
+        return da, db
+
+
+def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if not a.is_cuda:
+        return swiglu_reference(a, b)
+    if a.shape != b.shape or a.dtype != b.dtype or a.dtype not in _DT:
+        raise ValueError("swiglu: a and b must share shape and dtype (fp32/bf16)")
+    return _SwiGLU.apply(_aligned(a), _aligned(b))

@@ -33,6 +33,82 @@ def test_rmsnorm_matches_reference(dtype, shape):
                                atol=1e-3 if dtype == torch.float32 else 3e-1)
 
 
+@pytest.mark.parametrize("shape", [(37, 4096), (2, 3, 8192), (5, 1000)])
+def test_rmsnorm_fp32_in_bf16_out(shape):
+    """The autocast path: fp32 residual stream in, bf16 normalised output, bf16 dy back."""
+    from pytorch_operator_amd.ops.norm import rms_norm, rms_norm_reference
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(*shape, generator=g).cuda().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(shape[-1], generator=g)).cuda().requires_grad_(True)
+    dy = torch.randn(*shape, generator=g).to("cuda", torch.bfloat16)
+    y = rms_norm(x, w, 1e-5, torch.bfloat16)
+    assert y.dtype == torch.bfloat16
+    (y.float() * dy.float()).sum().backward()
+    assert x.grad.dtype == torch.float32
+    xr = x.detach().clone().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    (rms_norm_reference(xr, wr, 1e-5) * dy.float()).sum().backward()
+    torch.testing.assert_close(y.float(), rms_norm_reference(x.detach(), w.detach(), 1e-5), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 32, 128), (1, 7, 3, 16), (3, 128, 8, 64)])
+def test_rope_matches_reference(dtype, shape):
+    from pytorch_operator_amd.models.llama import rope_tables
+    from pytorch_operator_amd.ops.llm import rope, rope_reference
+    g = torch.Generator(device="cpu").manual_seed(2)
+    B, S, H, D = shape
+    cos, sin = rope_tables(D, S, 500000.0, "cuda")
+    x = torch.randn(*shape, generator=g).to("cuda", dtype).requires_grad_(True)
+    dy = torch.randn(*shape, generator=g).to("cuda", dtype)
+    y = rope(x, cos, sin)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    yr = rope_reference(xr, cos, sin)
+    yr.backward(dy.float())
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [8, 4099, 2 * 14336 * 3])
+def test_swiglu_matches_reference(dtype, n):
+    from pytorch_operator_amd.ops.llm import swiglu
+    g = torch.Generator(device="cpu").manual_seed(3)
+    a = (2 * torch.randn(n, generator=g)).to("cuda", dtype).requires_grad_(True)
+    b = torch.randn(n, generator=g).to("cuda", dtype).requires_grad_(True)
+    dy = torch.randn(n, generator=g).to("cuda", dtype)
+    y = swiglu(a, b)
+    y.backward(dy)
+    ar, br = (t.detach().float().requires_grad_(True) for t in (a, b))
+    yr = torch.nn.functional.silu(ar) * br
+    yr.backward(dy.float())
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(a.grad.float(), ar.grad, **tol)
+    torch.testing.assert_close(b.grad.float(), br.grad, **tol)
+
+
+def test_llama_tiny_fused_matches_eager_reference():
+    """Whole-model check: the tiny Llama with the HIP kernels vs the same weights on CPU (fp32)."""
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    torch.manual_seed(0)
+    cpu = Llama(CONFIGS["llama-tiny"])
+    gpu = Llama(CONFIGS["llama-tiny"]).cuda()
+    gpu.load_state_dict(cpu.state_dict())
+    tok = torch.randint(0, 256, (2, 33))
+    lc = cpu(tok[:, :-1], tok[:, 1:])
+    lc.backward()
+    lg = gpu(tok[:, :-1].cuda(), tok[:, 1:].cuda())
+    lg.backward()
+    torch.testing.assert_close(lg.cpu(), lc, rtol=1e-4, atol=1e-4)
+    for (n, pc), pg in zip(cpu.named_parameters(), gpu.parameters()):
+        torch.testing.assert_close(pg.grad.cpu(), pc.grad, rtol=2e-3, atol=2e-5, msg=n)
+
+
 def _run(*args):
     r = subprocess.run([sys.executable, "-m", "pytorch_operator_amd.harness.ddp_train", *args], capture_output=True,
                        text=True, timeout=600, cwd=ROOT, env=dict(os.environ, PYTHONPATH=str(ROOT)))
