@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <initializer_list>
+
 namespace {
 
 constexpr int kT = 256;
@@ -31,6 +33,39 @@ __device__ __forceinline__ void st<float>(float* p, long i, float v) { p[i] = v;
 template <>
 __device__ __forceinline__ void st<__hip_bfloat16>(__hip_bfloat16* p, long i, float v) {
   p[i] = __float2bfloat16(v);
+}
+
+// 4 consecutive elements per access (16 B fp32 / 8 B bf16): the D % 4 == 0 fast path.
+struct F4 {
+  float v[4];
+};
+template <typename T>
+__device__ __forceinline__ F4 ld4(const T* p);
+template <>
+__device__ __forceinline__ F4 ld4<float>(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  return F4{{a.x, a.y, a.z, a.w}};
+}
+template <>
+__device__ __forceinline__ F4 ld4<__hip_bfloat16>(const __hip_bfloat16* p) {
+  const uint2 q = *reinterpret_cast<const uint2*>(p);
+  return F4{{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
+             __uint_as_float(q.y & 0xffff0000u)}};
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const F4& r);
+template <>
+__device__ __forceinline__ void st4<float>(float* p, const F4& r) {
+  *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+}
+__device__ __forceinline__ uint32_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+template <>
+__device__ __forceinline__ void st4<__hip_bfloat16>(__hip_bfloat16* p, const F4& r) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(bf16_rne(r.v[0]) | (bf16_rne(r.v[1]) << 16),
+                                            bf16_rne(r.v[2]) | (bf16_rne(r.v[3]) << 16));
 }
 
 __device__ __forceinline__ float block_sum(float v, float* sh) {
@@ -117,6 +152,101 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const TY* __restrict__ 
   }
 }
 
+// ---- D % 4 == 0 fast path: lane owns column groups j = 4*(threadIdx.x + k*kT), k < P4.
+template <typename TX, typename TY, int P4>
+__global__ __launch_bounds__(kT) void rmsnorm_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w,
+                                                             TY* __restrict__ y, float* __restrict__ rstd, int D,
+                                                             float eps) {
+  __shared__ float sh[kT / 64];
+  const long row = blockIdx.x;
+  F4 v[P4];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < P4; ++k) {
+    const int j = 4 * (threadIdx.x + k * kT);
+    v[k] = j < D ? ld4(x + row * D + j) : F4{{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ss += v[k].v[e] * v[k].v[e];
+  }
+  const float r = rsqrtf(block_sum(ss, sh) / (float)D + eps);
+  if (threadIdx.x == 0) rstd[row] = r;
+#pragma unroll
+  for (int k = 0; k < P4; ++k) {
+    const int j = 4 * (threadIdx.x + k * kT);
+    if (j < D) {
+      const float4 wv = *reinterpret_cast<const float4*>(w + j);
+      st4(y + row * D + j, F4{{v[k].v[0] * r * wv.x, v[k].v[1] * r * wv.y, v[k].v[2] * r * wv.z,
+                               v[k].v[3] * r * wv.w}});
+    }
+  }
+}
+
+// Backward, software-pipelined: the next row's x / dy loads are issued before this row's
+// block reduction, so HBM latency overlaps the two LDS barriers of block_sum.
+template <typename TX, typename TY, int P4>
+__global__ __launch_bounds__(kT) void rmsnorm_bwd_vec_kernel(const TY* __restrict__ dy, const TX* __restrict__ x,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ rstd, TX* __restrict__ dx,
+                                                             float* __restrict__ dw_part, long rows, int D,
+                                                             int rows_per_block) {
+  __shared__ float sh[kT / 64];
+  F4 wv[P4], dwa[P4], xv[P4], gv[P4];
+#pragma unroll
+  for (int k = 0; k < P4; ++k) {
+    const int j = 4 * (threadIdx.x + k * kT);
+    const F4 z{{0.f, 0.f, 0.f, 0.f}};
+    wv[k] = j < D ? ld4(w + j) : z;
+    dwa[k] = z;
+  }
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  auto load_row = [&](long row, F4* xo, F4* go) {
+#pragma unroll
+    for (int k = 0; k < P4; ++k) {
+      const int j = 4 * (threadIdx.x + k * kT);
+      const F4 z{{0.f, 0.f, 0.f, 0.f}};
+      xo[k] = j < D ? ld4(x + row * D + j) : z;
+      go[k] = j < D ? ld4(dy + row * D + j) : z;
+    }
+  };
+  if (r0 < r1) load_row(r0, xv, gv);
+  for (long row = r0; row < r1; ++row) {
+    F4 xn[P4], gn[P4];
+    if (row + 1 < r1) load_row(row + 1, xn, gn);
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < P4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dot += gv[k].v[e] * wv[k].v[e] * xv[k].v[e];
+    const float r = rstd[row];
+    const float c = block_sum(dot, sh) * r * r * r / (float)D;
+#pragma unroll
+    for (int k = 0; k < P4; ++k) {
+      const int j = 4 * (threadIdx.x + k * kT);
+      if (j < D) {
+        F4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o.v[e] = r * wv[k].v[e] * gv[k].v[e] - xv[k].v[e] * c;
+          dwa[k].v[e] += gv[k].v[e] * xv[k].v[e] * r;
+        }
+        st4(dx + row * D + j, o);
+      }
+    }
+    if (row + 1 < r1) {
+#pragma unroll
+      for (int k = 0; k < P4; ++k) {
+        xv[k] = xn[k];
+        gv[k] = gn[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < P4; ++k) {
+    const int j = 4 * (threadIdx.x + k * kT);
+    if (j < D) st4(dw_part + (long)blockIdx.x * D + j, dwa[k]);
+  }
+}
+
 // Column sums of dw_part [nparts, D] in a fixed order (deterministic).  A workgroup owns
 // kColsPerWg columns: kCLanes lanes per row slice read them as float4 and kSlices slices
 // walk disjoint row ranges with all loads of a slice issued back to back, then the slices
@@ -170,8 +300,30 @@ void fwd_launch(const void* x, const float* w, void* y, float* rstd, long rows, 
                      (const TX*)x, w, (TY*)y, rstd, D, eps);
 }
 
+template <typename TX, typename TY, int P4>
+void fwd_vec_launch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps,
+                    void* stream) {
+  hipLaunchKernelGGL((rmsnorm_fwd_vec_kernel<TX, TY, P4>), dim3(rows), dim3(kT), 0, (hipStream_t)stream,
+                     (const TX*)x, w, (TY*)y, rstd, D, eps);
+}
+
+bool vec_ok(int D, std::initializer_list<const void*> ptrs) {
+  if (D % 4) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p & 15u) return false;
+  return true;
+}
+
 template <typename TX, typename TY>
 int fwd_dispatch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
+  if (vec_ok(D, {x, w, y})) {
+    const int p4 = (D + 4 * kT - 1) / (4 * kT);
+    if (p4 <= 1) fwd_vec_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream);
+    else if (p4 <= 2) fwd_vec_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream);
+    else if (p4 <= 4) fwd_vec_launch<TX, TY, 4>(x, w, y, rstd, rows, D, eps, stream);
+    else fwd_vec_launch<TX, TY, 8>(x, w, y, rstd, rows, D, eps, stream);
+    return (int)hipGetLastError();
+  }
   const int per = (D + kT - 1) / kT;
   if (per <= 1) fwd_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream);
   else if (per <= 2) fwd_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream);
@@ -189,9 +341,24 @@ void bwd_launch(const void* dy, const void* x, const float* w, const float* rstd
                      (const TY*)dy, (const TX*)x, w, rstd, (TX*)dx, dw_part, rows, D, rpb);
 }
 
+template <typename TX, typename TY, int P4>
+void bwd_vec_launch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
+                    long rows, int D, int rpb, long nb, void* stream) {
+  hipLaunchKernelGGL((rmsnorm_bwd_vec_kernel<TX, TY, P4>), dim3(nb), dim3(kT), 0, (hipStream_t)stream,
+                     (const TY*)dy, (const TX*)x, w, rstd, (TX*)dx, dw_part, rows, D, rpb);
+}
+
 template <typename TX, typename TY>
 void bwd_dispatch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
                   long rows, int D, int rpb, long nb, void* stream) {
+  if (vec_ok(D, {dy, x, w, dx, dw_part})) {
+    const int p4 = (D + 4 * kT - 1) / (4 * kT);
+    if (p4 <= 1) bwd_vec_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+    else if (p4 <= 2) bwd_vec_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+    else if (p4 <= 4) bwd_vec_launch<TX, TY, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+    else bwd_vec_launch<TX, TY, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+    return;
+  }
   const int per = (D + kT - 1) / kT;
   if (per <= 1) bwd_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
   else if (per <= 2) bwd_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);

@@ -19,7 +19,7 @@ _DT = {torch.float32: 0, torch.bfloat16: 1}
 # (x dtype, y dtype) -> kernel dtype-pair code (csrc/kernels/rmsnorm.hip)
 _PAIR = {(torch.float32, torch.float32): 0, (torch.bfloat16, torch.bfloat16): 1,
          (torch.float32, torch.bfloat16): 2}
-_ROWS_PER_BLOCK = 16
+_ROWS_PER_BLOCK = 8  # tools/llm_kernel_bench.py sweep at 8192x4096: 4/8/16/32 -> 82/75/80/121 us
 
 
 def _stream(t: torch.Tensor):
