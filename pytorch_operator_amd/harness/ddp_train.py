@@ -9,8 +9,10 @@ weights, and reports throughput as one JSON line (rank 0):
     python -m pytorch_operator_amd.harness.ddp_train --model resnet50 --batch-size 256
     python -m pytorch_operator_amd.harness.ddp_train --model llama3-8b --seq-len 2048 --batch-size 1
 
-MI355X specifics: bf16 autocast (MFMA bf16 through hipBLASLt/MIOpen), fused RMSNorm HIP
-kernel in the Llama blocks, DDP with flat gradient buckets sized for xGMI
+MI355X specifics: bf16 autocast (MFMA bf16 through hipBLASLt/MIOpen), fused RMSNorm / RoPE /
+SwiGLU HIP kernels in the Llama blocks, bf16 matmul weights with fp32 masters updated by the
+fused HIP AdamW (``--master-weights``, on by default on a GPU: no per-step weight/grad cast
+kernels, fp32 all-reduce kept through a comm hook), DDP with flat gradient buckets sized for xGMI
 (``--bucket-mb``, default 64: few, large RCCL collectives), ``gradient_as_bucket_view``
 (no gradient copy), optional bf16 gradient compression (``--allreduce-dtype bf16``), and
 the 288 GB HBM budget that lets Llama-3 8B train with plain DDP (whole fp32 model, grads
@@ -41,6 +43,8 @@ def parse_args(argv=None):
     p.add_argument("--bucket-mb", type=float, default=64.0)
     p.add_argument("--allreduce-dtype", choices=["fp32", "bf16"], default="fp32")
     p.add_argument("--grad-checkpoint", action="store_true", help="Llama: recompute blocks in backward")
+    p.add_argument("--master-weights", choices=["auto", "on", "off"], default="auto",
+                   help="Llama: bf16 matmul weights + fp32 masters in the fused HIP AdamW (auto: on with a GPU)")
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--json-out", default=None)
@@ -58,12 +62,38 @@ def build(args, device):
     from ..models.llama import CONFIGS, Llama
     with torch.device(device):
         model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
+    if use_master_weights(args, device):
+        from ..ops.optim import MasterAdamW, to_bf16_matmul_weights
+        to_bf16_matmul_weights(model)
+        opt = MasterAdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1)
+        return model, opt
     kw = {"fused": True} if device.type == "cuda" else {}
     try:
         opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1, **kw)
     except (RuntimeError, TypeError):
         opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1)
     return model, opt
+
+
+def use_master_weights(args, device) -> bool:
+    if not args.model.startswith("llama") or args.dtype != "bf16":
+        return False
+    return args.master_weights == "on" or (args.master_weights == "auto" and device.type == "cuda")
+
+
+def fp32_allreduce_hook(process_group, bucket):
+    """DDP comm hook: all-reduce a bf16 gradient bucket in fp32 (``--allreduce-dtype fp32`` with
+    bf16 master-weight training keeps the cross-rank sum at fp32 precision)."""
+    import torch.distributed as dist
+    buf = bucket.buffer()
+    group = process_group if process_group is not None else dist.group.WORLD
+    t = buf.float().div_(dist.get_world_size(group))
+    fut = dist.all_reduce(t, group=group, async_op=True).get_future()
+
+    def done(f):
+        buf.copy_(f.value()[0])
+        return buf
+    return fut.then(done)
 
 
 def train_flops_per_sample(args) -> float:
@@ -99,6 +129,8 @@ def main(argv=None) -> int:
         if args.allreduce_dtype == "bf16":
             from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
             model.register_comm_hook(None, default_hooks.bf16_compress_hook)
+        elif use_master_weights(args, dev):
+            model.register_comm_hook(None, fp32_allreduce_hook)
     g = torch.Generator(device="cpu").manual_seed(args.seed + rank)
     if is_llama:
         from ..models.llama import CONFIGS
@@ -162,7 +194,8 @@ def main(argv=None) -> int:
            "seq_len": args.seq_len if is_llama else None, "loss": float(loss),
            "tflops_per_gpu": round(per_sample * samples / dt / world / 1e12, 1) if per_sample else None,
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
-           "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype}
+           "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
+           "master_weights": use_master_weights(args, dev)}
     if rank == 0:
         print(json.dumps(res), flush=True)
         if args.json_out:

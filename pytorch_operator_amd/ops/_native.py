@@ -123,6 +123,8 @@ _SIGNATURES = {
     "pto_rope": [_VP, _VP, _VP, _VP, _L, _I, _I, _I, _F, _I, _VP],
     "pto_swiglu_fwd": [_VP, _VP, _VP, _L, _I, _VP],
     "pto_swiglu_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _VP],
+    # adamw.hip
+    "pto_adamw_step": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _VP],
 }
 _LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I]}
 _VOID_FNS = {"pto_set_debug_buffer": [_VP], "pto_xar_emu_stamps": [_VP, _VP]}

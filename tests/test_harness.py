@@ -196,6 +196,17 @@ def test_ddp_train_worker_llama_tiny_two_ranks(tmp_path):
     assert res["metric"] == "llama_tiny_ddp_train_tokens_per_sec" and res["n_gpus"] == 2
 
 
+def test_ddp_train_worker_llama_tiny_master_weights_two_ranks(tmp_path):
+    """bf16 matmul weights + fp32 masters (MasterAdamW) under DDP with the fp32 all-reduce hook."""
+    outs = _launch("pytorch_operator_amd.harness.ddp_train",
+                   ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--steps", "2", "--warmup", "1",
+                    "--backend", "gloo", "--master-weights", "on"], 2, tmp_path)
+    for rc, out in outs:
+        assert rc == 0, out
+    res = json.loads([ln for ln in outs[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    assert res["master_weights"] is True and res["loss"] == res["loss"]
+
+
 def test_ddp_train_worker_resnet_tiny(tmp_path):
     (rc, out), = _launch("pytorch_operator_amd.harness.ddp_train",
                          ["--model", "resnet-tiny", "--batch-size", "2", "--steps", "2", "--warmup", "1"], 1, tmp_path)

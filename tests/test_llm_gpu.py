@@ -92,6 +92,37 @@ def test_swiglu_matches_reference(dtype, n):
     torch.testing.assert_close(b.grad.float(), br.grad, **tol)
 
 
+@pytest.mark.parametrize("n", [4096, 1001, 3 * 1024 * 1024 + 3])
+@pytest.mark.parametrize("grad_dtype,param_dtype", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32)])
+def test_adamw_kernel_matches_reference(n, grad_dtype, param_dtype):
+    from pytorch_operator_amd.ops.optim import MasterAdamW
+    g0 = torch.Generator(device="cpu").manual_seed(4)
+    w = torch.randn(n, generator=g0)
+    pg = w.clone().to("cuda", param_dtype)
+    pc = w.clone().to(param_dtype)
+    og = MasterAdamW([pg], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    oc = MasterAdamW([pc], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for _ in range(4):
+        g = torch.randn(n, generator=g0).to(grad_dtype)
+        pg.grad, pc.grad = g.cuda(), g.clone()
+        og.step()
+        oc.step()
+    sg, sc = og.state[pg], oc.state[pc]
+    for k in ("exp_avg", "exp_avg_sq"):
+        torch.testing.assert_close(sg[k].cpu(), sc[k], rtol=1e-5, atol=1e-6)
+    if param_dtype == torch.bfloat16:
+        torch.testing.assert_close(sg["master"].cpu(), sc["master"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(pg.cpu().float(), sg["master"].cpu().bfloat16().float(), rtol=0, atol=0)
+    else:
+        torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
+
+
+def test_llama_tiny_master_weights_trains_on_gpu():
+    res = _run("--model", "llama-tiny", "--seq-len", "128", "--batch-size", "4", "--steps", "30", "--warmup", "2",
+               "--lr", "3e-3", "--master-weights", "on")
+    assert res["master_weights"] is True and res["loss"] < 5.0
+
+
 def test_llama_tiny_fused_matches_eager_reference():
     """Whole-model check: the tiny Llama with the HIP kernels vs the same weights on CPU (fp32)."""
     from pytorch_operator_amd.models.llama import CONFIGS, Llama
