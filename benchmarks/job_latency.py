@@ -60,7 +60,7 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
             break
         time.sleep(0.02)
     pods = sorted(p["metadata"]["name"] for p in c.rest.list(PODS, "default", f"pytorch-job-name={name}")["items"])
-    first, done = [], []
+    first, done, paths = [], [], set()
     for p in pods:
         for line in c.rest.pod_log(p, "default").splitlines():
             if line.startswith('{"event"'):
@@ -69,13 +69,31 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
                     first.append(ev["unix_ns"])
                 elif ev["event"] == "train_done":
                     done.append(ev)
+                elif ev["event"] == "grad_allreduce":
+                    paths.add(ev.get("path"))
     s = lambda t: None if t is None else round((t - t_create) / 1e9, 3)  # noqa: E731
+    # every rank reports the job-wide aggregate (steps * B * world / t): take rank 0's
+    rank0 = [d for d in done if d.get("rank") == 0]
     return {"replicas": replicas, "result": final,
             "create_to_running_s": s(t_running),
             "create_to_first_step_s": s(max(first)) if len(first) == replicas else None,
             "create_to_succeeded_s": s(t_done),
-            "worker_samples_per_sec_total": round(sum(d.get("samples_per_sec") or 0 for d in done), 1),
-            "accuracy": done[0]["accuracy"] if done else None}
+            "worker_samples_per_sec": rank0[0].get("samples_per_sec") if rank0 else None,
+            "grad_allreduce": sorted(x for x in paths if x) or None,
+            "accuracy": rank0[0]["accuracy"] if rank0 else None}
+
+
+def measure(replicas: int, gpus=None, backend: str = "rccl", timeout: float = 180.0,
+            extra_args=(), name: str = "bench-latency") -> dict:
+    """One job of ``replicas`` pods through the real operator (1 GPU per pod when ``gpus``
+    lists node GPU ids); the dict of ``run_one``.  Used by bench.py after its timed region."""
+    args = ["--backend", backend, *extra_args]
+    gpu = bool(gpus)
+    if not gpu:
+        args.append("--no-cuda")
+    with LocalCluster(gpus=list(gpus) if gpu else None) as c:
+        c.wait_operator_ready()
+        return run_one(c, name, replicas, args, gpu, timeout)
 
 
 def main(argv=None):

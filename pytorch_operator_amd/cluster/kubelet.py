@@ -70,7 +70,16 @@ SCRIPT_MAP = {
 
 
 _POD_SCOPED_ENV = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
-                   "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID", "KUBECONFIG", "PYTHONPATH"}
+                   "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE",
+                   "KUBECONFIG", "PYTHONPATH"}
+# a launcher's (torchrun) per-process state must never leak into a pod: e.g. an inherited
+# TORCHELASTIC_USE_AGENT_STORE makes the pod's env:// rendezvous a client of a store nobody hosts
+_POD_SCOPED_PREFIXES = ("TORCHELASTIC_", "TORCH_ELASTIC_")
+
+
+def _node_env() -> Dict[str, str]:
+    return {k: v for k, v in os.environ.items()
+            if k not in _POD_SCOPED_ENV and not k.startswith(_POD_SCOPED_PREFIXES)}
 
 
 def _now() -> str:
@@ -258,7 +267,7 @@ class PodRunner(threading.Thread):
 
     def _env(self, spec: dict) -> Dict[str, str]:
         # the node's environment minus anything a container must get from its pod spec
-        base = {k: v for k, v in os.environ.items() if k not in _POD_SCOPED_ENV}
+        base = _node_env()
         base["PYTHONPATH"] = os.pathsep.join([self.k.repo_root] + [p for p in
                                             os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
         base["HOSTNAME"] = self.name

@@ -64,6 +64,9 @@ def parse_args(argv=None):
     p.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"], default="auto",
                    help="HIP path, world>1: xGMI peer-memory all-reduce fused with SGD (self-tested, "
                         "RCCL fallback) or RCCL bucket all-reduce")
+    p.add_argument("--xgmi-timeout", type=float, default=5.0,
+                   help="bounded wait (s) inside the xGMI exchange before it flags an error; an error "
+                        "ends the worker with the retryable exit code 138")
     p.add_argument("--model-path", default="mnist_cnn.pt")
     p.add_argument("--checkpoint-dir", default=None,
                    help="write an end-of-epoch checkpoint (weights + optimizer state) here")
@@ -188,6 +191,34 @@ class _Trace:
         return rng()
 
 
+XGMI_FAILED_EXIT = 138  # SIGUSR1-class retryable code (tf-operator train_util.go:18-53)
+
+
+def _xgmi_guard(sync, emit, where: str) -> None:
+    """Fail fast when the fused xGMI exchange timed out: its kernel then falls back to a
+    rank-local SGD and the replicas diverge silently.  Exiting with a retryable code hands
+    the failure to the operator (ExitCode / OnFailure restart, ``--resume``)."""
+    if not getattr(sync, "fused_sgd", False):
+        return
+    code = sync.xar.error()
+    if code:
+        emit("xgmi_error", code=int(code), where=where)
+        print(f"xGMI gradient exchange failed (error {code}) at {where}; "
+              f"exiting with retryable code {XGMI_FAILED_EXIT}", flush=True)
+        os._exit(XGMI_FAILED_EXIT)
+
+
+def _maybe_stall(rank: int, block: int) -> None:
+    """Fault-injection hook: PTO_FAULT_STALL="rank:block:seconds" makes that rank sleep on
+    the host before step block ``block`` (its peers' bounded xGMI waits then time out)."""
+    spec = os.environ.get("PTO_FAULT_STALL")
+    if spec:
+        r, b, sec = spec.split(":")
+        if int(r) == rank and int(b) == block:
+            print(f"fault injection: rank {rank} stalls {sec}s before block {block}", flush=True)
+            time.sleep(float(sec))
+
+
 def _ckpt_path(args):
     return os.path.join(args.checkpoint_dir, "ckpt.pt") if args.checkpoint_dir else None
 
@@ -206,12 +237,13 @@ def _save_ckpt(args, rank, state: dict) -> None:
 
 def _maybe_fault(epoch: int, resumed: bool) -> None:
     """Fault-injection hook for recovery tests: PTO_FAULT_EXIT_AFTER_EPOCH=N makes a
-    fresh (non-resumed) run exit with 137 -- a retryable SIGKILL code -- right after it
-    checkpointed epoch N."""
+    fresh (non-resumed) run exit with PTO_FAULT_EXIT_CODE (default 137, a retryable SIGKILL
+    code; 138 is what a failed xGMI exchange exits with) right after it checkpointed epoch N."""
     n = os.environ.get("PTO_FAULT_EXIT_AFTER_EPOCH")
     if n and not resumed and epoch == int(n):
-        print(f"fault injection: exiting with 137 after epoch {epoch}", flush=True)
-        os._exit(137)
+        code = int(os.environ.get("PTO_FAULT_EXIT_CODE", "137"))
+        print(f"fault injection: exiting with {code} after epoch {epoch}", flush=True)
+        os._exit(code)
 
 
 def _load_ckpt(args):
@@ -259,8 +291,8 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
     if world > 1:
         from ..models.mnist import flat_layout
         from ..parallel.xgmi import try_xgmi
-        sync = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi") \
-            if args.allreduce != "rccl" else None
+        sync = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
+                        timeout_s=args.xgmi_timeout) if args.allreduce != "rccl" else None
         sync = sync or FlatGradAllReduce()
         emit("grad_allreduce", path="xgmi" if getattr(sync, "fused_sgd", False) else "rccl")
     tr = FusedMnistTrainer(batch_size=B, source=src, lr=args.lr, momentum=args.momentum,
@@ -318,11 +350,14 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         with trace(f"epoch{epoch}"):
             while b < steps_per_epoch:
                 chunk = min(log_iv, steps_per_epoch - b)
+                _maybe_stall(rank, b // log_iv)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 with trace("steps"):
                     if runner is not None and chunk % runner.steps_per_graph == 0:
                         runner.run(chunk)
+                    elif runner is not None:
+                        runner.warm(chunk)  # the one-step graph covers an epoch's odd tail
                     else:
                         for _ in range(chunk):
                             tr.train_step()
@@ -331,7 +366,9 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
                 b += chunk
                 if (b - 1) % log_iv == 0:
                     _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer)
+                    _xgmi_guard(sync, emit, f"epoch {epoch} batch {b - 1}")
         torch.cuda.synchronize(dev)
+        _xgmi_guard(sync, emit, f"end of epoch {epoch}")
         t_train += time.perf_counter() - t0
         step_ms += [e0.elapsed_time(e1) / c for e0, e1, c in events]
         steps_done += steps_per_epoch

@@ -128,7 +128,11 @@ class FusedMnistTrainer:
             else torch.zeros(1, device=dev, dtype=torch.int32)
         self.load_state_dict(reference_init(seed))
         self.grad_sync = grad_sync
-        self._first_step = True
+        # torch.optim.SGD's first step sets buf = d_p; with dampening == 0 the steady-state
+        # update buf = momentum * buf + d_p on the zero-initialised buffer is bit-identical
+        # (momentum * 0 + d_p == d_p), so every step -- the first included -- is the same
+        # graph-capturable launch sequence
+        self._first_step = dampening != 0.0
         self.source = source
         self._alloc(self.B)
         self.graph: Optional[torch.cuda.CUDAGraph] = None

@@ -125,8 +125,15 @@ _SIGNATURES = {
     "pto_swiglu_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _VP],
     # adamw.hip
     "pto_adamw_step": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _VP],
+    # graph_exec.hip
+    "pto_graph_begin": [_VP],
+    "pto_graph_end": [_VP, ctypes.POINTER(_VP)],
+    "pto_graph_upload": [_VP, _VP],
+    "pto_graph_launch": [_VP, _VP, _I],
+    "pto_graph_destroy": [_VP],
 }
-_LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I]}
+_LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I],
+             "pto_graph_nodes": [_VP]}
 _VOID_FNS = {"pto_set_debug_buffer": [_VP], "pto_xar_emu_stamps": [_VP, _VP]}
 
 

@@ -22,7 +22,7 @@ def _timed(runner: GraphedStep, steps: int, device) -> float:
     torch.cuda.synchronize(device)
     dist.barrier()
     t0 = time.perf_counter()
-    runner.run(steps)
+    runner.warm(steps)
     torch.cuda.synchronize(device)
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -31,9 +31,11 @@ def _timed(runner: GraphedStep, steps: int, device) -> float:
 
 def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 10,
                      trial_steps: int = 60, force: Optional[str] = None) -> Tuple[GraphedStep, str, dict]:
-    """Returns (runner, "xgmi" | "rccl", per-step times of both trials).  ``force`` overrides
-    the measured decision (tests use it to cover both hand-overs)."""
-    trial = max(spg, trial_steps - trial_steps % spg)
+    """Returns (runner, "xgmi" | "rccl", per-step times of both trials + ``steps``: the
+    training steps taken here).  ``force`` overrides the measured decision (tests use it to
+    cover both hand-overs).  ``spg``: whole steps per replay of the returned xGMI runner's
+    timed graph; the trials replay one-step graphs, so any ``trial_steps`` works."""
+    trial = max(1, int(trial_steps))
     # the RCCL step keeps momentum for every parameter: make it whole if fused xGMI steps
     # ran before (a no-op when it already is)
     xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
@@ -48,7 +50,8 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
     want = (t_xgmi < t_rccl) if force is None else (force == "xgmi")
     flag = torch.tensor([1 if want else 0], dtype=torch.int32, device=tr.device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # unanimous or RCCL
-    times = {"rccl_ms_per_step": round(t_rccl / trial * 1e3, 4), "xgmi_ms_per_step": round(t_xgmi / trial * 1e3, 4)}
+    times = {"rccl_ms_per_step": round(t_rccl / trial * 1e3, 4), "xgmi_ms_per_step": round(t_xgmi / trial * 1e3, 4),
+             "steps": r_rccl.internal_steps + r_xgmi.internal_steps + 2 * trial}
     if flag.item():
         return r_xgmi, "xgmi", times
     xgmi_sync.xar.gather_sharded_(tr.flat_momentum)

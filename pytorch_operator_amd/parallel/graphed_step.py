@@ -19,14 +19,24 @@ Modes
 With the xGMI peer-memory all-reduce (``parallel.xgmi``, ``grad_sync.fused_sgd``) the
 exchange is an ordinary kernel, so ``graph`` captures ``steps_per_graph`` whole DDP
 steps exactly like the single-GPU case.
+
+Whole-step graphs are captured natively (``csrc/kernels/graph_exec.hip``): the step
+launches only this library's kernels, so the HIP runtime can record it directly, and the
+executable graph is staged with ``hipGraphUpload`` right after capture.  Measured on
+MI355X (profiles/r2_launch_overhead.json): a graph's FIRST launch still costs ~0.75 us per
+node more than later ones, while back-to-back launches of a warm graph cost no more than
+one big graph -- so ``warm()`` replays the timed graph itself before falling back to a
+one-step graph for the remainder, and a caller sizes ``steps_per_graph`` to fit its warm-up.
 """
 from __future__ import annotations
 
-from typing import Optional
+import ctypes
+from typing import Callable, Optional
 
 import torch
 
 from ..models.mnist import FusedMnistTrainer
+from ..ops import _native
 
 
 def _capture(fn, device) -> torch.cuda.CUDAGraph:
@@ -36,16 +46,62 @@ def _capture(fn, device) -> torch.cuda.CUDAGraph:
     return g
 
 
+class NativeGraph:
+    """A hipGraph recorded from ``fn`` (which must only launch this library's kernels on
+    the current stream), instantiated and uploaded; ``replay(n)`` launches it n times."""
+
+    def __init__(self, fn: Callable[[], None], device: torch.device):
+        lib = _native.load()
+        self._lib = lib
+        self.device = device
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        h = ctypes.c_void_p()
+        with torch.cuda.stream(s):
+            _native.check(lib.pto_graph_begin(s.cuda_stream), "hipStreamBeginCapture")
+            try:
+                fn()
+            finally:
+                rc = lib.pto_graph_end(s.cuda_stream, ctypes.byref(h))
+        _native.check(rc, "hipStreamEndCapture/hipGraphInstantiate")
+        self._h = h
+        self.nodes = int(lib.pto_graph_nodes(h))
+        _native.check(lib.pto_graph_upload(h, s.cuda_stream), "hipGraphUpload")
+        s.synchronize()
+        torch.cuda.current_stream(device).wait_stream(s)
+
+    def replay(self, n: int = 1) -> None:
+        _native.check(self._lib.pto_graph_launch(
+            self._h, torch.cuda.current_stream(self.device).cuda_stream, int(n)), "hipGraphLaunch")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.pto_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class GraphedStep:
-    def __init__(self, trainer: FusedMnistTrainer, mode: str = "graph", steps_per_graph: int = 1):
+    """Replays whole training steps.  ``run(n)`` needs ``n % steps_per_graph == 0`` (the
+    timed graph); ``warm(n)`` takes any ``n`` (one-step graph)."""
+
+    def __init__(self, trainer: FusedMnistTrainer, mode: str = "graph", steps_per_graph: int = 1,
+                 native: bool = True):
         if mode not in ("eager", "graph", "graph-comm"):
             raise ValueError(f"unknown mode {mode}")
         self.tr = trainer
         self.sync = trainer.grad_sync  # the gradient path these graphs were built for
         self.mode = mode
-        self.steps_per_graph = steps_per_graph if mode != "eager" else 1
+        self.steps_per_graph = max(1, int(steps_per_graph)) if mode != "eager" else 1
         self.world = trainer.grad_sync.world if trainer.grad_sync is not None else 1
-        self._graphs = []
+        self._graph = None   # timed graph: steps_per_graph whole steps
+        self._warm = None    # one whole step (warm-up of any length)
+        self._split = False  # RCCL three-graph step
         self.internal_steps = 0  # untimed steps taken while preparing the graphs
         if mode == "eager":
             return
@@ -54,46 +110,95 @@ class GraphedStep:
             tr.train_step()  # momentum initialisation happens outside any graph
             self.internal_steps += 1
         torch.cuda.synchronize(tr.device)
-        # warm the allocator / RCCL on a side stream before capture (torch recommendation)
-        s = torch.cuda.Stream(device=tr.device)
-        s.wait_stream(torch.cuda.current_stream(tr.device))
-        with torch.cuda.stream(s):
-            tr.train_step()
-        self.internal_steps += 1
-        torch.cuda.current_stream(tr.device).wait_stream(s)
-        torch.cuda.synchronize(tr.device)
-        if self.world == 1 or mode == "graph-comm" or getattr(tr.grad_sync, "fused_sgd", False):
-            def whole():
-                for _ in range(self.steps_per_graph):
-                    tr.train_step()
-            self._graphs = [_capture(whole, tr.device)]
+        whole_step = self.world == 1 or getattr(tr.grad_sync, "fused_sgd", False)
+        if not whole_step or mode == "graph-comm":
+            # torch capture: RCCL collectives need torch's capture bookkeeping.  Warm the
+            # allocator / RCCL on a side stream before capture (torch recommendation).
+            s = torch.cuda.Stream(device=tr.device)
+            s.wait_stream(torch.cuda.current_stream(tr.device))
+            with torch.cuda.stream(s):
+                tr.train_step()
+            self.internal_steps += 1
+            torch.cuda.current_stream(tr.device).wait_stream(s)
+            torch.cuda.synchronize(tr.device)
+        if whole_step:
+            def steps(n):
+                def fn():
+                    for _ in range(n):
+                        tr.train_step()
+                return fn
+            if native:
+                self._graph = NativeGraph(steps(self.steps_per_graph), tr.device)
+                self._warm = self._graph if self.steps_per_graph == 1 else \
+                    NativeGraph(steps(1), tr.device)
+            else:
+                g = _capture(steps(self.steps_per_graph), tr.device)
+                self._graph = _TorchGraph(g)
+                self._warm = self._graph if self.steps_per_graph == 1 else \
+                    _TorchGraph(_capture(steps(1), tr.device))
+        elif mode == "graph-comm":
+            self._graph = self._warm = _TorchGraph(_capture(lambda: tr.train_step(), tr.device))
+            self.steps_per_graph = 1
         else:
             inv = 1.0 / self.world
+            self._split = True
+            self.steps_per_graph = 1
             self._g1 = _capture(lambda: tr.forward_backward_fc(), tr.device)
             self._g2 = _capture(lambda: tr.backward_conv(), tr.device)
             self._g3 = _capture(lambda: tr.optimizer_step(grad_scale=inv), tr.device)
         torch.cuda.synchronize(tr.device)
 
-    def run(self, n_steps: int) -> None:
-        """Execute ``n_steps`` training steps (must be a multiple of steps_per_graph in graph modes)."""
+    def _split_steps(self, n: int) -> None:
         tr = self.tr
-        tr.grad_sync = self.sync
-        if self.mode == "eager":
-            for _ in range(n_steps):
-                tr.train_step()
-            return
-        if self._graphs:
-            if n_steps % self.steps_per_graph:
-                raise ValueError("n_steps must be a multiple of steps_per_graph")
-            g = self._graphs[0]
-            for _ in range(n_steps // self.steps_per_graph):
-                g.replay()
-            return
         sync = tr.grad_sync
-        for _ in range(n_steps):
+        for _ in range(n):
             self._g1.replay()
             sync.fc_ready(tr.fc_bucket())
             self._g2.replay()
             sync.conv_ready(tr.conv_bucket())
             sync.finish()
             self._g3.replay()
+
+    def warm(self, n_steps: int) -> None:
+        """``n_steps`` untimed steps of any count: whole replays of the timed graph first (a
+        hipGraph's first launch costs ~0.75 us per node more than later ones, even after
+        hipGraphUpload -- profiles/r2_launch_overhead.json), then one-step replays."""
+        tr = self.tr
+        tr.grad_sync = self.sync
+        if n_steps <= 0:
+            return
+        if self.mode == "eager":
+            for _ in range(n_steps):
+                tr.train_step()
+        elif self._split:
+            self._split_steps(n_steps)
+        else:
+            full = n_steps // self.steps_per_graph
+            if full:
+                self._graph.replay(full)
+            if n_steps - full * self.steps_per_graph:
+                self._warm.replay(n_steps - full * self.steps_per_graph)
+
+    def run(self, n_steps: int) -> None:
+        """Execute ``n_steps`` training steps (a multiple of steps_per_graph in graph modes)."""
+        tr = self.tr
+        tr.grad_sync = self.sync
+        if self.mode == "eager":
+            for _ in range(n_steps):
+                tr.train_step()
+            return
+        if self._split:
+            self._split_steps(n_steps)
+            return
+        if n_steps % self.steps_per_graph:
+            raise ValueError("n_steps must be a multiple of steps_per_graph")
+        self._graph.replay(n_steps // self.steps_per_graph)
+
+
+class _TorchGraph:
+    def __init__(self, g: torch.cuda.CUDAGraph):
+        self.g = g
+
+    def replay(self, n: int = 1) -> None:
+        for _ in range(n):
+            self.g.replay()

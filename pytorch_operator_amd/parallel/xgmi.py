@@ -281,7 +281,8 @@ class XgmiGradSync:
         return 1.0 / self.world
 
 
-def try_xgmi(n: int, device, required: bool = False, log=print) -> Optional[XgmiGradSync]:
+def try_xgmi(n: int, device, required: bool = False, log=print,
+             timeout_s: float = 5.0) -> Optional[XgmiGradSync]:
     """The self-tested xGMI gradient path, or None (RCCL then carries the gradients).
 
     Only used under RCCL (one GPU per rank) unless ``required`` -- which also lets the
@@ -289,7 +290,7 @@ def try_xgmi(n: int, device, required: bool = False, log=print) -> Optional[Xgmi
     if not required and dist.get_backend() != "nccl":
         return None
     try:
-        xar = XgmiAllReduce(n, device=device)
+        xar = XgmiAllReduce(n, device=device, timeout_s=timeout_s)
     except XgmiUnavailable as e:
         if required:
             raise

@@ -326,18 +326,22 @@ def test_many_concurrent_jobs_with_threadiness(tmp_path):
         assert c.metric_value("pytorch_operator_jobs_successful_total") == 12
 
 
-def test_exit_code_restart_resumes_from_checkpoint(cluster, tmp_path):
-    """Elastic recovery end to end: the worker process dies with 137 after checkpointing
-    epoch 1, the operator recreates the pod (ExitCode policy) and the new pod resumes at
-    epoch 2 from the checkpoint instead of starting over."""
+@pytest.mark.parametrize("code", [137, 138])
+def test_exit_code_restart_resumes_from_checkpoint(cluster, tmp_path, code):
+    """Elastic recovery end to end: the worker process dies with a retryable code after
+    checkpointing epoch 1 (137 = SIGKILL; 138 = what the worker exits with when the xGMI
+    exchange fails, harness/mnist.py ``_xgmi_guard``), the operator recreates the pod
+    (ExitCode policy) and the new pod resumes at epoch 2 from the checkpoint."""
     c = cluster
+    name = f"e2e-resume-{code}"
     args = ["--backend", "gloo", "--dataset-size", "640", "--test-size", "128", "--epochs", "2",
             "--checkpoint-dir", str(tmp_path / "ck"), "--resume"]
     master = replica(1, "pytorch_dist_mnist:latest", args, policy="ExitCode",
-                     extra={"env": [{"name": "PTO_FAULT_EXIT_AFTER_EPOCH", "value": "1"}]})
-    c.rest.create(PYTORCHJOBS, make_job("e2e-resume", master), NS)
-    types, job = wait_finished(c, "e2e-resume", timeout=180)
+                     extra={"env": [{"name": "PTO_FAULT_EXIT_AFTER_EPOCH", "value": "1"},
+                                    {"name": "PTO_FAULT_EXIT_CODE", "value": str(code)}]})
+    c.rest.create(PYTORCHJOBS, make_job(name, master), NS)
+    types, job = wait_finished(c, name, timeout=180)
     assert types[-1] == "Succeeded", job["status"]
-    log = c.rest.pod_log("e2e-resume-master-0", NS)
-    assert "fault injection: exiting with 137 after epoch 1" in log
+    log = c.rest.pod_log(f"{name}-master-0", NS)
+    assert f"fault injection: exiting with {code} after epoch 1" in log
     assert '"event": "resumed"' in log and "Train Epoch: 2 [0/640" in log

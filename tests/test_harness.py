@@ -242,7 +242,8 @@ def test_util_pformat_and_rand_string():
 
 def test_bench_contract_cli_and_graph_chunking():
     """bench.py (driver contract): defaults are N=1 with a K/W that finish in seconds, and the
-    steps-per-graph choice always divides K and W so exactly K steps are timed."""
+    timed graph's size always divides K (exactly K steps are timed) -- independent of W, which
+    runs on a separate one-step graph; K <= 250 is a single replay."""
     import importlib.util
     import os
     spec = importlib.util.spec_from_file_location(
@@ -251,8 +252,11 @@ def test_bench_contract_cli_and_graph_chunking():
     spec.loader.exec_module(bench)
     a = bench.parse_args([])
     assert a.gpus == 1 and a.steps > 0 and a.warmup >= 0
-    for k, w in [(2000, 50), (4000, 100), (100, 10), (7, 3), (5, 1), (30, 0), (1, 1)]:
+    for k, w in [(2000, 50), (4000, 100), (100, 10), (7, 3), (5, 1), (30, 0), (1, 1), (1009, 5), (251, 0)]:
         spg = bench.pick_steps_per_graph(k, w)
-        assert k % spg == 0 and w % spg == 0 and spg >= 1
+        assert k % spg == 0 and 1 <= spg <= 250
+        assert spg <= w or not any(k % d == 0 for d in range(1, min(w, 250) + 1)) or w == 0
+    assert bench.pick_steps_per_graph(20, 5) == 5     # the driver's K/W: warm-up replays it once
     assert bench.pick_steps_per_graph(2000, 50) == 50
-    assert bench.pick_steps_per_graph(7, 3) == 1
+    assert bench.pick_steps_per_graph(2000, 0) == 250
+    assert bench.pick_steps_per_graph(1009, 5) == 1

@@ -35,3 +35,33 @@ def test_xgmi_allreduce_ranks(tmp_path, world):
     assert r.returncode == 0 and len(results) == world, r.stdout[-3000:] + r.stderr[-3000:]
     for res in results:
         assert res["all_ok"], res
+
+
+def test_xgmi_stall_makes_every_rank_exit_retryable(tmp_path):
+    """A rank that stalls past the exchange's bounded wait must not leave the job running
+    rank-local: every rank's worker notices the kernel's error word at its next
+    log interval and exits with the retryable code 138 (tf-operator train_util.go:18-53),
+    which the operator's ExitCode/OnFailure policies restart from the checkpoint."""
+    port = _port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, PYTHONPATH=str(ROOT), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   WORLD_SIZE="2", RANK=str(rank), LOCAL_RANK=str(rank),
+                   PTO_FAULT_STALL="1:3:4")  # rank 1 sleeps 4 s before its 4th step block
+        cmd = [sys.executable, "-u", "-m", "pytorch_operator_amd.harness.mnist", "--backend", "gloo",
+               "--allreduce", "xgmi", "--xgmi-timeout", "0.5", "--dataset-size", "6400",
+               "--test-size", "1000", "--log-interval", "10", "--dir", str(tmp_path / f"tb{rank}")]
+        procs.append(subprocess.Popen(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    codes = [p.returncode for p in procs]
+    assert codes == [138, 138], "\n----\n".join(o[-2500:] for o in outs)
+    for o in outs:
+        assert '"event": "xgmi_error"' in o and '"path": "xgmi"' in o
