@@ -54,6 +54,8 @@ def parse_args(argv=None):
     p.add_argument("--dataset-size", type=int, default=60000)
     p.add_argument("--overlap", type=int, default=0, help="side-stream overlap in the step (1/0)")
     p.add_argument("--fuse-conv12", type=int, default=1)
+    p.add_argument("--schedule", choices=["fused", "classic"], default="classic",
+                   help="single-GPU launch schedule (A/B): 5-launch fused or 6-launch classic")
     p.add_argument("--backend", default="nccl", choices=["nccl", "rccl", "gloo"],
                    help="collective backend (gloo only to rehearse the multi-rank path on one GPU)")
     p.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -64,6 +66,10 @@ def parse_args(argv=None):
                    help="after the timed region, run one PyTorchJob with one pod per GPU through "
                         "the native operator + local cluster and report create->first-step (1/0)")
     p.add_argument("--job-timeout", type=float, default=150.0)
+    p.add_argument("--prewarm-ms", type=int, default=40,
+                   help="keep the GPU busy (FMA spin, no training state touched) this long before "
+                        "the warm-up steps so the timed steps run at steady-state clocks "
+                        "(profiles/r2_cold_start.json); 0 = off")
     return p.parse_args(argv)
 
 
@@ -96,6 +102,20 @@ def job_latency(world: int, rank: int, timeout: float) -> dict:
         from datetime import timedelta
         store.wait(["pto_bench_job_latency"], timedelta(seconds=timeout + 120))
     return out
+
+
+def prewarm(ms: int, dev) -> None:
+    """Sustained GPU activity before the warm-up: a short timed region right after idle pays
+    the power-management clock ramp (~4 % at K=20 on MI355X, profiles/r2_cold_start.json)."""
+    if ms <= 0:
+        return
+    import torch
+    from pytorch_operator_amd.ops import _native
+    sink = torch.empty(256, device=dev)
+    _native.check(_native.load().pto_device_prewarm(int(ms * 1000), sink.data_ptr(),
+                                                    torch.cuda.current_stream(dev).cuda_stream),
+                  "device_prewarm")
+    torch.cuda.synchronize(dev)
 
 
 def main(argv=None):
@@ -136,6 +156,7 @@ def main(argv=None):
                                seed=1, grad_sync=sync)
         tr.overlap = bool(args.overlap)
         tr.fuse_conv12 = bool(args.fuse_conv12)
+        tr.schedule = args.schedule
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph if args.steps_per_graph > 0 else pick_steps_per_graph(args.steps, args.warmup)
@@ -153,13 +174,15 @@ def main(argv=None):
             runner = GraphedStep(tr, mode="graph" if args.mode != "eager" else "eager", steps_per_graph=spg)
         else:
             runner = GraphedStep(tr, mode=args.mode, steps_per_graph=spg)
+        prewarm(args.prewarm_ms, dev)
         runner.warm(max(0, args.warmup - done_w - runner.internal_steps))
 
         def run(n):
             runner.run(n)
         steps = args.steps - args.steps % runner.steps_per_graph
         xgmi_error = (lambda: xg.xar.error()) if xg is not None else (lambda: 0)
-        mode_desc = f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap},allreduce={ar_path})"
+        mode_desc = (f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap},allreduce={ar_path},"
+                     f"schedule={args.schedule})")
     else:
         from pytorch_operator_amd.models.mnist import Net
         import torch.nn.functional as F
@@ -181,6 +204,7 @@ def main(argv=None):
                 loss = F.nll_loss(model(xf[idx]), lab[idx])
                 loss.backward()
                 opt.step()
+        prewarm(args.prewarm_ms, dev)
         run(args.warmup)
         steps = args.steps
         mode_desc = "torch-eager"
@@ -234,6 +258,7 @@ def main(argv=None):
         "vs_baseline": round(value / (BASELINE_PER_RANK * world), 1),
         "replicas_in_sync": in_sync,
         "grad_allreduce_error": ar_err,
+        "device_prewarm_ms": args.prewarm_ms,
         **lat,
         "dtype": "fp32",
         "data": "synthetic (learnable MNIST-shaped uint8 images in HBM), random-init weights",

@@ -89,3 +89,37 @@ int pto_graph_destroy(void* handle) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device pre-warm: keep every CU issuing FMAs for `us` microseconds.
+//
+// Measured on MI355X (profiles/r2_cold_start.json): 20 graph-replayed steps timed right
+// after a short warm-up run ~4 % slower than the same steps after ~30 ms of sustained
+// GPU activity -- the power-management clock ramp, not the step itself.  bench.py runs
+// this before its warm-up steps so a 20-step timed region sees steady-state clocks.  It
+// touches no training state.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) prewarm_kernel(long long ticks, float* sink) {
+  const long long t_end = (long long)wall_clock64() + ticks;  // 100 MHz constant clock
+  float a = threadIdx.x * 1e-3f, b = 1.0001f, c = 0.5f, d = blockIdx.x * 1e-4f;
+  while ((long long)wall_clock64() < t_end) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      a = fmaf(a, b, c);
+      d = fmaf(d, b, a);
+    }
+  }
+  if (a + d == 1234.5f) sink[threadIdx.x] = a + d;  // keep the chain alive
+}
+}  // namespace
+
+extern "C" int pto_device_prewarm(int us, void* sink, void* stream) {
+  if (us <= 0 || us > 1000000 || sink == nullptr) return -1;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+  hipLaunchKernelGGL(prewarm_kernel, dim3(cus * 4), dim3(256), 0, (hipStream_t)stream,
+                     (long long)us * 100, (float*)sink);
+  return (int)hipGetLastError();
+}

@@ -860,6 +860,444 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// E': fc1 input gradient with the head folded in (the training path).
+//   grid = ceil(B/16) * 50 blocks of 512 threads; block (mt, kt) owns samples
+//   mt*16 .. +16 and pooled features kt*16 .. +16 of dz2.  Every block first rebuilds
+//   the head for its 16 samples -- h = relu(part0 + part1 + b1), logits = h W2^T + b2
+//   (MFMA, K split over the 8 waves), log-softmax / NLL / d(logits) (one wave),
+//   dh = (d(logits) W2) * (h > 0) (MFMA) -- in LDS, then runs the dz2 GEMM of the old
+//   job 2 with dh read from LDS.  The 50 kt-blocks of a sample tile recompute the same
+//   head (bit-identical: same code, same order); the kt == 0 block publishes h, dh,
+//   d(logits) and the per-sample (loss, correct) for the weight-gradient jobs.
+//   Recomputing costs ~1 us of MFMA + 84 KB of L2 reads per block and removes the head
+//   launch (a kernel boundary + its own memory round trip, ~5 us on the step's critical
+//   path).  Block -> (mt, kt) = (blk % MT, blk / MT): with MT = 4 the 8 XCDs
+//   (round-robin block placement) each see one sample tile, so its h rows and W2 are
+//   fetched into that XCD's L2 once.
+// ---------------------------------------------------------------------------
+constexpr int H_NT = 512;
+constexpr int H_NW = H_NT / 64;
+constexpr int H_HS = 514;  // h_s / dh_s row stride (== 2 mod 32: lanes (i, g) -> bank 2i + g)
+constexpr int H_WS = 530;  // w2_s row stride (== 18 mod 32: conflict-free row and column reads)
+constexpr int H_DS = 17;   // dl_s row stride
+
+__global__ __launch_bounds__(H_NT) void fc1_bwd_head_kernel(
+    const float* __restrict__ hp, const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ b2, const int* __restrict__ lab, const float* __restrict__ a2,
+    const uint8_t* __restrict__ idx2, const float* __restrict__ w1, float grad_scale,
+    float* __restrict__ dz2, float* __restrict__ h_out, float* __restrict__ dh_out,
+    float* __restrict__ dlogits, float* __restrict__ per_sample, int B, u64* dbg) {
+  __shared__ float h_s[16 * H_HS];  // h, overwritten in place by dh
+  __shared__ float w2_s[10 * H_WS];
+  __shared__ f32x4 red[H_NW][64];
+  __shared__ float dl_s[16 * H_DS];
+  __shared__ float lg_s[16 * H_DS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int MT = (B + 15) >> 4;
+  const int mt = blockIdx.x % MT, kt = blockIdx.x / MT;
+  const bool pub = kt == 0;
+  stamp(dbg, 0);
+
+  // ---- every global load of the block, issued before the first use
+  // (a) dz2 GEMM B operand: W1[k][f], k = 64 wv + 4 s + g (rows >= 500 clamped, their A is 0)
+  const int f = kt * 16 + i;
+  float bv[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bv[s] = w1[(size_t)min(64 * wv + 4 * s + g, 499) * 800 + f];
+  // (b) epilogue operands of threads < 256 (ReLU mask + pool argmax)
+  const int l = (tid & 255) >> 2, r = tid & 3;
+  const int bs = mt * 16 + (l >> 4) * 4 + r;
+  const int ff = kt * 16 + (l & 15);
+  const size_t o = (size_t)min(bs, B - 1) * 800 + ff;
+  float a2o = a2[o];
+  int p = idx2[o];
+  // (c) the two split-K halves of the tile's 16 h rows + b1 (16 x 125 float4 each)
+  const float4* hp4 = reinterpret_cast<const float4*>(hp);
+  const float4* b14 = reinterpret_cast<const float4*>(b1);
+  float4 h0[4], h1[4], bb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = min(tid + k * H_NT, 1999);
+    const int row = e / 125, c4 = e - row * 125;
+    const int rr = min(mt * 16 + row, B - 1);
+    h0[k] = hp4[(size_t)rr * 125 + c4];
+    h1[k] = hp4[(size_t)(B + rr) * 125 + c4];
+    bb[k] = b14[c4];
+  }
+  // (d) W2 (10 x 125 float4)
+  const float4* w24 = reinterpret_cast<const float4*>(w2);
+  float4 wq[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) wq[k] = w24[min(tid + k * H_NT, 1249)];
+  // (e) logits epilogue: b2 of this thread's class (tid & 15); softmax threads: their label
+  const float b2v = b2[min(tid & 15, 9)];
+  const int tlab = lab[min(mt * 16 + (tid & 15), B - 1)];
+
+  // ---- h = relu(part0 + part1 + b1) -> LDS (published by the kt == 0 block); W2 -> LDS
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = tid + k * H_NT;
+    if (e < 2000) {
+      const int row = e / 125, c4 = e - row * 125;
+      const float4 hv = make_float4(fmaxf(h0[k].x + h1[k].x + bb[k].x, 0.f), fmaxf(h0[k].y + h1[k].y + bb[k].y, 0.f),
+                                    fmaxf(h0[k].z + h1[k].z + bb[k].z, 0.f), fmaxf(h0[k].w + h1[k].w + bb[k].w, 0.f));
+      float2* d = reinterpret_cast<float2*>(h_s + row * H_HS + 4 * c4);
+      d[0] = make_float2(hv.x, hv.y);
+      d[1] = make_float2(hv.z, hv.w);
+      if (pub && mt * 16 + row < B) reinterpret_cast<float4*>(h_out)[(size_t)(mt * 16 + row) * 125 + c4] = hv;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int e = tid + k * H_NT;
+    if (e < 1250) {
+      const int j = e / 125, c4 = e - j * 125;
+      float2* d = reinterpret_cast<float2*>(w2_s + j * H_WS + 4 * c4);
+      d[0] = make_float2(wq[k].x, wq[k].y);
+      d[1] = make_float2(wq[k].z, wq[k].w);
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 1);
+
+  // ---- logits partials: M = 16 samples, N = 16 (10 classes), K = 500 in 125 steps, wave w
+  // takes steps w, w + 8, ...; A = h_s[i][4s + g], B = W2[i][4s + g] (0 for i >= 10); four
+  // independent accumulator chains hide the MFMA dependency latency
+  {
+    const int jr = min(i, 9);
+    const int nst = wv < 5 ? 16 : 15;  // 125 = 15 * 8 + 5
+    float av[16], wb[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int s = min(wv + 8 * q, 124);
+      av[q] = h_s[i * H_HS + 4 * s + g];
+      wb[q] = w2_s[jr * H_WS + 4 * s + g];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 c[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float a = q < nst ? av[q] : 0.f;
+      const float bq = i < 10 ? wb[q] : 0.f;
+      c[q & 3] = mfma16x16x4(a, bq, c[q & 3]);
+    }
+    red[wv][lane] = (c[0] + c[1]) + (c[2] + c[3]);
+  }
+  __syncthreads();
+  // ---- logits = sum of the 8 wave partials + b2 -> LDS (thread t: sample t >> 4, class t & 15)
+  if (tid < 256) {
+    const int row = tid >> 4, j = tid & 15;
+    const int src = (row >> 2) * 16 + j, rr = row & 3;  // C[row][j] = lane (j, row >> 2), reg row & 3
+    float x = red[0][src][rr];
+#pragma unroll
+    for (int q = 1; q < H_NW; ++q) x += red[q][src][rr];
+    lg_s[row * H_DS + j] = x + b2v;
+  }
+  __syncthreads();
+  // ---- log-softmax / NLL / d(logits): one thread per sample, no cross-lane traffic
+  if (tid < 16) {
+    const int row = tid;
+    float x[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) x[j] = lg_s[row * H_DS + j];
+    float m = x[0];
+    int pred = 0;
+#pragma unroll
+    for (int j = 1; j < 10; ++j)
+      if (x[j] > m) { m = x[j]; pred = j; }  // first maximum, as torch's argmax
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) se += __expf(x[j] - m);
+    const float lse = m + __logf(se);
+    const int t = tlab;
+    float lt = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j == t) lt = x[j];
+    const int sample = mt * 16 + row;
+    const bool out = pub && sample < B;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float dl = j < 10 ? (__expf(x[j < 10 ? j : 0] - lse) - (j == t ? 1.f : 0.f)) * grad_scale : 0.f;
+      dl_s[row * H_DS + j] = dl;
+      if (out && j < 10) dlogits[(size_t)sample * 10 + j] = dl;
+    }
+    if (out) {
+      per_sample[2 * sample] = lse - lt;
+      per_sample[2 * sample + 1] = pred == t ? 1.f : 0.f;
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 2);
+  // ---- dh = (d(logits) W2) * (h > 0): M = 16 samples, N = 500 (32 tiles, 4 per wave),
+  // K = 10 classes (3 steps of 4); every LDS operand of the wave's 4 tiles first, then the
+  // 4 tiles' MFMAs interleaved; written over h in place (each element has one owner)
+  {
+    float a3[3], b3[4][3], hq[4][4];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) a3[s] = 4 * s + g < 10 ? dl_s[i * H_DS + 4 * s + g] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kc = min((wv * 4 + u) * 16 + i, 499);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) b3[u][s] = w2_s[min(4 * s + g, 9) * H_WS + kc];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hq[u][q] = h_s[(g * 4 + q) * H_HS + kc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = (wv * 4 + u) * 16 + i;
+        const float bq = (4 * s + g < 10 && kk < 500) ? b3[u][s] : 0.f;
+        acc[u] = mfma16x16x4(a3[s], bq, acc[u]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kk = (wv * 4 + u) * 16 + i;
+      if (kk < 500) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int srow = g * 4 + q;
+          const float v = hq[u][q] > 0.f ? acc[u][q] : 0.f;
+          h_s[srow * H_HS + kk] = v;
+          if (pub && mt * 16 + srow < B) dh_out[(size_t)(mt * 16 + srow) * 500 + kk] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 3);
+  // ---- dz2 GEMM: da2[16 samples, 16 features] = dh . W1[:, f]  (K = 500 over 8 waves)
+  {
+    float av[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) av[s] = h_s[i * H_HS + min(64 * wv + 4 * s + g, 499)];
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 c[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float a = 64 * wv + 4 * s + g < 500 ? av[s] : 0.f;
+      c[s & 3] = mfma16x16x4(a, bv[s], c[s & 3]);
+    }
+    asm volatile("" : "+v"(a2o), "+v"(p));
+    red[wv][lane] = (c[0] + c[1]) + (c[2] + c[3]);
+  }
+  __syncthreads();
+  float v = red[0][l][r];
+#pragma unroll
+  for (int q = 1; q < H_NW; ++q) v += red[q][l][r];
+  if (tid < 256 && bs < B) {
+    const float d = a2o > 0.f ? v : 0.f;
+    const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
+    float* z = dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+    z[0] = p == 0 ? d : 0.f;
+    z[1] = p == 1 ? d : 0.f;
+    z[8] = p == 2 ? d : 0.f;
+    z[9] = p == 3 ? d : 0.f;
+  }
+  stamp(dbg, 4);
+}
+
+// ---------------------------------------------------------------------------
+// SGD element update + the fc weight-gradient tiles.  The tiles only depend on the
+// head's outputs (dh, d(logits), h) and a2, so they run in waves of whatever launch has
+// idle ones: conv_bwd's waves 9-15 sit out its col2im / dW_conv1 phases (no MFMA work
+// there), which covers all 1632 tiles at B = 64 (<= 7 per block).  Optionally the SGD of
+// each element is applied in the tile's epilogue (single process: the fc gradients never
+// make an HBM round trip before their update; they are still stored for inspection).
+// ---------------------------------------------------------------------------
+struct SgdHyper {
+  float lr, momentum, dampening, wd, grad_scale;
+  int nesterov, first_step;
+};
+
+__device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
+  float d = gv * hy.grad_scale + hy.wd * pv;
+  if (hy.momentum != 0.f) {
+    mv = hy.first_step ? d : hy.momentum * mv + (1.f - hy.dampening) * d;
+    d = hy.nesterov ? d + hy.momentum * mv : mv;
+  }
+  pv -= hy.lr * d;
+}
+
+struct FcTail {
+  const float *dh, *a2, *dlog, *h, *per_sample;
+  float *p_w1, *m_w1, *g_w1, *p_b1, *m_b1, *g_b1;
+  float *p_w2, *m_w2, *g_w2, *p_b2, *m_b2, *g_b2;
+  float* stats;
+  float loss_scale;
+};
+
+constexpr int FC_NT1 = 1600;  // dW_fc1 tiles: 32 n-tiles x 50 f-tiles of 16 x 16
+constexpr int FC_TILES = FC_NT1 + 32;  // + 32 dW_fc2 n-tiles (10 -> 16 rows)
+
+struct FcGrad {
+  const float *dh, *a2, *dlog, *h, *per_sample;
+  float *p_w1, *m_w1, *g_w1, *p_b1, *m_b1, *g_b1;
+  float *p_w2, *m_w2, *g_w2, *p_b2, *m_b2, *g_b2;
+  float* stats;
+  float loss_scale;
+  SgdHyper hy;
+  int mode;  // 0: off, 1: gradients, 2: gradients + fused SGD
+};
+
+struct FcRegs {
+  float av[16], bv[16], pw[4], mw[4], pb, mb;
+};
+
+// Buffer-descriptor loads (SRSRC, 32-bit lane offset + wave-uniform SGPR offset): one
+// address VGPR for all 16 loads of an operand instead of a 64-bit address each -- with 32
+// loads in flight per lane the flat form needs ~100 VGPRs and spills the host kernel.
+// Out-of-range offsets (rows >= B) read 0 by the descriptor's bounds check.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fc_rsrc(const float* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float fc_ld(__amdgpu_buffer_rsrc_t r, unsigned voff_bytes, int soff_bytes) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
+}
+
+// Loads of tile t for samples 0 .. 63 (and, when `params`, the parameters and momentum the
+// tile's epilogue updates): independent, unpredicated, all in flight at once.
+__device__ __forceinline__ void fc_tile_load(const FcGrad& fc, int t, int base, int B, int lane, FcRegs& r,
+                                             bool params) {
+  (void)base;
+  const int i = lane & 15, g = lane >> 4;
+  if (t < FC_NT1) {
+    const int nt = t / 50, kt = t - nt * 50;
+    const int nc = min(nt * 16 + i, 499), f = kt * 16 + i;
+    const auto rd = fc_rsrc(fc.dh, (unsigned)B * 2000u), ra = fc_rsrc(fc.a2, (unsigned)B * 3200u);
+    const unsigned vd = (unsigned)(g * 500 + nc) * 4u, va = (unsigned)(g * 800 + f) * 4u;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {  // sample 4 s + g
+      r.av[s] = fc_ld(rd, vd, s * 8000);
+      r.bv[s] = fc_ld(ra, va, s * 12800);
+    }
+    if (params) {
+      const auto rp = fc_rsrc(fc.p_w1, 1600000u), rm = fc_rsrc(fc.m_w1, 1600000u);
+      const unsigned vp = (unsigned)((nt * 16 + g * 4) * 800 + f) * 4u;  // rows >= 500: 0, never stored
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        r.pw[q] = fc_ld(rp, vp, q * 3200);
+        r.mw[q] = fc_ld(rm, vp, q * 3200);
+      }
+      r.pb = fc.p_b1[nc];
+      r.mb = fc.m_b1[nc];
+    }
+  } else {
+    const int nt = t - FC_NT1;
+    const int jc = min(i, 9), ncl = min(nt * 16 + i, 499);
+    const auto rl = fc_rsrc(fc.dlog, (unsigned)B * 40u), rh = fc_rsrc(fc.h, (unsigned)B * 2000u);
+    const unsigned vl = (unsigned)(g * 10 + jc) * 4u, vh = (unsigned)(g * 500 + ncl) * 4u;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      r.av[s] = fc_ld(rl, vl, s * 160);
+      r.bv[s] = fc_ld(rh, vh, s * 8000);
+    }
+    if (params) {
+      const auto rp = fc_rsrc(fc.p_w2, 20000u), rm = fc_rsrc(fc.m_w2, 20000u);
+      const unsigned vp = (unsigned)(g * 4 * 500 + ncl) * 4u;  // class rows >= 10: 0, never stored
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        r.pw[q] = fc_ld(rp, vp, q * 2000);
+        r.mw[q] = fc_ld(rm, vp, q * 2000);
+      }
+      r.pb = fc.p_b2[jc];
+      r.mb = fc.m_b2[jc];
+    }
+  }
+}
+
+// One whole tile by one wave (B <= 64: one K chunk, loaded by fc_tile_load(.., base 0, ..,
+// params = mode == 2)); gradient (+ SGD) epilogue; tile 1601 also writes the step's loss
+// statistics.
+template <bool SGD>
+__device__ __forceinline__ void fc_tile_run(const FcGrad& fc, int t, int B, int lane, FcRegs& r) {
+  const int i = lane & 15, g = lane >> 4;
+  const bool w1 = t < FC_NT1;
+  const int nt = w1 ? t / 50 : t - FC_NT1, kt = w1 ? t - nt * 50 : 0;
+  const bool rowv = w1 ? nt * 16 + i < 500 : i < 10;  // valid A row of this lane
+  f32x4 c0 = zero4(), c1 = zero4();
+  float dbsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const bool bvld = 4 * s + g < B;
+    const float a = (bvld && rowv) ? r.av[s] : 0.f;
+    dbsum += a;
+    const float b = bvld ? r.bv[s] : 0.f;
+    if (s & 1) c1 = mfma16x16x4(a, b, c1);
+    else c0 = mfma16x16x4(a, b, c0);
+  }
+  const f32x4 c = c0 + c1;
+  constexpr bool sgd = SGD;
+  const bool bias = w1 ? kt == 0 : nt == 0;
+  if (bias) {
+    dbsum += __shfl_xor(dbsum, 16, 64);
+    dbsum += __shfl_xor(dbsum, 32, 64);
+  }
+  if (w1) {
+    const int f = kt * 16 + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = nt * 16 + g * 4 + q;
+      if (row < 500) {
+        const size_t e = (size_t)row * 800 + f;
+        fc.g_w1[e] = c[q];
+        if (sgd) {
+          sgd_elem(r.pw[q], r.mw[q], c[q], fc.hy);
+          fc.p_w1[e] = r.pw[q];
+          fc.m_w1[e] = r.mw[q];
+        }
+      }
+    }
+    if (bias && g == 0 && rowv) {
+      const int n = nt * 16 + i;
+      fc.g_b1[n] = dbsum;
+      if (sgd) {
+        sgd_elem(r.pb, r.mb, dbsum, fc.hy);
+        fc.p_b1[n] = r.pb;
+        fc.m_b1[n] = r.mb;
+      }
+    }
+  } else {
+    const int n = nt * 16 + i;
+    if (n < 500) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = g * 4 + q;
+        if (j < 10) {
+          fc.g_w2[j * 500 + n] = c[q];
+          if (sgd) {
+            sgd_elem(r.pw[q], r.mw[q], c[q], fc.hy);
+            fc.p_w2[j * 500 + n] = r.pw[q];
+            fc.m_w2[j * 500 + n] = r.mw[q];
+          }
+        }
+      }
+    }
+    if (bias && g == 0 && i < 10) {
+      fc.g_b2[i] = dbsum;
+      if (sgd) {
+        sgd_elem(r.pb, r.mb, dbsum, fc.hy);
+        fc.p_b2[i] = r.pb;
+        fc.m_b2[i] = r.mb;
+      }
+    }
+    if (nt == 1 && fc.per_sample != nullptr && fc.stats != nullptr) {
+      float ls = 0.f, cs = 0.f;
+      for (int bb = lane; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // F: conv backward.  grid = (4 input-channel groups of 5, B samples), F_NT/64 waves.
 //   phase 1   stage dz2[b] (two layouts), the W2 column slice, a1 slice, xn[b], idx1 slice
 //   phase 2a  dcol[64 pos, 125 (ci,kh,kw)] = dz2[b]^T . W2[:, group]   (MFMA, K = 50)
@@ -905,11 +1343,15 @@ constexpr int F_NDZ = 4096 / F_NT;   // dz2 staging: 64 co (50 real) x 64 pos
 constexpr int F_NW2 = (6656 + F_NT - 1) / F_NT;  // W2 slice staging: 52 co x 128 j
 static_assert(F_NT >= 784 && 4096 % F_NT == 0 && 32 % F_NW == 0, "conv_bwd thread mapping");
 
+// FCM = fc tile mode (0: none, 1: gradients, 2: + fused SGD) as a template parameter: the
+// SGD epilogue raises the kernel to 128 VGPRs (the whole register file at 4 waves/SIMD),
+// which modes 0/1 -- the DDP and ranks-sharing-a-GPU paths -- do not pay.
+template <int FCM>
 __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ gw1, float* __restrict__ gb1,
-    float* __restrict__ dz1_out, int slab_stride, int B, u64* dbg) {
+    float* __restrict__ dz1_out, int slab_stride, int B, FcGrad fc, u64* dbg) {
   extern __shared__ float lds[];
   float* dz_s = lds + F_OFF_DZ;
   float* dz80_s = lds + F_OFF_D8;
@@ -925,6 +1367,16 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   stamp(dbg, 0);
+  // fc weight-gradient tiles in the waves the conv phases leave idle: wave 15 - k takes tile
+  // blk + k * (#blocks), k < 7 -- all 1632 tiles when 7 * 4B >= 1632 and B <= 64 (one K
+  // chunk), which the launcher checks (B = 59..64; other batches use fc1_bwd).  The tile
+  // operands are loaded when phase 3 starts (buffer loads: one address VGPR per operand,
+  // so holding them through col2im stays under 100 VGPRs) and the tiles run during phase 4,
+  // where waves 7-15 have no dW_conv1 items.
+  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int fk = 15 - wv;
+  const int ft0 = blk + nblk * fk;
+  const bool fc_wave = FCM != 0 && fk < 7 && ft0 < FC_TILES;
 
   // ---- phase 1: stage (all loads of a thread are independent and unrolled)
   {
@@ -1064,6 +1516,8 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 2);
+  FcRegs fr;  // fc tile operands: in flight during col2im, consumed in phase 4
+  if (fc_wave) fc_tile_load(fc, ft0, 0, B, lane, fr, FCM == 2);
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]
 #pragma unroll
@@ -1106,6 +1560,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 3);
+  if (fc_wave) fc_tile_run<FCM == 2>(fc, ft0, B, lane, fr);
 
   // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU.  As an MFMA GEMM this is
   // M = 5 channels padded to 16 (3/4 of every MFMA wasted, ~3 us); here 400 threads =
@@ -1314,6 +1769,202 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// T: the single-process step tail, one launch:
+//   blocks [0, red_blocks)           slab reduction + SGD(momentum) of the conv params
+//                                    (slab_reduce_sgd_kernel's body);
+//   next T_NJ1 blocks (4 waves)      dW_fc1 = dh^T a2 tiles (MFMA, K = B) + db_fc1, each
+//                                    tile's SGD applied in its epilogue -- the fc1 weight
+//                                    gradient never makes an HBM round trip before its
+//                                    update (it is still stored, for inspection);
+//   last T_NJ3 blocks                dW_fc2 = dlogits^T h + db_fc2 with fused SGD, and the
+//                                    step's loss statistics.
+//   Moving the fc weight gradients here (they only depend on the head's outputs) leaves
+//   the fc1_bwd_head launch with just the dz2 critical path.
+// ---------------------------------------------------------------------------
+constexpr int T_NW = 4;
+constexpr int T_NJ1 = 1600 / T_NW;  // dW_fc1 tiles (32 n-tiles x 50 f-tiles)
+constexpr int T_NJ3 = 32 / T_NW;    // dW_fc2 tiles (32 n-tiles)
+
+__global__ __launch_bounds__(256) void tail_sgd_kernel(
+    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ gout,
+    float* __restrict__ p, float* __restrict__ buf, SgdHyper hy, FcTail fc,
+    int* __restrict__ step_counter, int red_blocks, u64* dbg) {
+  __shared__ float4 red[SR_SL][SR_COLS];
+  stamp(dbg, 0);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int blk = blockIdx.x;
+  if (blk >= red_blocks + T_NJ1) {
+    // dW_fc2[10, 500] = dlogits^T h (M = 10 -> 16, N = 500 -> 32 tiles, K = B) + db_fc2 + stats
+    const int nt = (blk - red_blocks - T_NJ1) * T_NW + wv;  // 0..31
+    const int jc = min(i, 9);
+    const int nn = nt * 16 + i, ncl = min(nn, 499);
+    float pw[4], mw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = min(g * 4 + q, 9);
+      pw[q] = fc.p_w2[j * 500 + ncl];
+      mw[q] = fc.m_w2[j * 500 + ncl];
+    }
+    float pb = fc.p_b2[jc], mb = fc.m_b2[jc];
+    const bool do_stats = nt == 1 && fc.per_sample != nullptr && fc.stats != nullptr;
+    float ls = 0.f, cs = 0.f;
+    if (do_stats && lane < B) { ls = fc.per_sample[2 * lane]; cs = fc.per_sample[2 * lane + 1]; }
+    f32x4 c0 = zero4(), c1 = zero4();
+    float dbsum = 0.f;
+    for (int base = 0; base < B; base += 64) {
+      float av[16], hv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int bb = min(base + 4 * s + g, B - 1);
+        av[s] = fc.dlog[(size_t)bb * 10 + jc];
+        hv[s] = fc.h[(size_t)bb * 500 + ncl];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const bool bvld = base + 4 * s + g < B;
+        const float a = (bvld && i < 10) ? av[s] : 0.f;
+        dbsum += a;
+        const float hb = bvld ? hv[s] : 0.f;
+        if (s & 1) c1 = mfma16x16x4(a, hb, c1);
+        else c0 = mfma16x16x4(a, hb, c0);
+      }
+    }
+    const f32x4 c = c0 + c1;
+    if (nn < 500) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = g * 4 + q;
+        if (j < 10) {
+          sgd_elem(pw[q], mw[q], c[q], hy);
+          fc.g_w2[j * 500 + nn] = c[q];
+          fc.p_w2[j * 500 + nn] = pw[q];
+          fc.m_w2[j * 500 + nn] = mw[q];
+        }
+      }
+    }
+    if (nt == 0) {
+      dbsum += __shfl_xor(dbsum, 16, 64);
+      dbsum += __shfl_xor(dbsum, 32, 64);
+      if (g == 0 && i < 10) {
+        sgd_elem(pb, mb, dbsum, hy);
+        fc.g_b2[i] = dbsum;
+        fc.p_b2[i] = pb;
+        fc.m_b2[i] = mb;
+      }
+    }
+    if (do_stats) {
+      for (int bb = lane + 64; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
+    }
+    stamp(dbg, 1);
+    return;
+  }
+  if (blk >= red_blocks) {
+    // dW_fc1[500, 800] = dh^T a2 tile (n 16 x f 16, K = B) + fused SGD; db_fc1 (kt == 0)
+    const int tile = (blk - red_blocks) * T_NW + wv;
+    const int nt = tile / 50, kt = tile - nt * 50;
+    const int nn = nt * 16 + i, f = kt * 16 + i;
+    const bool nv = nn < 500;
+    const int nc = nv ? nn : 499;
+    float pw[4], mw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = min(nt * 16 + g * 4 + q, 499);
+      pw[q] = fc.p_w1[(size_t)row * 800 + f];
+      mw[q] = fc.m_w1[(size_t)row * 800 + f];
+    }
+    float pb = 0.f, mb = 0.f;
+    if (kt == 0) { pb = fc.p_b1[nc]; mb = fc.m_b1[nc]; }
+    f32x4 c0 = zero4(), c1 = zero4();
+    float dbsum = 0.f;
+    for (int base = 0; base < B; base += 64) {
+      float av[16], fv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int bb = min(base + 4 * s + g, B - 1);
+        av[s] = fc.dh[(size_t)bb * 500 + nc];
+        fv[s] = fc.a2[(size_t)bb * 800 + f];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const bool bvld = base + 4 * s + g < B;
+        const float a = (bvld && nv) ? av[s] : 0.f;
+        dbsum += a;
+        const float fb = bvld ? fv[s] : 0.f;
+        if (s & 1) c1 = mfma16x16x4(a, fb, c1);
+        else c0 = mfma16x16x4(a, fb, c0);
+      }
+    }
+    const f32x4 c = c0 + c1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = nt * 16 + g * 4 + q;
+      if (row < 500) {
+        const size_t e = (size_t)row * 800 + f;
+        sgd_elem(pw[q], mw[q], c[q], hy);
+        fc.g_w1[e] = c[q];
+        fc.p_w1[e] = pw[q];
+        fc.m_w1[e] = mw[q];
+      }
+    }
+    if (kt == 0) {
+      dbsum += __shfl_xor(dbsum, 16, 64);
+      dbsum += __shfl_xor(dbsum, 32, 64);
+      if (g == 0 && nv) {
+        sgd_elem(pb, mb, dbsum, hy);
+        fc.g_b1[nn] = dbsum;
+        fc.p_b1[nn] = pb;
+        fc.m_b1[nn] = mb;
+      }
+    }
+    stamp(dbg, 1);
+    return;
+  }
+  // slab reduction + SGD of the conv params (see slab_reduce_sgd_kernel)
+  const int col = blk * SR_COLS + (tid % SR_COLS);
+  const int slice = tid / SR_COLS;
+  const int n4 = n >> 2, s4 = stride >> 2;
+  const int cc = min(col, n4 - 1);
+  const float4* P4 = reinterpret_cast<const float4*>(P);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int per = (B + SR_SL - 1) / SR_SL;
+  const int b0 = slice * per, b1 = min(B, b0 + per);
+  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bq = pp;
+  if (tid < SR_COLS) {
+    pp = reinterpret_cast<const float4*>(p)[cc];
+    bq = reinterpret_cast<const float4*>(buf)[cc];
+  }
+  for (int base = b0; base < b1; base += SR_CH) {
+    float4 v[SR_CH];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k)
+      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+  }
+  red[slice][tid % SR_COLS] = acc;
+  __syncthreads();
+  if (tid < SR_COLS && col < n4) {
+    float4 rr = red[0][tid];
+#pragma unroll
+    for (int q = 1; q < SR_SL; ++q) { rr.x += red[q][tid].x; rr.y += red[q][tid].y; rr.z += red[q][tid].z; rr.w += red[q][tid].w; }
+    if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = rr;
+    sgd_elem(pp.x, bq.x, rr.x, hy);
+    sgd_elem(pp.y, bq.y, rr.y, hy);
+    sgd_elem(pp.z, bq.z, rr.z, hy);
+    sgd_elem(pp.w, bq.w, rr.w, hy);
+    reinterpret_cast<float4*>(p)[col] = pp;
+    reinterpret_cast<float4*>(buf)[col] = bq;
+  }
+  if (step_counter != nullptr && blk == 0 && tid == 0) atomicAdd(step_counter, 1);
+  stamp(dbg, 1);
+}
+
+// ---------------------------------------------------------------------------
 // H: SGD with momentum over a flat fp32 buffer (torch.optim.SGD semantics:
 // buf = momentum*buf + (1-dampening)*g (buf = g on the first step),
 // p -= lr * (nesterov ? g + momentum*buf : buf)); grad_scale folds the DDP 1/world.
@@ -1376,6 +2027,43 @@ u64* g_dbg = nullptr;  // phase-timestamp buffer (tools/phase_profile.py); null 
 // Returns hipSuccess (0) or a hipError_t / -1 for a host-side shape error.
 // ===========================================================================
 #define PTO_CHECK_B(B) do { if ((B) <= 0 || (B) > (1 << 20)) return -1; } while (0)
+
+static bool conv_bwd_fc_supported(int B) { return B <= 64 && 7 * 4 * B >= FC_TILES; }
+
+template <int FCM>
+static int conv_bwd_launch_t(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                             const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
+                             float* dz1_out, int slab_stride, int B, const FcGrad& fc, void* stream) {
+  // > 64 KB of dynamic LDS must be opted into once per device and instantiation
+  // (thread-safe: several host threads may drive different GPUs through this library)
+  static std::atomic<unsigned> attr_set{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
+  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel<FCM>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             F_LDS * (int)sizeof(float));
+    if (e != hipSuccess) return (int)e;
+    attr_set.fetch_or(1u << dev, std::memory_order_release);
+  }
+  hipLaunchKernelGGL(conv_bwd_kernel<FCM>, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float),
+                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
+                     slab_stride, B, fc, g_dbg);
+  return (int)hipGetLastError();
+}
+
+static int conv_bwd_launch(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                           const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
+                           float* dz1_out, int slab_stride, int B, const FcGrad& fc, void* stream) {
+  PTO_CHECK_B(B);
+  if (slab_stride < 0) return -1;
+  switch (fc.mode) {
+    case 0: return conv_bwd_launch_t<0>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
+    case 1: return conv_bwd_launch_t<1>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
+    case 2: return conv_bwd_launch_t<2>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
+    default: return -1;
+  }
+}
 
 extern "C" {
 
@@ -1476,24 +2164,39 @@ int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, con
 int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
                        const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
                        float* dz1_out, int slab_stride, int B, void* stream) {
-  PTO_CHECK_B(B);
-  if (slab_stride < 0) return -1;
-  // > 64 KB of dynamic LDS must be opted into once per device (thread-safe: several
-  // host threads may drive different GPUs through this library)
-  static std::atomic<unsigned> attr_set{0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
-  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             F_LDS * (int)sizeof(float));
-    if (e != hipSuccess) return (int)e;
-    attr_set.fetch_or(1u << dev, std::memory_order_release);
+  FcGrad fc{};
+  fc.mode = 0;
+  return conv_bwd_launch(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
+}
+
+// conv backward + the fc weight-gradient tiles in its idle waves (fc_mode 1: gradients,
+// 2: gradients + fused SGD with the given hyper-parameters) + the step's loss statistics.
+int pto_mnist_conv_bwd_fc(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                          const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
+                          int slab_stride, int B, int fc_mode, const float* dh, const float* a2,
+                          const float* dlog, const float* h, const float* per_sample, float* p_w1,
+                          float* m_w1, float* g_w1, float* p_b1, float* m_b1, float* g_b1,
+                          float* p_w2, float* m_w2, float* g_w2, float* p_b2, float* m_b2,
+                          float* g_b2, float* stats, float loss_scale, float lr, float momentum,
+                          float dampening, float wd, float grad_scale, int nesterov, int first_step,
+                          void* stream) {
+  if (fc_mode < 1 || fc_mode > 2) return -1;
+  if (!conv_bwd_fc_supported(B)) return -3;  // every tile needs a wave: B in [59, 64]
+  const float* ins[] = {dh, a2, dlog, h};
+  for (const float* q : ins)
+    if (q == nullptr) return -1;
+  float* grads[] = {g_w1, g_b1, g_w2, g_b2};
+  for (float* q : grads)
+    if (q == nullptr) return -1;
+  if (fc_mode == 2) {
+    float* ps[] = {p_w1, m_w1, p_b1, m_b1, p_w2, m_w2, p_b2, m_b2};
+    for (float* q : ps)
+      if (q == nullptr) return -1;
   }
-  hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float),
-                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
-                     slab_stride, B, g_dbg);
-  return (int)hipGetLastError();
+  FcGrad fc{dh, a2, dlog, h, per_sample, p_w1, m_w1, g_w1, p_b1, m_b1, g_b1,
+            p_w2, m_w2, g_w2, p_b2, m_b2, g_b2, stats, loss_scale,
+            SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step}, fc_mode};
+  return conv_bwd_launch(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, nullptr, slab_stride, B, fc, stream);
 }
 
 int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, void* stream) {
@@ -1538,6 +2241,54 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
                      nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks, g_dbg);
   return (int)hipGetLastError();
 }
+
+// fc1 input gradient with the head folded in (training path): dz2, and from the kt == 0
+// blocks h, dh, d(logits), per-sample (loss, correct).  hp = split-K halves [2][B][500].
+int pto_mnist_fc1_bwd_head(const float* hp, const float* b1, const float* w2, const float* b2,
+                           const int* lab, const float* a2, const uint8_t* idx2, const float* w1,
+                           float grad_scale, float* dz2, float* h_out, float* dh_out,
+                           float* dlogits, float* per_sample, int B, void* stream) {
+  PTO_CHECK_B(B);
+  if (lab == nullptr || h_out == nullptr || dh_out == nullptr || dlogits == nullptr ||
+      per_sample == nullptr)
+    return -1;
+  if ((((uintptr_t)hp) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out)) & 15) return -2;
+  const int blocks = ((B + 15) / 16) * 50;
+  hipLaunchKernelGGL(fc1_bwd_head_kernel, dim3(blocks), dim3(H_NT), 0, (hipStream_t)stream, hp, b1,
+                     w2, b2, lab, a2, idx2, w1, grad_scale, dz2, h_out, dh_out, dlogits,
+                     per_sample, B, g_dbg);
+  return (int)hipGetLastError();
+}
+
+// Single-process step tail: conv slab reduction + SGD, dW_fc1 / dW_fc2 (+ biases) with
+// fused SGD, loss statistics, batch-cursor advance -- one launch.
+int pto_mnist_tail_sgd(const float* P, int B, int n, int stride, float* gout, float* p, float* buf,
+                       float lr, float momentum, float dampening, float wd, float grad_scale,
+                       int nesterov, int first_step, int* step_counter, const float* dh,
+                       const float* a2, const float* dlog, const float* h, const float* per_sample,
+                       float* p_w1, float* m_w1, float* g_w1, float* p_b1, float* m_b1, float* g_b1,
+                       float* p_w2, float* m_w2, float* g_w2, float* p_b2, float* m_b2, float* g_b2,
+                       float* stats, float loss_scale, void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf)) & 15) return -2;
+  const float* ins[] = {dh, a2, dlog, h};
+  for (const float* q : ins)
+    if (q == nullptr) return -1;
+  float* outs[] = {p_w1, m_w1, g_w1, p_b1, m_b1, g_b1, p_w2, m_w2, g_w2, p_b2, m_b2, g_b2};
+  for (float* q : outs)
+    if (q == nullptr) return -1;
+  SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  FcTail fc{dh, a2, dlog, h, per_sample, p_w1, m_w1, g_w1, p_b1, m_b1, g_b1,
+            p_w2, m_w2, g_w2, p_b2, m_b2, g_b2, stats, loss_scale};
+  const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
+  hipLaunchKernelGGL(tail_sgd_kernel, dim3(red_blocks + T_NJ1 + T_NJ3), dim3(256), 0,
+                     (hipStream_t)stream, P, B, n, stride, gout, p, buf, hy, fc, step_counter,
+                     red_blocks, g_dbg);
+  return (int)hipGetLastError();
+}
+
+int pto_conv_bwd_fc_supported(int B) { return conv_bwd_fc_supported(B) ? 1 : 0; }
 
 int pto_conv_bwd_lds_bytes() { return F_LDS * (int)sizeof(float); }
 

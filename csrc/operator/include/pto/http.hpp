@@ -10,6 +10,7 @@
 #include <atomic>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <thread>
@@ -26,6 +27,7 @@ struct Url {
 struct TlsConfig {
   std::string ca_file, cert_file, key_file;
   std::string ca_data, cert_data, key_data;  // PEM (kubeconfig *-data, base64-decoded)
+  std::string server_name;  // kubeconfig tls-server-name: name checked instead of the URL host
   bool insecure_skip_verify = false;
 };
 
@@ -50,6 +52,8 @@ class HttpClient {
                    const std::atomic<bool>* stop, double idle_timeout_s, std::string* error);
 
   const Url& url() const { return url_; }
+  // Replace the bearer token (exec-plugin credential refresh); thread-safe.
+  void set_bearer_token(std::string token);
 
  private:
   struct Conn;
@@ -58,8 +62,10 @@ class HttpClient {
                             const std::string& body, const std::string& content_type, bool keepalive);
 
   Url url_;
+  std::string init_error_;  // TLS material that failed to load (reported per request)
   TlsConfig tls_;
   std::string token_;
+  mutable std::mutex token_mu_;
   double timeout_s_;
   void* ssl_ctx_ = nullptr;  // SSL_CTX*
 };

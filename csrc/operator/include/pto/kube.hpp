@@ -13,18 +13,32 @@
 #include <mutex>
 #include <optional>
 #include <string>
+#include <vector>
 
 #include "pto/http.hpp"
 #include "pto/json.hpp"
 
 namespace pto {
 
+// kubeconfig users[].user.exec credential plugin (client.authentication.k8s.io).
+struct ExecPlugin {
+  std::string command;
+  std::vector<std::string> args;
+  std::vector<std::pair<std::string, std::string>> env;
+  std::string api_version = "client.authentication.k8s.io/v1";
+};
+
 struct KubeConfig {
   std::string server;  // https://host:port
   std::string token;
   TlsConfig tls;
   std::string ns = "default";  // current-context namespace
+  std::optional<ExecPlugin> exec;
 };
+
+// Runs an exec plugin and applies its ExecCredential (token and/or client certificate)
+// to `kc`.  false + *error on failure.
+bool run_exec_plugin(const ExecPlugin& plugin, KubeConfig* kc, std::string* error);
 
 // --master/--kubeconfig/KUBECONFIG/in-cluster.  Returns nullopt + error on failure.
 std::optional<KubeConfig> load_kube_config(const std::string& master_url, const std::string& kubeconfig,

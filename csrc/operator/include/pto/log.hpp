@@ -18,6 +18,12 @@ void log_msg(LogLevel lvl, const LogFields& fields, const char* file, int line, 
     __attribute__((format(printf, 5, 6)));
 
 LogFields fields_for_job(const std::string& ns, const std::string& name, const std::string& uid = "");
+// LoggerForReplica / LoggerForPod (tf-operator/pkg/logger/logger.go:26-56): + replica-type
+// (lower-case), + pod=<ns>.<pod name>
+LogFields fields_for_replica(const std::string& ns, const std::string& name, const std::string& uid,
+                             const std::string& rtype);
+LogFields fields_for_pod(const std::string& ns, const std::string& job, const std::string& uid,
+                         const std::string& rtype, const std::string& pod);
 LogFields fields_for_key(const std::string& key);
 
 #define PTO_LOG(lvl, fields, ...) ::pto::log_msg(lvl, fields, __FILE__, __LINE__, __VA_ARGS__)

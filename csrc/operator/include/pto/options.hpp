@@ -28,6 +28,9 @@ struct ServerOption {
   // leader-election timings (client-go LeaderElectionConfig; reference hardcodes 15s/5s/3s)
   double lease_duration_s = 15.0, renew_deadline_s = 5.0, retry_period_s = 3.0;
   bool inject_rccl_env = false;
+  bool xgmi_pod_topology = false;
+  std::vector<std::pair<std::string, std::string>> rccl_env;  // --rccl-env KEY=VALUE (repeatable)
+  bool rccl_env_set = false;
   std::string init_container_template_file = "/etc/config/initContainer.yaml";
   std::string log_level = "info";
 };

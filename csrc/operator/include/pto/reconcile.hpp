@@ -35,13 +35,21 @@ struct ControllerConfig {
   std::string init_container_image = "alpine:3.10";
   std::string init_container_template = kDefaultInitContainerTemplate;
   // MI355X extensions (all off by default = reference behaviour):
-  // inject LOCAL_RANK (=0: one GPU per pod) and the RCCL tuning env below into
-  // every "pytorch" container that does not already set them.
+  // inject LOCAL_RANK (=0: one GPU per pod) and the env below into every "pytorch"
+  // container that does not already set them.  The default set holds only what the
+  // IPC path needs; tuning variables (e.g. NCCL_MIN_NCHANNELS, NCCL_PROTO) are added
+  // with --rccl-env KEY=VALUE once measured on the target node (docs/xgmi_pods.md).
   bool inject_rccl_env = false;
   std::vector<std::pair<std::string, std::string>> rccl_env = {
-      {"NCCL_MIN_NCHANNELS", "16"},  // spread a ring over the 7 xGMI links
-      {"HSA_ENABLE_IPC_MODE_LEGACY", "0"},
+      {"HSA_ENABLE_IPC_MODE_LEGACY", "0"},  // dmabuf IPC (what current amdgpu drivers support)
   };
+  // One node, one GPU per pod, peer memory over xGMI (docs/xgmi_pods.md): for replicas
+  // that request amd.com/gpu, share the node's PID namespace (dmabuf IPC import reads the
+  // exporter's /proc/<pid>/fd/<fd>), its IPC namespace and /dev/shm (RCCL SHM transport),
+  // give RCCL the node identity (NCCL_HOSTID <- spec.nodeName: pods otherwise hash as
+  // different hosts and fall back to the network transport) and co-locate the job's pods
+  // on one node (required pod affinity on kubernetes.io/hostname).
+  bool xgmi_pod_topology = false;
 };
 
 struct Event {
@@ -54,6 +62,7 @@ struct Event {
 
 struct ObjectRef {
   std::string ns, name;
+  std::string replica_type;  // pods: pytorch-replica-type label (log field), "" for services
 };
 
 struct MetricDeltas {

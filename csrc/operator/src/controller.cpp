@@ -113,7 +113,20 @@ void EventSink::flush(double timeout_s) {
   }
 }
 
+// Posts events on its own thread.  Repeats are aggregated like client-go's EventCorrelator
+// (vendor/k8s.io/client-go/tools/record/events_cache.go): an event with the same involved
+// object, type, reason and message as one posted less than kEventDedupS ago is a PATCH of
+// that Event's count and lastTimestamp, not a new object -- a crash-looping job does not
+// flood the namespace.  The cache is owned by this thread (no locking) and bounded.
 void EventSink::loop() {
+  constexpr double kEventDedupS = 600.0;
+  constexpr size_t kCacheMax = 4096;
+  struct Seen {
+    std::string name, ns;
+    long long count;
+    double last;
+  };
+  std::map<std::string, Seen> seen;
   while (true) {
     Json ev;
     {
@@ -124,8 +137,34 @@ void EventSink::loop() {
       q_.pop_front();
       inflight_++;
     }
+    const Json* io = ev.get("involvedObject");
+    const std::string ns = meta_str(ev, "namespace");
+    const std::string key = ns + "\x1f" + (io ? io->str_or("uid") + "\x1f" + io->str_or("name") : "") + "\x1f" +
+                            ev.str_or("type") + "\x1f" + ev.str_or("reason") + "\x1f" + ev.str_or("message");
+    const double now = mono();
     ApiError err;
-    client_->create(kEvents, meta_str(ev, "namespace"), ev, &err);
+    bool done = false;
+    auto it = seen.find(key);
+    if (it != seen.end() && now - it->second.last < kEventDedupS) {
+      Json patch = Json::object();
+      patch["count"] = it->second.count + 1;
+      patch["lastTimestamp"] = ev.str_or("lastTimestamp");
+      if (client_->patch_merge(kEvents, it->second.ns, it->second.name, patch, &err)) {
+        it->second.count++;
+        it->second.last = now;
+        done = true;
+      }
+    }
+    if (!done) {
+      if (seen.size() >= kCacheMax) {  // drop the stalest entry
+        auto oldest = seen.begin();
+        for (auto j = seen.begin(); j != seen.end(); ++j)
+          if (j->second.last < oldest->second.last) oldest = j;
+        seen.erase(oldest);
+      }
+      ApiError e2;
+      if (client_->create(kEvents, ns, ev, &e2)) seen[key] = Seen{meta_str(ev, "name"), ns, 1, now};
+    }
     std::lock_guard<std::mutex> g(mu_);
     inflight_--;
   }
@@ -368,7 +407,11 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
       events_.record(job, {"Warning", "FailedDeletePod", "Error deleting: " + e2.message});
       return "unable to delete pods: " + e2.message;
     }
-    if (!e2.not_found()) events_.record(job, {"Normal", "SuccessfulDeletePod", "Deleted pod: " + d.name});
+    if (!e2.not_found()) {
+      events_.record(job, {"Normal", "SuccessfulDeletePod", "Deleted pod: " + d.name});
+      PTO_LOG(LogLevel::Info, fields_for_pod(d.ns, job_name(job), job_uid(job), d.replica_type, d.name),
+              "Deleted pod %s", d.name.c_str());
+    }
   }
   // expectations: count creations per key, then set once (k8s ReplicaSet style)
   std::map<std::string, int> want;
@@ -386,6 +429,12 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
       return "create pod " + pname + ": " + e2.message;
     }
     events_.record(job, {"Normal", "SuccessfulCreatePod", "Created pod: " + pname});
+    {
+      const Json* lb = r.create_pods[i].path({"metadata", "labels"});
+      PTO_LOG(LogLevel::Info,
+              fields_for_pod(ns, job_name(job), job_uid(job), lb ? lb->str_or(kLabelReplicaType) : "", pname),
+              "Created pod %s", pname.c_str());
+    }
   }
   for (size_t i = 0; i < r.create_services.size(); ++i) {
     ApiError e2;

@@ -12,6 +12,7 @@
 #include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509.h>
+#include <openssl/x509v3.h>
 
 #include <chrono>
 #include <cstring>
@@ -156,38 +157,61 @@ static bool load_pem_ca(SSL_CTX* ctx, const std::string& pem) {
   return any;
 }
 
+static std::string ssl_err(const char* what) {
+  char buf[256];
+  ERR_error_string_n(ERR_get_error(), buf, sizeof buf);
+  ERR_clear_error();
+  return std::string(what) + ": " + buf;
+}
+
+// Verification follows client-go: the server certificate must chain to the configured CA
+// (kubeconfig certificate-authority[-data], the service-account ca.crt in-cluster, else the
+// system store) AND name the host -- the URL's host, or tls-server-name when set; an IP
+// literal is matched against the certificate's IP SANs.  A credential that fails to load
+// is an error on every request (never a silent anonymous/unverified connection).
 HttpClient::HttpClient(Url url, TlsConfig tls, std::string bearer_token, double timeout_s)
     : url_(std::move(url)), tls_(std::move(tls)), token_(std::move(bearer_token)), timeout_s_(timeout_s) {
   if (url_.scheme == "https") {
     SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+    SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
     if (tls_.insecure_skip_verify) {
       SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
     } else {
       SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
-      if (!tls_.ca_file.empty()) SSL_CTX_load_verify_locations(ctx, tls_.ca_file.c_str(), nullptr);
-      if (!tls_.ca_data.empty()) load_pem_ca(ctx, tls_.ca_data);
+      if (!tls_.ca_file.empty() && SSL_CTX_load_verify_locations(ctx, tls_.ca_file.c_str(), nullptr) != 1)
+        init_error_ = ssl_err(("cannot load CA file " + tls_.ca_file).c_str());
+      if (!tls_.ca_data.empty() && !load_pem_ca(ctx, tls_.ca_data))
+        init_error_ = "certificate-authority-data holds no PEM certificate";
       if (tls_.ca_file.empty() && tls_.ca_data.empty()) SSL_CTX_set_default_verify_paths(ctx);
     }
-    if (!tls_.cert_file.empty()) SSL_CTX_use_certificate_chain_file(ctx, tls_.cert_file.c_str());
-    if (!tls_.key_file.empty()) SSL_CTX_use_PrivateKey_file(ctx, tls_.key_file.c_str(), SSL_FILETYPE_PEM);
+    if (!tls_.cert_file.empty() && SSL_CTX_use_certificate_chain_file(ctx, tls_.cert_file.c_str()) != 1)
+      init_error_ = ssl_err(("cannot load client certificate " + tls_.cert_file).c_str());
+    if (!tls_.key_file.empty() && SSL_CTX_use_PrivateKey_file(ctx, tls_.key_file.c_str(), SSL_FILETYPE_PEM) != 1)
+      init_error_ = ssl_err(("cannot load client key " + tls_.key_file).c_str());
     if (!tls_.cert_data.empty()) {
       BIO* b = BIO_new_mem_buf(tls_.cert_data.data(), (int)tls_.cert_data.size());
-      if (X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr)) {
-        SSL_CTX_use_certificate(ctx, x);
-        X509_free(x);
-      }
+      X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr);
+      if (x == nullptr || SSL_CTX_use_certificate(ctx, x) != 1) init_error_ = ssl_err("client-certificate-data");
+      if (x) X509_free(x);
       BIO_free(b);
     }
     if (!tls_.key_data.empty()) {
       BIO* b = BIO_new_mem_buf(tls_.key_data.data(), (int)tls_.key_data.size());
-      if (EVP_PKEY* k = PEM_read_bio_PrivateKey(b, nullptr, nullptr, nullptr)) {
-        SSL_CTX_use_PrivateKey(ctx, k);
-        EVP_PKEY_free(k);
-      }
+      EVP_PKEY* k = PEM_read_bio_PrivateKey(b, nullptr, nullptr, nullptr);
+      if (k == nullptr || SSL_CTX_use_PrivateKey(ctx, k) != 1) init_error_ = ssl_err("client-key-data");
+      if (k) EVP_PKEY_free(k);
       BIO_free(b);
     }
+    if (init_error_.empty() && (!tls_.cert_file.empty() || !tls_.cert_data.empty()) &&
+        SSL_CTX_check_private_key(ctx) != 1)
+      init_error_ = ssl_err("client certificate and key do not match");
     ssl_ctx_ = ctx;
   }
+}
+
+void HttpClient::set_bearer_token(std::string token) {
+  std::lock_guard<std::mutex> g(token_mu_);
+  token_ = std::move(token);
 }
 
 HttpClient::~HttpClient() {
@@ -195,6 +219,10 @@ HttpClient::~HttpClient() {
 }
 
 std::unique_ptr<HttpClient::Conn> HttpClient::connect(std::string* error, double timeout_s) {
+  if (!init_error_.empty()) {
+    *error = init_error_;
+    return nullptr;
+  }
   struct addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;
@@ -226,11 +254,28 @@ std::unique_ptr<HttpClient::Conn> HttpClient::connect(std::string* error, double
   if (ssl_ctx_) {
     conn->ssl = SSL_new((SSL_CTX*)ssl_ctx_);
     SSL_set_fd(conn->ssl, conn->fd);
-    SSL_set_tlsext_host_name(conn->ssl, url_.host.c_str());
+    const std::string& name = tls_.server_name.empty() ? url_.host : tls_.server_name;
+    unsigned char ip[16];
+    const bool is_ip = inet_pton(AF_INET, name.c_str(), ip) == 1 || inet_pton(AF_INET6, name.c_str(), ip) == 1;
+    if (!is_ip) SSL_set_tlsext_host_name(conn->ssl, name.c_str());  // SNI carries DNS names only
+    if (!tls_.insecure_skip_verify) {
+      int ok;
+      if (is_ip) {
+        ok = X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(conn->ssl), name.c_str());
+      } else {
+        SSL_set_hostflags(conn->ssl, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS);
+        ok = SSL_set1_host(conn->ssl, name.c_str());
+      }
+      if (ok != 1) {
+        *error = "cannot set the expected server name " + name;
+        return nullptr;
+      }
+    }
     if (SSL_connect(conn->ssl) != 1) {
-      char buf[256];
-      ERR_error_string_n(ERR_get_error(), buf, sizeof buf);
-      *error = std::string("TLS handshake failed: ") + buf;
+      const long vr = SSL_get_verify_result(conn->ssl);
+      std::string detail = vr != X509_V_OK ? X509_verify_cert_error_string(vr) : ssl_err("handshake");
+      ERR_clear_error();
+      *error = "TLS handshake with " + url_.host + " failed: " + detail;
       return nullptr;
     }
   }
@@ -244,7 +289,10 @@ std::string HttpClient::build_request(const std::string& method, const std::stri
   req += "Host: " + url_.host + ":" + std::to_string(url_.port) + "\r\n";
   req += "User-Agent: pytorch-operator/v1 (mi355x-native)\r\n";
   req += "Accept: application/json\r\n";
-  if (!token_.empty()) req += "Authorization: Bearer " + token_ + "\r\n";
+  {
+    std::lock_guard<std::mutex> g(token_mu_);
+    if (!token_.empty()) req += "Authorization: Bearer " + token_ + "\r\n";
+  }
   if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
     req += "Content-Type: " + ctype + "\r\n";
     req += "Content-Length: " + std::to_string(body.size()) + "\r\n";

@@ -1,11 +1,18 @@
 #include "pto/kube.hpp"
 
+#include <poll.h>
+#include <spawn.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <thread>
 
 #include "pto/log.hpp"
+#include "pto/metrics.hpp"
 #include "pto/yaml_lite.hpp"
 
 namespace pto {
@@ -45,6 +52,84 @@ static const Json* named(const Json& doc, const char* key, const std::string& na
   return nullptr;
 }
 
+extern "C" char** environ;
+
+// client-go's exec credential flow: run the plugin with KUBERNETES_EXEC_INFO in its
+// environment, parse the ExecCredential it prints.  argv is passed as-is (no shell).
+bool run_exec_plugin(const ExecPlugin& plugin, KubeConfig* kc, std::string* error) {
+  std::vector<std::string> envs;
+  for (char** e = environ; e && *e; ++e) envs.emplace_back(*e);
+  for (const auto& kv : plugin.env) envs.push_back(kv.first + "=" + kv.second);
+  envs.push_back("KUBERNETES_EXEC_INFO={\"apiVersion\":\"" + plugin.api_version +
+                 "\",\"kind\":\"ExecCredential\",\"spec\":{\"interactive\":false}}");
+  std::vector<char*> envp;
+  for (auto& e : envs) envp.push_back(e.data());
+  envp.push_back(nullptr);
+  std::vector<std::string> args{plugin.command};
+  args.insert(args.end(), plugin.args.begin(), plugin.args.end());
+  std::vector<char*> argv;
+  for (auto& a : args) argv.push_back(a.data());
+  argv.push_back(nullptr);
+  int out[2];
+  if (pipe(out) != 0) {
+    *error = "exec plugin: pipe failed";
+    return false;
+  }
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, out[1], STDOUT_FILENO);
+  posix_spawn_file_actions_addclose(&fa, out[0]);
+  pid_t pid = 0;
+  const int rc = posix_spawnp(&pid, plugin.command.c_str(), &fa, nullptr, argv.data(), envp.data());
+  posix_spawn_file_actions_destroy(&fa);
+  close(out[1]);
+  if (rc != 0) {
+    close(out[0]);
+    *error = "exec plugin " + plugin.command + ": " + std::strerror(rc);
+    return false;
+  }
+  std::string text;
+  char buf[4096];
+  struct pollfd p{out[0], POLLIN, 0};
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+  while (std::chrono::steady_clock::now() < deadline) {
+    if (::poll(&p, 1, 200) <= 0) continue;
+    const ssize_t n = ::read(out[0], buf, sizeof buf);
+    if (n <= 0) break;
+    text.append(buf, (size_t)n);
+  }
+  close(out[0]);
+  int status = 0;
+  waitpid(pid, &status, 0);
+  if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) {
+    *error = "exec plugin " + plugin.command + " failed (status " + std::to_string(status) + ")";
+    return false;
+  }
+  try {
+    Json cred = Json::parse(text);
+    if (cred.str_or("kind") != "ExecCredential") {
+      *error = "exec plugin " + plugin.command + " did not print an ExecCredential";
+      return false;
+    }
+    const Json* st = cred.get("status");
+    if (!st) {
+      *error = "exec plugin " + plugin.command + ": ExecCredential without status";
+      return false;
+    }
+    if (!st->str_or("token").empty()) kc->token = st->str_or("token");
+    if (!st->str_or("clientCertificateData").empty() && !st->str_or("clientKeyData").empty()) {
+      kc->tls.cert_data = st->str_or("clientCertificateData");
+      kc->tls.key_data = st->str_or("clientKeyData");
+      kc->tls.cert_file.clear();
+      kc->tls.key_file.clear();
+    }
+  } catch (const std::exception& e) {
+    *error = std::string("exec plugin output: ") + e.what();
+    return false;
+  }
+  return true;
+}
+
 std::optional<KubeConfig> load_kube_config(const std::string& master_url, const std::string& kubeconfig,
                                            std::string* error) {
   KubeConfig kc;
@@ -79,6 +164,7 @@ std::optional<KubeConfig> load_kube_config(const std::string& master_url, const 
       if (!clv->str_or("certificate-authority-data").empty())
         kc.tls.ca_data = base64_decode(clv->str_or("certificate-authority-data"));
       kc.tls.insecure_skip_verify = clv->bool_or("insecure-skip-tls-verify", false);
+      kc.tls.server_name = clv->str_or("tls-server-name");
     }
     const Json* us = named(doc, "users", user_name);
     const Json* usv = us ? us->get("user") : nullptr;
@@ -94,6 +180,27 @@ std::optional<KubeConfig> load_kube_config(const std::string& master_url, const 
         kc.tls.cert_data = base64_decode(usv->str_or("client-certificate-data"));
       if (!usv->str_or("client-key-data").empty())
         kc.tls.key_data = base64_decode(usv->str_or("client-key-data"));
+      if (const Json* ex = usv->get("exec")) {
+        ExecPlugin pl;
+        pl.command = ex->str_or("command");
+        if (!ex->str_or("apiVersion").empty()) pl.api_version = ex->str_or("apiVersion");
+        if (const Json* a = ex->get("args"))
+          if (a->is_array())
+            for (const auto& v : a->as_array()) pl.args.push_back(v.is_string() ? v.as_string() : v.dump());
+        if (const Json* en = ex->get("env"))
+          if (en->is_array())
+            for (const auto& v : en->as_array()) pl.env.emplace_back(v.str_or("name"), v.str_or("value"));
+        if (pl.command.empty()) {
+          *error = "kubeconfig exec plugin without a command";
+          return std::nullopt;
+        }
+        if (!run_exec_plugin(pl, &kc, error)) return std::nullopt;
+        kc.exec = pl;
+      }
+      if (usv->get("auth-provider")) {
+        *error = "kubeconfig auth-provider plugins are not supported (removed from client-go); use an exec plugin";
+        return std::nullopt;
+      }
     }
   } else if (master_url.empty()) {
     // in-cluster config
@@ -143,7 +250,20 @@ void KubeClient::throttle() {
 std::optional<Json> KubeClient::call(const std::string& method, const std::string& path,
                                      const std::string& body, ApiError* err, const std::string& ctype) {
   throttle();
+  Metrics::instance().inc("pytorch_operator_api_requests_total");
   HttpResponse r = http_->request(method, path, body, ctype);
+  if (r.status == 401 && cfg_.exec) {
+    // an expired exec-plugin credential: refresh once and retry (client-go does the same)
+    std::string perr;
+    KubeConfig fresh = cfg_;
+    if (run_exec_plugin(*cfg_.exec, &fresh, &perr)) {
+      http_->set_bearer_token(fresh.token);
+      Metrics::instance().inc("pytorch_operator_api_requests_total");
+      r = http_->request(method, path, body, ctype);
+    } else {
+      LOG_WARN("exec credential refresh failed: %s", perr.c_str());
+    }
+  }
   if (r.status == 0) {
     if (err) *err = ApiError{0, r.error};
     return std::nullopt;

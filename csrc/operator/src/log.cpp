@@ -1,5 +1,7 @@
 #include "pto/log.hpp"
 
+#include <atomic>
+#include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -11,8 +13,10 @@
 namespace pto {
 
 namespace {
-bool g_json = true;
-LogLevel g_min = LogLevel::Info;
+// read on every log call from any thread, written by log_configure: atomics, so a late
+// reconfiguration is never a data race (the output mutex only serialises the writes)
+std::atomic<bool> g_json{true};
+std::atomic<int> g_min{(int)LogLevel::Info};
 std::mutex g_mu;
 
 const char* level_name(LogLevel l) {
@@ -38,13 +42,12 @@ std::string timestamp() {
 }  // namespace
 
 void log_configure(bool json, LogLevel min_level) {
-  std::lock_guard<std::mutex> g(g_mu);
-  g_json = json;
-  g_min = min_level;
+  g_json.store(json, std::memory_order_relaxed);
+  g_min.store((int)min_level, std::memory_order_relaxed);
 }
 
 void log_msg(LogLevel lvl, const LogFields& fields, const char* file, int line, const char* fmt, ...) {
-  if ((int)lvl < (int)g_min) return;
+  if ((int)lvl < g_min.load(std::memory_order_relaxed)) return;
   char buf[4096];
   va_list ap;
   va_start(ap, fmt);
@@ -54,7 +57,7 @@ void log_msg(LogLevel lvl, const LogFields& fields, const char* file, int line, 
   base = base ? base + 1 : file;
   std::string loc = std::string(base) + ":" + std::to_string(line);
   std::string out;
-  if (g_json) {
+  if (g_json.load(std::memory_order_relaxed)) {
     Json o = Json::object();
     o["filename"] = loc;
     for (const auto& kv : fields) o[kv.first] = kv.second;
@@ -74,6 +77,22 @@ void log_msg(LogLevel lvl, const LogFields& fields, const char* file, int line, 
 LogFields fields_for_job(const std::string& ns, const std::string& name, const std::string& uid) {
   LogFields f{{"job", ns + "." + name}};
   if (!uid.empty()) f.push_back({"uid", uid});
+  return f;
+}
+
+LogFields fields_for_replica(const std::string& ns, const std::string& name, const std::string& uid,
+                             const std::string& rtype) {
+  LogFields f = fields_for_job(ns, name, uid);
+  std::string rt = rtype;
+  for (auto& ch : rt) ch = (char)std::tolower((unsigned char)ch);
+  f.push_back({"replica-type", rt});
+  return f;
+}
+
+LogFields fields_for_pod(const std::string& ns, const std::string& job, const std::string& uid,
+                         const std::string& rtype, const std::string& pod) {
+  LogFields f = fields_for_replica(ns, job, uid, rtype);
+  f.push_back({"pod", ns + "." + pod});
   return f;
 }
 

@@ -127,6 +127,8 @@ int main(int argc, char** argv) {
   co.cfg.gang_scheduler_name = opt.gang_scheduler_name;
   co.cfg.init_container_image = opt.init_container_image;
   co.cfg.inject_rccl_env = opt.inject_rccl_env;
+  co.cfg.xgmi_pod_topology = opt.xgmi_pod_topology;
+  if (opt.rccl_env_set) co.cfg.rccl_env = opt.rccl_env;
   {
     std::ifstream f(opt.init_container_template_file);
     if (f) {

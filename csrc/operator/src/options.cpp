@@ -63,7 +63,10 @@ std::string usage() {
          "  -leader-elect-lease-duration duration   (default 15s)\n"
          "  -leader-elect-renew-deadline duration   (default 5s)\n"
          "  -leader-elect-retry-period duration     (default 3s)\n"
-         "  -inject-rccl-env          Inject LOCAL_RANK and RCCL tuning env into pytorch containers\n"
+         "  -inject-rccl-env          Inject LOCAL_RANK and the RCCL env set into pytorch containers\n"
+         "  -rccl-env KEY=VALUE       Replace the injected RCCL env set (repeatable; default\n"
+         "                            HSA_ENABLE_IPC_MODE_LEGACY=0)\n"
+         "  -xgmi-pod-topology        GPU pods: hostPID/hostIPC, NCCL_HOSTID=<node>, one-node affinity\n"
          "  -init-container-template-file  (default /etc/config/initContainer.yaml)\n"
          "  -log-level string         debug|info|warning|error (default info)\n";
 }
@@ -120,6 +123,14 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
       {"leader-elect-renew-deadline", duration(&o->renew_deadline_s)},
       {"leader-elect-retry-period", duration(&o->retry_period_s)},
       {"inject-rccl-env", boolean(&o->inject_rccl_env)},
+      {"xgmi-pod-topology", boolean(&o->xgmi_pod_topology)},
+      {"rccl-env", Flag{false, [o](const std::string& v) {
+         auto eq = v.find('=');
+         if (eq == std::string::npos || eq == 0) return std::string("expected KEY=VALUE, got \"") + v + "\"";
+         o->rccl_env.emplace_back(v.substr(0, eq), v.substr(eq + 1));
+         o->rccl_env_set = true;
+         return std::string();
+       }}},
       {"init-container-template-file", str(&o->init_container_template_file)},
       {"log-level", str(&o->log_level)},
       // glog flags accepted for compatibility with the reference Deployment

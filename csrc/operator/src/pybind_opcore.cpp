@@ -24,6 +24,12 @@ static ControllerConfig cfg_from(const std::string& s) {
   c.init_container_image = j.str_or("initContainerImage", c.init_container_image);
   c.init_container_template = j.str_or("initContainerTemplate", c.init_container_template);
   c.inject_rccl_env = j.bool_or("injectRcclEnv", false);
+  c.xgmi_pod_topology = j.bool_or("xgmiPodTopology", false);
+  if (const Json* re = j.get("rcclEnv"))
+    if (re->is_object()) {
+      c.rccl_env.clear();
+      for (const auto& kv : re->as_object()) c.rccl_env.emplace_back(kv.first, kv.second.as_string());
+    }
   return c;
 }
 

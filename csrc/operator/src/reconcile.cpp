@@ -147,6 +147,60 @@ static void inject_rccl_env(Json& tmpl, const ControllerConfig& cfg) {
   }
 }
 
+static bool requests_amd_gpu(const Json& tmpl) {
+  const Json* containers = tmpl.path({"spec", "containers"});
+  if (!containers || !containers->is_array()) return false;
+  for (const auto& c : containers->as_array())
+    for (const char* sect : {"limits", "requests"}) {
+      const Json* r = c.path({"resources", sect, "amd.com/gpu"});
+      if (r && !r->is_null()) return true;
+    }
+  return false;
+}
+
+// --xgmi-pod-topology (see ControllerConfig::xgmi_pod_topology).  Fields the user's template
+// already sets are left alone.
+static void apply_xgmi_topology(Json& tmpl, const std::string& job, const ControllerConfig& cfg) {
+  if (!cfg.xgmi_pod_topology || !requests_amd_gpu(tmpl)) return;
+  Json& spec = tmpl["spec"];
+  if (!spec.get("hostPID")) spec["hostPID"] = true;
+  if (!spec.get("hostIPC")) spec["hostIPC"] = true;
+  if (!spec.path({"affinity", "podAffinity"})) {
+    Json term = Json::object();
+    Json sel = Json::object();
+    Json ml = Json::object();
+    ml[kLabelJobName] = job;
+    sel["matchLabels"] = ml;
+    term["labelSelector"] = sel;
+    term["topologyKey"] = "kubernetes.io/hostname";
+    Json req = Json::array();
+    req.push_back(term);
+    Json pa = Json::object();
+    pa["requiredDuringSchedulingIgnoredDuringExecution"] = req;
+    Json& aff = spec["affinity"];
+    if (!aff.is_object()) aff = Json::object();
+    aff["podAffinity"] = pa;
+  }
+  Json* containers = tmpl.path({"spec", "containers"});
+  if (!containers || !containers->is_array()) return;
+  for (auto& c : containers->as_array()) {
+    if (c.str_or("name") != kDefaultContainerName) continue;
+    Json& env = c["env"];
+    if (!env.is_array()) env = Json::array();
+    bool has = false;
+    for (const auto& e : env.as_array()) has = has || e.str_or("name") == "NCCL_HOSTID";
+    if (has) continue;
+    Json fr = Json::object();
+    fr["fieldPath"] = "spec.nodeName";
+    Json vf = Json::object();
+    vf["fieldRef"] = fr;
+    Json e = Json::object();
+    e["name"] = "NCCL_HOSTID";
+    e["valueFrom"] = vf;
+    env.push_back(e);
+  }
+}
+
 Json build_pod(const Json& job, const std::string& rtype, int index, const ControllerConfig& cfg,
                std::vector<Event>* events, std::string* error) {
   const std::string rt = to_lower(rtype);
@@ -205,6 +259,7 @@ Json build_pod(const Json& job, const std::string& rtype, int index, const Contr
     (*ann)[kGangPodGroupAnnotation] = gen_pod_group_name(name);
   }
   if (cfg.inject_rccl_env) inject_rccl_env(tmpl, cfg);
+  apply_xgmi_topology(tmpl, name, cfg);
 
   // RealPodControl.GetPodFromTemplate: labels, annotations, finalizers, name, ownerRef, spec
   Json pod = Json::object();
@@ -307,10 +362,13 @@ void delete_pods_and_services(Ctx& c) {
   std::string policy = pol && pol->is_string() ? pol->as_string() : kCleanPodPolicyNone;
   // (Q1) None and Running both delete nothing -- kept for behavioural parity.
   if (policy == kCleanPodPolicyNone || policy == kCleanPodPolicyRunning) return;
-  for (const auto& p : c.in.pods)
+  for (const auto& p : c.in.pods) {
+    const Json* lb = p.path({"metadata", "labels"});
     c.res.delete_pods.push_back({p.path({"metadata", "namespace"}) ? p.path({"metadata", "namespace"})->as_string()
                                                                    : job_namespace(c.job),
-                                 p.path({"metadata", "name"})->as_string()});
+                                 p.path({"metadata", "name"})->as_string(),
+                                 lb ? lb->str_or(kLabelReplicaType) : ""});
+  }
   for (const auto& s : filter_by_replica_type(c.in.services, "master")) {
     const Json* ns = s.path({"metadata", "namespace"});
     c.res.delete_services.push_back({ns && ns->is_string() ? ns->as_string() : job_namespace(c.job),
@@ -423,7 +481,7 @@ void reconcile_pods(Ctx& c, const std::string& rtype) {
         }
       }
       if (pod_phase(pod) == "Failed" && is_retryable_exit_code(exit_code)) {
-        c.res.delete_pods.push_back({pns, pname});
+        c.res.delete_pods.push_back({pns, pname, rtype});
         restart = true;
       }
     }

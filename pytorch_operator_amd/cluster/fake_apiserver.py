@@ -354,9 +354,32 @@ class Handler(BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     server_version = "fake-kube-apiserver/1.0"
     store: Store = None  # set per server class
+    auth_tokens = None  # None: no authentication (plain local cluster)
 
     def log_message(self, fmt, *args):  # quiet
         pass
+
+    def setup(self):
+        import ssl
+        if isinstance(self.request, ssl.SSLSocket):  # TLS handshake in the handler thread
+            self.request.settimeout(10)
+            self.request.do_handshake()
+            self.request.settimeout(None)
+        super().setup()
+
+    def _authenticated(self) -> bool:
+        """Bearer token in ``auth_tokens`` or a client certificate the server's client CA
+        verified (the API server's token and x509 authenticators)."""
+        tokens = self.auth_tokens
+        if tokens is None:
+            return True
+        h = self.headers.get("Authorization") or ""
+        if h.startswith("Bearer ") and h[7:].strip() in tokens:
+            return True
+        try:
+            return bool(self.connection.getpeercert())
+        except (AttributeError, ValueError):
+            return False
 
     def _send(self, code: int, body, ctype="application/json"):
         data = body if isinstance(body, (bytes, bytearray)) else json.dumps(body).encode()
@@ -400,6 +423,9 @@ class Handler(BaseHTTPRequestHandler):
     def _handle(self, method):
         st = self.store
         st.request_count += 1
+        if not self._authenticated():
+            return self._send(401, {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                    "message": "Unauthorized", "reason": "Unauthorized", "code": 401})
         try:
             route, q, path = self._route()
             if route is None:
@@ -440,6 +466,8 @@ class Handler(BaseHTTPRequestHandler):
         import os
         st = self.store
         st.get(("", "v1", "pods"), ns, name)
+        if q.get("follow") in ("true", "1"):
+            return self._follow_log(ns, name)
         text = b""
         if st.log_dir:
             p = os.path.join(st.log_dir, f"{ns}_{name}.log")
@@ -450,6 +478,41 @@ class Handler(BaseHTTPRequestHandler):
         if tail:
             text = b"\n".join(text.splitlines()[-int(tail):]) + b"\n"
         return self._send(200, text, "text/plain")
+
+    def _follow_log(self, ns, name, max_s: float = 3600.0):
+        """``follow=true``: stream the container log as it grows; end the response once the
+        pod is terminal (Succeeded/Failed) or gone and the file is drained."""
+        import os
+        st = self.store
+        path = os.path.join(st.log_dir, f"{ns}_{name}.log") if st.log_dir else None
+        self.send_response(200)
+        self.send_header("Content-Type", "text/plain")
+        self.send_header("Transfer-Encoding", "chunked")
+        self.end_headers()
+        off, deadline = 0, time.time() + max_s
+        try:
+            while True:
+                try:
+                    phase = (st.get(("", "v1", "pods"), ns, name).get("status") or {}).get("phase")
+                    done = phase in ("Succeeded", "Failed")
+                except ApiException:
+                    done = True
+                data = b""
+                if path and os.path.exists(path):
+                    with open(path, "rb") as f:
+                        f.seek(off)
+                        data = f.read()
+                if data:
+                    off += len(data)
+                    self.wfile.write(f"{len(data):x}\r\n".encode() + data + b"\r\n")
+                    self.wfile.flush()
+                if done or time.time() > deadline:
+                    break
+                time.sleep(0.05)
+            self.wfile.write(b"0\r\n\r\n")
+        except (BrokenPipeError, ConnectionResetError, OSError):
+            pass
+        self.close_connection = True
 
     def _watch(self, gvr, ns, q):
         st = self.store
@@ -516,24 +579,55 @@ class Handler(BaseHTTPRequestHandler):
 
 
 class FakeApiServer:
-    """``with FakeApiServer() as api: api.url`` -- runs in a background thread."""
+    """``with FakeApiServer() as api: api.url`` -- runs in a background thread.
 
-    def __init__(self, host: str = "127.0.0.1", port: int = 0, log_dir: Optional[str] = None):
+    ``tls``: ``{"cert": path, "key": path, "client_ca": path | None}`` serves HTTPS (the
+    client CA enables x509 client-certificate authentication); ``tokens``: accepted bearer
+    tokens -- with it every request must present one of them or a verified client
+    certificate (401 otherwise); ``url_host``: the host name put in ``url`` / kubeconfigs
+    (e.g. ``localhost`` to exercise DNS-name certificate checks)."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, log_dir: Optional[str] = None,
+                 tls: Optional[dict] = None, tokens=None, url_host: Optional[str] = None):
+        import ssl
         self.store = Store()
         self.store.log_dir = log_dir
-        handler = type("BoundHandler", (Handler,), {"store": self.store})
+        handler = type("BoundHandler", (Handler,), {"store": self.store,
+                                                    "auth_tokens": None if tokens is None else set(tokens)})
+        ctx = None
+        if tls:
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(tls["cert"], tls["key"])
+            if tls.get("client_ca"):
+                ctx.load_verify_locations(tls["client_ca"])
+                ctx.verify_mode = ssl.CERT_OPTIONAL
+        self.tls = tls
 
         class Srv(ThreadingHTTPServer):
             daemon_threads = True
             allow_reuse_address = True
 
+            def get_request(self):
+                sock, addr = super().get_request()
+                if ctx is not None:
+                    sock = ctx.wrap_socket(sock, server_side=True, do_handshake_on_connect=False)
+                return sock, addr
+
+            def handle_error(self, request, client_address):
+                import sys
+                exc = sys.exc_info()[1]
+                if isinstance(exc, (ssl.SSLError, ConnectionError, TimeoutError, OSError)):
+                    return  # failed handshakes (e.g. a client rejecting our certificate) are expected
+                super().handle_error(request, client_address)
+
         self.httpd = Srv((host, port), handler)
         self.host, self.port = self.httpd.server_address[:2]
+        self.url_host = url_host or self.host
         self.thread = threading.Thread(target=self.httpd.serve_forever, name="fake-apiserver", daemon=True)
 
     @property
     def url(self) -> str:
-        return f"http://{self.host}:{self.port}"
+        return f"{'https' if self.tls else 'http'}://{self.url_host}:{self.port}"
 
     def start(self) -> "FakeApiServer":
         self.thread.start()
@@ -566,10 +660,32 @@ class FakeApiServer:
                         except ApiException:
                             pass
 
-    def write_kubeconfig(self, path: str, namespace: str = "default") -> str:
+    def write_kubeconfig(self, path: str, namespace: str = "default", token: Optional[str] = "fake-token",
+                         ca_file: Optional[str] = None, client_cert: Optional[str] = None,
+                         client_key: Optional[str] = None, server: Optional[str] = None,
+                         tls_server_name: Optional[str] = None, exec_plugin: Optional[dict] = None) -> str:
+        """kubeconfig for this server; PEM files are embedded as ``*-data`` (base64)."""
+        import base64
+
+        def b64(p):
+            with open(p, "rb") as f:
+                return base64.b64encode(f.read()).decode()
+        cluster = {"server": server or self.url}
+        if ca_file:
+            cluster["certificate-authority-data"] = b64(ca_file)
+        if tls_server_name:
+            cluster["tls-server-name"] = tls_server_name
+        user = {}
+        if token:
+            user["token"] = token
+        if client_cert:
+            user["client-certificate-data"] = b64(client_cert)
+            user["client-key-data"] = b64(client_key)
+        if exec_plugin:
+            user["exec"] = exec_plugin
         cfg = {"apiVersion": "v1", "kind": "Config", "current-context": "fake",
-               "clusters": [{"name": "fake", "cluster": {"server": self.url}}],
-               "users": [{"name": "fake", "user": {"token": "fake-token"}}],
+               "clusters": [{"name": "fake", "cluster": cluster}],
+               "users": [{"name": "fake", "user": user}],
                "contexts": [{"name": "fake", "context": {"cluster": "fake", "user": "fake",
                                                          "namespace": namespace}}]}
         with open(path, "w") as f:

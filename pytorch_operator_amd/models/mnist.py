@@ -140,6 +140,12 @@ class FusedMnistTrainer:
         # recomputes conv1 4x per sample and loses to two launches; side-stream overlap
         self.fuse_conv12 = True
         self.overlap = False
+        # "classic": 6 launches -- conv12_fwd, fc1_fwd<2>, head, fc1_bwd (dz2 beside the fc
+        # weight grads), conv_bwd, slab_reduce_sgd; "fused": 5 launches (head folded into
+        # fc1_bwd_head, fc weight grads + SGD in conv_bwd's idle waves).  Measured on MI355X
+        # (profiles/r2_schedule_ab.md): classic 42.0 us/step, fused 42.75 -- the fold saves
+        # 1.3 us but the fc weight gradients cost more anywhere else than beside dz2.
+        self.schedule = "classic"
 
     # ---------------------------------------------------------------- state
     def _alloc(self, B: int):
@@ -181,22 +187,24 @@ class FusedMnistTrainer:
 
     # ---------------------------------------------------------------- step
     #
-    # Launch schedule of one step (main = current stream, side = self._side):
+    # Launch schedules of one single-process step (one hipGraph; ``self.schedule``):
     #
-    #   main: conv12_fwd -> fc1_fwd -> head -+-> fc1_bwd[dgrad] -+-> conv_bwd -> tail(conv)
-    #   side:                                +-> fc1_bwd[wgrad+fc2] ------+-> tail(fc) -+
-    #                                                          (waits dgrad)            join
+    #   classic: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd -> slab_reduce_sgd
+    #   fused:   conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head -> conv_bwd(+fc) -> slab_reduce_sgd
     #
-    # fc1_bwd's weight-gradient half and the fc-parameter update run beside the
-    # input-gradient / conv-backward chain, which is the critical path.  tail() is the
-    # SGD update (single process) or the bucket all-reduce + SGD (DDP, grad_sync).
+    # fc1_bwd_head rebuilds the head (h, log-softmax/NLL, dh) per 16-sample tile and computes
+    # dz2, the critical path into the conv backward; conv_bwd's idle waves compute the fc
+    # weight gradients and apply their SGD; the tail reduces the per-sample conv gradients
+    # and updates the conv parameters.  DDP (xGMI) uses the same launches with the fc
+    # gradients only written (the exchange kernel updates every parameter).  Batches other
+    # than 59..64 compute the fc gradients in their own launch (fc1_bwd / tail_sgd).
     def _side_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
     def forward(self, source=None, B: Optional[int] = None) -> None:
-        """Launches conv12_fwd, fc1_fwd, head (loss, d(logits), dh)."""
+        """conv12_fwd + split-K fc1 (the head runs inside fc1_bwd_head)."""
         K, p = self.K, self.params
         src = source or self.source
         B = self.B if B is None else B
@@ -209,11 +217,23 @@ class FusedMnistTrainer:
                         idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
-        # split-K fc1 (256 workgroups); the head adds the halves + bias, applies ReLU, writes h1
-        hp = K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500))
+        # split-K fc1 (256 workgroups); fc1_bwd_head adds the halves + bias and applies ReLU
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500))
+
+    def _head(self, B: int) -> None:
+        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
+        K, p = self.K, self.params
+        hp = self.h_parts[:2 * B * 500].view(2, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
+
+    def _fc1_bwd_head(self, B: int) -> None:
+        K, p = self.K, self.params
+        K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"],
+                       p["fc2.bias"], self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"],
+                       grad_scale=1.0 / B, dz2=self.dz2[:B], h_out=self.h1[:B], dh=self.dh[:B],
+                       dlogits=self.dlogits[:B], per_sample=self.per_sample[:B])
 
     def _fc1_bwd(self, B: int, jobs: int) -> None:
         K, p, g = self.K, self.params, self.grads
@@ -221,6 +241,24 @@ class FusedMnistTrainer:
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
                   dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
                   loss_scale=1.0 / B, jobs=jobs)
+
+    def _conv_bwd_fc(self, B: int, sgd: bool) -> None:
+        """conv backward + fc weight grads (+ their SGD when ``sgd``) in one launch."""
+        K, p = self.K, self.params
+        fp, fm, fg = self._fc_dicts()
+        K.conv_bwd_fc(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
+                      self.conv_slab, self.slab_views, dh=self.dh[:B], a2=self.a2[:B],
+                      dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
+                      fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
+                      fc_params=fp if sgd else None, fc_bufs=fm if sgd else None, lr=self.lr,
+                      momentum=self.momentum, dampening=self.dampening,
+                      weight_decay=self.weight_decay, nesterov=self.nesterov,
+                      first_step=self._first_step)
+
+    def _fc_in_conv(self, B: int) -> bool:
+        if getattr(self, "_fc_in_conv_B", None) != B:
+            self._fc_in_conv_B, self._fc_in_conv_ok = B, self.K.conv_bwd_fc_supported(B)
+        return self._fc_in_conv_ok
 
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self.params
@@ -241,7 +279,12 @@ class FusedMnistTrainer:
         """Forward + loss + fc backward (the fc bucket and dz2 are complete after this)."""
         B = self.B if B is None else B
         self.forward(source, B)
-        self._fc1_bwd(B, self.K.FC1_BWD_ALL)
+        if self.schedule == "classic":
+            self._head(B)
+            self._fc1_bwd(B, self.K.FC1_BWD_ALL)
+        else:
+            self._fc1_bwd_head(B)
+            self._fc1_bwd(B, self.K.FC1_BWD_WGRAD | self.K.FC1_BWD_FC2)
 
     def backward_conv(self, source=None, B: Optional[int] = None) -> None:
         """conv backward + deterministic slab reduction into the conv bucket."""
@@ -264,6 +307,12 @@ class FusedMnistTrainer:
         self._sgd(0, self.layout.total, grad_scale, advance_cursor)
         self._first_step = False
 
+    def _fc_dicts(self):
+        names = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
+        mom = _views(self.flat_momentum, self.layout)
+        return ({k: self.params[k] for k in names}, {k: mom[k] for k in names},
+                {k: self.grads[k] for k in names})
+
     def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True,
                    overlap: Optional[bool] = None):
         """One full training step (forward, backward, [all-reduce], SGD)."""
@@ -273,8 +322,18 @@ class FusedMnistTrainer:
             # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
             # updated parameters (parallel/xgmi.py).  flat_grads[:conv_end] is not written.
             B_ = self.B if B is None else B
-            self.forward_backward_fc(source, B_)
-            self._conv_bwd(B_)
+            self.forward(source, B_)
+            if self.schedule == "classic":
+                self._head(B_)
+                self._fc1_bwd(B_, self.K.FC1_BWD_ALL)
+                self._conv_bwd(B_)
+            else:
+                self._fc1_bwd_head(B_)
+                if self._fc_in_conv(B_):
+                    self._conv_bwd_fc(B_, sgd=False)
+                else:
+                    self._fc1_bwd(B_, self.K.FC1_BWD_WGRAD | self.K.FC1_BWD_FC2)
+                    self._conv_bwd(B_)
             self.grad_sync.xar.allreduce_sgd_(
                 self.flat_grads, self.flat_params, self.flat_momentum, lr=self.lr,
                 momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
@@ -287,14 +346,15 @@ class FusedMnistTrainer:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return
-        if not overlap:
-            K = self.K
-            B = self.B if B is None else B
-            ce = self.layout.conv_end
+        K = self.K
+        B = self.B if B is None else B
+        ce = self.layout.conv_end
+        if not overlap and self.schedule == "classic":
+            # round-1 schedule (6 launches): head and fc1_bwd as their own launches
             self.forward(source, B)
+            self._head(B)
             self._fc1_bwd(B, K.FC1_BWD_ALL)
             self._conv_bwd(B)
-            # one tail launch: reduce conv slabs + SGD(conv) | SGD(fc), advance cursor
             K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
                                self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
                                dampening=self.dampening, weight_decay=self.weight_decay,
@@ -304,18 +364,41 @@ class FusedMnistTrainer:
                                       self.flat_momentum[ce:]))
             self._first_step = False
             return
-        K = self.K
-        B = self.B if B is None else B
-        ce = self.layout.conv_end
+        if not overlap and self._fc_in_conv(B):
+            self.forward(source, B)
+            self._fc1_bwd_head(B)
+            self._conv_bwd_fc(B, sgd=True)
+            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
+                               self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+                               dampening=self.dampening, weight_decay=self.weight_decay,
+                               nesterov=self.nesterov, first_step=self._first_step,
+                               step_counter=self.cursor if advance_cursor else None)
+            self._first_step = False
+            return
+        if not overlap:
+            self.forward(source, B)
+            self._fc1_bwd_head(B)
+            self._conv_bwd(B)
+            fp, fm, fg = self._fc_dicts()
+            K.tail_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
+                        self.flat_momentum[:ce], dh=self.dh[:B], a2=self.a2[:B],
+                        dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
+                        fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
+                        lr=self.lr, momentum=self.momentum, dampening=self.dampening,
+                        weight_decay=self.weight_decay, nesterov=self.nesterov,
+                        first_step=self._first_step,
+                        step_counter=self.cursor if advance_cursor else None)
+            self._first_step = False
+            return
+        # side-stream variant (measured slower on MI355X, kept for A/B): fc weight grads and
+        # their SGD beside the conv backward
         main = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         self.forward(source, B)
+        self._fc1_bwd_head(B)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)
-        self._fc1_bwd(B, K.FC1_BWD_DGRAD)
-        side.wait_stream(main)  # fc1.weight is read by the dgrad launch: update after it
-        with torch.cuda.stream(side):
             self._sgd(ce, self.layout.total, 1.0, False)
         self._conv_bwd(B)
         K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],

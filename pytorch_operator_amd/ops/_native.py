@@ -103,6 +103,11 @@ _SIGNATURES = {
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     "pto_conv_bwd_lds_bytes": [],
+    "pto_conv_bwd_fc_supported": [_I],
+    "pto_mnist_conv_bwd_fc": [_VP] * 9 + [_I, _I, _I] + [_VP] * 18 + [_F] * 6 + [_I, _I, _VP],
+    "pto_mnist_fc1_bwd_head": [_VP] * 8 + [_F] + [_VP] * 5 + [_I, _VP],
+    "pto_mnist_tail_sgd": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP]
+                          + [_VP] * 18 + [_F, _VP],
     # xgmi_allreduce.hip
     "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],
     "pto_xar_open": [_VP, _VP],
@@ -131,6 +136,7 @@ _SIGNATURES = {
     "pto_graph_upload": [_VP, _VP],
     "pto_graph_launch": [_VP, _VP, _I],
     "pto_graph_destroy": [_VP],
+    "pto_device_prewarm": [_I, _VP, _VP],
 }
 _LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I],
              "pto_graph_nodes": [_VP]}

@@ -308,6 +308,84 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     return dz2
 
 
+def fc1_bwd_head(hp: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                 lab: torch.Tensor, a2: torch.Tensor, idx2: torch.Tensor, w1: torch.Tensor, *,
+                 grad_scale: float, dz2: torch.Tensor, h_out: torch.Tensor, dh: torch.Tensor,
+                 dlogits: torch.Tensor, per_sample: torch.Tensor) -> torch.Tensor:
+    """fc1 input gradient with the head folded in (one launch).
+
+    From the split-K fc1 halves ``hp`` ([2, B, 500], ``fc1_fwd_parts``) every block rebuilds
+    h = relu(hp[0] + hp[1] + b1), logits, log-softmax, NLL and dh for its 16 samples, then
+    computes dz2 = unpool(relu'(dh . W1)).  Also writes h_out, dh, dlogits (scaled by
+    ``grad_scale``) and per_sample (loss, correct) for the weight-gradient launches.
+    """
+    lib = _native.load()
+    B = a2.shape[0]
+    _req(hp, (2, B, 500), torch.float32, "fc1 partials")
+    _req(b1, (500,), torch.float32, "fc1.bias")
+    _req(w2, (10, 500), torch.float32, "fc2.weight")
+    _req(b2, (10,), torch.float32, "fc2.bias")
+    _req(lab, (B,), torch.int32, "lab")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
+    _req(w1, (500, 800), torch.float32, "fc1.weight")
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    _req(h_out, (B, 500), torch.float32, "h_out")
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    rc = lib.pto_mnist_fc1_bwd_head(hp.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                    lab.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
+                                    float(grad_scale), dz2.data_ptr(), h_out.data_ptr(),
+                                    dh.data_ptr(), dlogits.data_ptr(), per_sample.data_ptr(), B,
+                                    _stream())
+    _native.check(rc, "fc1_bwd_head")
+    return dz2
+
+
+def tail_sgd_(slab: torch.Tensor, B: int, conv_grads: torch.Tensor, conv_params: torch.Tensor,
+              conv_buf: torch.Tensor, *, dh, a2, dlogits, h, per_sample, fc_params: dict,
+              fc_bufs: dict, fc_grads: dict, stats: Optional[torch.Tensor], loss_scale: float,
+              lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+              nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
+              step_counter: Optional[torch.Tensor] = None) -> None:
+    """Single-process step tail (one launch): conv grads = sum of the slab rows + SGD on the
+    conv params; dW_fc1 = dh^T a2, db_fc1, dW_fc2 = dlogits^T h, db_fc2, each with its SGD
+    applied in the epilogue (grads also stored); loss statistics; cursor advance.
+    ``fc_params`` / ``fc_bufs`` / ``fc_grads``: dicts of the fc1/fc2 weight/bias tensors."""
+    lib = _native.load()
+    n = conv_params.numel()
+    for t, nm in ((conv_grads, "conv grads"), (conv_params, "conv params"), (conv_buf, "conv momentum")):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
+    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
+            slab.shape[1] < n or slab.shape[0] < B:
+        raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
+    ptrs = []
+    for k, shp in shapes.items():
+        for d, nm in ((fc_params, "param"), (fc_bufs, "momentum"), (fc_grads, "grad")):
+            _req(d[k], shp, torch.float32, f"{k} {nm}")
+            ptrs.append(d[k].data_ptr())
+    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
+        raise ValueError("stats must be fp32 with >= 2 elements")
+    if step_counter is not None and (step_counter.dtype != torch.int32 or not step_counter.is_cuda):
+        raise ValueError("step_counter must be int32 CUDA")
+    rc = lib.pto_mnist_tail_sgd(slab.data_ptr(), B, n, slab.shape[1], conv_grads.data_ptr(),
+                                conv_params.data_ptr(), conv_buf.data_ptr(), float(lr),
+                                float(momentum), float(dampening), float(weight_decay),
+                                float(grad_scale), int(nesterov), int(first_step),
+                                _ptr(step_counter), dh.data_ptr(), a2.data_ptr(), dlogits.data_ptr(),
+                                h.data_ptr(), per_sample.data_ptr(), *ptrs, _ptr(stats),
+                                float(loss_scale), _stream())
+    _native.check(rc, "tail_sgd")
+
+
 def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
              slab: Optional[torch.Tensor] = None):
     """conv2 weight/bias grads, dz1 (internal), conv1 weight/bias grads.
@@ -345,6 +423,61 @@ def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
                                 gb1.data_ptr(), _ptr(dz1), stride, B, _stream())
     _native.check(rc, "conv_bwd")
     return dz1
+
+
+def conv_bwd_fc_supported(B: int) -> bool:
+    """Whether conv_bwd can carry every fc weight-gradient tile in its idle waves (B 59..64)."""
+    return bool(_native.load().pto_conv_bwd_fc_supported(int(B)))
+
+
+def conv_bwd_fc(dz2, w2, a1, idx1, xn, slab: torch.Tensor, slab_views: dict, *, dh, a2, dlogits, h,
+                per_sample, fc_grads: dict, stats: Optional[torch.Tensor], loss_scale: float,
+                fc_params: Optional[dict] = None, fc_bufs: Optional[dict] = None, lr: float = 0.0,
+                momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False) -> None:
+    """conv_bwd (per-sample slab rows) + the fc weight gradients dW_fc1 = dh^T a2, db_fc1,
+    dW_fc2 = dlogits^T h, db_fc2 and the loss statistics, computed in the conv kernel's idle
+    waves (one launch).  With ``fc_params``/``fc_bufs`` the SGD(momentum) update of the fc
+    parameters is applied in the same epilogue (the gradients are still written)."""
+    lib = _native.load()
+    B = dz2.shape[0]
+    if not conv_bwd_fc_supported(B):
+        raise ValueError(f"conv_bwd_fc needs B in 59..64 (got {B}); use conv_bwd + fc1_bwd")
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    _req(w2, (50, 20, 5, 5), torch.float32, "conv2.weight")
+    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
+    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(xn, (B, 784), torch.float32, "xn")
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
+        raise ValueError("slab must be contiguous fp32 [>=B, S]")
+    lo, hi = slab.data_ptr(), slab.data_ptr() + slab.shape[1] * 4
+    sv = [slab_views[k] for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
+    for t in sv:
+        if not (lo <= t.data_ptr() and t.data_ptr() + t.numel() * 4 <= hi):
+            raise ValueError("slab views must lie inside slab[0]")
+    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
+    sgd = fc_params is not None
+    ptrs = []
+    for k, shp in shapes.items():
+        _req(fc_grads[k], shp, torch.float32, f"{k} grad")
+        if sgd:
+            _req(fc_params[k], shp, torch.float32, f"{k} param")
+            _req(fc_bufs[k], shp, torch.float32, f"{k} momentum")
+        ptrs += [_ptr(fc_params[k]) if sgd else None, _ptr(fc_bufs[k]) if sgd else None, fc_grads[k].data_ptr()]
+    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
+        raise ValueError("stats must be fp32 with >= 2 elements")
+    rc = lib.pto_mnist_conv_bwd_fc(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
+                                   *[t.data_ptr() for t in sv], slab.shape[1], B, 2 if sgd else 1,
+                                   dh.data_ptr(), a2.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
+                                   per_sample.data_ptr(), *ptrs, _ptr(stats), float(loss_scale), float(lr),
+                                   float(momentum), float(dampening), float(weight_decay), float(grad_scale),
+                                   int(nesterov), int(first_step), _stream())
+    _native.check(rc, "conv_bwd_fc")
 
 
 def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor) -> torch.Tensor:

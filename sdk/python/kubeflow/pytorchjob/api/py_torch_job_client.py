@@ -4,7 +4,8 @@ Method-for-method the reference client (sdk/python/kubeflow/pytorchjob/api/
 py_torch_job_client.py): same names, arguments, defaults and error behaviour
 (``RuntimeError`` wrapping API errors; ``wait_for_condition`` raising on timeout).
 Differences: jobs may be V1PyTorchJob models *or* plain dicts; ``get_logs`` also
-returns ``{pod: log}``; ``wait_for_condition`` sleeps at most the remaining timeout
+returns ``{pod: log}`` (with ``follow=True`` each pod's log is streamed until its
+container terminates, as ``read_namespaced_pod_log(follow=True)`` does); ``wait_for_condition`` sleeps at most the remaining timeout
 (the reference rounds timeout/polling_interval and can overshoot); and the client can
 be pointed at an explicit ``Configuration`` (used with the local test cluster).
 """
@@ -14,7 +15,7 @@ import time
 from kubeflow.pytorchjob.api_client import ApiClient
 from kubeflow.pytorchjob.constants import constants
 from kubeflow.pytorchjob.utils import utils
-from pytorch_operator_amd.cluster import rest as k8s
+from kubeflow.pytorchjob import rest as k8s
 
 from .py_torch_job_watch import watch as pytorchjob_watch
 
@@ -162,8 +163,10 @@ class PyTorchJobClient(object):
 
     def get_logs(self, name, namespace=None, master=True, replica_type=None, replica_index=None,
                  follow=False):
-        """Log the (master's, by default) pod logs; returns {pod_name: log_text}."""
-        del follow  # logs are read to the current end
+        """Log the (master's, by default) pod logs; returns {pod_name: log_text}.
+
+        ``follow``: stream each pod's log until its container terminates; complete lines are
+        logged as they arrive."""
         if namespace is None:
             namespace = utils.get_default_target_namespace()
         pod_names = self.get_pod_names(name, namespace=namespace, master=master, replica_type=replica_type,
@@ -173,6 +176,18 @@ class PyTorchJobClient(object):
         out = {}
         for pod in sorted(pod_names):
             try:
+                if follow:
+                    pending = [b""]
+
+                    def on_chunk(data, pod=pod, pending=pending):
+                        pending[0] += data
+                        *lines, pending[0] = pending[0].split(b"\n")
+                        for line in lines:
+                            logging.info("[%s] %s", pod, line.decode(errors="replace"))
+                    out[pod] = self.api.pod_log(pod, namespace, follow=True, on_chunk=on_chunk)
+                    if pending[0]:
+                        logging.info("[%s] %s", pod, pending[0].decode(errors="replace"))
+                    continue
                 out[pod] = self.api.pod_log(pod, namespace)
             except k8s.ApiException as e:
                 raise RuntimeError("Exception when calling CoreV1Api->read_namespaced_pod_log: %s\n" % e)

@@ -8,7 +8,7 @@ import time
 
 from kubeflow.pytorchjob.constants import constants
 from kubeflow.pytorchjob.utils import utils
-from pytorch_operator_amd.cluster import rest as k8s
+from kubeflow.pytorchjob import rest as k8s
 
 _JOBS = k8s.GVR(constants.PYTORCHJOB_GROUP, constants.PYTORCHJOB_VERSION, constants.PYTORCHJOB_PLURAL)
 _COLS = (("NAME", 30), ("STATE", 20), ("TIME", 30))

@@ -96,5 +96,5 @@ def condition(status, ctype):
 def env_of(pod, container="pytorch"):
     for c in pod["spec"]["containers"]:
         if c["name"] == container:
-            return {e["name"]: e["value"] for e in c.get("env", [])}
+            return {e["name"]: e.get("value", e.get("valueFrom")) for e in c.get("env", [])}
     return {}

@@ -211,3 +211,67 @@ def test_conv12_fused_matches_separate_kernels(lib, B):
     assert torch.equal(f[4], a2) and torch.equal(f[5], idx2)
     rows = perm.cpu()[(torch.arange(B) + 250) % n].long()
     assert torch.equal(lab.cpu(), y[rows])
+
+
+@pytest.mark.parametrize("B", [64, 50, 130])
+def test_fc1_bwd_head_matches_head_plus_fc1_bwd(lib, B):
+    """The head folded into fc1_bwd_head (recomputed per 16-sample tile, MFMA logits and dh)
+    against the standalone head kernel + fc1_bwd job 2 on the same split-K fc1 halves."""
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    p = {k: v.to(dev) for k, v in reference_init(9).items()}
+    x, y = _data(B, seed=500 + B)
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    f = K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"], p["conv2.bias"], B)
+    lab, a2, idx2 = f[3], f[4], f[5]
+    hp = K.fc1_fwd_parts(a2, p["fc1.weight"])
+    # reference: head + fc1_bwd job 2
+    h_ref = torch.empty(B, 500, device=dev)
+    ps_ref = torch.empty(B, 2, device=dev)
+    dl_ref, dh_ref, _ = K.head(hp[0], p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B,
+                               per_sample=ps_ref, h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=h_ref)
+    g = {k: torch.empty_like(v) for k, v in p.items()}
+    dz_ref = K.fc1_bwd(dh_ref, a2, idx2, p["fc1.weight"], dl_ref, h_ref, g["fc1.weight"], g["fc1.bias"],
+                       g["fc2.weight"], g["fc2.bias"], jobs=K.FC1_BWD_DGRAD)
+    # folded
+    dz2 = torch.full((B, 50, 8, 8), float("nan"), device=dev)
+    h = torch.full((B, 500), float("nan"), device=dev)
+    dh = torch.full((B, 500), float("nan"), device=dev)
+    dl = torch.full((B, 10), float("nan"), device=dev)
+    ps = torch.full((B, 2), float("nan"), device=dev)
+    K.fc1_bwd_head(hp, p["fc1.bias"], p["fc2.weight"], p["fc2.bias"], lab, a2, idx2, p["fc1.weight"],
+                   grad_scale=1.0 / B, dz2=dz2, h_out=h, dh=dh, dlogits=dl, per_sample=ps)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    assert _rel(dl, dl_ref) < 1e-5
+    assert _rel(dh, dh_ref) < 1e-5
+    assert _rel(ps[:, 0], ps_ref[:, 0]) < 1e-5 and torch.equal(ps[:, 1], ps_ref[:, 1])
+    assert _rel(dz2, dz_ref) < 1e-5
+    assert torch.isfinite(dz2).all()
+
+
+@pytest.mark.parametrize("B", [64, 50])
+def test_fused_schedule_matches_classic(lib, B):
+    """The 5-launch schedule (fc1_bwd_head; fc weight grads + SGD in conv_bwd's idle waves at
+    B = 64, in tail_sgd otherwise) trains exactly like the 6-launch classic one."""
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    x, y = _data(4 * B, seed=700 + B)
+    perm = torch.arange(4 * B, dtype=torch.int32, device=dev)
+    res = {}
+    for sched in ("classic", "fused"):
+        cur = torch.zeros(1, dtype=torch.int32, device=dev)
+        src = K.BatchSource(x.to(dev), y.to(dev), perm=perm, cursor=cur)
+        tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.05, momentum=0.5, seed=3)
+        tr.schedule = sched
+        for _ in range(3):
+            tr.train_step()
+        torch.cuda.synchronize()
+        res[sched] = (tr.flat_params.clone(), tr.flat_momentum.clone(), tr.loss(), tr.flat_grads.clone())
+    (p0, m0, l0, g0), (p1, m1, l1, g1) = res["classic"], res["fused"]
+    assert _rel(p1, p0) < 1e-6 and _rel(m1, m0) < 1e-5
+    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
+    ce = tr.layout.conv_end
+    assert _rel(g1[ce:], g0[ce:]) < 1e-5  # fc grads are still written for inspection

@@ -5,10 +5,12 @@ pkg/apis/pytorch/validation/validation_test.go.  The Go tests drive the controll
 fake pod/service controls; here reconcile() is pure and returns the same side effects as data.
 """
 import json
+import subprocess
 import time
 
 import pytest
 
+from pytorch_operator_amd.cluster.local import operator_binary
 from opfixtures import (NAMESPACE, TEST_JOB_NAME, condition, env_of, labels, new_job, new_pod,
                         new_pods, new_service, opcore, reconcile)
 
@@ -393,8 +395,63 @@ def test_rccl_env_injection_extension():
     pod = json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, json.dumps({"injectRcclEnv": True})))
     env = env_of(pod)
     assert env["LOCAL_RANK"] == "0" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert "NCCL_MIN_NCHANNELS" not in env  # unmeasured tuning is not injected by default
     pod = json.loads(opcore().build_pod(json.dumps(job), "Worker", 0))
     assert "LOCAL_RANK" not in env_of(pod)
+    # --rccl-env replaces the set; a value the template already sets wins
+    job["spec"]["pytorchReplicaSpecs"]["Worker"]["template"]["spec"]["containers"][0]["env"] = [
+        {"name": "NCCL_PROTO", "value": "Simple"}]
+    cfg = {"injectRcclEnv": True, "rcclEnv": {"NCCL_PROTO": "LL128", "NCCL_ALGO": "Ring"}}
+    env = env_of(json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, json.dumps(cfg))))
+    assert env["NCCL_PROTO"] == "Simple" and env["NCCL_ALGO"] == "Ring"
+    assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env
+
+
+def _gpu_job(n_workers):
+    job = new_job(n_workers)
+    for rs in job["spec"]["pytorchReplicaSpecs"].values():
+        rs["template"]["spec"]["containers"][0]["resources"] = {"limits": {"amd.com/gpu": 1}}
+    return job
+
+
+def test_xgmi_pod_topology_fields():
+    """--xgmi-pod-topology (docs/xgmi_pods.md): what one-GPU pods on one node need for
+    peer memory over xGMI -- host PID namespace (dmabuf IPC import opens the exporter's
+    /proc/<pid>/fd/<fd>), host IPC namespace + /dev/shm (RCCL SHM transport), RCCL's host
+    identity from the node name, and all pods of the job on one node."""
+    job = _gpu_job(7)
+    cfg = json.dumps({"injectRcclEnv": True, "xgmiPodTopology": True})
+    for rt, idx in (("Master", 0), ("Worker", 6)):
+        pod = json.loads(opcore().build_pod(json.dumps(job), rt, idx, cfg))
+        spec = pod["spec"]
+        assert spec["hostPID"] is True and spec["hostIPC"] is True
+        term = spec["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
+        assert term["topologyKey"] == "kubernetes.io/hostname"
+        assert term["labelSelector"]["matchLabels"] == {"job-name": job["metadata"]["name"]}
+        c = [c for c in spec["containers"] if c["name"] == "pytorch"][0]
+        hid = [e for e in c["env"] if e["name"] == "NCCL_HOSTID"]
+        assert hid == [{"name": "NCCL_HOSTID", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}]
+        env = env_of(pod)
+        assert env["LOCAL_RANK"] == "0" and env["WORLD_SIZE"] == "8"
+    # CPU pods (no amd.com/gpu) and the flag off: untouched
+    pod = json.loads(opcore().build_pod(json.dumps(new_job(1)), "Worker", 0, cfg))
+    assert "hostPID" not in pod["spec"] and "affinity" not in pod["spec"]
+    pod = json.loads(opcore().build_pod(json.dumps(_gpu_job(1)), "Worker", 0))
+    assert "hostPID" not in pod["spec"]
+    # a template that decides for itself keeps its choice
+    job = _gpu_job(1)
+    job["spec"]["pytorchReplicaSpecs"]["Worker"]["template"]["spec"]["hostPID"] = False
+    pod = json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, cfg))
+    assert pod["spec"]["hostPID"] is False and pod["spec"]["hostIPC"] is True
+
+
+def test_operator_flags_for_xgmi_topology():
+    bin_ = operator_binary()
+    r = subprocess.run([bin_, "--rccl-env", "NOVALUE", "--version"], capture_output=True, text=True)
+    assert r.returncode != 0 and "KEY=VALUE" in (r.stderr + r.stdout)
+    r = subprocess.run([bin_, "--xgmi-pod-topology", "--rccl-env", "NCCL_PROTO=LL128", "--version"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
 
 
 # ------------------------------------------------------------- defaults / validation

@@ -19,6 +19,15 @@ from pytorch_operator_amd.models.mnist import FusedMnistTrainer  # noqa: E402
 from pytorch_operator_amd.ops import mnist as K  # noqa: E402
 
 
+def tail(tr, B):
+    fp, fm, fg = tr._fc_dicts()
+    ce = tr.layout.conv_end
+    K.tail_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce], tr.flat_momentum[:ce],
+                dh=tr.dh[:B], a2=tr.a2[:B], dlogits=tr.dlogits[:B], h=tr.h1[:B],
+                per_sample=tr.per_sample[:B], fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=tr.stats,
+                loss_scale=1.0 / B, lr=0.0, momentum=0.5)
+
+
 def main():
     dev = torch.device("cuda")
     ds = make_synthetic_mnist(6400, device=dev)
@@ -48,11 +57,14 @@ def main():
                                       fc1_bias=p["fc1.bias"], h_out=tr.h1)),
         ("fc1_bwd_w", lambda: tr._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)),
         ("fc1_bwd_d", lambda: tr._fc1_bwd(B, K.FC1_BWD_DGRAD)),
+        ("fc1_bwd_head", lambda: tr._fc1_bwd_head(B)),
         ("conv_bwd", lambda: tr._conv_bwd(B)),
+        ("conv_bwd_fc", lambda: tr._conv_bwd_fc(B, sgd=False)),
         ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(),
                                                     tr.flat_params[:tr.layout.conv_end],
                                                     tr.flat_momentum[:tr.layout.conv_end],
                                                     lr=0.0, momentum=0.5)),
+        ("tail_sgd", lambda: tail(tr, B)),
     ]
     reps = 20
     for name, fn in launches:
@@ -67,20 +79,31 @@ def main():
             used = dfull[:, 0] > 0
             d = dfull[used][:, :8].double()
             dc = dfull[used][:, 8:].double()
-            nph = int((d > 0).sum(1).max())
+            valid = d > 0  # blocks of different roles record different numbers of phases
+            nph = int(valid.sum(1).max())
             t0 = d[:, 0].min()
-            last = d[:, :nph].max()
-            spans.append(float(last - t0) / 100.0)  # 100 MHz -> us
-            deltas = (d[:, 1:nph] - d[:, 0:nph - 1]) / 100.0
-            ghz = float(((dc[:, nph - 1] - dc[:, 0]) / ((d[:, nph - 1] - d[:, 0]) * 10.0)).mean())
-            m = deltas.mean(0)
+            spans.append(float(d[valid].max() - t0) / 100.0)  # 100 MHz -> us
+            both = valid[:, 1:nph] & valid[:, :nph - 1]
+            deltas = ((d[:, 1:nph] - d[:, :nph - 1]) / 100.0) * both
+            cnt = both.sum(0).clamp_min(1)
+            m = deltas.sum(0) / cnt
             mx = deltas.max(0).values
+            # effective shader clock per block over its own recorded span (first -> last
+            # valid stamp; blocks without two stamps are skipped)
+            last = valid.sum(1) - 1
+            rows = torch.arange(d.shape[0])
+            wall = (d[rows, last] - d[:, 0]) * 10.0  # ns
+            cyc = dc[rows, last] - dc[:, 0]
+            ok = (last > 0) & (wall > 0)
+            ghz_b = (cyc[ok] / wall[ok]) if ok.any() else torch.zeros(0, dtype=torch.float64)
+            ghz = float(ghz_b.median()) if ghz_b.numel() else float("nan")
             phase_means = m if phase_means is None else phase_means + m
             phase_maxs = mx if phase_maxs is None else torch.maximum(phase_maxs, mx)
             starts = (d[:, 0] - t0) / 100.0
         spans.sort()
         pm = (phase_means / reps).tolist()
-        print(f"{name:10s} blocks={int(used.sum()):5d} clk={ghz:4.2f}GHz span med={spans[len(spans)//2]:7.2f}us "
+        clk = f"{ghz:4.2f}GHz" if 0.3 < ghz < 5.0 else "  n/a  "  # outside any real clock: not shown
+        print(f"{name:12s} blocks={int(used.sum()):5d} clk={clk} span med={spans[len(spans)//2]:7.2f}us "
               f"start-skew max={float(starts.max()):6.2f}us  phases(mean/max us): " +
               "  ".join(f"p{i}->{i+1} {a:.2f}/{b:.2f}" for i, (a, b) in
                         enumerate(zip(pm, phase_maxs.tolist()))), flush=True)
