@@ -92,6 +92,7 @@ def job_latency(world: int, rank: int, timeout: float) -> dict:
                    "job": {"replicas": r["replicas"], "result": r["result"],
                            "gpus_per_pod": 1, "grad_allreduce": r["grad_allreduce"],
                            "worker_samples_per_sec": r["worker_samples_per_sec"],
+                           "pod_topology": r.get("pod_topology"),
                            "reference_create_to_running_s": 121.0}}
         except Exception as e:  # noqa: BLE001 -- never lose the throughput line over this
             out = {"create_to_first_step_s": None, "create_to_succeeded_s": None,

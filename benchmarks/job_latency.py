@@ -84,16 +84,26 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
 
 
 def measure(replicas: int, gpus=None, backend: str = "rccl", timeout: float = 180.0,
-            extra_args=(), name: str = "bench-latency") -> dict:
+            extra_args=(), name: str = "bench-latency",
+            operator_args=("--inject-rccl-env", "--xgmi-pod-topology")) -> dict:
     """One job of ``replicas`` pods through the real operator (1 GPU per pod when ``gpus``
-    lists node GPU ids); the dict of ``run_one``.  Used by bench.py after its timed region."""
+    lists node GPU ids) on a kubelet that isolates pods like a real one where the host
+    allows it (docs/xgmi_pods.md); the dict of ``run_one`` plus how the pods were placed.
+    Used by bench.py after its timed region."""
     args = ["--backend", backend, *extra_args]
     gpu = bool(gpus)
     if not gpu:
         args.append("--no-cuda")
-    with LocalCluster(gpus=list(gpus) if gpu else None) as c:
+    with LocalCluster(gpus=list(gpus) if gpu else None, operator_args=list(operator_args),
+                      isolation="namespaces") as c:
         c.wait_operator_ready()
-        return run_one(c, name, replicas, args, gpu, timeout)
+        r = run_one(c, name, replicas, args, gpu, timeout)
+        pod = c.rest.get(PODS, f"{name}-master-0", "default")
+        ps = pod.get("spec") or {}
+        r["pod_topology"] = {"hostPID": bool(ps.get("hostPID")), "hostIPC": bool(ps.get("hostIPC")),
+                             "operator_args": list(operator_args),
+                             "kubelet_namespaces": c.kubelet.isolation_active}
+        return r
 
 
 def main(argv=None):

@@ -32,7 +32,15 @@ What it emulates
   that pod *name* to hit, default 1; counted across pod recreations) kill the container and
   report the given code -- e.g. 137 to exercise the ExitCode restart policy with a real job;
 * logs: stdout/stderr of every container go to ``<log_dir>/<ns>_<pod>.log``, served by the
-  fake API server's ``pods/{name}/log`` endpoint.
+  fake API server's ``pods/{name}/log`` endpoint;
+* namespaces (``isolation="namespaces"``): like a real kubelet, a pod gets its own PID and
+  IPC namespaces, a private ``/dev/shm`` and its own hostname unless its spec sets
+  ``hostPID`` / ``hostIPC`` (``unshare`` in a user namespace, before anything in the pod
+  touches the GPU).  A pod with both ``hostPID`` and ``hostIPC`` runs in the node's
+  namespaces (its UTS namespace too: isolating only the hostname would need a separate user
+  namespace, which a real kubelet does not create).  This is what makes the operator's
+  ``--xgmi-pod-topology`` observable on one node: without it, xGMI peer-memory IPC between
+  pods fails exactly as on a cluster (docs/xgmi_pods.md).
 """
 from __future__ import annotations
 
@@ -117,6 +125,26 @@ def _free_port(taken=()) -> int:
                 continue
             return port
     raise RuntimeError("no free rendezvous port")
+
+
+def namespaces_available(readable: Optional[str] = None) -> tuple:
+    """(ok, error): can this node give a pod its own user/PID/IPC/UTS/mount namespaces (and,
+    with ``readable``, can a process in them still read that path -- a checkout under
+    another user's 0700 home is not readable from a user namespace)?"""
+    import shutil
+    if not shutil.which("unshare"):
+        return False, "unshare not found"
+    probe = "echo $$" + (f" && test -r '{readable}'" if readable else "")
+    try:
+        r = subprocess.run(["unshare", "--user", "--map-root-user", "--fork", "--kill-child", "--mount", "--uts",
+                            "--pid", "--mount-proc", "--ipc", "sh", "-c", probe],
+                           capture_output=True, text=True, timeout=10)
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return False, repr(e)
+    if r.returncode != 0 or r.stdout.strip() != "1":
+        why = (r.stderr or r.stdout).strip()[-300:]
+        return False, why or f"{readable} is not readable inside a user namespace"
+    return True, ""
 
 
 class _Container:
@@ -265,6 +293,23 @@ class PodRunner(threading.Thread):
                 cmd = [cmd[0]] + SCRIPT_MAP[cmd[1]] + cmd[2:]
         return cmd + args
 
+    def _isolate(self, argv: List[str]) -> List[str]:
+        """Wrap ``argv`` in the namespaces this pod does not share with the node."""
+        if not self.k.isolation_active:
+            return argv
+        ps = self.pod.get("spec") or {}
+        host_pid, host_ipc = bool(ps.get("hostPID")), bool(ps.get("hostIPC"))
+        if host_pid and host_ipc:
+            return argv
+        wrap = ["unshare", "--user", "--map-root-user", "--fork", "--kill-child", "--mount", "--uts"]
+        if not host_pid:
+            wrap += ["--pid", "--mount-proc"]
+        setup = 'hostname "$0" 2>/dev/null; '
+        if not host_ipc:
+            wrap.append("--ipc")
+            setup += "mount -t tmpfs -o size=64m tmpfs /dev/shm 2>/dev/null; "
+        return wrap + ["sh", "-c", setup + 'exec "$@"', self.name] + argv
+
     def _env(self, spec: dict) -> Dict[str, str]:
         # the node's environment minus anything a container must get from its pod spec
         base = _node_env()
@@ -307,6 +352,8 @@ class PodRunner(threading.Thread):
 
     def _run_container(self, c: _Container, policy: str, init: bool = False):
         argv = self._argv(c.spec)
+        if argv is not None:
+            argv = self._isolate(argv)
         if argv is None:
             c.state = {"waiting": {"reason": "ErrImagePull",
                                    "message": f"image {c.spec.get('image')!r} not known to this node"}}
@@ -401,7 +448,8 @@ class LocalKubelet:
                  namespace: Optional[str] = None, gpus: Optional[List[int]] = None,
                  image_map: Optional[Dict[str, List[str]]] = None, python: str = sys.executable,
                  repo_root: str = REPO_ROOT, extra_env: Optional[Dict[str, str]] = None,
-                 hide_gpus_without_request: bool = True, dns_poll_s: float = 0.1, verbose: bool = False):
+                 hide_gpus_without_request: bool = True, dns_poll_s: float = 0.1, verbose: bool = False,
+                 isolation: str = "none", isolation_needs_repo: bool = True):
         self.rest = rest
         self.log_dir = os.path.abspath(log_dir)
         os.makedirs(self.log_dir, exist_ok=True)
@@ -422,6 +470,16 @@ class LocalKubelet:
         self.stopped = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="kubelet")
         self.finished_pods: List[str] = []
+        if isolation not in ("none", "namespaces"):
+            raise ValueError(f"unknown isolation {isolation!r}")
+        self.isolation = isolation
+        self.isolation_active = False
+        self.isolation_error = ""
+        if isolation == "namespaces":
+            probe = os.path.join(repo_root, "pytorch_operator_amd", "__init__.py") if isolation_needs_repo else None
+            self.isolation_active, self.isolation_error = namespaces_available(probe)
+            if not self.isolation_active:
+                self._log(f"pod namespaces unavailable ({self.isolation_error}); pods share the node's")
 
     def _log(self, msg: str):
         if self.verbose:

@@ -44,7 +44,7 @@ class LocalCluster:
     def __init__(self, workdir: Optional[str] = None, gpus: Optional[List[int]] = None,
                  operator_args: Optional[List[str]] = None, start_operator: bool = True,
                  operator_env: Optional[Dict[str, str]] = None, kubelet_env: Optional[Dict[str, str]] = None,
-                 verbose: bool = False):
+                 verbose: bool = False, isolation: str = "none", isolation_needs_repo: bool = True):
         self._tmp = None
         if workdir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="pto-cluster-")
@@ -59,6 +59,8 @@ class LocalCluster:
         self.operator_env = dict(operator_env or {})
         self.kubelet_env = kubelet_env
         self.verbose = verbose
+        self.isolation = isolation
+        self.isolation_needs_repo = isolation_needs_repo
         self.operator: Optional[subprocess.Popen] = None
         self.monitoring_port = free_port()
         self.operator_log = os.path.join(workdir, "operator.log")
@@ -72,7 +74,8 @@ class LocalCluster:
         self.api.write_kubeconfig(self.kubeconfig)
         self.rest = KubeRest(Configuration(host=self.api.url, token="fake-token"))
         self.kubelet = LocalKubelet(self.rest, self.log_dir, gpus=self.gpus, extra_env=self.kubelet_env,
-                                    verbose=self.verbose).start()
+                                    verbose=self.verbose, isolation=self.isolation,
+                                    isolation_needs_repo=self.isolation_needs_repo).start()
         if self.start_operator:
             self.start_operator_process()
         return self

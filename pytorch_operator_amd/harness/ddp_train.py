@@ -83,17 +83,38 @@ def use_master_weights(args, device) -> bool:
 
 def fp32_allreduce_hook(process_group, bucket):
     """DDP comm hook: all-reduce a bf16 gradient bucket in fp32 (``--allreduce-dtype fp32`` with
-    bf16 master-weight training keeps the cross-rank sum at fp32 precision)."""
+    bf16 master-weight training).  The fp32 mean is what the optimizer consumes: each
+    parameter gets ``_pto_grad32``, a view into the reduced fp32 bucket, which ``MasterAdamW``
+    reads instead of the bf16 ``.grad`` (also refreshed, rounded, for anything else)."""
     import torch.distributed as dist
     buf = bucket.buffer()
     group = process_group if process_group is not None else dist.group.WORLD
     t = buf.float().div_(dist.get_world_size(group))
     fut = dist.all_reduce(t, group=group, async_op=True).get_future()
+    params, grads = bucket.parameters(), bucket.gradients()
 
     def done(f):
-        buf.copy_(f.value()[0])
+        red = f.value()[0]
+        esz = buf.element_size()
+        for p, g in zip(params, grads):
+            off = (g.data_ptr() - buf.data_ptr()) // esz
+            p._pto_grad32 = red[off:off + g.numel()].view(g.shape)
+        buf.copy_(red)
         return buf
     return fut.then(done)
+
+
+def param_digest(model, opt) -> str:
+    """sha1 over every parameter and (MasterAdamW) fp32 master, in order: DDP replicas must agree."""
+    import hashlib
+    import torch
+    h = hashlib.sha1()
+    for p in model.parameters():
+        h.update(p.detach().float().cpu().numpy().tobytes())
+        st = opt.state.get(p) or {}
+        if isinstance(st.get("master"), torch.Tensor):
+            h.update(st["master"].detach().cpu().numpy().tobytes())
+    return h.hexdigest()
 
 
 def train_flops_per_sample(args) -> float:
@@ -103,7 +124,9 @@ def train_flops_per_sample(args) -> float:
     from ..models.llama import CONFIGS
     c = CONFIGS[args.model]
     n = c.num_params() - c.vocab_size * c.dim  # embedding lookup is not a matmul
-    attn = 12 * c.n_layers * c.dim * args.seq_len  # causal attention, fwd+bwd, per token (x1/2 causal, x2)
+    # causal attention per token: QK^T and PV over the (on average) S/2 visible keys = 2*S*d
+    # forward FLOPs per layer, x3 for forward + backward = 6*L*d*S
+    attn = 6 * c.n_layers * c.dim * args.seq_len
     return (6 * n + attn) * args.seq_len  # per sequence
 
 
@@ -196,6 +219,8 @@ def main(argv=None) -> int:
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev)}
+    digest = param_digest(model.module if hasattr(model, "module") else model, opt)
+    print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest}), flush=True)
     if rank == 0:
         print(json.dumps(res), flush=True)
         if args.json_out:

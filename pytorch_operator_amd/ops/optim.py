@@ -72,15 +72,20 @@ class MasterAdamW(torch.optim.Optimizer):
                 st = self._state(p)
                 st["step"] += 1
                 master = st["master"] if st["master"] is not None else p
+                # the DDP fp32 comm hook's reduced gradient (harness/ddp_train.py), else .grad
+                g32 = getattr(p, "_pto_grad32", None)
+                if g32 is not None:
+                    del p._pto_grad32
+                g = g32 if g32 is not None else p.grad
                 if p.is_cuda:
-                    self._step_hip(p, master, st, lr, b1, b2, eps, wd)
+                    self._step_hip(p, g, master, st, lr, b1, b2, eps, wd)
                 else:
-                    self._step_reference(p, master, st, lr, b1, b2, eps, wd)
+                    self._step_reference(p, g, master, st, lr, b1, b2, eps, wd)
         return loss
 
     @staticmethod
-    def _step_reference(p, master, st, lr, b1, b2, eps, wd):
-        g = p.grad.float()
+    def _step_reference(p, g, master, st, lr, b1, b2, eps, wd):
+        g = g.float()
         t = st["step"]
         master.mul_(1 - lr * wd)
         st["exp_avg"].lerp_(g, 1 - b1)
@@ -91,8 +96,7 @@ class MasterAdamW(torch.optim.Optimizer):
             p.copy_(master)
 
     @staticmethod
-    def _step_hip(p, master, st, lr, b1, b2, eps, wd):
-        g = p.grad
+    def _step_hip(p, g, master, st, lr, b1, b2, eps, wd):
         if not g.is_contiguous() or g.data_ptr() % 16:
             g = g.contiguous().clone()
         if g.dtype not in (torch.float32, torch.bfloat16) or not p.is_contiguous():

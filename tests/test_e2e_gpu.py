@@ -10,7 +10,7 @@ import time
 import pytest
 
 from pytorch_operator_amd.cluster.local import LocalCluster
-from pytorch_operator_amd.cluster.rest import PYTORCHJOBS
+from pytorch_operator_amd.cluster.rest import PODS, PYTORCHJOBS
 
 pytestmark = pytest.mark.gpu
 
@@ -49,3 +49,46 @@ def test_gpu_mnist_job_hip_kernels(tmp_path):
         assert start["kernels"] == "hip"
         assert done["accuracy"] > 0.9, log[-2000:]
         print(f"job wall {elapsed:.2f}s, train {done['samples_per_sec']} samples/s, acc {done['accuracy']}")
+
+
+@pytest.mark.parametrize("topology", [False, True])
+def test_two_pod_xgmi_job_needs_the_pod_topology(tmp_path, topology):
+    """Two one-GPU pods of one job exchanging gradients over peer memory (the xGMI kernel;
+    gloo carries only the rendezvous because both pods share this box's single GPU).
+    With the kubelet giving pods their own PID/IPC namespaces, the peer-memory IPC import
+    must FAIL unless the operator's --xgmi-pod-topology put the pods in the node's
+    namespaces (docs/xgmi_pods.md) -- then the job succeeds on the xGMI path."""
+    from pytorch_operator_amd.cluster.kubelet import namespaces_available
+    ok, why = namespaces_available()
+    if not ok and not topology:
+        # (the MI355X pool's boxes refuse user namespaces: "unshare failed: No space left on
+        # device"; the isolated case then cannot be built there -- the CPU suite covers the
+        # kubelet's isolation, tests/test_e2e_local.py::test_pod_namespaces_follow_host_pid_ipc)
+        pytest.skip(f"no user namespaces on this host: {why}")
+    name = f"xgmi-pods-{'topo' if topology else 'plain'}"
+    rs = {"replicas": 1, "restartPolicy": "Never",
+          "template": {"spec": {"containers": [{
+              "name": "pytorch", "image": "pytorch-operator-amd/worker:latest",
+              "args": ["--backend", "gloo", "--allreduce", "xgmi", "--dataset-size", "2560",
+                       "--test-size", "500", "--log-interval", "10"],
+              "resources": {"limits": {"amd.com/gpu": 1}}}]}}}
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name},
+           "spec": {"cleanPodPolicy": "None", "pytorchReplicaSpecs": {"Master": rs, "Worker": rs}}}
+    op_args = ["--inject-rccl-env"] + (["--xgmi-pod-topology"] if topology else [])
+    with LocalCluster(workdir=str(tmp_path / "c"), gpus=[0, 0], operator_args=op_args,
+                      isolation="namespaces") as c:
+        c.wait_operator_ready()
+        c.rest.create(PYTORCHJOBS, job, "default")
+        j, types = _wait(c, name, timeout=240)
+        logs = {p: c.rest.pod_log(p, "default") for p in (f"{name}-master-0", f"{name}-worker-0")}
+        pod = c.rest.get(PODS, f"{name}-worker-0", "default")
+        blob = "\n".join(v[-3000:] for v in logs.values())
+        if topology:
+            assert pod["spec"].get("hostPID") is True and pod["spec"].get("hostIPC") is True
+            assert types[-1] == "Succeeded", blob
+            for v in logs.values():
+                assert '"path": "xgmi"' in v
+        else:
+            assert not pod["spec"].get("hostPID")
+            assert types[-1] == "Failed", blob
+            assert "hipIpcOpenMemHandle failed" in blob, blob

@@ -345,3 +345,71 @@ def test_exit_code_restart_resumes_from_checkpoint(cluster, tmp_path, code):
     log = c.rest.pod_log(f"{name}-master-0", NS)
     assert f"fault injection: exiting with {code} after epoch 1" in log
     assert '"event": "resumed"' in log and "Train Epoch: 2 [0/640" in log
+
+
+def test_pod_namespaces_follow_host_pid_ipc(tmp_path):
+    """Kubelet isolation (docs/xgmi_pods.md): each pod gets its own PID / IPC namespace,
+    /dev/shm and hostname unless its spec shares the node's (hostPID / hostIPC) -- the
+    fields the operator's --xgmi-pod-topology sets on GPU pods."""
+    from pytorch_operator_amd.cluster.kubelet import namespaces_available
+    ok, why = namespaces_available()
+    if not ok:
+        pytest.skip(f"no user namespaces on this host: {why}")
+    code = ("import json, os, socket; print(json.dumps({'pid': os.getpid(), 'host': socket.gethostname(), "
+            "'pidns': os.readlink('/proc/self/ns/pid'), 'ipcns': os.readlink('/proc/self/ns/ipc'), "
+            "'shm': sorted(os.listdir('/dev/shm'))[:0]}))")
+    # (pods here only run `python -c`: they need not read the repo, which may sit in a 0700 home)
+    with LocalCluster(workdir=str(tmp_path / "c"), isolation="namespaces", isolation_needs_repo=False) as c:
+        c.wait_operator_ready()
+        for name, host in (("ns-isolated", False), ("ns-shared", True)):
+            specs = [replica(1, command=py(code), policy="Never") for _ in range(2)]
+            if host:
+                for sp in specs:
+                    sp["template"]["spec"].update(hostPID=True, hostIPC=True)
+            c.rest.create(PYTORCHJOBS, make_job(name, *specs), NS)
+            types, _ = wait_finished(c, name, timeout=120)
+            assert types[-1] == "Succeeded"
+            # the job's success is decided by the Master alone (reference quirk): wait for both
+            pods = (f"{name}-master-0", f"{name}-worker-0")
+            wait_until(lambda: all(c.rest.get(PODS, p, NS).get("status", {}).get("phase") == "Succeeded"
+                                   for p in pods), 60, what="both pods to finish")
+            outs = {}
+            for pod in pods:
+                lines = [x for x in c.rest.pod_log(pod, NS).splitlines() if x.startswith("{")]
+                outs[pod] = json.loads(lines[-1])
+            me = os.readlink("/proc/self/ns/pid")
+            if host:
+                assert all(o["pidns"] == me and o["pid"] != 1 for o in outs.values()), outs
+            else:
+                assert all(o["pid"] == 1 and o["pidns"] != me for o in outs.values()), outs
+                assert {o["host"] for o in outs.values()} == set(outs)  # hostname = pod name
+                assert len({o["pidns"] for o in outs.values()}) == 2 and len({o["ipcns"] for o in outs.values()}) == 2
+
+
+def test_repeated_events_are_aggregated(cluster, tmp_path):
+    """client-go's EventCorrelator semantics: an event identical to one posted recently (same
+    object, type, reason, message) bumps that Event's count instead of creating a new object
+    -- a crash-looping replica must not flood the namespace with Events."""
+    c = cluster
+    marker = tmp_path / "n"
+    # exits 130 (retryable) three times, then 0: the ExitCode policy deletes and recreates the
+    # pod each time, so "Created pod: <name>" / "Deleted pod: <name>" repeat verbatim
+    code = (f"import os,sys; p={str(marker)!r}; n=int(open(p).read()) if os.path.exists(p) else 0; "
+            f"open(p,'w').write(str(n+1)); sys.exit(0 if n >= 3 else 130)")
+    c.rest.create(PYTORCHJOBS, make_job("e2e-events", replica(1, "busybox", command=py(code), policy="ExitCode")), NS)
+    types, job = wait_finished(c, "e2e-events", timeout=120)
+    assert types[-1] == "Succeeded", job["status"]
+    time.sleep(0.5)  # the event sink posts asynchronously
+    evs = [e for e in c.rest.list(EVENTS, NS)["items"]
+           if (e.get("involvedObject") or {}).get("name") == "e2e-events"]
+    created = [e for e in evs if e["reason"] == "SuccessfulCreatePod" and e["message"] == "Created pod: e2e-events-master-0"]
+    assert len(created) == 1, [(e["metadata"]["name"], e.get("count")) for e in created]
+    deleted = [e for e in evs if e["reason"] == "SuccessfulDeletePod"]
+    assert len(deleted) == 1 and deleted[0]["count"] >= 2, [(e["metadata"]["name"], e.get("count")) for e in deleted]
+    # every restart recreated the pod: one more creation than deletions
+    assert created[0]["count"] == deleted[0]["count"] + 1
+    assert created[0]["lastTimestamp"] >= created[0]["firstTimestamp"]
+    # LoggerForPod fields (tf-operator logger.go:26-56) on the pod lifecycle lines
+    log = open(c.operator_log).read()
+    assert "replica-type=master" in log and "pod=default.e2e-events-master-0" in log
+    assert c.metric_value("pytorch_operator_api_requests_total") > 0

@@ -205,6 +205,10 @@ def test_ddp_train_worker_llama_tiny_master_weights_two_ranks(tmp_path):
         assert rc == 0, out
     res = json.loads([ln for ln in outs[0][1].splitlines() if ln.startswith('{"metric"')][-1])
     assert res["master_weights"] is True and res["loss"] == res["loss"]
+    # replicas stay identical: every rank's parameters AND fp32 masters hash the same
+    digests = [json.loads([ln for ln in out.splitlines() if '"param_digest"' in ln][-1])["digest"]
+               for _, out in outs]
+    assert len(set(digests)) == 1, digests
 
 
 def test_ddp_train_worker_resnet_tiny(tmp_path):
@@ -225,6 +229,16 @@ def test_example_yamls_are_valid_jobs():
         for spec in job["spec"]["pytorchReplicaSpecs"].values():
             for c in spec["template"]["spec"]["containers"]:
                 assert "nvidia.com/gpu" not in json.dumps(c), path  # MI355X-only resources
+        total = sum(int(s.get("replicas", 1)) for s in job["spec"]["pytorchReplicaSpecs"].values())
+        if total == 8:  # the one-node 8 x MI355X jobs carry the xGMI pod topology (docs/xgmi_pods.md)
+            for spec in job["spec"]["pytorchReplicaSpecs"].values():
+                ps = spec["template"]["spec"]
+                assert ps.get("hostPID") is True and ps.get("hostIPC") is True, path
+                term = ps["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
+                assert term["topologyKey"] == "kubernetes.io/hostname", path
+                assert term["labelSelector"]["matchLabels"] == {"job-name": job["metadata"]["name"]}, path
+                env = {e["name"]: e for e in ps["containers"][0].get("env", [])}
+                assert env["NCCL_HOSTID"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName", path
 
 
 def test_util_pformat_and_rand_string():

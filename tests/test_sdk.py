@@ -159,3 +159,72 @@ def test_generated_schema_is_up_to_date():
     root = Path(__file__).resolve().parent.parent
     r = subprocess.run([sys.executable, str(root / "tools" / "gen_schema.py"), "--check"], capture_output=True)
     assert r.returncode == 0, "run `make schema`"
+
+
+def test_sdk_is_a_standalone_distribution(cluster, tmp_path):
+    """``kubeflow-pytorchjob`` (reference sdk/python/setup.py:26-61) installs and runs on its
+    own: pip-install it into an empty target, then drive the SDK e2e flow from a process whose
+    sys.path holds that target but not this repository (no pytorch_operator_amd)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    target = tmp_path / "site"
+    r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-deps", "--no-build-isolation",
+                        "--no-index", "--target", str(target), os.path.join(root, "sdk", "python")],
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    dist = [p.name for p in target.iterdir() if p.name.endswith(".dist-info")]
+    assert any(d.startswith("kubeflow_pytorchjob-0.1.4") for d in dist), dist
+    script = f"""
+import sys, json
+assert not any(p.rstrip('/').endswith('repo') for p in sys.path), sys.path
+try:
+    import pytorch_operator_amd
+    raise SystemExit("framework importable: the SDK is not standalone")
+except ImportError:
+    pass
+import kubeflow.pytorchjob as kp
+assert kp.__file__.startswith({str(target)!r}), kp.__file__
+from kubeflow.pytorchjob import (PyTorchJobClient, V1Container, V1ObjectMeta, V1PodSpec,
+                                 V1PodTemplateSpec, V1PyTorchJob, V1PyTorchJobSpec, V1ReplicaSpec)
+c = V1Container(name="pytorch", image="gcr.io/kubeflow-ci/pytorch-dist-mnist-test:v1.0",
+                args=["--backend", "gloo", "--dataset-size", "640", "--test-size", "128", "--max-steps", "3"])
+rs = V1ReplicaSpec(replicas=1, restart_policy="OnFailure",
+                   template=V1PodTemplateSpec(spec=V1PodSpec(containers=[c])))
+job = V1PyTorchJob(api_version="kubeflow.org/v1", kind="PyTorchJob",
+                   metadata=V1ObjectMeta(name="standalone-sdk", namespace="default"),
+                   spec=V1PyTorchJobSpec(clean_pod_policy="None", pytorch_replica_specs={{"Master": rs}}))
+cl = PyTorchJobClient(config_file={cluster.kubeconfig!r})
+cl.create(job)
+cl.wait_for_job("standalone-sdk", namespace="default", timeout_seconds=180, polling_interval=1)
+assert cl.is_job_succeeded("standalone-sdk", namespace="default")
+logs = cl.get_logs("standalone-sdk", namespace="default", follow=True)
+assert any("accuracy=" in v for v in logs.values()), logs
+cl.delete("standalone-sdk", namespace="default")
+print("STANDALONE_OK")
+"""
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    env["PYTHONPATH"] = str(target)
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path), env=env)
+    assert r.returncode == 0 and "STANDALONE_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_get_logs_follow_streams_until_the_container_ends(client, cluster):
+    """get_logs(follow=True) (reference py_torch_job_client.py:385-386) blocks while the pod
+    runs and returns the whole log once its container terminates."""
+    import threading
+    import time
+    code = "import time\nfor i in range(6):\n    print('tick', i, flush=True)\n    time.sleep(0.4)\n"
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": "follow-logs"},
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "restartPolicy": "Never", "template": {
+               "spec": {"containers": [{"name": "pytorch", "image": "x", "command": ["python", "-c", code]}]}}}}}}
+    client.create(job, namespace=NS)
+    client.wait_for_condition("follow-logs", ["Running", "Succeeded"], namespace=NS, timeout_seconds=60,
+                              polling_interval=0.1)
+    t0 = time.time()
+    out = client.get_logs("follow-logs", namespace=NS, follow=True)
+    log = out["follow-logs-master-0"]
+    assert "tick 5" in log and time.time() - t0 > 0.5
+    client.delete("follow-logs", namespace=NS)
