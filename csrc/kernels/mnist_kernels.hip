@@ -1470,7 +1470,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
     int boff[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-      const int jc = min((ntw + n) * 16 + i, 124);
+      const int jc = min(max((ntw + n) * 16 + i - cig, 0), 124);
       const int ci = jc / 25, t = jc - ci * 25;
       boff[n] = ci * F_A1C + (t / 5) * F_A1R + (t % 5);
     }
@@ -1486,8 +1486,8 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
       }
 #pragma unroll
       for (int s2 = 0; s2 < 16; ++s2) {
-        gacc[0] = mfma16x16x4(av[s2], b0[s2], gacc[0]);
-        gacc[1] = mfma16x16x4(av[s2], b1[s2], gacc[1]);
+        gacc[0] = mfma16x16x4(b0[s2], av[s2], gacc[0]);
+        gacc[1] = mfma16x16x4(b1[s2], av[s2], gacc[1]);
       }
     } else {
       float av[16], b0[16];
@@ -1498,7 +1498,33 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
         b0[s2] = a1_s[boff[0] + poff];
       }
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) gacc[0] = mfma16x16x4(av[s2], b0[s2], gacc[0]);
+      for (int s2 = 0; s2 < 16; ++s2) gacc[0] = mfma16x16x4(b0[s2], av[s2], gacc[0]);
+    }
+    // store the tiles now, so they drain under phases 3-4.  The tile is transposed
+    // (A = im2col, B = dz2): lane (i, g) holds co = mt*16 + i and 4 consecutive
+    // j = t*16 + g*4 - cig + r.  The -cig shift makes every full group start on a 16-byte
+    // boundary of the slab row (544 + co*500 + cig*125 + j0 = 4 * (...)), so it is one
+    // float4 store; groups cut by j < 0 or j > 124 store element-wise.
+    const size_t so = slab_stride > 0 ? (size_t)b * slab_stride : 0;
+    float* rowp = gw2 + so + (size_t)(mt * 16 + i) * 500 + cig * 125;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      if (n < nt2) {
+        const int j0 = (ntw + n) * 16 + g * 4 - cig;
+        if (slab_stride > 0 && j0 >= 0 && j0 + 3 < 125) {
+          *reinterpret_cast<float4*>(rowp + j0) =
+              make_float4(gacc[n][0], gacc[n][1], gacc[n][2], gacc[n][3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = j0 + r;
+            if (j >= 0 && j < 125) {
+              if (slab_stride > 0) rowp[j] = gacc[n][r];
+              else atomicAdd(rowp + j, gacc[n][r]);
+            }
+          }
+        }
+      }
     }
     if (item >= 0 && item < 250) {
       const int co = 48 + item / 125, j = item % 125;
@@ -1607,19 +1633,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   // slab_stride == 0: fp32 atomics straight into the grads (standalone use).
   const bool slab = slab_stride > 0;
   const size_t so = slab ? (size_t)b * slab_stride : 0;
-#pragma unroll
-  for (int n = 0; n < 2; ++n) {
-    const int j = (ntw + n) * 16 + i;
-    if (n < nt2 && j < 125) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = mt * 16 + g * 4 + r;
-        float* dst = gw2 + so + (size_t)co * 500 + cig * 125 + j;
-        if (slab) *dst = gacc[n][r];
-        else atomicAdd(dst, gacc[n][r]);
-      }
-    }
-  }
   if (item >= 0 && item < 250) {
     float* dst = gw2 + so + (size_t)(48 + item / 125) * 500 + cig * 125 + item % 125;
     if (slab) *dst = grow;
@@ -2057,6 +2070,8 @@ static int conv_bwd_launch(const float* dz2, const float* w2, const float* a1, c
                            float* dz1_out, int slab_stride, int B, const FcGrad& fc, void* stream) {
   PTO_CHECK_B(B);
   if (slab_stride < 0) return -1;
+  // the slab path writes dW_conv2 as float4: row starts and gw2 + 544-float offsets aligned
+  if (slab_stride > 0 && (slab_stride % 4 != 0 || (reinterpret_cast<uintptr_t>(gw2) & 15) != 0)) return -2;
   switch (fc.mode) {
     case 0: return conv_bwd_launch_t<0>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
     case 1: return conv_bwd_launch_t<1>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
