@@ -178,6 +178,11 @@ __device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb)
 }
 
 constexpr int AB_NT = 1024;  // conv forward blocks: 16 waves, 4 per SIMD keep the matrix pipe fed
+// conv12's LDS image row stride: with 44 (== 12 mod 32) the conv1 MFMA operand reads (lane
+// rows {r, r+1} x 8 columns, lane groups one tap apart) and the VALU windows touch 32
+// distinct banks per half-wave; the dense 28 gave 2-way conflicts (bank model: profiles/
+// r2_lds_banks.md)
+constexpr int AB_IRS = 44;
 
 // conv2 implicit GEMM of one block: 4 position tiles x 4 K quarters (the 25
 // (ci-group, kh) rows split 6/7/6/6) over 16 waves; the quarters meet in LDS in a fixed
@@ -287,7 +292,7 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
   for (int u = 0; u < NU; ++u) {
     const int pt1 = t0 + 16 * u;
     const int py = pt1 / 3, px = pt1 - py * 3;
-    ibs[u] = img + (2 * py + (i >> 3)) * 28 + 8 * px + (i & 7);
+    ibs[u] = img + (2 * py + (i >> 3)) * AB_IRS + 8 * px + (i & 7);
     acc[u] = zero4();
   }
   // every LDS operand read is issued before the first MFMA (the scheduler would otherwise
@@ -321,34 +326,34 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
       if (pB > mB) { mB = pB; aB = 2 + paB; }
       const int pw = 4 * px + 2 * (g & 1);
       const float va = fmaxf(mA, 0.f), vb = fmaxf(mB, 0.f);
-      in_s[c * C2_CS + py * C2_RS + pw] = va;
-      in_s[c * C2_CS + py * C2_RS + pw + 1] = vb;
+      // pw is even: one 8-byte LDS / global store per pair
+      *reinterpret_cast<float2*>(in_s + c * C2_CS + py * C2_RS + pw) = make_float2(va, vb);
       if (pub) {
         const size_t o = (size_t)b * 2880 + c * 144 + py * 12 + pw;
-        a1[o] = va;
-        a1[o + 1] = vb;
-        idx1[o] = (uint8_t)aA;
-        idx1[o + 1] = (uint8_t)aB;
+        *reinterpret_cast<float2*>(a1 + o) = make_float2(va, vb);
+        *reinterpret_cast<uchar2*>(idx1 + o) = make_uchar2((uint8_t)aA, (uint8_t)aB);
       }
     }
   }
 }
 
 // conv1 channels 16-19 on the VALU (f32 FMA runs at the f32 MFMA rate): one pooled output
-// per thread, item = (c - 16) * 144 + pooled position.  Same tap order as the MFMA chain
-// and the standalone conv1 kernel (bit-identical results).
+// per thread, item = pooled position * 4 + (c - 16): the four channels of a position share
+// the image reads (broadcast), so a 32-lane half reads 8 windows at stride 2 -- with the
+// AB_IRS row stride every read is conflict-free.  Same tap order as the MFMA chain and the
+// standalone conv1 kernel (bit-identical results).
 __device__ __forceinline__ void conv1_valu_window(int item, const float* img, const float* w1s,
                                                   float* in_s, bool pub, float* a1, uint8_t* idx1,
                                                   int b) {
-  const int c = 16 + item / 144, p = item - (c - 16) * 144;
+  const int c = 16 + (item & 3), p = item >> 2;
   const int ph = p / 12, pw = p - ph * 12;
-  const float* im = img + (2 * ph) * 28 + 2 * pw;
+  const float* im = img + (2 * ph) * AB_IRS + 2 * pw;
   const float* wc = w1s + c * 25;
   float patch[6][6];
 #pragma unroll
   for (int r = 0; r < 6; ++r)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) patch[r][q] = im[r * 28 + q];
+    for (int q = 0; q < 6; ++q) patch[r][q] = im[r * AB_IRS + q];
   float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
 #pragma unroll
   for (int kh = 0; kh < 5; ++kh)
@@ -380,9 +385,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
     uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
-  __shared__ float img[784];
+  __shared__ float img[28 * AB_IRS];
   __shared__ float w1s[520];
-  __shared__ float in_s[20 * C2_CS];
+  __shared__ __align__(16) float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
       const int co = min(cg * 16 + j, 49);
       wq[k] = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
     }
-    if (tid < 784) img[tid] = x0;
+    if (tid < 784) img[(tid / 28) * AB_IRS + tid % 28] = x0;
     if (tid < 500) w1s[tid] = wv;
     if (tid < 20) w1s[500 + tid] = bv1;
 #pragma unroll
@@ -440,7 +445,7 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     for (int s = 0; s < 7; ++s) {
       const int tap = 4 * s + g;
       const int tc = tap < 25 ? tap : 24;
-      toff[s] = (tc / 5) * 28 + (tc % 5);
+      toff[s] = (tc / 5) * AB_IRS + (tc % 5);
       const float wv_ = w1s[i * 25 + tc];
       bw[s] = tap < 25 ? wv_ : 0.f;
     }
@@ -2115,7 +2120,7 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
   PTO_CHECK_B(B);
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
-  if (((uintptr_t)w2) & 15) return -2;
+  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 1)) return -2;
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
   hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
                      b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, g_dbg);
