@@ -45,6 +45,12 @@ def parse_args(argv=None):
     p.add_argument("--grad-checkpoint", action="store_true", help="Llama: recompute blocks in backward")
     p.add_argument("--master-weights", choices=["auto", "on", "off"], default="auto",
                    help="Llama: bf16 matmul weights + fp32 masters in the fused HIP AdamW (auto: on with a GPU)")
+    p.add_argument("--conv-algo-search", choices=["on", "off"], default="on",
+                   help="ResNet: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)")
+    p.add_argument("--memory-format", choices=["channels_last", "contiguous"], default="channels_last",
+                   help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
+    p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
+                   help="ResNet SGD implementation (fused: one multi-tensor kernel per step)")
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--json-out", default=None)
@@ -56,8 +62,14 @@ def build(args, device):
     if args.model.startswith("resnet"):
         from ..models.resnet import resnet50, resnet_tiny
         model = resnet50() if args.model == "resnet50" else resnet_tiny()
-        model = model.to(device=device, memory_format=torch.channels_last)
-        opt = torch.optim.SGD(model.parameters(), lr=args.lr or 0.1, momentum=0.9, weight_decay=1e-4)
+        fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format
+        model = model.to(device=device, memory_format=fmt)
+        if device.type == "cuda":
+            torch.backends.cudnn.benchmark = args.conv_algo_search == "on"
+        kw = {}
+        if device.type == "cuda":
+            kw = {"fused": True} if args.sgd == "fused" else {"foreach": True}
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr or 0.1, momentum=0.9, weight_decay=1e-4, **kw)
         return model, opt
     from ..models.llama import CONFIGS, Llama
     with torch.device(device):
@@ -162,7 +174,9 @@ def main(argv=None) -> int:
         x, y = data[:, :-1].contiguous(), data[:, 1:].contiguous()
     else:
         H = args.image_size if args.model == "resnet50" else 32
-        x = torch.randn(B, 3, H, H, generator=g).to(dev).to(memory_format=torch.channels_last)
+        x = torch.randn(B, 3, H, H, generator=g).to(dev)
+        if args.memory_format == "channels_last":
+            x = x.to(memory_format=torch.channels_last)
         y = torch.randint(0, 1000 if args.model == "resnet50" else 10, (B,), generator=g).to(dev)
     amp = torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=args.dtype == "bf16")
 
@@ -219,6 +233,8 @@ def main(argv=None) -> int:
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev)}
+    if not is_llama:
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd)
     digest = param_digest(model.module if hasattr(model, "module") else model, opt)
     print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest}), flush=True)
     if rank == 0:
