@@ -49,6 +49,8 @@ def parse_args(argv=None):
                    help="ResNet: let MIOpen benchmark conv algorithms per shape (torch.backends.cudnn.benchmark)")
     p.add_argument("--memory-format", choices=["channels_last", "contiguous"], default="channels_last",
                    help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
+    p.add_argument("--bn", choices=["hip", "library"], default="hip",
+                   help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
     p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
                    help="ResNet SGD implementation (fused: one multi-tensor kernel per step)")
     p.add_argument("--lr", type=float, default=None)
@@ -60,8 +62,8 @@ def parse_args(argv=None):
 def build(args, device):
     import torch
     if args.model.startswith("resnet"):
-        from ..models.resnet import resnet50, resnet_tiny
-        model = resnet50() if args.model == "resnet50" else resnet_tiny()
+        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl
+        model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
         fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format
         model = model.to(device=device, memory_format=fmt)
         if device.type == "cuda":
@@ -234,7 +236,7 @@ def main(argv=None) -> int:
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev)}
     if not is_llama:
-        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd)
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn)
     digest = param_digest(model.module if hasattr(model, "module") else model, opt)
     print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest}), flush=True)
     if rank == 0:

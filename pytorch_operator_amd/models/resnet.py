@@ -5,7 +5,10 @@ north-star job shape: Master=1 Worker=7, one ``amd.com/gpu`` each, bf16.  The ne
 the standard torchvision-style ResNet-50 v1.5 (stride on the 3x3 conv of each
 bottleneck), written out here because torchvision is not in this image.  On MI355X it
 runs channels-last under bf16 autocast: convolutions go to MIOpen, the classifier GEMM to
-hipBLASLt -- plain library kernels, as the MI355X guidance prescribes for non-fused work.
+hipBLASLt (plain library kernels), while every batch-norm with the ReLU and residual add
+around it is one fused HIP op (``ops/batchnorm.py``: ``relu(bn(x) [+ identity])`` in one
+statistics + one normalise pass, its backward in one reduction + one dx pass).
+``set_bn_impl(model, "library")`` switches back to PyTorch's batch-norm / add / ReLU ops.
 """
 from __future__ import annotations
 
@@ -13,6 +16,8 @@ from typing import List, Optional
 
 import torch
 import torch.nn as nn
+
+from ..ops.batchnorm import BatchNormAct2d
 
 
 class Bottleneck(nn.Module):
@@ -22,20 +27,18 @@ class Bottleneck(nn.Module):
         super().__init__()
         width = planes
         self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = BatchNormAct2d(width, relu=True)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = BatchNormAct2d(width, relu=True)
         self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BatchNormAct2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), idt)
 
 
 class ResNet(nn.Module):
@@ -43,8 +46,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = width
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct2d(width, relu=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(width, layers[0])
         self.layer2 = self._make(width * 2, layers[1], stride=2)
@@ -66,16 +68,26 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
             down = nn.Sequential(nn.Conv2d(self.inplanes, planes * Bottleneck.expansion, 1, stride=stride, bias=False),
-                                 nn.BatchNorm2d(planes * Bottleneck.expansion))
+                                 BatchNormAct2d(planes * Bottleneck.expansion))
         layers = [Bottleneck(self.inplanes, planes, stride, down)]
         self.inplanes = planes * Bottleneck.expansion
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def set_bn_impl(model: nn.Module, impl: str) -> nn.Module:
+    """``"hip"``: fused HIP batch-norm(+add)(+ReLU) kernels; ``"library"``: PyTorch's ops."""
+    if impl not in ("hip", "library"):
+        raise ValueError(impl)
+    for m in model.modules():
+        if isinstance(m, BatchNormAct2d):
+            m.impl = impl
+    return model
 
 
 def resnet50(num_classes: int = 1000) -> ResNet:

@@ -130,6 +130,10 @@ _SIGNATURES = {
     "pto_swiglu_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _VP],
     # adamw.hip
     "pto_adamw_step": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _VP],
+    # batchnorm.hip
+    "pto_bn_plan": [_L, _I, ctypes.POINTER(_I)],
+    "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP],
+    "pto_bn_bwd": [_VP] * 13 + [_L, _I, _I, _I, _I, _I, _VP],
     # graph_exec.hip
     "pto_graph_begin": [_VP],
     "pto_graph_end": [_VP, ctypes.POINTER(_VP)],

@@ -1,0 +1,147 @@
+"""Training-mode BatchNorm2d (+ residual add) (+ ReLU) on HIP kernels (``csrc/kernels/batchnorm.hip``).
+
+The ResNet-50 worker's step is 58 % batch-norm and elementwise passes on the library path
+(MIOpen mean/variance + normalise, then separate clamp / add / threshold-backward kernels:
+``profiles/r2_resnet50_kernels.md``).  ``batch_norm_act`` fuses a bottleneck's
+``relu(bn(x) [+ residual])`` into one statistics pass and one normalise pass, and its
+backward into one reduction pass and one dx pass (the ReLU mask is recomputed from x when no
+residual was added), for channels-last fp32/bf16 activations.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and state dict)
+whose forward takes an optional residual and applies the ReLU itself.  Its ``impl``
+(``"hip"`` / ``"library"``) selects the HIP kernels or PyTorch's own ops on a GPU; on CPU, in
+eval mode, for unsupported shapes (C/8 must divide 256) or cumulative-average momentum it
+always runs the PyTorch ops -- the numerics reference of the tests.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def supported(x: torch.Tensor) -> bool:
+    C = x.shape[1] if x.dim() == 4 else 0
+    return x.is_cuda and x.dim() == 4 and x.dtype in _DT and C % 8 == 0 and 8 <= C <= 2048 and 256 % (C // 8) == 0
+
+
+def reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual):
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def _nhwc(t: torch.Tensor, dtype) -> torch.Tensor:
+    return t.to(dtype).contiguous(memory_format=torch.channels_last)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _plan(lib, M: int, C: int):
+    rpb = ctypes.c_int(0)
+    G = lib.pto_bn_plan(M, C, ctypes.byref(rpb))
+    if G <= 0:
+        raise ValueError(f"batch_norm_act: unsupported channel count {C}")
+    return G, rpb.value
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        lib = _native.load()
+        N, C, H, W = x.shape
+        M = N * H * W
+        xc = _nhwc(x, x.dtype)
+        z = _nhwc(residual, x.dtype) if residual is not None else None
+        y = torch.empty_like(xc, memory_format=torch.channels_last)
+        G, rpb = _plan(lib, M, C)
+        f32 = dict(device=x.device, dtype=torch.float32)
+        part = torch.empty(G * (2 * C + 1), **f32)
+        stats = torch.empty(4 * C, **f32)  # mean | rstd | scale | shift
+        _native.check(lib.pto_bn_fwd_train(
+            xc.data_ptr(), _ptr(z), y.data_ptr(), weight.data_ptr(), bias.data_ptr(), _ptr(running_mean),
+            _ptr(running_var), _ptr(nbt), stats.data_ptr(), stats[C:].data_ptr(), stats[2 * C:].data_ptr(),
+            part.data_ptr(), M, C, G, rpb, float(momentum), float(eps), _DT[x.dtype], int(relu), _stream(x)),
+            "bn_fwd_train")
+        ctx.mask = 0 if not relu else (2 if residual is not None else 1)
+        ctx.has_res = residual is not None
+        ctx.res_dtype = residual.dtype if residual is not None else None
+        ctx.plan = (M, C, G, rpb)
+        ctx.save_for_backward(xc, y if ctx.mask == 2 else None, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _native.load()
+        xc, y, weight, stats = ctx.saved_tensors
+        M, C, G, rpb = ctx.plan
+        dyc = _nhwc(dy, xc.dtype)
+        dx = torch.empty_like(xc, memory_format=torch.channels_last)
+        dz = torch.empty_like(xc, memory_format=torch.channels_last) if ctx.has_res else None
+        f32 = dict(device=xc.device, dtype=torch.float32)
+        part = torch.empty(G * 2 * C, **f32)
+        coef = torch.empty(3 * C, **f32)
+        dgb = torch.empty(2 * C, **f32)
+        _native.check(lib.pto_bn_bwd(
+            dyc.data_ptr(), xc.data_ptr(), _ptr(y), weight.data_ptr(), stats.data_ptr(), stats[C:].data_ptr(),
+            stats[2 * C:].data_ptr(), dgb.data_ptr(), dgb[C:].data_ptr(), dx.data_ptr(), _ptr(dz), part.data_ptr(),
+            coef.data_ptr(), M, C, G, rpb, _DT[xc.dtype], ctx.mask, _stream(xc)), "bn_bwd")
+        dgamma, dbeta = dgb[:C].to(weight.dtype), dgb[C:].to(weight.dtype)
+        if dz is not None and dz.dtype != ctx.res_dtype:
+            dz = dz.to(ctx.res_dtype)
+        return dx, dgamma, dbeta, dz, None, None, None, None, None, None
+
+
+def batch_norm_act(x, weight, bias, running_mean=None, running_var=None, num_batches_tracked=None,
+                   training=True, momentum=0.1, eps=1e-5, relu=False, residual=None, impl="hip"):
+    """``relu(batch_norm(x) [+ residual])`` (training statistics when ``training``)."""
+    if (impl != "hip" or not training or momentum is None or not supported(x) or weight is None
+            or weight.dtype != torch.float32):
+        if training and num_batches_tracked is not None:
+            num_batches_tracked.add_(1)
+        return reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual)
+    return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, num_batches_tracked, momentum, eps,
+                        relu)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + optional residual add + optional ReLU, one fused op on MI355X."""
+
+    def __init__(self, num_features: int, relu: bool = False, **kw):
+        super().__init__(num_features, **kw)
+        self.relu = relu
+        self.impl = "hip"
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        training = self.training or not self.track_running_stats
+        momentum = self.momentum
+        if momentum is None and training and self.track_running_stats:
+            return self._cumulative(x, residual)
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
+        return batch_norm_act(x, self.weight, self.bias, rm, rv, nbt, training, momentum if momentum is not None else 0.0,
+                              self.eps, self.relu, residual, self.impl)
+
+    def _cumulative(self, x, residual):
+        self.num_batches_tracked.add_(1)
+        f = 1.0 / float(self.num_batches_tracked)
+        return reference(x, self.weight, self.bias, self.running_mean, self.running_var, True, f, self.eps,
+                         self.relu, residual)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", relu={self.relu}"
