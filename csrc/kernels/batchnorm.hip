@@ -20,7 +20,9 @@
 namespace {
 
 constexpr int BN_NT = 256;
-constexpr int FIN_CH = 64;  // channels per finalize block (4 partial groups x 64 channels)
+constexpr int FIN_CH = 16;  // finalize blocks: 16 channels x 64 partial groups = 1024 threads
+constexpr int FIN_G = 64;
+constexpr int FIN_NT = FIN_CH * FIN_G;
 
 typedef __hip_bfloat16 bf16;
 
@@ -135,27 +137,33 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_kernel(const T* __restrict__ x
 
 // ---- forward 2: merge the G partials; mean / rstd for the backward, scale/shift for the
 // apply kernel, running statistics (and num_batches_tracked) updated in place
-__global__ __launch_bounds__(BN_NT) void bn_stats_finalize_kernel(
+__global__ __launch_bounds__(FIN_NT) void bn_stats_finalize_kernel(
     const float* __restrict__ part, const float* __restrict__ part_n, int G, int C, float eps, float momentum,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, float* __restrict__ ss, float* __restrict__ run_mean,
     float* __restrict__ run_var, long long* __restrict__ nbt) {
-  __shared__ float s_n[4][FIN_CH], s_m[4][FIN_CH], s_q[4][FIN_CH];
+  __shared__ float s_n[FIN_G][FIN_CH], s_m[FIN_G][FIN_CH], s_q[FIN_G][FIN_CH];
   const int pg = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH, c = blockIdx.x * FIN_CH + cl;
   float n = 0.f, m = 0.f, q = 0.f;
   if (c < C)
-    for (int g = pg; g < G; g += 4) chan(n, m, q, part_n[g], part[(size_t)g * 2 * C + c], part[(size_t)g * 2 * C + C + c]);
+    for (int g = pg; g < G; g += FIN_G) chan(n, m, q, part_n[g], part[(size_t)g * 2 * C + c], part[(size_t)g * 2 * C + C + c]);
   s_n[pg][cl] = n; s_m[pg][cl] = m; s_q[pg][cl] = q;
   __syncthreads();
+  for (int w = FIN_G / 2; w >= 1; w >>= 1) {  // fixed-shape tree: deterministic
+    if (pg < w) {
+      chan(n, m, q, s_n[pg + w][cl], s_m[pg + w][cl], s_q[pg + w][cl]);
+      s_n[pg][cl] = n; s_m[pg][cl] = m; s_q[pg][cl] = q;
+    }
+    __syncthreads();
+  }
   if (pg == 0 && c < C) {
-    for (int p = 1; p < 4; ++p) chan(n, m, q, s_n[p][cl], s_m[p][cl], s_q[p][cl]);
     const float var = n > 0.f ? q / n : 0.f;
     const float rstd = rsqrtf(var + eps);
     const float sc = gamma[c] * rstd;
     mean_out[c] = m;
     rstd_out[c] = rstd;
     ss[c] = sc;
-    ss[C + c] = beta[c] - m * sc;
+    ss[C + c] = beta[c];
     if (run_mean != nullptr) {
       const float unb = n > 1.f ? q / (n - 1.f) : var;
       run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * m;
@@ -165,18 +173,20 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_finalize_kernel(
   if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
 }
 
-// ---- forward 3: y = x * scale + shift [+ z] [ReLU]; the grid stride is a multiple of C/8,
-// so a thread's channels (and its scale/shift registers) never change
+// ---- forward 3: y = (x - mean) * scale + beta [+ z] [ReLU] (centred first: no cancellation
+// of x * scale against mean * scale near the ReLU boundary); the grid stride is a multiple
+// of C/8, so a thread's channels (and its per-channel registers) never change
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
-                                                         const float* __restrict__ ss, T* __restrict__ y,
+                                                         const float* __restrict__ ss,
+                                                         const float* __restrict__ mean, T* __restrict__ y,
                                                          long nvec, int C) {
   const int tpr = C >> 3;
   const long i0 = (long)blockIdx.x * BN_NT + threadIdx.x, stride = (long)gridDim.x * BN_NT;
   const int cv = (int)(i0 % tpr);
-  float sc[8], sh[8];
+  float sc[8], sh[8], mu[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { sc[j] = ss[cv * 8 + j]; sh[j] = ss[C + cv * 8 + j]; }
+  for (int j = 0; j < 8; ++j) { sc[j] = ss[cv * 8 + j]; sh[j] = ss[C + cv * 8 + j]; mu[j] = mean[cv * 8 + j]; }
   long i = i0;
   for (; i + stride < nvec; i += 2 * stride) {
     float a[2][8], b[2][8];
@@ -189,7 +199,7 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = fmaf(a[u][j], sc[j], sh[j]);
+        float v = fmaf(a[u][j] - mu[j], sc[j], sh[j]);
         if (RES) v += b[u][j];
         a[u][j] = RELU ? fmaxf(v, 0.f) : v;
       }
@@ -202,7 +212,7 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
     if (RES) V8<T>::ld(z + i * 8, b);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float v = fmaf(a[j], sc[j], sh[j]);
+      float v = fmaf(a[j] - mu[j], sc[j], sh[j]);
       if (RES) v += b[j];
       a[j] = RELU ? fmaxf(v, 0.f) : v;
     }
@@ -210,16 +220,17 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
   }
 }
 
-// ReLU mask of the backward: MASK 0 = no ReLU, 1 = recompute x*scale+shift > 0 (bitwise the
-// forward's value), 2 = y > 0 (a residual was added before the ReLU)
+// ReLU mask of the backward: MASK 0 = no ReLU, 1 = recompute (x-mean)*scale+beta > 0 (bitwise
+// the forward's value), 2 = y > 0 (a residual was added before the ReLU)
 template <typename T, int MASK>
 __device__ __forceinline__ void masked_grad(const T* dy, const T* x, const T* y, long e, const float (&sc)[8],
-                                            const float (&sh)[8], float (&g)[8], float (&xv)[8]) {
+                                            const float (&sh)[8], const float (&mu)[8], float (&g)[8],
+                                            float (&xv)[8]) {
   V8<T>::ld(dy + e, g);
   V8<T>::ld(x + e, xv);
   if (MASK == 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j] - mu[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
   } else if (MASK == 2) {
     float yv[8];
     V8<T>::ld(y + e, yv);
@@ -248,7 +259,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
   for (; r + rpi < r1; r += 2 * rpi) {
     float g[2][8], xv[2][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) masked_grad<T, MASK>(dy, x, y, (r + u * rpi) * C + cv * 8, sc, sh, g[u], xv[u]);
+    for (int u = 0; u < 2; ++u) masked_grad<T, MASK>(dy, x, y, (r + u * rpi) * C + cv * 8, sc, sh, mu, g[u], xv[u]);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -256,7 +267,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
   }
   for (; r < r1; r += rpi) {
     float g[8], xv[8];
-    masked_grad<T, MASK>(dy, x, y, r * C + cv * 8, sc, sh, g, xv);
+    masked_grad<T, MASK>(dy, x, y, r * C + cv * 8, sc, sh, mu, g, xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { a[j] += g[j]; b[j] = fmaf(g[j], xv[j] - mu[j], b[j]); }
   }
@@ -275,21 +286,27 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
 
 // ---- backward 2: dgamma, dbeta and the per-channel dx = ca*g + cb*(x - mean) + cc coefficients
 // (x - mean, not x: no cancellation against a large mean)
-__global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, long M,
+__global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_kernel(const float* __restrict__ part, int G, int C, long M,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ rstd,
                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                 float* __restrict__ coef) {
-  __shared__ float s_a[4][FIN_CH], s_b[4][FIN_CH];
+  __shared__ float s_a[FIN_G][FIN_CH], s_b[FIN_G][FIN_CH];
   const int pg = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH, c = blockIdx.x * FIN_CH + cl;
   float a = 0.f, b = 0.f;
   if (c < C)
-    for (int g = pg; g < G; g += 4) { a += part[(size_t)g * 2 * C + c]; b += part[(size_t)g * 2 * C + C + c]; }
+    for (int g = pg; g < G; g += FIN_G) { a += part[(size_t)g * 2 * C + c]; b += part[(size_t)g * 2 * C + C + c]; }
   s_a[pg][cl] = a; s_b[pg][cl] = b;
   __syncthreads();
+  for (int w = FIN_G / 2; w >= 1; w >>= 1) {
+    if (pg < w) {
+      a += s_a[pg + w][cl]; b += s_b[pg + w][cl];
+      s_a[pg][cl] = a; s_b[pg][cl] = b;
+    }
+    __syncthreads();
+  }
   if (pg == 0 && c < C) {
-    for (int p = 1; p < 4; ++p) { a += s_a[p][cl]; b += s_b[p][cl]; }
     const float rs = rstd[c], sc = gamma[c] * rs, inv = 1.f / (float)M;
     dgamma[c] = b * rs;
     dbeta[c] = a;
@@ -318,7 +335,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_kernel(const T* __restrict__ 
   }
   for (long i = i0; i < nvec; i += stride) {
     float g[8], xv[8];
-    masked_grad<T, MASK>(dy, x, y, i * 8, sc, sh, g, xv);
+    masked_grad<T, MASK>(dy, x, y, i * 8, sc, sh, mu, g, xv);
     if (DZ) V8<T>::st(dz + i * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = fmaf(ca[j], g[j], fmaf(cb[j], xv[j] - mu[j], cc[j]));
@@ -340,18 +357,18 @@ int fwd_t(const void* x, const void* z, void* y, const float* gamma, const float
           float momentum, float eps, int relu, hipStream_t s) {
   const T* xt = static_cast<const T*>(x);
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G), dim3(BN_NT), 0, s, xt, M, C, rpb, part, part + (size_t)G * 2 * C);
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(BN_NT), 0, s, part,
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part,
                      part + (size_t)G * 2 * C, G, C, eps, momentum, gamma, beta, mean, rstd, ss, rm, rv, nbt);
   const long nvec = M * (long)C / 8;
   const int gr = grid_for(nvec, C);
   const T* zt = static_cast<const T*>(z);
   T* yt = static_cast<T*>(y);
   if (z != nullptr) {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, yt, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, yt, nvec, C);
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, yt, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, yt, nvec, C);
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
   }
   return (int)hipGetLastError();
 }
@@ -372,7 +389,7 @@ int bwd_t(const void* dy, const void* x, const void* y, const float* gamma, cons
   const T* xt = static_cast<const T*>(x);
   const T* yt = static_cast<const T*>(y);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK>), dim3(G), dim3(BN_NT), 0, s, dyt, xt, yt, ss, mean, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(BN_NT), 0, s, part, G, C, M, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part, G, C, M, gamma,
                      mean, rstd, dgamma, dbeta, coef);
   bwd_dx_launch<T, MASK>(dyt, xt, yt, ss, coef, mean, static_cast<T*>(dx), static_cast<T*>(dz), M * (long)C / 8, C, s);
   return (int)hipGetLastError();

@@ -17,4 +17,4 @@ timeout -k 10 500 python3 -m pytorch_operator_amd.harness.ddp_train --model resn
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d /tmp/rprof -o run --output-format csv -- python3 -m pytorch_operator_amd.harness.ddp_train --model resnet50 --batch-size 256 --steps 10 --warmup 5 "$@" > gpurun_out/rprof/out.log 2>&1 || { tail -20 gpurun_out/rprof/out.log; exit 1; }
 grep '"metric"' gpurun_out/rprof/out.log
 f=$(find /tmp/rprof -name "*kernel_trace.csv" | head -1)
-python3 tools/kstats_summary.py --trace "$f" FusedSgd 8 15 | tee gpurun_out/rprof/summary.md
+python3 tools/kstats_summary.py --trace "$f" FusedSgd 8 15 | tee gpurun_out/rprof/summary_${TAG:-run}.md; rm -rf /tmp/rprof

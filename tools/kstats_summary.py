@@ -13,8 +13,9 @@ import re
 import sys
 
 FAMILIES = [
-    ("conv bwd-weight", r"bwd_weight|wrw"), ("conv bwd-data", r"bwd_data|_bwd_"), ("conv fwd", r"conv.*fwd|fwd.*conv|igemm|xdl.*conv"),
-    ("batch-norm", r"batch_norm|batchnorm|MIOpenBatchNorm|bn_"), ("gemm", r"Cijk|gemm|hipblaslt"),
+    ("batch-norm", r"batch_norm|batchnorm|MIOpenBatchNorm|\bbn_|::bn_"),
+    ("conv bwd-weight", r"bwd_weight|wrw"), ("conv bwd-data", r"bwd_data|igemm_bwd|naive_conv.*_bwd_"),
+    ("conv fwd", r"conv.*fwd|fwd.*conv|igemm|xdl.*conv"), ("gemm", r"Cijk|gemm|hipblaslt"),
     ("sgd/optimizer", r"sgd|multi_tensor|foreach|_fused_"), ("reduce", r"reduce"),
     ("elementwise", r"elementwise|vectorized|unrolled"), ("pool", r"pool"),
 ]
