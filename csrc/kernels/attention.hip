@@ -1,0 +1,508 @@
+// Causal / full GQA flash attention, forward and backward, bf16 in / bf16 out, for the Llama
+// DDP worker (BASELINE "Llama-3 8B DDP bf16").  Replaces scaled_dot_product_attention (whose
+// ROCm kernels ran at 328 TF/s forward and 156 TF/s backward on the 8B step,
+// profiles/r1_llama3_8b_kernel_stats_master_adamw.md) and the [B,S,H,D] <-> [B,H,S,D]
+// transposes around it: q/k/v/o/dq/dk/dv are read and written in the projections' own
+// token-major layout [B, S, H, D].
+//
+// Layout and MFMA plan (v_mfma_f32_32x32x16_bf16; D = 128 = 8 k-steps / 4 output tiles):
+//   * every kernel keeps one index "on the lane" (MFMA column = lane & 31) so that the
+//     softmax statistics are per-lane scalars and an accumulator tile feeds the next MFMA
+//     as its B operand with no data movement (the accumulator-as-operand k permutation:
+//     registers 8s..8s+7 are k-step s; the other operand is read in the matching order);
+//   * K/V (forward, dQ pass) and Q/dO (dK/dV pass) tiles are staged global -> registers ->
+//     LDS once per tile (loads of tile t+1 in flight under the MFMAs of tile t, one
+//     barrier per tile) in an XOR-swizzled 256-byte-row image that serves BOTH the row
+//     reads (ds_read_b128) and the hardware-transposed reads (ds_read_b64_tr_b16)
+//     conflict-free;
+//   * forward: 4 waves x 32 queries per workgroup, 64-key tiles; S^T = K.Q^T (query on the
+//     lane), online softmax in exp2 units, O^T += V^T.P^T; O is staged through LDS and
+//     stored as whole rows; lse2 = m + log2(l) (log2 units) is kept for the backward;
+//   * backward, pass 1 (dQ): same shape as the forward; recomputes S^T and dP^T = V.dO^T,
+//     dS = P*(dP - delta), dQ^T += K^T.dS^T; computes delta = rowsum(dO*O) itself and
+//     writes it for pass 2.  Every dQ row is finished inside one workgroup: no atomics;
+//   * backward, pass 2 (dK, dV): 4 waves x 32 keys per workgroup (key on the lane), sweeps
+//     the Hq/Hkv query heads of its kv head and every query tile at or after its keys;
+//     S = Q.K^T, dP = dO.V^T, dV^T += dO^T.P, dK^T += Q^T.dS.  Deterministic, no atomics.
+//   Causal workgroups run heaviest-first; tiles wholly above the diagonal are skipped per
+//   wave.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t bf16_t;
+// native clang vectors (HIP's u32x4 is a struct: copies of it into arrays become memcpys that
+// keep the staging arrays in scratch)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int D = 128;       // head dim (the 8B / 70B Llama-3 value)
+constexpr int NDS = D / 16;  // k-steps of a d-contraction
+constexpr int NDT = D / 32;  // 32-wide output tiles along d
+constexpr int BM = 128;      // query rows per forward / dQ workgroup (32 per wave)
+constexpr int BN = 64;       // keys per K/V tile
+constexpr int BK = 128;      // keys per dK/dV workgroup (32 per wave)
+constexpr int QT = 32;       // query rows per dK/dV tile
+constexpr int NT = 256;
+constexpr int CH = D / 8;    // 16-byte chunks per row (16)
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// XOR-swizzled image of a [rows][128] bf16 tile, in 16-byte units: chunk ch of row r.
+// Row reads of 16 consecutive rows at one chunk and transposed 4-row x 16-column reads both
+// hit 64 distinct banks.
+__device__ __forceinline__ int xo(int r, int ch) { return r * CH + (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
+
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+// registers 8s..8s+7 of an accumulator as a bf16 MFMA operand (k-step s)
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  u32x4 u;
+  u.x = pk_bf16(a[8 * s + 0], a[8 * s + 1]);
+  u.y = pk_bf16(a[8 * s + 2], a[8 * s + 3]);
+  u.z = pk_bf16(a[8 * s + 4], a[8 * s + 5]);
+  u.w = pk_bf16(a[8 * s + 6], a[8 * s + 7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+// operand whose k runs along the tile's COLUMNS: element j <- [row][ch*8 + j]
+__device__ __forceinline__ bf16x8 row_frag(const u32x4* tile, int row, int ch) {
+  return __builtin_bit_cast(bf16x8, tile[xo(row, ch)]);
+}
+
+__device__ __forceinline__ s16x4 tr_read(const u32x4* tile, int row, int ch, int sub_bytes) {
+  const char* p = reinterpret_cast<const char*>(tile + xo(row, ch)) + sub_bytes;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// operand whose k runs along the tile's ROWS, in the accumulator-as-operand order: element j
+// of lane half h <- row rbase + 8*(j>>2) + 4h + (j&3), column cbase + (lane & 31).
+__device__ __forceinline__ bf16x8 tr_frag(const u32x4* tile, int rbase, int cbase, int lane) {
+  const int l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
+  const int r0 = rbase + 4 * (lane >> 5) + q;
+  const s16x4 lo = tr_read(tile, r0, col >> 3, (col & 7) * 2);
+  const s16x4 hi = tr_read(tile, r0 + 8, col >> 3, (col & 7) * 2);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v;
+  v.lo = lo;
+  v.hi = hi;
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// key/query row index of accumulator register i in lane half h (C/D map of 32x32x16)
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
+
+// Stage a [ROWS][128] bf16 tile (rows ROWS apart in global by `stride` elements) into the
+// XOR image: each thread moves ROWS*16/NT 16-byte chunks.
+template <int ROWS>
+struct Stage {
+  static constexpr int N = ROWS * CH / NT;
+  u32x4 r[N];
+  __device__ __forceinline__ void load(const bf16_t* base, size_t stride, int tid) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int e = tid + NT * i, row = e / CH, ch = e % CH;
+      r[i] = *reinterpret_cast<const u32x4*>(base + (size_t)row * stride + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(u32x4* tile, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int e = tid + NT * i, row = e / CH, ch = e % CH;
+      tile[xo(row, ch)] = r[i];
+    }
+  }
+};
+
+// Write a wave's 32 x 128 transposed accumulator (acc[dt] reg i = [d = dt*32 + acc_row(i,h)]
+// [col = lane & 31]) as rows [col][d] bf16 to global via the wave's LDS region (8 KB).
+__device__ __forceinline__ void store_rows_T(const f32x16 (&acc)[NDT], float scale, u32x4* stage, int lane,
+                                             bf16_t* out, size_t row_stride) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      u32x2 w;
+      w.x = pk_bf16(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+      w.y = pk_bf16(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+      *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(stage + xo(c, d0 >> 3)) + (d0 & 7) * 2) = w;
+    }
+  __syncthreads();  // every wave calls this together (after its tile loop)
+#pragma unroll
+  for (int i = 0; i < 32 * CH / 64; ++i) {
+    const int e = lane + 64 * i, row = e / CH, ch = e % CH;
+    *reinterpret_cast<u32x4*>(out + (size_t)row * row_stride + ch * 8) = stage[xo(row, ch)];
+  }
+}
+
+// ------------------------------------------------------------------------------- forward
+__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                         const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                         float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
+                                                         int causal) {
+  __shared__ u32x4 smem[4 * BN * CH];  // K0 V0 K1 V1 (64 KB)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int nqb = S / BM;
+  const int qblk = causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int bh = blockIdx.y, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
+  const int q0w = qblk * BM + w * 32;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS];
+  {
+    const bf16_t* qrow = q + ((size_t)b * S + q0w + r) * qstride + (size_t)hq * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) qf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(qrow + 16 * s));
+  }
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const int ntiles = causal ? (qblk * BM + BM) / BN : S / BN;
+
+  Stage<BN> ks, vs;
+  ks.load(kb, kvstride, tid);
+  vs.load(vb, kvstride, tid);
+  ks.store(smem, tid);
+  vs.store(smem + BN * CH, tid);
+  __syncthreads();
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  float m2 = -INFINITY, l = 0.f;
+  const int qme = q0w + r;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const u32x4* Ks = smem + cur * 2 * BN * CH;
+    const u32x4* Vs = Ks + BN * CH;
+    if (t + 1 < ntiles) {
+      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+    }
+    const int kv0 = t * BN;
+    if (!causal || kv0 <= q0w + 31) {
+      f32x16 sacc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        sacc[kt] = zero16();
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) sacc[kt] = mfma(row_frag(Ks, kt * 32 + r, 2 * s + h), qf[s], sacc[kt]);
+      }
+      if (causal && kv0 + BN - 1 > q0w) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kv0 + kt * 32 + acc_row(i, h) > qme) sacc[kt][i] = -INFINITY;
+      }
+      float mx = sacc[0][0];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kt][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mnew = fmaxf(m2, mx * c);
+      const float alpha = __builtin_amdgcn_exp2f(m2 - mnew);
+      m2 = mnew;
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], c, -mnew));
+          sacc[kt][i] = p;
+          rs += p;
+        }
+      l = fmaf(l, alpha, rs);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pb = acc_frag(sacc[kt], s2);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt)
+            oacc[dt] = mfma(tr_frag(Vs, kt * 32 + 16 * s2, dt * 32, lane), pb, oacc[dt]);
+        }
+    }
+    if (t + 1 < ntiles) {
+      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+      ks.store(nk, tid);
+      vs.store(nk + BN * CH, tid);
+    }
+    __syncthreads();
+  }
+  l += __shfl_xor(l, 32);
+  const float inv = 1.f / l;
+  store_rows_T(oacc, inv, smem + w * 32 * CH, lane, o + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+  if (h == 0) lse2[((size_t)b * Hq + hq) * S + qme] = m2 + log2f(l);
+}
+
+// ------------------------------------------------------------------- backward pass 1: dQ
+__global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
+    float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c, float scale, int causal) {
+  __shared__ u32x4 smem[4 * BN * CH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int nqb = S / BM;
+  const int qblk = causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int bh = blockIdx.y, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
+  const int q0w = qblk * BM + w * 32, qme = q0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS], df[NDS];
+  float dl;
+  {
+    const size_t off = ((size_t)b * S + qme) * qstride + (size_t)hq * D + 8 * h;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      const u32x4 qq = *reinterpret_cast<const u32x4*>(q + off + 16 * s);
+      const u32x4 dd = *reinterpret_cast<const u32x4*>(dout + off + 16 * s);
+      const u32x4 oo = *reinterpret_cast<const u32x4*>(o + off + 16 * s);
+      qf[s] = __builtin_bit_cast(bf16x8, qq);
+      df[s] = __builtin_bit_cast(bf16x8, dd);
+      const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w}, ow[4] = {oo.x, oo.y, oo.z, oo.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part = fmaf(bf2f(dw[e] & 0xffffu), bf2f(ow[e] & 0xffffu), part);
+        part = fmaf(bf2f(dw[e] >> 16), bf2f(ow[e] >> 16), part);
+      }
+    }
+    dl = part + __shfl_xor(part, 32);
+  }
+  const size_t srow = ((size_t)b * Hq + hq) * S + qme;
+  const float lq = lse2[srow];
+  if (h == 0) delta[srow] = dl;
+
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const int ntiles = causal ? (qblk * BM + BM) / BN : S / BN;
+  Stage<BN> ks, vs;
+  ks.load(kb, kvstride, tid);
+  vs.load(vb, kvstride, tid);
+  ks.store(smem, tid);
+  vs.store(smem + BN * CH, tid);
+  __syncthreads();
+
+  f32x16 dacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dacc[dt] = zero16();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const u32x4* Ks = smem + cur * 2 * BN * CH;
+    const u32x4* Vs = Ks + BN * CH;
+    if (t + 1 < ntiles) {
+      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+    }
+    const int kv0 = t * BN;
+    if (!causal || kv0 <= q0w + 31) {
+      const bool diag = causal && kv0 + BN - 1 > q0w;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 sa = zero16(), pa = zero16();
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) {
+          sa = mfma(row_frag(Ks, kt * 32 + r, 2 * s + h), qf[s], sa);
+          pa = mfma(row_frag(Vs, kt * 32 + r, 2 * s + h), df[s], pa);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lq));
+          if (diag && kv0 + kt * 32 + acc_row(i, h) > qme) p = 0.f;
+          sa[i] = p * (pa[i] - dl);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 db = acc_frag(sa, s2);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane), db, dacc[dt]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) {
+      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+      ks.store(nk, tid);
+      vs.store(nk + BN * CH, tid);
+    }
+    __syncthreads();
+  }
+  store_rows_T(dacc, scale, smem + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+}
+
+// -------------------------------------------------------------- backward pass 2: dK, dV
+__global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int Hq, int Hkv, float c, float scale, int causal) {
+  __shared__ u32x4 smem[4 * QT * CH];  // Q0 dO0 Q1 dO1 (32 KB); reused for the dK/dV epilogue
+  __shared__ float4 stat[2][2][QT / 4];  // [buf][lse2 | delta][32 rows]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int kblk = blockIdx.x;  // causal: kblk 0 (the most query tiles) launches first
+  const int bh = blockIdx.y, b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
+  const int k0w = kblk * BK + w * 32, kme = k0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 kf[NDS], vf[NDS];
+  {
+    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
+      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(v + off + 16 * s));
+    }
+  }
+  const int qt0 = causal ? (kblk * BK) / QT : 0;
+  const int nqt = S / QT - qt0;  // query tiles per head
+  const int ntiles = G * nqt;
+
+  auto tile_ptrs = [&](int t, const bf16_t*& qp, const bf16_t*& dp, size_t& srow) {
+    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
+    const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
+    qp = q + off;
+    dp = dout + off;
+    srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
+  };
+  Stage<QT> qs, ds;
+  float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](int t) {
+    const bf16_t *qp, *dp;
+    size_t srow;
+    tile_ptrs(t, qp, dp, srow);
+    qs.load(qp, qstride, tid);
+    ds.load(dp, qstride, tid);
+    if (tid < 16) st = reinterpret_cast<const float4*>((tid < 8 ? lse2 : delta) + srow)[tid & 7];
+  };
+  auto store = [&](int buf) {
+    qs.store(smem + buf * 2 * QT * CH, tid);
+    ds.store(smem + buf * 2 * QT * CH + QT * CH, tid);
+    if (tid < 16) stat[buf][tid >> 3][tid & 7] = st;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+
+  f32x16 dka[NDT], dva[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    dka[dt] = zero16();
+    dva[dt] = zero16();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const u32x4* Qs = smem + cur * 2 * QT * CH;
+    const u32x4* Ds = Qs + QT * CH;
+    if (t + 1 < ntiles) load(t + 1);
+    const int q0 = (qt0 + t % nqt) * QT;
+    if (!causal || k0w <= q0 + QT - 1) {
+      f32x16 sa = zero16(), pa = zero16();
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) {
+        sa = mfma(row_frag(Qs, r, 2 * s + h), kf[s], sa);
+        pa = mfma(row_frag(Ds, r, 2 * s + h), vf[s], pa);
+      }
+      const bool diag = causal && k0w + 31 > q0;
+      // rows (queries) of register group g: 8g + 4h + 0..3 -> one float4 of lse2 / delta
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 L4 = stat[cur][0][2 * g + h];
+        const float4 D4 = stat[cur][1][2 * g + h];
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
+          if (diag && kme > q0 + 8 * g + 4 * h + e) p = 0.f;
+          sa[i] = p;
+          pa[i] = p * (pa[i] - Dv[e]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pb = acc_frag(sa, s2), db = acc_frag(pa, s2);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          dva[dt] = mfma(tr_frag(Ds, 16 * s2, dt * 32, lane), pb, dva[dt]);
+          dka[dt] = mfma(tr_frag(Qs, 16 * s2, dt * 32, lane), db, dka[dt]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) store(cur ^ 1);
+    __syncthreads();
+  }
+  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+  store_rows_T(dva, 1.f, smem + w * 32 * CH, lane, dv + off, kvstride);
+  __syncthreads();
+  store_rows_T(dka, scale, smem + w * 32 * CH, lane, dk + off, kvstride);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
+  if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Dh != D) return -1;
+  if (S % BM || S % BK || Hq % Hkv) return -1;
+  if ((long)B * Hq > 65535 || (long)B * Hkv > 65535) return -1;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// q [B,S,Hq,128], k/v [B,S,Hkv,128] bf16 contiguous; o [B,S,Hq,128] bf16; lse2 [B,Hq,S] f32
+// (log2 units of the scaled scores).  S a multiple of 128, Hq a multiple of Hkv.
+int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse2, int B, int S, int Hq, int Hkv,
+                 int Dh, float scale, int causal, void* stream) {
+  if (check_shapes(B, S, Hq, Hkv, Dh)) return -1;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(lse2)) return -2;
+  const float c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / BM, B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, S, Hq, Hkv, c, causal);
+  return (int)hipGetLastError();
+}
+
+// dq [B,S,Hq,128], dk/dv [B,S,Hkv,128] bf16; delta [B,Hq,S] f32 scratch (rowsum(dO * O)).
+int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse2,
+                 float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int Dh, float scale,
+                 int causal, void* stream) {
+  if (check_shapes(B, S, Hq, Hkv, Dh)) return -1;
+  const void* ps[] = {q, k, v, o, dout, lse2, delta, dq, dk, dv};
+  for (const void* p : ps)
+    if (!aligned16(p)) return -2;
+  const float c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / BM, B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout, lse2, delta,
+                     (bf16_t*)dq, S, Hq, Hkv, c, scale, causal);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / BK, B * Hkv), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
+                     (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, S, Hq, Hkv, c, scale, causal);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -9,7 +9,10 @@ no sharding is needed -- every rank keeps the whole model and only gradients cro
 Architecture (Meta's reference layout): token embedding, ``n_layers`` x [RMSNorm ->
 GQA attention with RoPE (theta 500 000) -> residual, RMSNorm -> SwiGLU FFN -> residual],
 final RMSNorm, untied output projection.  Matmuls run in bf16 under autocast
-(hipBLASLt); attention uses ``scaled_dot_product_attention`` (ROCm flash attention).
+(hipBLASLt); attention runs the hand-written HIP flash attention (``ops.attention``, forward
+and backward on MFMA, token-major [B, S, H, D] in and out, so no transposes around it) for
+bf16 head_dim-128 shapes and ``scaled_dot_product_attention`` otherwise (``impl`` = "sdpa"
+forces the library path for A/B runs).
 The elementwise work between the matmuls runs as hand-written HIP kernels on a GPU:
 RMSNorm (``ops.norm``, fp32 statistics over the fp32 residual stream, bf16 output under
 autocast so the next matmul reads it directly), RoPE and SwiGLU (``ops.llm``, one HBM pass
@@ -54,6 +57,9 @@ CONFIGS = {
     "llama3-1b": LlamaConfig(dim=2048, n_layers=16, n_heads=32, n_kv_heads=8, ffn_hidden=8192),
     "llama-tiny": LlamaConfig(dim=64, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=256, ffn_hidden=128,
                               max_seq_len=256),
+    # smallest config with the 8B model's head_dim (128): exercises the HIP flash attention
+    "llama-mini": LlamaConfig(dim=512, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=512, ffn_hidden=1024,
+                              max_seq_len=1024),
 }
 
 
@@ -85,6 +91,8 @@ class RMSNorm(nn.Module):
 
 
 class Attention(nn.Module):
+    impl = "auto"  # "auto": HIP flash attention where it applies; "sdpa": library kernels
+
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.nh, self.nkv, self.hd = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
@@ -98,9 +106,12 @@ class Attention(nn.Module):
         q = apply_rope(self.wq(x).view(B, S, self.nh, self.hd), cos, sin)
         k = apply_rope(self.wk(x).view(B, S, self.nkv, self.hd), cos, sin)
         v = self.wv(x).view(B, S, self.nkv, self.hd)
-        q, k, v = (t.transpose(1, 2) for t in (q, k, v))  # [B, H, S, D]
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.nkv != self.nh)
-        return self.wo(o.transpose(1, 2).reshape(B, S, self.nh * self.hd))
+        from ..ops import attention as A
+        if self.impl != "sdpa" and A.hip_supported(q, k, v):
+            o = A.flash_attention(q, k, v, causal=True)  # [B, S, H, D], no transposes
+        else:
+            o = A.sdpa_bshd(q, k, v, causal=True)
+        return self.wo(o.reshape(B, S, self.nh * self.hd))
 
 
 class FeedForward(nn.Module):

@@ -134,6 +134,9 @@ _SIGNATURES = {
     "pto_bn_plan": [_L, _I, ctypes.POINTER(_I)],
     "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP],
     "pto_bn_bwd": [_VP] * 13 + [_L, _I, _I, _I, _I, _I, _VP],
+    # attention.hip
+    "pto_attn_fwd": [_VP] * 5 + [_I] * 5 + [_F, _I, _VP],
+    "pto_attn_bwd": [_VP] * 10 + [_I] * 5 + [_F, _I, _VP],
     # graph_exec.hip
     "pto_graph_begin": [_VP],
     "pto_graph_end": [_VP, ctypes.POINTER(_VP)],

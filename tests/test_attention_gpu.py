@@ -1,0 +1,97 @@
+"""Numerics of the HIP flash attention (csrc/kernels/attention.hip) against an fp32 PyTorch
+reference of the same op (forward output, log-sum-exp, and the three input gradients), with
+the library SDPA's own bf16 error as the yardstick."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # B, S, Hq, Hkv
+    (2, 256, 8, 2),
+    (1, 384, 4, 4),
+    (1, 512, 8, 1),
+]
+
+
+def _inputs(B, S, Hq, Hkv, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    mk = lambda H: torch.randn(B, S, H, 128, device="cuda", generator=g).to(torch.bfloat16)  # noqa: E731
+    return mk(Hq), mk(Hkv), mk(Hkv)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_flash_forward_matches_fp32_reference(shape, causal):
+    from pytorch_operator_amd.ops import _native
+    from pytorch_operator_amd.ops.attention import attention_reference, sdpa_bshd
+    B, S, Hq, Hkv = shape
+    q, k, v = _inputs(*shape)
+    ref, lse = attention_reference(q, k, v, causal, return_lse=True)
+    ref32 = attention_reference(q.float(), k.float(), v.float(), causal)
+    o = torch.empty_like(q)
+    lse2 = torch.empty(B, Hq, S, device="cuda")
+    _native.check(_native.load().pto_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                              lse2.data_ptr(), B, S, Hq, Hkv, 128, 1 / math.sqrt(128), int(causal),
+                                              torch.cuda.current_stream().cuda_stream), "attn_fwd")
+    torch.cuda.synchronize()
+    err = _rel(o, ref32)
+    lib = _rel(sdpa_bshd(q, k, v, causal), ref32)
+    assert err < max(2.0 * lib, 4e-3), (err, lib)
+    assert float((o.float() - ref32).abs().max()) < 3e-2
+    # lse2 is log2 units of the scaled scores
+    assert torch.allclose(lse2, lse * math.log2(math.e), atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_flash_backward_matches_fp32_reference(shape, causal):
+    from pytorch_operator_amd.ops.attention import attention_reference, flash_attention, sdpa_bshd
+    q, k, v = _inputs(*shape, seed=1)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    do = torch.randn(q.shape, device="cuda", generator=g).to(torch.bfloat16)
+
+    def grads(fn, *xs):
+        xs = [x.detach().clone().requires_grad_(True) for x in xs]
+        out = fn(*xs)
+        out.backward(do.to(out.dtype))
+        return [out.detach()] + [x.grad for x in xs]
+
+    ref = grads(lambda a, b, c: attention_reference(a, b, c, causal).float(), q.float(), k.float(), v.float())
+    ours = grads(lambda a, b, c: flash_attention(a, b, c, causal), q, k, v)
+    lib = grads(lambda a, b, c: sdpa_bshd(a, b, c, causal), q, k, v)
+    for name, a, r, lb in zip(("o", "dq", "dk", "dv"), ours, ref, lib):
+        e, el = _rel(a, r), _rel(lb, r)
+        assert e < max(2.0 * el, 6e-3), (name, e, el)
+        assert torch.isfinite(a.float()).all(), name
+
+
+def test_flash_llama_block_matches_sdpa_path():
+    """A D = 128 Llama config through the model's attention dispatch: HIP flash vs library SDPA."""
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    torch.manual_seed(0)
+    m = Llama(CONFIGS["llama-mini"]).cuda()
+    tok = torch.randint(0, CONFIGS["llama-mini"].vocab_size, (2, 256), device="cuda")
+    out = {}
+    for impl in ("hip", "sdpa"):
+        for blk in m.layers:
+            blk.attention.impl = impl
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):  # the worker's setting
+            loss = m(tok, tok)
+        loss.backward()
+        out[impl] = (float(loss), m.layers[0].attention.wq.weight.grad.float().clone())
+    assert abs(out["hip"][0] - out["sdpa"][0]) < 2e-2 * abs(out["sdpa"][0])
+    assert _rel(out["hip"][1], out["sdpa"][1]) < 5e-2
+
+
+def test_flash_rejects_unsupported_shape_on_gpu():
+    from pytorch_operator_amd.ops.attention import flash_attention
+    q = torch.zeros(1, 100, 2, 128, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        flash_attention(q, q, q)
