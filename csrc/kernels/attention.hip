@@ -24,8 +24,7 @@
 //   * backward, pass 2 (dK, dV): 4 waves x 32 keys per workgroup (key on the lane), sweeps
 //     the Hq/Hkv query heads of its kv head and every query tile at or after its keys;
 //     S = Q.K^T, dP = dO.V^T, dV^T += dO^T.P, dK^T += Q^T.dS.  Deterministic, no atomics.
-//   Causal workgroups run heaviest-first; tiles wholly above the diagonal are skipped per
-//   wave.
+//   Causal workgroups run heaviest-first (the block index is the slowest grid index).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -157,16 +156,27 @@ __device__ __forceinline__ void store_rows_T(const f32x16 (&acc)[NDT], float sca
   }
 }
 
+// Forward / dQ workgroup -> (query block, batch, q head, kv head).  The query block is the
+// slowest index of the launch order, heaviest (last) block first under the causal mask, so
+// the light blocks fill in behind the heavy ones across the whole grid.
+__device__ __forceinline__ void block_coords(int S, int B, int Hq, int Hkv, int causal, int& qblk, int& b, int& hq,
+                                             int& hk) {
+  const int nqb = S / BM, qi = (int)blockIdx.x / (B * Hq), bh = (int)blockIdx.x % (B * Hq);
+  qblk = causal ? nqb - 1 - qi : qi;
+  b = bh / Hq;
+  hq = bh % Hq;
+  hk = hq / (Hq / Hkv);
+}
+
 // ------------------------------------------------------------------------------- forward
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                          const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
-                                                         float* __restrict__ lse2, int S, int Hq, int Hkv, float c,
-                                                         int causal) {
+                                                         float* __restrict__ lse2, int B, int S, int Hq, int Hkv,
+                                                         float c, int causal) {
   __shared__ u32x4 smem[4 * BN * CH];  // K0 V0 K1 V1 (64 KB)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-  const int nqb = S / BM;
-  const int qblk = causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int bh = blockIdx.y, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
+  int qblk, b, hq, hk;
+  block_coords(S, B, Hq, Hkv, causal, qblk, b, hq, hk);
   const int q0w = qblk * BM + w * 32;
   const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
 
@@ -197,19 +207,34 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restric
     const int cur = t & 1;
     const u32x4* Ks = smem + cur * 2 * BN * CH;
     const u32x4* Vs = Ks + BN * CH;
-    if (t + 1 < ntiles) {
+    const int kv0 = t * BN;
+    const bool more = t + 1 < ntiles;
+    // No per-wave skip of tiles wholly above the diagonal (a wave's last tile at most): a
+    // branch around the accumulators makes the compiler shuttle them through AGPRs.  Such a
+    // tile gives p = 0 everywhere (never the first tile, so the running max stays finite).
+    f32x16 sacc[2];
+    {
+      // S^T = K . Q^T: all 16 K row operands in flight, then two independent MFMA chains
+      bf16x8 a0[NDS], a1[NDS];
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) {
+        a0[s] = row_frag(Ks, r, 2 * s + h);
+        a1[s] = row_frag(Ks, 32 + r, 2 * s + h);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      sacc[0] = zero16();
+      sacc[1] = zero16();
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) {
+        sacc[0] = mfma(a0[s], qf[s], sacc[0]);
+        sacc[1] = mfma(a1[s], qf[s], sacc[1]);
+      }
+    }
+    if (more) {  // next tile's global loads fly under the softmax and P.V
       ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
       vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
     }
-    const int kv0 = t * BN;
-    if (!causal || kv0 <= q0w + 31) {
-      f32x16 sacc[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        sacc[kt] = zero16();
-#pragma unroll
-        for (int s = 0; s < NDS; ++s) sacc[kt] = mfma(row_frag(Ks, kt * 32 + r, 2 * s + h), qf[s], sacc[kt]);
-      }
+    {
       if (causal && kv0 + BN - 1 > q0w) {
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
@@ -239,16 +264,22 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restric
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 pb[2], vv[2][NDT];
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pb = acc_frag(sacc[kt], s2);
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt)
-            oacc[dt] = mfma(tr_frag(Vs, kt * 32 + 16 * s2, dt * 32, lane), pb, oacc[dt]);
-        }
+          for (int dt = 0; dt < NDT; ++dt) vv[s2][dt] = tr_frag(Vs, kt * 32 + 16 * s2, dt * 32, lane);
+        pb[0] = acc_frag(sacc[kt], 0);
+        pb[1] = acc_frag(sacc[kt], 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma(vv[s2][dt], pb[s2], oacc[dt]);
+      }
     }
-    if (t + 1 < ntiles) {
+    if (more) {
       u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
       ks.store(nk, tid);
       vs.store(nk + BN * CH, tid);
@@ -265,12 +296,12 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restric
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
-    float* __restrict__ delta, bf16_t* __restrict__ dq, int S, int Hq, int Hkv, float c, float scale, int causal) {
+    float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
   __shared__ u32x4 smem[4 * BN * CH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-  const int nqb = S / BM;
-  const int qblk = causal ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int bh = blockIdx.y, b = bh / Hq, hq = bh % Hq, hk = hq / (Hq / Hkv);
+  int qblk, b, hq, hk;
+  block_coords(S, B, Hq, Hkv, causal, qblk, b, hq, hk);
   const int q0w = qblk * BM + w * 32, qme = q0w + r;
   const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
 
@@ -317,20 +348,30 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
     const int cur = t & 1;
     const u32x4* Ks = smem + cur * 2 * BN * CH;
     const u32x4* Vs = Ks + BN * CH;
-    if (t + 1 < ntiles) {
-      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
-      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
-    }
     const int kv0 = t * BN;
-    if (!causal || kv0 <= q0w + 31) {
+    const bool more = t + 1 < ntiles;
+    {  // no per-wave skip of masked tiles (see the forward)
       const bool diag = causal && kv0 + BN - 1 > q0w;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f32x16 sa = zero16(), pa = zero16();
+        {
+          bf16x8 ka[NDS], va[NDS];
 #pragma unroll
-        for (int s = 0; s < NDS; ++s) {
-          sa = mfma(row_frag(Ks, kt * 32 + r, 2 * s + h), qf[s], sa);
-          pa = mfma(row_frag(Vs, kt * 32 + r, 2 * s + h), df[s], pa);
+          for (int s = 0; s < NDS; ++s) {
+            ka[s] = row_frag(Ks, kt * 32 + r, 2 * s + h);
+            va[s] = row_frag(Vs, kt * 32 + r, 2 * s + h);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 0; s < NDS; ++s) {
+            sa = mfma(ka[s], qf[s], sa);
+            pa = mfma(va[s], df[s], pa);
+          }
+        }
+        if (kt == 0 && more) {  // next tile's global loads fly under the rest of this one
+          ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+          vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -338,15 +379,21 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
           if (diag && kv0 + kt * 32 + acc_row(i, h) > qme) p = 0.f;
           sa[i] = p * (pa[i] - dl);
         }
+        bf16x8 db[2], kk[2][NDT];
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 db = acc_frag(sa, s2);
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane), db, dacc[dt]);
-        }
+          for (int dt = 0; dt < NDT; ++dt) kk[s2][dt] = tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane);
+        db[0] = acc_frag(sa, 0);
+        db[1] = acc_frag(sa, 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(kk[s2][dt], db[s2], dacc[dt]);
       }
     }
-    if (t + 1 < ntiles) {
+    if (more) {
       u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
       ks.store(nk, tid);
       vs.store(nk + BN * CH, tid);
@@ -360,12 +407,15 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
-    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int S, int Hq, int Hkv, float c, float scale, int causal) {
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
   __shared__ u32x4 smem[4 * QT * CH];  // Q0 dO0 Q1 dO1 (32 KB); reused for the dK/dV epilogue
   __shared__ float4 stat[2][2][QT / 4];  // [buf][lse2 | delta][32 rows]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-  const int kblk = blockIdx.x;  // causal: kblk 0 (the most query tiles) launches first
-  const int bh = blockIdx.y, b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
+  // key block slowest in the launch order: under the causal mask kblk 0 (the most query tiles)
+  // is dispatched first, so the light blocks fill in behind the heavy ones
+  const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
+  const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
   const int k0w = kblk * BK + w * 32, kme = k0w + r;
   const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
 
@@ -418,15 +468,25 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
     const int cur = t & 1;
     const u32x4* Qs = smem + cur * 2 * QT * CH;
     const u32x4* Ds = Qs + QT * CH;
-    if (t + 1 < ntiles) load(t + 1);
     const int q0 = (qt0 + t % nqt) * QT;
-    if (!causal || k0w <= q0 + QT - 1) {
-      f32x16 sa = zero16(), pa = zero16();
+    const bool more = t + 1 < ntiles;
+    f32x16 sa = zero16(), pa = zero16();
+    {  // no per-wave skip of masked tiles (see the forward)
+      bf16x8 qa[NDS], da[NDS];
 #pragma unroll
       for (int s = 0; s < NDS; ++s) {
-        sa = mfma(row_frag(Qs, r, 2 * s + h), kf[s], sa);
-        pa = mfma(row_frag(Ds, r, 2 * s + h), vf[s], pa);
+        qa[s] = row_frag(Qs, r, 2 * s + h);
+        da[s] = row_frag(Ds, r, 2 * s + h);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) {
+        sa = mfma(qa[s], kf[s], sa);
+        pa = mfma(da[s], vf[s], pa);
+      }
+    }
+    if (more) load(t + 1);
+    {
       const bool diag = causal && k0w + 31 > q0;
       // rows (queries) of register group g: 8g + 4h + 0..3 -> one float4 of lse2 / delta
 #pragma unroll
@@ -443,17 +503,29 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
           pa[i] = p * (pa[i] - Dv[e]);
         }
       }
+      bf16x8 pb[2], db[2], td[2][NDT], tq[2][NDT];
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pb = acc_frag(sa, s2), db = acc_frag(pa, s2);
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-          dva[dt] = mfma(tr_frag(Ds, 16 * s2, dt * 32, lane), pb, dva[dt]);
-          dka[dt] = mfma(tr_frag(Qs, 16 * s2, dt * 32, lane), db, dka[dt]);
+          td[s2][dt] = tr_frag(Ds, 16 * s2, dt * 32, lane);
+          tq[s2][dt] = tr_frag(Qs, 16 * s2, dt * 32, lane);
         }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        pb[s2] = acc_frag(sa, s2);
+        db[s2] = acc_frag(pa, s2);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          dva[dt] = mfma(td[s2][dt], pb[s2], dva[dt]);
+          dka[dt] = mfma(tq[s2][dt], db[s2], dka[dt]);
+        }
     }
-    if (t + 1 < ntiles) store(cur ^ 1);
+    if (more) store(cur ^ 1);
     __syncthreads();
   }
   const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
@@ -467,7 +539,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
   if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Dh != D) return -1;
   if (S % BM || S % BK || Hq % Hkv) return -1;
-  if ((long)B * Hq > 65535 || (long)B * Hkv > 65535) return -1;
+  if ((long)(S / BM) * B * Hq > (1L << 30)) return -1;
   return 0;
 }
 
@@ -482,8 +554,8 @@ int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   if (check_shapes(B, S, Hq, Hkv, Dh)) return -1;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(lse2)) return -2;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(S / BM, B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, S, Hq, Hkv, c, causal);
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c, causal);
   return (int)hipGetLastError();
 }
 
@@ -496,12 +568,12 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   for (const void* p : ps)
     if (!aligned16(p)) return -2;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / BM, B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout, lse2, delta,
-                     (bf16_t*)dq, S, Hq, Hkv, c, scale, causal);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / BK, B * Hkv), dim3(NT), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout,
+                     lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
-                     (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, S, Hq, Hkv, c, scale, causal);
+                     (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
   return (int)hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ def main():
     p.add_argument("--hkv", type=int, default=8)
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--causal", type=int, default=1)
+    p.add_argument("--impl", default="hip,sdpa")
     p.add_argument("--json-out", default=None)
     a = p.parse_args()
     from pytorch_operator_amd.ops.attention import flash_attention, sdpa_bshd
@@ -51,6 +52,8 @@ def main():
     fwd_flop = 4 * B * Hq * S * S * D * frac
     res = {"shape": {"B": B, "S": S, "Hq": Hq, "Hkv": Hkv, "D": D, "causal": bool(a.causal)}}
     for name, fn in (("hip", flash_attention), ("sdpa", sdpa_bshd)):
+        if name not in a.impl.split(","):
+            continue
         with torch.no_grad():
             fn(q, k, v, bool(a.causal))
             t_f = timed(lambda: fn(q, k, v, bool(a.causal)), a.reps)
@@ -66,7 +69,8 @@ def main():
                      "bwd_tflops": round(2.5 * fwd_flop / t_b / 1e6, 1)}
         print(name, res[name], flush=True)
         q.grad = k.grad = v.grad = None
-    res["speedup_fwd_bwd"] = round(res["sdpa"]["fwd_bwd_us"] / res["hip"]["fwd_bwd_us"], 2)
+    if "hip" in res and "sdpa" in res:
+        res["speedup_fwd_bwd"] = round(res["sdpa"]["fwd_bwd_us"] / res["hip"]["fwd_bwd_us"], 2)
     print(json.dumps(res))
     if a.json_out:
         Path(a.json_out).write_text(json.dumps(res, indent=1) + "\n")
