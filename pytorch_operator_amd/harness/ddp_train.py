@@ -53,6 +53,8 @@ def parse_args(argv=None):
                    help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
     p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
                    help="ResNet SGD implementation (fused: one multi-tensor kernel per step)")
+    p.add_argument("--attn", choices=["auto", "sdpa"], default="auto",
+                   help="Llama attention: hand-written HIP flash attention where it applies, or SDPA")
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--json-out", default=None)
@@ -73,7 +75,8 @@ def build(args, device):
             kw = {"fused": True} if args.sgd == "fused" else {"foreach": True}
         opt = torch.optim.SGD(model.parameters(), lr=args.lr or 0.1, momentum=0.9, weight_decay=1e-4, **kw)
         return model, opt
-    from ..models.llama import CONFIGS, Llama
+    from ..models.llama import CONFIGS, Attention, Llama
+    Attention.impl = args.attn
     with torch.device(device):
         model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
     if use_master_weights(args, device):
@@ -235,6 +238,8 @@ def main(argv=None) -> int:
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev)}
+    if is_llama:
+        res.update(attn=args.attn)
     if not is_llama:
         res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn)
     digest = param_digest(model.module if hasattr(model, "module") else model, opt)
