@@ -11,6 +11,11 @@
 //            of a row = (row / H) % S, tables cos/sin [S, D/2] fp32.  sign = +1 forward,
 //            -1 backward (the adjoint of a rotation is the rotation by -theta).
 //   swiglu:  y = silu(a) * b ; backward da = dy*b*sig(a)*(1 + a*(1-sig(a))), db = dy*silu(a)
+//   xent:    cross-entropy over the vocabulary straight from the lm-head's logits (bf16 or
+//            fp32, [rows, V]): forward = one read of each row (per-lane online max / sum-exp,
+//            one block reduction) -> per-row lse and loss; backward = one read + one write,
+//            d(logits) = (exp(x - lse) - onehot(t)) * scale, written in place over the logits
+//            (no fp32 copy of the 128k-wide logits, no separate softmax / NLL kernels).
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -145,6 +150,83 @@ __global__ __launch_bounds__(kT) void swiglu_bwd_kernel(const T* __restrict__ dy
   }
 }
 
+// ---------------------------------------------------------------------------- xent
+// One workgroup per row (rows = tokens: thousands of workgroups), kX threads, 8 elements
+// (one 16-byte bf16 / two 16-byte fp32 loads) per lane per iteration.  V % 8 == 0.
+constexpr int kX = 512;
+
+template <typename T>
+__global__ __launch_bounds__(kX) void xent_fwd_kernel(const T* __restrict__ x, const long* __restrict__ tgt,
+                                                      float* __restrict__ lse_out, float* __restrict__ loss_out,
+                                                      int V, long ignore_index) {
+  __shared__ float sm[kX / 64], ss[kX / 64];
+  const long row = blockIdx.x;
+  const T* xr = x + row * (long)V;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float m = -INFINITY, s = 0.f;
+  const int n8 = V / 8;
+  for (int g = tid; g < n8; g += kX) {
+    const V8 v = Vec<T>::load(xr + (long)g * 8);
+    float mx = v.v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) mx = fmaxf(mx, v.v[i]);
+    const float mn = fmaxf(m, mx);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += __expf(v.v[i] - mn);
+    s = s * __expf(m - mn) + acc;  // m = -inf on the first group: exp(-inf) = 0
+    m = mn;
+  }
+  // wave, then block: combine (m, s) pairs
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
+    const float mn = fmaxf(m, mo);
+    s = (mn == -INFINITY) ? 0.f : s * __expf(m - mn) + so * __expf(mo - mn);
+    m = mn;
+  }
+  if (lane == 0) { sm[wv] = m; ss[wv] = s; }
+  __syncthreads();
+  if (tid == 0) {
+    float M = sm[0], Ssum = ss[0];
+#pragma unroll
+    for (int q = 1; q < kX / 64; ++q) {
+      const float mn = fmaxf(M, sm[q]);
+      Ssum = Ssum * __expf(M - mn) + ss[q] * __expf(sm[q] - mn);
+      M = mn;
+    }
+    const float lse = M + __logf(Ssum);
+    const long t = tgt[row];
+    lse_out[row] = lse;
+    loss_out[row] = (t == ignore_index || t < 0 || t >= V) ? 0.f : lse - Vec<T>::load1(xr + t);
+  }
+}
+
+// d(logits)[row] = (exp(x - lse) - onehot(t)) * scale[0]; rows whose target is ignored get 0.
+// dx may alias x (each element is read, then written, by the same lane).
+template <typename T>
+__global__ __launch_bounds__(kX) void xent_bwd_kernel(const T* x, const long* __restrict__ tgt,
+                                                      const float* __restrict__ lse_in,
+                                                      const float* __restrict__ scale, T* dx, int V,
+                                                      long ignore_index) {
+  const long row = blockIdx.x;
+  const T* xr = x + row * (long)V;
+  T* dr = dx + row * (long)V;
+  const long t = tgt[row];
+  const bool ign = t == ignore_index || t < 0 || t >= V;
+  const float lse = lse_in[row], sc = ign ? 0.f : scale[0];
+  const int n8 = V / 8;
+  for (int g = threadIdx.x; g < n8; g += kX) {
+    V8 v = Vec<T>::load(xr + (long)g * 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float p = __expf(v.v[i] - lse);
+      v.v[i] = (p - ((long)(g * 8 + i) == t ? 1.f : 0.f)) * sc;
+    }
+    Vec<T>::store(dr + (long)g * 8, v);
+  }
+}
+
 // Enough workgroups to fill 256 CUs several times over; grid-stride beyond that.
 unsigned grid_for(long work) {
   const long b = (work + kT - 1) / kT;
@@ -197,6 +279,33 @@ int pto_swiglu_bwd(const void* dy, const void* a, const void* b, void* da, void*
     hipLaunchKernelGGL(swiglu_bwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
                        (const uint16_t*)dy, (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)da,
                        (uint16_t*)db, n);
+  return (int)hipGetLastError();
+}
+
+// Cross-entropy over [rows, V] logits (dtype 0 = fp32, 1 = bf16), int64 targets.
+int pto_xent_fwd(const void* x, const long* tgt, float* lse, float* loss, long rows, int V, long ignore_index,
+                 int dtype, void* stream) {
+  if (rows <= 0 || rows > 0x7fffffffL || V <= 0 || V % 8 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(x)) return -2;
+  if (dtype == 0)
+    hipLaunchKernelGGL(xent_fwd_kernel<float>, dim3((unsigned)rows), dim3(kX), 0, (hipStream_t)stream,
+                       (const float*)x, tgt, lse, loss, V, ignore_index);
+  else
+    hipLaunchKernelGGL(xent_fwd_kernel<uint16_t>, dim3((unsigned)rows), dim3(kX), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, tgt, lse, loss, V, ignore_index);
+  return (int)hipGetLastError();
+}
+
+int pto_xent_bwd(const void* x, const long* tgt, const float* lse, const float* scale, void* dx, long rows, int V,
+                 long ignore_index, int dtype, void* stream) {
+  if (rows <= 0 || rows > 0x7fffffffL || V <= 0 || V % 8 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(x) || !aligned16(dx)) return -2;
+  if (dtype == 0)
+    hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3((unsigned)rows), dim3(kX), 0, (hipStream_t)stream,
+                       (const float*)x, tgt, lse, scale, (float*)dx, V, ignore_index);
+  else
+    hipLaunchKernelGGL(xent_bwd_kernel<uint16_t>, dim3((unsigned)rows), dim3(kX), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, tgt, lse, scale, (uint16_t*)dx, V, ignore_index);
   return (int)hipGetLastError();
 }
 

@@ -55,6 +55,13 @@ def parse_args(argv=None):
                    help="ResNet SGD implementation (fused: one multi-tensor kernel per step)")
     p.add_argument("--attn", choices=["auto", "sdpa"], default="auto",
                    help="Llama attention: hand-written HIP flash attention where it applies, or SDPA")
+    p.add_argument("--gemm-tuning", choices=["off", "use", "tune"], default="use",
+                   help="PyTorch TunableOp over hipBLASLt/rocBLAS for the model's GEMM shapes: 'use' "
+                        "replays the measured per-shape winners in --gemm-tuning-file (shapes not in "
+                        "it take the library default), 'tune' benchmarks every candidate solution "
+                        "during the first (untimed) step and writes the file, 'off' = library default")
+    p.add_argument("--gemm-tuning-file", default=None,
+                   help="TunableOp results CSV (default: pytorch_operator_amd/tuning/gemm_mi355x.csv)")
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--json-out", default=None)
@@ -90,6 +97,51 @@ def build(args, device):
     except (RuntimeError, TypeError):
         opt = torch.optim.AdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1)
     return model, opt
+
+
+def default_tuning_file() -> str:
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                        "gemm_mi355x.csv")
+
+
+def setup_gemm_tuning(args, device) -> dict:
+    """TunableOp: each GEMM shape the model issues is dispatched to the hipBLASLt/rocBLAS
+    solution measured fastest for it on MI355X (results CSV kept in-tree, validated by the
+    library against the ROCm / hipBLASLt / gfx versions it was tuned on).  'tune' runs the
+    search inside the first, untimed step; the timed steps only replay the winners."""
+    if device.type != "cuda" or args.gemm_tuning == "off":
+        return {"mode": "off"}
+    import torch.cuda.tunable as tunable
+    path = args.gemm_tuning_file or default_tuning_file()
+    if args.gemm_tuning == "use" and not os.path.exists(path):
+        return {"mode": "off", "missing": path}
+    tunable.enable(True)
+    tunable.tuning_enable(args.gemm_tuning == "tune")
+    if args.gemm_tuning == "tune":
+        tunable.set_max_tuning_duration(20)
+        tunable.set_max_tuning_iterations(30)
+        # the library appends the rank to the file name when it writes; keep ours explicit
+        tunable.set_filename(path + ".tuning", False)
+    elif not tunable.read_file(path):
+        # validators differ (another ROCm / hipBLASLt / torch build): library defaults
+        tunable.enable(False)
+        print(f"warning: TunableOp rejected {path}; GEMMs use the library default", file=sys.stderr)
+        return {"mode": "off", "rejected": path}
+    return {"mode": args.gemm_tuning, "file": os.path.relpath(path, os.getcwd())}
+
+
+def write_tuning_file(path: str) -> int:
+    """Write TunableOp's in-memory results (validators first, then one line per tuned GEMM
+    shape) in the CSV format ``read_file`` accepts; returns the number of shapes."""
+    import torch.cuda.tunable as tunable
+    rows = tunable.get_results()
+    with open(path, "w") as f:
+        vals = tunable.get_validators()
+        for name, value in (vals.items() if isinstance(vals, dict) else vals):
+            f.write(f"Validator,{name},{value}\n")
+        for op, params, sol, ms in rows:
+            f.write(f"{op},{params},{sol},{float(ms):.6f}\n")
+    return len(rows)
 
 
 def use_master_weights(args, device) -> bool:
@@ -161,6 +213,7 @@ def main(argv=None) -> int:
     is_llama = args.model.startswith("llama")
     B = args.batch_size or (1 if is_llama else (256 if use_gpu else 2))
     model, opt = build(args, dev)
+    tuning = setup_gemm_tuning(args, dev)
     n_params = sum(p.numel() for p in model.parameters())
     if world > 1:
         from torch.nn.parallel import DistributedDataParallel as DDP
@@ -238,8 +291,15 @@ def main(argv=None) -> int:
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev)}
+    res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
         res.update(attn=args.attn)
+    if tuning.get("mode") == "tune" and rank == 0:
+        import torch.cuda.tunable as tunable
+        out = args.gemm_tuning_file or default_tuning_file()
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        write_tuning_file(out)
+        res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
         res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn)
     digest = param_digest(model.module if hasattr(model, "module") else model, opt)

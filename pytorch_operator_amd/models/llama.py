@@ -172,4 +172,5 @@ class Llama(nn.Module):
         logits = self.output(self.norm(h))
         if targets is None:
             return logits
-        return F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), targets.reshape(-1))
+        from ..ops.llm import cross_entropy
+        return cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))

@@ -97,3 +97,49 @@ def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if a.shape != b.shape or a.dtype != b.dtype or a.dtype not in _DT:
         raise ValueError("swiglu: a and b must share shape and dtype (fp32/bf16)")
     return _SwiGLU.apply(_aligned(a), _aligned(b))
+
+
+# ---------------------------------------------------------------------------- cross-entropy
+_IGNORE = -100
+
+
+def cross_entropy_reference(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    return F.cross_entropy(logits.float(), targets, ignore_index=_IGNORE)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    """Mean cross-entropy of [N, V] logits: the forward reads the logits once (per-row lse,
+    per-row loss); the backward writes d(logits) over the saved logits in place (they are
+    an intermediate only this op consumes: the lm-head matmul's backward needs its input
+    and weight, not its output)."""
+
+    @staticmethod
+    def forward(ctx, logits, targets):
+        N, V = logits.shape
+        lse = torch.empty(N, device=logits.device, dtype=torch.float32)
+        loss = torch.empty(N, device=logits.device, dtype=torch.float32)
+        tgt = targets.contiguous().long()
+        _native.check(_native.load().pto_xent_fwd(logits.data_ptr(), tgt.data_ptr(), lse.data_ptr(),
+                                                  loss.data_ptr(), N, V, _IGNORE, _DT[logits.dtype],
+                                                  _stream(logits)), "xent_fwd")
+        count = (tgt != _IGNORE).sum().clamp_min(1).float()
+        ctx.save_for_backward(logits, tgt, lse, count)
+        return loss.sum() / count
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, tgt, lse, count = ctx.saved_tensors
+        N, V = logits.shape
+        scale = (g.float() / count).reshape(1).contiguous()
+        _native.check(_native.load().pto_xent_bwd(logits.data_ptr(), tgt.data_ptr(), lse.data_ptr(),
+                                                  scale.data_ptr(), logits.data_ptr(), N, V, _IGNORE,
+                                                  _DT[logits.dtype], _stream(logits)), "xent_bwd")
+        return logits, None
+
+
+def cross_entropy(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    """Mean token cross-entropy (ignore_index -100) over [N, V] logits in their own dtype
+    (fp32 math inside the kernels).  GPU: the fused HIP kernels; CPU: PyTorch."""
+    if logits.is_cuda and logits.dtype in _DT and logits.shape[-1] % 8 == 0 and logits.dim() == 2:
+        return _CrossEntropy.apply(_aligned(logits), targets)
+    return cross_entropy_reference(logits, targets)

@@ -117,6 +117,29 @@ def test_adamw_kernel_matches_reference(n, grad_dtype, param_dtype):
         torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,v", [(64, 256), (7, 1000), (5, 128256)])
+def test_cross_entropy_matches_reference(dtype, n, v):
+    """Fused HIP cross-entropy (loss + in-place d(logits)) vs fp32 F.cross_entropy, with
+    ignored (-100) targets and large-magnitude logits (the online max must rescale)."""
+    from pytorch_operator_amd.ops.llm import cross_entropy
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = (torch.randn(n, v, generator=g) * 8).to(dtype)
+    t = torch.randint(0, v, (n,), generator=g)
+    t[1] = -100
+    xg = x.cuda().requires_grad_(True)
+    y = xg * 1  # the op overwrites its (intermediate) input with the gradient
+    loss = cross_entropy(y, t.cuda())
+    (loss * 3).backward()
+    xr = x.float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(xr, t, ignore_index=-100)
+    (lr * 3).backward()
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-5)
+    torch.testing.assert_close(loss.cpu(), lr, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
+    assert xg.grad[1].abs().max().item() == 0
+
+
 def test_llama_tiny_master_weights_trains_on_gpu():
     res = _run("--model", "llama-tiny", "--seq-len", "128", "--batch-size", "4", "--steps", "30", "--warmup", "2",
                "--lr", "3e-3", "--master-weights", "on")
