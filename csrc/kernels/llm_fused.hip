@@ -11,6 +11,11 @@
 //            of a row = (row / H) % S, tables cos/sin [S, D/2] fp32.  sign = +1 forward,
 //            -1 backward (the adjoint of a rotation is the rotation by -theta).
 //   swiglu:  y = silu(a) * b ; backward da = dy*b*sig(a)*(1 + a*(1-sig(a))), db = dy*silu(a)
+//   rope_qkv: the fused QKV projection's output [rows = B*S, (Hq + 2 Hkv) * D] split into
+//            contiguous q [B,S,Hq,D], k [B,S,Hkv,D] (both rotated) and v (copied) in one pass;
+//            dir = 1 is its adjoint (dq, dk rotated by -theta, dv) -> packed d(qkv).
+//   swiglu_packed: the fused W1|W3 projection's output x [rows, 2F]: y = silu(x[:, :F]) * x[:, F:],
+//            backward writes the packed d(x) -- no gradient accumulation between two matmuls.
 //   xent:    cross-entropy over the vocabulary straight from the lm-head's logits (bf16 or
 //            fp32, [rows, V]): forward = one read of each row (per-lane online max / sum-exp,
 //            one block reduction) -> per-row lse and loss; backward = one read + one write,
@@ -99,8 +104,90 @@ __global__ __launch_bounds__(kT) void rope_kernel(const T* __restrict__ x, const
   }
 }
 
+// One thread per 8-element group of the packed row; heads [0, Hq) -> q, [Hq, Hq+Hkv) -> k,
+// the rest -> v.  dir 0: packed -> q/k/v (sign +1); dir 1: dq/dk/dv -> packed (sign -1).
+template <typename T>
+__global__ __launch_bounds__(kT) void rope_qkv_kernel(T* __restrict__ pk, T* __restrict__ q, T* __restrict__ k,
+                                                      T* __restrict__ v, const float* __restrict__ cosb,
+                                                      const float* __restrict__ sinb, long tokens, int S, int Hq,
+                                                      int Hkv, int D, int dir) {
+  const int W = (Hq + 2 * Hkv) * D, gpr = W / 8;
+  const long groups = tokens * gpr;
+  for (long gi = (long)blockIdx.x * kT + threadIdx.x; gi < groups; gi += (long)gridDim.x * kT) {
+    const long tok = gi / gpr;
+    const int c = (int)(gi - tok * gpr) * 8;
+    const int hh = c / D, d0 = c - hh * D;
+    T* other;
+    bool rot = true;
+    if (hh < Hq) {
+      other = q + (tok * Hq + hh) * D + d0;
+    } else if (hh < Hq + Hkv) {
+      other = k + (tok * Hkv + (hh - Hq)) * D + d0;
+    } else {
+      other = v + (tok * Hkv + (hh - Hq - Hkv)) * D + d0;
+      rot = false;
+    }
+    T* packed = pk + tok * W + c;
+    const V8 in = dir == 0 ? Vec<T>::load(packed) : Vec<T>::load(other);
+    V8 out = in;
+    if (rot) {
+      const int s = (int)(tok % S);
+      const float sign = dir == 0 ? 1.f : -1.f;
+      const float4 cv = *reinterpret_cast<const float4*>(cosb + (long)s * (D / 2) + d0 / 2);
+      const float4 sv = *reinterpret_cast<const float4*>(sinb + (long)s * (D / 2) + d0 / 2);
+      const float cs[4] = {cv.x, cv.y, cv.z, cv.w}, sn[4] = {sign * sv.x, sign * sv.y, sign * sv.z, sign * sv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x0 = in.v[2 * i], x1 = in.v[2 * i + 1];
+        out.v[2 * i] = x0 * cs[i] - x1 * sn[i];
+        out.v[2 * i + 1] = x0 * sn[i] + x1 * cs[i];
+      }
+    }
+    Vec<T>::store(dir == 0 ? other : packed, out);
+  }
+}
+
 // -------------------------------------------------------------------------------- swiglu
 __device__ __forceinline__ float sigmoid(float a) { return 1.f / (1.f + __expf(-a)); }
+
+// Packed form: x [rows, 2F] (a = x[:, :F], b = x[:, F:]), y / dy [rows, F].  F % 8 == 0.
+template <typename T>
+__global__ __launch_bounds__(kT) void swiglu_packed_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                               long rows, int F) {
+  const int gpr = F / 8;
+  const long groups = rows * gpr;
+  for (long g = (long)blockIdx.x * kT + threadIdx.x; g < groups; g += (long)gridDim.x * kT) {
+    const long r = g / gpr;
+    const int c = (int)(g - r * gpr) * 8;
+    const V8 av = Vec<T>::load(x + r * 2 * F + c), bv = Vec<T>::load(x + r * 2 * F + F + c);
+    V8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o.v[i] = av.v[i] * sigmoid(av.v[i]) * bv.v[i];
+    Vec<T>::store(y + r * F + c, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kT) void swiglu_packed_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               T* __restrict__ dx, long rows, int F) {
+  const int gpr = F / 8;
+  const long groups = rows * gpr;
+  for (long g = (long)blockIdx.x * kT + threadIdx.x; g < groups; g += (long)gridDim.x * kT) {
+    const long r = g / gpr;
+    const int c = (int)(g - r * gpr) * 8;
+    const V8 gv = Vec<T>::load(dy + r * F + c);
+    const V8 av = Vec<T>::load(x + r * 2 * F + c), bv = Vec<T>::load(x + r * 2 * F + F + c);
+    V8 oa, ob;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sg = sigmoid(av.v[i]);
+      oa.v[i] = gv.v[i] * bv.v[i] * sg * (1.f + av.v[i] * (1.f - sg));
+      ob.v[i] = gv.v[i] * av.v[i] * sg;
+    }
+    Vec<T>::store(dx + r * 2 * F + c, oa);
+    Vec<T>::store(dx + r * 2 * F + F + c, ob);
+  }
+}
 
 template <typename T>
 __global__ __launch_bounds__(kT) void swiglu_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b,
@@ -279,6 +366,52 @@ int pto_swiglu_bwd(const void* dy, const void* a, const void* b, void* da, void*
     hipLaunchKernelGGL(swiglu_bwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
                        (const uint16_t*)dy, (const uint16_t*)a, (const uint16_t*)b, (uint16_t*)da,
                        (uint16_t*)db, n);
+  return (int)hipGetLastError();
+}
+
+// packed [tokens, (Hq + 2 Hkv) * D] <-> q [tokens, Hq, D], k / v [tokens, Hkv, D]; dir 0 / 1.
+int pto_rope_qkv(void* packed, void* q, void* k, void* v, const float* cosb, const float* sinb, long tokens,
+                 int S, int Hq, int Hkv, int D, int dir, int dtype, void* stream) {
+  if (tokens <= 0 || S <= 0 || tokens % S || Hq <= 0 || Hkv <= 0 || D <= 0 || D % 8 || dir < 0 || dir > 1 ||
+      dtype < 0 || dtype > 1)
+    return -1;
+  if (!aligned16(packed) || !aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(cosb) ||
+      !aligned16(sinb))
+    return -2;
+  const long groups = tokens * ((Hq + 2 * Hkv) * D / 8);
+  if (dtype == 0)
+    hipLaunchKernelGGL(rope_qkv_kernel<float>, dim3(grid_for(groups)), dim3(kT), 0, (hipStream_t)stream,
+                       (float*)packed, (float*)q, (float*)k, (float*)v, cosb, sinb, tokens, S, Hq, Hkv, D, dir);
+  else
+    hipLaunchKernelGGL(rope_qkv_kernel<uint16_t>, dim3(grid_for(groups)), dim3(kT), 0, (hipStream_t)stream,
+                       (uint16_t*)packed, (uint16_t*)q, (uint16_t*)k, (uint16_t*)v, cosb, sinb, tokens, S, Hq,
+                       Hkv, D, dir);
+  return (int)hipGetLastError();
+}
+
+int pto_swiglu_packed_fwd(const void* x, void* y, long rows, int F, int dtype, void* stream) {
+  if (rows <= 0 || F <= 0 || F % 8 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(x) || !aligned16(y)) return -2;
+  const unsigned grid = grid_for(rows * (F / 8));
+  if (dtype == 0)
+    hipLaunchKernelGGL(swiglu_packed_fwd_kernel<float>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const float*)x, (float*)y, rows, F);
+  else
+    hipLaunchKernelGGL(swiglu_packed_fwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const uint16_t*)x, (uint16_t*)y, rows, F);
+  return (int)hipGetLastError();
+}
+
+int pto_swiglu_packed_bwd(const void* dy, const void* x, void* dx, long rows, int F, int dtype, void* stream) {
+  if (rows <= 0 || F <= 0 || F % 8 || dtype < 0 || dtype > 1) return -1;
+  if (!aligned16(dy) || !aligned16(x) || !aligned16(dx)) return -2;
+  const unsigned grid = grid_for(rows * (F / 8));
+  if (dtype == 0)
+    hipLaunchKernelGGL(swiglu_packed_bwd_kernel<float>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const float*)dy, (const float*)x, (float*)dx, rows, F);
+  else
+    hipLaunchKernelGGL(swiglu_packed_bwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
+                       (const uint16_t*)dy, (const uint16_t*)x, (uint16_t*)dx, rows, F);
   return (int)hipGetLastError();
 }
 

@@ -118,6 +118,8 @@ def setup_gemm_tuning(args, device) -> dict:
     tunable.enable(True)
     tunable.tuning_enable(args.gemm_tuning == "tune")
     if args.gemm_tuning == "tune":
+        if os.path.exists(path):
+            tunable.read_file(path)  # keep the shapes tuned before; search only new ones
         tunable.set_max_tuning_duration(20)
         tunable.set_max_tuning_iterations(30)
         # the library appends the rank to the file name when it writes; keep ours explicit

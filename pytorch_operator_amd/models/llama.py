@@ -96,17 +96,16 @@ class Attention(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.nh, self.nkv, self.hd = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
-        self.wq = nn.Linear(cfg.dim, self.nh * self.hd, bias=False)
-        self.wk = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
-        self.wv = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
+        # one fused Q|K|V projection: one GEMM (N = (Hq + 2 Hkv) * D) forward and one for
+        # the input gradient backward, instead of three plus a gradient sum
+        self.wqkv = nn.Linear(cfg.dim, (self.nh + 2 * self.nkv) * self.hd, bias=False)
         self.wo = nn.Linear(self.nh * self.hd, cfg.dim, bias=False)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
-        q = apply_rope(self.wq(x).view(B, S, self.nh, self.hd), cos, sin)
-        k = apply_rope(self.wk(x).view(B, S, self.nkv, self.hd), cos, sin)
-        v = self.wv(x).view(B, S, self.nkv, self.hd)
         from ..ops import attention as A
+        from ..ops.llm import rope_qkv
+        q, k, v = rope_qkv(self.wqkv(x), cos, sin, self.nh, self.nkv)
         if self.impl != "sdpa" and A.hip_supported(q, k, v):
             o = A.flash_attention(q, k, v, causal=True)  # [B, S, H, D], no transposes
         else:
@@ -117,13 +116,13 @@ class Attention(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.w1 = nn.Linear(cfg.dim, cfg.ffn_hidden, bias=False)
-        self.w3 = nn.Linear(cfg.dim, cfg.ffn_hidden, bias=False)
+        # fused W1|W3 (gate | up) projection: one GEMM each way, packed SwiGLU between
+        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_hidden, bias=False)
         self.w2 = nn.Linear(cfg.ffn_hidden, cfg.dim, bias=False)
 
     def forward(self, x):
-        from ..ops.llm import swiglu
-        return self.w2(swiglu(self.w1(x), self.w3(x)))
+        from ..ops.llm import swiglu_packed
+        return self.w2(swiglu_packed(self.w13(x)))
 
 
 class Block(nn.Module):

@@ -66,6 +66,64 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     return _Rope.apply(_aligned(x), _aligned(cos.float()), _aligned(sin.float()))
 
 
+# --------------------------------------------------------------------------------- rope_qkv
+def rope_qkv_reference(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int):
+    B, S, W = qkv.shape
+    D = W // (hq + 2 * hkv)
+    q, k, v = qkv.split([hq * D, hkv * D, hkv * D], dim=-1)
+    return (rope_reference(q.reshape(B, S, hq, D), cos, sin), rope_reference(k.reshape(B, S, hkv, D), cos, sin),
+            v.reshape(B, S, hkv, D))
+
+
+def _rope_qkv_launch(packed, q, k, v, cos, sin, S, hq, hkv, D, direction):
+    _native.check(_native.load().pto_rope_qkv(packed.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                                              cos.data_ptr(), sin.data_ptr(), packed.numel() // packed.shape[-1],
+                                              S, hq, hkv, D, direction, _DT[packed.dtype], _stream(packed)),
+                  "rope_qkv")
+
+
+class _RopeQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, hq, hkv):
+        B, S, W = qkv.shape
+        D = W // (hq + 2 * hkv)
+        q = qkv.new_empty(B, S, hq, D)
+        k = qkv.new_empty(B, S, hkv, D)
+        v = qkv.new_empty(B, S, hkv, D)
+        _rope_qkv_launch(qkv, q, k, v, cos, sin, S, hq, hkv, D, 0)
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (B, S, W, hq, hkv, D)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors
+        B, S, W, hq, hkv, D = ctx.dims
+        ref = next(t for t in (dq, dk, dv) if t is not None)
+        dq = _aligned(dq) if dq is not None else ref.new_zeros(B, S, hq, D)
+        dk = _aligned(dk) if dk is not None else ref.new_zeros(B, S, hkv, D)
+        dv = _aligned(dv) if dv is not None else ref.new_zeros(B, S, hkv, D)
+        dt = dq.dtype
+        dk, dv = dk.to(dt), dv.to(dt)
+        dqkv = dq.new_empty(B, S, W)
+        _rope_qkv_launch(dqkv, dq, dk, dv, cos, sin, S, hq, hkv, D, 1)
+        return dqkv, None, None, None, None
+
+
+def rope_qkv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, hq: int, hkv: int):
+    """Split the fused QKV projection's output [B, S, (hq + 2 hkv) * D] into contiguous
+    q [B, S, hq, D], k, v [B, S, hkv, D] with RoPE applied to q and k -- one HBM pass, and
+    one pass back to a packed d(qkv) in the backward (so the three input-gradient matmuls
+    become one and no gradient sum is needed)."""
+    if not qkv.is_cuda:
+        return rope_qkv_reference(qkv, cos, sin, hq, hkv)
+    B, S, W = qkv.shape
+    if qkv.dtype not in _DT or W % (hq + 2 * hkv) or (W // (hq + 2 * hkv)) % 8 or \
+            cos.shape != (S, W // (hq + 2 * hkv) // 2):
+        raise ValueError(f"rope_qkv: bad shapes qkv {tuple(qkv.shape)} cos {tuple(cos.shape)} hq {hq} hkv {hkv}")
+    return _RopeQKV.apply(_aligned(qkv), _aligned(cos.float()), _aligned(sin.float()), hq, hkv)
+
+
 # ---------------------------------------------------------------------------------- swiglu
 def swiglu_reference(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     return F.silu(a) * b
@@ -97,6 +155,42 @@ def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if a.shape != b.shape or a.dtype != b.dtype or a.dtype not in _DT:
         raise ValueError("swiglu: a and b must share shape and dtype (fp32/bf16)")
     return _SwiGLU.apply(_aligned(a), _aligned(b))
+
+
+def swiglu_packed_reference(x: torch.Tensor) -> torch.Tensor:
+    a, b = x.chunk(2, dim=-1)
+    return F.silu(a) * b
+
+
+class _SwiGLUPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        F2 = x.shape[-1]
+        y = x.new_empty(*x.shape[:-1], F2 // 2)
+        _native.check(_native.load().pto_swiglu_packed_fwd(x.data_ptr(), y.data_ptr(), x.numel() // F2, F2 // 2,
+                                                           _DT[x.dtype], _stream(x)), "swiglu_packed_fwd")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = _aligned(dy.to(x.dtype))
+        dx = torch.empty_like(x)
+        F2 = x.shape[-1]
+        _native.check(_native.load().pto_swiglu_packed_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(),
+                                                           x.numel() // F2, F2 // 2, _DT[x.dtype], _stream(x)),
+                      "swiglu_packed_bwd")
+        return dx
+
+
+def swiglu_packed(x: torch.Tensor) -> torch.Tensor:
+    """``silu(a) * b`` of the fused W1|W3 projection's output x = [a | b] (last dim 2F)."""
+    if not x.is_cuda:
+        return swiglu_packed_reference(x)
+    if x.dtype not in _DT or x.shape[-1] % 16:
+        raise ValueError(f"swiglu_packed: fp32/bf16 with last dim % 16 == 0, got {tuple(x.shape)} {x.dtype}")
+    return _SwiGLUPacked.apply(_aligned(x))
 
 
 # ---------------------------------------------------------------------------- cross-entropy

@@ -33,4 +33,4 @@ def test_llama_mini_attention_dispatch_on_cpu():
     tok = torch.randint(0, cfg.vocab_size, (1, 128))
     loss = m(tok, tok)
     loss.backward()
-    assert torch.isfinite(loss) and m.layers[0].attention.wq.weight.grad is not None
+    assert torch.isfinite(loss) and m.layers[0].attention.wqkv.weight.grad is not None

@@ -85,7 +85,7 @@ def test_flash_llama_block_matches_sdpa_path():
         with torch.autocast("cuda", dtype=torch.bfloat16):  # the worker's setting
             loss = m(tok, tok)
         loss.backward()
-        out[impl] = (float(loss), m.layers[0].attention.wq.weight.grad.float().clone())
+        out[impl] = (float(loss), m.layers[0].attention.wqkv.weight.grad.float().clone())
     assert abs(out["hip"][0] - out["sdpa"][0]) < 2e-2 * abs(out["sdpa"][0])
     assert _rel(out["hip"][1], out["sdpa"][1]) < 5e-2
 

@@ -118,6 +118,49 @@ def test_adamw_kernel_matches_reference(n, grad_dtype, param_dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 32, 8, 128), (1, 7, 4, 2, 16), (3, 33, 8, 8, 64)])
+def test_rope_qkv_matches_reference(dtype, shape):
+    """Fused QKV split + RoPE (and its packed backward) vs the fp32 split/rotate reference."""
+    from pytorch_operator_amd.models.llama import rope_tables
+    from pytorch_operator_amd.ops.llm import rope_qkv, rope_qkv_reference
+    B, S, hq, hkv, D = shape
+    W = (hq + 2 * hkv) * D
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(B, S, W, generator=g).to(dtype)
+    cos, sin = rope_tables(D, S, 500000.0)
+    dq, dk, dv = (torch.randn(B, S, h, D, generator=g).to(dtype) for h in (hq, hkv, hkv))
+    xg = x.cuda().requires_grad_(True)
+    outs = rope_qkv(xg, cos.cuda(), sin.cuda(), hq, hkv)
+    sum((o.float() * d.cuda().float()).sum() for o, d in zip(outs, (dq, dk, dv))).backward()
+    xr = x.float().requires_grad_(True)
+    refs = rope_qkv_reference(xr, cos, sin, hq, hkv)
+    sum((o * d.float()).sum() for o, d in zip(refs, (dq, dk, dv))).backward()
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    for o, r in zip(outs, refs):
+        assert o.is_contiguous()
+        torch.testing.assert_close(o.float().cpu(), r.detach(), **tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 2 * 14336), (7, 2 * 136), (3, 5, 32)])
+def test_swiglu_packed_matches_reference(dtype, shape):
+    from pytorch_operator_amd.ops.llm import swiglu_packed, swiglu_packed_reference
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.randn(*shape, generator=g).to(dtype)
+    dy = torch.randn(*shape[:-1], shape[-1] // 2, generator=g).to(dtype)
+    xg = x.cuda().requires_grad_(True)
+    y = swiglu_packed(xg)
+    (y.float() * dy.cuda().float()).sum().backward()
+    xr = x.float().requires_grad_(True)
+    yr = swiglu_packed_reference(xr)
+    (yr * dy.float()).sum().backward()
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), **tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,v", [(64, 256), (7, 1000), (5, 128256)])
 def test_cross_entropy_matches_reference(dtype, n, v):
     """Fused HIP cross-entropy (loss + in-place d(logits)) vs fp32 F.cross_entropy, with
