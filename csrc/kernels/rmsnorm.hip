@@ -153,10 +153,13 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_kernel(const TY* __restrict__ 
 }
 
 // ---- D % 4 == 0 fast path: lane owns column groups j = 4*(threadIdx.x + k*kT), k < P4.
+// Fused residual form (delta != nullptr): s = x + delta is written to s_out (the residual
+// stream, dtype TX) and normalised, so the block's residual add costs no separate pass.
 template <typename TX, typename TY, int P4>
 __global__ __launch_bounds__(kT) void rmsnorm_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w,
                                                              TY* __restrict__ y, float* __restrict__ rstd, int D,
-                                                             float eps) {
+                                                             float eps, const TY* __restrict__ delta,
+                                                             TX* __restrict__ s_out) {
   __shared__ float sh[kT / 64];
   const long row = blockIdx.x;
   F4 v[P4];
@@ -165,6 +168,12 @@ __global__ __launch_bounds__(kT) void rmsnorm_fwd_vec_kernel(const TX* __restric
   for (int k = 0; k < P4; ++k) {
     const int j = 4 * (threadIdx.x + k * kT);
     v[k] = j < D ? ld4(x + row * D + j) : F4{{0.f, 0.f, 0.f, 0.f}};
+    if (delta != nullptr && j < D) {
+      const F4 dd = ld4(delta + row * D + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k].v[e] += dd.v[e];
+      st4(s_out + row * D + j, v[k]);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) ss += v[k].v[e] * v[k].v[e];
   }
@@ -183,12 +192,16 @@ __global__ __launch_bounds__(kT) void rmsnorm_fwd_vec_kernel(const TX* __restric
 
 // Backward, software-pipelined: the next row's x / dy loads are issued before this row's
 // block reduction, so HBM latency overlaps the two LDS barriers of block_sum.
+// Fused residual form (gres != nullptr): dx = gres + d(norm)/dx -- the residual stream's
+// gradient is summed here instead of by a separate add; with dbranch != nullptr the same
+// value is also written in the branch dtype TY (the gradient of the block's bf16 output).
 template <typename TX, typename TY, int P4>
 __global__ __launch_bounds__(kT) void rmsnorm_bwd_vec_kernel(const TY* __restrict__ dy, const TX* __restrict__ x,
                                                              const float* __restrict__ w,
                                                              const float* __restrict__ rstd, TX* __restrict__ dx,
                                                              float* __restrict__ dw_part, long rows, int D,
-                                                             int rows_per_block) {
+                                                             int rows_per_block, const TX* __restrict__ gres,
+                                                             TY* __restrict__ dbranch) {
   __shared__ float sh[kT / 64];
   F4 wv[P4], dwa[P4], xv[P4], gv[P4];
 #pragma unroll
@@ -229,6 +242,12 @@ __global__ __launch_bounds__(kT) void rmsnorm_bwd_vec_kernel(const TY* __restric
           o.v[e] = r * wv[k].v[e] * gv[k].v[e] - xv[k].v[e] * c;
           dwa[k].v[e] += gv[k].v[e] * xv[k].v[e] * r;
         }
+        if (gres != nullptr) {
+          const F4 gr = ld4(gres + row * D + j);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o.v[e] += gr.v[e];
+        }
+        if (dbranch != nullptr) st4(dbranch + row * D + j, o);
         st4(dx + row * D + j, o);
       }
     }
@@ -302,9 +321,9 @@ void fwd_launch(const void* x, const float* w, void* y, float* rstd, long rows, 
 
 template <typename TX, typename TY, int P4>
 void fwd_vec_launch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps,
-                    void* stream) {
+                    void* stream, const void* delta = nullptr, void* s_out = nullptr) {
   hipLaunchKernelGGL((rmsnorm_fwd_vec_kernel<TX, TY, P4>), dim3(rows), dim3(kT), 0, (hipStream_t)stream,
-                     (const TX*)x, w, (TY*)y, rstd, D, eps);
+                     (const TX*)x, w, (TY*)y, rstd, D, eps, (const TY*)delta, (TX*)s_out);
 }
 
 bool vec_ok(int D, std::initializer_list<const void*> ptrs) {
@@ -315,15 +334,17 @@ bool vec_ok(int D, std::initializer_list<const void*> ptrs) {
 }
 
 template <typename TX, typename TY>
-int fwd_dispatch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream) {
-  if (vec_ok(D, {x, w, y})) {
+int fwd_dispatch(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, void* stream,
+                 const void* delta = nullptr, void* s_out = nullptr) {
+  if (vec_ok(D, {x, w, y}) && (delta == nullptr || vec_ok(D, {delta, s_out}))) {
     const int p4 = (D + 4 * kT - 1) / (4 * kT);
-    if (p4 <= 1) fwd_vec_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream);
-    else if (p4 <= 2) fwd_vec_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream);
-    else if (p4 <= 4) fwd_vec_launch<TX, TY, 4>(x, w, y, rstd, rows, D, eps, stream);
-    else fwd_vec_launch<TX, TY, 8>(x, w, y, rstd, rows, D, eps, stream);
+    if (p4 <= 1) fwd_vec_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+    else if (p4 <= 2) fwd_vec_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+    else if (p4 <= 4) fwd_vec_launch<TX, TY, 4>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+    else fwd_vec_launch<TX, TY, 8>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
     return (int)hipGetLastError();
   }
+  if (delta != nullptr) return -3;  // the fused residual form needs the vector path
   const int per = (D + kT - 1) / kT;
   if (per <= 1) fwd_launch<TX, TY, 1>(x, w, y, rstd, rows, D, eps, stream);
   else if (per <= 2) fwd_launch<TX, TY, 2>(x, w, y, rstd, rows, D, eps, stream);
@@ -343,22 +364,28 @@ void bwd_launch(const void* dy, const void* x, const float* w, const float* rstd
 
 template <typename TX, typename TY, int P4>
 void bwd_vec_launch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
-                    long rows, int D, int rpb, long nb, void* stream) {
+                    long rows, int D, int rpb, long nb, void* stream, const void* gres, void* dbranch) {
   hipLaunchKernelGGL((rmsnorm_bwd_vec_kernel<TX, TY, P4>), dim3(nb), dim3(kT), 0, (hipStream_t)stream,
-                     (const TY*)dy, (const TX*)x, w, rstd, (TX*)dx, dw_part, rows, D, rpb);
+                     (const TY*)dy, (const TX*)x, w, rstd, (TX*)dx, dw_part, rows, D, rpb, (const TX*)gres,
+                     (TY*)dbranch);
 }
 
 template <typename TX, typename TY>
-void bwd_dispatch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
-                  long rows, int D, int rpb, long nb, void* stream) {
-  if (vec_ok(D, {dy, x, w, dx, dw_part})) {
+int bwd_dispatch(const void* dy, const void* x, const float* w, const float* rstd, void* dx, float* dw_part,
+                 long rows, int D, int rpb, long nb, void* stream, const void* gres = nullptr,
+                 void* dbranch = nullptr) {
+  if (vec_ok(D, {dy, x, w, dx, dw_part}) && (gres == nullptr || vec_ok(D, {gres})) &&
+      (dbranch == nullptr || vec_ok(D, {dbranch}))) {
     const int p4 = (D + 4 * kT - 1) / (4 * kT);
-    if (p4 <= 1) bwd_vec_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-    else if (p4 <= 2) bwd_vec_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-    else if (p4 <= 4) bwd_vec_launch<TX, TY, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-    else bwd_vec_launch<TX, TY, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
-    return;
+    if (p4 <= 1) bwd_vec_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream, gres, dbranch);
+    else if (p4 <= 2)
+      bwd_vec_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream, gres, dbranch);
+    else if (p4 <= 4)
+      bwd_vec_launch<TX, TY, 4>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream, gres, dbranch);
+    else bwd_vec_launch<TX, TY, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream, gres, dbranch);
+    return 0;
   }
+  if (gres != nullptr || dbranch != nullptr) return -3;
   const int per = (D + kT - 1) / kT;
   if (per <= 1) bwd_launch<TX, TY, 1>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
   else if (per <= 2) bwd_launch<TX, TY, 2>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
@@ -366,6 +393,7 @@ void bwd_dispatch(const void* dy, const void* x, const float* w, const float* rs
   else if (per <= 8) bwd_launch<TX, TY, 8>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
   else if (per <= 16) bwd_launch<TX, TY, 16>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
   else bwd_launch<TX, TY, 32>(dy, x, w, rstd, dx, dw_part, rows, D, rpb, nb, stream);
+  return 0;
 }
 
 // dtype pair code: 0 = (x fp32, y fp32), 1 = (bf16, bf16), 2 = (x fp32, y bf16)
@@ -374,6 +402,10 @@ bool valid_pair(int code) { return code >= 0 && code <= 2; }
 }  // namespace
 
 extern "C" {
+
+int pto_add_rmsnorm_bwd(const void* dy, const void* x, const float* w, const float* rstd, const void* gres,
+                        void* dx, void* dbranch, float* dw, float* dw_part, long rows, int D, int rows_per_block,
+                        int dtype, void* stream);
 
 int pto_rmsnorm_fwd(const void* x, const float* w, void* y, float* rstd, long rows, int D, float eps, int dtype,
                     void* stream) {
@@ -391,10 +423,39 @@ int pto_rmsnorm_bwd(const void* dy, const void* x, const float* w, const float* 
   if (D <= 0 || D > kT * kMaxPer || rows <= 0 || rows_per_block <= 0 || !valid_pair(dtype)) return -1;
   const long nb = (rows + rows_per_block - 1) / rows_per_block;
   if (nb > (1L << 30)) return -1;
-  if (dtype == 0) bwd_dispatch<float, float>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+  return pto_add_rmsnorm_bwd(dy, x, w, rstd, nullptr, dx, nullptr, dw, dw_part, rows, D, rows_per_block, dtype,
+                             stream);
+}
+
+// Residual-fused forms.  fwd: s = x + delta (written to s_out), y = rmsnorm(s).  bwd: x is s,
+// gres the residual stream's incoming gradient; dx = gres + d(norm), dbranch = the same in
+// the y dtype (nullable).  Vector path only (D % 4 == 0, 16-byte aligned): -3 otherwise.
+int pto_add_rmsnorm_fwd(const void* x, const void* delta, const float* w, void* y, void* s_out, float* rstd,
+                        long rows, int D, float eps, int dtype, void* stream) {
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || !valid_pair(dtype) || delta == nullptr || s_out == nullptr)
+    return -1;
+  if (dtype == 0) return fwd_dispatch<float, float>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+  if (dtype == 1)
+    return fwd_dispatch<__hip_bfloat16, __hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+  return fwd_dispatch<float, __hip_bfloat16>(x, w, y, rstd, rows, D, eps, stream, delta, s_out);
+}
+
+int pto_add_rmsnorm_bwd(const void* dy, const void* x, const float* w, const float* rstd, const void* gres,
+                        void* dx, void* dbranch, float* dw, float* dw_part, long rows, int D, int rows_per_block,
+                        int dtype, void* stream) {
+  if (D <= 0 || D > kT * kMaxPer || rows <= 0 || rows_per_block <= 0 || !valid_pair(dtype)) return -1;
+  const long nb = (rows + rows_per_block - 1) / rows_per_block;
+  if (nb > (1L << 30)) return -1;
+  int rc;
+  if (dtype == 0)
+    rc = bwd_dispatch<float, float>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream, gres, dbranch);
   else if (dtype == 1)
-    bwd_dispatch<__hip_bfloat16, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
-  else bwd_dispatch<float, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream);
+    rc = bwd_dispatch<__hip_bfloat16, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb,
+                                                      stream, gres, dbranch);
+  else
+    rc = bwd_dispatch<float, __hip_bfloat16>(dy, x, w, rstd, dx, dw_part, rows, D, rows_per_block, nb, stream, gres,
+                                             dbranch);
+  if (rc != 0) return rc;
   hipLaunchKernelGGL(colsum_kernel, dim3((D + kColsPerWg - 1) / kColsPerWg), dim3(kT), 0, (hipStream_t)stream,
                      dw_part, (int)nb, D, dw);
   return (int)hipGetLastError();

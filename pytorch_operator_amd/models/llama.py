@@ -89,6 +89,16 @@ class RMSNorm(nn.Module):
             out_dtype = torch.get_autocast_dtype("cuda")  # consumed by a bf16 matmul next
         return rms_norm(x, self.weight, self.eps, out_dtype)
 
+    def add_forward(self, x: torch.Tensor, delta: Optional[torch.Tensor]):
+        """(x + delta, norm(x + delta)) -- the residual add fused into this norm."""
+        if delta is None:
+            return x, self(x)
+        from ..ops.norm import add_rms_norm
+        out_dtype = None
+        if x.is_cuda and x.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):
+            out_dtype = torch.get_autocast_dtype("cuda")
+        return add_rms_norm(x, delta, self.weight, self.eps, out_dtype)
+
 
 class Attention(nn.Module):
     impl = "auto"  # "auto": HIP flash attention where it applies; "sdpa": library kernels
@@ -133,9 +143,13 @@ class Block(nn.Module):
         self.ffn_norm = RMSNorm(cfg.dim, cfg.norm_eps)
         self.feed_forward = FeedForward(cfg)
 
-    def forward(self, x, cos, sin):
-        x = x + self.attention(self.attention_norm(x), cos, sin)
-        return x + self.feed_forward(self.ffn_norm(x))
+    def forward(self, x, delta, cos, sin):
+        """x: residual stream entering the block minus the previous block's FFN output
+        ``delta`` (None for the first block): each residual add happens inside the next
+        RMSNorm.  Returns (residual stream before the FFN add, FFN output)."""
+        h, y = self.attention_norm.add_forward(x, delta)
+        h, y = self.ffn_norm.add_forward(h, self.attention(y, cos, sin))
+        return h, self.feed_forward(y)
 
 
 class Llama(nn.Module):
@@ -162,13 +176,13 @@ class Llama(nn.Module):
     def forward(self, tokens: torch.Tensor, targets: Optional[torch.Tensor] = None):
         B, S = tokens.shape
         cos, sin = rope_tables(self.cfg.head_dim, S, self.cfg.rope_theta, tokens.device)
-        h = self.tok_embeddings(tokens)
+        h, d = self.tok_embeddings(tokens), None
         for blk in self.layers:
             if self.checkpoint_layers and self.training:
-                h = torch.utils.checkpoint.checkpoint(blk, h, cos, sin, use_reentrant=False)
+                h, d = torch.utils.checkpoint.checkpoint(blk, h, d, cos, sin, use_reentrant=False)
             else:
-                h = blk(h, cos, sin)
-        logits = self.output(self.norm(h))
+                h, d = blk(h, d, cos, sin)
+        logits = self.output(self.norm.add_forward(h, d)[1])
         if targets is None:
             return logits
         from ..ops.llm import cross_entropy

@@ -124,6 +124,8 @@ _SIGNATURES = {
     # rmsnorm.hip
     "pto_rmsnorm_fwd": [_VP, _VP, _VP, _VP, _L, _I, _F, _I, _VP],
     "pto_rmsnorm_bwd": [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _L, _I, _I, _I, _VP],
+    "pto_add_rmsnorm_fwd": [_VP, _VP, _VP, _VP, _VP, _VP, _L, _I, _F, _I, _VP],
+    "pto_add_rmsnorm_bwd": [_VP] * 9 + [_L, _I, _I, _I, _VP],
     # llm_fused.hip
     "pto_rope": [_VP, _VP, _VP, _VP, _L, _I, _I, _I, _F, _I, _VP],
     "pto_swiglu_fwd": [_VP, _VP, _VP, _L, _I, _VP],

@@ -71,3 +71,64 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5, out_dtype=None
     if (x.dtype, out_dtype) not in _PAIR or w.dtype != torch.float32 or x.shape[-1] > 8192:
         raise ValueError("rms_norm: fp32/bf16 activations (y fp32/bf16), fp32 weight, D <= 8192")
     return _RMSNorm.apply(x, w, eps, out_dtype)
+
+
+# ------------------------------------------------------------------ residual-fused RMSNorm
+class _AddRMSNorm(torch.autograd.Function):
+    """(s, y) = (x + delta, rmsnorm(x + delta)): the transformer block's residual add folded
+    into the next norm (one pass instead of add + norm), and in the backward the residual
+    gradient sum folded into the norm's dx (which is also written in the branch dtype, the
+    gradient of ``delta``): no separate add or cast kernels around the norms."""
+
+    @staticmethod
+    def forward(ctx, x, delta, w, eps, out_dtype):
+        lib = _native.load()
+        D = x.shape[-1]
+        rows = x.numel() // D
+        s = torch.empty_like(x)
+        y = torch.empty(x.shape, device=x.device, dtype=out_dtype)
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+        pair = _PAIR[(x.dtype, out_dtype)]
+        _native.check(lib.pto_add_rmsnorm_fwd(x.data_ptr(), delta.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                              s.data_ptr(), rstd.data_ptr(), rows, D, float(eps), pair,
+                                              _stream(x)), "add_rmsnorm_fwd")
+        ctx.save_for_backward(s, w, rstd)
+        ctx.pair, ctx.out_dtype, ctx.delta_dtype = pair, out_dtype, delta.dtype
+        return s, y
+
+    @staticmethod
+    def backward(ctx, gs, gy):
+        lib = _native.load()
+        s, w, rstd = ctx.saved_tensors
+        D = s.shape[-1]
+        rows = s.numel() // D
+        gy = torch.zeros(s.shape, device=s.device, dtype=ctx.out_dtype) if gy is None else \
+            _aligned(gy.to(ctx.out_dtype))
+        gs = None if gs is None else _aligned(gs.to(s.dtype))
+        dx = torch.empty_like(s)
+        dbranch = torch.empty(s.shape, device=s.device, dtype=ctx.out_dtype)
+        dw = torch.empty(D, device=s.device, dtype=torch.float32)
+        parts = lib.pto_rmsnorm_bwd_parts(rows, _ROWS_PER_BLOCK)
+        part = torch.empty((parts, D), device=s.device, dtype=torch.float32)
+        _native.check(lib.pto_add_rmsnorm_bwd(gy.data_ptr(), s.data_ptr(), w.data_ptr(), rstd.data_ptr(),
+                                              gs.data_ptr() if gs is not None else None, dx.data_ptr(),
+                                              dbranch.data_ptr(), dw.data_ptr(), part.data_ptr(), rows, D,
+                                              _ROWS_PER_BLOCK, ctx.pair, _stream(s)), "add_rmsnorm_bwd")
+        return dx, dbranch, dw.to(w.dtype), None, None
+
+
+def _aligned(t: torch.Tensor) -> torch.Tensor:
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+def add_rms_norm(x: torch.Tensor, delta: torch.Tensor, w: torch.Tensor, eps: float = 1e-5, out_dtype=None):
+    """Returns ``(s, y)`` with ``s = x + delta`` (dtype of x: the residual stream) and
+    ``y = rms_norm(s)`` in ``out_dtype``.  Fused HIP kernels on a GPU when ``delta`` has the
+    output dtype and D % 4 == 0; otherwise the unfused ops (CPU, odd shapes)."""
+    out_dtype = out_dtype or x.dtype
+    if (x.is_cuda and (x.dtype, out_dtype) in _PAIR and delta.dtype == out_dtype and w.dtype == torch.float32
+            and x.shape == delta.shape and x.shape[-1] % 4 == 0 and x.shape[-1] <= 8192):
+        return _AddRMSNorm.apply(_aligned(x), _aligned(delta), w, eps, out_dtype)
+    s = x + delta
+    return s, rms_norm(s, w, eps, out_dtype)

@@ -117,6 +117,39 @@ def test_adamw_kernel_matches_reference(n, grad_dtype, param_dtype):
         torch.testing.assert_close(pg.cpu(), pc, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("xdt,ydt", [(torch.float32, torch.bfloat16), (torch.float32, torch.float32),
+                                     (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("shape", [(37, 4096), (2, 3, 64)])
+@pytest.mark.parametrize("with_gs", [True, False])
+def test_add_rms_norm_matches_reference(xdt, ydt, shape, with_gs):
+    """Residual-fused RMSNorm: s = x + delta, y = norm(s); backward dx = gs + d(norm) (also
+    written as d(delta) in the branch dtype) and dw, vs fp32 autograd of the unfused ops."""
+    from pytorch_operator_amd.ops.norm import add_rms_norm, rms_norm_reference
+    g = torch.Generator(device="cpu").manual_seed(8)
+    x = torch.randn(*shape, generator=g).to(xdt)
+    d = torch.randn(*shape, generator=g).to(ydt)
+    w = 1 + 0.1 * torch.randn(shape[-1], generator=g)
+    gy = torch.randn(*shape, generator=g).to(ydt)
+    gs = torch.randn(*shape, generator=g).to(xdt)
+    xg, dg, wg = (t.cuda().requires_grad_(True) for t in (x, d, w))
+    s, y = add_rms_norm(xg, dg, wg, 1e-5, ydt)
+    assert s.dtype == xdt and y.dtype == ydt
+    loss = (y.float() * gy.cuda().float()).sum() + ((s.float() * gs.cuda().float()).sum() if with_gs else 0)
+    loss.backward()
+    xr, dr, wr = (t.float().requires_grad_(True) for t in (x, d, w))
+    sr = xr + dr
+    yr = rms_norm_reference(sr, wr, 1e-5)
+    lr = (yr * gy.float()).sum() + ((sr * gs.float()).sum() if with_gs else 0)
+    lr.backward()
+    lo = xdt == torch.bfloat16 or ydt == torch.bfloat16
+    tol = dict(rtol=2e-2, atol=2e-2) if lo else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(s.float().cpu(), sr.detach(), **tol)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), **tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
+    torch.testing.assert_close(dg.grad.float().cpu(), dr.grad, **tol)
+    torch.testing.assert_close(wg.grad.cpu(), wr.grad, rtol=3e-2 if lo else 1e-3, atol=3e-1 if lo else 1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 64, 32, 8, 128), (1, 7, 4, 2, 16), (3, 33, 8, 8, 64)])
 def test_rope_qkv_matches_reference(dtype, shape):
