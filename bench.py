@@ -49,6 +49,10 @@ def parse_args(argv=None):
     p.add_argument("--batch-size", type=int, default=64)
     p.add_argument("--kernels", choices=["hip", "torch"], default="hip")
     p.add_argument("--mode", choices=["eager", "graph", "graph-comm"], default="graph")
+    p.add_argument("--launch", choices=["graph", "stream"], default="stream",
+                   help="whole-step execution: replay the hipGraph, or launch the captured one-step "
+                        "kernel list straight onto the stream from C++ (no per-replay graph-launch "
+                        "gap, no first-launch cost; profiles/r2_k20_timeline.json)")
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per hipGraph replay (world 1 only; 0 = auto)")
     p.add_argument("--dataset-size", type=int, default=60000)
@@ -168,13 +172,15 @@ def main(argv=None):
             from pytorch_operator_amd.parallel.autotune import choose_grad_sync
             tr.train_step()  # momentum initialisation + library load, outside any graph
             done_w = 1
-            runner, ar_path, tune = choose_grad_sync(tr, sync, xg, mode=args.mode, spg=spg, trial_steps=40)
+            runner, ar_path, tune = choose_grad_sync(tr, sync, xg, mode=args.mode, spg=spg, trial_steps=40,
+                                                     launch=args.launch)
             done_w += tune.pop("steps")
         elif xg is not None:
             tr.grad_sync, ar_path = xg, "xgmi"
-            runner = GraphedStep(tr, mode="graph" if args.mode != "eager" else "eager", steps_per_graph=spg)
+            runner = GraphedStep(tr, mode="graph" if args.mode != "eager" else "eager", steps_per_graph=spg,
+                                 launch=args.launch)
         else:
-            runner = GraphedStep(tr, mode=args.mode, steps_per_graph=spg)
+            runner = GraphedStep(tr, mode=args.mode, steps_per_graph=spg, launch=args.launch)
         prewarm(args.prewarm_ms, dev)
         runner.warm(max(0, args.warmup - done_w - runner.internal_steps))
 
@@ -182,7 +188,8 @@ def main(argv=None):
             runner.run(n)
         steps = args.steps - args.steps % runner.steps_per_graph
         xgmi_error = (lambda: xg.xar.error()) if xg is not None else (lambda: 0)
-        mode_desc = (f"{args.mode}(spg={runner.steps_per_graph},overlap={args.overlap},allreduce={ar_path},"
+        mode_desc = (f"{args.mode}(launch={runner.launch},spg={runner.steps_per_graph},overlap={args.overlap},"
+                     f"allreduce={ar_path},"
                      f"schedule={args.schedule})")
     else:
         from pytorch_operator_amd.models.mnist import Net

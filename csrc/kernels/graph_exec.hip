@@ -12,18 +12,71 @@
 //   pto_graph_upload(h, stream)     hipGraphUpload: device-side staging, no execution
 //   pto_graph_launch(h, stream, n)  n back-to-back hipGraphLaunch
 //   pto_graph_destroy(h)
+//   pto_graph_launch_stream(h, stream, n)   the captured kernels launched directly on
+//                                    `stream`, n times in dependency order (no graph launch)
+//
+// Why the stream form exists: on ROCm 7.2 each hipGraphLaunch costs the GPU ~8.6 us of
+// idle between the previous replay's last kernel and this replay's first (rocprofv3 trace
+// of bench.py --steps 20, profiles/r2_k20_timeline.json), and a graph's first launch ~0.75
+// us per node, while a plain dependent launch on a busy stream costs the same kernel
+// boundary as a node inside a graph.  With kernels of 5-12 us the host's ~3.5 us per
+// launch stays ahead of the GPU, so replaying the recorded launch list costs neither.
 //
 // `stream` must be a non-default stream (capture on the null stream is invalid).
 #include <hip/hip_runtime.h>
 
 #include <new>
+#include <vector>
 
 namespace {
 struct PtoGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   size_t nodes = 0;
+  // kernel nodes in dependency order (empty if the graph holds anything but kernels);
+  // kernelParams point into the nodes of `graph`, which lives as long as this handle
+  std::vector<hipKernelNodeParams> launches;
 };
+
+// Topological order of a captured graph's nodes; false if a node is not a kernel.
+bool kernel_order(hipGraph_t g, std::vector<hipKernelNodeParams>& out) {
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess || n == 0) return false;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) return false;
+  std::vector<size_t> indeg(n, 0);
+  std::vector<std::vector<size_t>> succ(n);
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) return false;
+    size_t nd = 0;
+    if (hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) != hipSuccess) return false;
+    std::vector<hipGraphNode_t> deps(nd);
+    if (nd && hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd) != hipSuccess) return false;
+    indeg[i] = nd;
+    for (hipGraphNode_t d : deps)
+      for (size_t j = 0; j < n; ++j)
+        if (nodes[j] == d) succ[j].push_back(i);
+  }
+  std::vector<size_t> ready;
+  for (size_t i = 0; i < n; ++i)
+    if (indeg[i] == 0) ready.push_back(i);
+  out.clear();
+  while (!ready.empty()) {
+    // lowest index first among the ready nodes: capture order for a single-stream chain
+    size_t k = 0;
+    for (size_t q = 1; q < ready.size(); ++q)
+      if (ready[q] < ready[k]) k = q;
+    const size_t i = ready[k];
+    ready.erase(ready.begin() + (long)k);
+    hipKernelNodeParams p{};
+    if (hipGraphKernelNodeGetParams(nodes[i], &p) != hipSuccess) return false;
+    out.push_back(p);
+    for (size_t j : succ[i])
+      if (--indeg[j] == 0) ready.push_back(j);
+  }
+  return out.size() == n;
+}
 }  // namespace
 
 extern "C" {
@@ -47,6 +100,7 @@ int pto_graph_end(void* stream, void** out) {
   }
   h->graph = g;
   (void)hipGraphGetNodes(g, nullptr, &h->nodes);
+  if (!kernel_order(g, h->launches)) h->launches.clear();
   e = hipGraphInstantiate(&h->exec, g, nullptr, nullptr, 0);
   if (e != hipSuccess) {
     (void)hipGraphDestroy(g);
@@ -70,6 +124,21 @@ int pto_graph_launch(void* handle, void* stream, int n) {
     const hipError_t e = hipGraphLaunch(h->exec, (hipStream_t)stream);
     if (e != hipSuccess) return (int)e;
   }
+  return 0;
+}
+
+// Launch the recorded kernels directly on `stream` (see the header): -2 if the graph holds
+// nodes other than kernels.
+int pto_graph_launch_stream(void* handle, void* stream, int n) {
+  auto* h = static_cast<PtoGraph*>(handle);
+  if (h == nullptr || n < 0) return -1;
+  if (h->launches.empty()) return -2;
+  for (int i = 0; i < n; ++i)
+    for (const hipKernelNodeParams& p : h->launches) {
+      const hipError_t e =
+          hipLaunchKernel(p.func, p.gridDim, p.blockDim, p.kernelParams, p.sharedMemBytes, (hipStream_t)stream);
+      if (e != hipSuccess) return (int)e;
+    }
   return 0;
 }
 

@@ -30,7 +30,8 @@ def _timed(runner: GraphedStep, steps: int, device) -> float:
 
 
 def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 10,
-                     trial_steps: int = 60, force: Optional[str] = None) -> Tuple[GraphedStep, str, dict]:
+                     trial_steps: int = 60, force: Optional[str] = None,
+                     launch: str = "graph") -> Tuple[GraphedStep, str, dict]:
     """Returns (runner, "xgmi" | "rccl", per-step times of both trials + ``steps``: the
     training steps taken here).  ``force`` overrides the measured decision (tests use it to
     cover both hand-overs).  ``spg``: whole steps per replay of the returned xGMI runner's
@@ -43,7 +44,7 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
     r_rccl = GraphedStep(tr, mode=mode, steps_per_graph=1 if mode == "graph" else spg)
     t_rccl = _timed(r_rccl, trial, tr.device)
     tr.grad_sync = xgmi_sync
-    r_xgmi = GraphedStep(tr, mode="graph", steps_per_graph=spg)
+    r_xgmi = GraphedStep(tr, mode="graph", steps_per_graph=spg, launch=launch)
     t_xgmi = _timed(r_xgmi, trial, tr.device)
     if xgmi_sync.xar.error():
         t_xgmi = float("inf")

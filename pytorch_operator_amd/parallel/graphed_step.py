@@ -74,6 +74,12 @@ class NativeGraph:
         _native.check(self._lib.pto_graph_launch(
             self._h, torch.cuda.current_stream(self.device).cuda_stream, int(n)), "hipGraphLaunch")
 
+    def replay_stream(self, n: int = 1) -> None:
+        """The captured kernels launched directly on the current stream, ``n`` times over
+        (same kernels and arguments as ``replay``; no per-replay graph-launch cost)."""
+        _native.check(self._lib.pto_graph_launch_stream(
+            self._h, torch.cuda.current_stream(self.device).cuda_stream, int(n)), "graph stream replay")
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.pto_graph_destroy(self._h)
@@ -91,9 +97,14 @@ class GraphedStep:
     timed graph); ``warm(n)`` takes any ``n`` (one-step graph)."""
 
     def __init__(self, trainer: FusedMnistTrainer, mode: str = "graph", steps_per_graph: int = 1,
-                 native: bool = True):
+                 native: bool = True, launch: str = "graph"):
+        """``launch`` (whole-step native graphs only): "graph" replays the hipGraph,
+        "stream" launches the one-step graph's recorded kernels directly on the stream
+        (``NativeGraph.replay_stream``) -- any step count, no graph-launch gaps."""
         if mode not in ("eager", "graph", "graph-comm"):
             raise ValueError(f"unknown mode {mode}")
+        if launch not in ("graph", "stream"):
+            raise ValueError(f"unknown launch {launch}")
         self.tr = trainer
         self.sync = trainer.grad_sync  # the gradient path these graphs were built for
         self.mode = mode
@@ -103,6 +114,7 @@ class GraphedStep:
         self._warm = None    # one whole step (warm-up of any length)
         self._split = False  # RCCL three-graph step
         self.internal_steps = 0  # untimed steps taken while preparing the graphs
+        self.launch = "graph"
         if mode == "eager":
             return
         tr = trainer
@@ -121,6 +133,9 @@ class GraphedStep:
             self.internal_steps += 1
             torch.cuda.current_stream(tr.device).wait_stream(s)
             torch.cuda.synchronize(tr.device)
+        if whole_step and native and launch == "stream" and mode == "graph":
+            self.launch = "stream"
+            self.steps_per_graph = 1
         if whole_step:
             def steps(n):
                 def fn():
@@ -173,6 +188,9 @@ class GraphedStep:
         elif self._split:
             self._split_steps(n_steps)
         else:
+            if self.launch == "stream":
+                self._graph.replay_stream(n_steps)
+                return
             full = n_steps // self.steps_per_graph
             if full:
                 self._graph.replay(full)
@@ -189,6 +207,9 @@ class GraphedStep:
             return
         if self._split:
             self._split_steps(n_steps)
+            return
+        if self.launch == "stream":
+            self._graph.replay_stream(n_steps)
             return
         if n_steps % self.steps_per_graph:
             raise ValueError("n_steps must be a multiple of steps_per_graph")

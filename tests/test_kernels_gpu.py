@@ -173,6 +173,36 @@ def test_graph_replay_matches_eager(lib):
     assert _rel(graphed.flat_params, eager.flat_params) < 1e-5
 
 
+def test_stream_launch_matches_graph_replay(lib):
+    """GraphedStep(launch="stream") -- the captured one-step kernel list launched straight
+    onto the stream from C++ -- is bit-identical to hipGraph replay and walks the cursor."""
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    from pytorch_operator_amd.parallel.graphed_step import GraphedStep
+    dev = torch.device("cuda")
+    n = 1280  # 20 batches: no epoch wrap within the 14 steps
+    x, y = _data(n, seed=43, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(1)).to(torch.int32)
+
+    def make():
+        cur = torch.zeros(1, dtype=torch.int32, device=dev)
+        src = K.BatchSource(x.to(dev), y.to(dev), perm=perm.to(dev), cursor=cur)
+        return FusedMnistTrainer(batch_size=64, source=src, seed=9)
+
+    a, b = make(), make()
+    ra = GraphedStep(a, mode="graph", steps_per_graph=5, launch="graph")
+    rb = GraphedStep(b, mode="graph", steps_per_graph=5, launch="stream")
+    assert ra.launch == "graph" and rb.launch == "stream" and rb.steps_per_graph == 1
+    ra.warm(3)
+    ra.run(10)
+    rb.warm(3)
+    rb.run(10)
+    torch.cuda.synchronize()
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 14
+    assert torch.equal(a.flat_params, b.flat_params)
+    assert torch.equal(a.flat_momentum, b.flat_momentum)
+
+
 def test_training_reduces_loss_on_learnable_synthetic_data(lib):
     from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
     from pytorch_operator_amd.models.mnist import FusedMnistTrainer
