@@ -61,6 +61,9 @@ def parse_args(argv=None):
     p.add_argument("--no-shard", dest="shard", action="store_false")
     p.add_argument("--max-steps", type=int, default=0, help="cap steps per epoch (0 = full epoch)")
     p.add_argument("--no-graph", action="store_true", help="HIP path: eager launches, no hipGraphs")
+    p.add_argument("--launch", choices=["graph", "stream"], default="stream",
+                   help="HIP path: replay log-interval hipGraphs, or launch the captured one-step kernel "
+                        "list from C++ onto the stream (no per-replay graph-launch gap)")
     p.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"], default="auto",
                    help="HIP path, world>1: xGMI peer-memory all-reduce fused with SGD (self-tested, "
                         "RCCL fallback) or RCCL bucket all-reduce")
@@ -340,7 +343,7 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
             # trajectory is exactly the eager one (a log block = one graph replay)
             saved = (tr.flat_params.clone(), tr.flat_momentum.clone())
             whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
-            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1)
+            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1, launch=args.launch)
             tr.flat_params.copy_(saved[0])
             tr.flat_momentum.copy_(saved[1])
             cursor.fill_(1)

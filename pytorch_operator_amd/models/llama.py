@@ -89,10 +89,15 @@ class RMSNorm(nn.Module):
             out_dtype = torch.get_autocast_dtype("cuda")  # consumed by a bf16 matmul next
         return rms_norm(x, self.weight, self.eps, out_dtype)
 
+    fuse_residual = True  # False: plain add + norm (A/B of the residual-fused kernels)
+
     def add_forward(self, x: torch.Tensor, delta: Optional[torch.Tensor]):
         """(x + delta, norm(x + delta)) -- the residual add fused into this norm."""
         if delta is None:
             return x, self(x)
+        if not self.fuse_residual:
+            s = x + delta
+            return s, self(s)
         from ..ops.norm import add_rms_norm
         out_dtype = None
         if x.is_cuda and x.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):

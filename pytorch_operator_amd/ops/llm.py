@@ -222,6 +222,10 @@ class _CrossEntropy(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("fused cross_entropy: the logits were overwritten by the first backward "
+                               "(retain_graph double backward is not supported)")
+        ctx.consumed = True
         logits, tgt, lse, count = ctx.saved_tensors
         N, V = logits.shape
         scale = (g.float() / count).reshape(1).contiguous()
