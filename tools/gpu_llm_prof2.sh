@@ -11,6 +11,11 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/p -o run --output-forma
   python3 -m pytorch_operator_amd.harness.ddp_train --model llama3-8b --seq-len 2048 --batch-size 4 --steps 1 --warmup 2 \
   > $O/prof.log 2>&1 || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
 grep '"metric"' $O/prof.log
+for r in fused plain fused plain; do
+timeout -k 10 400 python3 -m pytorch_operator_amd.harness.ddp_train --model llama3-8b --seq-len 2048 --batch-size 4 --steps 6 --warmup 3 --residual-norm $r \
+  > $O/llama_$r.log 2>&1 || { echo "llama $r failed"; tail -20 $O/llama_$r.log; exit 1; }
+echo "$r $(grep -o '"ms_per_step": [0-9.]*' $O/llama_$r.log)"
+done
 timeout -k 10 420 python3 -m pytorch_operator_amd.harness.ddp_train --model resnet50 --batch-size 256 --steps 20 --warmup 8 \
   > $O/resnet50.log 2>&1 || { echo "resnet failed"; tail -20 $O/resnet50.log; exit 1; }
 grep '"metric"' $O/resnet50.log
