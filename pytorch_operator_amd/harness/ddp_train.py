@@ -51,6 +51,8 @@ def parse_args(argv=None):
                    help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
     p.add_argument("--bn", choices=["hip", "library"], default="hip",
                    help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
+    p.add_argument("--conv1x1", choices=["gemm", "library"], default="gemm",
+                   help="ResNet: 1x1 convolutions as hipBLASLt GEMMs on the NHWC view, or MIOpen convs")
     p.add_argument("--sgd", choices=["fused", "foreach"], default="fused",
                    help="ResNet SGD implementation (fused: one multi-tensor kernel per step)")
     p.add_argument("--attn", choices=["auto", "sdpa"], default="auto",
@@ -73,8 +75,9 @@ def parse_args(argv=None):
 def build(args, device):
     import torch
     if args.model.startswith("resnet"):
-        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl
+        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl
         model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
+        set_conv1x1_impl(model, args.conv1x1)
         fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format
         model = model.to(device=device, memory_format=fmt)
         if device.type == "cuda":
@@ -306,7 +309,8 @@ def main(argv=None) -> int:
         write_tuning_file(out)
         res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
-        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn)
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
+                   conv1x1=args.conv1x1)
     digest = param_digest(model.module if hasattr(model, "module") else model, opt)
     print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest}), flush=True)
     if rank == 0:

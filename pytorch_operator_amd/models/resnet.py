@@ -16,8 +16,31 @@ from typing import List, Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from ..ops.batchnorm import BatchNormAct2d
+
+
+class Conv1x1(nn.Conv2d):
+    """1x1 convolution that, on channels-last activations, runs as ONE GEMM on hipBLASLt:
+    NHWC memory viewed as [N*H*W, Cin] times W^T [Cin, Cout] gives the NHWC output with no
+    layout copies (stride 2 first takes the strided subsample).  Its backward is the two
+    GEMMs of ``F.linear`` (dX = dY.W, dW = dY^T.X).  Same parameter, init and state dict as
+    ``nn.Conv2d``; ``impl = "library"`` (or a non-channels-last input) keeps MIOpen's conv."""
+
+    impl = "gemm"
+
+    def __init__(self, cin: int, cout: int, stride: int = 1):
+        super().__init__(cin, cout, 1, stride=stride, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.impl != "gemm" or x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last):
+            return super().forward(x)
+        if self.stride[0] != 1:
+            x = x[:, :, ::self.stride[0], ::self.stride[1]].contiguous(memory_format=torch.channels_last)
+        N, C, H, W = x.shape
+        y = F.linear(x.permute(0, 2, 3, 1).reshape(N * H * W, C), self.weight.view(self.out_channels, C))
+        return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
 class Bottleneck(nn.Module):
@@ -26,11 +49,11 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None):
         super().__init__()
         width = planes
-        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.conv1 = Conv1x1(inplanes, width)
         self.bn1 = BatchNormAct2d(width, relu=True)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormAct2d(width, relu=True)
-        self.conv3 = nn.Conv2d(width, planes * self.expansion, 1, bias=False)
+        self.conv3 = Conv1x1(width, planes * self.expansion)
         self.bn3 = BatchNormAct2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
         self.downsample = downsample
 
@@ -67,7 +90,7 @@ class ResNet(nn.Module):
     def _make(self, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
         down = None
         if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
-            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * Bottleneck.expansion, 1, stride=stride, bias=False),
+            down = nn.Sequential(Conv1x1(self.inplanes, planes * Bottleneck.expansion, stride=stride),
                                  BatchNormAct2d(planes * Bottleneck.expansion))
         layers = [Bottleneck(self.inplanes, planes, stride, down)]
         self.inplanes = planes * Bottleneck.expansion
@@ -86,6 +109,16 @@ def set_bn_impl(model: nn.Module, impl: str) -> nn.Module:
         raise ValueError(impl)
     for m in model.modules():
         if isinstance(m, BatchNormAct2d):
+            m.impl = impl
+    return model
+
+
+def set_conv1x1_impl(model: nn.Module, impl: str) -> nn.Module:
+    """``"gemm"``: 1x1 convolutions as hipBLASLt GEMMs on the NHWC view; ``"library"``: MIOpen."""
+    if impl not in ("gemm", "library"):
+        raise ValueError(impl)
+    for m in model.modules():
+        if isinstance(m, Conv1x1):
             m.impl = impl
     return model
 
