@@ -314,6 +314,40 @@ __global__ __launch_bounds__(kX) void xent_bwd_kernel(const T* x, const long* __
   }
 }
 
+// ------------------------------------------------------------------------------ transpose
+// out[c][r] = in[r][c] for a [rows, cols] 16-bit matrix (bf16 bits), rows % 64 == cols % 64 == 0.
+// One 64x64 tile per workgroup: 16-byte row loads into a padded LDS tile (row stride 66
+// halfwords: the column reads of the store phase spread over the banks), 16-byte row
+// stores of the transposed tile.  Used to give hipBLASLt K-contiguous operands (the "TN"
+// form it runs fastest) for the Llama linears' backward GEMMs.
+constexpr int kTT = 64;
+__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* __restrict__ in,
+                                                          uint16_t* __restrict__ out, long rows, long cols) {
+  __shared__ uint16_t t[kTT][kTT + 2];
+  const long r0 = (long)blockIdx.y * kTT, c0 = (long)blockIdx.x * kTT;
+  const int tid = threadIdx.x, rr = tid >> 3, cc = (tid & 7) * 8;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = rr + 32 * p;
+    const uint4 q = *reinterpret_cast<const uint4*>(in + (r0 + r) * cols + c0 + cc);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      t[r][cc + 2 * i] = (uint16_t)(w[i] & 0xffffu);
+      t[r][cc + 2 * i + 1] = (uint16_t)(w[i] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int oc = rr + 32 * p;  // output row = input column
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)t[cc + 2 * i][oc] | ((uint32_t)t[cc + 2 * i + 1][oc] << 16);
+    *reinterpret_cast<uint4*>(out + (c0 + oc) * rows + r0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // Enough workgroups to fill 256 CUs several times over; grid-stride beyond that.
 unsigned grid_for(long work) {
   const long b = (work + kT - 1) / kT;
@@ -412,6 +446,15 @@ int pto_swiglu_packed_bwd(const void* dy, const void* x, void* dx, long rows, in
   else
     hipLaunchKernelGGL(swiglu_packed_bwd_kernel<uint16_t>, dim3(grid), dim3(kT), 0, (hipStream_t)stream,
                        (const uint16_t*)dy, (const uint16_t*)x, (uint16_t*)dx, rows, F);
+  return (int)hipGetLastError();
+}
+
+// [rows, cols] 16-bit -> [cols, rows]; rows % 64 == cols % 64 == 0, 16-byte aligned.
+int pto_transpose16(const void* in, void* out, long rows, long cols, void* stream) {
+  if (rows <= 0 || cols <= 0 || rows % kTT || cols % kTT || rows / kTT > 65535 || cols / kTT > 0x7fffffffL) return -1;
+  if (!aligned16(in) || !aligned16(out)) return -2;
+  hipLaunchKernelGGL(transpose16_kernel, dim3((unsigned)(cols / kTT), (unsigned)(rows / kTT)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint16_t*)in, (uint16_t*)out, rows, cols);
   return (int)hipGetLastError();
 }
 

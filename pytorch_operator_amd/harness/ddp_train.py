@@ -61,6 +61,9 @@ def parse_args(argv=None):
                    help="Llama attention: hand-written HIP flash attention where it applies, or SDPA")
     p.add_argument("--residual-norm", choices=["fused", "plain"], default="fused",
                    help="Llama: residual adds fused into the next RMSNorm (fwd and bwd) or plain add + norm")
+    p.add_argument("--linear-bwd", choices=["tn", "autograd"], default="tn",
+                   help="Llama projections: backward GEMMs with K-contiguous (transposed-copy) operands, "
+                        "or autograd's dy.W / dy^T.x layouts")
     p.add_argument("--gemm-tuning", choices=["off", "use", "tune"], default="use",
                    help="PyTorch TunableOp over hipBLASLt/rocBLAS for the model's GEMM shapes: 'use' "
                         "replays the measured per-shape winners in --gemm-tuning-file (shapes not in "
@@ -89,8 +92,9 @@ def build(args, device):
             kw = {"fused": True} if args.sgd == "fused" else {"foreach": True}
         opt = torch.optim.SGD(model.parameters(), lr=args.lr or 0.1, momentum=0.9, weight_decay=1e-4, **kw)
         return model, opt
-    from ..models.llama import CONFIGS, Attention, Llama, RMSNorm
+    from ..models.llama import CONFIGS, Attention, Llama, RMSNorm, TNLinear
     Attention.impl = args.attn
+    TNLinear.impl = args.linear_bwd
     RMSNorm.fuse_residual = args.residual_norm == "fused"
     with torch.device(device):
         model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
@@ -303,7 +307,7 @@ def main(argv=None) -> int:
            "master_weights": use_master_weights(args, dev)}
     res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
-        res.update(attn=args.attn, residual_norm=args.residual_norm)
+        res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd)
     if tuning.get("mode") == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
         out = args.gemm_tuning_file or default_tuning_file()

@@ -105,6 +105,22 @@ class RMSNorm(nn.Module):
         return add_rms_norm(x, delta, self.weight, self.eps, out_dtype)
 
 
+class TNLinear(nn.Linear):
+    """Bias-free projection whose backward GEMMs take K-contiguous operands (``ops.llm.linear_tn``)
+    when ``impl == "tn"``; ``"autograd"`` is the plain ``nn.Linear`` backward (A/B)."""
+
+    impl = "tn"
+
+    def __init__(self, fin: int, fout: int):
+        super().__init__(fin, fout, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.impl == "tn" and x.is_cuda:
+            from ..ops.llm import linear_tn
+            return linear_tn(x, self.weight)
+        return super().forward(x)
+
+
 class Attention(nn.Module):
     impl = "auto"  # "auto": HIP flash attention where it applies; "sdpa": library kernels
 
@@ -113,8 +129,8 @@ class Attention(nn.Module):
         self.nh, self.nkv, self.hd = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
         # one fused Q|K|V projection: one GEMM (N = (Hq + 2 Hkv) * D) forward and one for
         # the input gradient backward, instead of three plus a gradient sum
-        self.wqkv = nn.Linear(cfg.dim, (self.nh + 2 * self.nkv) * self.hd, bias=False)
-        self.wo = nn.Linear(self.nh * self.hd, cfg.dim, bias=False)
+        self.wqkv = TNLinear(cfg.dim, (self.nh + 2 * self.nkv) * self.hd)
+        self.wo = TNLinear(self.nh * self.hd, cfg.dim)
 
     def forward(self, x, cos, sin):
         B, S, _ = x.shape
@@ -132,8 +148,8 @@ class FeedForward(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         # fused W1|W3 (gate | up) projection: one GEMM each way, packed SwiGLU between
-        self.w13 = nn.Linear(cfg.dim, 2 * cfg.ffn_hidden, bias=False)
-        self.w2 = nn.Linear(cfg.ffn_hidden, cfg.dim, bias=False)
+        self.w13 = TNLinear(cfg.dim, 2 * cfg.ffn_hidden)
+        self.w2 = TNLinear(cfg.ffn_hidden, cfg.dim)
 
     def forward(self, x):
         from ..ops.llm import swiglu_packed

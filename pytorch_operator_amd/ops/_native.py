@@ -133,6 +133,7 @@ _SIGNATURES = {
     "pto_rope_qkv": [_VP] * 6 + [_L, _I, _I, _I, _I, _I, _I, _VP],
     "pto_swiglu_packed_fwd": [_VP, _VP, _L, _I, _I, _VP],
     "pto_swiglu_packed_bwd": [_VP, _VP, _VP, _L, _I, _I, _VP],
+    "pto_transpose16": [_VP, _VP, _L, _L, _VP],
     "pto_xent_fwd": [_VP, _VP, _VP, _VP, _L, _I, _L, _I, _VP],
     "pto_xent_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _L, _I, _VP],
     # adamw.hip

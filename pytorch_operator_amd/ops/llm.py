@@ -241,3 +241,55 @@ def cross_entropy(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
     if logits.is_cuda and logits.dtype in _DT and logits.shape[-1] % 8 == 0 and logits.dim() == 2:
         return _CrossEntropy.apply(_aligned(logits), targets)
     return cross_entropy_reference(logits, targets)
+
+
+# ---------------------------------------------------------------------------- TN linear
+def transpose2d(x: torch.Tensor) -> torch.Tensor:
+    """Contiguous transpose of a 2-D bf16 matrix (HIP LDS-tiled kernel when both dims are
+    multiples of 64, PyTorch's copy otherwise)."""
+    R, C = x.shape
+    if not x.is_cuda or x.dtype != torch.bfloat16 or R % 64 or C % 64 or R // 64 > 65535:
+        return x.t().contiguous()
+    x = _aligned(x)
+    out = torch.empty((C, R), device=x.device, dtype=x.dtype)
+    _native.check(_native.load().pto_transpose16(x.data_ptr(), out.data_ptr(), R, C, _stream(x)), "transpose16")
+    return out
+
+
+class _LinearTN(torch.autograd.Function):
+    """y = x.W^T whose backward GEMMs are issued with both operands K-contiguous -- the
+    layout hipBLASLt runs fastest on MI355X (tools/gemm_layout_probe.py) -- instead of
+    autograd's dy.W (W K-strided) and dy^T.x (both K-strided): dX = dy.(W^T)^T and
+    dW = (dy^T).(x^T)^T, with the transposed copies made by one LDS-tiled pass each."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.save_for_backward(x2, w)
+        ctx.xshape = x.shape
+        return F.linear(x2, w).view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = _aligned(dy.reshape(-1, w.shape[0]).to(x2.dtype))
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = F.linear(dy2, transpose2d(w)).view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = F.linear(transpose2d(dy2), transpose2d(x2))
+        return dx, dw
+
+
+def linear_tn(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``F.linear(x, w)`` (no bias) with K-contiguous backward GEMMs on a GPU; under bf16
+    autocast both operands are taken in bf16 (as autocast's linear would)."""
+    if not x.is_cuda:
+        return F.linear(x, w)
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast(device_type="cuda", enabled=False):
+            return _LinearTN.apply(x.to(dt), w.to(dt))
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return F.linear(x, w)
+    return _LinearTN.apply(x, w)

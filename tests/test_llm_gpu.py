@@ -216,6 +216,35 @@ def test_cross_entropy_matches_reference(dtype, n, v):
     assert xg.grad[1].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("shape", [(64, 128), (8192 // 8, 28672 // 8), (192, 64)])
+def test_transpose2d_bf16(shape):
+    from pytorch_operator_amd.ops.llm import transpose2d
+    x = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+    assert torch.equal(transpose2d(x), x.t().contiguous())
+
+
+@pytest.mark.parametrize("dims", [(2, 64, 128, 192), (1, 128, 256, 64), (3, 5, 24, 40)])
+def test_linear_tn_matches_reference(dims):
+    """TN-backward linear (transposed operand copies) vs fp32 autograd of x.W^T, bf16 in/out;
+    the last shape is not a multiple of 64 (PyTorch transpose fallback)."""
+    from pytorch_operator_amd.ops.llm import linear_tn
+    B, S, fin, fout = dims
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.randn(B, S, fin, generator=g).to(torch.bfloat16)
+    w = (torch.randn(fout, fin, generator=g) * 0.05).to(torch.bfloat16)
+    dy = torch.randn(B, S, fout, generator=g).to(torch.bfloat16)
+    xg, wg = x.cuda().requires_grad_(True), w.cuda().requires_grad_(True)
+    y = linear_tn(xg, wg)
+    y.backward(dy.cuda())
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr, wr)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(wg.grad.float().cpu(), wr.grad, rtol=2e-2, atol=1e-1)
+    assert xg.grad.dtype == wg.grad.dtype == torch.bfloat16
+
+
 def test_llama_tiny_master_weights_trains_on_gpu():
     res = _run("--model", "llama-tiny", "--seq-len", "128", "--batch-size", "4", "--steps", "30", "--warmup", "2",
                "--lr", "3e-3", "--master-weights", "on")
