@@ -266,6 +266,7 @@ def test_bench_contract_cli_and_graph_chunking():
     spec.loader.exec_module(bench)
     a = bench.parse_args([])
     assert a.gpus == 1 and a.steps > 0 and a.warmup >= 0
+    assert a.launch == "stream"  # measured default (profiles/r2_launch_ab.json); graph kept for A/B
     for k, w in [(2000, 50), (4000, 100), (100, 10), (7, 3), (5, 1), (30, 0), (1, 1), (1009, 5), (251, 0)]:
         spg = bench.pick_steps_per_graph(k, w)
         assert k % spg == 0 and 1 <= spg <= 250
