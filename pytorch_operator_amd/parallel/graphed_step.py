@@ -27,6 +27,12 @@ MI355X (profiles/r2_launch_overhead.json): a graph's FIRST launch still costs ~0
 node more than later ones, while back-to-back launches of a warm graph cost no more than
 one big graph -- so ``warm()`` replays the timed graph itself before falling back to a
 one-step graph for the remainder, and a caller sizes ``steps_per_graph`` to fit its warm-up.
+
+``launch="stream"`` (the bench / worker default since round 2) avoids both costs: the
+one-step graph's kernel nodes are launched straight onto the stream from C++
+(``pto_graph_launch_stream``), because each hipGraphLaunch leaves the GPU idle ~8.6 us
+before its first kernel (profiles/r2_k20_timeline.json, r2_launch_ab.json).  A graph with
+any non-kernel node keeps graph replay.
 """
 from __future__ import annotations
 
@@ -66,6 +72,8 @@ class NativeGraph:
         _native.check(rc, "hipStreamEndCapture/hipGraphInstantiate")
         self._h = h
         self.nodes = int(lib.pto_graph_nodes(h))
+        # a zero-count stream replay reports whether every node is a kernel (-2 otherwise)
+        self.stream_ok = lib.pto_graph_launch_stream(h, s.cuda_stream, 0) == 0
         _native.check(lib.pto_graph_upload(h, s.cuda_stream), "hipGraphUpload")
         s.synchronize()
         torch.cuda.current_stream(device).wait_stream(s)
@@ -133,20 +141,24 @@ class GraphedStep:
             self.internal_steps += 1
             torch.cuda.current_stream(tr.device).wait_stream(s)
             torch.cuda.synchronize(tr.device)
-        if whole_step and native and launch == "stream" and mode == "graph":
-            self.launch = "stream"
-            self.steps_per_graph = 1
         if whole_step:
             def steps(n):
                 def fn():
                     for _ in range(n):
                         tr.train_step()
                 return fn
-            if native:
+            if native and launch == "stream" and mode == "graph":
+                one = NativeGraph(steps(1), tr.device)
+                if one.stream_ok:
+                    self.launch, self.steps_per_graph = "stream", 1
+                    self._graph = self._warm = one
+                else:  # a captured node that is not a kernel: graph replay
+                    self._warm = one
+            if native and self._graph is None:
                 self._graph = NativeGraph(steps(self.steps_per_graph), tr.device)
-                self._warm = self._graph if self.steps_per_graph == 1 else \
-                    NativeGraph(steps(1), tr.device)
-            else:
+                self._warm = self._warm or (self._graph if self.steps_per_graph == 1 else
+                                            NativeGraph(steps(1), tr.device))
+            elif not native:
                 g = _capture(steps(self.steps_per_graph), tr.device)
                 self._graph = _TorchGraph(g)
                 self._warm = self._graph if self.steps_per_graph == 1 else \

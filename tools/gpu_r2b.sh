@@ -6,6 +6,8 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r2b
 O=gpurun_out/r2b
+( while sleep 30; do echo "hb $(date +%T)"; done ) & HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $O/pytest_gpu.log; exit 1; }
 tail -3 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $O/smoke.log; exit 1; }
