@@ -64,6 +64,9 @@ def parse_args(argv=None):
     p.add_argument("--linear-bwd", choices=["tn", "autograd"], default="tn",
                    help="Llama projections: backward GEMMs with K-contiguous (transposed-copy) operands, "
                         "or autograd's dy.W / dy^T.x layouts")
+    p.add_argument("--opt-overlap", choices=["on", "off"], default="on",
+                   help="Llama (master weights): AdamW updates on a side stream, overlapped with the next "
+                        "forward (each module waits only for its own parameters' updates)")
     p.add_argument("--gemm-tuning", choices=["off", "use", "tune"], default="use",
                    help="PyTorch TunableOp over hipBLASLt/rocBLAS for the model's GEMM shapes: 'use' "
                         "replays the measured per-shape winners in --gemm-tuning-file (shapes not in "
@@ -99,9 +102,13 @@ def build(args, device):
     with torch.device(device):
         model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
     if use_master_weights(args, device):
-        from ..ops.optim import MasterAdamW, to_bf16_matmul_weights
+        from ..ops.optim import MasterAdamW, install_overlap, to_bf16_matmul_weights
         to_bf16_matmul_weights(model)
-        opt = MasterAdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1)
+        overlap = args.opt_overlap == "on" and device.type == "cuda"
+        opt = MasterAdamW(model.parameters(), lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1,
+                          overlap=overlap)
+        if overlap:
+            install_overlap(model)
         return model, opt
     kw = {"fused": True} if device.type == "cuda" else {}
     try:
@@ -307,7 +314,8 @@ def main(argv=None) -> int:
            "master_weights": use_master_weights(args, dev)}
     res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
-        res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd)
+        res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd,
+                   opt_overlap=args.opt_overlap if res["master_weights"] else None)
     if tuning.get("mode") == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
         out = args.gemm_tuning_file or default_tuning_file()

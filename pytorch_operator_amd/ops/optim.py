@@ -37,8 +37,17 @@ def to_bf16_matmul_weights(model: nn.Module) -> int:
 
 
 class MasterAdamW(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+    """``overlap=True`` (GPU): ``step()`` enqueues the updates on a side stream, in parameter
+    order, and returns at once; each parameter gets a ready event, and ``install_overlap
+    (model)`` makes every module wait (on the compute stream) for its own parameters' events
+    just before its forward.  The next step's forward then starts while the updates of the
+    later layers are still streaming -- the memory-bound optimizer (~11 % of a Llama-3 8B
+    step) runs under the compute-bound forward GEMMs instead of after them."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, overlap=False):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.overlap = overlap
+        self._side = None
 
     def _state(self, p):
         st = self.state[p]
@@ -62,6 +71,25 @@ class MasterAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        side = None
+        for group in self.param_groups:
+            for p in group["params"]:
+                if self.overlap and p.is_cuda and p.grad is not None:
+                    if self._side is None:
+                        self._side = torch.cuda.Stream(device=p.device)
+                    side = self._side
+                    side.wait_stream(torch.cuda.current_stream(p.device))  # gradients complete
+                break
+            if side is not None:
+                break
+        if side is None:
+            self._step_all(None)
+        else:
+            with torch.cuda.stream(side):
+                self._step_all(side)
+        return loss
+
+    def _step_all(self, side):
         for group in self.param_groups:
             lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
             for p in group["params"]:
@@ -78,10 +106,16 @@ class MasterAdamW(torch.optim.Optimizer):
                     del p._pto_grad32
                 g = g32 if g32 is not None else p.grad
                 if p.is_cuda:
+                    if side is not None:
+                        g.record_stream(side)  # the next backward may reuse the memory otherwise
                     self._step_hip(p, g, master, st, lr, b1, b2, eps, wd)
+                    if side is not None:
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                        p._pto_ready = ev
                 else:
                     self._step_reference(p, g, master, st, lr, b1, b2, eps, wd)
-        return loss
+
 
     @staticmethod
     def _step_reference(p, g, master, st, lr, b1, b2, eps, wd):
@@ -107,3 +141,20 @@ class MasterAdamW(torch.optim.Optimizer):
             master.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), g.data_ptr(), out,
             p.numel(), 1 if g.dtype == torch.bfloat16 else 0, lr, b1, b2, eps, wd, st["step"], stream),
             "adamw_step")
+
+
+def install_overlap(model: nn.Module) -> int:
+    """Forward pre-hooks: each module with parameters of its own makes the current stream wait
+    for those parameters' optimizer-update events (``MasterAdamW(overlap=True)``); returns the
+    number of hooked modules."""
+    def hook(mod, _inputs):
+        for p in mod.parameters(recurse=False):
+            ev = getattr(p, "_pto_ready", None)
+            if ev is not None:
+                torch.cuda.current_stream(p.device).wait_event(ev)
+    n = 0
+    for mod in model.modules():
+        if any(True for _ in mod.parameters(recurse=False)):
+            mod.register_forward_pre_hook(hook)
+            n += 1
+    return n

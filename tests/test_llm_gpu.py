@@ -245,6 +245,34 @@ def test_linear_tn_matches_reference(dims):
     assert xg.grad.dtype == wg.grad.dtype == torch.bfloat16
 
 
+def test_master_adamw_overlap_matches_serial():
+    """AdamW on a side stream overlapped with the next forward (per-module ready events) gives
+    bit-identical weights and masters to the serial optimizer step."""
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    from pytorch_operator_amd.ops.optim import MasterAdamW, install_overlap, to_bf16_matmul_weights
+    torch.manual_seed(0)
+    tok = torch.randint(0, 256, (2, 65)).cuda()
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(3)
+        m = Llama(CONFIGS["llama-tiny"]).cuda()
+        to_bf16_matmul_weights(m)
+        opt = MasterAdamW(m.parameters(), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, overlap=overlap)
+        if overlap:
+            assert install_overlap(m) > 0
+        for _ in range(4):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(tok[:, :-1], tok[:, 1:])
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append(([p.detach().clone() for p in m.parameters()],
+                     [opt.state[p]["exp_avg"].clone() for p in m.parameters()]))
+    for a, b in zip(runs[0][0] + runs[0][1], runs[1][0] + runs[1][1]):
+        assert torch.equal(a, b)
+
+
 def test_llama_tiny_master_weights_trains_on_gpu():
     res = _run("--model", "llama-tiny", "--seq-len", "128", "--batch-size", "4", "--steps", "30", "--warmup", "2",
                "--lr", "3e-3", "--master-weights", "on")
