@@ -23,11 +23,13 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_allreduce_ranks(tmp_path, world):
+@pytest.mark.parametrize("world,nblk", [(2, 0), (4, 0), (2, 256)])
+def test_xgmi_allreduce_ranks(tmp_path, world, nblk):
+    """nblk=0 picks 128 workgroups per rank here (ranks share the box's GPU); nblk=256 runs the
+    geometry a one-GPU-per-rank job uses (2 x 256 small workgroups still fit co-resident)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
-           "--backend", "gloo", "--out", str(tmp_path)]
+           "--backend", "gloo", "--out", str(tmp_path), "--nblk", str(nblk)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=dict(os.environ, PYTHONPATH=str(ROOT)))
     results = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(world)
@@ -35,6 +37,7 @@ def test_xgmi_allreduce_ranks(tmp_path, world):
     assert r.returncode == 0 and len(results) == world, r.stdout[-3000:] + r.stderr[-3000:]
     for res in results:
         assert res["all_ok"], res
+        assert res["nblk"] == nblk or (nblk == 0 and res["nblk"] in (128, 256)), res
 
 
 def test_xgmi_stall_makes_every_rank_exit_retryable(tmp_path):

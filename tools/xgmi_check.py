@@ -54,6 +54,9 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--out", default=None, help="also write <out>/rank<r>.json")
+    ap.add_argument("--nblk", type=int, default=0,
+                    help="workgroups per rank (0 = auto: 256 when every rank owns its GPU, 128 "
+                         "when ranks share one; 256 on a shared GPU runs the cross-device geometry)")
     ap.add_argument("--bench", action="store_true",
                     help="time the fused exchange alone (graph of back-to-back launches)")
     a = ap.parse_args(argv)
@@ -71,7 +74,8 @@ def main(argv=None) -> int:
     rank, world, dev = env.rank, env.world_size, env.device
     res = {"rank": rank, "world": world}
     L = flat_layout().total
-    xar = XgmiAllReduce(L, device=dev)
+    xar = XgmiAllReduce(L, device=dev, nblk=a.nblk)
+    res["nblk"] = xar.nblk
     res["alloc_kind"] = xar.alloc_kind
     res["self_test"] = xar.self_test()
     res["self_test_report"] = xar.last_report[:4]
