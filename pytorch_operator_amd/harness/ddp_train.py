@@ -64,9 +64,16 @@ def parse_args(argv=None):
     p.add_argument("--linear-bwd", choices=["tn", "autograd"], default="tn",
                    help="Llama projections: backward GEMMs with K-contiguous (transposed-copy) operands, "
                         "or autograd's dy.W / dy^T.x layouts")
-    p.add_argument("--opt-overlap", choices=["on", "off"], default="on",
+    p.add_argument("--opt-overlap", choices=["on", "off"], default="off",
                    help="Llama (master weights): AdamW updates on a side stream, overlapped with the next "
-                        "forward (each module waits only for its own parameters' updates)")
+                        "forward (each module waits only for its own parameters' updates); measured neutral "
+                        "(358-360 ms both ways, profiles/r2_llama3_8b_opt_overlap_ab.json): the forward "
+                        "GEMMs hold every CU")
+    p.add_argument("--zero", choices=["auto", "0", "1"], default="auto",
+                   help="Llama (master weights): ZeRO-1 -- reduce-scatter fp32 gradients, AdamW on this "
+                        "rank's 1/W shard, all-gather bf16 weights (parallel/zero.py) instead of DDP's "
+                        "fp32 all-reduce + a full optimizer per rank; auto = on when world > 1")
+    p.add_argument("--zero-bucket-mb", type=float, default=256.0)
     p.add_argument("--gemm-tuning", choices=["off", "use", "tune"], default="use",
                    help="PyTorch TunableOp over hipBLASLt/rocBLAS for the model's GEMM shapes: 'use' "
                         "replays the measured per-shape winners in --gemm-tuning-file (shapes not in "
@@ -80,7 +87,15 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def build(args, device):
+def use_zero(args, device, world: int) -> bool:
+    if not args.model.startswith("llama") or args.dtype != "bf16":
+        return False
+    if args.zero == "1":
+        return True
+    return args.zero == "auto" and world > 1 and use_master_weights(args, device)
+
+
+def build(args, device, world: int = 1):
     import torch
     if args.model.startswith("resnet"):
         from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl
@@ -101,6 +116,14 @@ def build(args, device):
     RMSNorm.fuse_residual = args.residual_norm == "fused"
     with torch.device(device):
         model = Llama(CONFIGS[args.model], checkpoint_layers=args.grad_checkpoint)
+    if use_zero(args, device, world):
+        from ..ops.optim import to_bf16_matmul_weights
+        from ..parallel.zero import ZeroAdamW
+        to_bf16_matmul_weights(model)
+        opt = ZeroAdamW(model, lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1,
+                        bucket_mb=args.zero_bucket_mb,
+                        reduce_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else torch.float32)
+        return model, opt
     if use_master_weights(args, device):
         from ..ops.optim import MasterAdamW, install_overlap, to_bf16_matmul_weights
         to_bf16_matmul_weights(model)
@@ -207,6 +230,15 @@ def param_digest(model, opt) -> str:
     return h.hexdigest()
 
 
+def weights_digest(model) -> str:
+    """sha1 over every parameter tensor as the model holds it (bf16 weights, fp32 norms)."""
+    import hashlib
+    h = hashlib.sha1()
+    for p in model.parameters():
+        h.update(p.detach().float().cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
 def train_flops_per_sample(args) -> float:
     if args.model.startswith("resnet"):
         scale = (args.image_size / 224.0) ** 2
@@ -233,10 +265,11 @@ def main(argv=None) -> int:
     torch.manual_seed(args.seed)
     is_llama = args.model.startswith("llama")
     B = args.batch_size or (1 if is_llama else (256 if use_gpu else 2))
-    model, opt = build(args, dev)
+    model, opt = build(args, dev, world)
+    zero = use_zero(args, dev, world)
     tuning = setup_gemm_tuning(args, dev)
     n_params = sum(p.numel() for p in model.parameters())
-    if world > 1:
+    if world > 1 and not zero:
         from torch.nn.parallel import DistributedDataParallel as DDP
         model = DDP(model, device_ids=[dev.index] if use_gpu else None, bucket_cap_mb=args.bucket_mb,
                     gradient_as_bucket_view=True, static_graph=True)
@@ -311,11 +344,13 @@ def main(argv=None) -> int:
            "tflops_per_gpu": round(per_sample * samples / dt / world / 1e12, 1) if per_sample else None,
            "max_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if use_gpu else None,
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
-           "master_weights": use_master_weights(args, dev)}
+           "master_weights": use_master_weights(args, dev) or zero, "zero": 1 if zero else 0}
+    if zero:
+        res.update(optimizer_state_gb_per_rank=round(opt.state_bytes() / 2 ** 30, 2), zero_buckets=len(opt.buckets))
     res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
         res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd,
-                   opt_overlap=args.opt_overlap if res["master_weights"] else None)
+                   opt_overlap=args.opt_overlap if res["master_weights"] and not zero else None)
     if tuning.get("mode") == "tune" and rank == 0:
         import torch.cuda.tunable as tunable
         out = args.gemm_tuning_file or default_tuning_file()
@@ -325,8 +360,14 @@ def main(argv=None) -> int:
     if not is_llama:
         res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
                    conv1x1=args.conv1x1)
-    digest = param_digest(model.module if hasattr(model, "module") else model, opt)
-    print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest}), flush=True)
+    if zero:
+        opt.synchronize()
+        digest = opt.full_masters_digest()
+    else:
+        digest = param_digest(model.module if hasattr(model, "module") else model, opt)
+    wdig = weights_digest(model.module if hasattr(model, "module") else model)
+    print(json.dumps({"event": "param_digest", "rank": rank, "digest": digest, "weights_digest": wdig}),
+          flush=True)
     if rank == 0:
         print(json.dumps(res), flush=True)
         if args.json_out:

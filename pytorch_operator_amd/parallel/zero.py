@@ -1,0 +1,232 @@
+"""ZeRO-1 data parallelism for bf16 master-weight training (the Llama DDP worker, ``--zero 1``).
+
+The reference's DDP contract (``examples/mnist/mnist.py:136-138``: every replica steps the
+same model on its own data, gradients averaged) is kept; what changes is where the optimizer
+state lives.  ``DistributedDataParallel`` + ``MasterAdamW`` keeps, on EVERY rank, fp32
+masters + both AdamW moments (12 B/param: 96 GB for Llama-3 8B) and runs the memory-bound
+update over all of them (~40 ms of a 360 ms step on one MI355X,
+``profiles/r2_llama3_8b_step_kernels.md``).  Here each rank owns 1/W of every bucket:
+
+* backward: each gradient is copied (fp32) into its flat bucket as soon as autograd has
+  accumulated it (post-accumulate hook; the bf16 ``.grad`` is freed right away), the bucket
+  is scaled by 1/W and **reduce-scattered** (fp32 sum) asynchronously while backward goes on;
+* ``step()``: fused HIP AdamW (``csrc/kernels/adamw.hip``) on the rank's shard only
+  (master, m, v, grad shard -> new master + the bf16 weight shard, in place in the flat
+  weight bucket), then an async in-place **all-gather** of the bucket's weights;
+* next forward: a pre-hook per module waits (stream-side) for the all-gather of the buckets
+  holding that module's weights, so later buckets' all-gathers run under earlier layers.
+
+Bytes per rank and step over xGMI: reduce-scatter 4 B x (W-1)/W + all-gather 2 B x (W-1)/W
+per parameter, against 2 x 4 B x (W-1)/W for the fp32 all-reduce it replaces; optimizer state
+and update time are divided by W.  Buckets are large (``bucket_mb``, default 256 MB of
+fp32 gradient): few collectives, each well into RCCL's bandwidth regime on point-to-point
+xGMI links.
+
+``reduce_dtype=torch.bfloat16`` (``--allreduce-dtype bf16``) halves the reduce-scatter bytes,
+like DDP's ``bf16_compress_hook``.
+
+Numerics (fp32 reduction) equal ``DDP(fp32 comm hook) + MasterAdamW``: the same fp32 sum of the same
+``grad / W`` terms, the same AdamW per element (tests/test_harness.py pins the parameter
+digest of both paths equal on gloo).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+_ALIGN = 64  # shard lengths are multiples of this (16-byte aligned fp32 / bf16 shard pointers)
+
+
+class _Bucket:
+    def __init__(self, params: List[nn.Parameter], world: int, rank: int, reduce_dtype=torch.float32):
+        self.params = params
+        self.dtype = params[0].dtype
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        self.shard = -(-n // (world * _ALIGN)) * _ALIGN
+        self.npad = self.shard * world
+        self.lo = rank * self.shard
+        self.flat_w = torch.zeros(self.npad, dtype=self.dtype, device=dev)
+        self.grad32 = torch.zeros(self.npad, dtype=reduce_dtype, device=dev)  # gradient bucket
+        self.gshard = torch.zeros(self.shard, dtype=reduce_dtype, device=dev)
+        self.slot: Dict[int, int] = {}
+        masters = torch.zeros(self.npad, dtype=torch.float32, device=dev) if self.dtype != torch.float32 else None
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                self.slot[id(p)] = off
+                self.flat_w[off:off + k].copy_(p.detach().reshape(-1))
+                if masters is not None:
+                    init = getattr(p, "_pto_master", None)  # exact fp32 init (ops/optim.py)
+                    masters[off:off + k].copy_((init if init is not None else p.detach()).reshape(-1))
+                    if init is not None:
+                        del p._pto_master
+                p.data = self.flat_w[off:off + k].view(p.shape)
+                off += k
+        # fp32 master of the owned shard (None: fp32 weights are their own master)
+        self.master = masters[self.lo:self.lo + self.shard].clone() if masters is not None else None
+        del masters
+        self.exp_avg = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(self.shard, dtype=torch.float32, device=dev)
+        self.pending = len(params)
+        self.rs_work = None
+        self.ag_work = None
+
+    def w_shard(self) -> torch.Tensor:
+        return self.flat_w[self.lo:self.lo + self.shard]
+
+
+class ZeroAdamW:
+    """Replaces ``DDP(model) + MasterAdamW``: construct on the (unwrapped) model after
+    ``to_bf16_matmul_weights``; call ``zero_grad`` / forward / backward / ``step`` as usual.
+    Weights are broadcast from rank 0 at construction (DDP constructor semantics)."""
+
+    def __init__(self, model: nn.Module, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 group=None, bucket_mb: float = 256.0, reduce_dtype=torch.float32):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.t = 0
+        if reduce_dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError("reduce_dtype: float32 or bfloat16")
+        self.reduce_dtype = reduce_dtype
+        params = [p for p in model.parameters() if p.requires_grad]
+        if self.world > 1:
+            with torch.no_grad():
+                for p in params:
+                    dist.broadcast(p.data, 0, group=group)
+                    init = getattr(p, "_pto_master", None)
+                    if init is not None:
+                        dist.broadcast(init, 0, group=group)
+        # buckets in backward order (reverse registration), one dtype each, <= bucket_mb of fp32
+        cap = int(bucket_mb * 2 ** 20) // 4
+        self.buckets: List[_Bucket] = []
+        cur: List[nn.Parameter] = []
+        size = 0
+        for p in reversed(params):
+            if cur and (size + p.numel() > cap or p.dtype != cur[0].dtype):
+                self.buckets.append(_Bucket(cur, self.world, self.rank, reduce_dtype))
+                cur, size = [], 0
+            cur.append(p)
+            size += p.numel()
+        if cur:
+            self.buckets.append(_Bucket(cur, self.world, self.rank, reduce_dtype))
+        self._of: Dict[int, _Bucket] = {id(p): b for b in self.buckets for p in b.params}
+        for p in params:
+            p.register_post_accumulate_grad_hook(self._on_grad)
+        self._hooked = 0
+        for mod in model.modules():
+            own = [self._of[id(p)] for p in mod.parameters(recurse=False) if id(p) in self._of]
+            if own:
+                uniq = list({id(b): b for b in own}.values())
+                mod.register_forward_pre_hook(lambda _m, _i, bs=uniq: self._wait_weights(bs))
+                self._hooked += 1
+
+    # ------------------------------------------------------------------ backward side
+    def _on_grad(self, p: torch.Tensor) -> None:
+        b = self._of[id(p)]
+        off = b.slot[id(p)]
+        b.grad32[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        p.grad = None
+        b.pending -= 1
+        if b.pending == 0:
+            self._reduce_scatter(b)
+
+    def _reduce_scatter(self, b: _Bucket) -> None:
+        b.grad32.div_(self.world)  # the comm hooks' grad / W, then summed (fp32, or bf16 like bf16_compress_hook)
+        if self.world == 1:
+            b.gshard.copy_(b.grad32)
+            b.rs_work = None
+        else:
+            b.rs_work = dist.reduce_scatter_tensor(b.gshard, b.grad32, group=self.group, async_op=True)
+        b.pending = -1  # launched
+
+    def zero_grad(self, set_to_none: bool = True) -> None:  # noqa: ARG002 -- grads never persist
+        for b in self.buckets:
+            for p in b.params:
+                p.grad = None
+
+    # ------------------------------------------------------------------ optimizer side
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self.t += 1
+        for b in self.buckets:
+            if b.pending >= 0:  # some parameter got no gradient this step: it contributes zeros
+                for p in b.params:
+                    off = b.slot[id(p)]
+                    if p.grad is None:
+                        b.grad32[off:off + p.numel()].zero_()
+                    else:
+                        b.grad32[off:off + p.numel()].copy_(p.grad.reshape(-1))
+                        p.grad = None
+                self._reduce_scatter(b)
+        # forward order (the last bucket holds the first layers): their all-gathers go first
+        for b in reversed(self.buckets):
+            if b.rs_work is not None:
+                b.rs_work.wait()
+                b.rs_work = None
+            self._adamw(b)
+            if self.world > 1:
+                src = b.w_shard() if b.flat_w.is_cuda else b.w_shard().clone()
+                b.ag_work = dist.all_gather_into_tensor(b.flat_w, src, group=self.group, async_op=True)
+            b.pending = len(b.params)
+        return loss
+
+    def _adamw(self, b: _Bucket) -> None:
+        b1, b2 = self.betas
+        w = b.w_shard()
+        master = b.master if b.master is not None else w
+        if w.is_cuda:
+            from ..ops import _native
+            stream = ctypes.c_void_p(torch.cuda.current_stream(w.device).cuda_stream)
+            out = w.data_ptr() if b.master is not None else None
+            _native.check(_native.load().pto_adamw_step(
+                master.data_ptr(), b.exp_avg.data_ptr(), b.exp_avg_sq.data_ptr(), b.gshard.data_ptr(), out,
+                b.shard, 1 if self.reduce_dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps, self.weight_decay, self.t, stream), "adamw_step")
+        else:
+            from ..ops.optim import MasterAdamW
+            st = {"step": self.t, "exp_avg": b.exp_avg, "exp_avg_sq": b.exp_avg_sq}
+            MasterAdamW._step_reference(w, b.gshard, master, st, self.lr, b1, b2, self.eps, self.weight_decay)
+
+    def _wait_weights(self, buckets) -> None:
+        for b in buckets:
+            if b.ag_work is not None:
+                b.ag_work.wait()  # stream-side wait on GPU backends
+                b.ag_work = None
+
+    def synchronize(self) -> None:
+        """Wait for every outstanding weight all-gather (before reading the weights)."""
+        self._wait_weights(self.buckets)
+
+    # ------------------------------------------------------------------ inspection
+    def state_bytes(self) -> int:
+        """Optimizer-state bytes held by this rank (masters + moments of its shards)."""
+        n = 0
+        for b in self.buckets:
+            n += (b.exp_avg.numel() + b.exp_avg_sq.numel()) * 4
+            n += b.master.numel() * 4 if b.master is not None else 0
+        return n
+
+    def full_masters_digest(self) -> Optional[str]:
+        """sha1 of every bucket's fp32 masters gathered in rank order (all ranks must call)."""
+        import hashlib
+        h = hashlib.sha1()
+        for b in self.buckets:
+            m = b.master if b.master is not None else b.w_shard().float()
+            full = torch.zeros(b.npad, dtype=torch.float32, device=m.device)
+            if self.world > 1:
+                dist.all_gather_into_tensor(full, m.contiguous(), group=self.group)
+            else:
+                full.copy_(m)
+            h.update(full.cpu().numpy().tobytes())
+        return h.hexdigest()

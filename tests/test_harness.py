@@ -200,15 +200,75 @@ def test_ddp_train_worker_llama_tiny_master_weights_two_ranks(tmp_path):
     """bf16 matmul weights + fp32 masters (MasterAdamW) under DDP with the fp32 all-reduce hook."""
     outs = _launch("pytorch_operator_amd.harness.ddp_train",
                    ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--steps", "2", "--warmup", "1",
-                    "--backend", "gloo", "--master-weights", "on"], 2, tmp_path)
+                    "--backend", "gloo", "--master-weights", "on", "--zero", "0"], 2, tmp_path)
     for rc, out in outs:
         assert rc == 0, out
     res = json.loads([ln for ln in outs[0][1].splitlines() if ln.startswith('{"metric"')][-1])
-    assert res["master_weights"] is True and res["loss"] == res["loss"]
+    assert res["master_weights"] is True and res["zero"] == 0 and res["loss"] == res["loss"]
     # replicas stay identical: every rank's parameters AND fp32 masters hash the same
     digests = [json.loads([ln for ln in out.splitlines() if '"param_digest"' in ln][-1])["digest"]
                for _, out in outs]
     assert len(set(digests)) == 1, digests
+
+
+def _digests(outs):
+    return [json.loads([ln for ln in out.splitlines() if '"param_digest"' in ln][-1]) for _, out in outs]
+
+
+def test_ddp_train_llama_zero1_matches_ddp_master_adamw(tmp_path):
+    """ZeRO-1 (parallel/zero.py: fp32 reduce-scatter, AdamW on a 1/W shard, bf16 all-gather)
+    must produce bit-identical weights to DDP + fp32 all-reduce hook + MasterAdamW, with the
+    gathered fp32 masters identical on every rank, and hold 1/W of the optimizer state."""
+    base = ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--steps", "3", "--warmup", "1",
+            "--backend", "gloo", "--master-weights", "on", "--zero-bucket-mb", "0.05"]
+    (tmp_path / "z").mkdir()
+    (tmp_path / "d").mkdir()
+    outs_z = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--zero", "1"], 2, tmp_path / "z")
+    outs_d = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--zero", "0"], 2, tmp_path / "d")
+    for rc, out in outs_z + outs_d:
+        assert rc == 0, out
+    rz = json.loads([ln for ln in outs_z[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    rd = json.loads([ln for ln in outs_d[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    assert rz["zero"] == 1 and rz["zero_buckets"] > 2 and rd["zero"] == 0
+    assert rz["loss"] == rd["loss"]
+    dz, dd = _digests(outs_z), _digests(outs_d)
+    assert len({d["weights_digest"] for d in dz + dd}) == 1, (dz, dd)
+    assert len({d["digest"] for d in dz}) == 1, dz
+    from pytorch_operator_amd.models.llama import CONFIGS
+    n = CONFIGS["llama-tiny"].num_params()
+    assert rz["optimizer_state_gb_per_rank"] * 2 ** 30 < 12 * n * 0.6  # ~1/2 of 12 B/param
+
+
+@pytest.mark.parametrize("reduce_dtype", ["float32", "bfloat16"])
+def test_zero_adamw_single_process_matches_master_adamw(reduce_dtype):
+    """World 1 (no process group): ZeroAdamW's update equals MasterAdamW's, element for element;
+    a bf16 gradient bucket (bf16_compress_hook semantics) rounds the fp32 embedding/norm
+    gradients, so there the weights only agree to within AdamW's per-step bound (2 x lr)."""
+    import copy
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    from pytorch_operator_amd.ops.optim import MasterAdamW, to_bf16_matmul_weights
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+    torch.manual_seed(0)
+    m1 = Llama(CONFIGS["llama-tiny"])
+    m2 = copy.deepcopy(m1)
+    to_bf16_matmul_weights(m1)
+    to_bf16_matmul_weights(m2)
+    o1 = MasterAdamW(m1.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+    o2 = ZeroAdamW(m2, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=0.02,
+                   reduce_dtype=getattr(torch, reduce_dtype))
+    x = torch.randint(0, 256, (2, 17))
+    for _ in range(3):
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad(set_to_none=True)
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                loss = m(x[:, :-1], x[:, 1:])
+            loss.backward()
+            o.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        if reduce_dtype == "float32":
+            assert torch.equal(a, b)
+        else:
+            assert (a.float() - b.float()).abs().max() <= 3 * 2e-3
 
 
 def test_ddp_train_worker_resnet_tiny(tmp_path):

@@ -273,6 +273,35 @@ def test_master_adamw_overlap_matches_serial():
         assert torch.equal(a, b)
 
 
+def test_zero_adamw_matches_master_adamw_on_gpu():
+    """ZeRO-1 optimizer (world 1: flat fp32 gradient buckets, HIP AdamW on the bucket shard,
+    weights as views of flat bf16 buckets) gives bit-identical weights to MasterAdamW."""
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    from pytorch_operator_amd.ops.optim import MasterAdamW, to_bf16_matmul_weights
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+    tok = torch.randint(0, 256, (2, 65), generator=torch.Generator().manual_seed(0)).cuda()
+    runs = []
+    for zero in (False, True):
+        torch.manual_seed(3)
+        m = Llama(CONFIGS["llama-tiny"]).cuda()
+        to_bf16_matmul_weights(m)
+        if zero:
+            opt = ZeroAdamW(m, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=0.05)
+            assert len(opt.buckets) > 2
+        else:
+            opt = MasterAdamW(m.parameters(), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+        for _ in range(4):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(tok[:, :-1], tok[:, 1:])
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append([p.detach().clone() for p in m.parameters()])
+    for a, b in zip(runs[0], runs[1]):
+        assert torch.equal(a, b)
+
+
 def test_llama_tiny_master_weights_trains_on_gpu():
     res = _run("--model", "llama-tiny", "--seq-len", "128", "--batch-size", "4", "--steps", "30", "--warmup", "2",
                "--lr", "3e-3", "--master-weights", "on")
