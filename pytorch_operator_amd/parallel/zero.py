@@ -52,7 +52,8 @@ class _Bucket:
         self.lo = rank * self.shard
         self.flat_w = torch.zeros(self.npad, dtype=self.dtype, device=dev)
         self.grad32 = torch.zeros(self.npad, dtype=reduce_dtype, device=dev)  # gradient bucket
-        self.gshard = torch.zeros(self.shard, dtype=reduce_dtype, device=dev)
+        # world 1: the shard IS the bucket (no reduce-scatter, no copy)
+        self.gshard = self.grad32 if world == 1 else torch.zeros(self.shard, dtype=reduce_dtype, device=dev)
         self.slot: Dict[int, int] = {}
         masters = torch.zeros(self.npad, dtype=torch.float32, device=dev) if self.dtype != torch.float32 else None
         off = 0
@@ -132,16 +133,27 @@ class ZeroAdamW:
     def _on_grad(self, p: torch.Tensor) -> None:
         b = self._of[id(p)]
         off = b.slot[id(p)]
-        b.grad32[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
         p.grad = None
         b.pending -= 1
         if b.pending == 0:
             self._reduce_scatter(b)
 
+    def _deposit(self, dst: torch.Tensor, g: torch.Tensor) -> None:
+        """dst = g / W in the bucket dtype -- the comm hooks' ``grad / W`` before the sum.  For a
+        power-of-two W the scale is exact, so it rides on the cast copy (one pass)."""
+        w = self.world
+        if w == 1:
+            dst.copy_(g)
+        elif w & (w - 1) == 0:
+            src = g if dst.dtype == torch.float32 else g.to(dst.dtype)  # (out= never downcasts)
+            torch.mul(src, 1.0 / w, out=dst)
+        else:
+            dst.copy_(g)
+            dst.div_(w)
+
     def _reduce_scatter(self, b: _Bucket) -> None:
-        b.grad32.div_(self.world)  # the comm hooks' grad / W, then summed (fp32, or bf16 like bf16_compress_hook)
         if self.world == 1:
-            b.gshard.copy_(b.grad32)
             b.rs_work = None
         else:
             b.rs_work = dist.reduce_scatter_tensor(b.gshard, b.grad32, group=self.group, async_op=True)
@@ -167,7 +179,7 @@ class ZeroAdamW:
                     if p.grad is None:
                         b.grad32[off:off + p.numel()].zero_()
                     else:
-                        b.grad32[off:off + p.numel()].copy_(p.grad.reshape(-1))
+                        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
                         p.grad = None
                 self._reduce_scatter(b)
         # forward order (the last bucket holds the first layers): their all-gathers go first
