@@ -2,7 +2,8 @@
 """List the kernels of ONE steady-state step that match a regex, in launch order, with grid size,
 duration and the kernels launched just before / after them (where in the step they sit).
 
-usage: trace_context.py <kernel_trace.csv> <match-regex> <step-marker-regex> [min_us]
+usage: trace_context.py <kernel_trace.csv> <match-regex> <step-marker-regex> <total-steps> [min_us]
+(the marker, e.g. the optimizer kernel, launches the same number of times every step)
 """
 import csv
 import re
@@ -16,10 +17,14 @@ def short(n):
 
 def main():
     path, pat, marker = sys.argv[1], sys.argv[2], sys.argv[3]
-    min_us = float(sys.argv[4]) if len(sys.argv) > 4 else 0.0
+    total = int(sys.argv[4])
+    min_us = float(sys.argv[5]) if len(sys.argv) > 5 else 0.0
     ks = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(ks) if re.search(marker, r["Kernel_Name"])]
-    lo, hi = marks[-2] + 1, marks[-1] + 1  # the last whole step
+    per = len(marks) // total
+    if per < 1 or len(marks) % total:
+        raise SystemExit(f"{len(marks)} marker kernels do not divide into {total} steps")
+    lo, hi = marks[-per - 1] + 1, marks[-1] + 1  # the last whole step
     for i in range(lo, hi):
         r = ks[i]
         if not re.search(pat, r["Kernel_Name"]):
