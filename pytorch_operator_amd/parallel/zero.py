@@ -105,19 +105,24 @@ class ZeroAdamW:
                     init = getattr(p, "_pto_master", None)
                     if init is not None:
                         dist.broadcast(init, 0, group=group)
-        # buckets in backward order (reverse registration), one dtype each, <= bucket_mb of fp32
+        # buckets in backward order (reverse registration), <= bucket_mb of fp32 each; one open
+        # bucket per dtype, so the small fp32 norm weights between the bf16 projections share
+        # buckets instead of each cutting a bf16 run into a tiny collective
         cap = int(bucket_mb * 2 ** 20) // 4
         self.buckets: List[_Bucket] = []
-        cur: List[nn.Parameter] = []
-        size = 0
+        open_: Dict[torch.dtype, List[nn.Parameter]] = {}
+        size: Dict[torch.dtype, int] = {}
         for p in reversed(params):
-            if cur and (size + p.numel() > cap or p.dtype != cur[0].dtype):
+            cur = open_.setdefault(p.dtype, [])
+            if cur and size[p.dtype] + p.numel() > cap:
                 self.buckets.append(_Bucket(cur, self.world, self.rank, reduce_dtype))
-                cur, size = [], 0
+                cur = open_[p.dtype] = []
+                size[p.dtype] = 0
             cur.append(p)
-            size += p.numel()
-        if cur:
-            self.buckets.append(_Bucket(cur, self.world, self.rank, reduce_dtype))
+            size[p.dtype] = size.get(p.dtype, 0) + p.numel()
+        for cur in open_.values():
+            if cur:
+                self.buckets.append(_Bucket(cur, self.world, self.rank, reduce_dtype))
         self._of: Dict[int, _Bucket] = {id(p): b for b in self.buckets for p in b.params}
         for p in params:
             p.register_post_accumulate_grad_hook(self._on_grad)

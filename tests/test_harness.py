@@ -239,6 +239,20 @@ def test_ddp_train_llama_zero1_matches_ddp_master_adamw(tmp_path):
     assert rz["optimizer_state_gb_per_rank"] * 2 ** 30 < 12 * n * 0.6  # ~1/2 of 12 B/param
 
 
+def test_ddp_train_llama_zero1_three_ranks_bf16_reduce(tmp_path):
+    """Non-power-of-two world (copy + divide path) with the bf16 reduce-scatter: replicas agree."""
+    outs = _launch("pytorch_operator_amd.harness.ddp_train",
+                   ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--steps", "2", "--warmup", "1",
+                    "--backend", "gloo", "--master-weights", "on", "--zero", "1", "--allreduce-dtype", "bf16"],
+                   3, tmp_path)
+    for rc, out in outs:
+        assert rc == 0, out
+    res = json.loads([ln for ln in outs[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    assert res["zero"] == 1 and res["n_gpus"] == 3 and res["loss"] == res["loss"]
+    d = _digests(outs)
+    assert len({x["weights_digest"] for x in d}) == 1 and len({x["digest"] for x in d}) == 1, d
+
+
 @pytest.mark.parametrize("reduce_dtype", ["float32", "bfloat16"])
 def test_zero_adamw_single_process_matches_master_adamw(reduce_dtype):
     """World 1 (no process group): ZeroAdamW's update equals MasterAdamW's, element for element;
