@@ -81,6 +81,10 @@ def parse_args(argv=None):
                         "during the first (untimed) step and writes the file, 'off' = library default")
     p.add_argument("--gemm-tuning-file", default=None,
                    help="TunableOp results CSV (default: pytorch_operator_amd/tuning/gemm_mi355x.csv)")
+    p.add_argument("--ckpt-dir", default=None,
+                   help="checkpoint directory (utils/train_ckpt.py): resume from it if it holds one, save "
+                        "there at the end (and every --ckpt-every steps); shared by all ranks")
+    p.add_argument("--ckpt-every", type=int, default=0)
     p.add_argument("--lr", type=float, default=None)
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--json-out", default=None)
@@ -291,8 +295,17 @@ def main(argv=None) -> int:
             x = x.to(memory_format=torch.channels_last)
         y = torch.randint(0, 1000 if args.model == "resnet50" else 10, (B,), generator=g).to(dev)
     amp = torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=args.dtype == "bf16")
+    from ..utils import train_ckpt
+    bare = model.module if hasattr(model, "module") else model
+    gstep = train_ckpt.load(args.ckpt_dir, bare, opt, rank, world, dev)
+    if gstep and rank == 0:
+        print(json.dumps({"event": "resumed", "step": gstep, "dir": args.ckpt_dir}), flush=True)
 
     def step():
+        nonlocal gstep
+        gstep += 1
+        if args.ckpt_dir and args.ckpt_every and gstep % args.ckpt_every == 0:
+            pending_ckpt.append(gstep)
         opt.zero_grad(set_to_none=True)
         with amp:
             if is_llama:
@@ -301,7 +314,11 @@ def main(argv=None) -> int:
                 loss = F.cross_entropy(model(x).float(), y)
         loss.backward()
         opt.step()
+        if pending_ckpt:
+            train_ckpt.save(args.ckpt_dir, pending_ckpt.pop(), bare, opt, rank, world)
         return loss
+
+    pending_ckpt = []
 
     def sync():
         if use_gpu:
@@ -360,6 +377,9 @@ def main(argv=None) -> int:
     if not is_llama:
         res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
                    conv1x1=args.conv1x1)
+    if args.ckpt_dir:
+        train_ckpt.save(args.ckpt_dir, gstep, bare, opt, rank, world)
+        res.update(checkpoint_step=gstep)
     if zero:
         opt.synchronize()
         digest = opt.full_masters_digest()

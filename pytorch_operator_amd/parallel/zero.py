@@ -225,6 +225,27 @@ class ZeroAdamW:
         """Wait for every outstanding weight all-gather (before reading the weights)."""
         self._wait_weights(self.buckets)
 
+    # ------------------------------------------------------------------ checkpoint (utils/train_ckpt.py)
+    def shard_state_dict(self) -> dict:
+        """This rank's optimizer shard: step count + fp32 master / moments of each bucket's slice
+        (the weights themselves are in the model's state_dict)."""
+        return {"t": self.t, "world": self.world, "rank": self.rank,
+                "buckets": [{"npad": b.npad, "master": b.master, "exp_avg": b.exp_avg,
+                             "exp_avg_sq": b.exp_avg_sq} for b in self.buckets]}
+
+    @torch.no_grad()
+    def load_shard_state_dict(self, sd: dict) -> None:
+        if sd["world"] != self.world or sd["rank"] != self.rank or len(sd["buckets"]) != len(self.buckets):
+            raise ValueError("ZeRO shard checkpoint was written by a different world / rank / bucket layout")
+        for b, s in zip(self.buckets, sd["buckets"]):
+            if s["npad"] != b.npad or (s["master"] is None) != (b.master is None):
+                raise ValueError("ZeRO shard checkpoint bucket layout differs")
+            if b.master is not None:
+                b.master.copy_(s["master"])
+            b.exp_avg.copy_(s["exp_avg"])
+            b.exp_avg_sq.copy_(s["exp_avg_sq"])
+        self.t = int(sd["t"])
+
     # ------------------------------------------------------------------ inspection
     def state_bytes(self) -> int:
         """Optimizer-state bytes held by this rank (masters + moments of its shards)."""

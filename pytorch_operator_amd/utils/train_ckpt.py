@@ -1,0 +1,116 @@
+"""Checkpoint / resume for the large-model DDP worker (``harness/ddp_train.py --ckpt-dir``).
+
+BASELINE's "Llama-3 8B DDP ... OnFailure restart" only pays off if a restarted replica set
+continues where it stopped: the operator restarts the pods (retryable exit codes,
+``pkg/controller.v1/pytorch/controller.go`` + tf-operator ``train_util.go:18-53``), the worker
+reloads the last checkpoint.  The MNIST worker has the reference's own ``--save-model`` plus
+epoch checkpoints (``harness/mnist.py``); this is the same contract for the bigger workers.
+
+Layout of ``<dir>``:
+  model.pt            weights as the model holds them (bf16 matmul weights, fp32 rest), rank 0
+  optim.pt            replicated optimizer state (DDP paths), rank 0
+  optim_rank<r>.pt    this rank's shard (ZeRO-1: fp32 master + moments of its 1/W of each bucket)
+  meta.json           {"step", "world", "sharded"}: written last, after every rank finished,
+                      so a crash mid-save leaves the previous checkpoint loadable
+
+All files are written to a temporary name and renamed; tensors are loaded with
+``torch.load(weights_only=True)``.  A sharded checkpoint needs the same world size to resume.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def _atomic_save(obj, path: str) -> None:
+    tmp = path + ".tmp"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
+def _barrier(world: int) -> None:
+    if world > 1:
+        dist.barrier()
+
+
+def _cpu(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu()
+    if isinstance(x, dict):
+        return {k: _cpu(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_cpu(v) for v in x)
+    return x
+
+
+def optimizer_state(opt) -> dict:
+    """Replicated optimizer state in a form that reloads without dtype casts: MasterAdamW keeps
+    fp32 masters/moments for bf16 parameters, which ``Optimizer.load_state_dict`` would cast
+    to the parameter dtype, so its per-parameter state is stored by parameter index."""
+    from ..ops.optim import MasterAdamW
+    if isinstance(opt, MasterAdamW):
+        params = [p for g in opt.param_groups for p in g["params"]]
+        return {"kind": "master_adamw",
+                "state": [{k: v for k, v in opt.state[p].items()} if p in opt.state else None for p in params]}
+    return {"kind": "torch", "state_dict": opt.state_dict()}
+
+
+def load_optimizer_state(opt, blob: dict) -> None:
+    if blob["kind"] == "master_adamw":
+        params = [p for g in opt.param_groups for p in g["params"]]
+        if len(params) != len(blob["state"]):
+            raise ValueError("checkpoint optimizer state does not match the parameters")
+        for p, st in zip(params, blob["state"]):
+            if st is None:
+                continue
+            opt.state[p] = {k: (v.to(p.device) if isinstance(v, torch.Tensor) else v) for k, v in st.items()}
+            if hasattr(p, "_pto_master"):
+                del p._pto_master  # the checkpoint's master replaces the init copy
+    else:
+        opt.load_state_dict(blob["state_dict"])
+
+
+def save(dirpath: str, step: int, model, opt, rank: int, world: int) -> None:
+    os.makedirs(dirpath, exist_ok=True)
+    sharded = hasattr(opt, "shard_state_dict")
+    if hasattr(opt, "synchronize"):
+        opt.synchronize()  # ZeRO: weights all-gathered before they are written
+    if rank == 0:
+        _atomic_save(_cpu(model.state_dict()), os.path.join(dirpath, "model.pt"))
+        if not sharded:
+            _atomic_save(_cpu(optimizer_state(opt)), os.path.join(dirpath, "optim.pt"))
+    if sharded:
+        _atomic_save(_cpu(opt.shard_state_dict()), os.path.join(dirpath, f"optim_rank{rank}.pt"))
+    _barrier(world)
+    if rank == 0:
+        tmp = os.path.join(dirpath, "meta.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump({"step": int(step), "world": int(world), "sharded": sharded}, f)
+        os.replace(tmp, os.path.join(dirpath, "meta.json"))
+    _barrier(world)
+
+
+def load(dirpath: Optional[str], model, opt, rank: int, world: int, device) -> int:
+    """Restore the last checkpoint in ``dirpath`` (if any); returns the step it was taken at (0: none)."""
+    if not dirpath or not os.path.exists(os.path.join(dirpath, "meta.json")):
+        return 0
+    with open(os.path.join(dirpath, "meta.json")) as f:
+        meta = json.load(f)
+    sharded = hasattr(opt, "shard_state_dict")
+    if meta["sharded"] != sharded or (sharded and meta["world"] != world):
+        raise ValueError(f"checkpoint {dirpath} (world {meta['world']}, sharded {meta['sharded']}) cannot "
+                         f"resume a world-{world} {'sharded' if sharded else 'replicated'} optimizer")
+    sd = torch.load(os.path.join(dirpath, "model.pt"), map_location=device, weights_only=True)
+    with torch.no_grad():
+        model.load_state_dict(sd)  # copies into the existing (bucket-view) parameters
+    if sharded:
+        opt.load_shard_state_dict(torch.load(os.path.join(dirpath, f"optim_rank{rank}.pt"), map_location=device,
+                                             weights_only=True))
+    else:
+        load_optimizer_state(opt, torch.load(os.path.join(dirpath, "optim.pt"), map_location=device,
+                                             weights_only=True))
+    return int(meta["step"])

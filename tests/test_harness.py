@@ -239,6 +239,47 @@ def test_ddp_train_llama_zero1_matches_ddp_master_adamw(tmp_path):
     assert rz["optimizer_state_gb_per_rank"] * 2 ** 30 < 12 * n * 0.6  # ~1/2 of 12 B/param
 
 
+@pytest.mark.parametrize("zero", ["0", "1"])
+def test_ddp_train_checkpoint_resume_matches_uninterrupted(tmp_path, zero):
+    """OnFailure-restart contract for the Llama worker: 2 steps + checkpoint, then a fresh process
+    pair resuming for 2 more, ends bit-identical to 4 uninterrupted steps (DDP + MasterAdamW and
+    ZeRO-1 sharded optimizer state)."""
+    base = ["--model", "llama-tiny", "--seq-len", "32", "--batch-size", "2", "--warmup", "1",
+            "--backend", "gloo", "--master-weights", "on", "--zero", zero, "--zero-bucket-mb", "0.05"]
+    for d in ("a", "b"):
+        (tmp_path / d).mkdir()
+    ck = str(tmp_path / "b" / "ckpt")
+    outs_a = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "3"], 2, tmp_path / "a")
+    outs_b1 = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "1", "--ckpt-dir", ck], 2,
+                      tmp_path / "b")
+    outs_b2 = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "1", "--ckpt-dir", ck], 2,
+                      tmp_path / "b")
+    for rc, out in outs_a + outs_b1 + outs_b2:
+        assert rc == 0, out
+    assert '"event": "resumed", "step": 2' in outs_b2[0][1]
+    ra = json.loads([ln for ln in outs_a[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    rb = json.loads([ln for ln in outs_b2[0][1].splitlines() if ln.startswith('{"metric"')][-1])
+    assert rb["checkpoint_step"] == 4 and rb["loss"] == ra["loss"]
+    da, db = _digests(outs_a), _digests(outs_b2)
+    assert {x["weights_digest"] for x in da} == {x["weights_digest"] for x in db}
+    assert {x["digest"] for x in da} == {x["digest"] for x in db}
+
+
+def test_ddp_train_resnet_tiny_checkpoint_resume(tmp_path):
+    """The torch-optimizer path (ResNet, SGD momentum buffers): resume equals uninterrupted."""
+    base = ["--model", "resnet-tiny", "--batch-size", "4", "--warmup", "1", "--backend", "gloo", "--dtype", "fp32"]
+    for d in ("a", "b"):
+        (tmp_path / d).mkdir()
+    ck = str(tmp_path / "b" / "ckpt")
+    (ra, oa), = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "3"], 1, tmp_path / "a")
+    (r1, o1), = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "1", "--ckpt-dir", ck], 1,
+                        tmp_path / "b")
+    (r2, o2), = _launch("pytorch_operator_amd.harness.ddp_train", base + ["--steps", "1", "--ckpt-dir", ck], 1,
+                        tmp_path / "b")
+    assert ra == r1 == r2 == 0, o1 + o2
+    assert _digests([(0, oa)])[0]["weights_digest"] == _digests([(0, o2)])[0]["weights_digest"]
+
+
 def test_ddp_train_llama_zero1_three_ranks_bf16_reduce(tmp_path):
     """Non-power-of-two world (copy + divide path) with the bf16 reduce-scatter: replicas agree."""
     outs = _launch("pytorch_operator_amd.harness.ddp_train",
