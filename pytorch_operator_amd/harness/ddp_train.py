@@ -51,6 +51,8 @@ def parse_args(argv=None):
                    help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
     p.add_argument("--bn", choices=["hip", "library"], default="hip",
                    help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
+    p.add_argument("--pool", choices=["hip", "library"], default="hip",
+                   help="ResNet stem max-pool: HIP kernels (1-byte taps, gather backward) or PyTorch's op")
     p.add_argument("--conv1x1", choices=["gemm", "library"], default="library",
                    help="ResNet: 1x1 convolutions as hipBLASLt GEMMs on the NHWC view, or MIOpen convs "
                         "(library: 30.5 vs 47.3 ms/step at B=256 -- hipBLASLt's picks for the K = N*H*W "
@@ -102,8 +104,9 @@ def use_zero(args, device, world: int) -> bool:
 def build(args, device, world: int = 1):
     import torch
     if args.model.startswith("resnet"):
-        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl
+        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl, set_pool_impl
         model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
+        set_pool_impl(model, args.pool)
         set_conv1x1_impl(model, args.conv1x1)
         fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format
         model = model.to(device=device, memory_format=fmt)
@@ -375,7 +378,7 @@ def main(argv=None) -> int:
         write_tuning_file(out)
         res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
-        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn, pool=args.pool,
                    conv1x1=args.conv1x1)
     if args.ckpt_dir:
         train_ckpt.save(args.ckpt_dir, gstep, bare, opt, rank, world)

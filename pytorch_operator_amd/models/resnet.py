@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.pool import MaxPool3x3s2
 
 
 class Conv1x1(nn.Conv2d):
@@ -70,7 +71,7 @@ class ResNet(nn.Module):
         self.inplanes = width
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(width, relu=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool3x3s2()  # nn.MaxPool2d(3, 2, 1); HIP kernels for channels-last bf16
         self.layer1 = self._make(width, layers[0])
         self.layer2 = self._make(width * 2, layers[1], stride=2)
         self.layer3 = self._make(width * 4, layers[2], stride=2)
@@ -109,6 +110,16 @@ def set_bn_impl(model: nn.Module, impl: str) -> nn.Module:
         raise ValueError(impl)
     for m in model.modules():
         if isinstance(m, BatchNormAct2d):
+            m.impl = impl
+    return model
+
+
+def set_pool_impl(model: nn.Module, impl: str) -> nn.Module:
+    """``"hip"``: the stem max-pool on ``csrc/kernels/pool.hip``; ``"library"``: PyTorch's op."""
+    if impl not in ("hip", "library"):
+        raise ValueError(impl)
+    for m in model.modules():
+        if isinstance(m, MaxPool3x3s2):
             m.impl = impl
     return model
 

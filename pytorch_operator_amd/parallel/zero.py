@@ -137,6 +137,9 @@ class ZeroAdamW:
     # ------------------------------------------------------------------ backward side
     def _on_grad(self, p: torch.Tensor) -> None:
         b = self._of[id(p)]
+        if b.pending < 0:
+            raise RuntimeError("ZeroAdamW: a second backward before step() -- gradient accumulation "
+                               "across backward passes is not supported (the bucket was already reduced)")
         off = b.slot[id(p)]
         self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
         p.grad = None

@@ -338,6 +338,20 @@ def test_llama_tiny_trains_on_gpu():
     assert res["loss"] < 5.0  # log(256) = 5.55 at init; memorising a fixed batch drives it down
 
 
+@pytest.mark.parametrize("zero", ["0", "1"])
+def test_llama_tiny_checkpoint_resume_on_gpu(tmp_path, zero):
+    """GPU (HIP AdamW, bf16 weights + fp32 masters; ZeRO-1 shard state): 2 steps + checkpoint +
+    2 resumed steps give the loss of 4 uninterrupted steps."""
+    base = ["--model", "llama-tiny", "--seq-len", "64", "--batch-size", "2", "--warmup", "1", "--lr", "3e-3",
+            "--zero", zero]
+    full = _run(*base, "--steps", "3")
+    ck = str(tmp_path / "ck")
+    _run(*base, "--steps", "1", "--ckpt-dir", ck)
+    res = _run(*base, "--steps", "1", "--ckpt-dir", ck)
+    assert res["checkpoint_step"] == 4 and res["zero"] == int(zero)
+    assert res["loss"] == full["loss"]
+
+
 def test_resnet50_bf16_step_on_gpu():
     res = _run("--model", "resnet50", "--batch-size", "32", "--steps", "3", "--warmup", "1")
     assert res["value"] > 0 and res["loss"] == res["loss"]
