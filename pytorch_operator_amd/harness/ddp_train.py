@@ -378,7 +378,8 @@ def main(argv=None) -> int:
         write_tuning_file(out)
         res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
-        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn, pool=args.pool,
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
+                   pool=args.pool,
                    conv1x1=args.conv1x1)
     if args.ckpt_dir:
         train_ckpt.save(args.ckpt_dir, gstep, bare, opt, rank, world)

@@ -212,7 +212,8 @@ class ZeroAdamW:
             out = w.data_ptr() if b.master is not None else None
             _native.check(_native.load().pto_adamw_step(
                 master.data_ptr(), b.exp_avg.data_ptr(), b.exp_avg_sq.data_ptr(), b.gshard.data_ptr(), out,
-                b.shard, 1 if self.reduce_dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps, self.weight_decay, self.t, stream), "adamw_step")
+                b.shard, 1 if self.reduce_dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps,
+                self.weight_decay, self.t, stream), "adamw_step")
         else:
             from ..ops.optim import MasterAdamW
             st = {"step": self.t, "exp_avg": b.exp_avg, "exp_avg_sq": b.exp_avg_sq}
