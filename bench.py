@@ -60,6 +60,13 @@ def parse_args(argv=None):
     p.add_argument("--fuse-conv12", type=int, default=1)
     p.add_argument("--schedule", choices=["fused", "classic"], default="classic",
                    help="single-GPU launch schedule (A/B): 5-launch fused or 6-launch classic")
+    p.add_argument("--conv-chunk", type=int, default=4, choices=[1, 4],
+                   help="conv backward: dW_conv2 per 4-sample chunk (slab 4x smaller) or per sample")
+    p.add_argument("--fc-sgd", default="tail", choices=["fused", "tail"],
+                   help="fc parameters' SGD inside fc1_bwd's weight-gradient tiles, or in the tail launch")
+    p.add_argument("--stage", type=int, default=1, help="stage the next batch during fc1_bwd (1/0)")
+    p.add_argument("--store-fc-grads", type=int, default=1,
+                   help="fused fc SGD: also store the fc gradients (1/0)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "rccl", "gloo"],
                    help="collective backend (gloo only to rehearse the multi-rank path on one GPU)")
     p.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -162,6 +169,8 @@ def main(argv=None):
         tr.overlap = bool(args.overlap)
         tr.fuse_conv12 = bool(args.fuse_conv12)
         tr.schedule = args.schedule
+        tr.conv_chunk, tr.fc_sgd = args.conv_chunk, args.fc_sgd
+        tr.stage_batches, tr.store_fc_grads = bool(args.stage), bool(args.store_fc_grads)
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph if args.steps_per_graph > 0 else pick_steps_per_graph(args.steps, args.warmup)
@@ -189,8 +198,8 @@ def main(argv=None):
         steps = args.steps - args.steps % runner.steps_per_graph
         xgmi_error = (lambda: xg.xar.error()) if xg is not None else (lambda: 0)
         mode_desc = (f"{args.mode}(launch={runner.launch},spg={runner.steps_per_graph},overlap={args.overlap},"
-                     f"allreduce={ar_path},"
-                     f"schedule={args.schedule})")
+                     f"allreduce={ar_path},schedule={args.schedule},conv_chunk={args.conv_chunk},"
+                     f"fc_sgd={args.fc_sgd},stage={args.stage},store_fc_grads={args.store_fc_grads})")
     else:
         from pytorch_operator_amd.models.mnist import Net
         import torch.nn.functional as F

@@ -39,6 +39,18 @@
 
 using namespace pto;
 
+// Experiment switches (tools/build_exp.sh builds -D variants for same-box A/B; defaults = the
+// measured winners, profiles/r3_*)
+#ifndef PTO_C1_ROLES
+#define PTO_C1_ROLES 1      // conv12: conv1 MFMA tiles and VALU windows on separate waves
+#endif
+#ifndef PTO_C12_DEFER_W2
+#define PTO_C12_DEFER_W2 1  // conv12: conv2 weight slice lands in LDS after conv1
+#endif
+#ifndef PTO_B4_SPLIT
+#define PTO_B4_SPLIT 1      // conv_bwd4: chunk samples' loads overlap phase 2a
+#endif
+
 namespace {
 
 typedef unsigned long long u64;
@@ -282,7 +294,7 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
 // rows {2py, 2py+1} x cols 8px..8px+7) as NU independent accumulator chains, then bias +
 // ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1 if pub).  Channels 16-19
 // would fill only a quarter of a second 16-wide channel tile: conv1_valu_window does them.
-template <int NU>
+template <int NU, int TS = 16>
 __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int (&toff)[7],
                                             const float (&bw)[7], float bc, float* in_s,
                                             bool pub, float* a1, uint8_t* idx1, int b, int i, int g) {
@@ -290,7 +302,7 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
   const float* ibs[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int pt1 = t0 + 16 * u;
+    const int pt1 = t0 + TS * u;
     const int py = pt1 / 3, px = pt1 - py * 3;
     ibs[u] = img + (2 * py + (i >> 3)) * AB_IRS + 8 * px + (i & 7);
     acc[u] = zero4();
@@ -309,7 +321,7 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     for (int u = 0; u < NU; ++u) acc[u] = mfma16x16x4(av[u][s], bw[s], acc[u]);
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int pt1 = t0 + 16 * u;
+    const int pt1 = t0 + TS * u;
     const int py = pt1 / 3, px = pt1 - py * 3;
     const int c = i;
     const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc, v3 = acc[u][3] + bc;
@@ -380,11 +392,28 @@ __device__ __forceinline__ void conv1_valu_window(int item, const float* img, co
   }
 }
 
+// conv2 weight slice of output-channel group cg (16 rows of 500) from registers into LDS
+__device__ __forceinline__ void conv12_store_w2(float* w_s, const float4 (&wq)[2], int cg, int tid) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = tid + k * AB_NT;
+    if (e < 16 * 125) {
+      const int j = e / 125, q = e - j * 125;
+      float4 v = wq[k];
+      if (cg * 16 + j >= 50) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
+      d[0] = make_float2(v.x, v.y);
+      d[1] = make_float2(v.z, v.w);
+    }
+  }
+}
+
 __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     BatchSrc src, const float* __restrict__ w1, const float* __restrict__ b1,
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
     uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
-    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
+    float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, const uint8_t* __restrict__ stg_x,
+    const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, u64* dbg) {
   __shared__ float img[28 * AB_IRS];
   __shared__ float w1s[520];
   __shared__ __align__(16) float in_s[20 * C2_CS];
@@ -392,16 +421,34 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   stamp(dbg, 0);
-  const int row = batch_row(src, b, B);
   const bool pub = cg == 0;
   // conv2 epilogue bias, loaded with the staging loads (no round trip after the last barrier)
   const int co_pre = cg * 16 + (tid & 15);
   const float bco = co_pre < 50 ? bias[co_pre] : 0.f;
+  float4 wq[2];
   {
-    const float x0 = load_px(src, row, min(tid, 783));
+    // the batch: from the staging buffer the previous step's fc1_bwd filled (one load, no
+    // cursor -> permutation -> pixel chain) when its tag is this step's cursor, else gathered
+    float x0;
+    int lab = 0;
+    if (stg_x != nullptr) {
+      x0 = (float)stg_x[(size_t)b * 784 + min(tid, 783)] * src.scale + src.shift;
+      lab = stg_lab[b];
+      if (stg_tag[0] != src.cursor[0]) {  // block-uniform
+        const int row = batch_row(src, b, B);
+        x0 = load_px(src, row, min(tid, 783));
+        if (src.labels != nullptr) lab = src.labels[row];
+      }
+    } else {
+      const int row = batch_row(src, b, B);
+      x0 = load_px(src, row, min(tid, 783));
+      if (src.labels != nullptr) lab = src.labels[row];
+    }
     const float wv = w1[min(tid, 499)];
     const float bv1 = b1[min(tid, 19)];
-    float4 wq[2];
+    // the conv2 weight slice is only needed after conv1: its loads stay in flight through the
+    // conv1 phase and land in LDS right before the conv1 -> conv2 barrier (issued after the
+    // image / conv1 loads, so waiting for those does not wait for these)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = min(tid + k * AB_NT, 16 * 125 - 1);
@@ -412,32 +459,26 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     if (tid < 784) img[(tid / 28) * AB_IRS + tid % 28] = x0;
     if (tid < 500) w1s[tid] = wv;
     if (tid < 20) w1s[500 + tid] = bv1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + k * AB_NT;
-      if (e < 16 * 125) {
-        const int j = e / 125, q = e - j * 125;
-        float4 v = wq[k];
-        if (cg * 16 + j >= 50) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
-        d[0] = make_float2(v.x, v.y);
-        d[1] = make_float2(v.z, v.w);
-      }
-    }
+#if !PTO_C12_DEFER_W2
+    conv12_store_w2(w_s, wq, cg, tid);
+#endif
     if (pub && tid < 784) {
       xn_out[(size_t)b * 784 + tid] = x0;
-      if (tid == 0 && lab_out != nullptr) lab_out[b] = src.labels[row];
+      if (tid == 0 && lab_out != nullptr) lab_out[b] = lab;
     }
   }
   __syncthreads();
   stamp(dbg, 1);
   // conv1 + bias + ReLU + 2x2 max-pool.  Channels 0-15: implicit GEMM on MFMA, 36
   // position tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 7 K-steps (25 taps,
-  // zero-padded to 28 through the weight fragments); wave w takes tiles w, w+16 (+ w+32
-  // for w < 4): 9 tiles per SIMD.  The pool epilogue is the same register/lane^32
-  // pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
+  // zero-padded to 28 through the weight fragments).  The pool epilogue is the same
+  // register/lane^32 pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU.
+  // Wave roles (any 8 consecutive waves cover every SIMD twice): waves 0-7 run the MFMA
+  // tiles -- wave w takes tiles w, w+8, .. (5 for w < 4, 4 otherwise: 9 per SIMD, 4-5
+  // independent accumulator chains per wave) -- while waves 8-15 run 512 of the VALU windows
+  // at the same time; the last 64 windows go to lanes 0-15 of waves 4-7 (one tile short).
   {
-    const int lane = tid & 63, wv = tid >> 6;
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
     int toff[7];
     float bw[7];
@@ -451,10 +492,24 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
+#if PTO_C1_ROLES
+    if (wv < 4) {
+      conv1_tasks<5, 8>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+    } else if (wv < 8) {
+      conv1_tasks<4, 8>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+      if (lane < 16) conv1_valu_window(512 + (wv - 4) * 16 + lane, img, w1s, in_s, pub, a1, idx1, b);
+    } else {
+      conv1_valu_window(tid - 512, img, w1s, in_s, pub, a1, idx1, b);
+    }
+#else
     conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
+#endif
   }
+#if PTO_C12_DEFER_W2
+  conv12_store_w2(w_s, wq, cg, tid);  // the conv2 weight slice (loaded before conv1)
+#endif
   __syncthreads();
   stamp(dbg, 2);
 
@@ -706,20 +761,64 @@ constexpr int E_NW = E_NT / 64;
 constexpr int E_NJ1 = 1600 / E_NW;  // job-1 blocks
 constexpr int E_NJ3 = 32 / E_NW;    // job-3 blocks
 
-__global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
-    const float* __restrict__ dh, const float* __restrict__ a2, const uint8_t* __restrict__ idx2,
-    const float* __restrict__ w1, const float* __restrict__ dlog, const float* __restrict__ h,
-    float* __restrict__ gw1, float* __restrict__ gb1, float* __restrict__ gw2,
-    float* __restrict__ gb2, float* __restrict__ dz2, const float* __restrict__ per_sample,
-    float* __restrict__ stats, float loss_scale, int jobs, int B, u64* dbg) {
+struct SgdHyper {
+  float lr, momentum, dampening, wd, grad_scale;
+  int nesterov, first_step;
+};
+
+// torch.optim.SGD on one element (buf = momentum*buf + (1-dampening)*d, or d on the first step)
+__device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
+  float d = gv * hy.grad_scale + hy.wd * pv;
+  if (hy.momentum != 0.f) {
+    mv = hy.first_step ? d : hy.momentum * mv + (1.f - hy.dampening) * d;
+    d = hy.nesterov ? d + hy.momentum * mv : mv;
+  }
+  pv -= hy.lr * d;
+}
+
+// Row of sample b of the batch taken at step `step` (perm required).
+__device__ __forceinline__ int batch_row_at(const BatchSrc& s, long long step, int b, int B) {
+  long long i = (step * B) % s.n_total + b;
+  if (i >= s.n_total) i -= s.n_total;
+  return s.perm[i];
+}
+
+struct Fc1Bwd {
+  const float *dh, *a2;
+  const uint8_t* idx2;
+  const float *w1, *dlog, *h;
+  float *gw1, *gb1, *gw2, *gb2, *dz2;  // gw1 / gw2 may be null with sgd (not stored)
+  const float* per_sample;
+  float* stats;
+  float loss_scale;
+  int jobs, B;
+  // fused SGD (sgd != 0): job 1 writes the UPDATED fc1.weight to w1_next -- job 2 of this
+  // launch still reads w1 -- and updates m_w1 / fc1.bias / m_b1 in place; job 3 updates
+  // fc2.weight / fc2.bias (+ momentum) in place (nothing in this launch reads them)
+  int sgd;
+  SgdHyper hy;
+  float *w1_next, *m_w1, *p_b1, *m_b1, *p_w2, *m_w2, *p_b2, *m_b2;
+  // next-batch staging (stage_x != null): ceil(B/4) extra blocks copy the uint8 pixels and
+  // labels of the batch of step cursor + stage_adv into stage_x / stage_lab and write that
+  // step number to stage_tag (conv12_fwd uses the staged batch when its tag matches)
+  BatchSrc nsrc;
+  int stage_adv;
+  uint8_t* stage_x;
+  int* stage_lab;
+  int* stage_tag;
+};
+
+__global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   __shared__ f32x4 red[E_NW][64];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, g = lane >> 4;
+  const int B = a.B;
   // jobs bit0: dW_fc1/db_fc1, bit1: dz2, bit2: dW_fc2/db_fc2/stats.  Block ids are
-  // laid out job1 | job2 | job3 with absent jobs taking no blocks.
-  const int nJ1 = (jobs & 1) ? E_NJ1 : 0;
-  const int nJ2 = (jobs & 2) ? ((B + 15) / 16) * 50 : 0;
+  // laid out job1 | job2 | job3 | staging with absent jobs taking no blocks.
+  const int nJ1 = (a.jobs & 1) ? E_NJ1 : 0;
+  const int nJ2 = (a.jobs & 2) ? ((B + 15) / 16) * 50 : 0;
+  const int nJ3 = (a.jobs & 4) ? E_NJ3 : 0;
   const int blk = blockIdx.x;
   stamp(dbg, 0);
   if (blk < nJ1) {
@@ -728,6 +827,18 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
     const int n = nt * 16 + i, f = kt * 16 + i;
     const bool nv = n < 500;
     const int nc = nv ? n : 499;
+    // SGD operands of the tile (rows nt*16 + 4g + q, column f) and of the bias (kt == 0),
+    // in flight with the GEMM loads
+    float pw[4], mw[4], pb = 0.f, mb = 0.f;
+    if (a.sgd) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const size_t e = (size_t)min(nt * 16 + g * 4 + q, 499) * 800 + f;
+        pw[q] = a.w1[e];
+        mw[q] = a.m_w1[e];
+      }
+      if (kt == 0) { pb = a.p_b1[nc]; mb = a.m_b1[nc]; }
+    }
     f32x4 c0 = zero4(), c1 = zero4();
     float dbsum = 0.f;
     for (int base = 0; base < B; base += 64) {
@@ -735,29 +846,44 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int bb = min(base + 4 * s + g, B - 1);
-        av[s] = dh[(size_t)bb * 500 + nc];
-        fv[s] = a2[(size_t)bb * 800 + f];
+        av[s] = a.dh[(size_t)bb * 500 + nc];
+        fv[s] = a.a2[(size_t)bb * 800 + f];
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const bool bv = base + 4 * s + g < B;
-        const float a = (bv && nv) ? av[s] : 0.f;
-        dbsum += a;
+        const float x = (bv && nv) ? av[s] : 0.f;
+        dbsum += x;
         const float fb = bv ? fv[s] : 0.f;
-        if (s & 1) c1 = mfma16x16x4(a, fb, c1);
-        else c0 = mfma16x16x4(a, fb, c0);
+        if (s & 1) c1 = mfma16x16x4(x, fb, c1);
+        else c0 = mfma16x16x4(x, fb, c0);
       }
     }
     const f32x4 c = c0 + c1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int nn = nt * 16 + g * 4 + r;
-      if (nn < 500) gw1[(size_t)nn * 800 + kt * 16 + i] = c[r];
+      if (nn < 500) {
+        const size_t e = (size_t)nn * 800 + kt * 16 + i;
+        if (a.gw1 != nullptr) a.gw1[e] = c[r];
+        if (a.sgd) {
+          sgd_elem(pw[r], mw[r], c[r], a.hy);
+          a.w1_next[e] = pw[r];
+          a.m_w1[e] = mw[r];
+        }
+      }
     }
     if (kt == 0) {
       dbsum += __shfl_xor(dbsum, 16, 64);
       dbsum += __shfl_xor(dbsum, 32, 64);
-      if (g == 0 && nv) gb1[n] = dbsum;
+      if (g == 0 && nv) {
+        if (a.gb1 != nullptr) a.gb1[n] = dbsum;
+        if (a.sgd) {
+          sgd_elem(pb, mb, dbsum, a.hy);
+          a.p_b1[n] = pb;
+          a.m_b1[n] = mb;
+        }
+      }
     }
   } else if (blk < nJ1 + nJ2) {
     const int t2 = blk - nJ1;
@@ -773,7 +899,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int kq = kb + 4 * q;
-      const float4 d4 = *reinterpret_cast<const float4*>(dh + (size_t)rc * 500 + min(kq, 496));
+      const float4 d4 = *reinterpret_cast<const float4*>(a.dh + (size_t)rc * 500 + min(kq, 496));
       const bool ok = rv && kq < 500;
       av[4 * q] = ok ? d4.x : 0.f;
       av[4 * q + 1] = ok ? d4.y : 0.f;
@@ -781,15 +907,15 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
       av[4 * q + 3] = ok ? d4.w : 0.f;
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) bv[s] = w1[(size_t)min(kb + s, 499) * 800 + f];
+    for (int s = 0; s < 16; ++s) bv[s] = a.w1[(size_t)min(kb + s, 499) * 800 + f];
     // epilogue operands of threads tid < 256 (ReLU mask + pool argmax), in flight with
     // the GEMM loads
     const int l = (tid & 255) >> 2, r = tid & 3;
     const int bs = mt * 16 + (l >> 4) * 4 + r;
     const int ff = kt * 16 + (l & 15);
     const size_t o = (size_t)min(bs, B - 1) * 800 + ff;
-    float a2o = a2[o];
-    int p = idx2[o];
+    float a2o = a.a2[o];
+    int p = a.idx2[o];
     f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -805,22 +931,32 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
     if (tid < 256 && bs < B) {
       const float d = a2o > 0.f ? v : 0.f;
       const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
-      float* z = dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+      float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
       z[0] = p == 0 ? d : 0.f;
       z[1] = p == 1 ? d : 0.f;
       z[8] = p == 2 ? d : 0.f;
       z[9] = p == 3 ? d : 0.f;
     }
-  } else {
+  } else if (blk < nJ1 + nJ2 + nJ3) {
     // dW_fc2[10,500] = dlogits^T . h : M = 10 (16), N = 500 (32 tiles), K = B
     const int nt = (blk - nJ1 - nJ2) * E_NW + wv;  // 0..31
     const int jc = min(i, 9);
     const int n = nt * 16 + i;
     const int ncl = min(n, 499);
     // loss statistics (wave nt == 1): the first 64 samples' values, in flight with the GEMM loads
-    const bool do_stats = nt == 1 && per_sample != nullptr && stats != nullptr;
+    const bool do_stats = nt == 1 && a.per_sample != nullptr && a.stats != nullptr;
     float ls = 0.f, cs = 0.f;
-    if (do_stats && lane < B) { ls = per_sample[2 * lane]; cs = per_sample[2 * lane + 1]; }
+    if (do_stats && lane < B) { ls = a.per_sample[2 * lane]; cs = a.per_sample[2 * lane + 1]; }
+    float pw[4], mw[4], pb = 0.f, mb = 0.f;
+    if (a.sgd) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = min(g * 4 + q, 9);
+        pw[q] = a.p_w2[j * 500 + ncl];
+        mw[q] = a.m_w2[j * 500 + ncl];
+      }
+      if (nt == 0) { pb = a.p_b2[jc]; mb = a.m_b2[jc]; }
+    }
     f32x4 c0 = zero4(), c1 = zero4();
     float dbsum = 0.f;
     for (int base = 0; base < B; base += 64) {
@@ -828,17 +964,17 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int bb = min(base + 4 * s + g, B - 1);
-        av[s] = dlog[(size_t)bb * 10 + jc];
-        hv[s] = h[(size_t)bb * 500 + ncl];
+        av[s] = a.dlog[(size_t)bb * 10 + jc];
+        hv[s] = a.h[(size_t)bb * 500 + ncl];
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const bool bv = base + 4 * s + g < B;
-        const float a = (bv && i < 10) ? av[s] : 0.f;
-        dbsum += a;
+        const float x = (bv && i < 10) ? av[s] : 0.f;
+        dbsum += x;
         const float hb = bv ? hv[s] : 0.f;
-        if (s & 1) c1 = mfma16x16x4(a, hb, c1);
-        else c0 = mfma16x16x4(a, hb, c0);
+        if (s & 1) c1 = mfma16x16x4(x, hb, c1);
+        else c0 = mfma16x16x4(x, hb, c0);
       }
     }
     const f32x4 c = c0 + c1;
@@ -846,20 +982,48 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = g * 4 + r;
-        if (j < 10) gw2[j * 500 + n] = c[r];
+        if (j < 10) {
+          if (a.gw2 != nullptr) a.gw2[j * 500 + n] = c[r];
+          if (a.sgd) {
+            sgd_elem(pw[r], mw[r], c[r], a.hy);
+            a.p_w2[j * 500 + n] = pw[r];
+            a.m_w2[j * 500 + n] = mw[r];
+          }
+        }
       }
     }
     if (nt == 0) {
       dbsum += __shfl_xor(dbsum, 16, 64);
       dbsum += __shfl_xor(dbsum, 32, 64);
-      if (g == 0 && i < 10) gb2[i] = dbsum;
+      if (g == 0 && i < 10) {
+        if (a.gb2 != nullptr) a.gb2[i] = dbsum;
+        if (a.sgd) {
+          sgd_elem(pb, mb, dbsum, a.hy);
+          a.p_b2[i] = pb;
+          a.m_b2[i] = mb;
+        }
+      }
     }
     if (do_stats) {
-      for (int bb = lane + 64; bb < B; bb += 64) { ls += per_sample[2 * bb]; cs += per_sample[2 * bb + 1]; }
+      for (int bb = lane + 64; bb < B; bb += 64) { ls += a.per_sample[2 * bb]; cs += a.per_sample[2 * bb + 1]; }
       ls = wave_sum(ls);
       cs = wave_sum(cs);
-      if (lane == 0) { stats[0] = ls * loss_scale; stats[1] = cs; }
+      if (lane == 0) { a.stats[0] = ls * a.loss_scale; a.stats[1] = cs; }
     }
+  } else {
+    // next-batch staging: samples 4 j4 .. 4 j4 + 3, 49 x 16 B of pixels each
+    const int j4 = blk - nJ1 - nJ2 - nJ3;
+    const long long step = (long long)a.nsrc.cursor[0] + a.stage_adv;
+    if (tid < 196) {
+      const int s = tid / 49, c = tid - s * 49, smp = 4 * j4 + s;
+      if (smp < B) {
+        const int row = batch_row_at(a.nsrc, step, smp, B);
+        const uint4 v = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(a.nsrc.x) + (size_t)row * 784)[c];
+        reinterpret_cast<uint4*>(a.stage_x + (size_t)smp * 784)[c] = v;
+        if (c == 0) a.stage_lab[smp] = a.nsrc.labels[row];
+      }
+    }
+    if (j4 == 0 && tid == 0) a.stage_tag[0] = (int)step;
   }
   stamp(dbg, 1);
 }
@@ -1115,20 +1279,6 @@ __global__ __launch_bounds__(H_NT) void fc1_bwd_head_kernel(
 // each element is applied in the tile's epilogue (single process: the fc gradients never
 // make an HBM round trip before their update; they are still stored for inspection).
 // ---------------------------------------------------------------------------
-struct SgdHyper {
-  float lr, momentum, dampening, wd, grad_scale;
-  int nesterov, first_step;
-};
-
-__device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
-  float d = gv * hy.grad_scale + hy.wd * pv;
-  if (hy.momentum != 0.f) {
-    mv = hy.first_step ? d : hy.momentum * mv + (1.f - hy.dampening) * d;
-    d = hy.nesterov ? d + hy.momentum * mv : mv;
-  }
-  pv -= hy.lr * d;
-}
-
 struct FcTail {
   const float *dh, *a2, *dlog, *h, *per_sample;
   float *p_w1, *m_w1, *g_w1, *p_b1, *m_b1, *g_b1;
@@ -1660,38 +1810,391 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// G: deterministic reduction of the per-sample conv-grad slabs:
-//   out[o] = sum_b P[b * stride + o],  o < n   (n, stride multiples of 4).
-//   256 threads = 64 float4 columns x 4 sample slices; each thread preloads up to
-//   16 samples (one latency round), slices meet in LDS.
+// F4: conv backward with dW_conv2 summed over 4-sample chunks (the training path).
+//   grid = (4 input-channel groups, 4 * ceil(B / 4)); block (cig, b): chunk q = b / 4,
+//   quarter r = b % 4.  The per-sample input-gradient work of sample b < B is the same as
+//   conv_bwd_kernel's (dcol = W2^T dz2[b] on MFMA, col2im + un-pool + ReLU mask -> dz1,
+//   dW_conv1 / db_conv1 / db_conv2 partials into slab row b).  dW_conv2 instead sums the
+//   chunk's FOUR samples (K = 256 positions) over one quarter of the group's 125 (ci, kh, kw)
+//   columns: the same 384 MFMAs per block as the per-sample form, written to slab row q.  The
+//   conv2.weight part of the slab the tail reduces shrinks 4x (B rows -> ceil(B/4): 6.4 -> 1.6
+//   MB at B = 64), and so does this launch's dirty write-back at its boundary.  Deterministic:
+//   every slab element has one writer, K halves and sample partials meet in a fixed order.
+//   Blocks b >= B (B % 4 != 0) only compute their quarter of the last chunk.
 // ---------------------------------------------------------------------------
+constexpr int G_DZS = 82;             // dz row stride (== 18 mod 32: 2a reads 2-way on 2 banks, 2b free)
+constexpr int G_DZR = 52;             // rows per sample: 50 co + 2 zero rows (2a's K padding to 52)
+constexpr int G_DZN = G_DZR * G_DZS;  // 4264 floats per sample
+constexpr int G_A1S = 2 * F_A1C;      // 2b im2col source per sample: the (at most) 2 channels touched
+constexpr int G_OFF_DZ = 0;
+constexpr int G_OFF_W = G_OFF_DZ + 4 * G_DZN;
+constexpr int G_OFF_DCOL = G_OFF_W + 52 * F_WS;
+constexpr int G_OFF_A1 = G_OFF_DCOL + 128 * F_DC;
+constexpr int G_OFF_A1C = G_OFF_A1 + 4 * F_A1C + 12 * F_A1R;
+constexpr int G_OFF_X = G_OFF_A1C + 4 * G_A1S;
+constexpr int G_OFF_IDX = G_OFF_X + 28 * F_XR;
+constexpr int G_OFF_PK = G_OFF_IDX + 180;     // 2b K-half-1 partial tiles: 6 x 64 lanes x f32x4
+constexpr int G_OFF_PV = G_OFF_PK + 6 * 256;  // co 48/49 per-sample partials: 4 x 64
+constexpr int G_LDS = G_OFF_PV + 4 * 64;
+constexpr int G_OFF_DZ1 = G_OFF_W;            // aliases of the W2 slice (dead after phase 2a)
+constexpr int G_OFF_RED = G_OFF_W + 5 * F_Z1;
+static_assert(G_LDS * 4 <= 160 * 1024, "conv_bwd4 LDS budget");
+static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
+
+__global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
+    const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
+    int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, u64* dbg) {
+  extern __shared__ float lds[];
+  float* dzc_s = lds + G_OFF_DZ;
+  float* w_s = lds + G_OFF_W;
+  float* dcol_s = lds + G_OFF_DCOL;
+  float* a1_s = lds + G_OFF_A1;
+  float* a1c_s = lds + G_OFF_A1C;
+  float* x_s = lds + G_OFF_X;
+  uint8_t* idx_s = reinterpret_cast<uint8_t*>(lds + G_OFF_IDX);
+  f32x4* pk_s = reinterpret_cast<f32x4*>(lds + G_OFF_PK);
+  float* pv_s = lds + G_OFF_PV;
+  float* dz1_s = lds + G_OFF_DZ1;
+  float* red = lds + G_OFF_RED;
+
+  const int cig = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int q = b >> 2, r = b & 3;
+  const bool own = b < B;  // block-uniform: this block also does sample b's input-gradient work
+  const int bo = own ? b : B - 1;
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  // dW_conv2 columns of this block: j in [32r - cig, 32r - cig + 32) of the group's 125; the
+  // -cig shift puts every whole 4-column group on a 16-byte slab boundary (epilogue float4s)
+  const int jbase = 32 * r - cig;
+  const int c0 = max(jbase, 0) / 25;  // first of the <= 2 input channels those columns touch
+  stamp(dbg, 0);
+
+  // ---- phase 1: stage.  Group 1 (what 2a needs: the own sample's dz2 and the W2 slice) is
+  // loaded first and written to LDS before the first barrier; group 2 (the chunk's other
+  // three samples, the 2b im2col source, and the own a1 / idx1 / xn for phases 3-4) stays in
+  // flight through phase 2a and lands before the second barrier.  Every load independent and
+  // unpredicated (clamped addresses + selects).
+  float4 dv2[3];
+  float cv[2], av1;
+  uint8_t iv1;
+  float xv1;
+  {
+    const float4 dv1 = reinterpret_cast<const float4*>(dz2 + (size_t)bo * 3200)[min(tid, 799)];
+    float wv_[F_NW2];
+#pragma unroll
+    for (int k = 0; k < F_NW2; ++k) {
+      const int e = tid + k * F_NT;
+      const int co = min(e >> 7, 49), j = min(e & 127, 124);
+      wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
+    }
+    // group 2 (issued after group 1: waiting for group 1 leaves these in flight)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = min(tid + k * F_NT, 2399);
+      const int o = e / 800, s = o < r ? o : o + 1;  // the chunk's other samples
+      dv2[k] = reinterpret_cast<const float4*>(dz2 + (size_t)min(4 * q + s, B - 1) * 3200)[e - o * 800];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = min(tid + k * F_NT, 1151);
+      const int s = e / 288, rem = e - s * 288, c = rem / 144, p = rem - c * 144;
+      cv[k] = a1[(size_t)min(4 * q + s, B - 1) * 2880 + (cig * 5 + c0 + c) * 144 + p];
+    }
+    const int ec = min(tid, 719);
+    av1 = a1[(size_t)bo * 2880 + cig * 720 + ec];
+    iv1 = idx1[(size_t)bo * 2880 + cig * 720 + ec];
+    xv1 = xn[(size_t)bo * 784 + min(tid, 783)];
+    // group 1 -> LDS
+    if (tid < 800) {
+      const int co = tid >> 4, c4 = tid & 15;
+      const float4 v = own ? dv1 : make_float4(0.f, 0.f, 0.f, 0.f);
+      float2* d = reinterpret_cast<float2*>(dzc_s + r * G_DZN + co * G_DZS + 4 * c4);
+      d[0] = make_float2(v.x, v.y);
+      d[1] = make_float2(v.z, v.w);
+    }
+    if (tid < 512) {  // zero rows 50, 51 of every sample (2a reads co up to 51)
+      const int s = tid >> 7, rr = 50 + ((tid >> 6) & 1);
+      dzc_s[s * G_DZN + rr * G_DZS + (tid & 63)] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < F_NW2; ++k) {
+      const int e = tid + k * F_NT;
+      if (e < 6656) w_s[(e >> 7) * F_WS + (e & 127)] = ((e >> 7) >= 50 || (e & 127) >= 125) ? 0.f : wv_[k];
+    }
+  }
+  // group 2 -> LDS (samples >= B of the chunk read as 0)
+  auto stage_g2 = [&]() {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + k * F_NT;
+      if (e < 2400) {
+        const int o = e / 800, s = o < r ? o : o + 1, rem = e - o * 800, co = rem >> 4, c4 = rem & 15;
+        const float4 v = 4 * q + s < B ? dv2[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float2* d = reinterpret_cast<float2*>(dzc_s + s * G_DZN + co * G_DZS + 4 * c4);
+        d[0] = make_float2(v.x, v.y);
+        d[1] = make_float2(v.z, v.w);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = tid + k * F_NT;
+      if (e < 1152) {
+        const int s = e / 288, rem = e - s * 288, c = rem / 144, p = rem - c * 144, y = p / 12;
+        a1c_s[s * G_A1S + c * F_A1C + y * F_A1R + (p - y * 12)] = 4 * q + s < B ? cv[k] : 0.f;
+      }
+    }
+    if (tid < 720) {
+      const int c = tid / 144, pp = tid - c * 144, yy = pp / 12;
+      a1_s[c * F_A1C + yy * F_A1R + (pp - yy * 12)] = av1;
+      idx_s[tid] = iv1;
+    }
+    if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv1;
+  };
+#if !PTO_B4_SPLIT
+  stage_g2();
+#endif
+  __syncthreads();
+  stamp(dbg, 1);
+
+  // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
+  if (own) {
+    const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
+    const float* dzo = dzc_s + r * G_DZN;
+    f32x4 acc[F_TPW];
+#pragma unroll
+    for (int n = 0; n < F_TPW; ++n) acc[n] = zero4();
+    float bv[13], av[F_TPW][13];
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      bv[s] = dzo[(4 * s + g) * G_DZS + pt * 16 + i];
+#pragma unroll
+      for (int n = 0; n < F_TPW; ++n) av[n][s] = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 13; ++s)
+#pragma unroll
+      for (int n = 0; n < F_TPW; ++n) acc[n] = mfma16x16x4(av[n][s], bv[s], acc[n]);
+#pragma unroll
+    for (int n = 0; n < F_TPW; ++n)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        dcol_s[((jt0 + n) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[n][rr];
+  }
+#if PTO_B4_SPLIT
+  stage_g2();  // phase 1b: group 2 -> LDS (landed during 2a)
+#endif
+  __syncthreads();
+  // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
+  //   waves 0-11: tile pair tp = wv % 6 (co tile ct = tp / 2 of 0..47, column tile jt = tp % 2),
+  //   K half wv / 6 (samples {0,1} or {2,3}); A = im2col (rows = columns jl), B = dz (cols = co).
+  //   waves 12-15: co 48 and 49 (a fourth 16-row tile would be 7/8 padding) as 256 VALU dot
+  //   products, one sample each, summed in sample order after the barrier.
+  f32x4 gacc = zero4();
+  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
+  if (wv < 12) {
+    const int kh2 = wv / 6;
+    const int jc = min(max(jbase + jt * 16 + i, 0), 124);  // clamped (unstored columns read finite data)
+    const int ci = jc / 25, t = jc - ci * 25;
+    const float* ab = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
+    const float* bb = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
+    float av[32], bv[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {  // k-step u: sample 2 kh2 + u / 16, position 4 (u % 16) + g
+      const int s = u >> 4, uu = u & 15;
+      av[u] = ab[s * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];
+      bv[u] = bb[s * G_DZN + 4 * uu];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 e0 = zero4(), e1 = zero4();
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      if (u & 1) e1 = mfma16x16x4(av[u], bv[u], e1);
+      else e0 = mfma16x16x4(av[u], bv[u], e0);
+    }
+    gacc = e0 + e1;
+    if (kh2 == 1) pk_s[tp * 64 + lane] = gacc;
+  } else {
+    const int item = tid - 768;  // (sample s, co 48 + cr, column jl)
+    const int s = item >> 6, cr = (item >> 5) & 1, jl = item & 31;
+    const int jc = min(max(jbase + jl, 0), 124);
+    const int ci = jc / 25, t = jc - ci * 25;
+    const float* ar = a1c_s + s * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5);
+    const float* dr = dzc_s + s * G_DZN + (48 + cr) * G_DZS;
+    float accv = 0.f;
+#pragma unroll 16
+    for (int pos = 0; pos < 64; ++pos) accv = fmaf(dr[pos], ar[(pos >> 3) * F_A1R + (pos & 7)], accv);
+    pv_s[item] = accv;
+  }
+  float b2sum = 0.f;
+  if (own && cig == 0 && tid < 50) {
+    const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
+#pragma unroll 8
+    for (int p = 0; p < 64; ++p) b2sum += dzo[p];
+  }
+  __syncthreads();
+  stamp(dbg, 2);
+  {
+    float* rowq = slab + (size_t)q * stride + o_gw2 + cig * 125;
+    if (wv < 6) {
+      gacc += pk_s[tp * 64 + lane];  // K half 0 + K half 1
+      // lane (i, g) holds co = 16 ct + i, columns jbase + 16 jt + 4 g + [0, 4)
+      float* rp = rowq + (ct * 16 + i) * 500;
+      const int j0 = jbase + jt * 16 + 4 * g;
+      if (j0 >= 0 && j0 + 3 < 125) {
+        *reinterpret_cast<float4*>(rp + j0) = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
+      }
+    } else if (wv == 12) {
+      const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
+      const int j = jbase + (lane & 31);
+      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
+    }
+  }
+  if (!own) return;  // block-uniform: padding blocks of the last chunk are done
+
+  // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
+  if (tid < 720) {
+    const int c = tid / 144, p = tid - c * 144;
+    const int y = p / 12, x = p - y * 12;
+    const float* base = dcol_s + c * 25 * F_DC + y * 8 + x;
+    bool colok[5];
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) colok[kw] = (x - kw >= 0) & (x - kw <= 7);
+    float da = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      float dr = 0.f;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const float v = base[kh * (5 * F_DC - 8) + kw * (F_DC - 1)];
+        dr += colok[kw] ? v : 0.f;
+      }
+      da += ((y - kh >= 0) & (y - kh <= 7)) ? dr : 0.f;
+    }
+    const float d = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
+    const int pidx = idx_s[tid];
+    float* z = dz1_s + c * F_Z1 + (2 * y) * F_Z1R + 2 * x;
+    z[0] = pidx == 0 ? d : 0.f;
+    z[1] = pidx == 1 ? d : 0.f;
+    z[F_Z1R] = pidx == 2 ? d : 0.f;
+    z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
+  }
+  __syncthreads();
+  stamp(dbg, 3);
+  // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU (as conv_bwd_kernel)
+  if (tid < 400) {
+    const int c = tid / 80, rem = tid - c * 80;
+    const int part = rem / 5, kh = rem - part * 5;
+    const int ry = part & 7, cx = (part >> 3) * 12;
+    const float* zr = dz1_s + c * F_Z1;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float bs = 0.f;
+#pragma unroll
+    for (int yy = 0; yy < 3; ++yy) {
+      const int y = ry * 3 + yy;
+      const float* xr = x_s + (y + kh) * F_XR + cx;
+      float xw[16];
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) xw[qq] = xr[qq];
+#pragma unroll
+      for (int x = 0; x < 12; ++x) {
+        const float a = zr[y * F_Z1R + cx + x];
+        bs += a;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
+      }
+    }
+    float* pr = red + part * F_RED1;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
+    if (kh == 0) pr[125 + c] = bs;
+  }
+  __syncthreads();
+  stamp(dbg, 4);
+  // ---- epilogue: sample b's small partials into slab row b
+  float* rowb = slab + (size_t)b * stride;
+  if (tid < 130) {
+    float w1sum = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < 16; ++qq) w1sum += red[qq * F_RED1 + tid];
+    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
+    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
+  }
+  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
+  stamp(dbg, 5);
+}
+
+// ---------------------------------------------------------------------------
+// G: deterministic reduction of the conv-grad slabs:
+//   out[c] = sum_{row < rows(c)} P[row * stride + c],  rows(c) = rows_big for the float4
+//   columns [big_lo4, big_hi4) (conv2.weight: one row per 4-sample chunk, conv_bwd4_kernel)
+//   and B elsewhere (the per-sample conv1 / bias partials).  Rows are summed in a fixed
+//   order (slices of consecutive rows, then the slices in order): bit-reproducible.
+// ---------------------------------------------------------------------------
+// Slab reduction geometry: SR_COLS float4 columns per workgroup x SR_SL row slices, SR_CH
+// loads in flight per thread.  32 columns (200 reduction workgroups at B = 64, 32 KB each)
+// beat 64 (100 x 64 KB): 0.25 us off the load phase.
+constexpr int SR_COLS = 32;
+constexpr int SR_CH = 8;
+constexpr int SR_SL = 256 / SR_COLS;
+
+__device__ __forceinline__ void add4(float4& a, const float4& v) {
+  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+}
+
+// Rows [slice * per, min(rows, (slice + 1) * per)) of float4 column cc summed in row order,
+// per = ceil(rows / nsl).  Every load is issued before the first add (clamped addresses).
+__device__ __forceinline__ float4 slab_col_sum(const float4* __restrict__ P4, long s4, int cc, int rows,
+                                               int slice, int nsl) {
+  const int per = (rows + nsl - 1) / nsl;
+  const int b0 = slice * per, b1 = min(rows, b0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (per <= 2) {  // chunked conv2.weight rows: 16 rows / 8 slices at B = 64
+    const float4 v0 = P4[(size_t)min(b0, rows - 1) * s4 + cc];
+    const float4 v1 = P4[(size_t)min(b0 + 1, rows - 1) * s4 + cc];
+    if (b0 < b1) add4(acc, v0);
+    if (b0 + 1 < b1) add4(acc, v1);
+    return acc;
+  }
+  for (int base = b0; base < b1; base += SR_CH) {
+    float4 v[SR_CH];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, rows - 1) * s4 + cc];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k)
+      if (base + k < b1) add4(acc, v[k]);
+  }
+  return acc;
+}
+
+struct SlabRows {
+  int rows;      // rows of every column outside [big_lo4, big_hi4)
+  int rows_big;  // rows of the columns inside
+  int big_lo4, big_hi4;
+  __device__ __forceinline__ int of(int c4) const { return (c4 >= big_lo4 && c4 < big_hi4) ? rows_big : rows; }
+};
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(
-    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ out, u64* dbg) {
-  __shared__ float4 red[4][64];
+    const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ out, u64* dbg) {
+  __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
-  const int col = blockIdx.x * 64 + (tid & 63);
-  const int slice = tid >> 6;
-  const int n4 = n >> 2, s4 = stride >> 2;
+  const int col = blockIdx.x * SR_COLS + (tid % SR_COLS);
+  const int slice = tid / SR_COLS;
+  const int n4 = n >> 2;
   const int cc = min(col, n4 - 1);
-  const float4* P4 = reinterpret_cast<const float4*>(P);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int per = (B + 3) / 4;  // samples per slice
-  const int b0 = slice * per, b1 = min(B, b0 + per);
-  for (int base = b0; base < b1; base += 16) {
-    float4 v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
-  }
-  red[slice][tid & 63] = acc;
+  red[slice][tid % SR_COLS] = slab_col_sum(reinterpret_cast<const float4*>(P), stride >> 2, cc, sr.of(cc),
+                                           slice, SR_SL);
   __syncthreads();
-  if (tid < 64 && col < n4) {
+  if (tid < SR_COLS && col < n4) {
     float4 r = red[0][tid];
 #pragma unroll
-    for (int q = 1; q < 4; ++q) { r.x += red[q][tid].x; r.y += red[q][tid].y; r.z += red[q][tid].z; r.w += red[q][tid].w; }
+    for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
     reinterpret_cast<float4*>(out)[col] = r;
   }
   stamp(dbg, 1);
@@ -1701,24 +2204,32 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(
 // G+H: slab reduction fused with the SGD(momentum) update of the same elements
 //   (single-process path: the conv grads never make a round trip before the
 //   update).  Also writes the reduced grads (inspection / grad-norm logging) and
-//   advances the device batch cursor.
+//   advances the device batch cursor.  Blocks past the reduction: plain SGD over a
+//   second, already-reduced range (p2/g2/buf2), then a float4 copy cp_src -> cp_dst (the
+//   fused-SGD schedule: fc1_bwd wrote the updated fc1.weight to a scratch buffer because
+//   its own dz2 job still reads fc1.weight; nothing reads it after fc1_bwd).
 // ---------------------------------------------------------------------------
-// Slab reduction geometry: SR_COLS float4 columns per workgroup x SR_SL row slices of
-// ceil(B / SR_SL) rows, SR_CH loads in flight per thread.  32 columns (200 reduction
-// workgroups at B = 64, 32 KB each) beat 64 (100 x 64 KB): 0.25 us off the load phase.
-constexpr int SR_COLS = 32;
-constexpr int SR_CH = 8;
-constexpr int SR_SL = 256 / SR_COLS;
-
+constexpr int SR_CP = 2;  // float4s per thread of the copy blocks
 __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
-    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ gout,
+    const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ gout,
     float* __restrict__ p, float* __restrict__ buf, float lr, float momentum, float dampening,
     float wd, float grad_scale, int nesterov, int first_step, int* __restrict__ step_counter,
     float* __restrict__ p2, const float* __restrict__ g2, float* __restrict__ buf2, int n2,
-    int red_blocks, u64* dbg) {
+    int red_blocks, const float4* __restrict__ cp_src, float4* __restrict__ cp_dst, int cp_n4, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
+  const int sgd_blocks = (n2 / 4 + 255) / 256;
+  if ((int)blockIdx.x >= red_blocks + sgd_blocks) {
+    const int v0 = (blockIdx.x - red_blocks - sgd_blocks) * 256 * SR_CP + tid;
+    float4 v[SR_CP];
+#pragma unroll
+    for (int k = 0; k < SR_CP; ++k) v[k] = cp_src[min(v0 + k * 256, cp_n4 - 1)];
+#pragma unroll
+    for (int k = 0; k < SR_CP; ++k)
+      if (v0 + k * 256 < cp_n4) cp_dst[v0 + k * 256] = v[k];
+    return;
+  }
   if ((int)blockIdx.x >= red_blocks) {
     // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
     const int v = (blockIdx.x - red_blocks) * 256 + tid;
@@ -1743,31 +2254,20 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
   }
   const int col = blockIdx.x * SR_COLS + (tid % SR_COLS);
   const int slice = tid / SR_COLS;
-  const int n4 = n >> 2, s4 = stride >> 2;
+  const int n4 = n >> 2;
   const int cc = min(col, n4 - 1);
-  const float4* P4 = reinterpret_cast<const float4*>(P);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int per = (B + SR_SL - 1) / SR_SL;
-  const int b0 = slice * per, b1 = min(B, b0 + per);
   float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bb = pp;
   if (tid < SR_COLS) {  // prefetch the parameters + momentum this column updates
     pp = reinterpret_cast<const float4*>(p)[cc];
     bb = reinterpret_cast<const float4*>(buf)[cc];
   }
-  for (int base = b0; base < b1; base += SR_CH) {
-    float4 v[SR_CH];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k)
-      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
-  }
-  red[slice][tid % SR_COLS] = acc;
+  red[slice][tid % SR_COLS] = slab_col_sum(reinterpret_cast<const float4*>(P), stride >> 2, cc, sr.of(cc),
+                                           slice, SR_SL);
   __syncthreads();
   if (tid < SR_COLS && col < n4) {
     float4 r = red[0][tid];
 #pragma unroll
-    for (int q = 1; q < SR_SL; ++q) { r.x += red[q][tid].x; r.y += red[q][tid].y; r.z += red[q][tid].z; r.w += red[q][tid].w; }
+    for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
     if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
     float* pe = &pp.x; float* be = &bb.x; const float* ge = &r.x;
 #pragma unroll
@@ -1804,7 +2304,7 @@ constexpr int T_NJ1 = 1600 / T_NW;  // dW_fc1 tiles (32 n-tiles x 50 f-tiles)
 constexpr int T_NJ3 = 32 / T_NW;    // dW_fc2 tiles (32 n-tiles)
 
 __global__ __launch_bounds__(256) void tail_sgd_kernel(
-    const float* __restrict__ P, int B, int n, int stride, float* __restrict__ gout,
+    const float* __restrict__ P, int B, SlabRows sr, int n, int stride, float* __restrict__ gout,
     float* __restrict__ p, float* __restrict__ buf, SgdHyper hy, FcTail fc,
     int* __restrict__ step_counter, int red_blocks, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
@@ -1945,26 +2445,15 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
   // slab reduction + SGD of the conv params (see slab_reduce_sgd_kernel)
   const int col = blk * SR_COLS + (tid % SR_COLS);
   const int slice = tid / SR_COLS;
-  const int n4 = n >> 2, s4 = stride >> 2;
+  const int n4 = n >> 2;
   const int cc = min(col, n4 - 1);
-  const float4* P4 = reinterpret_cast<const float4*>(P);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int per = (B + SR_SL - 1) / SR_SL;
-  const int b0 = slice * per, b1 = min(B, b0 + per);
   float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bq = pp;
   if (tid < SR_COLS) {
     pp = reinterpret_cast<const float4*>(p)[cc];
     bq = reinterpret_cast<const float4*>(buf)[cc];
   }
-  for (int base = b0; base < b1; base += SR_CH) {
-    float4 v[SR_CH];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, B - 1) * s4 + cc];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k)
-      if (base + k < b1) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
-  }
-  red[slice][tid % SR_COLS] = acc;
+  red[slice][tid % SR_COLS] = slab_col_sum(reinterpret_cast<const float4*>(P), stride >> 2, cc, sr.of(cc),
+                                           slice, SR_SL);
   __syncthreads();
   if (tid < SR_COLS && col < n4) {
     float4 rr = red[0][tid];
@@ -2116,14 +2605,19 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
                          const int* cursor, int host_offset, int n_total, float scale,
                          float shift, const float* w1, const float* b1, const float* w2,
                          const float* b2, float* a1, uint8_t* idx1, float* xn_out, int* lab_out,
-                         float* a2, uint8_t* idx2, int B, void* stream) {
+                         float* a2, uint8_t* idx2, int B, const uint8_t* stg_x, const int* stg_lab,
+                         const int* stg_tag, void* stream) {
   PTO_CHECK_B(B);
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
   if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 1)) return -2;
+  // staged batches exist only for uint8 sources walked by a device cursor
+  if (stg_x != nullptr && (stg_lab == nullptr || stg_tag == nullptr || cursor == nullptr || perm == nullptr ||
+                           !is_u8 || labels == nullptr))
+    return -1;
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
   hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
-                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, g_dbg);
+                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, stg_x, stg_lab, stg_tag, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -2166,18 +2660,107 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
   return (int)hipGetLastError();
 }
 
+static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
+  const int B = a.B;
+  PTO_CHECK_B(B);
+  if (a.jobs <= 0 || a.jobs > 7) return -1;
+  if (((uintptr_t)a.dh) & 15) return -2;  // float4 dh rows (job 2)
+  if (a.sgd && (a.w1_next == nullptr || a.m_w1 == nullptr || a.p_b1 == nullptr || a.m_b1 == nullptr ||
+                a.p_w2 == nullptr || a.m_w2 == nullptr || a.p_b2 == nullptr || a.m_b2 == nullptr ||
+                a.w1_next == a.w1))
+    return -1;
+  int nst = 0;
+  if (a.stage_x != nullptr) {
+    if (a.nsrc.perm == nullptr || a.nsrc.cursor == nullptr || a.nsrc.labels == nullptr || !a.nsrc.is_u8 ||
+        a.stage_lab == nullptr || a.stage_tag == nullptr || a.nsrc.n_total <= 0 ||
+        ((((uintptr_t)a.nsrc.x) | ((uintptr_t)a.stage_x)) & 15))
+      return -1;
+    nst = (B + 3) / 4;
+  }
+  const int blocks = ((a.jobs & 1) ? E_NJ1 : 0) + ((a.jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
+                     ((a.jobs & 4) ? E_NJ3 : 0) + nst;
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, a, g_dbg);
+  return (int)hipGetLastError();
+}
+
 int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                       const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                       float* gb2, float* dz2, const float* per_sample, float* stats,
                       float loss_scale, int jobs, int B, void* stream) {
+  Fc1Bwd a{};
+  a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
+  a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
+  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = jobs; a.B = B;
+  if (gw1 == nullptr || gb1 == nullptr || gw2 == nullptr || gb2 == nullptr) return -1;
+  return fc1_bwd_launch(a, stream);
+}
+
+// fc1_bwd with the fc parameters' SGD fused into the weight-gradient jobs (the updated
+// fc1.weight goes to w1_next; the tail copies it back) and the next batch staged.
+// Gradient pointers may be null (not stored).  stage_x null: no staging.
+int pto_mnist_fc1_bwd_sgd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
+                          const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
+                          float* gb2, float* dz2, const float* per_sample, float* stats, float loss_scale,
+                          int B, float* w1_next, float* m_w1, float* p_b1, float* m_b1, float* p_w2,
+                          float* m_w2, float* p_b2, float* m_b2, float lr, float momentum, float dampening,
+                          float wd, float grad_scale, int nesterov, int first_step, const void* nx,
+                          const int* nlabels, const int* nperm, const int* ncursor, int n_total,
+                          int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
+  Fc1Bwd a{};
+  a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
+  a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
+  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
+  a.sgd = 1;
+  a.hy = SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  a.w1_next = w1_next; a.m_w1 = m_w1; a.p_b1 = p_b1; a.m_b1 = m_b1;
+  a.p_w2 = p_w2; a.m_w2 = m_w2; a.p_b2 = p_b2; a.m_b2 = m_b2;
+  if (stage_x != nullptr) {
+    a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
+    a.stage_adv = stage_adv;
+    a.stage_x = stage_x;
+    a.stage_lab = stage_lab;
+    a.stage_tag = stage_tag;
+  }
+  return fc1_bwd_launch(a, stream);
+}
+
+// fc1_bwd (gradients only, every job) + next-batch staging blocks.
+int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
+                            const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
+                            float* gb2, float* dz2, const float* per_sample, float* stats,
+                            float loss_scale, int B, const void* nx, const int* nlabels, const int* nperm,
+                            const int* ncursor, int n_total, int stage_adv, uint8_t* stage_x, int* stage_lab,
+                            int* stage_tag, void* stream) {
+  Fc1Bwd a{};
+  a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
+  a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
+  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
+  if (gw1 == nullptr || gb1 == nullptr || gw2 == nullptr || gb2 == nullptr || stage_x == nullptr) return -1;
+  a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
+  a.stage_adv = stage_adv;
+  a.stage_x = stage_x;
+  a.stage_lab = stage_lab;
+  a.stage_tag = stage_tag;
+  return fc1_bwd_launch(a, stream);
+}
+
+// Stage the batch of step cursor[0] + adv (uint8 pixels + labels + tag) on its own (first
+// step of a staged schedule, or after anything moved the cursor).
+int pto_mnist_stage_batch(const void* x, const int* labels, const int* perm, const int* cursor, int n_total,
+                          int B, int adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
+  Fc1Bwd a{};
+  a.B = B;
+  a.jobs = 0;
+  a.nsrc = make_src(x, 1, labels, perm, cursor, 0, n_total, 1.f, 0.f);
+  a.stage_adv = adv;
+  a.stage_x = stage_x;
+  a.stage_lab = stage_lab;
+  a.stage_tag = stage_tag;
   PTO_CHECK_B(B);
-  if (jobs <= 0 || jobs > 7) return -1;
-  if (((uintptr_t)dh) & 15) return -2;  // float4 dh rows (job 2)
-  const int blocks = ((jobs & 1) ? E_NJ1 : 0) + ((jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
-                     ((jobs & 4) ? E_NJ3 : 0);
-  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, dh, a2,
-                     idx2, w1, dlog, h, gw1, gb1, gw2, gb2, dz2, per_sample, stats, loss_scale,
-                     jobs, B, g_dbg);
+  if (perm == nullptr || cursor == nullptr || labels == nullptr || stage_x == nullptr || stage_lab == nullptr ||
+      stage_tag == nullptr || n_total <= 0 || ((((uintptr_t)x) | ((uintptr_t)stage_x)) & 15))
+    return -1;
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3((B + 3) / 4), dim3(E_NT), 0, (hipStream_t)stream, a, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -2219,12 +2802,24 @@ int pto_mnist_conv_bwd_fc(const float* dz2, const float* w2, const float* a1, co
   return conv_bwd_launch(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, nullptr, slab_stride, B, fc, stream);
 }
 
-int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, void* stream) {
+// Conv-grad slab reduction.  rows_big / [big_lo, big_hi) (floats, multiples of 4): the
+// columns summed over rows_big rows (conv_bwd4's chunk rows); every other column over B.
+static bool slab_rows_ok(int B, int n, int rows_big, int big_lo, int big_hi, SlabRows& sr) {
+  if (rows_big <= 0 || rows_big > B || big_lo < 0 || big_hi < big_lo || big_hi > n || (big_lo & 3) || (big_hi & 3))
+    return false;
+  sr = SlabRows{B, rows_big, big_lo >> 2, big_hi >> 2};
+  return true;
+}
+
+int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, int rows_big, int big_lo,
+                    int big_hi, void* stream) {
   PTO_CHECK_B(B);
   if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
   if ((((uintptr_t)P) | ((uintptr_t)out)) & 15) return -2;
-  const int blocks = (n / 4 + 63) / 64;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P, B, n,
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
+  const int blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P, sr, n,
                      stride, out, g_dbg);
   return (int)hipGetLastError();
 }
@@ -2246,7 +2841,8 @@ int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, flo
 int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, float* p,
                         float* buf, float lr, float momentum, float dampening, float wd,
                         float grad_scale, int nesterov, int first_step, int* step_counter,
-                        float* p2, const float* g2, float* buf2, int n2, void* stream) {
+                        float* p2, const float* g2, float* buf2, int n2, int rows_big, int big_lo,
+                        int big_hi, const float* cp_src, float* cp_dst, int cp_n, void* stream) {
   PTO_CHECK_B(B);
   if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
   if (n2 < 0 || (n2 & 3) || (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)))
@@ -2254,11 +2850,46 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
   if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) |
        ((uintptr_t)p2) | ((uintptr_t)g2) | ((uintptr_t)buf2)) & 15)
     return -2;
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
+  if (cp_n < 0 || (cp_n & 3) || (cp_n > 0 && (cp_src == nullptr || cp_dst == nullptr)) ||
+      ((((uintptr_t)cp_src) | ((uintptr_t)cp_dst)) & 15))
+    return -1;
   const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
-  const int blocks = red_blocks + (n2 / 4 + 255) / 256;
+  const int cp_n4 = cp_n / 4;
+  const int blocks = red_blocks + (n2 / 4 + 255) / 256 + (cp_n4 + 256 * SR_CP - 1) / (256 * SR_CP);
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
-                     B, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
-                     nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks, g_dbg);
+                     sr, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
+                     nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks,
+                     reinterpret_cast<const float4*>(cp_src), reinterpret_cast<float4*>(cp_dst), cp_n4, g_dbg);
+  return (int)hipGetLastError();
+}
+
+// conv backward, dW_conv2 over 4-sample chunks (conv_bwd4_kernel): slab rows 0..ceil(B/4)-1
+// get the chunk partials of conv2.weight at row offset o_gw2; rows 0..B-1 the per-sample
+// conv1.weight / conv1.bias / conv2.bias partials at o_gw1 / o_gb1 / o_gb2.
+int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                        const float* xn, float* slab, int stride, int o_gw2, int o_gb2, int o_gw1,
+                        int o_gb1, int B, void* stream) {
+  PTO_CHECK_B(B);
+  if (4 * ((B + 3) / 4) > 65535) return -1;  // grid y
+  if ((stride & 3) || (o_gw2 & 3) || (((uintptr_t)slab) & 15) || (((uintptr_t)dz2) & 15)) return -2;
+  if (o_gw2 < 0 || o_gb2 < 0 || o_gw1 < 0 || o_gb1 < 0 || o_gw2 + 25000 > stride || o_gb2 + 50 > stride ||
+      o_gw1 + 500 > stride || o_gb1 + 20 > stride)
+    return -1;
+  static std::atomic<unsigned> attr_set{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
+  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
+    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd4_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             G_LDS * (int)sizeof(float));
+    if (e != hipSuccess) return (int)e;
+    attr_set.fetch_or(1u << dev, std::memory_order_release);
+  }
+  const int nb = 4 * ((B + 3) / 4);
+  hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
+                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -2282,7 +2913,8 @@ int pto_mnist_fc1_bwd_head(const float* hp, const float* b1, const float* w2, co
 
 // Single-process step tail: conv slab reduction + SGD, dW_fc1 / dW_fc2 (+ biases) with
 // fused SGD, loss statistics, batch-cursor advance -- one launch.
-int pto_mnist_tail_sgd(const float* P, int B, int n, int stride, float* gout, float* p, float* buf,
+int pto_mnist_tail_sgd(const float* P, int B, int n, int stride, int rows_big, int big_lo, int big_hi,
+                       float* gout, float* p, float* buf,
                        float lr, float momentum, float dampening, float wd, float grad_scale,
                        int nesterov, int first_step, int* step_counter, const float* dh,
                        const float* a2, const float* dlog, const float* h, const float* per_sample,
@@ -2301,9 +2933,11 @@ int pto_mnist_tail_sgd(const float* P, int B, int n, int stride, float* gout, fl
   SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
   FcTail fc{dh, a2, dlog, h, per_sample, p_w1, m_w1, g_w1, p_b1, m_b1, g_b1,
             p_w2, m_w2, g_w2, p_b2, m_b2, g_b2, stats, loss_scale};
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
   const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
   hipLaunchKernelGGL(tail_sgd_kernel, dim3(red_blocks + T_NJ1 + T_NJ3), dim3(256), 0,
-                     (hipStream_t)stream, P, B, n, stride, gout, p, buf, hy, fc, step_counter,
+                     (hipStream_t)stream, P, B, sr, n, stride, gout, p, buf, hy, fc, step_counter,
                      red_blocks, g_dbg);
   return (int)hipGetLastError();
 }

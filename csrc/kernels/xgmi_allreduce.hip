@@ -70,9 +70,11 @@ struct XarArgs {
   int* step_counter;     // optional: advanced once per launch (the trainer's batch cursor)
   // optional fused slab reduction: the first conv4 f4s of the gradient are
   // sum_{r < slab_rows} slab[r * slab_stride + .] (the conv backward's per-sample partials)
+  // (conv_bwd4: the columns [big_lo4, big_hi4) hold one row per 4-sample chunk and are
+  // summed over slab_rows_big rows)
   const float* slab;
-  int slab_rows;
-  long slab_stride, conv4;
+  int slab_rows, slab_rows_big;
+  long slab_stride, conv4, big_lo4, big_hi4;
   int* err;
   long long timeout_ticks;  // wall_clock64 ticks (100 MHz)
   unsigned long long* stamps;  // optional: 4 wall_clock64 stamps per (rank, block)
@@ -256,12 +258,13 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       nsplit = nsplit < 1 ? 1 : (nsplit > 8 ? 8 : nsplit);
       const int grp = tid / per_c, ci = tid - grp * per_c;
       const long col = (long)b * per_c + ci;
-      const int rows_per = (a.slab_rows + nsplit - 1) / nsplit;
+      const int rows = (col >= a.big_lo4 && col < a.big_hi4) ? a.slab_rows_big : a.slab_rows;
+      const int rows_per = (rows + nsplit - 1) / nsplit;
       f4 acc = zero4;
       if (grp < nsplit && col < c4) {
         const f4* sp = reinterpret_cast<const f4*>(a.slab) + col;
         const long s4 = a.slab_stride >> 2;
-        const int r0 = grp * rows_per, r1 = min(a.slab_rows, r0 + rows_per);
+        const int r0 = grp * rows_per, r1 = min(rows, r0 + rows_per);
 #pragma unroll 8
         for (int r = r0; r < r1; ++r) acc += sp[(long)r * s4];
       }
@@ -528,7 +531,7 @@ int pto_xar_allreduce(void* ctx, const float* in, float* out, float scale, void*
 int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
                           float dampening, float wd, float scale, int nesterov, int first_step,
                           int* step_counter, const float* slab, int slab_rows, long slab_stride,
-                          long conv_n, void* stream) {
+                          long conv_n, int slab_rows_big, long big_lo, long big_hi, void* stream) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
   XarArgs a{};
   a.mode = 1;
@@ -547,8 +550,14 @@ int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, 
     if (slab_rows <= 0 || (conv_n & 3) || (slab_stride & 3) || slab_stride < conv_n || conv_n > c->n ||
         ((uintptr_t)slab & 15))
       return -1;
+    if (slab_rows_big <= 0 || slab_rows_big > slab_rows || big_lo < 0 || big_hi < big_lo || big_hi > conv_n ||
+        (big_lo & 3) || (big_hi & 3))
+      return -1;
     a.slab = slab;
     a.slab_rows = slab_rows;
+    a.slab_rows_big = slab_rows_big;
+    a.big_lo4 = big_lo >> 2;
+    a.big_hi4 = big_hi >> 2;
     a.slab_stride = slab_stride;
     a.conv4 = conv_n >> 2;
     if ((a.conv4 + c->nblk - 1) / c->nblk > kThreads) return -1;  // one column per thread
@@ -608,8 +617,9 @@ void pto_xar_emu_stamps(void* ctx, unsigned long long* buf) { static_cast<XarEmu
 // Per-rank tensors as arrays of `world` device addresses.  mode 0: dst = out (mean);
 // mode 1: dst = parameters, mbuf = momentum (SGD).  slab may be null.
 int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* dst, const long long* mbuf,
-                    const long long* slab, int slab_rows, long slab_stride, long conv_n, float lr,
-                    float momentum, float dampening, float wd, int nesterov, int first_step) {
+                    const long long* slab, int slab_rows, long slab_stride, long conv_n, int slab_rows_big,
+                    long big_lo, long big_hi, float lr, float momentum, float dampening, float wd,
+                    int nesterov, int first_step) {
   XarEmu* e = static_cast<XarEmu*>(ctx);
   XarArgs h[kMaxWorld];
   for (int r = 0; r < e->world; ++r) {
@@ -640,8 +650,14 @@ int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* d
     if (slab != nullptr) {
       if (slab_rows <= 0 || (conv_n & 3) || (slab_stride & 3) || slab_stride < conv_n || conv_n > e->n)
         return -1;
+      if (slab_rows_big <= 0 || slab_rows_big > slab_rows || big_lo < 0 || big_hi < big_lo || big_hi > conv_n ||
+          (big_lo & 3) || (big_hi & 3))
+        return -1;
       a.slab = reinterpret_cast<const float*>(slab[r]);
       a.slab_rows = slab_rows;
+      a.slab_rows_big = slab_rows_big;
+      a.big_lo4 = big_lo >> 2;
+      a.big_hi4 = big_hi >> 2;
       a.slab_stride = slab_stride;
       a.conv4 = conv_n >> 2;
       if ((a.conv4 + e->nblk - 1) / e->nblk > kThreads) return -1;

@@ -330,6 +330,7 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         if epoch > 1:
             perm.copy_(_epoch_perm(n, args.seed, epoch, rank, args.shard, dev))
         cursor.zero_()
+        tr.invalidate_stage()  # a batch staged from the old permutation must not be reused
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         # batch 0: eager (initialises momentum on the first epoch), logged

@@ -81,6 +81,12 @@ def _views(flat: torch.Tensor, layout: FlatLayout) -> Dict[str, torch.Tensor]:
     return out
 
 
+def K_stage(source, B: int, device):
+    """A next-batch staging slot when the source supports one (uint8 + perm + cursor)."""
+    from ..ops.mnist import BatchStage
+    return BatchStage(B, device) if source is not None and BatchStage.supported(source) else None
+
+
 def reference_init(seed: int = 1) -> Dict[str, torch.Tensor]:
     """Parameters exactly as ``torch.manual_seed(seed); Net()`` creates them."""
     g = torch.random.get_rng_state()
@@ -146,6 +152,19 @@ class FusedMnistTrainer:
         # (profiles/r2_schedule_ab.md): classic 42.0 us/step, fused 42.75 -- the fold saves
         # 1.3 us but the fc weight gradients cost more anywhere else than beside dz2.
         self.schedule = "classic"
+        # round-3 step pieces (A/B knobs, measured in profiles/r3_*):
+        #   conv_chunk 4: conv_bwd4 sums dW_conv2 over 4-sample chunks -> the slab the tail
+        #                 reduces is 4x smaller (1: the per-sample conv_bwd of round 2)
+        #   fc_sgd "tail": the tail launch streams fc params / grads / momentum (its span is
+        #                 latency-bound: measured cheaper than "fused", where fc1_bwd's
+        #                 weight-gradient tiles apply the SGD -- updated fc1.weight via w1_next,
+        #                 copied back by the tail -- and become fc1_bwd's critical path)
+        #   stage: fc1_bwd stages the next step's batch; conv12 reads it with one load
+        #   store_fc_grads: also store the fc gradients in the fused-SGD path (inspection)
+        self.conv_chunk = 4
+        self.fc_sgd = "tail"
+        self.stage_batches = True
+        self.store_fc_grads = True
 
     # ---------------------------------------------------------------- state
     def _alloc(self, B: int):
@@ -162,7 +181,10 @@ class FusedMnistTrainer:
         self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
         self.per_sample = torch.empty((B, 2), device=dev)
         self.h_parts = torch.empty(2 * B * 500, device=dev)  # split-K fc1 pre-activations
-        # per-sample conv-grad slabs in the flat conv-segment layout (pads stay 0)
+        self.w1_next = torch.empty((500, 800), device=dev)  # fused-SGD fc1.weight (tail copies back)
+        self.stage = K_stage(self.source, B, dev)
+        # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
+        # (conv_bwd4) per-4-sample-chunk rows for conv2.weight
         self.conv_slab = torch.zeros((B, self.layout.conv_end), device=dev)
         self.slab_views = {
             k: self.conv_slab[0][self.layout.offsets[k]:self.layout.offsets[k] +
@@ -203,6 +225,15 @@ class FusedMnistTrainer:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def _stage_for(self, source) -> object:
+        return self.stage if (self.stage_batches and self.stage is not None and
+                              (source is None or source is self.source)) else None
+
+    def invalidate_stage(self) -> None:
+        """Drop the staged next batch (call after changing the source's perm in place)."""
+        if self.stage is not None:
+            self.stage.invalidate()
+
     def forward(self, source=None, B: Optional[int] = None) -> None:
         """conv12_fwd + split-K fc1 (the head runs inside fc1_bwd_head)."""
         K, p = self.K, self.params
@@ -211,7 +242,8 @@ class FusedMnistTrainer:
         if self.fuse_conv12:
             K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
                          p["conv2.bias"], B, a1=self.a1[:B], idx1=self.idx1[:B], xn=self.xn[:B],
-                         lab=self.lab[:B], a2=self.a2[:B], idx2=self.idx2[:B])
+                         lab=self.lab[:B], a2=self.a2[:B], idx2=self.idx2[:B],
+                         stage=self._stage_for(source))
         else:
             K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=self.a1[:B],
                         idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
@@ -235,17 +267,21 @@ class FusedMnistTrainer:
                        grad_scale=1.0 / B, dz2=self.dz2[:B], h_out=self.h1[:B], dh=self.dh[:B],
                        dlogits=self.dlogits[:B], per_sample=self.per_sample[:B])
 
-    def _fc1_bwd(self, B: int, jobs: int) -> None:
+    def _fc1_bwd(self, B: int, jobs: int, stage_adv: Optional[int] = None) -> None:
+        """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv."""
         K, p, g = self.K, self.params, self.grads
+        st = self._stage_for(None) if stage_adv is not None and jobs == K.FC1_BWD_ALL else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
                   dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
-                  loss_scale=1.0 / B, jobs=jobs)
+                  loss_scale=1.0 / B, jobs=jobs, src=self.source if st is not None else None, stage=st,
+                  stage_adv=stage_adv or 0)
 
     def _conv_bwd_fc(self, B: int, sgd: bool) -> None:
         """conv backward + fc weight grads (+ their SGD when ``sgd``) in one launch."""
         K, p = self.K, self.params
         fp, fm, fg = self._fc_dicts()
+        self._last_big = None  # per-sample slab rows
         K.conv_bwd_fc(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
                       self.conv_slab, self.slab_views, dh=self.dh[:B], a2=self.a2[:B],
                       dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
@@ -262,10 +298,33 @@ class FusedMnistTrainer:
 
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self.params
+        if self.conv_chunk == 4:
+            K.conv_bwd4(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
+                        self.conv_slab, self.layout.offsets, B)
+            self._last_big = K.conv_bwd4_rows(B, self.layout.offsets)
+            return
+        self._last_big = None
         sv = self.slab_views
         K.conv_bwd(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
                    sv["conv2.weight"], sv["conv2.bias"], sv["conv1.weight"], sv["conv1.bias"],
                    slab=self.conv_slab)
+
+    def _slab_big(self, B: int):
+        """Chunk-row geometry of the slab the last conv backward wrote (None: per-sample rows)."""
+        return getattr(self, "_last_big", None)
+
+    def _fc1_bwd_sgd(self, B: int, advance_cursor: bool) -> None:
+        """fc1_bwd with the fc SGD fused in (updated fc1.weight -> w1_next) + next-batch staging."""
+        K, p = self.K, self.params
+        fp, fm, fg = self._fc_dicts()
+        st = self._stage_for(None)
+        K.fc1_bwd_sgd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
+                      self.h1[:B], dz2=self.dz2[:B], w1_next=self.w1_next, params=fp, bufs=fm,
+                      grads=fg if self.store_fc_grads else None, per_sample=self.per_sample[:B],
+                      stats=self.stats, loss_scale=1.0 / B, lr=self.lr, momentum=self.momentum,
+                      dampening=self.dampening, weight_decay=self.weight_decay, nesterov=self.nesterov,
+                      first_step=self._first_step, src=self.source if st is not None else None, stage=st,
+                      stage_adv=1 if advance_cursor else 0)
 
     def _sgd(self, lo: int, hi: int, grad_scale: float, advance_cursor: bool) -> None:
         self.K.sgd_momentum_(self.flat_params[lo:hi], self.flat_grads[lo:hi],
@@ -290,7 +349,7 @@ class FusedMnistTrainer:
         """conv backward + deterministic slab reduction into the conv bucket."""
         B = self.B if B is None else B
         self._conv_bwd(B)
-        self.K.slab_reduce(self.conv_slab, B, self.conv_bucket())
+        self.K.slab_reduce(self.conv_slab, B, self.conv_bucket(), big=self._slab_big(B))
 
     def forward_backward(self, source=None, B: Optional[int] = None) -> None:
         """All fwd/bwd launches for one batch; grads land in flat_grads (DDP hooks fire)."""
@@ -339,7 +398,8 @@ class FusedMnistTrainer:
                 momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
                 nesterov=self.nesterov, first_step=self._first_step,
                 step_counter=self.cursor if advance_cursor else None,
-                slab=self.conv_slab, slab_rows=B_, conv_n=self.layout.conv_end)
+                slab=self.conv_slab, slab_rows=B_, conv_n=self.layout.conv_end,
+                slab_big=self._slab_big(B_))
             self._first_step = False
             return
         if self.grad_sync is not None:
@@ -350,18 +410,24 @@ class FusedMnistTrainer:
         B = self.B if B is None else B
         ce = self.layout.conv_end
         if not overlap and self.schedule == "classic":
-            # round-1 schedule (6 launches): head and fc1_bwd as their own launches
+            # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd -> tail
             self.forward(source, B)
             self._head(B)
-            self._fc1_bwd(B, K.FC1_BWD_ALL)
+            fused_sgd = self.fc_sgd == "fused"
+            if fused_sgd:
+                self._fc1_bwd_sgd(B, advance_cursor)
+            else:
+                self._fc1_bwd(B, K.FC1_BWD_ALL, stage_adv=1 if advance_cursor else 0)
             self._conv_bwd(B)
+            w1 = self.params["fc1.weight"]
             K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
                                self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
                                dampening=self.dampening, weight_decay=self.weight_decay,
                                nesterov=self.nesterov, first_step=self._first_step,
                                step_counter=self.cursor if advance_cursor else None,
-                               extra=(self.flat_params[ce:], self.flat_grads[ce:],
-                                      self.flat_momentum[ce:]))
+                               extra=None if fused_sgd else (self.flat_params[ce:], self.flat_grads[ce:],
+                                                             self.flat_momentum[ce:]),
+                               big=self._slab_big(B), copy=(self.w1_next, w1) if fused_sgd else None)
             self._first_step = False
             return
         if not overlap and self._fc_in_conv(B):
@@ -381,7 +447,7 @@ class FusedMnistTrainer:
             self._conv_bwd(B)
             fp, fm, fg = self._fc_dicts()
             K.tail_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
-                        self.flat_momentum[:ce], dh=self.dh[:B], a2=self.a2[:B],
+                        self.flat_momentum[:ce], big=self._slab_big(B), dh=self.dh[:B], a2=self.a2[:B],
                         dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
                         fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
                         lr=self.lr, momentum=self.momentum, dampening=self.dampening,
@@ -405,7 +471,7 @@ class FusedMnistTrainer:
                            self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
                            dampening=self.dampening, weight_decay=self.weight_decay,
                            nesterov=self.nesterov, first_step=self._first_step,
-                           step_counter=self.cursor if advance_cursor else None)
+                           step_counter=self.cursor if advance_cursor else None, big=self._slab_big(B))
         main.wait_stream(side)
         self._first_step = False
 

@@ -149,10 +149,33 @@ def conv2_fwd(a1: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out, idx
 
 
+class BatchStage:
+    """Device staging slot for the NEXT step's batch (uint8 pixels [B, 784], int32 labels,
+    and the step number they belong to).  ``fc1_bwd_sgd`` fills it during step t for step
+    t + 1; ``conv12_fwd(..., stage=)`` then reads the batch with one load instead of the
+    cursor -> permutation -> pixel chain, and falls back to the gather on its own whenever the
+    tag is not the current cursor (first step, or the cursor was moved from the host)."""
+
+    def __init__(self, B: int, device):
+        self.B = int(B)
+        self.x = torch.zeros((self.B, 784), dtype=torch.uint8, device=device)
+        self.lab = torch.zeros((self.B,), dtype=torch.int32, device=device)
+        self.tag = torch.full((1,), -1, dtype=torch.int32, device=device)
+
+    def invalidate(self) -> None:
+        """Forget the staged batch (call after changing the source's permutation in place)."""
+        self.tag.fill_(-1)
+
+    @staticmethod
+    def supported(src: "BatchSource") -> bool:
+        return src.is_u8 and src.perm is not None and src.cursor is not None and src.labels is not None
+
+
 def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
                b2: torch.Tensor, B: int, a1=None, idx1=None, xn=None, lab=None, a2=None,
-               idx2=None):
-    """conv1+pool+conv2+pool fused (one launch): returns (a1, idx1, xn, lab, a2, idx2)."""
+               idx2=None, stage: Optional[BatchStage] = None):
+    """conv1+pool+conv2+pool fused (one launch): returns (a1, idx1, xn, lab, a2, idx2).
+    ``stage``: take the batch from a ``BatchStage`` when its tag matches the cursor."""
     lib = _native.load()
     src.check_batch(B)
     _req(w1, (20, 1, 5, 5), torch.float32, "conv1.weight")
@@ -176,11 +199,17 @@ def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.T
         if src.labels is None:
             raise ValueError("lab output requested but BatchSource has no labels")
         _req(lab, (B,), torch.int32, "lab")
+    if stage is not None:
+        if not BatchStage.supported(src):
+            raise ValueError("a staged batch needs a uint8 source with labels, perm and a device cursor")
+        if stage.B < B:
+            raise ValueError("stage holds fewer samples than B")
     rc = lib.pto_mnist_conv12_fwd(
         src.x.data_ptr(), int(src.is_u8), _ptr(src.labels), _ptr(src.perm), _ptr(src.cursor),
         src.host_offset, src.n_total, src.scale, src.shift, w1.data_ptr(), b1.data_ptr(),
         w2.data_ptr(), b2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(), _ptr(lab),
-        a2.data_ptr(), idx2.data_ptr(), B, _stream())
+        a2.data_ptr(), idx2.data_ptr(), B, _ptr(stage.x if stage else None),
+        _ptr(stage.lab if stage else None), _ptr(stage.tag if stage else None), _stream())
     _native.check(rc, "conv12_fwd")
     return a1, idx1, xn, lab, a2, idx2
 
@@ -276,13 +305,16 @@ FC1_BWD_ALL = 7
 
 
 def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_sample=None,
-            stats=None, loss_scale: float = 1.0, jobs: int = FC1_BWD_ALL):
+            stats=None, loss_scale: float = 1.0, jobs: int = FC1_BWD_ALL,
+            src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None, stage_adv: int = 1):
     """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked).
 
     ``jobs`` selects which of the three independent parts to launch (so the weight
     gradients can run on a side stream concurrently with the input gradient).
     With ``per_sample`` (head output) and ``stats``, job FC2 also writes
     ``stats[0] = sum(loss)*loss_scale`` and ``stats[1] = #correct``.
+    With ``src`` + ``stage`` (all jobs), ceil(B/4) extra blocks stage the batch of step
+    ``cursor + stage_adv`` for the next conv12_fwd.
     """
     lib = _native.load()
     B = dh.shape[0]
@@ -300,12 +332,96 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
     if per_sample is not None:
         _req(per_sample, (B, 2), torch.float32, "per_sample")
+    if stage is not None:
+        if jobs != FC1_BWD_ALL or src is None or not BatchStage.supported(src):
+            raise ValueError("staging needs jobs=FC1_BWD_ALL and a uint8 BatchSource with labels, perm, cursor")
+        if stage.B < B or src.x.data_ptr() % 16:
+            raise ValueError("stage too small or unaligned source")
+        rc = lib.pto_mnist_fc1_bwd_stage(
+            dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
+            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
+            _ptr(stats), float(loss_scale), B, src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(),
+            src.cursor.data_ptr(), src.n_total, int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(),
+            stage.tag.data_ptr(), _stream())
+        _native.check(rc, "fc1_bwd(stage)")
+        return dz2
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),
                                gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
                                _ptr(stats), float(loss_scale), int(jobs), B, _stream())
     _native.check(rc, "fc1_bwd")
     return dz2
+
+
+def fc1_bwd_sgd(dh, a2, idx2, w1, dlogits, h, *, dz2, w1_next, params: dict, bufs: dict,
+                grads: Optional[dict] = None, per_sample=None, stats=None, loss_scale: float = 1.0,
+                lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
+                src: Optional[BatchSource] = None, stage: Optional[BatchStage] = None,
+                stage_adv: int = 1):
+    """fc1_bwd (dz2, dW_fc1, db_fc1, dW_fc2, db_fc2, loss statistics) with the SGD(momentum)
+    of every fc parameter fused into the weight-gradient tiles: the updated fc1.weight is
+    written to ``w1_next`` (this launch's dz2 job still reads ``w1``; copy it back after the
+    launch -- ``slab_reduce_sgd_(copy=...)`` does), fc1.bias / fc2.* and all fc momentum
+    buffers are updated in place.  ``params`` / ``bufs`` / ``grads``: dicts of the fc1/fc2
+    weight/bias tensors (``grads`` optional: stored when given).  With ``src`` + ``stage``,
+    ceil(B/4) extra blocks stage the batch of step ``cursor + stage_adv``."""
+    lib = _native.load()
+    B = dh.shape[0]
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
+    _req(w1, (500, 800), torch.float32, "fc1.weight")
+    _req(w1_next, (500, 800), torch.float32, "fc1.weight (next)")
+    if w1_next.data_ptr() == w1.data_ptr():
+        raise ValueError("w1_next must not alias w1")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h1")
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
+    for k, shp in shapes.items():
+        _req(bufs[k], shp, torch.float32, f"{k} momentum")
+        if k != "fc1.weight":
+            _req(params[k], shp, torch.float32, f"{k} param")
+        if grads is not None:
+            _req(grads[k], shp, torch.float32, f"{k} grad")
+    if per_sample is not None:
+        _req(per_sample, (B, 2), torch.float32, "per_sample")
+    g = (lambda k: _ptr(grads[k])) if grads is not None else (lambda k: None)
+    if stage is not None:
+        if src is None or not BatchStage.supported(src):
+            raise ValueError("staging needs a uint8 BatchSource with labels, perm and a device cursor")
+        if stage.B < B:
+            raise ValueError("stage holds fewer samples than B")
+        if src.x.data_ptr() % 16:
+            raise ValueError("source pixels must be 16-byte aligned")
+    st = stage is not None
+    rc = lib.pto_mnist_fc1_bwd_sgd(
+        dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
+        g("fc1.weight"), g("fc1.bias"), g("fc2.weight"), g("fc2.bias"), dz2.data_ptr(), _ptr(per_sample),
+        _ptr(stats), float(loss_scale), B, w1_next.data_ptr(), bufs["fc1.weight"].data_ptr(),
+        params["fc1.bias"].data_ptr(), bufs["fc1.bias"].data_ptr(), params["fc2.weight"].data_ptr(),
+        bufs["fc2.weight"].data_ptr(), params["fc2.bias"].data_ptr(), bufs["fc2.bias"].data_ptr(),
+        float(lr), float(momentum), float(dampening), float(weight_decay), float(grad_scale), int(nesterov),
+        int(first_step), _ptr(src.x) if st else None, _ptr(src.labels) if st else None,
+        _ptr(src.perm) if st else None, _ptr(src.cursor) if st else None, src.n_total if st else 0,
+        int(stage_adv), _ptr(stage.x) if st else None, _ptr(stage.lab) if st else None,
+        _ptr(stage.tag) if st else None, _stream())
+    _native.check(rc, "fc1_bwd_sgd")
+    return dz2
+
+
+def stage_batch(src: BatchSource, stage: BatchStage, B: int, adv: int = 0) -> None:
+    """Gather the batch of step ``cursor + adv`` into ``stage`` (one small launch)."""
+    lib = _native.load()
+    if not BatchStage.supported(src):
+        raise ValueError("staging needs a uint8 BatchSource with labels, perm and a device cursor")
+    if stage.B < B or src.x.data_ptr() % 16:
+        raise ValueError("stage too small or unaligned source")
+    rc = lib.pto_mnist_stage_batch(src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(),
+                                   src.cursor.data_ptr(), src.n_total, int(B), int(adv), stage.x.data_ptr(),
+                                   stage.lab.data_ptr(), stage.tag.data_ptr(), _stream())
+    _native.check(rc, "stage_batch")
 
 
 def fc1_bwd_head(hp: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
@@ -348,7 +464,7 @@ def tail_sgd_(slab: torch.Tensor, B: int, conv_grads: torch.Tensor, conv_params:
               fc_bufs: dict, fc_grads: dict, stats: Optional[torch.Tensor], loss_scale: float,
               lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
               nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-              step_counter: Optional[torch.Tensor] = None) -> None:
+              step_counter: Optional[torch.Tensor] = None, big: Optional[tuple] = None) -> None:
     """Single-process step tail (one launch): conv grads = sum of the slab rows + SGD on the
     conv params; dW_fc1 = dh^T a2, db_fc1, dW_fc2 = dlogits^T h, db_fc2, each with its SGD
     applied in the epilogue (grads also stored); loss statistics; cursor advance.
@@ -376,7 +492,9 @@ def tail_sgd_(slab: torch.Tensor, B: int, conv_grads: torch.Tensor, conv_params:
         raise ValueError("stats must be fp32 with >= 2 elements")
     if step_counter is not None and (step_counter.dtype != torch.int32 or not step_counter.is_cuda):
         raise ValueError("step_counter must be int32 CUDA")
-    rc = lib.pto_mnist_tail_sgd(slab.data_ptr(), B, n, slab.shape[1], conv_grads.data_ptr(),
+    rb, lo, hi = big if big is not None else (B, 0, 0)
+    rc = lib.pto_mnist_tail_sgd(slab.data_ptr(), B, n, slab.shape[1], int(rb), int(lo), int(hi),
+                                conv_grads.data_ptr(),
                                 conv_params.data_ptr(), conv_buf.data_ptr(), float(lr),
                                 float(momentum), float(dampening), float(weight_decay),
                                 float(grad_scale), int(nesterov), int(first_step),
@@ -423,6 +541,39 @@ def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
                                 gb1.data_ptr(), _ptr(dz1), stride, B, _stream())
     _native.check(rc, "conv_bwd")
     return dz1
+
+
+CONV2_W = (50, 20, 5, 5)
+
+
+def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optional[int] = None):
+    """conv backward with dW_conv2 summed over 4-sample chunks (deterministic, no atomics).
+
+    ``slab``: contiguous fp32 [>= B, S]; ``offsets``: the row offsets (floats) of
+    ``conv2.weight`` / ``conv2.bias`` / ``conv1.weight`` / ``conv1.bias`` inside a row (the
+    flat conv-segment layout).  Rows 0..ceil(B/4)-1 receive the chunk partials of
+    conv2.weight, rows 0..B-1 the per-sample partials of the other three; reduce with
+    ``slab_reduce(..., big=conv_bwd4_rows(B, offsets))``.
+    """
+    lib = _native.load()
+    B = dz2.shape[0] if B is None else B
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    _req(w2, CONV2_W, torch.float32, "conv2.weight")
+    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
+    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
+    _req(xn, (B, 784), torch.float32, "xn")
+    if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
+        raise ValueError("slab must be contiguous fp32 [>=B, S]")
+    o = [int(offsets[k]) for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
+    rc = lib.pto_mnist_conv_bwd4(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
+                                 slab.data_ptr(), slab.shape[1], *o, B, _stream())
+    _native.check(rc, "conv_bwd4")
+
+
+def conv_bwd4_rows(B: int, offsets: dict) -> tuple:
+    """(rows, lo, hi): the slab columns conv_bwd4 writes per 4-sample chunk."""
+    lo = int(offsets["conv2.weight"])
+    return ((B + 3) // 4, lo, lo + 25000)
 
 
 def conv_bwd_fc_supported(B: int) -> bool:
@@ -480,8 +631,10 @@ def conv_bwd_fc(dz2, w2, a1, idx1, xn, slab: torch.Tensor, slab_views: dict, *, 
     _native.check(rc, "conv_bwd_fc")
 
 
-def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor) -> torch.Tensor:
-    """out[o] = sum_{b<B} slab[b, o] for o < out.numel() (deterministic order)."""
+def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor, big: Optional[tuple] = None) -> torch.Tensor:
+    """out[o] = sum_{b<B} slab[b, o] for o < out.numel() (deterministic order).
+    ``big = (rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows
+    (``conv_bwd4_rows``)."""
     lib = _native.load()
     if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2:
         raise ValueError("slab must be contiguous fp32 [rows, S]")
@@ -490,7 +643,9 @@ def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor) -> torch.Tensor:
     n = out.numel()
     if out.dtype != torch.float32 or not out.is_contiguous() or n > slab.shape[1]:
         raise ValueError("out must be contiguous fp32 with <= S elements")
-    rc = lib.pto_slab_reduce(slab.data_ptr(), B, n, slab.shape[1], out.data_ptr(), _stream())
+    rb, lo, hi = big if big is not None else (B, 0, 0)
+    rc = lib.pto_slab_reduce(slab.data_ptr(), B, n, slab.shape[1], out.data_ptr(), int(rb), int(lo), int(hi),
+                             _stream())
     _native.check(rc, "slab_reduce")
     return out
 
@@ -500,11 +655,14 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                      dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                      grad_scale: float = 1.0, first_step: bool = False,
                      step_counter: Optional[torch.Tensor] = None,
-                     extra: Optional[tuple] = None) -> None:
+                     extra: Optional[tuple] = None, big: Optional[tuple] = None,
+                     copy: Optional[tuple] = None) -> None:
     """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch).
 
     ``extra=(params2, grads2, buf2)``: also apply the same SGD to a second,
     already-reduced range in the same launch (e.g. the fc parameters).
+    ``big=(rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows.
+    ``copy=(src, dst)``: also copy ``src`` into ``dst`` (equal-size contiguous fp32).
     """
     lib = _native.load()
     n = params.numel()
@@ -522,11 +680,21 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
         for t, nm in ((p2, "params2"), (g2, "grads2"), (b2, "buf2")):
             if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n2:
                 raise ValueError(f"{nm} must be contiguous fp32 with {n2} elements")
+    rb, lo, hi = big if big is not None else (B, 0, 0)
+    cs = cd = None
+    cn = 0
+    if copy is not None:
+        cs, cd = copy
+        if cs.dtype != torch.float32 or cd.dtype != torch.float32 or not cs.is_contiguous() or \
+                not cd.is_contiguous() or cs.numel() != cd.numel():
+            raise ValueError("copy=(src, dst) must be equal-size contiguous fp32 tensors")
+        cn = cs.numel()
     rc = lib.pto_slab_reduce_sgd(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
                                  params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
                                  float(dampening), float(weight_decay), float(grad_scale),
                                  int(nesterov), int(first_step), _ptr(step_counter), _ptr(p2),
-                                 _ptr(g2), _ptr(b2), n2, _stream())
+                                 _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi), _ptr(cs), _ptr(cd),
+                                 int(cn), _stream())
     _native.check(rc, "slab_reduce_sgd")
 
 

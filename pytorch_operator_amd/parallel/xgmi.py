@@ -96,11 +96,14 @@ class XgmiAllReduce:
                        lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
                        nesterov: bool = False, first_step: bool = False,
                        step_counter: Optional[torch.Tensor] = None,
-                       slab: Optional[torch.Tensor] = None, slab_rows: int = 0, conv_n: int = 0) -> None:
+                       slab: Optional[torch.Tensor] = None, slab_rows: int = 0, conv_n: int = 0,
+                       slab_big: Optional[tuple] = None) -> None:
         """SGD with the mean gradient over ranks.  With ``slab`` ([rows, stride] fp32), the
         first ``conv_n`` gradient entries are the sum of its first ``slab_rows`` rows
-        (fused deterministic reduction of the per-sample conv partials); ``grads`` then
-        only needs to hold the entries after ``conv_n``."""
+        (fused deterministic reduction of the conv backward's partials); ``grads`` then
+        only needs to hold the entries after ``conv_n``.  ``slab_big = (rows, lo, hi)``: the
+        entries [lo, hi) (conv2.weight, written per 4-sample chunk by conv_bwd4) sum only
+        their first ``rows`` rows."""
         for t in (grads, params, momentum_buf):
             self._check(t)
         sc = step_counter.data_ptr() if step_counter is not None else None
@@ -110,10 +113,12 @@ class XgmiAllReduce:
                     and slab_rows <= slab.shape[0] and conv_n <= slab.shape[1]):
                 raise ValueError("slab must be a contiguous fp32 CUDA [rows, stride] tensor")
             sp, stride = slab.data_ptr(), slab.shape[1]
+        big_rows, big_lo, big_hi = slab_big if slab_big is not None else (max(1, slab_rows), 0, 0)
         _native.check(self.lib.pto_xar_allreduce_sgd(
             self._ctx, grads.data_ptr(), params.data_ptr(), momentum_buf.data_ptr(), lr, momentum,
             dampening, weight_decay, 1.0 / self.world, int(nesterov), int(first_step), sc,
-            sp, int(slab_rows), int(stride), int(conv_n), self._stream()), "pto_xar_allreduce_sgd")
+            sp, int(slab_rows), int(stride), int(conv_n), int(big_rows), int(big_lo), int(big_hi),
+            self._stream()), "pto_xar_allreduce_sgd")
 
     def gather_sharded_(self, t: torch.Tensor) -> None:
         """Reassemble a tensor each rank only kept for its own shard (e.g. the momentum
@@ -230,17 +235,18 @@ class XgmiEmulation:
 
     def configure(self, mode: int, inputs, dst, mbuf=None, slab=None, slab_rows: int = 0, conv_n: int = 0,
                   lr: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                  nesterov: bool = False, first_step: bool = False) -> None:
+                  nesterov: bool = False, first_step: bool = False, slab_big: Optional[tuple] = None) -> None:
         for t in list(inputs) + list(dst) + list(mbuf or []):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == self.n
                     and t.data_ptr() % 16 == 0):
                 raise ValueError(f"expected aligned contiguous fp32 CUDA tensors of {self.n} elements")
         stride = slab[0].shape[1] if slab is not None else 0
+        big_rows, big_lo, big_hi = slab_big if slab_big is not None else (max(1, slab_rows), 0, 0)
         self._keep = (inputs, dst, mbuf, slab)  # the kernel holds raw pointers
         _native.check(self.lib.pto_xar_emu_set(
             self._ctx, int(mode), self._ptrs(inputs), self._ptrs(dst), self._ptrs(mbuf), self._ptrs(slab),
-            int(slab_rows), int(stride), int(conv_n), lr, momentum, dampening, weight_decay,
-            int(nesterov), int(first_step)), "pto_xar_emu_set")
+            int(slab_rows), int(stride), int(conv_n), int(big_rows), int(big_lo), int(big_hi), lr, momentum,
+            dampening, weight_decay, int(nesterov), int(first_step)), "pto_xar_emu_set")
 
     def launch(self) -> None:
         _native.check(self.lib.pto_xar_emu_launch(

@@ -75,6 +75,7 @@ class _Bucket:
         self.exp_avg = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(self.shard, dtype=torch.float32, device=dev)
         self.pending = len(params)
+        self.arrived: set = set()  # ids of the parameters whose gradient was deposited this step
         self.rs_work = None
         self.ag_work = None
 
@@ -143,6 +144,7 @@ class ZeroAdamW:
         off = b.slot[id(p)]
         self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
         p.grad = None
+        b.arrived.add(id(p))
         b.pending -= 1
         if b.pending == 0:
             self._reduce_scatter(b)
@@ -180,12 +182,23 @@ class ZeroAdamW:
             with torch.enable_grad():
                 loss = closure()
         self.t += 1
+        skip: Dict[int, List[tuple]] = {}
         for b in self.buckets:
-            if b.pending >= 0:  # some parameter got no gradient this step: it contributes zeros
+            if b.pending >= 0:
+                # some parameter of this bucket got no gradient through the hook this step.  Only
+                # the slots that never arrived are filled (zeros, or a gradient set outside
+                # backward); deposited gradients are kept.  At world > 1 a missing gradient
+                # contributes zeros to the sum (DDP's find_unused_parameters semantics); at world 1
+                # a parameter without any gradient is left untouched, as MasterAdamW /
+                # torch.optim.AdamW skip it.
                 for p in b.params:
+                    if id(p) in b.arrived:
+                        continue
                     off = b.slot[id(p)]
                     if p.grad is None:
                         b.grad32[off:off + p.numel()].zero_()
+                        if self.world == 1:
+                            skip.setdefault(id(b), []).append((off, p.numel()))
                     else:
                         self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
                         p.grad = None
@@ -195,12 +208,35 @@ class ZeroAdamW:
             if b.rs_work is not None:
                 b.rs_work.wait()
                 b.rs_work = None
+            keep = self._save_ranges(b, skip.get(id(b), []))
             self._adamw(b)
+            self._restore_ranges(b, keep)
             if self.world > 1:
                 src = b.w_shard() if b.flat_w.is_cuda else b.w_shard().clone()
                 b.ag_work = dist.all_gather_into_tensor(b.flat_w, src, group=self.group, async_op=True)
             b.pending = len(b.params)
+            b.arrived.clear()
         return loss
+
+    @staticmethod
+    def _save_ranges(b: _Bucket, ranges) -> list:
+        """Copies of the optimizer state + weights of the bucket ranges AdamW must not touch
+        (world 1 only: the shard is the whole bucket)."""
+        out = []
+        for off, n in ranges:
+            sl = slice(off, off + n)
+            out.append((sl, b.flat_w[sl].clone(), b.exp_avg[sl].clone(), b.exp_avg_sq[sl].clone(),
+                        b.master[sl].clone() if b.master is not None else None))
+        return out
+
+    @staticmethod
+    def _restore_ranges(b: _Bucket, saved) -> None:
+        for sl, w, m, v, ms in saved:
+            b.flat_w[sl].copy_(w)
+            b.exp_avg[sl].copy_(m)
+            b.exp_avg_sq[sl].copy_(v)
+            if ms is not None:
+                b.master[sl].copy_(ms)
 
     def _adamw(self, b: _Bucket) -> None:
         b1, b2 = self.betas

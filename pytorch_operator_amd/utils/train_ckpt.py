@@ -7,19 +7,26 @@ reloads the last checkpoint.  The MNIST worker has the reference's own ``--save-
 epoch checkpoints (``harness/mnist.py``); this is the same contract for the bigger workers.
 
 Layout of ``<dir>``:
-  model.pt            weights as the model holds them (bf16 matmul weights, fp32 rest), rank 0
-  optim.pt            replicated optimizer state (DDP paths), rank 0
-  optim_rank<r>.pt    this rank's shard (ZeRO-1: fp32 master + moments of its 1/W of each bucket)
-  meta.json           {"step", "world", "sharded"}: written last, after every rank finished,
-                      so a crash mid-save leaves the previous checkpoint loadable
+  step_<N>/model.pt          weights as the model holds them (bf16 matmul weights, fp32 rest), rank 0
+  step_<N>/optim.pt          replicated optimizer state (DDP paths), rank 0
+  step_<N>/optim_rank<r>.pt  this rank's shard (ZeRO-1: fp32 master + moments of its 1/W of each bucket)
+  meta.json                  {"step", "world", "sharded", "subdir"}: the pointer to the newest COMPLETE
+                             checkpoint, replaced atomically by rank 0 after every rank finished
+                             writing step_<N>/ (a barrier); older step_* directories are pruned
+                             after the pointer moved (``keep`` newest are kept)
 
-All files are written to a temporary name and renamed; tensors are loaded with
-``torch.load(weights_only=True)``.  A sharded checkpoint needs the same world size to resume.
+A crash at any point of ``save`` leaves meta.json pointing at the previous complete checkpoint:
+files of the interrupted save live only in their own step_<N>/ directory, which no pointer
+names, so ``load`` never mixes shards of different steps.  All files are written to a
+temporary name and renamed; tensors are loaded with ``torch.load(weights_only=True)``.  A
+sharded checkpoint needs the same world size to resume.  (Checkpoints written before this
+layout -- files directly in ``<dir>``, meta.json without "subdir" -- still load.)
 """
 from __future__ import annotations
 
 import json
 import os
+import shutil
 from typing import Optional
 
 import torch
@@ -74,23 +81,39 @@ def load_optimizer_state(opt, blob: dict) -> None:
         opt.load_state_dict(blob["state_dict"])
 
 
-def save(dirpath: str, step: int, model, opt, rank: int, world: int) -> None:
-    os.makedirs(dirpath, exist_ok=True)
+def _step_dirs(dirpath: str):
+    out = []
+    for name in os.listdir(dirpath):
+        if name.startswith("step_") and name[5:].isdigit() and os.path.isdir(os.path.join(dirpath, name)):
+            out.append((int(name[5:]), name))
+    return sorted(out)
+
+
+def save(dirpath: str, step: int, model, opt, rank: int, world: int, keep: int = 2) -> None:
+    sub = f"step_{int(step)}"
+    path = os.path.join(dirpath, sub)
+    os.makedirs(path, exist_ok=True)
     sharded = hasattr(opt, "shard_state_dict")
     if hasattr(opt, "synchronize"):
         opt.synchronize()  # ZeRO: weights all-gathered before they are written
     if rank == 0:
-        _atomic_save(_cpu(model.state_dict()), os.path.join(dirpath, "model.pt"))
+        _atomic_save(_cpu(model.state_dict()), os.path.join(path, "model.pt"))
         if not sharded:
-            _atomic_save(_cpu(optimizer_state(opt)), os.path.join(dirpath, "optim.pt"))
+            _atomic_save(_cpu(optimizer_state(opt)), os.path.join(path, "optim.pt"))
     if sharded:
-        _atomic_save(_cpu(opt.shard_state_dict()), os.path.join(dirpath, f"optim_rank{rank}.pt"))
-    _barrier(world)
+        _atomic_save(_cpu(opt.shard_state_dict()), os.path.join(path, f"optim_rank{rank}.pt"))
+    _barrier(world)  # every rank's files of step_<N> are complete
     if rank == 0:
         tmp = os.path.join(dirpath, "meta.json.tmp")
         with open(tmp, "w") as f:
-            json.dump({"step": int(step), "world": int(world), "sharded": sharded}, f)
+            json.dump({"step": int(step), "world": int(world), "sharded": sharded, "subdir": sub}, f)
+            f.flush()
+            os.fsync(f.fileno())
         os.replace(tmp, os.path.join(dirpath, "meta.json"))
+        # prune: never the directory the pointer names, keep the newest `keep`
+        dirs = [d for d in _step_dirs(dirpath) if d[1] != sub]
+        for _, name in dirs[:max(0, len(dirs) - (keep - 1))]:
+            shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
     _barrier(world)
 
 
@@ -104,13 +127,14 @@ def load(dirpath: Optional[str], model, opt, rank: int, world: int, device) -> i
     if meta["sharded"] != sharded or (sharded and meta["world"] != world):
         raise ValueError(f"checkpoint {dirpath} (world {meta['world']}, sharded {meta['sharded']}) cannot "
                          f"resume a world-{world} {'sharded' if sharded else 'replicated'} optimizer")
-    sd = torch.load(os.path.join(dirpath, "model.pt"), map_location=device, weights_only=True)
+    path = os.path.join(dirpath, meta["subdir"]) if meta.get("subdir") else dirpath
+    sd = torch.load(os.path.join(path, "model.pt"), map_location=device, weights_only=True)
     with torch.no_grad():
         model.load_state_dict(sd)  # copies into the existing (bucket-view) parameters
     if sharded:
-        opt.load_shard_state_dict(torch.load(os.path.join(dirpath, f"optim_rank{rank}.pt"), map_location=device,
+        opt.load_shard_state_dict(torch.load(os.path.join(path, f"optim_rank{rank}.pt"), map_location=device,
                                              weights_only=True))
     else:
-        load_optimizer_state(opt, torch.load(os.path.join(dirpath, "optim.pt"), map_location=device,
+        load_optimizer_state(opt, torch.load(os.path.join(path, "optim.pt"), map_location=device,
                                              weights_only=True))
     return int(meta["step"])

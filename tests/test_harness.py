@@ -326,6 +326,44 @@ def test_zero_adamw_single_process_matches_master_adamw(reduce_dtype):
             assert (a.float() - b.float()).abs().max() <= 3 * 2e-3
 
 
+def test_zero_adamw_unused_parameter_matches_master_adamw():
+    """A bucket with a parameter that gets no gradient: the gradients that did
+    arrive are kept (not zeroed by the partial-bucket fallback) and the unused parameter is left
+    untouched, as MasterAdamW skips parameters without a gradient."""
+    import copy
+    import torch.nn as nn
+    from pytorch_operator_amd.ops.optim import MasterAdamW
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+
+    class TwoHead(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(8, 8)
+            self.unused = nn.Linear(8, 8)  # same bucket, never in the graph
+            self.b = nn.Linear(8, 4)
+
+        def forward(self, x):
+            return self.b(torch.relu(self.a(x)))
+
+    torch.manual_seed(1)
+    m1 = TwoHead()
+    m2 = copy.deepcopy(m1)
+    o1 = MasterAdamW(m1.parameters(), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+    o2 = ZeroAdamW(m2, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=1.0)
+    assert len(o2.buckets) == 1  # the unused parameter shares the bucket with the used ones
+    x = torch.randn(5, 8)
+    before = m2.unused.weight.detach().clone()
+    for _ in range(3):
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad(set_to_none=True)
+            m(x).square().mean().backward()
+            o.step()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(a, b, rtol=0, atol=1e-6), n
+    assert torch.equal(m2.unused.weight, before)
+    assert not torch.equal(m2.a.weight, m1.a.weight * 0)  # the used parameters did move
+
+
 def test_ddp_train_worker_resnet_tiny(tmp_path):
     (rc, out), = _launch("pytorch_operator_amd.harness.ddp_train",
                          ["--model", "resnet-tiny", "--batch-size", "2", "--steps", "2", "--warmup", "1"], 1, tmp_path)
@@ -390,3 +428,33 @@ def test_bench_contract_cli_and_graph_chunking():
     assert bench.pick_steps_per_graph(2000, 50) == 50
     assert bench.pick_steps_per_graph(2000, 0) == 250
     assert bench.pick_steps_per_graph(1009, 5) == 1
+
+
+def test_train_ckpt_interrupted_save_keeps_previous_checkpoint(tmp_path):
+    """a save that dies after writing some files of step N+k must leave the step-N
+    checkpoint loadable and unmixed (files go to step_<N>/, the meta.json pointer moves last)."""
+    import torch.nn as nn
+    from pytorch_operator_amd.utils import train_ckpt
+    torch.manual_seed(0)
+    m = nn.Linear(4, 3)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+    m(torch.randn(2, 4)).sum().backward()
+    opt.step()
+    d = str(tmp_path / "ck")
+    train_ckpt.save(d, 5, m, opt, rank=0, world=1)
+    w5 = m.weight.detach().clone()
+    # a later save that crashed after model.pt: its directory exists, the pointer did not move
+    with torch.no_grad():
+        m.weight.add_(1.0)
+    os.makedirs(os.path.join(d, "step_9"))
+    torch.save({k: v.clone() for k, v in m.state_dict().items()}, os.path.join(d, "step_9", "model.pt"))
+    m2 = nn.Linear(4, 3)
+    opt2 = torch.optim.SGD(m2.parameters(), lr=0.1, momentum=0.9)
+    assert train_ckpt.load(d, m2, opt2, rank=0, world=1, device="cpu") == 5
+    assert torch.equal(m2.weight, w5)
+    # the next complete save moves the pointer and prunes all but the newest `keep`
+    for st in (10, 11, 12):
+        train_ckpt.save(d, st, m, opt, rank=0, world=1, keep=2)
+    assert sorted(os.listdir(d)) == ["meta.json", "step_11", "step_12"]
+    assert train_ckpt.load(d, m2, opt2, rank=0, world=1, device="cpu") == 12
+    assert torch.equal(m2.weight, m.weight)

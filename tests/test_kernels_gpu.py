@@ -305,3 +305,156 @@ def test_fused_schedule_matches_classic(lib, B):
     assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
     ce = tr.layout.conv_end
     assert _rel(g1[ce:], g0[ce:]) < 1e-5  # fc grads are still written for inspection
+
+
+# ---------------------------------------------------------------------------- round 3
+@pytest.mark.parametrize("B", [64, 37, 13, 1])
+def test_conv_bwd4_chunked_slab_matches_autograd(lib, B):
+    """conv_bwd4 (dW_conv2 summed over 4-sample chunks, per-sample conv1/bias rows) reduced
+    with the two-segment slab reduction equals torch's conv gradients and the per-sample
+    conv_bwd path."""
+    from pytorch_operator_amd.models.mnist import flat_layout, reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    sd = reference_init(8)
+    x, y = _data(B, seed=900 + B)
+    xn = _norm(x)
+    c1w = sd["conv1.weight"].clone().requires_grad_(True)
+    c1b = sd["conv1.bias"].clone().requires_grad_(True)
+    c2w = sd["conv2.weight"].clone().requires_grad_(True)
+    c2b = sd["conv2.bias"].clone().requires_grad_(True)
+    r1 = F.max_pool2d(F.relu(F.conv2d(xn, c1w, c1b)), 2, 2)
+    z2 = F.conv2d(r1, c2w, c2b)
+    z2.retain_grad()
+    out = F.max_pool2d(F.relu(z2), 2, 2)
+    (out * torch.randn(out.shape, generator=torch.Generator().manual_seed(B))).sum().backward()
+    p = {k: v.to(dev).contiguous() for k, v in sd.items()}
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    a1, idx1, xnk, _ = K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B)
+    dz2 = z2.grad.contiguous().to(dev)
+    lay = flat_layout()
+    ce = lay.conv_end
+    slab = torch.full((B, ce), float("nan"), device=dev)
+    slab.zero_()
+    K.conv_bwd4(dz2, p["conv2.weight"], a1, idx1, xnk, slab, lay.offsets, B)
+    got = torch.empty(ce, device=dev)
+    K.slab_reduce(slab, B, got, big=K.conv_bwd4_rows(B, lay.offsets))
+    # per-sample path
+    slab1 = torch.zeros((B, ce), device=dev)
+    v = {k: slab1[0][lay.offsets[k]:lay.offsets[k] + n].view(s) for k, s, n in
+         (("conv2.weight", (50, 20, 5, 5), 25000), ("conv2.bias", (50,), 50),
+          ("conv1.weight", (20, 1, 5, 5), 500), ("conv1.bias", (20,), 20))}
+    K.conv_bwd(dz2, p["conv2.weight"], a1, idx1, xnk, v["conv2.weight"], v["conv2.bias"], v["conv1.weight"],
+               v["conv1.bias"], slab=slab1)
+    ref1 = torch.empty(ce, device=dev)
+    K.slab_reduce(slab1, B, ref1)
+    torch.cuda.synchronize()
+    for name, t in (("conv2.weight", c2w), ("conv2.bias", c2b), ("conv1.weight", c1w), ("conv1.bias", c1b)):
+        o, n = lay.offsets[name], t.numel()
+        assert _rel(got[o:o + n].view(t.shape), t.grad) < 2e-4, name
+        assert _rel(got[o:o + n], ref1[o:o + n]) < 1e-5, name
+    # the per-sample small partials and chunk rows are deterministic: a second launch is bit-identical
+    slab2 = torch.zeros_like(slab)
+    K.conv_bwd4(dz2, p["conv2.weight"], a1, idx1, xnk, slab2, lay.offsets, B)
+    got2 = torch.empty(ce, device=dev)
+    K.slab_reduce(slab2, B, got2, big=K.conv_bwd4_rows(B, lay.offsets))
+    torch.cuda.synchronize()
+    assert torch.equal(got, got2)
+
+
+@pytest.mark.parametrize("B", [64, 50])
+def test_fc1_bwd_fused_sgd_matches_grads_plus_sgd(lib, B):
+    """fc1_bwd_sgd: dz2 and the fc gradients equal fc1_bwd's; the fused update equals
+    torch.optim.SGD semantics applied to those gradients; fc1.weight goes to w1_next only."""
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    p = {k: v.to(dev).contiguous() for k, v in reference_init(12).items()}
+    x, y = _data(B, seed=1200 + B)
+    src = K.BatchSource(x.to(dev), y.to(dev))
+    f = K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"], p["conv2.bias"], B)
+    lab, a2, idx2 = f[3], f[4], f[5]
+    h = K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"])
+    dl, dh, _ = K.head(h, p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B)
+    names = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
+    g_ref = {k: torch.empty_like(p[k]) for k in names}
+    dz_ref = K.fc1_bwd(dh, a2, idx2, p["fc1.weight"], dl, h, *[g_ref[k] for k in names])
+    g = torch.Generator().manual_seed(B)
+    mom = {k: torch.randn(p[k].shape, generator=g).to(dev) for k in names}
+    params = {k: p[k].clone() for k in names}
+    bufs = {k: mom[k].clone() for k in names}
+    grads = {k: torch.full_like(p[k], float("nan")) for k in names}
+    w1n = torch.full_like(p["fc1.weight"], float("nan"))
+    dz2 = torch.full((B, 50, 8, 8), float("nan"), device=dev)
+    lr, m = 0.05, 0.5
+    K.fc1_bwd_sgd(dh, a2, idx2, params["fc1.weight"], dl, h, dz2=dz2, w1_next=w1n, params=params, bufs=bufs,
+                  grads=grads, lr=lr, momentum=m)
+    torch.cuda.synchronize()
+    assert torch.equal(dz2, dz_ref)
+    for k in names:
+        assert torch.equal(grads[k], g_ref[k]), k
+        m_ref = m * mom[k] + g_ref[k]
+        p_ref = p[k] - lr * m_ref
+        assert _rel(bufs[k], m_ref) < 1e-6, k
+        got = w1n if k == "fc1.weight" else params[k]
+        assert _rel(got, p_ref) < 1e-6, k
+    assert torch.equal(params["fc1.weight"], p["fc1.weight"])  # read-only in this launch
+
+
+def _stage_trainer(x, y, perm, B=64, seed=9, **knobs):
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    cur = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(x.to(dev), y.to(dev), perm=perm.to(dev), cursor=cur)
+    tr = FusedMnistTrainer(batch_size=B, source=src, seed=seed, lr=0.05, momentum=0.5)
+    for k, v in knobs.items():
+        setattr(tr, k, v)
+    return tr
+
+
+def test_staged_batches_are_bit_identical_to_gathered(lib):
+    """The next-batch staging (fc1_bwd fills it, conv12 reads it when the tag matches the
+    cursor) trains bit-identically to the per-step gather, also across a host-side cursor
+    move (the tag no longer matches -> conv12 gathers) and with advance_cursor=False."""
+    n = 640
+    x, y = _data(n, seed=77, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    a = _stage_trainer(x, y, perm, stage_batches=True)
+    b = _stage_trainer(x, y, perm, stage_batches=False)
+    assert a.stage is not None
+    for tr in (a, b):
+        for _ in range(3):
+            tr.train_step()
+        tr.train_step(advance_cursor=False)
+        tr.cursor.fill_(7)  # host moves the cursor: the staged batch (tag 3) must not be used
+        for _ in range(2):
+            tr.train_step()
+    torch.cuda.synchronize()
+    assert int(a.stage.tag.item()) == int(a.cursor.item()) == 9
+    assert torch.equal(a.flat_params, b.flat_params)
+    assert torch.equal(a.flat_momentum, b.flat_momentum)
+    assert torch.equal(a.lab, b.lab)
+
+
+@pytest.mark.parametrize("B", [64, 37])
+def test_round3_step_matches_round2_step(lib, B):
+    """chunked conv backward + fc SGD fused into fc1_bwd + staged batches vs the round-2
+    step (per-sample slab, SGD in the tail, gathered batches): same training trajectory up to
+    summation order; fc gradients stored identically."""
+    n = 8 * B
+    x, y = _data(n, seed=300 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(5)).to(torch.int32)
+    new = _stage_trainer(x, y, perm, B=B)
+    old = _stage_trainer(x, y, perm, B=B, conv_chunk=1, fc_sgd="tail", stage_batches=False)
+    for _ in range(5):
+        new.train_step()
+        old.train_step()
+    torch.cuda.synchronize()
+    assert int(new.cursor.item()) == int(old.cursor.item()) == 5
+    assert _rel(new.flat_params, old.flat_params) < 1e-6
+    assert _rel(new.flat_momentum, old.flat_momentum) < 1e-5
+    assert abs(new.loss() - old.loss()) < 1e-5 * max(1.0, abs(old.loss()))
+    ce = new.layout.conv_end
+    assert _rel(new.flat_grads[ce:], old.flat_grads[ce:]) < 1e-5
+    assert _rel(new.flat_grads[:ce], old.flat_grads[:ce]) < 1e-5

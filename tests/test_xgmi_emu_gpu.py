@@ -43,8 +43,9 @@ def test_mean_allreduce(world, n):
         emu.close()
 
 
-@pytest.mark.parametrize("world,nblk", [(2, 128), (4, 128), (8, 128), (2, 256)])
-def test_fused_sgd_with_slab(world, nblk):
+@pytest.mark.parametrize("world,nblk,chunked", [(2, 128, False), (4, 128, False), (8, 128, False),
+                                                (2, 256, False), (2, 256, True), (8, 128, True)])
+def test_fused_sgd_with_slab(world, nblk, chunked):
     from pytorch_operator_amd.models.mnist import flat_layout
     dev = torch.device("cuda", 0)
     L = flat_layout().total
@@ -60,14 +61,19 @@ def test_fused_sgd_with_slab(world, nblk):
         for step in range(4):
             grads = [torch.randn(L, generator=g).to(dev) for _ in range(world)]
             slabs = [torch.randn(B, ce, generator=g).to(dev) for _ in range(world)]
+            # chunked: the conv2.weight columns hold conv_bwd4's 16 chunk rows (rows 16.. unused)
+            lo = flat_layout().offsets["conv2.weight"]
+            big = (B // 4, lo, lo + 25000) if chunked else None
             emu.configure(1, grads, ps, ms, slab=slabs, slab_rows=B, conv_n=ce, lr=lr, momentum=mom,
-                          first_step=step == 0)
+                          first_step=step == 0, slab_big=big)
             emu.launch()
             torch.cuda.synchronize()
             mean = torch.zeros(L, device=dev)
             for gr, sl in zip(grads, slabs):
                 full = gr.clone()
                 full[:ce] = sl.sum(0)
+                if chunked:
+                    full[lo:lo + 25000] = sl[:B // 4, lo:lo + 25000].sum(0)
                 mean += full
             mean /= world
             m_ref = mean.clone() if step == 0 else mom * m_ref + mean

@@ -66,6 +66,23 @@ def main():
                                                     lr=0.0, momentum=0.5)),
         ("tail_sgd", lambda: tail(tr, B)),
     ]
+    fp, fm, fg = tr._fc_dicts()
+    lay = tr.layout
+    launches += [
+        ("conv_bwd4", lambda: K.conv_bwd4(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn, tr.conv_slab,
+                                          lay.offsets, B)),
+        ("fc1_bwd_sgd", lambda: K.fc1_bwd_sgd(tr.dh, tr.a2, tr.idx2, p["fc1.weight"], tr.dlogits, tr.h1,
+                                              dz2=tr.dz2, w1_next=tr.w1_next, params=fp, bufs=fm, grads=fg,
+                                              per_sample=tr.per_sample, stats=tr.stats, lr=0.0, momentum=0.5,
+                                              src=src, stage=tr.stage, stage_adv=0)),
+        ("tail4_copy", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:lay.conv_end],
+                                                  tr.flat_momentum[:lay.conv_end], lr=0.0, momentum=0.5,
+                                                  big=K.conv_bwd4_rows(B, lay.offsets),
+                                                  copy=(p["fc1.weight"].reshape(-1), tr.w1_next.reshape(-1)))),
+        ("conv12_staged", lambda: K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
+                                               p["conv2.bias"], B, a1=tr.a1, idx1=tr.idx1, xn=tr.xn, lab=tr.lab,
+                                               a2=tr.a2, idx2=tr.idx2, stage=tr.stage)),
+    ]
     reps = 20
     for name, fn in launches:
         spans, phase_means, phase_maxs = [], None, None

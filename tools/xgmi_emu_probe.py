@@ -4,6 +4,8 @@
 For each buffer allocation kind and world size: us per fused launch (graph of 50
 back-to-back launches) and, for one stamped launch, the mean/max per-block phase times
 (produce+push | wait flags1 + reduce/SGD + push | wait flags2 + gather) and the span.
+XAR_SLAB=chunk (default): the conv2.weight slab columns hold conv_bwd4's ceil(B/4) chunk rows
+(the round-3 step); XAR_SLAB=sample: B per-sample rows everywhere (round 1-2).
 Prints one JSON line per configuration.
 """
 from __future__ import annotations
@@ -27,7 +29,9 @@ def main() -> int:
     worlds = [int(w) for w in os.environ.get("XAR_WORLDS", "2,8").split(",")]
     nblks = [int(b) for b in os.environ.get("XAR_NBLK", "128").split(",")]
     fences = [int(f) for f in os.environ.get("XAR_FENCE", "-1").split(",")]
-    for kind, fence in [(k, f) for k in kinds for f in fences]:
+    slab_modes = os.environ.get("XAR_SLAB", "chunk").split(",")
+    lo = flat_layout().offsets["conv2.weight"]
+    for kind, fence, sm in [(k, f, m) for k in kinds for f in fences for m in slab_modes]:
         for world in worlds:
             for nblk in nblks:
                 emu = XgmiEmulation(world, L, nblk=nblk, alloc_kind=kind, fence=fence)
@@ -35,7 +39,8 @@ def main() -> int:
                 ms = [torch.zeros(L, device=dev) for _ in range(world)]
                 grads = [torch.randn(L, device=dev) for _ in range(world)]
                 slabs = [torch.randn(B, ce, device=dev) for _ in range(world)]
-                cfg = dict(slab=slabs, slab_rows=B, conv_n=ce, lr=0.0, momentum=0.5)
+                cfg = dict(slab=slabs, slab_rows=B, conv_n=ce, lr=0.0, momentum=0.5,
+                           slab_big=((B + 3) // 4, lo, lo + 25000) if sm == "chunk" else None)
                 emu.configure(1, grads, ps, ms, **cfg)
                 emu.launch()
                 torch.cuda.synchronize()
@@ -58,7 +63,7 @@ def main() -> int:
                 s = st.view(world, nblk, 4).double().cpu() / 100.0  # us (100 MHz)
                 t0 = s[..., 0].min()
                 ph = s[..., 1:] - s[..., :-1]
-                res = {"alloc_kind": kind, "fence": fence, "world": world, "nblk": nblk,
+                res = {"alloc_kind": kind, "fence": fence, "slab": sm, "world": world, "nblk": nblk,
                        "us_per_launch": round(best / 50 * 1e6, 2),
                        "span_us": round(float(s[..., 3].max() - t0), 2),
                        "start_skew_us": round(float(s[..., 0].max() - t0), 2),
