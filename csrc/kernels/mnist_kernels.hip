@@ -39,18 +39,6 @@
 
 using namespace pto;
 
-// Experiment switches (tools/build_exp.sh builds -D variants for same-box A/B; defaults = the
-// measured winners, profiles/r3_*)
-#ifndef PTO_C1_ROLES
-#define PTO_C1_ROLES 1      // conv12: conv1 MFMA tiles and VALU windows on separate waves
-#endif
-#ifndef PTO_C12_DEFER_W2
-#define PTO_C12_DEFER_W2 1  // conv12: conv2 weight slice lands in LDS after conv1
-#endif
-#ifndef PTO_B4_SPLIT
-#define PTO_B4_SPLIT 1      // conv_bwd4: chunk samples' loads overlap phase 2a
-#endif
-
 namespace {
 
 typedef unsigned long long u64;
@@ -446,9 +434,8 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float wv = w1[min(tid, 499)];
     const float bv1 = b1[min(tid, 19)];
-    // the conv2 weight slice is only needed after conv1: its loads stay in flight through the
-    // conv1 phase and land in LDS right before the conv1 -> conv2 barrier (issued after the
-    // image / conv1 loads, so waiting for those does not wait for these)
+    // conv2 weight slice of this output-channel group (measured: landing it after conv1
+    // instead, with its loads in flight through conv1, was no faster -- profiles/r3_*)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int e = min(tid + k * AB_NT, 16 * 125 - 1);
@@ -459,9 +446,7 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     if (tid < 784) img[(tid / 28) * AB_IRS + tid % 28] = x0;
     if (tid < 500) w1s[tid] = wv;
     if (tid < 20) w1s[500 + tid] = bv1;
-#if !PTO_C12_DEFER_W2
     conv12_store_w2(w_s, wq, cg, tid);
-#endif
     if (pub && tid < 784) {
       xn_out[(size_t)b * 784 + tid] = x0;
       if (tid == 0 && lab_out != nullptr) lab_out[b] = lab;
@@ -471,12 +456,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   stamp(dbg, 1);
   // conv1 + bias + ReLU + 2x2 max-pool.  Channels 0-15: implicit GEMM on MFMA, 36
   // position tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 7 K-steps (25 taps,
-  // zero-padded to 28 through the weight fragments).  The pool epilogue is the same
-  // register/lane^32 pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU.
-  // Wave roles (any 8 consecutive waves cover every SIMD twice): waves 0-7 run the MFMA
-  // tiles -- wave w takes tiles w, w+8, .. (5 for w < 4, 4 otherwise: 9 per SIMD, 4-5
-  // independent accumulator chains per wave) -- while waves 8-15 run 512 of the VALU windows
-  // at the same time; the last 64 windows go to lanes 0-15 of waves 4-7 (one tile short).
+  // zero-padded to 28 through the weight fragments); wave w takes tiles w, w+16 (+ w+32
+  // for w < 4): 9 tiles per SIMD.  The pool epilogue is the same register/lane^32
+  // pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
+  // (Measured: giving the MFMA tiles and the VALU windows to disjoint waves was no faster.)
   {
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
@@ -492,24 +475,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
-#if PTO_C1_ROLES
-    if (wv < 4) {
-      conv1_tasks<5, 8>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
-    } else if (wv < 8) {
-      conv1_tasks<4, 8>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
-      if (lane < 16) conv1_valu_window(512 + (wv - 4) * 16 + lane, img, w1s, in_s, pub, a1, idx1, b);
-    } else {
-      conv1_valu_window(tid - 512, img, w1s, in_s, pub, a1, idx1, b);
-    }
-#else
     conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
-#endif
   }
-#if PTO_C12_DEFER_W2
-  conv12_store_w2(w_s, wq, cg, tid);  // the conv2 weight slice (loaded before conv1)
-#endif
   __syncthreads();
   stamp(dbg, 2);
 
@@ -1841,6 +1810,78 @@ constexpr int G_OFF_RED = G_OFF_W + 5 * F_Z1;
 static_assert(G_LDS * 4 <= 160 * 1024, "conv_bwd4 LDS budget");
 static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
 
+#ifndef PTO_PIPE
+#define PTO_PIPE 1  // software-pipelined LDS operand reads in conv_bwd4 phase 2 (0: read-all-then-MFMA)
+#endif
+
+// Phase 2 of conv_bwd4 for one wave, software-pipelined: the LDS operand reads of chunk c+1
+// are issued before the MFMAs of chunk c (sched_barrier groups; the compiler's counted
+// lgkmcnt waits then only wait for chunk c), so every wave keeps its MFMA chain and its next
+// reads in flight together instead of all 16 waves alternating read bursts and MFMA bursts.
+//   DO_A: 2a, dcolT tiles (jt0, jt0+1) x position tile pt, K = 52 co in chunks of 4 k-steps
+//   DO_B: 2b, dW_conv2 tile pair tp over K half kh2 (32 k-steps, chunks of 8)
+template <bool DO_A, bool DO_B>
+__device__ __forceinline__ void bwd4_phase2(const float* dzc_s, const float* w_s, float* dcol_s,
+                                            const float* a1c_s, int r, int wv, int lane, int jbase,
+                                            int c0, f32x4& gacc) {
+  const int i = lane & 15, g = lane >> 4;
+  const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
+  const float* qa_b = dzc_s + r * G_DZN + g * G_DZS + pt * 16 + i;
+  const float* qa_a = w_s + g * F_WS + jt0 * 16 + i;
+  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1, kh2 = wv / 6;
+  const int jc = min(max(jbase + jt * 16 + i, 0), 124);  // clamped: unstored columns read finite data
+  const int ci = jc / 25, t = jc - ci * 25;
+  const float* qb_a = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
+  const float* qb_b = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
+  float xa[2][13], ya[13], xb[32], yb[32];
+  f32x4 a0 = zero4(), a1 = zero4(), e0 = zero4(), e1 = zero4();
+#define B4_RA(c)                                                  \
+  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s)   \
+    if (s < 13) {                                                 \
+      ya[s] = qa_b[4 * s * G_DZS];                                \
+      xa[0][s] = qa_a[4 * s * F_WS];                              \
+      xa[1][s] = qa_a[4 * s * F_WS + 16];                         \
+    }
+#define B4_MA(c)                                                  \
+  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s)   \
+    if (s < 13) {                                                 \
+      a0 = mfma16x16x4(xa[0][s], ya[s], a0);                      \
+      a1 = mfma16x16x4(xa[1][s], ya[s], a1);                      \
+    }
+#define B4_RB(c)                                                  \
+  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
+    const int s_ = u >> 4, uu = u & 15;                           \
+    xb[u] = qb_a[s_ * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];  \
+    yb[u] = qb_b[s_ * G_DZN + 4 * uu];                            \
+  }
+#define B4_MB(c)                                                  \
+  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
+    if (u & 1) e1 = mfma16x16x4(xb[u], yb[u], e1);                \
+    else e0 = mfma16x16x4(xb[u], yb[u], e0);                      \
+  }
+#define B4_SB __builtin_amdgcn_sched_barrier(0);
+  if constexpr (DO_A) {
+    B4_RA(0) B4_SB B4_RA(1) B4_SB B4_MA(0) B4_SB B4_RA(2) B4_SB B4_MA(1) B4_SB B4_RA(3) B4_SB B4_MA(2) B4_SB
+    if constexpr (DO_B) { B4_RB(0) B4_SB }
+    B4_MA(3) B4_SB
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      dcol_s[(jt0 * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = a0[rr];
+      dcol_s[((jt0 + 1) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = a1[rr];
+    }
+    if constexpr (DO_B) { B4_RB(1) B4_SB B4_MB(0) B4_SB B4_RB(2) B4_SB B4_MB(1) B4_SB B4_RB(3) B4_SB B4_MB(2) B4_SB B4_MB(3) }
+  } else {
+    B4_RB(0) B4_SB B4_RB(1) B4_SB B4_MB(0) B4_SB B4_RB(2) B4_SB B4_MB(1) B4_SB B4_RB(3) B4_SB B4_MB(2) B4_SB B4_MB(3)
+  }
+#undef B4_RA
+#undef B4_MA
+#undef B4_RB
+#undef B4_MB
+#undef B4_SB
+  if constexpr (DO_B) gacc = e0 + e1;
+}
+static_assert(F_TPW == 2, "bwd4_phase2 holds two 2a tiles per wave");
+
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
@@ -1870,11 +1911,10 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   const int c0 = max(jbase, 0) / 25;  // first of the <= 2 input channels those columns touch
   stamp(dbg, 0);
 
-  // ---- phase 1: stage.  Group 1 (what 2a needs: the own sample's dz2 and the W2 slice) is
-  // loaded first and written to LDS before the first barrier; group 2 (the chunk's other
-  // three samples, the 2b im2col source, and the own a1 / idx1 / xn for phases 3-4) stays in
-  // flight through phase 2a and lands before the second barrier.  Every load independent and
-  // unpredicated (clamped addresses + selects).
+  // ---- phase 1: stage.  Group 1: the own sample's dz2 and the W2 slice; group 2: the chunk's
+  // other three samples, the 2b im2col source, the own a1 / idx1 / xn (measured: keeping group
+  // 2 in flight through phase 2a behind a second barrier was slower).  Every load independent
+  // and unpredicated (clamped addresses + selects).
   float4 dv2[3];
   float cv[2], av1;
   uint8_t iv1;
@@ -1888,7 +1928,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       const int co = min(e >> 7, 49), j = min(e & 127, 124);
       wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
     }
-    // group 2 (issued after group 1: waiting for group 1 leaves these in flight)
+    // group 2
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int e = min(tid + k * F_NT, 2399);
@@ -1951,12 +1991,26 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     }
     if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv1;
   };
-#if !PTO_B4_SPLIT
   stage_g2();
-#endif
   __syncthreads();
   stamp(dbg, 1);
 
+  // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
+  // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
+  //   waves 0-11: tile pair tp = wv % 6 (co tile ct = tp / 2 of 0..47, column tile jt = tp % 2),
+  //   K half wv / 6 (samples {0,1} or {2,3}); A = im2col (rows = columns jl), B = dz (cols = co).
+  //   waves 12-15: co 48 and 49 (a fourth 16-row tile would be 7/8 padding) as 256 VALU dot
+  //   products, one sample each, summed in sample order after the barrier.
+  f32x4 gacc = zero4();
+  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
+#if PTO_PIPE
+  if (wv < 12) {
+    if (own) bwd4_phase2<true, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
+    else bwd4_phase2<false, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
+    if (wv >= 6) pk_s[tp * 64 + lane] = gacc;
+  } else {
+    if (own) bwd4_phase2<true, false>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
+#else
   // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
   if (own) {
     const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
@@ -1982,17 +2036,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       for (int rr = 0; rr < 4; ++rr)
         dcol_s[((jt0 + n) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[n][rr];
   }
-#if PTO_B4_SPLIT
-  stage_g2();  // phase 1b: group 2 -> LDS (landed during 2a)
-#endif
-  __syncthreads();
-  // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
-  //   waves 0-11: tile pair tp = wv % 6 (co tile ct = tp / 2 of 0..47, column tile jt = tp % 2),
-  //   K half wv / 6 (samples {0,1} or {2,3}); A = im2col (rows = columns jl), B = dz (cols = co).
-  //   waves 12-15: co 48 and 49 (a fourth 16-row tile would be 7/8 padding) as 256 VALU dot
-  //   products, one sample each, summed in sample order after the barrier.
-  f32x4 gacc = zero4();
-  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
   if (wv < 12) {
     const int kh2 = wv / 6;
     const int jc = min(max(jbase + jt * 16 + i, 0), 124);  // clamped (unstored columns read finite data)
@@ -2016,6 +2059,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     gacc = e0 + e1;
     if (kh2 == 1) pk_s[tp * 64 + lane] = gacc;
   } else {
+#endif
     const int item = tid - 768;  // (sample s, co 48 + cr, column jl)
     const int s = item >> 6, cr = (item >> 5) & 1, jl = item & 31;
     const int jc = min(max(jbase + jl, 0), 124);
@@ -2086,7 +2130,39 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   __syncthreads();
   stamp(dbg, 3);
-  // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU (as conv_bwd_kernel)
+#ifndef PTO_DW1W
+#define PTO_DW1W 1  // phase 4 on 600 threads (one output row each) instead of 400 (3 half rows)
+#endif
+#if PTO_DW1W
+  // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU: 600 threads = (channel c, output row
+  // y, kernel row kh), each slides a 28-wide register window of input row y + kh across the
+  // 24 outputs of dz1 row y: 5 FMAs per LDS read of dz1; 24 row partials meet in LDS.
+  constexpr int NPART = 24;
+  if (tid < 600) {
+    const int c = tid / 120, rem = tid - c * 120;
+    const int y = rem / 5, kh = rem - y * 5;
+    const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
+    const float* xr = x_s + (y + kh) * F_XR;
+    float xw[28];
+#pragma unroll
+    for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float bs = 0.f;
+#pragma unroll
+    for (int x = 0; x < 24; ++x) {
+      const float a = zr[x];
+      bs += a;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
+    }
+    float* pr = red + y * F_RED1;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
+    if (kh == 0) pr[125 + c] = bs;
+  }
+  static_assert(5 * F_Z1 + NPART * F_RED1 <= 52 * F_WS, "phase-4 partials alias the W2 slice");
+#else
+  constexpr int NPART = 16;
   if (tid < 400) {
     const int c = tid / 80, rem = tid - c * 80;
     const int part = rem / 5, kh = rem - part * 5;
@@ -2114,6 +2190,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
     if (kh == 0) pr[125 + c] = bs;
   }
+#endif
   __syncthreads();
   stamp(dbg, 4);
   // ---- epilogue: sample b's small partials into slab row b
@@ -2121,7 +2198,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   if (tid < 130) {
     float w1sum = 0.f;
 #pragma unroll
-    for (int qq = 0; qq < 16; ++qq) w1sum += red[qq * F_RED1 + tid];
+    for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
     if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
     else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
   }

@@ -1,6 +1,9 @@
 #include "pto/kube.hpp"
 
 #include <poll.h>
+#include <algorithm>
+#include <cerrno>
+#include <signal.h>
 #include <spawn.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -91,7 +94,11 @@ bool run_exec_plugin(const ExecPlugin& plugin, KubeConfig* kc, std::string* erro
   std::string text;
   char buf[4096];
   struct pollfd p{out[0], POLLIN, 0};
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+  // one deadline for output AND exit (client-go's exec credential timeout is 60 s too);
+  // PTO_EXEC_PLUGIN_TIMEOUT_S overrides it (tests)
+  long timeout_s = 60;
+  if (const char* t = std::getenv("PTO_EXEC_PLUGIN_TIMEOUT_S")) timeout_s = std::max(1L, std::atol(t));
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
   while (std::chrono::steady_clock::now() < deadline) {
     if (::poll(&p, 1, 200) <= 0) continue;
     const ssize_t n = ::read(out[0], buf, sizeof buf);
@@ -99,8 +106,26 @@ bool run_exec_plugin(const ExecPlugin& plugin, KubeConfig* kc, std::string* erro
     text.append(buf, (size_t)n);
   }
   close(out[0]);
+  // reap without blocking past the deadline: a plugin that hangs (with or without its stdout
+  // open) is killed, so a reconcile worker refreshing credentials never blocks forever
   int status = 0;
-  waitpid(pid, &status, 0);
+  bool exited = false;
+  while (true) {
+    const pid_t w = waitpid(pid, &status, WNOHANG);
+    if (w == pid || (w < 0 && errno != EINTR)) {
+      exited = w == pid;
+      break;
+    }
+    if (std::chrono::steady_clock::now() >= deadline) break;
+    ::poll(nullptr, 0, 20);
+  }
+  if (!exited) {
+    ::kill(pid, SIGKILL);
+    while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+    }
+    *error = "exec plugin " + plugin.command + " timed out after " + std::to_string(timeout_s) + " s (killed)";
+    return false;
+  }
   if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) {
     *error = "exec plugin " + plugin.command + " failed (status " + std::to_string(status) + ")";
     return false;

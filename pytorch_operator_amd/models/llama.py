@@ -207,4 +207,5 @@ class Llama(nn.Module):
         if targets is None:
             return logits
         from ..ops.llm import cross_entropy
-        return cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))
+        # the logits are this op's own intermediate: d(logits) may overwrite them
+        return cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1), overwrite_logits=True)

@@ -42,18 +42,31 @@ class Configuration:
     extra_headers: Dict[str, str] = field(default_factory=dict)
     exec_plugin: Optional[ExecPlugin] = None
     _exec_expiry: float = 0.0
+    _exec_files: Optional[tuple] = None  # (cert, key) paths of the plugin's last client certificate
+
+    def _has_exec_credential(self) -> bool:
+        return bool(self.token) or self._exec_files is not None
 
     def refresh_credentials(self, force: bool = False) -> None:
-        """Run the exec credential plugin when there is one and its credential expired."""
-        if self.exec_plugin is None or (not force and self.token and time.time() < self._exec_expiry):
+        """Run the exec credential plugin when there is one and its credential (a token or a
+        client certificate) is missing or expired."""
+        if self.exec_plugin is None or (not force and self._has_exec_credential() and
+                                        time.time() < self._exec_expiry):
             return
         cred = run_exec_plugin(self.exec_plugin)
         st = cred.get("status") or {}
         if st.get("token"):
             self.token = st["token"]
         if st.get("clientCertificateData") and st.get("clientKeyData"):
-            self.cert_file = _materialise_text(st["clientCertificateData"])
-            self.key_file = _materialise_text(st["clientKeyData"])
+            # one pair of files per Configuration, rewritten in place on refresh and removed at
+            # exit (the key is a secret: never leave one temp file per request behind)
+            if self._exec_files is None:
+                self._exec_files = (_new_private_file(".crt"), _new_private_file(".key"))
+                import atexit
+                atexit.register(_remove_files, self._exec_files)
+            _write_private(self._exec_files[0], st["clientCertificateData"])
+            _write_private(self._exec_files[1], st["clientKeyData"])
+            self.cert_file, self.key_file = self._exec_files
         exp = st.get("expirationTimestamp")
         self._exec_expiry = _parse_rfc3339(exp) - 10 if exp else float("inf")
 
@@ -79,11 +92,26 @@ def _parse_rfc3339(s: str) -> float:
     return float(calendar.timegm(time.strptime(s, "%Y-%m-%dT%H:%M:%S")))
 
 
-def _materialise_text(pem: str) -> str:
-    f = tempfile.NamedTemporaryFile(delete=False, suffix=".pem", mode="w")
-    f.write(pem)
-    f.close()
-    return f.name
+def _new_private_file(suffix: str) -> str:
+    fd, path = tempfile.mkstemp(suffix=suffix, prefix="pytorchjob-exec-")  # mode 0600
+    os.close(fd)
+    return path
+
+
+def _write_private(path: str, text: str) -> None:
+    tmp = path + ".tmp"
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    with os.fdopen(fd, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
+def _remove_files(paths) -> None:
+    for p in paths:
+        try:
+            os.unlink(p)
+        except OSError:
+            pass
 
 
 def _materialise(data_b64: Optional[str]) -> Optional[str]:

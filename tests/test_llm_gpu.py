@@ -193,19 +193,22 @@ def test_swiglu_packed_matches_reference(dtype, shape):
     torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
 
 
+@pytest.mark.parametrize("overwrite", [True, False])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,v", [(64, 256), (7, 1000), (5, 128256)])
-def test_cross_entropy_matches_reference(dtype, n, v):
-    """Fused HIP cross-entropy (loss + in-place d(logits)) vs fp32 F.cross_entropy, with
-    ignored (-100) targets and large-magnitude logits (the online max must rescale)."""
+def test_cross_entropy_matches_reference(dtype, n, v, overwrite):
+    """Fused HIP cross-entropy (loss + d(logits), in place or into a new tensor) vs fp32
+    F.cross_entropy, with ignored (-100) targets and large-magnitude logits (the online max
+    must rescale).  The default keeps the caller's logits intact."""
     from pytorch_operator_amd.ops.llm import cross_entropy
     g = torch.Generator(device="cpu").manual_seed(7)
     x = (torch.randn(n, v, generator=g) * 8).to(dtype)
     t = torch.randint(0, v, (n,), generator=g)
     t[1] = -100
     xg = x.cuda().requires_grad_(True)
-    y = xg * 1  # the op overwrites its (intermediate) input with the gradient
-    loss = cross_entropy(y, t.cuda())
+    y = xg * 1  # an intermediate (overwritten by the backward when overwrite=True)
+    y_before = y.detach().clone()
+    loss = cross_entropy(y, t.cuda(), overwrite_logits=overwrite)
     (loss * 3).backward()
     xr = x.float().requires_grad_(True)
     lr = torch.nn.functional.cross_entropy(xr, t, ignore_index=-100)
@@ -214,6 +217,10 @@ def test_cross_entropy_matches_reference(dtype, n, v):
     torch.testing.assert_close(loss.cpu(), lr, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, **tol)
     assert xg.grad[1].abs().max().item() == 0
+    if not overwrite:
+        assert torch.equal(y.detach(), y_before)  # the caller may still read its logits
+    else:
+        assert y._version > y_before._version  # reuse of the overwritten logits is detectable
 
 
 @pytest.mark.parametrize("shape", [(64, 128), (8192 // 8, 28672 // 8), (192, 64)])

@@ -247,3 +247,64 @@ def test_operator_rejects_unloadable_credentials(pki, tmp_path):
         assert "key values mismatch" in log.read_text() or "do not match" in log.read_text()
     finally:
         api.stop()
+
+
+# ---------------------------------------------------------------------------- exec plugin hygiene
+def test_sdk_cert_only_exec_plugin_runs_once_and_reuses_one_key_file(pki, tmp_path):
+    """A plugin that returns only a client certificate is not rerun on every request (the
+    credential check looks at any credential, not just a token), and its key lands in one
+    private file per Configuration, rewritten in place."""
+    from kubeflow.pytorchjob.configuration import ExecPlugin, Configuration
+    crt, key = pki["client"]
+    counter = tmp_path / "runs"
+    script = tmp_path / "cert_plugin.py"
+    script.write_text(
+        "import json, os, sys\n"
+        f"open({str(counter)!r}, 'a').write('x')\n"
+        f"crt = open({crt!r}).read(); key = open({key!r}).read()\n"
+        "print(json.dumps({'apiVersion': 'client.authentication.k8s.io/v1', 'kind': 'ExecCredential',"
+        " 'status': {'clientCertificateData': crt, 'clientKeyData': key}}))\n")
+    cfg = Configuration(host="https://127.0.0.1:1", exec_plugin=ExecPlugin(command=sys.executable, args=[str(script)]))
+    cfg.refresh_credentials(force=True)
+    first = (cfg.cert_file, cfg.key_file)
+    for _ in range(5):
+        cfg.refresh_credentials()
+    assert counter.read_text() == "x"  # ran once
+    assert os.stat(cfg.key_file).st_mode & 0o077 == 0
+    cfg.refresh_credentials(force=True)  # a forced refresh rewrites the same two files
+    assert (cfg.cert_file, cfg.key_file) == first and counter.read_text() == "xx"
+    assert open(cfg.key_file).read() == open(key).read()
+
+
+def test_operator_kills_a_hanging_exec_plugin(pki, tmp_path):
+    """An exec credential plugin that never exits is killed at the deadline (here
+    PTO_EXEC_PLUGIN_TIMEOUT_S=2) instead of blocking the operator forever in waitpid."""
+    api = _server(pki)
+    pidfile = tmp_path / "plugin.pid"
+    script = tmp_path / "hang.py"
+    script.write_text(f"import os, time\nopen({str(pidfile)!r}, 'w').write(str(os.getpid()))\ntime.sleep(600)\n")
+    kc = api.write_kubeconfig(str(tmp_path / "kc-hang.json"), ca_file=pki["ca"], token=None,
+                              exec_plugin={"apiVersion": "client.authentication.k8s.io/v1",
+                                           "command": sys.executable, "args": [str(script)]})
+    env = dict(os.environ, KUBEFLOW_NAMESPACE="kubeflow", PTO_EXEC_PLUGIN_TIMEOUT_S="2")
+    env.pop("KUBECONFIG", None)
+    log = tmp_path / "op-hang.log"
+    try:
+        t0 = time.time()
+        with open(log, "wb") as lf:
+            p = subprocess.Popen([operator_binary(), "--kubeconfig", kc, f"--monitoring-port={free_port()}",
+                                  "--json-log-format=false"], env=env, stdout=lf, stderr=subprocess.STDOUT,
+                                 start_new_session=True)
+        try:
+            p.wait(30)
+        except subprocess.TimeoutExpired:
+            _stop(p)
+            raise AssertionError("operator blocked on the hung plugin:\n" + log.read_text()[-2000:])
+        assert time.time() - t0 < 25
+        assert p.returncode != 0
+        assert "timed out" in log.read_text(), log.read_text()[-2000:]
+        pid = int(pidfile.read_text())
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)  # killed and reaped
+    finally:
+        api.stop()
