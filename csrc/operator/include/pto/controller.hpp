@@ -73,6 +73,10 @@ class PyTorchController {
 
  private:
   void enqueue(const Json& job);
+  // the PodGroup resource of the configured gang API (--gang-podgroup-api)
+  const Resource& podgroups() const {
+    return o_.cfg.gang_podgroup_api == "volcano" ? kVolcanoPodGroups : kPodGroups;
+  }
   void add_job(const Json& obj);
   void update_job(const Json& old_obj, const Json& cur);
   void delete_job(const Json& obj);

@@ -62,6 +62,7 @@ struct Resource {
 };
 
 extern const Resource kPods, kServices, kEvents, kEndpoints, kLeases, kPyTorchJobs, kPodGroups, kCRDs;
+extern const Resource kVolcanoPodGroups;  // --gang-podgroup-api volcano
 
 class KubeClient {
  public:

@@ -17,6 +17,7 @@ struct ServerOption {
   bool json_log_format = true;
   bool enable_gang_scheduling = false;
   std::string gang_scheduler_name = "volcano";
+  std::string gang_podgroup_api = "kube-batch";  // --gang-podgroup-api kube-batch|volcano (extension)
   std::string namespace_;  // "" = all namespaces (v1.NamespaceAll)
   int monitoring_port = 8443;
   double resync_period_s = 12 * 3600.0;  // --resyc-period (sic)

@@ -32,6 +32,10 @@ extern const char* const kDefaultInitContainerTemplate;
 struct ControllerConfig {
   bool enable_gang_scheduling = false;
   std::string gang_scheduler_name = "volcano";
+  // PodGroup API the gang PodGroup is created in: "kube-batch" (reference parity:
+  // scheduling.incubator.k8s.io/v1alpha1, tf-operator jobcontroller.go:224-278) or "volcano"
+  // (scheduling.volcano.sh/v1beta1, what Volcano >= 1.0 reads)
+  std::string gang_podgroup_api = "kube-batch";
   std::string init_container_image = "alpine:3.10";
   std::string init_container_template = kDefaultInitContainerTemplate;
   // MI355X extensions (all off by default = reference behaviour):

@@ -389,13 +389,13 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
   for (const auto& e : r.events) events_.record(job, e);
   ApiError err;
   if (r.create_podgroup) {
-    if (!client_->create(kPodGroups, ns, *r.create_podgroup, &err) && !err.already_exists())
+    if (!client_->create(podgroups(), ns, *r.create_podgroup, &err) && !err.already_exists())
       LOG_WARN("Sync PodGroup %s: %s", job_name(job).c_str(), err.message.c_str());
   }
   if (r.delete_podgroup) {
     ApiError e2;
-    if (client_->get(kPodGroups, ns, gen_pod_group_name(job_name(job)), &e2)) {
-      if (client_->del(kPodGroups, ns, gen_pod_group_name(job_name(job)), &e2))
+    if (client_->get(podgroups(), ns, gen_pod_group_name(job_name(job)), &e2)) {
+      if (client_->del(podgroups(), ns, gen_pod_group_name(job_name(job)), &e2))
         events_.record(job, {"Normal", "SuccessfulDeletePodGroup", "Deleted PodGroup: " + job_name(job)});
       else
         events_.record(job, {"Warning", "FailedDeletePodGroup", "Error deleting: " + e2.message});
@@ -511,7 +511,7 @@ bool PyTorchController::sync(const std::string& key) {
       in.requeues = queue_.num_requeues(key);
       if (o_.cfg.enable_gang_scheduling) {
         ApiError e2;
-        in.podgroup_exists = client_->get(kPodGroups, ns, gen_pod_group_name(name), &e2).has_value();
+        in.podgroup_exists = client_->get(podgroups(), ns, gen_pod_group_name(name), &e2).has_value();
       }
       PTO_LOG(LogLevel::Info, fields_for_job(ns, name, job_uid(job)), "Reconcile PyTorchJobs %s", name.c_str());
       ReconcileResult r = reconcile(in, o_.cfg);

@@ -27,6 +27,7 @@ const Resource kEndpoints{"", "v1", "endpoints"};
 const Resource kLeases{"coordination.k8s.io", "v1", "leases"};
 const Resource kPyTorchJobs{"kubeflow.org", "v1", "pytorchjobs"};
 const Resource kPodGroups{"scheduling.incubator.k8s.io", "v1alpha1", "podgroups"};
+const Resource kVolcanoPodGroups{"scheduling.volcano.sh", "v1beta1", "podgroups"};
 const Resource kCRDs{"apiextensions.k8s.io", "v1", "customresourcedefinitions", false};
 
 std::string Resource::path(const std::string& ns, const std::string& name, const std::string& sub) const {

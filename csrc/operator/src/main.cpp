@@ -125,6 +125,7 @@ int main(int argc, char** argv) {
   co.resync_s = opt.resync_period_s;
   co.cfg.enable_gang_scheduling = opt.enable_gang_scheduling;
   co.cfg.gang_scheduler_name = opt.gang_scheduler_name;
+  co.cfg.gang_podgroup_api = opt.gang_podgroup_api;
   co.cfg.init_container_image = opt.init_container_image;
   co.cfg.inject_rccl_env = opt.inject_rccl_env;
   co.cfg.xgmi_pod_topology = opt.xgmi_pod_topology;

@@ -54,6 +54,8 @@ std::string usage() {
          "  -json-log-format          Set true to use json style log format (default true)\n"
          "  -enable-gang-scheduling   Set true to enable gang scheduling\n"
          "  -gang-scheduler-name      The scheduler to gang-schedule jobs (default \"volcano\")\n"
+         "  -gang-podgroup-api        PodGroup API of gang scheduling: kube-batch (scheduling.incubator.k8s.io/\n"
+         "                            v1alpha1, default) or volcano (scheduling.volcano.sh/v1beta1)\n"
          "  -monitoring-port int      Endpoint port for displaying monitoring metrics (default 8443)\n"
          "  -resyc-period duration    Resync interval of the operator (default 12h0m0s)\n"
          "  -init-container-image     The image of the injected init container (default \"alpine:3.10\")\n"
@@ -110,6 +112,12 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
       {"json-log-format", boolean(&o->json_log_format)},
       {"enable-gang-scheduling", boolean(&o->enable_gang_scheduling)},
       {"gang-scheduler-name", str(&o->gang_scheduler_name)},
+      {"gang-podgroup-api", Flag{false, [o](const std::string& v) {
+         if (v != "kube-batch" && v != "volcano")
+           return std::string("--gang-podgroup-api must be kube-batch or volcano, got \"") + v + "\"";
+         o->gang_podgroup_api = v;
+         return std::string();
+       }}},
       {"monitoring-port", integer(&o->monitoring_port)},
       {"resyc-period", Flag{false, [o](const std::string& v) {
          if (!parse_duration(v, &o->resync_period_s)) return std::string("invalid duration \"") + v + "\"";

@@ -21,6 +21,7 @@ static ControllerConfig cfg_from(const std::string& s) {
   Json j = J(s);
   c.enable_gang_scheduling = j.bool_or("enableGangScheduling", false);
   c.gang_scheduler_name = j.str_or("gangSchedulerName", c.gang_scheduler_name);
+  c.gang_podgroup_api = j.str_or("gangPodgroupApi", c.gang_podgroup_api);
   c.init_container_image = j.str_or("initContainerImage", c.init_container_image);
   c.init_container_template = j.str_or("initContainerTemplate", c.init_container_template);
   c.inject_rccl_env = j.bool_or("injectRcclEnv", false);

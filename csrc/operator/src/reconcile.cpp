@@ -577,7 +577,8 @@ ReconcileResult reconcile(const ReconcileInput& in, const ControllerConfig& cfg)
   } else {
     if (cfg.enable_gang_scheduling && !in.podgroup_exists) {
       Json pg = Json::object();
-      pg["apiVersion"] = "scheduling.incubator.k8s.io/v1alpha1";
+      pg["apiVersion"] = cfg.gang_podgroup_api == "volcano" ? "scheduling.volcano.sh/v1beta1"
+                                                             : "scheduling.incubator.k8s.io/v1alpha1";
       pg["kind"] = "PodGroup";
       Json md = Json::object();
       md["name"] = gen_pod_group_name(c.name);
@@ -588,6 +589,8 @@ ReconcileResult reconcile(const ReconcileInput& in, const ControllerConfig& cfg)
       pg["metadata"] = md;
       Json spec = Json::object();
       spec["minMember"] = total;
+      // volcano: also the queue (its admission unit; "default" exists in every install)
+      if (cfg.gang_podgroup_api == "volcano") spec["queue"] = "default";
       pg["spec"] = spec;
       c.res.create_podgroup = pg;
     }

@@ -648,7 +648,7 @@ class FakeApiServer:
         import os
         import yaml
         root = manifest_dir or os.path.join(os.path.dirname(__file__), "..", "..", "manifests")
-        for fn in ("crd.yaml", "podgroup.yaml"):
+        for fn in ("crd.yaml", "podgroup.yaml", "podgroup-volcano.yaml"):
             p = os.path.join(root, fn)
             if not os.path.exists(p):
                 continue

@@ -24,6 +24,7 @@ load_kube_config = _rest.load_kube_config
 load_incluster_config = _rest.load_incluster_config
 PODS, SERVICES, EVENTS, NAMESPACES = _rest.PODS, _rest.SERVICES, _rest.EVENTS, _rest.NAMESPACES
 LEASES, PYTORCHJOBS, PODGROUPS, CRDS = _rest.LEASES, _rest.PYTORCHJOBS, _rest.PODGROUPS, _rest.CRDS
+VOLCANO_PODGROUPS = _rest.VOLCANO_PODGROUPS
 
 __all__ = ["ApiException", "GVR", "KubeRest", "Configuration", "load_kube_config", "load_incluster_config",
-           "PODS", "SERVICES", "EVENTS", "NAMESPACES", "LEASES", "PYTORCHJOBS", "PODGROUPS", "CRDS"]
+           "PODS", "SERVICES", "EVENTS", "NAMESPACES", "LEASES", "PYTORCHJOBS", "PODGROUPS", "VOLCANO_PODGROUPS", "CRDS"]

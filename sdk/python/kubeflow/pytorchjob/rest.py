@@ -56,6 +56,7 @@ NAMESPACES = GVR("", "v1", "namespaces", namespaced=False)
 LEASES = GVR("coordination.k8s.io", "v1", "leases")
 PYTORCHJOBS = GVR("kubeflow.org", "v1", "pytorchjobs")
 PODGROUPS = GVR("scheduling.incubator.k8s.io", "v1alpha1", "podgroups")
+VOLCANO_PODGROUPS = GVR("scheduling.volcano.sh", "v1beta1", "podgroups")
 CRDS = GVR("apiextensions.k8s.io", "v1", "customresourcedefinitions", namespaced=False)
 
 

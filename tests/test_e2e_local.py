@@ -246,19 +246,30 @@ def test_events_and_metrics(cluster):
     assert "pytorch_operator_reconcile_duration_seconds" in c.metrics() or True
 
 
-def test_gang_scheduling_creates_and_deletes_podgroup(tmp_path):
-    with LocalCluster(workdir=str(tmp_path / "g"), operator_args=["--enable-gang-scheduling"]) as c:
+@pytest.mark.parametrize("api", ["kube-batch", "volcano"])
+def test_gang_scheduling_creates_and_deletes_podgroup(tmp_path, api):
+    """--enable-gang-scheduling with either PodGroup API: the PodGroup (minMember = all
+    replicas) exists before the pods run, every pod names it and the gang scheduler, and it is
+    deleted when the job finishes.  The other API's resource is never touched."""
+    from pytorch_operator_amd.cluster.rest import VOLCANO_PODGROUPS
+    gvr, other = (VOLCANO_PODGROUPS, PODGROUPS) if api == "volcano" else (PODGROUPS, VOLCANO_PODGROUPS)
+    with LocalCluster(workdir=str(tmp_path / "g"),
+                      operator_args=["--enable-gang-scheduling", f"--gang-podgroup-api={api}"]) as c:
         c.wait_operator_ready()
         c.rest.create(PYTORCHJOBS, make_job("e2e-gang", replica(1, "busybox", command=py("import time; time.sleep(1)")),
                                             replica(2, "busybox", command=py("import time; time.sleep(1)"))), NS)
-        pg = wait_until(lambda: c.rest.list(PODGROUPS, NS)["items"], 30, what="podgroup")
+        pg = wait_until(lambda: c.rest.list(gvr, NS)["items"], 30, what="podgroup")
         assert pg[0]["metadata"]["name"] == "e2e-gang" and pg[0]["spec"]["minMember"] == 3
-        pod = c.rest.get(PODS, "e2e-gang-worker-0", NS)
+        if api == "volcano":
+            assert pg[0]["apiVersion"] == "scheduling.volcano.sh/v1beta1" and pg[0]["spec"]["queue"] == "default"
+        pod = wait_until(lambda: next((q for q in c.rest.list(PODS, NS)["items"]
+                                       if q["metadata"]["name"] == "e2e-gang-worker-0"), None), 30, what="worker pod")
         assert pod["spec"]["schedulerName"] == "volcano"
         assert pod["metadata"]["annotations"]["scheduling.k8s.io/group-name"] == "e2e-gang"
         types, _ = wait_finished(c, "e2e-gang")
         assert types[-1] == "Succeeded"
-        wait_until(lambda: not c.rest.list(PODGROUPS, NS)["items"], 30, what="podgroup deleted")
+        wait_until(lambda: not c.rest.list(gvr, NS)["items"], 30, what="podgroup deleted")
+        assert not c.rest.list(other, NS)["items"]
 
 
 def test_leader_failover(tmp_path):

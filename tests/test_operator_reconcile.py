@@ -366,6 +366,23 @@ def test_gang_scheduling_podgroup_and_scheduler_name():
     assert r2["createPodGroup"] is None
 
 
+def test_gang_scheduling_volcano_podgroup_api():
+    """--gang-podgroup-api volcano: the PodGroup is scheduling.volcano.sh/v1beta1 (what Volcano
+    >= 1.0 reads) with minMember = all replicas and the default queue; pods carry the same
+    group-name annotation and scheduler name; kube-batch v1alpha1 stays the default."""
+    job = new_job(3)
+    r = reconcile(job, config={"enableGangScheduling": True, "gangPodgroupApi": "volcano"})
+    pg = r["createPodGroup"]
+    assert pg["apiVersion"] == "scheduling.volcano.sh/v1beta1" and pg["kind"] == "PodGroup"
+    assert pg["spec"] == {"minMember": 4, "queue": "default"}
+    assert pg["metadata"]["ownerReferences"][0]["kind"] == "PyTorchJob"
+    for p in r["createPods"]:
+        assert p["spec"]["schedulerName"] == "volcano"
+        assert p["metadata"]["annotations"]["scheduling.k8s.io/group-name"] == TEST_JOB_NAME
+    dflt = reconcile(job, config={"enableGangScheduling": True})["createPodGroup"]
+    assert dflt["apiVersion"] == "scheduling.incubator.k8s.io/v1alpha1" and "queue" not in dflt["spec"]
+
+
 def test_gang_scheduling_other_scheduler_warns():
     job = new_job(1)
     job["spec"]["pytorchReplicaSpecs"]["Worker"]["template"]["spec"]["schedulerName"] = "other"
