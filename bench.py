@@ -62,8 +62,9 @@ def parse_args(argv=None):
                    help="single-GPU launch schedule (A/B): 5-launch fused or 6-launch classic")
     p.add_argument("--conv-chunk", type=int, default=4, choices=[1, 4],
                    help="conv backward: dW_conv2 per 4-sample chunk (slab 4x smaller) or per sample")
-    p.add_argument("--fc-sgd", default="tail", choices=["fused", "tail"],
-                   help="fc parameters' SGD inside fc1_bwd's weight-gradient tiles, or in the tail launch")
+    p.add_argument("--fc-sgd", default="tail", choices=["fused", "tail", "next"],
+                   help="fc parameters' SGD inside fc1_bwd's weight-gradient tiles, in the tail launch, "
+                        "or deferred into extra blocks of the next step's conv12 launch")
     p.add_argument("--stage", type=int, default=1, help="stage the next batch during fc1_bwd (1/0)")
     p.add_argument("--store-fc-grads", type=int, default=1,
                    help="fused fc SGD: also store the fc gradients (1/0)")
@@ -77,6 +78,11 @@ def parse_args(argv=None):
                    help="after the timed region, run one PyTorchJob with one pod per GPU through "
                         "the native operator + local cluster and report create->first-step (1/0)")
     p.add_argument("--job-timeout", type=float, default=150.0)
+    p.add_argument("--job-gpus", default="",
+                   help="node GPU ids of the job's pods, comma-separated (default 0..N-1); repeated ids "
+                        "let pods share a GPU (e.g. 0,0 on a 1-GPU box) and switch the job to gloo")
+    p.add_argument("--job-backend", default="",
+                   help="the job's torch.distributed backend (default rccl; gloo with shared GPUs)")
     p.add_argument("--prewarm-ms", type=int, default=40,
                    help="keep the GPU busy (FMA spin, no training state touched) this long before "
                         "the warm-up steps so the timed steps run at steady-state clocks "
@@ -84,7 +90,17 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def job_latency(world: int, rank: int, timeout: float) -> dict:
+def job_gpu_plan(world: int, job_gpus: str, job_backend: str):
+    """(node GPU ids, backend) of the bench's PyTorchJob: one pod per GPU over RCCL unless
+    ``job_gpus`` repeats an id (pods sharing a device need gloo: RCCL wants one GPU per rank)."""
+    gpus = [int(g) for g in job_gpus.split(",") if g.strip()] if job_gpus else list(range(world))
+    if len(gpus) != world:
+        raise ValueError(f"--job-gpus lists {len(gpus)} ids for {world} replicas")
+    backend = job_backend or ("gloo" if len(set(gpus)) < len(gpus) else "rccl")
+    return gpus, backend
+
+
+def job_latency(world: int, rank: int, timeout: float, gpus=None, backend: str = "rccl") -> dict:
     """create->first-step / create->Succeeded of a real job (BASELINE's second metric):
     fake API server -> pytorch-operator binary -> kubelet emulator -> ``world`` worker pods,
     each pinned to one GPU (HIP_VISIBLE_DEVICES narrowed like the amd.com/gpu plugin).
@@ -96,13 +112,18 @@ def job_latency(world: int, rank: int, timeout: float) -> dict:
         try:
             sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "benchmarks"))
             from job_latency import measure
-            r = measure(world, gpus=list(range(world)), backend="rccl", timeout=timeout)
+            r = measure(world, gpus=list(gpus) if gpus else list(range(world)), backend=backend,
+                        timeout=timeout)
             out = {"create_to_first_step_s": r["create_to_first_step_s"],
                    "create_to_running_s": r["create_to_running_s"],
                    "create_to_succeeded_s": r["create_to_succeeded_s"],
                    "job": {"replicas": r["replicas"], "result": r["result"],
-                           "gpus_per_pod": 1, "grad_allreduce": r["grad_allreduce"],
+                           "gpus_per_pod": 1, "node_gpus": list(gpus) if gpus else list(range(world)),
+                           "backend": backend, "grad_allreduce": r["grad_allreduce"],
                            "worker_samples_per_sec": r["worker_samples_per_sec"],
+                           "worker_step_ms": r.get("worker_step_ms"),
+                           "worker_train_seconds": r.get("worker_train_seconds"),
+                           "worker_capture_seconds": r.get("worker_capture_seconds"),
                            "pod_topology": r.get("pod_topology"),
                            "reference_create_to_running_s": 121.0}}
         except Exception as e:  # noqa: BLE001 -- never lose the throughput line over this
@@ -145,6 +166,7 @@ def main(argv=None):
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
                   file=sys.stderr)
     B = args.batch_size
+    job_plan = job_gpu_plan(world, args.job_gpus, args.job_backend)  # validated before any work
 
     from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
     ds = make_synthetic_mnist(args.dataset_size, seed=1 + rank, device=dev)
@@ -258,7 +280,7 @@ def main(argv=None):
         dist.all_reduce(diff, op=dist.ReduceOp.MAX)
         in_sync = bool(float(diff.item()) == 0.0) and ar_err == 0
 
-    lat = job_latency(world, rank, args.job_timeout) if args.job_latency else {}
+    lat = job_latency(world, rank, args.job_timeout, *job_plan) if args.job_latency else {}
 
     samples = steps * B * world
     value = samples / dt

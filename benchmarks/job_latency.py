@@ -79,6 +79,11 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
             "create_to_first_step_s": s(max(first)) if len(first) == replicas else None,
             "create_to_succeeded_s": s(t_done),
             "worker_samples_per_sec": rank0[0].get("samples_per_sec") if rank0 else None,
+            # steady state inside the pod: per-step ms of the graphed log blocks (p50/p90/p99),
+            # the one-off graph capture kept out of train_seconds
+            "worker_step_ms": rank0[0].get("step_ms") if rank0 else None,
+            "worker_train_seconds": rank0[0].get("train_seconds") if rank0 else None,
+            "worker_capture_seconds": rank0[0].get("capture_seconds") if rank0 else None,
             "grad_allreduce": sorted(x for x in paths if x) or None,
             "accuracy": rank0[0]["accuracy"] if rank0 else None}
 

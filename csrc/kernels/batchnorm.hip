@@ -221,12 +221,21 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
 }
 
 // ReLU mask of the backward: MASK 0 = no ReLU, 1 = recompute (x-mean)*scale+beta > 0 (bitwise
-// the forward's value), 2 = y > 0 (a residual was added before the ReLU)
-template <typename T, int MASK>
-__device__ __forceinline__ void masked_grad(const T* dy, const T* x, const T* y, long e, const float (&sc)[8],
-                                            const float (&sh)[8], const float (&mu)[8], float (&g)[8],
-                                            float (&xv)[8]) {
+// the forward's value), 2 = y > 0 (a residual was added before the ReLU).
+// ADD2: the output has two consumers whose gradients arrive separately (a bottleneck's output
+// feeds the next block's conv1 AND, as the identity, its residual add): g = dy + dy2, summed
+// in fp32 here instead of by an extra elementwise pass over the activation.
+template <typename T, int MASK, bool ADD2>
+__device__ __forceinline__ void masked_grad(const T* dy, const T* dy2, const T* x, const T* y, long e,
+                                            const float (&sc)[8], const float (&sh)[8], const float (&mu)[8],
+                                            float (&g)[8], float (&xv)[8]) {
   V8<T>::ld(dy + e, g);
+  if (ADD2) {
+    float g2[8];
+    V8<T>::ld(dy2 + e, g2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] += g2[j];
+  }
   V8<T>::ld(x + e, xv);
   if (MASK == 1) {
 #pragma unroll
@@ -240,8 +249,9 @@ __device__ __forceinline__ void masked_grad(const T* dy, const T* x, const T* y,
 }
 
 // ---- backward 1: per-block sums of g and g * (x - mean) per channel
-template <typename T, int MASK>
-__global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int MASK, bool ADD2>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                              const T* __restrict__ x,
                                                               const T* __restrict__ y, const float* __restrict__ ss,
                                                               const float* __restrict__ mean, long M, int C, int rpb,
                                                               float* __restrict__ part) {
@@ -259,7 +269,8 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
   for (; r + rpi < r1; r += 2 * rpi) {
     float g[2][8], xv[2][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) masked_grad<T, MASK>(dy, x, y, (r + u * rpi) * C + cv * 8, sc, sh, mu, g[u], xv[u]);
+    for (int u = 0; u < 2; ++u)
+      masked_grad<T, MASK, ADD2>(dy, dy2, x, y, (r + u * rpi) * C + cv * 8, sc, sh, mu, g[u], xv[u]);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -267,7 +278,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
   }
   for (; r < r1; r += rpi) {
     float g[8], xv[8];
-    masked_grad<T, MASK>(dy, x, y, r * C + cv * 8, sc, sh, mu, g, xv);
+    masked_grad<T, MASK, ADD2>(dy, dy2, x, y, r * C + cv * 8, sc, sh, mu, g, xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { a[j] += g[j]; b[j] = fmaf(g[j], xv[j] - mu[j], b[j]); }
   }
@@ -317,8 +328,9 @@ __global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_kernel(const float* __
 }
 
 // ---- backward 3: dx = ca*g + cb*(x - mean) + cc  (and dz = g for the residual branch)
-template <typename T, int MASK, bool DZ>
-__global__ __launch_bounds__(BN_NT) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int MASK, bool DZ, bool ADD2>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                          const T* __restrict__ x,
                                                           const T* __restrict__ y, const float* __restrict__ ss,
                                                           const float* __restrict__ coef,
                                                           const float* __restrict__ mean, T* __restrict__ dx,
@@ -335,7 +347,7 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_kernel(const T* __restrict__ 
   }
   for (long i = i0; i < nvec; i += stride) {
     float g[8], xv[8];
-    masked_grad<T, MASK>(dy, x, y, i * 8, sc, sh, mu, g, xv);
+    masked_grad<T, MASK, ADD2>(dy, dy2, x, y, i * 8, sc, sh, mu, g, xv);
     if (DZ) V8<T>::st(dz + i * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = fmaf(ca[j], g[j], fmaf(cb[j], xv[j] - mu[j], cc[j]));
@@ -373,26 +385,44 @@ int fwd_t(const void* x, const void* z, void* y, const float* gamma, const float
   return (int)hipGetLastError();
 }
 
-template <typename T, int MASK>
-void bwd_dx_launch(const T* dy, const T* x, const T* y, const float* ss, const float* coef, const float* mean, T* dx,
-                   T* dz, long nvec, int C, hipStream_t s) {
+template <typename T, int MASK, bool ADD2>
+void bwd_dx_launch(const T* dy, const T* dy2, const T* x, const T* y, const float* ss, const float* coef,
+                   const float* mean, T* dx, T* dz, long nvec, int C, hipStream_t s) {
   const int gr = grid_for(nvec, C);
-  if (dz != nullptr) hipLaunchKernelGGL((bn_bwd_dx_kernel<T, MASK, true>), dim3(gr), dim3(BN_NT), 0, s, dy, x, y, ss, coef, mean, dx, dz, nvec, C);
-  else hipLaunchKernelGGL((bn_bwd_dx_kernel<T, MASK, false>), dim3(gr), dim3(BN_NT), 0, s, dy, x, y, ss, coef, mean, dx, dz, nvec, C);
+  if (dz != nullptr)
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<T, MASK, true, ADD2>), dim3(gr), dim3(BN_NT), 0, s, dy, dy2, x, y, ss, coef,
+                       mean, dx, dz, nvec, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_dx_kernel<T, MASK, false, ADD2>), dim3(gr), dim3(BN_NT), 0, s, dy, dy2, x, y, ss, coef,
+                       mean, dx, dz, nvec, C);
+}
+
+template <typename T, int MASK, bool ADD2>
+int bwd_t2(const T* dyt, const T* dy2t, const T* xt, const T* yt, const float* gamma, const float* mean,
+           const float* rstd, const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part,
+           float* coef, long M, int C, int G, int rpb, hipStream_t s) {
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(G), dim3(BN_NT), 0, s, dyt, dy2t, xt, yt, ss, mean,
+                     M, C, rpb, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part, G, C, M, gamma,
+                     mean, rstd, dgamma, dbeta, coef);
+  bwd_dx_launch<T, MASK, ADD2>(dyt, dy2t, xt, yt, ss, coef, mean, static_cast<T*>(dx), static_cast<T*>(dz),
+                               M * (long)C / 8, C, s);
+  return (int)hipGetLastError();
 }
 
 template <typename T, int MASK>
-int bwd_t(const void* dy, const void* x, const void* y, const float* gamma, const float* mean, const float* rstd,
-          const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part, float* coef, long M, int C,
-          int G, int rpb, hipStream_t s) {
+int bwd_t(const void* dy, const void* dy2, const void* x, const void* y, const float* gamma, const float* mean,
+          const float* rstd, const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part,
+          float* coef, long M, int C, int G, int rpb, hipStream_t s) {
   const T* dyt = static_cast<const T*>(dy);
+  const T* dy2t = static_cast<const T*>(dy2);
   const T* xt = static_cast<const T*>(x);
   const T* yt = static_cast<const T*>(y);
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK>), dim3(G), dim3(BN_NT), 0, s, dyt, xt, yt, ss, mean, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part, G, C, M, gamma,
-                     mean, rstd, dgamma, dbeta, coef);
-  bwd_dx_launch<T, MASK>(dyt, xt, yt, ss, coef, mean, static_cast<T*>(dx), static_cast<T*>(dz), M * (long)C / 8, C, s);
-  return (int)hipGetLastError();
+  if (dy2 != nullptr)
+    return bwd_t2<T, MASK, true>(dyt, dy2t, xt, yt, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G,
+                                 rpb, s);
+  return bwd_t2<T, MASK, false>(dyt, dy2t, xt, yt, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G,
+                                rpb, s);
 }
 
 bool shape_ok(long M, int C, int G, int rpb) {
@@ -439,23 +469,24 @@ int pto_bn_fwd_train(const void* x, const void* z, void* y, const float* gamma, 
 
 // mask_mode: 0 no ReLU, 1 ReLU (mask recomputed from x), 2 ReLU after a residual add (mask
 // from y).  dz (the residual's gradient = the masked dy) only with mask_mode 2 (may be null).
+// dy2 (may be null): a second incoming gradient of the output, summed with dy in-kernel.
 // coef: fp32 workspace of 3C floats.
-int pto_bn_bwd(const void* dy, const void* x, const void* y, const float* gamma, const float* mean, const float* rstd,
-               const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part, float* coef, long M,
-               int C, int G, int rows_per_block, int dtype, int mask_mode, void* stream) {
-  if (!shape_ok(M, C, G, rows_per_block) || !aligned16(dy) || !aligned16(x) || !aligned16(y) || !aligned16(dx) ||
-      !aligned16(dz))
+int pto_bn_bwd(const void* dy, const void* dy2, const void* x, const void* y, const float* gamma, const float* mean,
+               const float* rstd, const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part,
+               float* coef, long M, int C, int G, int rows_per_block, int dtype, int mask_mode, void* stream) {
+  if (!shape_ok(M, C, G, rows_per_block) || !aligned16(dy) || !aligned16(dy2) || !aligned16(x) || !aligned16(y) ||
+      !aligned16(dx) || !aligned16(dz))
     return -2;
   if (mask_mode == 2 && y == nullptr) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 1) {
-    if (mask_mode == 0) return bwd_t<bf16, 0>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
-    if (mask_mode == 1) return bwd_t<bf16, 1>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
-    if (mask_mode == 2) return bwd_t<bf16, 2>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 0) return bwd_t<bf16, 0>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 1) return bwd_t<bf16, 1>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 2) return bwd_t<bf16, 2>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
   } else if (dtype == 0) {
-    if (mask_mode == 0) return bwd_t<float, 0>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
-    if (mask_mode == 1) return bwd_t<float, 1>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
-    if (mask_mode == 2) return bwd_t<float, 2>(dy, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 0) return bwd_t<float, 0>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 1) return bwd_t<float, 1>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 2) return bwd_t<float, 2>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
   }
   return -1;
 }

@@ -39,6 +39,13 @@
 
 using namespace pto;
 
+// PTO_ABL (timing ablations for tools/build_exp.sh variants only, never numerically valid):
+// bit 0 tail fc SGD, 1 conv1, 2 conv2, 3 conv_bwd4 phase 2, 4 fc1_bwd job 1, 5 head,
+// 6 conv_bwd4 phases 3-4
+#ifndef PTO_ABL
+#define PTO_ABL 0
+#endif
+
 namespace {
 
 typedef unsigned long long u64;
@@ -154,6 +161,49 @@ __device__ __forceinline__ float from_upper_half(float v) {
 }
 __device__ __forceinline__ int from_upper_half(int v) {
   return (int)__builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false)[1];
+}
+
+struct SgdHyper {
+  float lr, momentum, dampening, wd, grad_scale;
+  int nesterov, first_step;
+};
+
+// torch.optim.SGD on one element (buf = momentum*buf + (1-dampening)*d, or d on the first step).
+// Explicit fmas: every kernel that inlines this (tail, fc1_bwd, conv12's deferred rows, the
+// flush, xgmi_allreduce.hip's sgd4) rounds identically, whatever the contraction choices.
+__device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
+  float d = __builtin_fmaf(hy.wd, pv, gv * hy.grad_scale);
+  if (hy.momentum != 0.f) {
+    mv = hy.first_step ? d : __builtin_fmaf(hy.momentum, mv, (1.f - hy.dampening) * d);
+    d = hy.nesterov ? __builtin_fmaf(hy.momentum, mv, d) : mv;
+  }
+  pv = __builtin_fmaf(-hy.lr, d, pv);
+}
+
+// A deferred SGD(momentum) over a flat float4 range, run by extra blocks of another launch
+// when *pend != 0 (fc_sgd "next": the fc parameters' update of step t rides in step t+1's
+// conv12 launch, whose blocks leave half of every CU's wave slots and LDS free).
+struct SgdRange {
+  float4* p;
+  const float4* g;
+  float4* m;
+  int n4;
+  const int* pend;
+  SgdHyper hy;
+};
+
+__device__ __forceinline__ void sgd_range_block(const SgdRange& r, int blk, int nthreads) {
+  if (*r.pend == 0) return;
+  const int v = blk * nthreads + (int)threadIdx.x;
+  if (v >= r.n4) return;
+  float4 pp = r.p[v], bb = r.m[v];
+  const float4 gg = r.g[v];
+  sgd_elem(pp.x, bb.x, gg.x, r.hy);
+  sgd_elem(pp.y, bb.y, gg.y, r.hy);
+  sgd_elem(pp.z, bb.z, gg.z, r.hy);
+  sgd_elem(pp.w, bb.w, gg.w, r.hy);
+  r.p[v] = pp;
+  r.m[v] = bb;
 }
 
 constexpr int C2_RS = 16;
@@ -401,13 +451,17 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
     uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, const uint8_t* __restrict__ stg_x,
-    const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, u64* dbg) {
+    const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, SgdRange sg, u64* dbg) {
   __shared__ float img[28 * AB_IRS];
   __shared__ float w1s[520];
   __shared__ __align__(16) float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  if (b >= B) {  // deferred SGD rows of the grid (dispatched after every conv block)
+    sgd_range_block(sg, (b - B) * gridDim.x + cg, AB_NT);
+    return;
+  }
   stamp(dbg, 0);
   const bool pub = cg == 0;
   // conv2 epilogue bias, loaded with the staging loads (no round trip after the last barrier)
@@ -475,16 +529,18 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
+    if (!(PTO_ABL & 2)) {
     conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
+    }
   }
   __syncthreads();
   stamp(dbg, 2);
 
   const int lane = tid & 63, wv = tid >> 6;
   const int pt = wv & 3, i = lane & 15, g = lane >> 4;
-  f32x4 acc = conv2_block(in_s, w_s, red, wv, lane);
+  f32x4 acc = (PTO_ABL & 4) ? zero4() : conv2_block(in_s, w_s, red, wv, lane);
   stamp(dbg, 3);
   if (wv >= 4) return;
   const int co = cg * 16 + i;
@@ -522,11 +578,12 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
 template <int KS>
 __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ h, int B, u64* dbg) {
+    float* __restrict__ h, int B, int* __restrict__ clr, u64* dbg) {
   constexpr int NW = 10 / KS;
   __shared__ f32x4 red[NW][64];
   const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, tid = threadIdx.x;
   stamp(dbg, 0);
+  if (clr != nullptr && (nt | mt | kz | tid) == 0) *clr = 0;  // conv12 consumed the deferred update
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int row = mt * 16 + i, col = nt * 16 + i;
@@ -594,6 +651,7 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
   const int b = blockIdx.x * WPB + wq;
   const bool bvalid = b < B;
   const int bc = bvalid ? b : B - 1;
+  if (PTO_ABL & 32) return;
   const int t = lab[bc];
   // lane owns k = 8 lane + [0, 8): two float4 per row (h, every W2 row), 22 loads per
   // lane, all in flight at once (lane 62 has half a chunk, lane 63 none)
@@ -730,21 +788,6 @@ constexpr int E_NW = E_NT / 64;
 constexpr int E_NJ1 = 1600 / E_NW;  // job-1 blocks
 constexpr int E_NJ3 = 32 / E_NW;    // job-3 blocks
 
-struct SgdHyper {
-  float lr, momentum, dampening, wd, grad_scale;
-  int nesterov, first_step;
-};
-
-// torch.optim.SGD on one element (buf = momentum*buf + (1-dampening)*d, or d on the first step)
-__device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
-  float d = gv * hy.grad_scale + hy.wd * pv;
-  if (hy.momentum != 0.f) {
-    mv = hy.first_step ? d : hy.momentum * mv + (1.f - hy.dampening) * d;
-    d = hy.nesterov ? d + hy.momentum * mv : mv;
-  }
-  pv -= hy.lr * d;
-}
-
 // Row of sample b of the batch taken at step `step` (perm required).
 __device__ __forceinline__ int batch_row_at(const BatchSrc& s, long long step, int b, int B) {
   long long i = (step * B) % s.n_total + b;
@@ -791,6 +834,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   const int blk = blockIdx.x;
   stamp(dbg, 0);
   if (blk < nJ1) {
+    if (PTO_ABL & 16) return;
     const int tile = blk * E_NW + wv;
     const int nt = tile / 50, kt = tile - nt * 50;
     const int n = nt * 16 + i, f = kt * 16 + i;
@@ -2004,7 +2048,8 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   f32x4 gacc = zero4();
   const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
 #if PTO_PIPE
-  if (wv < 12) {
+  if (PTO_ABL & 8) {
+  } else if (wv < 12) {
     if (own) bwd4_phase2<true, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
     else bwd4_phase2<false, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
     if (wv >= 6) pk_s[tp * 64 + lane] = gacc;
@@ -2100,6 +2145,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     }
   }
   if (!own) return;  // block-uniform: padding blocks of the last chunk are done
+  if (PTO_ABL & 64) return;
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
   if (tid < 720) {
@@ -2292,10 +2338,12 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     float* __restrict__ p, float* __restrict__ buf, float lr, float momentum, float dampening,
     float wd, float grad_scale, int nesterov, int first_step, int* __restrict__ step_counter,
     float* __restrict__ p2, const float* __restrict__ g2, float* __restrict__ buf2, int n2,
-    int red_blocks, const float4* __restrict__ cp_src, float4* __restrict__ cp_dst, int cp_n4, u64* dbg) {
+    int red_blocks, const float4* __restrict__ cp_src, float4* __restrict__ cp_dst, int cp_n4,
+    int* __restrict__ pend, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
+  if (pend != nullptr && (blockIdx.x | tid) == 0) *pend = 1;  // fc update deferred to the next conv12
   const int sgd_blocks = (n2 / 4 + 255) / 256;
   if ((int)blockIdx.x >= red_blocks + sgd_blocks) {
     const int v0 = (blockIdx.x - red_blocks - sgd_blocks) * 256 * SR_CP + tid;
@@ -2308,22 +2356,18 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     return;
   }
   if ((int)blockIdx.x >= red_blocks) {
+    if (PTO_ABL & 1) return;
     // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
     const int v = (blockIdx.x - red_blocks) * 256 + tid;
     if (v < (n2 >> 2)) {
       float4 pp = reinterpret_cast<float4*>(p2)[v];
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];
       float4 bb = reinterpret_cast<float4*>(buf2)[v];
-      float* pe = &pp.x; const float* ge = &gg.x; float* be = &bb.x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float d = ge[e] * grad_scale + wd * pe[e];
-        if (momentum != 0.f) {
-          be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
-          d = nesterov ? d + momentum * be[e] : be[e];
-        }
-        pe[e] -= lr * d;
-      }
+      const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+      sgd_elem(pp.x, bb.x, gg.x, hy);
+      sgd_elem(pp.y, bb.y, gg.y, hy);
+      sgd_elem(pp.z, bb.z, gg.z, hy);
+      sgd_elem(pp.w, bb.w, gg.w, hy);
       reinterpret_cast<float4*>(p2)[v] = pp;
       reinterpret_cast<float4*>(buf2)[v] = bb;
     }
@@ -2346,16 +2390,11 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
 #pragma unroll
     for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
     if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
-    float* pe = &pp.x; float* be = &bb.x; const float* ge = &r.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float d = ge[e] * grad_scale + wd * pe[e];
-      if (momentum != 0.f) {
-        be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
-        d = nesterov ? d + momentum * be[e] : be[e];
-      }
-      pe[e] -= lr * d;
-    }
+    const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+    sgd_elem(pp.x, bb.x, r.x, hy);
+    sgd_elem(pp.y, bb.y, r.y, hy);
+    sgd_elem(pp.z, bb.z, r.z, hy);
+    sgd_elem(pp.w, bb.w, r.w, hy);
     reinterpret_cast<float4*>(p)[col] = pp;
     reinterpret_cast<float4*>(buf)[col] = bb;
   }
@@ -2556,7 +2595,9 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(
     float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ buf, long n,
     float lr, float momentum, float dampening, float wd, float grad_scale, int nesterov,
-    int first_step, int* __restrict__ step_counter) {
+    int first_step, int* __restrict__ step_counter, const int* __restrict__ cond) {
+  if (cond != nullptr && *cond == 0) return;  // conditional (deferred-update flush)
+  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
   const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < n4 + 4; v += stride) {
@@ -2568,25 +2609,17 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(
       float4 pp = reinterpret_cast<float4*>(p)[v];
       const float4 gg = reinterpret_cast<const float4*>(gr)[v];
       float4 bb = reinterpret_cast<float4*>(buf)[v];
-      float* pe = &pp.x; const float* ge = &gg.x; float* be = &bb.x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float d = ge[e] * grad_scale + wd * pe[e];
-        if (momentum != 0.f) {
-          be[e] = first_step ? d : momentum * be[e] + (1.f - dampening) * d;
-          d = nesterov ? d + momentum * be[e] : be[e];
-        }
-        pe[e] -= lr * d;
-      }
+      sgd_elem(pp.x, bb.x, gg.x, hy);
+      sgd_elem(pp.y, bb.y, gg.y, hy);
+      sgd_elem(pp.z, bb.z, gg.z, hy);
+      sgd_elem(pp.w, bb.w, gg.w, hy);
       reinterpret_cast<float4*>(p)[v] = pp;
       reinterpret_cast<float4*>(buf)[v] = bb;
     } else {
-      float d = gr[lo] * grad_scale + wd * p[lo];
-      if (momentum != 0.f) {
-        buf[lo] = first_step ? d : momentum * buf[lo] + (1.f - dampening) * d;
-        d = nesterov ? d + momentum * buf[lo] : buf[lo];
-      }
-      p[lo] -= lr * d;
+      float pv = p[lo], mv = buf[lo];
+      sgd_elem(pv, mv, gr[lo], hy);
+      p[lo] = pv;
+      buf[lo] = mv;
     }
   }
   if (step_counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(step_counter, 1);
@@ -2683,7 +2716,9 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
                          float shift, const float* w1, const float* b1, const float* w2,
                          const float* b2, float* a1, uint8_t* idx1, float* xn_out, int* lab_out,
                          float* a2, uint8_t* idx2, int B, const uint8_t* stg_x, const int* stg_lab,
-                         const int* stg_tag, void* stream) {
+                         const int* stg_tag, float* sg_p, const float* sg_g, float* sg_m, int sg_n,
+                         const int* sg_pend, float lr, float momentum, float dampening, float wd,
+                         float grad_scale, int nesterov, int first_step, void* stream) {
   PTO_CHECK_B(B);
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
@@ -2693,8 +2728,19 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
                            !is_u8 || labels == nullptr))
     return -1;
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
-  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
-                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, stg_x, stg_lab, stg_tag, g_dbg);
+  SgdRange sg{};
+  int rows = 0;
+  if (sg_n > 0) {
+    if (sg_p == nullptr || sg_g == nullptr || sg_m == nullptr || sg_pend == nullptr || (sg_n & 3) ||
+        ((((uintptr_t)sg_p) | ((uintptr_t)sg_g) | ((uintptr_t)sg_m)) & 15))
+      return -1;
+    sg = SgdRange{reinterpret_cast<float4*>(sg_p), reinterpret_cast<const float4*>(sg_g),
+                  reinterpret_cast<float4*>(sg_m), sg_n / 4, sg_pend,
+                  SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step}};
+    rows = (sg.n4 + 4 * AB_NT - 1) / (4 * AB_NT);
+  }
+  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B + rows), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
+                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, stg_x, stg_lab, stg_tag, sg, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -2703,16 +2749,16 @@ int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* 
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return -2;  // float4 loads
   hipLaunchKernelGGL(fc1_fwd_kernel<1>, dim3(32, (B + 15) / 16), dim3(640), 0,
-                     (hipStream_t)stream, x, w, bias, h, B, g_dbg);
+                     (hipStream_t)stream, x, w, bias, h, B, nullptr, g_dbg);
   return (int)hipGetLastError();
 }
 
 // Split-K fc1: pre-activation halves to parts[2][B][500] (head_kernel finishes h).
-int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, void* stream) {
+int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, int* clr, void* stream) {
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)parts)) & 15) return -2;
   hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3(32, (B + 15) / 16, 2), dim3(320), 0,
-                     (hipStream_t)stream, x, w, nullptr, parts, B, g_dbg);
+                     (hipStream_t)stream, x, w, nullptr, parts, B, clr, g_dbg);
   return (int)hipGetLastError();
 }
 
@@ -2903,7 +2949,7 @@ int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, int ro
 
 int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, float momentum,
                      float dampening, float wd, float grad_scale, int nesterov, int first_step,
-                     int* step_counter, void* stream) {
+                     int* step_counter, const int* cond, void* stream) {
   if (n <= 0) return -1;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) & 15) return -2;  // float4 path
   long v = (n >> 2) + 4;
@@ -2911,7 +2957,7 @@ int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, flo
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g,
                      buf, n, lr, momentum, dampening, wd, grad_scale, nesterov, first_step,
-                     step_counter);
+                     step_counter, cond);
   return (int)hipGetLastError();
 }
 
@@ -2919,7 +2965,7 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
                         float* buf, float lr, float momentum, float dampening, float wd,
                         float grad_scale, int nesterov, int first_step, int* step_counter,
                         float* p2, const float* g2, float* buf2, int n2, int rows_big, int big_lo,
-                        int big_hi, const float* cp_src, float* cp_dst, int cp_n, void* stream) {
+                        int big_hi, const float* cp_src, float* cp_dst, int cp_n, int* pend, void* stream) {
   PTO_CHECK_B(B);
   if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
   if (n2 < 0 || (n2 & 3) || (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)))
@@ -2938,7 +2984,7 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
                      sr, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
                      nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks,
-                     reinterpret_cast<const float4*>(cp_src), reinterpret_cast<float4*>(cp_dst), cp_n4, g_dbg);
+                     reinterpret_cast<const float4*>(cp_src), reinterpret_cast<float4*>(cp_dst), cp_n4, pend, g_dbg);
   return (int)hipGetLastError();
 }
 

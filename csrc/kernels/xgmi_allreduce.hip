@@ -153,13 +153,15 @@ __device__ bool wait_flag(const unsigned* p, unsigned target, long long deadline
 }
 
 // torch.optim.SGD (momentum, dampening, weight decay, nesterov) on four elements
+// (explicit fmas in mnist_kernels.hip's sgd_elem order: bit-identical to the 1-GPU step)
 __device__ __forceinline__ void sgd4(f4& p, f4 g, f4& m, const XarArgs& a, float scale) {
-  f4 d = g * scale + a.wd * p;
+  const f4 wd = a.wd, mo = a.momentum, nlr = -a.lr;
+  f4 d = __builtin_elementwise_fma(wd, p, g * scale);
   if (a.momentum != 0.f) {
-    m = a.first_step ? d : a.momentum * m + (1.f - a.dampening) * d;
-    d = a.nesterov ? d + a.momentum * m : m;
+    m = a.first_step ? d : __builtin_elementwise_fma(mo, m, (1.f - a.dampening) * d);
+    d = a.nesterov ? __builtin_elementwise_fma(mo, m, d) : m;
   }
-  p -= a.lr * d;
+  p = __builtin_elementwise_fma(nlr, d, p);
 }
 
 // Element v (float4 units, v < npad4) of this rank's flat gradient outside the slab-reduced

@@ -322,7 +322,7 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         dist.broadcast(tr.flat_params, 0)  # DDP constructor semantics
     log_iv = max(1, args.log_interval)
     runner = None
-    t_train = 0.0
+    t_train = t_capture = 0.0
     steps_done = 0
     step_ms = []
     loss = acc = float("nan")
@@ -341,13 +341,19 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer)
         if runner is None and not args.no_graph:
             # capturing runs warm-up steps: snapshot the state, capture, restore, so the
-            # trajectory is exactly the eager one (a log block = one graph replay)
+            # trajectory is exactly the eager one (a log block = one graph replay).  The
+            # capture is one-off set-up: its time is reported apart from train_seconds.
+            torch.cuda.synchronize(dev)
+            t_cap0 = time.perf_counter()
             saved = (tr.flat_params.clone(), tr.flat_momentum.clone())
             whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
             runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1, launch=args.launch)
             tr.flat_params.copy_(saved[0])
             tr.flat_momentum.copy_(saved[1])
             cursor.fill_(1)
+            torch.cuda.synchronize(dev)
+            t_capture = time.perf_counter() - t_cap0
+            t0 += t_capture
         # blocks of log_iv steps ending on a logged batch (batches 1..L, L+1..2L, ...)
         b = 1
         events = []
@@ -389,7 +395,7 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         torch.save({k: v.detach().cpu().clone() for k, v in tr.state_dict().items()}, args.model_path)
     return {"steps": steps_done, "train_seconds": round(t_train, 4),
             "samples_per_sec": round(steps_done * B * world / t_train, 1) if t_train else None,
-            "step_ms": _percentiles(step_ms),
+            "step_ms": _percentiles(step_ms), "capture_seconds": round(t_capture, 4),
             "test_loss": round(loss, 5), "accuracy": round(acc, 5)}
 
 

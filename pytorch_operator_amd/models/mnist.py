@@ -121,14 +121,19 @@ class FusedMnistTrainer:
         self.layout = flat_layout()
         L = self.layout.total
         dev = self.device
-        self.flat_params = torch.zeros(L, device=dev)
+        self._fp = torch.zeros(L, device=dev)
         # grads are fully overwritten every step (no zeroing): fc grads by fc1_bwd, conv
         # grads by the deterministic slab reduction; stats = (loss, #correct) of the step
         self.flat_grads = torch.zeros(L, device=dev)
         self.stats = torch.zeros(16, device=dev)
-        self.flat_momentum = torch.zeros(L, device=dev)
-        self.params = _views(self.flat_params, self.layout)
+        self._fm = torch.zeros(L, device=dev)
+        self._pv = _views(self._fp, self.layout)
         self.grads = _views(self.flat_grads, self.layout)
+        # fc_sgd "next": device flag "an fc update is pending" (set by the tail, applied and
+        # cleared by the next step's conv12 / fc1_fwd launches, or by flush_deferred())
+        self._pend = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._defer_used = False
+        self._defer_first = False
         # device batch cursor: advanced by the SGD launch, read by conv1_fwd/head/conv_bwd
         self.cursor = source.cursor if (source is not None and source.cursor is not None) \
             else torch.zeros(1, device=dev, dtype=torch.int32)
@@ -161,12 +166,49 @@ class FusedMnistTrainer:
         #                 copied back by the tail -- and become fc1_bwd's critical path)
         #   stage: fc1_bwd stages the next step's batch; conv12 reads it with one load
         #   store_fc_grads: also store the fc gradients in the fused-SGD path (inspection)
+        #   fc_sgd "next": the tail leaves the fc update pending; extra grid rows of the next
+        #                 step's conv12 launch apply it (conv12 leaves half of every CU idle).
+        #                 Parameters, momentum and state are flushed on every public access.
         self.conv_chunk = 4
         self.fc_sgd = "tail"
         self.stage_batches = True
         self.store_fc_grads = True
 
     # ---------------------------------------------------------------- state
+    @property
+    def flat_params(self) -> torch.Tensor:
+        self.flush_deferred()
+        return self._fp
+
+    @property
+    def flat_momentum(self) -> torch.Tensor:
+        self.flush_deferred()
+        return self._fm
+
+    @property
+    def params(self) -> Dict[str, torch.Tensor]:
+        self.flush_deferred()
+        return self._pv
+
+    def flush_deferred(self) -> None:
+        """Apply a pending fc_sgd="next" update (conditional on the device flag; no-op when
+        no deferred step ever ran).  Stream-ordered, so callers just use the tensors."""
+        if not self._defer_used:
+            return
+        ce = self.layout.conv_end
+        self.K.sgd_momentum_(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:], lr=self.lr,
+                             momentum=self.momentum, dampening=self.dampening,
+                             weight_decay=self.weight_decay, nesterov=self.nesterov,
+                             first_step=self._defer_first, cond=self._pend)
+        self._pend.zero_()
+        self._defer_first = False
+
+    def _deferred_arg(self) -> dict:
+        ce = self.layout.conv_end
+        return dict(params=self._fp[ce:], grads=self.flat_grads[ce:], buf=self._fm[ce:], pend=self._pend,
+                    lr=self.lr, momentum=self.momentum, dampening=self.dampening,
+                    weight_decay=self.weight_decay, nesterov=self.nesterov, first_step=self._defer_first)
+
     def _alloc(self, B: int):
         dev = self.device
         self.a1 = torch.empty((B, 20, 12, 12), device=dev)
@@ -234,34 +276,38 @@ class FusedMnistTrainer:
         if self.stage is not None:
             self.stage.invalidate()
 
-    def forward(self, source=None, B: Optional[int] = None) -> None:
-        """conv12_fwd + split-K fc1 (the head runs inside fc1_bwd_head)."""
-        K, p = self.K, self.params
+    def forward(self, source=None, B: Optional[int] = None, _defer: bool = False) -> None:
+        """conv12_fwd + split-K fc1 (the head runs inside fc1_bwd_head).  ``_defer``
+        (fc_sgd "next" steps): conv12 applies the pending fc update instead of a flush."""
+        if not _defer:
+            self.flush_deferred()
+        K, p = self.K, self._pv
         src = source or self.source
         B = self.B if B is None else B
         if self.fuse_conv12:
             K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
                          p["conv2.bias"], B, a1=self.a1[:B], idx1=self.idx1[:B], xn=self.xn[:B],
                          lab=self.lab[:B], a2=self.a2[:B], idx2=self.idx2[:B],
-                         stage=self._stage_for(source))
+                         stage=self._stage_for(source), deferred=self._deferred_arg() if _defer else None)
         else:
             K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=self.a1[:B],
                         idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
         # split-K fc1 (256 workgroups); fc1_bwd_head adds the halves + bias and applies ReLU
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500))
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500),
+                        clear=self._pend if _defer else None)
 
     def _head(self, B: int) -> None:
         """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
-        K, p = self.K, self.params
+        K, p = self.K, self._pv
         hp = self.h_parts[:2 * B * 500].view(2, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
     def _fc1_bwd_head(self, B: int) -> None:
-        K, p = self.K, self.params
+        K, p = self.K, self._pv
         K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"],
                        p["fc2.bias"], self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"],
                        grad_scale=1.0 / B, dz2=self.dz2[:B], h_out=self.h1[:B], dh=self.dh[:B],
@@ -269,7 +315,7 @@ class FusedMnistTrainer:
 
     def _fc1_bwd(self, B: int, jobs: int, stage_adv: Optional[int] = None) -> None:
         """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv."""
-        K, p, g = self.K, self.params, self.grads
+        K, p, g = self.K, self._pv, self.grads
         st = self._stage_for(None) if stage_adv is not None and jobs == K.FC1_BWD_ALL else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
@@ -279,7 +325,7 @@ class FusedMnistTrainer:
 
     def _conv_bwd_fc(self, B: int, sgd: bool) -> None:
         """conv backward + fc weight grads (+ their SGD when ``sgd``) in one launch."""
-        K, p = self.K, self.params
+        K, p = self.K, self._pv
         fp, fm, fg = self._fc_dicts()
         self._last_big = None  # per-sample slab rows
         K.conv_bwd_fc(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
@@ -297,7 +343,7 @@ class FusedMnistTrainer:
         return self._fc_in_conv_ok
 
     def _conv_bwd(self, B: int) -> None:
-        K, p = self.K, self.params
+        K, p = self.K, self._pv
         if self.conv_chunk == 4:
             K.conv_bwd4(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
                         self.conv_slab, self.layout.offsets, B)
@@ -315,7 +361,7 @@ class FusedMnistTrainer:
 
     def _fc1_bwd_sgd(self, B: int, advance_cursor: bool) -> None:
         """fc1_bwd with the fc SGD fused in (updated fc1.weight -> w1_next) + next-batch staging."""
-        K, p = self.K, self.params
+        K, p = self.K, self._pv
         fp, fm, fg = self._fc_dicts()
         st = self._stage_for(None)
         K.fc1_bwd_sgd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
@@ -327,8 +373,8 @@ class FusedMnistTrainer:
                       stage_adv=1 if advance_cursor else 0)
 
     def _sgd(self, lo: int, hi: int, grad_scale: float, advance_cursor: bool) -> None:
-        self.K.sgd_momentum_(self.flat_params[lo:hi], self.flat_grads[lo:hi],
-                             self.flat_momentum[lo:hi], lr=self.lr, momentum=self.momentum,
+        self.K.sgd_momentum_(self._fp[lo:hi], self.flat_grads[lo:hi],
+                             self._fm[lo:hi], lr=self.lr, momentum=self.momentum,
                              dampening=self.dampening, weight_decay=self.weight_decay,
                              nesterov=self.nesterov, grad_scale=grad_scale,
                              first_step=self._first_step,
@@ -361,6 +407,7 @@ class FusedMnistTrainer:
             self.grad_sync.conv_ready(self.conv_bucket())
 
     def optimizer_step(self, advance_cursor: bool = True, grad_scale: Optional[float] = None) -> None:
+        self.flush_deferred()
         if grad_scale is None:
             grad_scale = self.grad_sync.finish() if self.grad_sync is not None else 1.0
         self._sgd(0, self.layout.total, grad_scale, advance_cursor)
@@ -368,14 +415,18 @@ class FusedMnistTrainer:
 
     def _fc_dicts(self):
         names = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
-        mom = _views(self.flat_momentum, self.layout)
-        return ({k: self.params[k] for k in names}, {k: mom[k] for k in names},
+        mom = _views(self._fm, self.layout)
+        return ({k: self._pv[k] for k in names}, {k: mom[k] for k in names},
                 {k: self.grads[k] for k in names})
 
     def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True,
                    overlap: Optional[bool] = None):
         """One full training step (forward, backward, [all-reduce], SGD)."""
         overlap = self.overlap if overlap is None else overlap
+        defer = (self.fc_sgd == "next" and self.grad_sync is None and not overlap and
+                 self.schedule == "classic" and self.fuse_conv12)
+        if not defer:
+            self.flush_deferred()
         if getattr(self.grad_sync, "fused_sgd", False):
             # xGMI path: one kernel reduces the per-sample conv-grad slabs, does the
             # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
@@ -394,7 +445,7 @@ class FusedMnistTrainer:
                     self._fc1_bwd(B_, self.K.FC1_BWD_WGRAD | self.K.FC1_BWD_FC2)
                     self._conv_bwd(B_)
             self.grad_sync.xar.allreduce_sgd_(
-                self.flat_grads, self.flat_params, self.flat_momentum, lr=self.lr,
+                self.flat_grads, self._fp, self._fm, lr=self.lr,
                 momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
                 nesterov=self.nesterov, first_step=self._first_step,
                 step_counter=self.cursor if advance_cursor else None,
@@ -411,7 +462,7 @@ class FusedMnistTrainer:
         ce = self.layout.conv_end
         if not overlap and self.schedule == "classic":
             # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd -> tail
-            self.forward(source, B)
+            self.forward(source, B, _defer=defer)
             self._head(B)
             fused_sgd = self.fc_sgd == "fused"
             if fused_sgd:
@@ -419,23 +470,26 @@ class FusedMnistTrainer:
             else:
                 self._fc1_bwd(B, K.FC1_BWD_ALL, stage_adv=1 if advance_cursor else 0)
             self._conv_bwd(B)
-            w1 = self.params["fc1.weight"]
-            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
-                               self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+            w1 = self._pv["fc1.weight"]
+            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
+                               self._fm[:ce], lr=self.lr, momentum=self.momentum,
                                dampening=self.dampening, weight_decay=self.weight_decay,
                                nesterov=self.nesterov, first_step=self._first_step,
                                step_counter=self.cursor if advance_cursor else None,
-                               extra=None if fused_sgd else (self.flat_params[ce:], self.flat_grads[ce:],
-                                                             self.flat_momentum[ce:]),
-                               big=self._slab_big(B), copy=(self.w1_next, w1) if fused_sgd else None)
+                               extra=None if (fused_sgd or defer) else
+                               (self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
+                               big=self._slab_big(B), copy=(self.w1_next, w1) if fused_sgd else None,
+                               set_pend=self._pend if defer else None)
+            if defer:
+                self._defer_used, self._defer_first = True, self._first_step
             self._first_step = False
             return
         if not overlap and self._fc_in_conv(B):
             self.forward(source, B)
             self._fc1_bwd_head(B)
             self._conv_bwd_fc(B, sgd=True)
-            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
-                               self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
+                               self._fm[:ce], lr=self.lr, momentum=self.momentum,
                                dampening=self.dampening, weight_decay=self.weight_decay,
                                nesterov=self.nesterov, first_step=self._first_step,
                                step_counter=self.cursor if advance_cursor else None)
@@ -446,8 +500,8 @@ class FusedMnistTrainer:
             self._fc1_bwd_head(B)
             self._conv_bwd(B)
             fp, fm, fg = self._fc_dicts()
-            K.tail_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
-                        self.flat_momentum[:ce], big=self._slab_big(B), dh=self.dh[:B], a2=self.a2[:B],
+            K.tail_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
+                        self._fm[:ce], big=self._slab_big(B), dh=self.dh[:B], a2=self.a2[:B],
                         dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
                         fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
                         lr=self.lr, momentum=self.momentum, dampening=self.dampening,
@@ -467,8 +521,8 @@ class FusedMnistTrainer:
             self._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)
             self._sgd(ce, self.layout.total, 1.0, False)
         self._conv_bwd(B)
-        K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self.flat_params[:ce],
-                           self.flat_momentum[:ce], lr=self.lr, momentum=self.momentum,
+        K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
+                           self._fm[:ce], lr=self.lr, momentum=self.momentum,
                            dampening=self.dampening, weight_decay=self.weight_decay,
                            nesterov=self.nesterov, first_step=self._first_step,
                            step_counter=self.cursor if advance_cursor else None, big=self._slab_big(B))
@@ -490,6 +544,7 @@ class FusedMnistTrainer:
             raise ValueError("graph capture needs a BatchSource with a device cursor")
         if self._first_step:
             self.train_step()
+            self.flush_deferred()  # a deferred first-step update must not be baked into the graph
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

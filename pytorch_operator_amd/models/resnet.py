@@ -55,7 +55,9 @@ class Bottleneck(nn.Module):
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormAct2d(width, relu=True)
         self.conv3 = Conv1x1(width, planes * self.expansion)
-        self.bn3 = BatchNormAct2d(planes * self.expansion, relu=True)  # relu(bn3(.) + identity)
+        # relu(bn3(.) + identity); its output feeds the next block's conv1 and residual add, whose
+        # two gradients bn3's backward sums in-kernel (ops/batchnorm.py GradLink)
+        self.bn3 = BatchNormAct2d(planes * self.expansion, relu=True, link_output=True)
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -92,12 +92,13 @@ _SIGNATURES = {
     "pto_mnist_conv1_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _I, _VP,
                             _I, _VP, _VP, _VP],
     "pto_mnist_conv2_fwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_conv12_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F] + [_VP] * 10 + [_I, _VP, _VP, _VP, _VP],
+    "pto_mnist_conv12_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F] + [_VP] * 10 + [_I, _VP, _VP, _VP]
+                            + [_VP, _VP, _VP, _I, _VP] + [_F] * 5 + [_I, _I, _VP],
     "pto_slab_reduce_sgd": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
-                            _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP, _I, _VP],
+                            _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP],
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
-    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
+    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP, _VP],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
@@ -106,7 +107,7 @@ _SIGNATURES = {
                              + [_I, _I, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
     "pto_mnist_stage_batch": [_VP, _VP, _VP, _VP, _I, _I, _I, _VP, _VP, _VP, _VP],
-    "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
+    "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _VP],
     "pto_conv_bwd_lds_bytes": [],
     "pto_conv_bwd_fc_supported": [_I],
     "pto_mnist_conv_bwd_fc": [_VP] * 9 + [_I, _I, _I] + [_VP] * 18 + [_F] * 6 + [_I, _I, _VP],
@@ -147,7 +148,7 @@ _SIGNATURES = {
     # batchnorm.hip
     "pto_bn_plan": [_L, _I, ctypes.POINTER(_I)],
     "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP],
-    "pto_bn_bwd": [_VP] * 13 + [_L, _I, _I, _I, _I, _I, _VP],
+    "pto_bn_bwd": [_VP] * 14 + [_L, _I, _I, _I, _I, _I, _VP],
     # attention.hip
     "pto_attn_fwd": [_VP] * 5 + [_I] * 5 + [_F, _I, _VP],
     "pto_attn_bwd": [_VP] * 10 + [_I] * 5 + [_F, _I, _VP],

@@ -7,6 +7,13 @@ The ResNet-50 worker's step is 58 % batch-norm and elementwise passes on the lib
 backward into one reduction pass and one dx pass (the ReLU mask is recomputed from x when no
 residual was added), for channels-last fp32/bf16 activations.
 
+Residual gradient fusion (``link_output``): a bottleneck's output y feeds the next block twice
+-- its conv1 and, as the identity, its residual add -- so autograd would sum the two incoming
+gradients with an extra elementwise pass (2 reads + 1 write of the activation).  Here the
+consumer's backward hands its residual gradient to the producer through a ``GradLink``
+(returning no autograd gradient for that input, so the edge only orders the two backwards)
+and the producer's backward kernels load both gradients and add them in fp32.
+
 ``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and state dict)
 whose forward takes an optional residual and applies the ReLU itself.  Its ``impl``
 (``"hip"`` / ``"library"``) selects the HIP kernels or PyTorch's own ops on a GPU; on CPU, in
@@ -59,9 +66,21 @@ def _plan(lib, M: int, C: int):
     return G, rpb.value
 
 
+class GradLink:
+    """Out-of-band second gradient of a ``BatchNormAct2d`` output (see the module docstring).
+    ``claimed``: a consumer took the residual role; ``dz``: the gradient it left for the
+    producer's backward (consumed, then cleared, there)."""
+    __slots__ = ("claimed", "dz")
+
+    def __init__(self):
+        self.claimed = False
+        self.dz = None
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu,
+                res_link=None, out_link=None):
         lib = _native.load()
         N, C, H, W = x.shape
         M = N * H * W
@@ -81,6 +100,7 @@ class _BNAct(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.plan = (M, C, G, rpb)
+        ctx.res_link, ctx.out_link = res_link, out_link
         ctx.save_for_backward(xc, y if ctx.mask == 2 else None, weight, stats)
         return y
 
@@ -90,6 +110,9 @@ class _BNAct(torch.autograd.Function):
         xc, y, weight, stats = ctx.saved_tensors
         M, C, G, rpb = ctx.plan
         dyc = _nhwc(dy, xc.dtype)
+        dy2 = None
+        if ctx.out_link is not None and ctx.out_link.dz is not None:
+            dy2, ctx.out_link.dz = _nhwc(ctx.out_link.dz, xc.dtype), None
         dx = torch.empty_like(xc, memory_format=torch.channels_last)
         dz = torch.empty_like(xc, memory_format=torch.channels_last) if ctx.has_res else None
         f32 = dict(device=xc.device, dtype=torch.float32)
@@ -97,34 +120,55 @@ class _BNAct(torch.autograd.Function):
         coef = torch.empty(3 * C, **f32)
         dgb = torch.empty(2 * C, **f32)
         _native.check(lib.pto_bn_bwd(
-            dyc.data_ptr(), xc.data_ptr(), _ptr(y), weight.data_ptr(), stats.data_ptr(), stats[C:].data_ptr(),
+            dyc.data_ptr(), _ptr(dy2), xc.data_ptr(), _ptr(y), weight.data_ptr(), stats.data_ptr(), stats[C:].data_ptr(),
             stats[2 * C:].data_ptr(), dgb.data_ptr(), dgb[C:].data_ptr(), dx.data_ptr(), _ptr(dz), part.data_ptr(),
             coef.data_ptr(), M, C, G, rpb, _DT[xc.dtype], ctx.mask, _stream(xc)), "bn_bwd")
         dgamma, dbeta = dgb[:C].to(weight.dtype), dgb[C:].to(weight.dtype)
+        if dz is not None and ctx.res_link is not None:
+            # the producer of the residual adds this in its own backward kernels; the
+            # autograd edge only orders the two backwards (no gradient sum pass)
+            ctx.res_link.dz, dz = dz, None
         if dz is not None and dz.dtype != ctx.res_dtype:
             dz = dz.to(ctx.res_dtype)
-        return dx, dgamma, dbeta, dz, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dz, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, weight, bias, running_mean=None, running_var=None, num_batches_tracked=None,
-                   training=True, momentum=0.1, eps=1e-5, relu=False, residual=None, impl="hip"):
-    """``relu(batch_norm(x) [+ residual])`` (training statistics when ``training``)."""
+                   training=True, momentum=0.1, eps=1e-5, relu=False, residual=None, impl="hip",
+                   link_output=False):
+    """``relu(batch_norm(x) [+ residual])`` (training statistics when ``training``).
+
+    ``link_output``: the result carries a ``GradLink`` so that a later ``batch_norm_act``
+    taking it as ``residual`` returns its residual gradient through the link and this op's
+    backward sums it in-kernel.  A residual that carries a link is claimed by its first such
+    consumer only (any other use goes through autograd as usual)."""
     if (impl != "hip" or not training or momentum is None or not supported(x) or weight is None
             or weight.dtype != torch.float32):
         if training and num_batches_tracked is not None:
             num_batches_tracked.add_(1)
         return reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu, residual)
-    return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, num_batches_tracked, momentum, eps,
-                        relu)
+    res_link = None
+    if residual is not None and torch.is_grad_enabled() and residual.requires_grad:
+        link = getattr(residual, "_pto_link", None)
+        if (link is not None and not link.claimed and residual.dtype == x.dtype and residual.shape == x.shape
+                and residual.is_contiguous(memory_format=torch.channels_last)):
+            link.claimed, res_link = True, link
+    out_link = GradLink() if link_output and torch.is_grad_enabled() else None
+    y = _BNAct.apply(x, weight, bias, residual, running_mean, running_var, num_batches_tracked, momentum, eps,
+                     relu, res_link, out_link)
+    if out_link is not None:
+        y._pto_link = out_link
+    return y
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` + optional residual add + optional ReLU, one fused op on MI355X."""
 
-    def __init__(self, num_features: int, relu: bool = False, **kw):
+    def __init__(self, num_features: int, relu: bool = False, link_output: bool = False, **kw):
         super().__init__(num_features, **kw)
         self.relu = relu
         self.impl = "hip"
+        self.link_output = link_output  # output's second gradient summed in-kernel (GradLink)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         training = self.training or not self.track_running_stats
@@ -135,7 +179,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         nbt = self.num_batches_tracked if (self.training and self.track_running_stats) else None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, nbt, training, momentum if momentum is not None else 0.0,
-                              self.eps, self.relu, residual, self.impl)
+                              self.eps, self.relu, residual, self.impl, self.link_output)
 
     def _cumulative(self, x, residual):
         self.num_batches_tracked.add_(1)

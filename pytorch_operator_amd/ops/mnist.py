@@ -173,9 +173,13 @@ class BatchStage:
 
 def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
                b2: torch.Tensor, B: int, a1=None, idx1=None, xn=None, lab=None, a2=None,
-               idx2=None, stage: Optional[BatchStage] = None):
+               idx2=None, stage: Optional[BatchStage] = None, deferred: Optional[dict] = None):
     """conv1+pool+conv2+pool fused (one launch): returns (a1, idx1, xn, lab, a2, idx2).
-    ``stage``: take the batch from a ``BatchStage`` when its tag matches the cursor."""
+    ``stage``: take the batch from a ``BatchStage`` when its tag matches the cursor.
+    ``deferred``: dict(params, grads, buf, pend, lr, momentum, dampening, weight_decay,
+    nesterov, grad_scale, first_step) -- extra grid rows apply SGD(momentum) to the flat
+    range when the int32 device flag ``pend`` is non-zero (an update deferred from the
+    previous step; ``fc1_fwd_parts(clear=pend)`` clears the flag after this launch)."""
     lib = _native.load()
     src.check_batch(B)
     _req(w1, (20, 1, 5, 5), torch.float32, "conv1.weight")
@@ -204,12 +208,27 @@ def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.T
             raise ValueError("a staged batch needs a uint8 source with labels, perm and a device cursor")
         if stage.B < B:
             raise ValueError("stage holds fewer samples than B")
+    d = deferred or {}
+    sg_n = 0
+    if deferred is not None:
+        sg_n = d["params"].numel()
+        for t, nm in ((d["params"], "params"), (d["grads"], "grads"), (d["buf"], "buf")):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != sg_n or t.data_ptr() % 16:
+                raise ValueError(f"deferred {nm} must be 16-byte aligned contiguous fp32 with {sg_n} elements")
+        if sg_n % 4:
+            raise ValueError("deferred range must be a multiple of 4 elements")
+        if d["pend"].dtype != torch.int32:
+            raise ValueError("deferred pend flag must be int32")
     rc = lib.pto_mnist_conv12_fwd(
         src.x.data_ptr(), int(src.is_u8), _ptr(src.labels), _ptr(src.perm), _ptr(src.cursor),
         src.host_offset, src.n_total, src.scale, src.shift, w1.data_ptr(), b1.data_ptr(),
         w2.data_ptr(), b2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(), _ptr(lab),
         a2.data_ptr(), idx2.data_ptr(), B, _ptr(stage.x if stage else None),
-        _ptr(stage.lab if stage else None), _ptr(stage.tag if stage else None), _stream())
+        _ptr(stage.lab if stage else None), _ptr(stage.tag if stage else None),
+        _ptr(d.get("params")), _ptr(d.get("grads")), _ptr(d.get("buf")), sg_n, _ptr(d.get("pend")),
+        float(d.get("lr", 0.0)), float(d.get("momentum", 0.0)), float(d.get("dampening", 0.0)),
+        float(d.get("weight_decay", 0.0)), float(d.get("grad_scale", 1.0)), int(d.get("nesterov", False)),
+        int(d.get("first_step", False)), _stream())
     _native.check(rc, "conv12_fwd")
     return a1, idx1, xn, lab, a2, idx2
 
@@ -230,18 +249,20 @@ def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out
 
 
-def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  clear: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Split-K fc1 forward: the two pre-activation halves ``out[z] = x[:, Kz] @ w[:, Kz].T``
     (K halves of 400) as fp32 [2, B, 500]; ``head(..., h_second=out[1], fc1_bias=b,
     h_out=h)`` finishes ``h = relu(out[0] + out[1] + b)``.  256 workgroups instead of 128:
-    half the operand bytes per CU on the latency-bound load phase."""
+    half the operand bytes per CU on the latency-bound load phase.  ``clear``: int32 device
+    flag set to 0 by the launch (conv12_fwd's deferred-SGD flag)."""
     lib = _native.load()
     B = x.shape[0]
     _req(x, (B, 800), torch.float32, "x")
     _req(w, (500, 800), torch.float32, "fc1.weight")
     out = torch.empty((2, B, 500), device=x.device) if out is None else out
     _req(out, (2, B, 500), torch.float32, "fc1 partials")
-    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _stream())
+    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _ptr(clear), _stream())
     _native.check(rc, "fc1_fwd_parts")
     return out
 
@@ -656,13 +677,14 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                      grad_scale: float = 1.0, first_step: bool = False,
                      step_counter: Optional[torch.Tensor] = None,
                      extra: Optional[tuple] = None, big: Optional[tuple] = None,
-                     copy: Optional[tuple] = None) -> None:
+                     copy: Optional[tuple] = None, set_pend: Optional[torch.Tensor] = None) -> None:
     """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch).
 
     ``extra=(params2, grads2, buf2)``: also apply the same SGD to a second,
     already-reduced range in the same launch (e.g. the fc parameters).
     ``big=(rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows.
     ``copy=(src, dst)``: also copy ``src`` into ``dst`` (equal-size contiguous fp32).
+    ``set_pend``: int32 device flag set to 1 (a deferred update is pending, see conv12_fwd).
     """
     lib = _native.load()
     n = params.numel()
@@ -694,7 +716,7 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                                  float(dampening), float(weight_decay), float(grad_scale),
                                  int(nesterov), int(first_step), _ptr(step_counter), _ptr(p2),
                                  _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi), _ptr(cs), _ptr(cd),
-                                 int(cn), _stream())
+                                 int(cn), _ptr(set_pend), _stream())
     _native.check(rc, "slab_reduce_sgd")
 
 
@@ -706,8 +728,9 @@ def set_debug_buffer(buf: Optional[torch.Tensor]) -> None:
 def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, *, lr: float,
                   momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
                   nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-                  step_counter: Optional[torch.Tensor] = None) -> None:
-    """In-place fused SGD(momentum) over flat fp32 buffers (torch.optim.SGD math)."""
+                  step_counter: Optional[torch.Tensor] = None, cond: Optional[torch.Tensor] = None) -> None:
+    """In-place fused SGD(momentum) over flat fp32 buffers (torch.optim.SGD math).
+    ``cond``: int32 device flag; the update is skipped when it is 0."""
     lib = _native.load()
     n = params.numel()
     for t, nm in ((params, "params"), (grads, "grads"), (buf, "momentum_buffer")):
@@ -718,5 +741,5 @@ def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, 
     rc = lib.pto_sgd_momentum(params.data_ptr(), grads.data_ptr(), buf.data_ptr(), n, float(lr),
                               float(momentum), float(dampening), float(weight_decay),
                               float(grad_scale), int(nesterov), int(first_step),
-                              _ptr(step_counter), _stream())
+                              _ptr(step_counter), _ptr(cond), _stream())
     _native.check(rc, "sgd_momentum")

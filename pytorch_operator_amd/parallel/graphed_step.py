@@ -12,7 +12,9 @@ Modes
                 world  > 1: three graphs per step -- G1 (forward + fc backward),
                 G2 (conv backward), G3 (SGD) -- with the two bucket all-reduces
                 issued eagerly between them (the fc bucket's RCCL all-reduce
-                overlaps G2 on RCCL's own stream; G3 waits for both).
+                overlaps G2 on RCCL's own stream; G3 waits for both).  With
+                ``launch="stream"`` the three pieces are native recordings whose
+                kernel lists are launched directly on the stream.
 ``graph-comm``  the all-reduces are captured too: one graph per step (RCCL
                 collectives support stream capture).  Fewest host calls.
 
@@ -128,6 +130,7 @@ class GraphedStep:
         tr = trainer
         if tr._first_step:
             tr.train_step()  # momentum initialisation happens outside any graph
+            tr.flush_deferred()  # and a deferred (fc_sgd="next") first-step update too
             self.internal_steps += 1
         torch.cuda.synchronize(tr.device)
         whole_step = self.world == 1 or getattr(tr.grad_sync, "fused_sgd", False)
@@ -170,21 +173,31 @@ class GraphedStep:
             inv = 1.0 / self.world
             self._split = True
             self.steps_per_graph = 1
-            self._g1 = _capture(lambda: tr.forward_backward_fc(), tr.device)
-            self._g2 = _capture(lambda: tr.backward_conv(), tr.device)
-            self._g3 = _capture(lambda: tr.optimizer_step(grad_scale=inv), tr.device)
+            pieces = (lambda: tr.forward_backward_fc(), lambda: tr.backward_conv(),
+                      lambda: tr.optimizer_step(grad_scale=inv))
+            if native and launch == "stream":
+                # the three pieces launch only this library's kernels: record them natively
+                # and launch their kernel lists straight onto the stream (no ~8.6 us
+                # hipGraphLaunch gap per piece, three per step); profiles/r3_split_launch_ab.md
+                gs = [NativeGraph(f, tr.device) for f in pieces]
+                if all(g.stream_ok for g in gs):
+                    self.launch = "stream"
+                    self._g1, self._g2, self._g3 = gs
+            if self.launch != "stream":
+                self._g1, self._g2, self._g3 = (_TorchGraph(_capture(f, tr.device)) for f in pieces)
         torch.cuda.synchronize(tr.device)
 
     def _split_steps(self, n: int) -> None:
         tr = self.tr
         sync = tr.grad_sync
+        go = (lambda g: g.replay_stream(1)) if self.launch == "stream" else (lambda g: g.replay(1))
         for _ in range(n):
-            self._g1.replay()
+            go(self._g1)
             sync.fc_ready(tr.fc_bucket())
-            self._g2.replay()
+            go(self._g2)
             sync.conv_ready(tr.conv_bucket())
             sync.finish()
-            self._g3.replay()
+            go(self._g3)
 
     def warm(self, n_steps: int) -> None:
         """``n_steps`` untimed steps of any count: whole replays of the timed graph first (a

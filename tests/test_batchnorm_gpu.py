@@ -100,3 +100,70 @@ def test_module_matches_library_module_and_is_deterministic():
     torch.testing.assert_close(outs[0][1], xr.grad, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(outs[0][2], ref.weight.grad, rtol=1e-3, atol=1e-3)
     assert int(m.num_batches_tracked) == 2 and int(ref.num_batches_tracked) == 1
+
+
+def _chain(dtype, link, seed=0, C=64, shape=(4, 64, 9, 7)):
+    """Two bottleneck-style BNs: y1 = relu(bn1(x1)) [producer], y2 = relu(bn2(h(y1)) + y1)
+    [consumer: y1 feeds both a 1x1 mixing 'conv' h and the residual add]; loss = <y2, dy>."""
+    from pytorch_operator_amd.ops.batchnorm import batch_norm_act
+    g = torch.Generator().manual_seed(seed)
+    x1 = torch.randn(shape, generator=g).to(dtype)
+    wm = (torch.randn(C, C, generator=g) / C ** 0.5).to(dtype)
+    w1, b1 = 0.5 + torch.rand(C, generator=g), 0.2 * torch.randn(C, generator=g)
+    w2, b2 = 0.5 + torch.rand(C, generator=g), 0.2 * torch.randn(C, generator=g)
+    dy = torch.randn(shape, generator=g).to(dtype)
+    cl = dict(memory_format=torch.channels_last)
+
+    def h(y, w):
+        return torch.einsum("nchw,dc->ndhw", y, w).contiguous(**cl)
+
+    xg = x1.cuda().contiguous(**cl).requires_grad_(True)
+    p = [t.cuda().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    y1 = batch_norm_act(xg, p[0], p[1], relu=True, impl="hip", link_output=link)
+    y2 = batch_norm_act(h(y1, wm.cuda()), p[2], p[3], relu=True, residual=y1, impl="hip")
+    y2.backward(dy.cuda().contiguous(**cl))
+    got = [xg.grad] + [t.grad for t in p]
+
+    xr = x1.double().requires_grad_(True)
+    pr = [t.double().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    y1r = F.relu(F.batch_norm(xr, None, None, pr[0], pr[1], True, 0.1, 1e-5))
+    y2r = F.relu(F.batch_norm(h(y1r, wm.double()), None, None, pr[2], pr[3], True, 0.1, 1e-5) + y1r)
+    y2r.backward(dy.double())
+    return got, [xr.grad] + [t.grad for t in pr], y1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_residual_gradient_summed_in_bn_backward_matches_fp64(dtype):
+    """GradLink: the consumer BN hands the residual gradient to the producer BN, whose backward
+    sums it with the conv-branch gradient in-kernel (fp32) -- dx and every dgamma/dbeta match
+    an fp64 autograd reference, the link was claimed and drained, and the result agrees with
+    the unfused path (autograd's own gradient sum)."""
+    got, ref, y1 = _chain(dtype, link=True)
+    assert y1._pto_link.claimed and y1._pto_link.dz is None
+    t = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    for name, a, r in zip(["dx", "dgamma1", "dbeta1", "dgamma2", "dbeta2"], got, ref):
+        tt = t if name == "dx" else dict(rtol=2e-3, atol=2e-3) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+        torch.testing.assert_close(a.detach().cpu().double(), r.double(), msg=name, **tt)
+    unfused, _, y1u = _chain(dtype, link=False)
+    assert getattr(y1u, "_pto_link", None) is None
+    for a, b in zip(got, unfused):
+        torch.testing.assert_close(a, b, rtol=t["rtol"], atol=t["atol"])
+
+
+def test_resnet_blocks_claim_links():
+    """In the ResNet every identity bottleneck's residual comes from the previous bn3 through a
+    link (12 of ResNet-50's 16 blocks); downsample blocks keep autograd's path."""
+    from pytorch_operator_amd.models.resnet import ResNet
+    m = ResNet((2, 2, 1, 1), num_classes=10, width=8).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+    links = []
+    hook = lambda mod, inp, out: links.append(getattr(out, "_pto_link", None))  # noqa: E731
+    hs = [b.bn3.register_forward_hook(hook) for b in m.modules() if hasattr(b, "bn3")]
+    out = m(x)
+    out.sum().backward()
+    for h in hs:
+        h.remove()
+    assert len(links) == 6 and all(lk is not None for lk in links)
+    # blocks 2 of layer1 / layer2 take their residual from the previous block's bn3
+    assert [lk.claimed for lk in links] == [True, False, True, False, False, False]
+    assert all(lk.dz is None for lk in links)

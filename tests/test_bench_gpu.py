@@ -1,0 +1,56 @@
+"""bench.py at world 2 on the box's one GPU: the driver's multi-GPU command shape
+(``torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 ...``), with gloo as the
+process-group backend (RCCL wants one GPU per rank) and both ranks sharing cuda:0.
+
+Checks the JSON line's DDP invariants (n_gpus, replicas_in_sync, grad_allreduce_error)
+and the PyTorchJob it runs after the timed region: two pods through the real operator and
+kubelet emulator (``--job-gpus 0,0`` lets them share the GPU), Succeeded, with the pods'
+steady-state step-time percentiles in the line.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("allreduce", ["xgmi", "auto"])
+def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
+    out = tmp_path / "bench.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--allreduce", allreduce, "--steps", "20", "--warmup", "5",
+           "--job-gpus", "0,0", "--job-timeout", "200", "--json-out", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=ROOT,
+                       env=dict(os.environ, PYTHONPATH=str(ROOT)))
+    assert r.returncode == 0 and out.exists(), r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
+    assert line["config"]["parallelism"] == "dp2" and line["config"]["backend"] == "gloo"
+    assert line["replicas_in_sync"] is True, line
+    assert line["grad_allreduce_error"] == 0, line
+    if allreduce == "xgmi":
+        assert line["config"]["grad_allreduce"] == "xgmi", line
+    else:
+        assert line["config"]["grad_allreduce"] in ("xgmi", "rccl"), line
+        assert line["config"]["allreduce_trial"] is not None, line
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    job = line["job"]
+    assert job.get("result") == "Succeeded" and job.get("replicas") == 2, job
+    assert job["node_gpus"] == [0, 0] and job["backend"] == "gloo", job
+    sm = job.get("worker_step_ms")
+    assert sm and sm["n"] > 0 and 0 < sm["p50"] <= sm["p90"], job
+    assert job["worker_capture_seconds"] is not None and job["worker_train_seconds"] > 0, job

@@ -410,9 +410,16 @@ def test_repeated_events_are_aggregated(cluster, tmp_path):
     c.rest.create(PYTORCHJOBS, make_job("e2e-events", replica(1, "busybox", command=py(code), policy="ExitCode")), NS)
     types, job = wait_finished(c, "e2e-events", timeout=120)
     assert types[-1] == "Succeeded", job["status"]
-    time.sleep(0.5)  # the event sink posts asynchronously
-    evs = [e for e in c.rest.list(EVENTS, NS)["items"]
-           if (e.get("involvedObject") or {}).get("name") == "e2e-events"]
+    # the event sink posts asynchronously: poll until the create/delete counts settle
+    deadline = time.time() + 15
+    while True:
+        evs = [e for e in c.rest.list(EVENTS, NS)["items"]
+               if (e.get("involvedObject") or {}).get("name") == "e2e-events"]
+        cr = [e.get("count", 1) for e in evs if e["reason"] == "SuccessfulCreatePod"]
+        de = [e.get("count", 1) for e in evs if e["reason"] == "SuccessfulDeletePod"]
+        if (len(cr) == 1 and len(de) == 1 and cr[0] == de[0] + 1) or time.time() > deadline:
+            break
+        time.sleep(0.2)
     created = [e for e in evs if e["reason"] == "SuccessfulCreatePod" and e["message"] == "Created pod: e2e-events-master-0"]
     assert len(created) == 1, [(e["metadata"]["name"], e.get("count")) for e in created]
     deleted = [e for e in evs if e["reason"] == "SuccessfulDeletePod"]

@@ -458,3 +458,42 @@ def test_round3_step_matches_round2_step(lib, B):
     ce = new.layout.conv_end
     assert _rel(new.flat_grads[ce:], old.flat_grads[ce:]) < 1e-5
     assert _rel(new.flat_grads[:ce], old.flat_grads[:ce]) < 1e-5
+
+
+@pytest.mark.parametrize("dampening", [0.0, 0.3])
+def test_deferred_fc_sgd_is_bit_identical_to_tail(lib, dampening):
+    """fc_sgd="next" (the tail leaves the fc update pending; the next conv12 launch's extra
+    grid rows apply it, fc1_fwd clears the flag) trains bit-identically to the tail SGD:
+    eager steps, a mid-run public read (flush), a graph captured after the eager first step
+    (dampening != 0 exercises the first-step buffer rule), state_dict and momentum."""
+    n = 640
+    x, y = _data(n, seed=91, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(4)).to(torch.int32)
+    a = _stage_trainer(x, y, perm, fc_sgd="next")
+    b = _stage_trainer(x, y, perm, fc_sgd="tail")
+    for tr in (a, b):
+        tr.dampening = dampening
+        tr._first_step = dampening != 0.0
+        for _ in range(2):
+            tr.train_step()
+    torch.cuda.synchronize()
+    assert a._defer_used and int(a._pend.item()) == 1
+    assert torch.equal(a.flat_params, b.flat_params)  # the read flushes the pending update
+    assert int(a._pend.item()) == 0
+    for tr in (a, b):
+        tr.train_step()
+        tr.train_step()
+        g = tr.capture(1)
+        for _ in range(3):
+            g.replay()
+    torch.cuda.synchronize()
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 7
+    assert torch.equal(a.flat_params, b.flat_params)
+    assert torch.equal(a.flat_momentum, b.flat_momentum)
+    sa, sb = a.state_dict(), b.state_dict()
+    assert all(torch.equal(sa[k], sb[k]) for k in sb)
+    # a flush with nothing pending is a no-op
+    before = a._fp.clone()
+    a.flush_deferred()
+    torch.cuda.synchronize()
+    assert torch.equal(a._fp, before)

@@ -10,7 +10,7 @@ REPS=${REPS:-3}
 for rep in $(seq $REPS); do
 for lib in "" $(ls pytorch_operator_amd/_lib/exp/*.so 2>/dev/null); do
   a="$(PTO_HIP_LIB=$lib timeout -k 10 120 python bench.py --steps 2000 --warmup 50 --job-latency 0 $BENCH_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*' | cut -d' ' -f2)" || exit 1
-  b=""; for i in 1 2; do b="$b $(PTO_HIP_LIB=$lib timeout -k 10 120 python bench.py --steps 20 --warmup 5 --job-latency 0 $BENCH_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*' | cut -d' ' -f2)" || exit 1; done
+  b=""; for i in $(seq ${K20N:-2}); do b="$b $(PTO_HIP_LIB=$lib timeout -k 10 120 python bench.py --steps 20 --warmup 5 --job-latency 0 $BENCH_ARGS 2>/dev/null | grep -o '"ms_per_step": [0-9.]*' | cut -d' ' -f2)" || exit 1; done
   echo "${lib:-in-tree} | K2000: $a | K20:$b" | tee -a gpurun_out/ab_libs.txt
 done
 done
