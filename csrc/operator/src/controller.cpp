@@ -132,7 +132,10 @@ void EventSink::loop() {
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-      if (q_.empty()) return;
+      // on shutdown the queue is dropped (main() already gave flush() its bounded drain):
+      // posting a backlog through the client's 5-qps limiter could hold the exit for tens
+      // of seconds under job churn, like a broadcaster that outlives its process
+      if (stop_ || q_.empty()) return;
       ev = q_.front();
       q_.pop_front();
       inflight_++;

@@ -125,3 +125,92 @@ def test_sanitized_operator_runs_a_job(tmp_path, san):
     assert c.operator.returncode == 0, log[-4000:]
     assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-4000:]
     assert "WARNING: ThreadSanitizer" not in log, log[-6000:]
+
+
+def _churn_job(name, kind, marker_dir):
+    """kind: ok (Master+2 Workers exit 0), retry (ExitCode policy: exit 130 twice, then 0),
+    fail (Never policy, exit 1 -> Failed), slow (sleeps; deleted while running)."""
+    def ctr(cmd):
+        return [{"name": "pytorch", "image": "busybox", "command": ["python", "-c", cmd]}]
+    if kind == "retry":
+        m = str(marker_dir / f"{name}.n")
+        cmd = (f"import os,sys; p={m!r}; n=int(open(p).read()) if os.path.exists(p) else 0; "
+               f"open(p,'w').write(str(n+1)); sys.exit(0 if n >= 2 else 130)")
+        master = {"replicas": 1, "restartPolicy": "ExitCode", "template": {"spec": {"containers": ctr(cmd)}}}
+        return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name},
+                "spec": {"cleanPodPolicy": "All", "pytorchReplicaSpecs": {"Master": master}}}
+    cmd = {"ok": "pass", "fail": "import sys; sys.exit(1)", "slow": "import time; time.sleep(30)"}[kind]
+    pol = "Never" if kind == "fail" else "OnFailure"
+    rs = {"Master": {"replicas": 1, "restartPolicy": pol, "template": {"spec": {"containers": ctr(cmd)}}},
+          "Worker": {"replicas": 2, "restartPolicy": pol, "template": {"spec": {"containers": ctr(
+              "import time; time.sleep(30)" if kind == "slow" else "pass")}}}}
+    return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": name},
+            "spec": {"cleanPodPolicy": "All", "pytorchReplicaSpecs": rs}}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_sanitized_operator_concurrent_jobs_with_churn(tmp_path, san):
+    """Sanitizer builds under contention: --threadiness=4 workers reconcile 12 concurrent jobs
+    (succeeding, ExitCode-restarting, failing, and long-running ones deleted mid-run and
+    recreated under the same name) while pods churn.  Every surviving job must reach its
+    terminal condition and the sanitizer must stay silent (no data race, no memory error,
+    no leak at exit)."""
+    from pytorch_operator_amd.cluster.local import LocalCluster
+    from pytorch_operator_amd.cluster.rest import PYTORCHJOBS
+    exe = nb.build_operator(sanitize=san)
+    env = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1",
+           "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}
+    c = LocalCluster(workdir=str(tmp_path / "c"), start_operator=False, operator_env=env,
+                     operator_args=["--threadiness=4"])
+    c.start()
+    marks = tmp_path / "marks"
+    marks.mkdir()
+    kinds = ["ok"] * 4 + ["retry"] * 3 + ["fail"] * 2 + ["slow"] * 3
+    names = [f"churn-{i}-{k}" for i, k in enumerate(kinds)]
+    try:
+        import pytorch_operator_amd.cluster.local as local
+        orig = local.operator_binary
+        local.operator_binary = lambda: str(exe)
+        try:
+            c.start_operator_process()
+        finally:
+            local.operator_binary = orig
+        c.wait_operator_ready(timeout=90)
+        for n, k in zip(names, kinds):
+            c.rest.create(PYTORCHJOBS, _churn_job(n, k, marks), "default")
+        # churn: delete the long-running jobs while their pods run, recreate one of them
+        time.sleep(2.0)
+        slow = [n for n, k in zip(names, kinds) if k == "slow"]
+        for n in slow:
+            c.rest.delete(PYTORCHJOBS, n, "default")
+        time.sleep(1.0)
+        c.rest.create(PYTORCHJOBS, _churn_job(slow[0], "ok", marks), "default")
+        want = {n: ("Failed" if k == "fail" else "Succeeded") for n, k in zip(names, kinds) if k != "slow"}
+        want[slow[0]] = "Succeeded"
+        done = {}
+        t0 = time.time()
+        while len(done) < len(want) and time.time() - t0 < 240:
+            for n in want:
+                if n in done:
+                    continue
+                try:
+                    st = c.rest.get(PYTORCHJOBS, n, "default").get("status") or {}
+                except Exception:  # noqa: BLE001 -- a recreate can race the first get
+                    continue
+                types = [x["type"] for x in st.get("conditions") or [] if x.get("status") == "True"]
+                for t in ("Succeeded", "Failed"):
+                    if t in types:
+                        done[n] = t
+            time.sleep(0.3)
+        assert done == want, (done, open(c.operator_log).read()[-4000:])
+        for n in want:
+            c.rest.delete(PYTORCHJOBS, n, "default")
+        time.sleep(1.0)
+    finally:
+        c.stop()
+    log = open(c.operator_log).read()
+    assert c.operator.returncode == 0, log[-4000:]
+    assert "ERROR: AddressSanitizer" not in log and "runtime error:" not in log, log[-4000:]
+    assert "ERROR: LeakSanitizer" not in log, log[-4000:]
+    assert "WARNING: ThreadSanitizer" not in log, log[-6000:]
