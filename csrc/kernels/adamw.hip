@@ -20,7 +20,7 @@ namespace {
 constexpr int kT = 256;
 
 struct AdamArgs {
-  float lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2;
+  float lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2, gscale;
 };
 
 __device__ __forceinline__ uint32_t bf16_rne(float f) {
@@ -29,6 +29,7 @@ __device__ __forceinline__ uint32_t bf16_rne(float f) {
 }
 
 __device__ __forceinline__ float adam1(float& p, float& m, float& v, float g, const AdamArgs& a) {
+  g *= a.gscale;  // 1, or the data-parallel 1/W of an unscaled gradient sum (exact for W = 2^k)
   p *= 1.f - a.lr * a.wd;
   m = a.b1 * m + (1.f - a.b1) * g;
   v = a.b2 * v + (1.f - a.b2) * g * g;
@@ -86,14 +87,16 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 extern "C" {
 
 // grad_bf16: gradient dtype (1 = bf16, 0 = fp32).  out: bf16 weight to refresh (nullptr for
-// fp32 parameters, whose master IS the parameter).  step >= 1.
-int pto_adamw_step(float* master, float* m, float* v, const void* grad, void* out, long n, int grad_bf16,
-                   float lr, float b1, float b2, float eps, float wd, int step, void* stream) {
+// fp32 parameters, whose master IS the parameter).  step >= 1.  grad_scale multiplies the
+// gradient first (ZeRO's gradient-view buckets hold the unscaled sum over ranks).
+int pto_adamw_step_scaled(float* master, float* m, float* v, const void* grad, void* out, long n, int grad_bf16,
+                          float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
+                          void* stream) {
   if (n <= 0 || step < 1) return -1;
   if (!aligned16(master) || !aligned16(m) || !aligned16(v) || !aligned16(grad) || (out && !aligned16(out)))
     return -2;
   AdamArgs a;
-  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
+  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd; a.gscale = grad_scale;
   a.inv_bc1 = (float)(1.0 / (1.0 - pow((double)b1, step)));
   a.inv_sqrt_bc2 = (float)(1.0 / sqrt(1.0 - pow((double)b2, step)));
   const long work = n / 4 + 1;
@@ -110,6 +113,11 @@ int pto_adamw_step(float* master, float* m, float* v, const void* grad, void* ou
   else hipLaunchKernelGGL((adamw_kernel<false, false>), grid, block, 0, s, master, m, v, grad,
                           (uint16_t*)nullptr, n, a);
   return (int)hipGetLastError();
+}
+
+int pto_adamw_step(float* master, float* m, float* v, const void* grad, void* out, long n, int grad_bf16,
+                   float lr, float b1, float b2, float eps, float wd, int step, void* stream) {
+  return pto_adamw_step_scaled(master, m, v, grad, out, n, grad_bf16, lr, b1, b2, eps, wd, step, 1.f, stream);
 }
 
 }  // extern "C"

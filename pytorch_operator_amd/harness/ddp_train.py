@@ -51,6 +51,9 @@ def parse_args(argv=None):
                    help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
     p.add_argument("--bn", choices=["hip", "library"], default="hip",
                    help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
+    p.add_argument("--bn-link", type=int, default=1,
+                   help="ResNet: each bottleneck's bn3 backward also sums the next block's residual "
+                        "gradient in-kernel (ops/batchnorm.py GradLink) instead of autograd's add pass (1/0)")
     p.add_argument("--pool", choices=["hip", "library"], default="hip",
                    help="ResNet stem max-pool: HIP kernels (1-byte taps, gather backward) or PyTorch's op")
     p.add_argument("--conv1x1", choices=["gemm", "library"], default="library",
@@ -76,6 +79,8 @@ def parse_args(argv=None):
                         "rank's 1/W shard, all-gather bf16 weights (parallel/zero.py) instead of DDP's "
                         "fp32 all-reduce + a full optimizer per rank; auto = on when world > 1")
     p.add_argument("--zero-bucket-mb", type=float, default=256.0)
+    p.add_argument("--zero-grad-view", type=int, default=1,
+                   help="ZeRO bf16 buckets: backward GEMMs write weight gradients into the bucket (1/0)")
     p.add_argument("--gemm-tuning", choices=["off", "use", "tune"], default="use",
                    help="PyTorch TunableOp over hipBLASLt/rocBLAS for the model's GEMM shapes: 'use' "
                         "replays the measured per-shape winners in --gemm-tuning-file (shapes not in "
@@ -106,6 +111,10 @@ def build(args, device, world: int = 1):
     if args.model.startswith("resnet"):
         from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl, set_pool_impl
         model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
+        from ..ops.batchnorm import BatchNormAct2d
+        for m in model.modules():
+            if isinstance(m, BatchNormAct2d) and m.link_output:
+                m.link_output = bool(args.bn_link)
         set_pool_impl(model, args.pool)
         set_conv1x1_impl(model, args.conv1x1)
         fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format
@@ -127,9 +136,13 @@ def build(args, device, world: int = 1):
         from ..ops.optim import to_bf16_matmul_weights
         from ..parallel.zero import ZeroAdamW
         to_bf16_matmul_weights(model)
+        # bf16 gradient buckets with a bf16 reduce (at world 1 the buckets always take the
+        # parameters' dtype): gradient-as-bucket-view then lets the backward GEMMs write dW
+        # into the buckets directly
         opt = ZeroAdamW(model, lr=args.lr or 3e-4, betas=(0.9, 0.95), weight_decay=0.1,
                         bucket_mb=args.zero_bucket_mb,
-                        reduce_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else torch.float32)
+                        reduce_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else torch.float32,
+                        grad_view=bool(args.zero_grad_view))
         return model, opt
     if use_master_weights(args, device):
         from ..ops.optim import MasterAdamW, install_overlap, to_bf16_matmul_weights
@@ -366,7 +379,8 @@ def main(argv=None) -> int:
            "parallelism": f"dp{world}", "bucket_mb": args.bucket_mb, "allreduce_dtype": args.allreduce_dtype,
            "master_weights": use_master_weights(args, dev) or zero, "zero": 1 if zero else 0}
     if zero:
-        res.update(optimizer_state_gb_per_rank=round(opt.state_bytes() / 2 ** 30, 2), zero_buckets=len(opt.buckets))
+        res.update(optimizer_state_gb_per_rank=round(opt.state_bytes() / 2 ** 30, 2), zero_buckets=len(opt.buckets),
+                   zero_grad_sinks=opt.sinks, zero_grad_dtypes=sorted({str(b.grad32.dtype).replace("torch.", "") for b in opt.buckets}))
     res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
         res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd,
@@ -378,7 +392,7 @@ def main(argv=None) -> int:
         write_tuning_file(out)
         res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
-        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn,
+        res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn, bn_link=args.bn_link,
                    pool=args.pool,
                    conv1x1=args.conv1x1)
     if args.ckpt_dir:

@@ -145,6 +145,7 @@ _SIGNATURES = {
     "pto_xent_bwd": [_VP, _VP, _VP, _VP, _VP, _L, _I, _L, _I, _VP],
     # adamw.hip
     "pto_adamw_step": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _VP],
+    "pto_adamw_step_scaled": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _F, _VP],
     # batchnorm.hip
     "pto_bn_plan": [_L, _I, ctypes.POINTER(_I)],
     "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP],

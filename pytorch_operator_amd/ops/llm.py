@@ -276,6 +276,9 @@ class _LinearTN(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.save_for_backward(x2, w)
         ctx.xshape = x.shape
+        # a gradient sink (parallel/zero.py, gradient-as-bucket-view): dW is written by the
+        # GEMM straight into the optimizer's bucket slot -- no .grad tensor, no copy pass
+        ctx.sink = getattr(w, "_pto_grad_sink", None)
         return F.linear(x2, w).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -286,7 +289,12 @@ class _LinearTN(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = F.linear(dy2, transpose2d(w)).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = F.linear(transpose2d(dy2), transpose2d(x2))
+            sink = ctx.sink
+            if sink is not None and sink.view.dtype == x2.dtype and sink.view.shape == w.shape:
+                torch.mm(transpose2d(dy2), transpose2d(x2).t(), out=sink.view)
+                sink.ready()
+            else:
+                dw = F.linear(transpose2d(dy2), transpose2d(x2))
         return dx, dw
 
 

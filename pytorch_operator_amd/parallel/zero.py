@@ -22,8 +22,13 @@ and update time are divided by W.  Buckets are large (``bucket_mb``, default 256
 fp32 gradient): few collectives, each well into RCCL's bandwidth regime on point-to-point
 xGMI links.
 
-``reduce_dtype=torch.bfloat16`` (``--allreduce-dtype bf16``) halves the reduce-scatter bytes,
-like DDP's ``bf16_compress_hook``.
+``reduce_dtype=torch.bfloat16`` (``--allreduce-dtype bf16``; at world 1, where nothing is
+reduced, every bucket takes its parameters' dtype) halves the reduce-scatter bytes, like DDP's
+``bf16_compress_hook``, and enables **gradient-as-bucket-view** (``grad_view``): every bf16
+matmul weight gets a ``_pto_grad_sink`` whose view IS its bucket slot, and ``linear_tn``'s
+backward GEMM writes dW there directly (``ops/llm.py``) -- no bf16 ``.grad`` allocation and no
+deposit copy pass (the round-2 world-1 cost: 389 vs 365 ms/step and +30 GB).  Such buckets
+hold the unscaled gradient sum; the 1/W rides on the AdamW kernel (exact for W = 2^k).
 
 Numerics (fp32 reduction) equal ``DDP(fp32 comm hook) + MasterAdamW``: the same fp32 sum of the same
 ``grad / W`` terms, the same AdamW per element (tests/test_harness.py pins the parameter
@@ -41,6 +46,14 @@ import torch.nn as nn
 _ALIGN = 64  # shard lengths are multiples of this (16-byte aligned fp32 / bf16 shard pointers)
 
 
+class _Sink:
+    """Destination of a weight gradient written in place by a backward GEMM."""
+    __slots__ = ("view", "ready")
+
+    def __init__(self, view: torch.Tensor, ready):
+        self.view, self.ready = view, ready
+
+
 class _Bucket:
     def __init__(self, params: List[nn.Parameter], world: int, rank: int, reduce_dtype=torch.float32):
         self.params = params
@@ -51,9 +64,12 @@ class _Bucket:
         self.npad = self.shard * world
         self.lo = rank * self.shard
         self.flat_w = torch.zeros(self.npad, dtype=self.dtype, device=dev)
-        self.grad32 = torch.zeros(self.npad, dtype=reduce_dtype, device=dev)  # gradient bucket
+        # gradient bucket: the reduce dtype; at world 1 (nothing is reduced) the parameters' own
+        # dtype, i.e. exactly the .grad autograd would have produced
+        gdt = reduce_dtype if world > 1 else self.dtype
+        self.grad32 = torch.zeros(self.npad, dtype=gdt, device=dev)
         # world 1: the shard IS the bucket (no reduce-scatter, no copy)
-        self.gshard = self.grad32 if world == 1 else torch.zeros(self.shard, dtype=reduce_dtype, device=dev)
+        self.gshard = self.grad32 if world == 1 else torch.zeros(self.shard, dtype=gdt, device=dev)
         self.slot: Dict[int, int] = {}
         masters = torch.zeros(self.npad, dtype=torch.float32, device=dev) if self.dtype != torch.float32 else None
         off = 0
@@ -78,6 +94,7 @@ class _Bucket:
         self.arrived: set = set()  # ids of the parameters whose gradient was deposited this step
         self.rs_work = None
         self.ag_work = None
+        self.unscaled = False  # grad_view bucket: holds sum(g), AdamW applies 1/W
 
     def w_shard(self) -> torch.Tensor:
         return self.flat_w[self.lo:self.lo + self.shard]
@@ -89,7 +106,7 @@ class ZeroAdamW:
     Weights are broadcast from rank 0 at construction (DDP constructor semantics)."""
 
     def __init__(self, model: nn.Module, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
-                 group=None, bucket_mb: float = 256.0, reduce_dtype=torch.float32):
+                 group=None, bucket_mb: float = 256.0, reduce_dtype=torch.float32, grad_view: bool = True):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -127,6 +144,18 @@ class ZeroAdamW:
         self._of: Dict[int, _Bucket] = {id(p): b for b in self.buckets for p in b.params}
         for p in params:
             p.register_post_accumulate_grad_hook(self._on_grad)
+        self.sinks = 0
+        if grad_view:
+            for b in self.buckets:
+                if b.grad32.dtype != b.dtype or not b.flat_w.is_cuda:
+                    continue
+                b.unscaled = True
+                for p in b.params:
+                    if p.dim() == 2:
+                        off = b.slot[id(p)]
+                        p._pto_grad_sink = _Sink(b.grad32[off:off + p.numel()].view(p.shape),
+                                                 lambda p=p, b=b: self._arrive(b, p))
+                        self.sinks += 1
         self._hooked = 0
         for mod in model.modules():
             own = [self._of[id(p)] for p in mod.parameters(recurse=False) if id(p) in self._of]
@@ -142,18 +171,28 @@ class ZeroAdamW:
             raise RuntimeError("ZeroAdamW: a second backward before step() -- gradient accumulation "
                                "across backward passes is not supported (the bucket was already reduced)")
         off = b.slot[id(p)]
-        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
+        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1), b.unscaled)
         p.grad = None
+        self._arrive(b, p)
+
+    def _arrive(self, b: _Bucket, p: torch.Tensor) -> None:
+        if b.pending < 0:
+            raise RuntimeError("ZeroAdamW: a second backward before step() -- gradient accumulation "
+                               "across backward passes is not supported (the bucket was already reduced)")
+        if id(p) in b.arrived:
+            raise RuntimeError("ZeroAdamW: a parameter received two gradients in one backward (a weight "
+                               "used twice cannot write its gradient in place; construct with grad_view=False)")
         b.arrived.add(id(p))
         b.pending -= 1
         if b.pending == 0:
             self._reduce_scatter(b)
 
-    def _deposit(self, dst: torch.Tensor, g: torch.Tensor) -> None:
+    def _deposit(self, dst: torch.Tensor, g: torch.Tensor, unscaled: bool = False) -> None:
         """dst = g / W in the bucket dtype -- the comm hooks' ``grad / W`` before the sum.  For a
-        power-of-two W the scale is exact, so it rides on the cast copy (one pass)."""
+        power-of-two W the scale is exact, so it rides on the cast copy (one pass).  ``unscaled``
+        (grad_view buckets): plain copy, the 1/W is applied by AdamW."""
         w = self.world
-        if w == 1:
+        if w == 1 or unscaled:
             dst.copy_(g)
         elif w & (w - 1) == 0:
             src = g if dst.dtype == torch.float32 else g.to(dst.dtype)  # (out= never downcasts)
@@ -200,7 +239,7 @@ class ZeroAdamW:
                         if self.world == 1:
                             skip.setdefault(id(b), []).append((off, p.numel()))
                     else:
-                        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1))
+                        self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1), b.unscaled)
                         p.grad = None
                 self._reduce_scatter(b)
         # forward order (the last bucket holds the first layers): their all-gathers go first
@@ -246,10 +285,10 @@ class ZeroAdamW:
             from ..ops import _native
             stream = ctypes.c_void_p(torch.cuda.current_stream(w.device).cuda_stream)
             out = w.data_ptr() if b.master is not None else None
-            _native.check(_native.load().pto_adamw_step(
+            _native.check(_native.load().pto_adamw_step_scaled(
                 master.data_ptr(), b.exp_avg.data_ptr(), b.exp_avg_sq.data_ptr(), b.gshard.data_ptr(), out,
-                b.shard, 1 if self.reduce_dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps,
-                self.weight_decay, self.t, stream), "adamw_step")
+                b.shard, 1 if b.gshard.dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps,
+                self.weight_decay, self.t, 1.0 / self.world if b.unscaled else 1.0, stream), "adamw_step")
         else:
             from ..ops.optim import MasterAdamW
             st = {"step": self.t, "exp_avg": b.exp_avg, "exp_avg_sq": b.exp_avg_sq}

@@ -140,14 +140,22 @@ def test_residual_gradient_summed_in_bn_backward_matches_fp64(dtype):
     the unfused path (autograd's own gradient sum)."""
     got, ref, y1 = _chain(dtype, link=True)
     assert y1._pto_link.claimed and y1._pto_link.dz is None
-    t = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
-    for name, a, r in zip(["dx", "dgamma1", "dbeta1", "dgamma2", "dbeta2"], got, ref):
-        tt = t if name == "dx" else dict(rtol=2e-3, atol=2e-3) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
-        torch.testing.assert_close(a.detach().cpu().double(), r.double(), msg=name, **tt)
     unfused, _, y1u = _chain(dtype, link=False)
     assert getattr(y1u, "_pto_link", None) is None
-    for a, b in zip(got, unfused):
-        torch.testing.assert_close(a, b, rtol=t["rtol"], atol=t["atol"])
+    names = ["dx", "dgamma1", "dbeta1", "dgamma2", "dbeta2"]
+
+    def rel(a, r):
+        a, r = a.detach().cpu().double(), r.double()
+        return float((a - r).norm() / r.norm().clamp_min(1e-30))
+
+    for name, a, u, r in zip(names, got, unfused, ref):
+        ea, eu = rel(a, r), rel(u, r)
+        if dtype == torch.float32:
+            assert ea < 2e-5, (name, ea, eu)
+        else:
+            # bf16 activations: both paths round y1, h(y1) and the gradients to bf16; the fused
+            # fp32 sum must be no less accurate than autograd's bf16 sum (vs fp64)
+            assert ea < 2e-2 and ea <= 1.05 * eu + 1e-4, (name, ea, eu)
 
 
 def test_resnet_blocks_claim_links():

@@ -362,3 +362,36 @@ def test_llama_tiny_checkpoint_resume_on_gpu(tmp_path, zero):
 def test_resnet50_bf16_step_on_gpu():
     res = _run("--model", "resnet50", "--batch-size", "32", "--steps", "3", "--warmup", "1")
     assert res["value"] > 0 and res["loss"] == res["loss"]
+
+
+def test_zero_grad_view_matches_master_adamw():
+    """ZeRO-1 gradient-as-bucket-view at world 1 on the GPU: the TN-linear backward GEMMs write
+    dW straight into the bf16 buckets (no .grad, no copy pass) and the result is bit-identical
+    to MasterAdamW stepping autograd's bf16 .grad -- also with the AdamW grad scale path."""
+    import copy
+    from pytorch_operator_amd.models.llama import CONFIGS, Llama
+    from pytorch_operator_amd.ops.optim import MasterAdamW, to_bf16_matmul_weights
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+    torch.manual_seed(0)
+    with torch.device("cuda"):
+        m1 = Llama(CONFIGS["llama-tiny"])
+    m2 = copy.deepcopy(m1)
+    to_bf16_matmul_weights(m1)
+    to_bf16_matmul_weights(m2)
+    o1 = MasterAdamW(m1.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
+    o2 = ZeroAdamW(m2, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=0.05)
+    assert o2.sinks > 0 and all(b.unscaled for b in o2.buckets if b.grad32.dtype == torch.bfloat16)
+    assert {b.grad32.dtype for b in o2.buckets} == {torch.bfloat16, torch.float32}
+    x = torch.randint(0, 256, (2, 65), device="cuda")
+    for _ in range(3):
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(x[:, :-1], x[:, 1:])
+            loss.backward()
+            if o is o2:  # the sinks took every matmul weight's gradient: no .grad was materialised
+                assert all(p.grad is None for p in m2.parameters())
+            o.step()
+    torch.cuda.synchronize()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a, b), n
