@@ -228,3 +228,19 @@ def test_get_logs_follow_streams_until_the_container_ends(client, cluster):
     log = out["follow-logs-master-0"]
     assert "tick 5" in log and time.time() - t0 > 0.5
     client.delete("follow-logs", namespace=NS)
+
+
+def test_sdk_reference_docs_are_current():
+    """sdk/python/docs/*.md (one page per model + PyTorchJobClient, like the reference SDK's
+    docs/) are generated from the field tables and signatures; the committed pages must match."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_sdk_docs", os.path.join(root, "tools", "gen_sdk_docs.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    pages = mod.pages()
+    assert len(pages) == 9
+    for fn, text in pages.items():
+        with open(os.path.join(root, "sdk", "python", "docs", fn)) as f:
+            assert f.read() == text, f"{fn} is stale: run tools/gen_sdk_docs.py"
