@@ -99,6 +99,23 @@ __device__ __forceinline__ bf16x8 tr_frag(const u32x4* tile, int rbase, int cbas
   return __builtin_bit_cast(bf16x8, v);
 }
 
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// combine a lane's value with lane ^ 32's (v_permlane32_swap: one VALU op, no LDS round trip);
+// both halves get the same result (lower half's value first)
+__device__ __forceinline__ float half_max(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3(__uint_as_float(s[0]), __uint_as_float(s[1]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -113,21 +130,21 @@ __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint
 
 // Stage a [ROWS][128] bf16 tile (rows ROWS apart in global by `stride` elements) into the
 // XOR image: each thread moves ROWS*16/NT 16-byte chunks.
-template <int ROWS>
+template <int ROWS, int NTH = NT>
 struct Stage {
-  static constexpr int N = ROWS * CH / NT;
+  static constexpr int N = ROWS * CH / NTH;
   u32x4 r[N];
   __device__ __forceinline__ void load(const bf16_t* base, size_t stride, int tid) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int e = tid + NT * i, row = e / CH, ch = e % CH;
+      const int e = tid + NTH * i, row = e / CH, ch = e % CH;
       r[i] = *reinterpret_cast<const u32x4*>(base + (size_t)row * stride + ch * 8);
     }
   }
   __device__ __forceinline__ void store(u32x4* tile, int tid) const {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int e = tid + NT * i, row = e / CH, ch = e % CH;
+      const int e = tid + NTH * i, row = e / CH, ch = e % CH;
       tile[xo(row, ch)] = r[i];
     }
   }
@@ -287,6 +304,162 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restric
     __syncthreads();
   }
   l += __shfl_xor(l, 32);
+  const float inv = 1.f / l;
+  store_rows_T(oacc, inv, smem + w * 32 * CH, lane, o + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+  if (h == 0) lse2[((size_t)b * Hq + hq) * S + qme] = m2 + log2f(l);
+}
+
+// ------------------------------------------------------------- forward, 8-wave workgroup
+// 8 waves x 32 queries (BM8 = 256 rows) share each staged K/V tile: half the LDS writes and
+// the L2 -> CU tile traffic per FLOP of the 4-wave kernel above at the same occupancy (one
+// workgroup per CU = two waves per SIMD).  Differences besides the shape:
+//   * workgroup -> (q block, b, q head in group, kv head) with the kv head FASTEST: block i
+//     runs on XCD i % 8, so at Hkv = 8 every workgroup that reads one (b, kv head)'s K/V sits
+//     on one XCD and its L2 holds them (K/V leave HBM once, not once per XCD);
+//   * deferred rescale (defer-max): the running max only moves, and O / l are only rescaled,
+//     when some row of the wave sees a tile max more than DEFER (log2 units) above it, so
+//     p = exp2(s*c - m) stays <= 2^DEFER; most tiles after the first few skip the O-wide
+//     multiply pass;
+//   * wave-uniform skip of tiles wholly above a wave's diagonal (the last ones of its block);
+//   * the younger half (waves 4-7) runs at priority 1 from the start (static form of
+//     s_setprio: it otherwise loses VALU arbitration to the older half on every segment).
+constexpr int NT8 = 512;
+constexpr int BM8 = 256;
+constexpr float DEFER = 8.f;
+
+__global__ __launch_bounds__(NT8, 1) void attn_fwd8_kernel(const bf16_t* __restrict__ q,
+                                                          const bf16_t* __restrict__ k,
+                                                          const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                          float* __restrict__ lse2, int B, int S, int Hq, int Hkv,
+                                                          float c, int causal) {
+  __shared__ u32x4 smem[4 * BN * CH];  // K0 V0 K1 V1 (64 KB); the O staging image after the loop
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  if (__builtin_amdgcn_readfirstlane(tid) >= NT8 / 2) __builtin_amdgcn_s_setprio(1);
+  const int G = Hq / Hkv, nqb = S / BM8;
+  int bi = (int)blockIdx.x;
+  const int hk = bi % Hkv;
+  bi /= Hkv;
+  const int hq = hk * G + bi % G;
+  bi /= G;
+  const int b = bi % B, qi = bi / B;
+  const int qblk = causal ? nqb - 1 - qi : qi;
+  const int q0w = qblk * BM8 + w * 32, qme = q0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS];
+  {
+    const bf16_t* qrow = q + ((size_t)b * S + qme) * qstride + (size_t)hq * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) qf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(qrow + 16 * s));
+  }
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const int ntiles = causal ? (qblk * BM8 + BM8) / BN : S / BN;
+  // tiles this wave needs: under the mask the ones starting at or before its last row
+  const int wtiles = causal ? (q0w + 31) / BN + 1 : ntiles;
+
+  Stage<BN, NT8> ks, vs;
+  ks.load(kb, kvstride, tid);
+  vs.load(vb, kvstride, tid);
+  ks.store(smem, tid);
+  vs.store(smem + BN * CH, tid);
+  __syncthreads();
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  float m2 = -INFINITY, l = 0.f;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const u32x4* Ks = smem + cur * 2 * BN * CH;
+    const u32x4* Vs = Ks + BN * CH;
+    const int kv0 = t * BN;
+    const bool more = t + 1 < ntiles;
+    if (more) {  // next tile's global loads fly under this tile's MFMAs
+      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+    }
+    if (t < wtiles) {  // wave-uniform
+      f32x16 sacc[2];
+      {
+        bf16x8 a0[NDS], a1[NDS];
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) {
+          a0[s] = row_frag(Ks, r, 2 * s + h);
+          a1[s] = row_frag(Ks, 32 + r, 2 * s + h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sacc[0] = zero16();
+        sacc[1] = zero16();
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) {
+          sacc[0] = mfma(a0[s], qf[s], sacc[0]);
+          sacc[1] = mfma(a1[s], qf[s], sacc[1]);
+        }
+      }
+      if (causal && kv0 + BN - 1 > q0w) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          // key kv0 + 32kt + acc_row(i, h) > qme  <=>  (i&3) + 8(i>>2) > lim
+          const int lim = qme - kv0 - kt * 32 - 4 * h;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if ((i & 3) + 8 * (i >> 2) > lim) sacc[kt][i] = -INFINITY;
+        }
+      }
+      // max3 chain in asm: plain fmaxf on MFMA results gets a canonicalising v_max per operand
+      float mx = max3(sacc[0][0], sacc[0][1], sacc[0][2]);
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) mx = max3(mx, sacc[0][i], sacc[0][i + 1]);
+      mx = max3(mx, sacc[0][15], sacc[1][0]);
+#pragma unroll
+      for (int i = 1; i < 15; i += 2) mx = max3(mx, sacc[1][i], sacc[1][i + 1]);
+      mx = max3(mx, sacc[1][15], sacc[1][15]);
+      mx = half_max(mx);
+      const float mt = mx * c;
+      if (__builtin_amdgcn_ballot_w64(mt > m2 + DEFER) != 0) {  // wave-uniform: rescale
+        const float mnew = fmaxf(m2, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m2 - mnew);
+        m2 = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], c, -m2));
+          sacc[kt][i] = p;
+          rs += p;
+        }
+      l += rs;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 pb[2], vv[2][NDT];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) vv[s2][dt] = tr_frag(Vs, kt * 32 + 16 * s2, dt * 32, lane);
+        pb[0] = acc_frag(sacc[kt], 0);
+        pb[1] = acc_frag(sacc[kt], 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma(vv[s2][dt], pb[s2], oacc[dt]);
+      }
+    }
+    if (more) {
+      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+      ks.store(nk, tid);
+      vs.store(nk + BN * CH, tid);
+    }
+    __syncthreads();
+  }
+  l = half_sum(l);
   const float inv = 1.f / l;
   store_rows_T(oacc, inv, smem + w * 32 * CH, lane, o + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
   if (h == 0) lse2[((size_t)b * Hq + hq) * S + qme] = m2 + log2f(l);
@@ -536,6 +709,17 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// forward variant: 8 = the 8-wave kernel where S % 256 == 0 (default), 4 = the 4-wave kernel;
+// PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
+int g_fwd_variant = -1;
+int fwd_variant() {
+  if (g_fwd_variant < 0) {
+    const char* e = getenv("PTO_ATTN_FWD");
+    g_fwd_variant = e != nullptr ? atoi(e) : 8;
+  }
+  return g_fwd_variant;
+}
+
 int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
   if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Dh != D) return -1;
   if (S % BM || S % BK || Hq % Hkv) return -1;
@@ -547,6 +731,12 @@ int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
 
 extern "C" {
 
+int pto_attn_set_variant(int fwd) {
+  const int old = fwd_variant();
+  if (fwd == 4 || fwd == 8) g_fwd_variant = fwd;
+  return old;
+}
+
 // q [B,S,Hq,128], k/v [B,S,Hkv,128] bf16 contiguous; o [B,S,Hq,128] bf16; lse2 [B,Hq,S] f32
 // (log2 units of the scaled scores).  S a multiple of 128, Hq a multiple of Hkv.
 int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse2, int B, int S, int Hq, int Hkv,
@@ -554,8 +744,14 @@ int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   if (check_shapes(B, S, Hq, Hkv, Dh)) return -1;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(lse2)) return -2;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c, causal);
+  if (fwd_variant() == 8 && S % BM8 == 0)
+    hipLaunchKernelGGL(attn_fwd8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
+                       causal);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
+                       causal);
   return (int)hipGetLastError();
 }
 

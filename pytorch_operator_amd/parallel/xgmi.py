@@ -24,6 +24,7 @@ falls back to RCCL (``FlatGradAllReduce``).
 from __future__ import annotations
 
 import ctypes
+import os
 import socket
 from typing import Optional
 
@@ -291,9 +292,10 @@ def try_xgmi(n: int, device, required: bool = False, log=print,
              timeout_s: float = 5.0) -> Optional[XgmiGradSync]:
     """The self-tested xGMI gradient path, or None (RCCL then carries the gradients).
 
-    Only used under RCCL (one GPU per rank) unless ``required`` -- which also lets the
-    1-GPU rehearsal run it under gloo with ranks sharing a device."""
-    if not required and dist.get_backend() != "nccl":
+    Only used under RCCL (one GPU per rank) unless ``required`` or ``PTO_XGMI_ANY_BACKEND=1``
+    -- which let the 1-GPU rehearsal run it under gloo with ranks sharing a device (the
+    latter keeps the start-up race against the gloo bucket path, ``--allreduce auto``)."""
+    if not required and dist.get_backend() != "nccl" and os.environ.get("PTO_XGMI_ANY_BACKEND") != "1":
         return None
     try:
         xar = XgmiAllReduce(n, device=device, timeout_s=timeout_s)

@@ -71,6 +71,67 @@ def test_flash_backward_matches_fp32_reference(shape, causal):
         assert torch.isfinite(a.float()).all(), name
 
 
+@pytest.fixture
+def fwd_variant():
+    """Select the forward kernel (8-wave default / 4-wave) for one test, then restore."""
+    from pytorch_operator_amd.ops import _native
+    lib = _native.load()
+    old = lib.pto_attn_set_variant(0)  # 0: query only
+    yield lambda v: lib.pto_attn_set_variant(v)
+    lib.pto_attn_set_variant(old)
+
+
+def _fwd(q, k, v, causal):
+    from pytorch_operator_amd.ops import _native
+    B, S, Hq, _ = q.shape
+    o = torch.empty_like(q)
+    lse2 = torch.empty(B, Hq, S, device="cuda")
+    _native.check(_native.load().pto_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                              lse2.data_ptr(), B, S, Hq, k.shape[2], 128, 1 / math.sqrt(128),
+                                              int(causal), torch.cuda.current_stream().cuda_stream), "attn_fwd")
+    torch.cuda.synchronize()
+    return o, lse2
+
+
+@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal):
+    """Both forward kernels on scores whose row maximum keeps growing along the keys (large,
+    ramped logits): the 8-wave kernel's deferred rescale must fire mid-row, more than once,
+    and still give the fp32 reference's output and log-sum-exp."""
+    from pytorch_operator_amd.ops.attention import attention_reference
+    fwd_variant(variant)
+    B, S, Hq, Hkv = 1, 1024, 4, 2
+    g = torch.Generator(device="cuda").manual_seed(3)
+    q = torch.randn(B, S, Hq, 128, device="cuda", generator=g)
+    k = torch.randn(B, S, Hkv, 128, device="cuda", generator=g)
+    v = torch.randn(B, S, Hkv, 128, device="cuda", generator=g)
+    # a shared direction whose weight grows with the key index: for every query the best key
+    # moves right tile after tile, by more than the deferral threshold per 64-key tile
+    d = torch.randn(128, device="cuda", generator=g)
+    d = d / d.norm()
+    q = q + 6.0 * d
+    k = k + (torch.arange(S, device="cuda", dtype=torch.float32) / 64.0 * 3.0).view(1, S, 1, 1) * d
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    ref32, lse = attention_reference(q.float(), k.float(), v.float(), causal, return_lse=True)
+    o, lse2 = _fwd(q, k, v, causal)
+    assert torch.isfinite(o.float()).all()
+    assert _rel(o, ref32) < 8e-3, _rel(o, ref32)
+    assert torch.allclose(lse2, lse * math.log2(math.e), atol=5e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 768, 4, 4)])
+def test_flash_forward_variants_agree(fwd_variant, shape):
+    """8-wave vs 4-wave forward on the same inputs (bf16 outputs within rounding)."""
+    q, k, v = _inputs(*shape, seed=5)
+    outs = {}
+    for var in (4, 8):
+        fwd_variant(var)
+        outs[var] = _fwd(q, k, v, True)
+    assert _rel(outs[8][0], outs[4][0]) < 4e-3
+    assert torch.allclose(outs[8][1], outs[4][1], atol=1e-3, rtol=1e-5)
+
+
 def test_flash_llama_block_matches_sdpa_path():
     """A D = 128 Llama config through the model's attention dispatch: HIP flash vs library SDPA."""
     from pytorch_operator_amd.models.llama import CONFIGS, Llama

@@ -35,7 +35,7 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
            "--gpus", "2", "--backend", "gloo", "--allreduce", allreduce, "--steps", "20", "--warmup", "5",
            "--job-gpus", "0,0", "--job-timeout", "200", "--json-out", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=ROOT,
-                       env=dict(os.environ, PYTHONPATH=str(ROOT)))
+                       env=dict(os.environ, PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1"))
     assert r.returncode == 0 and out.exists(), r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads(out.read_text())
     assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
