@@ -576,6 +576,132 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
   store_rows_T(dacc, scale, smem + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
 }
 
+// ------------------------------------------------- backward pass 1, 8-wave workgroup
+// The dQ pass in the forward's 8-wave shape (256 query rows share each K/V tile, two waves
+// per SIMD, kv head fastest in the block order, causal per-wave tile skip, younger half at
+// priority 1).  Registers: the S and dP operand reads are issued per 32-key half as two
+// 8-fragment groups so Q, dO, dQ^T and both chains fit the 256 of two waves per SIMD.
+__global__ __launch_bounds__(NT8, 1) void attn_bwd_dq8_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
+    float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
+  __shared__ u32x4 smem[4 * BN * CH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  if (__builtin_amdgcn_readfirstlane(tid) >= NT8 / 2) __builtin_amdgcn_s_setprio(1);
+  const int G = Hq / Hkv, nqb = S / BM8;
+  int bi = (int)blockIdx.x;
+  const int hk = bi % Hkv;
+  bi /= Hkv;
+  const int hq = hk * G + bi % G;
+  bi /= G;
+  const int b = bi % B, qi = bi / B;
+  const int qblk = causal ? nqb - 1 - qi : qi;
+  const int q0w = qblk * BM8 + w * 32, qme = q0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS], df[NDS];
+  float dl;
+  {
+    const size_t off = ((size_t)b * S + qme) * qstride + (size_t)hq * D + 8 * h;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      const u32x4 qq = *reinterpret_cast<const u32x4*>(q + off + 16 * s);
+      const u32x4 dd = *reinterpret_cast<const u32x4*>(dout + off + 16 * s);
+      const u32x4 oo = *reinterpret_cast<const u32x4*>(o + off + 16 * s);
+      qf[s] = __builtin_bit_cast(bf16x8, qq);
+      df[s] = __builtin_bit_cast(bf16x8, dd);
+      const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w}, ow[4] = {oo.x, oo.y, oo.z, oo.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part = fmaf(bf2f(dw[e] & 0xffffu), bf2f(ow[e] & 0xffffu), part);
+        part = fmaf(bf2f(dw[e] >> 16), bf2f(ow[e] >> 16), part);
+      }
+    }
+    dl = half_sum(part);
+  }
+  const size_t srow = ((size_t)b * Hq + hq) * S + qme;
+  const float lq = lse2[srow];
+  if (h == 0) delta[srow] = dl;
+
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const int ntiles = causal ? (qblk * BM8 + BM8) / BN : S / BN;
+  const int wtiles = causal ? (q0w + 31) / BN + 1 : ntiles;
+  Stage<BN, NT8> ks, vs;
+  ks.load(kb, kvstride, tid);
+  vs.load(vb, kvstride, tid);
+  ks.store(smem, tid);
+  vs.store(smem + BN * CH, tid);
+  __syncthreads();
+
+  f32x16 dacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) dacc[dt] = zero16();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const u32x4* Ks = smem + cur * 2 * BN * CH;
+    const u32x4* Vs = Ks + BN * CH;
+    const int kv0 = t * BN;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+    }
+    if (t < wtiles) {  // wave-uniform
+      const bool diag = causal && kv0 + BN - 1 > q0w;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x16 sa = zero16(), pa = zero16();
+        {
+          bf16x8 ka[NDS];
+#pragma unroll
+          for (int s = 0; s < NDS; ++s) ka[s] = row_frag(Ks, kt * 32 + r, 2 * s + h);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 0; s < NDS; ++s) sa = mfma(ka[s], qf[s], sa);
+        }
+        {
+          bf16x8 va[NDS];
+#pragma unroll
+          for (int s = 0; s < NDS; ++s) va[s] = row_frag(Vs, kt * 32 + r, 2 * s + h);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int s = 0; s < NDS; ++s) pa = mfma(va[s], df[s], pa);
+        }
+        const int lim = qme - kv0 - kt * 32 - 4 * h;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lq));
+          if (diag && (i & 3) + 8 * (i >> 2) > lim) p = 0.f;
+          sa[i] = p * (pa[i] - dl);
+        }
+        bf16x8 db[2], kk[2][NDT];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) kk[s2][dt] = tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane);
+        db[0] = acc_frag(sa, 0);
+        db[1] = acc_frag(sa, 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(kk[s2][dt], db[s2], dacc[dt]);
+      }
+    }
+    if (more) {
+      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+      ks.store(nk, tid);
+      vs.store(nk + BN * CH, tid);
+    }
+    __syncthreads();
+  }
+  store_rows_T(dacc, scale, smem + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+}
+
 // -------------------------------------------------------------- backward pass 2: dK, dV
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
@@ -709,7 +835,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// forward variant: 8 = the 8-wave kernel where S % 256 == 0 (default), 4 = the 4-wave kernel;
+// forward + dQ-pass variant: 8 = the 8-wave kernels where S % 256 == 0 (default), 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
 int fwd_variant() {
@@ -764,9 +890,14 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   for (const void* p : ps)
     if (!aligned16(p)) return -2;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout,
-                     lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  if (fwd_variant() == 8 && S % BM8 == 0)
+    hipLaunchKernelGGL(attn_bwd_dq8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
+                       (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
+                       (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
                      (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);

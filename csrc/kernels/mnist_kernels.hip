@@ -163,6 +163,26 @@ __device__ __forceinline__ int from_upper_half(int v) {
   return (int)__builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false)[1];
 }
 
+// PTO_NT (A/B): nontemporal stores for the bytes one launch hands to the next on other XCDs
+// (conv-grad slab, dW_fc1, the tail's parameters/momentum), so they stream out of the
+// writing XCD's L2 during the kernel instead of in the end-of-kernel write-back
+#ifndef PTO_NT
+#define PTO_NT 0
+#endif
+__device__ __forceinline__ void st_h(float* p, float v) {
+  if (PTO_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void st_h4(float4* p, float4 v) {
+  if (PTO_NT) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 struct SgdHyper {
   float lr, momentum, dampening, wd, grad_scale;
   int nesterov, first_step;
@@ -878,7 +898,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
       const int nn = nt * 16 + g * 4 + r;
       if (nn < 500) {
         const size_t e = (size_t)nn * 800 + kt * 16 + i;
-        if (a.gw1 != nullptr) a.gw1[e] = c[r];
+        if (a.gw1 != nullptr) st_h(a.gw1 + e, c[r]);
         if (a.sgd) {
           sgd_elem(pw[r], mw[r], c[r], a.hy);
           a.w1_next[e] = pw[r];
@@ -2132,16 +2152,16 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       float* rp = rowq + (ct * 16 + i) * 500;
       const int j0 = jbase + jt * 16 + 4 * g;
       if (j0 >= 0 && j0 + 3 < 125) {
-        *reinterpret_cast<float4*>(rp + j0) = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
+        st_h4(reinterpret_cast<float4*>(rp + j0), make_float4(gacc[0], gacc[1], gacc[2], gacc[3]));
       } else {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
+          if (j0 + rr >= 0 && j0 + rr < 125) st_h(rp + j0 + rr, gacc[rr]);
       }
     } else if (wv == 12) {
       const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
       const int j = jbase + (lane & 31);
-      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
+      if (j >= 0 && j < 125) st_h(rowq + (48 + (lane >> 5)) * 500 + j, v);
     }
   }
   if (!own) return;  // block-uniform: padding blocks of the last chunk are done
@@ -2245,10 +2265,10 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     float w1sum = 0.f;
 #pragma unroll
     for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
-    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
-    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
+    if (tid < 125) st_h(rowb + o_gw1 + cig * 125 + tid, w1sum);  // tid = c * 25 + kh * 5 + kw
+    else st_h(rowb + o_gb1 + cig * 5 + (tid - 125), w1sum);
   }
-  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
+  if (cig == 0 && tid < 50) st_h(rowb + o_gb2 + tid, b2sum);
   stamp(dbg, 5);
 }
 
@@ -2368,8 +2388,8 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
       sgd_elem(pp.y, bb.y, gg.y, hy);
       sgd_elem(pp.z, bb.z, gg.z, hy);
       sgd_elem(pp.w, bb.w, gg.w, hy);
-      reinterpret_cast<float4*>(p2)[v] = pp;
-      reinterpret_cast<float4*>(buf2)[v] = bb;
+      st_h4(reinterpret_cast<float4*>(p2) + v, pp);
+      st_h4(reinterpret_cast<float4*>(buf2) + v, bb);
     }
     return;
   }
@@ -2395,8 +2415,8 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     sgd_elem(pp.y, bb.y, r.y, hy);
     sgd_elem(pp.z, bb.z, r.z, hy);
     sgd_elem(pp.w, bb.w, r.w, hy);
-    reinterpret_cast<float4*>(p)[col] = pp;
-    reinterpret_cast<float4*>(buf)[col] = bb;
+    st_h4(reinterpret_cast<float4*>(p) + col, pp);
+    st_h4(reinterpret_cast<float4*>(buf) + col, bb);
   }
   if (step_counter != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(step_counter, 1);
   stamp(dbg, 1);

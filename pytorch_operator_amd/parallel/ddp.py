@@ -125,7 +125,10 @@ class BucketedDDP(nn.Module):
     def _on_grad(self, p: torch.Tensor) -> None:
         bi, off = self._slot[id(p)]
         flat = self._flat[bi]
-        flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        if p.grad is None:  # hooks also run when a backward returned no gradient for the leaf
+            flat[off:off + p.numel()].zero_()
+        else:
+            flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._works[bi] = dist.all_reduce(flat, group=self.group, async_op=True)

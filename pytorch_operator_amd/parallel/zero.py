@@ -166,6 +166,11 @@ class ZeroAdamW:
 
     # ------------------------------------------------------------------ backward side
     def _on_grad(self, p: torch.Tensor) -> None:
+        if p.grad is None:
+            # autograd runs post-accumulate hooks even when the backward returned no gradient
+            # for the leaf -- the case of a weight whose gradient sink was written in place
+            # (it arrived through _arrive already) or of no gradient at all (step() fills it)
+            return
         b = self._of[id(p)]
         if b.pending < 0:
             raise RuntimeError("ZeroAdamW: a second backward before step() -- gradient accumulation "

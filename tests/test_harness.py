@@ -360,6 +360,53 @@ def test_zero_adamw_unused_parameter_matches_master_adamw():
     assert not torch.equal(m2.a.weight, m1.a.weight * 0)  # the used parameters did move
 
 
+def test_zero_adamw_hook_without_gradient():
+    """Autograd runs post-accumulate hooks even when a backward returns None for a leaf -- what
+    linear_tn does for a weight whose gradient sink it wrote in place.  ZeroAdamW must treat
+    that as "no gradient through the hook" (the GPU failure: a sink arrival followed by the
+    hook raised "a second backward before step()").  Here the frozen-gradient weight behaves
+    like an unused parameter: untouched, as MasterAdamW leaves it."""
+    import copy
+    import torch.nn as nn
+    from pytorch_operator_amd.ops.optim import MasterAdamW
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+
+    class NoWGrad(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.save_for_backward(w)
+            return x @ w.t()
+
+        @staticmethod
+        def backward(ctx, dy):
+            (w,) = ctx.saved_tensors
+            return dy @ w, None
+
+    class M(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(8, 8)
+            self.frozen = nn.Parameter(torch.randn(8, 8))
+            self.b = nn.Linear(8, 4)
+
+        def forward(self, x):
+            return self.b(NoWGrad.apply(torch.relu(self.a(x)), self.frozen))
+
+    torch.manual_seed(2)
+    m1 = M()
+    m2 = copy.deepcopy(m1)
+    o1 = MasterAdamW(m1.parameters(), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+    o2 = ZeroAdamW(m2, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=1.0)
+    x = torch.randn(5, 8)
+    for _ in range(3):
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad(set_to_none=True)
+            m(x).square().mean().backward()
+            o.step()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(a, b, rtol=0, atol=1e-6), n
+
+
 def test_ddp_train_worker_resnet_tiny(tmp_path):
     (rc, out), = _launch("pytorch_operator_amd.harness.ddp_train",
                          ["--model", "resnet-tiny", "--batch-size", "2", "--steps", "2", "--warmup", "1"], 1, tmp_path)
