@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/final; mkdir -p $O
 ( while sleep 30; do echo "hb $(date +%T)"; done ) & HB=$!
 trap "kill $HB" EXIT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest ${PYTEST_SEL:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log

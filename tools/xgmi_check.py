@@ -81,12 +81,24 @@ def main(argv=None) -> int:
     res["self_test_report"] = xar.last_report[:4]
 
     ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
+    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each):
+    # a rank's exchange blocks spin on every CU until its peer reaches the same step, so the
+    # peer's conv backward must fit on a CU NEXT to them.  The 4-sample-chunk conv_bwd4 block
+    # (152 KB of LDS, 16 waves) does not fit beside two ranks' exchange blocks and the shared-GPU
+    # rehearsal then times out (the job topology never has this: one rank per GPU runs its own
+    # kernels in stream order); the per-sample conv_bwd block (105 KB) does.  The chunked slab
+    # path of the exchange is covered by the auto-geometry runs (128 workgroups per rank).
+    peers = [None] * world
+    dist.all_gather_object(peers, dev.index)
+    shared_256 = len(set(peers)) < world and xar.nblk >= 256
+    res["conv_chunk"] = 1 if shared_256 else 4
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
         tr = FusedMnistTrainer(batch_size=64, source=src, lr=0.01, momentum=0.5, device=dev, seed=1,
                                grad_sync=sync)
+        tr.conv_chunk = res["conv_chunk"]
         dist.broadcast(tr.flat_params, 0)
         return tr
 
