@@ -833,11 +833,159 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
   store_rows_T(dka, scale, smem + w * 32 * CH, lane, dk + off, kvstride);
 }
 
+// ----------------------------------------- backward pass 2, software-pipelined (dK, dV)
+// Same work split as attn_bwd_dkdv_kernel (one wave per SIMD: dK^T / dV^T of 32 keys, K and V
+// fragments in registers, 390 of the 512), with the free registers spent on a pipeline: the
+// Q / dO tiles cycle through a 3-deep LDS ring, so the row operands of tile t+1 are read into
+// registers while tile t's dV / dK MFMAs run, and tile t+1's S / dP chains start without an LDS
+// round trip (a single wave per SIMD has no sibling to hide it).  Stored tile t+2 and the
+// global loads of tile t+3 ride behind the same MFMAs.
+__global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_p_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
+  __shared__ u32x4 smem[3 * 2 * QT * CH];  // 3 x (Q, dO) tiles (48 KB); the dK/dV epilogue
+  __shared__ float4 stat[3][2][QT / 4];    // [buf][lse2 | delta][32 rows]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
+  const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
+  const int k0w = kblk * BK + w * 32, kme = k0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 kf[NDS], vf[NDS];
+  {
+    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
+      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(v + off + 16 * s));
+    }
+  }
+  const int qt0 = causal ? (kblk * BK) / QT : 0;
+  const int nqt = S / QT - qt0;
+  const int ntiles = G * nqt;
+
+  Stage<QT> qs, ds;
+  float4 st = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](int t) {
+    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
+    const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
+    const size_t srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
+    qs.load(q + off, qstride, tid);
+    ds.load(dout + off, qstride, tid);
+    if (tid < 16) st = reinterpret_cast<const float4*>((tid < 8 ? lse2 : delta) + srow)[tid & 7];
+  };
+  auto store = [&](int buf) {
+    qs.store(smem + buf * 2 * QT * CH, tid);
+    ds.store(smem + buf * 2 * QT * CH + QT * CH, tid);
+    if (tid < 16) stat[buf][tid >> 3][tid & 7] = st;
+  };
+  load(0);
+  store(0);
+  if (ntiles > 1) {
+    load(1);
+    store(1);
+  }
+  if (ntiles > 2) load(2);
+  __syncthreads();
+
+  bf16x8 qa[NDS], da[NDS];
+#pragma unroll
+  for (int s = 0; s < NDS; ++s) {
+    qa[s] = row_frag(smem, r, 2 * s + h);
+    da[s] = row_frag(smem + QT * CH, r, 2 * s + h);
+  }
+  f32x16 dka[NDT], dva[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    dka[dt] = zero16();
+    dva[dt] = zero16();
+  }
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const u32x4* Qs = smem + cur * 2 * QT * CH;
+    const u32x4* Ds = Qs + QT * CH;
+    const int nxt = cur == 2 ? 0 : cur + 1, nn2 = nxt == 2 ? 0 : nxt + 1;
+    const int q0 = (qt0 + t % nqt) * QT;
+    f32x16 sa = zero16(), pa = zero16();
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      sa = mfma(qa[s], kf[s], sa);
+      pa = mfma(da[s], vf[s], pa);
+    }
+    const bool diag = causal && k0w + 31 > q0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 L4 = stat[cur][0][2 * g + h];
+      const float4 D4 = stat[cur][1][2 * g + h];
+      const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e;
+        float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
+        if (diag && kme > q0 + 8 * g + 4 * h + e) p = 0.f;
+        sa[i] = p;
+        pa[i] = p * (pa[i] - Dv[e]);
+      }
+    }
+    bf16x8 pb[2], db[2], td[2][NDT], tq[2][NDT];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        td[s2][dt] = tr_frag(Ds, 16 * s2, dt * 32, lane);
+        tq[s2][dt] = tr_frag(Qs, 16 * s2, dt * 32, lane);
+      }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      pb[s2] = acc_frag(sa, s2);
+      db[s2] = acc_frag(pa, s2);
+    }
+    if (t + 1 < ntiles) {  // next tile's row operands: in flight under this tile's dV / dK MFMAs
+      const u32x4* Qn = smem + nxt * 2 * QT * CH;
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) {
+        qa[s] = row_frag(Qn, r, 2 * s + h);
+        da[s] = row_frag(Qn + QT * CH, r, 2 * s + h);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        dva[dt] = mfma(td[s2][dt], pb[s2], dva[dt]);
+        dka[dt] = mfma(tq[s2][dt], db[s2], dka[dt]);
+      }
+    if (t + 2 < ntiles) {
+      store(nn2);
+      if (t + 3 < ntiles) load(t + 3);
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+  store_rows_T(dva, 1.f, smem + w * 32 * CH, lane, dv + off, kvstride);
+  __syncthreads();
+  store_rows_T(dka, scale, smem + w * 32 * CH, lane, dk + off, kvstride);
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // forward + dQ-pass variant: 8 = the 8-wave kernels where S % 256 == 0 (default), 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
+// dK/dV pass: 2 = software-pipelined (default), 1 = the plain one; PTO_ATTN_DKDV or
+// pto_attn_set_dkdv_variant()
+int g_dkdv_variant = -1;
+int dkdv_variant() {
+  if (g_dkdv_variant < 0) {
+    const char* e = getenv("PTO_ATTN_DKDV");
+    g_dkdv_variant = e != nullptr ? atoi(e) : 2;
+  }
+  return g_dkdv_variant;
+}
 int fwd_variant() {
   if (g_fwd_variant < 0) {
     const char* e = getenv("PTO_ATTN_FWD");
@@ -856,6 +1004,12 @@ int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
 }  // namespace
 
 extern "C" {
+
+int pto_attn_set_dkdv_variant(int v) {
+  const int old = dkdv_variant();
+  if (v == 1 || v == 2) g_dkdv_variant = v;
+  return old;
+}
 
 int pto_attn_set_variant(int fwd) {
   const int old = fwd_variant();
@@ -898,7 +1052,8 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                        (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel : attn_bwd_dkdv_kernel,
+                     dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
                      (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
   return (int)hipGetLastError();

@@ -459,8 +459,6 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
     }
     if (!e2.not_found()) events_.record(job, {"Normal", "SuccessfulDeleteService", "Deleted service: " + d.name});
   }
-  M.inc("pytorch_operator_jobs_successful_total", r.metrics.successful);
-  M.inc("pytorch_operator_jobs_failed_total", r.metrics.failed);
   M.inc("pytorch_operator_jobs_restarted_total", r.metrics.restarted);
   if (!r.error.empty()) return r.error;
   if (r.delete_job) {
@@ -472,6 +470,11 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
     std::string e = write_status(job, r.status);
     if (!e.empty()) return e;
   }
+  // a job's Succeeded / Failed transition is counted once it is persisted: a status write that
+  // loses a resourceVersion race requeues the key, and the retry (which still sees the old
+  // status in the cache) would otherwise count the same transition again
+  M.inc("pytorch_operator_jobs_successful_total", r.metrics.successful);
+  M.inc("pytorch_operator_jobs_failed_total", r.metrics.failed);
   for (double d : r.requeue_after_s) queue_.add_after(key, d);
   if (r.requeue_rate_limited) queue_.add_rate_limited(key);
   return "";

@@ -132,6 +132,38 @@ def test_flash_forward_variants_agree(fwd_variant, shape):
     assert torch.allclose(outs[8][1], outs[4][1], atol=1e-3, rtol=1e-5)
 
 
+@pytest.mark.parametrize("dkdv", [1, 2])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_backward_dkdv_variants(dkdv, causal):
+    """Plain and software-pipelined dK/dV passes (3-deep Q/dO ring, 1-5 tiles per head cover
+    the ring's prologue/epilogue cases) against the fp32 reference gradients."""
+    from pytorch_operator_amd.ops import _native
+    from pytorch_operator_amd.ops.attention import attention_reference, flash_attention, sdpa_bshd
+    lib = _native.load()
+    old = lib.pto_attn_set_dkdv_variant(dkdv)
+    try:
+        for shape in ((1, 128, 2, 2), (2, 256, 8, 2), (1, 640, 4, 1)):
+            q, k, v = _inputs(*shape, seed=9)
+            g = torch.Generator(device="cuda").manual_seed(4)
+            do = torch.randn(q.shape, device="cuda", generator=g).to(torch.bfloat16)
+
+            def grads(fn, *xs):
+                xs = [x.detach().clone().requires_grad_(True) for x in xs]
+                out = fn(*xs)
+                out.backward(do.to(out.dtype))
+                return [x.grad for x in xs]
+
+            ref = grads(lambda a, b, c: attention_reference(a, b, c, causal).float(), q.float(), k.float(),
+                        v.float())
+            ours = grads(lambda a, b, c: flash_attention(a, b, c, causal), q, k, v)
+            lib_g = grads(lambda a, b, c: sdpa_bshd(a, b, c, causal), q, k, v)
+            for name, a, r, lb in zip(("dq", "dk", "dv"), ours, ref, lib_g):
+                e, el = _rel(a, r), _rel(lb, r)
+                assert e < max(2.0 * el, 6e-3), (shape, name, e, el)
+    finally:
+        lib.pto_attn_set_dkdv_variant(old)
+
+
 def test_flash_llama_block_matches_sdpa_path():
     """A D = 128 Llama config through the model's attention dispatch: HIP flash vs library SDPA."""
     from pytorch_operator_amd.models.llama import CONFIGS, Llama
