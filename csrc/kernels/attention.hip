@@ -150,6 +150,23 @@ struct Stage {
   }
 };
 
+// The same XOR image filled by LDS-DMA (global_load_lds_dwordx4: no staging registers).  A
+// wave-instruction writes 64 consecutive 16-byte slots (wave-uniform base + 16 x lane), so the
+// swizzle moves to the per-lane SOURCE address: slot j of row R holds chunk j ^ swz(R).  Wave w
+// issues pieces w, w + NW, ...  The LDS writes count on vmcnt: __syncthreads() retires them.
+template <int ROWS, int NTH>
+__device__ __forceinline__ void glds_tile(const bf16_t* base, size_t stride, u32x4* tile, int tid) {
+  constexpr int NP = ROWS * CH / 64, NW = NTH / 64;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+#pragma unroll
+  for (int p = w; p < NP; p += NW) {
+    const int e = 64 * p + lane, row = e / CH, j = e % CH;
+    const int ch = j ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    __builtin_amdgcn_global_load_lds(base + (size_t)row * stride + ch * 8,
+                                     (__attribute__((address_space(3))) void*)(tile + 64 * p), 16, 0, 0);
+  }
+}
+
 // Write a wave's 32 x 128 transposed accumulator (acc[dt] reg i = [d = dt*32 + acc_row(i,h)]
 // [col = lane & 31]) as rows [col][d] bf16 to global via the wave's LDS region (8 KB).
 __device__ __forceinline__ void store_rows_T(const f32x16 (&acc)[NDT], float scale, u32x4* stage, int lane,
@@ -576,6 +593,179 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_kernel(
   store_rows_T(dacc, scale, smem + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
 }
 
+// ------------------------------------------------ forward, 8-wave ping-pong workgroup
+// attn_fwd8_kernel's barrier per K/V tile re-aligns the two waves of every SIMD each tile, so
+// both run their QK^T MFMAs, then both their softmax (matrix pipe idle), then both P.V.  Here
+// the younger half (waves 4-7) runs its loop rotated by one phase -- softmax(t), P.V(t),
+// QK^T(t+1) -- against the older half's QK^T(t), softmax(t), P.V(t) between the same two
+// barriers, so one wave's softmax issues under the other's MFMAs.  The rotated half reads
+// K(t+1) while tile t is current: K/V tiles cycle through a 3-deep LDS ring (96 KB), stored two
+// tiles ahead.  Numerics are those of attn_fwd8_kernel (same per-row operation order).
+__global__ __launch_bounds__(NT8, 1) void attn_fwd8p_kernel(const bf16_t* __restrict__ q,
+                                                           const bf16_t* __restrict__ k,
+                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                           float* __restrict__ lse2, int B, int S, int Hq, int Hkv,
+                                                           float c, int causal) {
+  __shared__ u32x4 smem[6 * BN * CH];  // (K, V) x 3 (96 KB); the O staging image after the loop
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const bool rot = __builtin_amdgcn_readfirstlane(tid) >= NT8 / 2;  // wave-uniform
+  if (rot) __builtin_amdgcn_s_setprio(1);
+  const int G = Hq / Hkv, nqb = S / BM8;
+  int bi = (int)blockIdx.x;
+  const int hk = bi % Hkv;
+  bi /= Hkv;
+  const int hq = hk * G + bi % G;
+  bi /= G;
+  const int b = bi % B, qi = bi / B;
+  const int qblk = causal ? nqb - 1 - qi : qi;
+  const int q0w = qblk * BM8 + w * 32, qme = q0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS];
+  {
+    const bf16_t* qrow = q + ((size_t)b * S + qme) * qstride + (size_t)hq * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) qf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(qrow + 16 * s));
+  }
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const int ntiles = causal ? (qblk * BM8 + BM8) / BN : S / BN;
+  const int wtiles = causal ? (q0w + 31) / BN + 1 : ntiles;
+  // ring slot base, opaque to the optimiser: otherwise it hoists every (slot, operand address)
+  // combination out of the loop and spills them
+  auto kbuf = [&](int t) {
+    int off = (t % 3) * 2 * BN * CH;
+    asm volatile("" : "+s"(off));
+    return smem + off;
+  };
+
+  // K/V by LDS-DMA (no staging registers: both halves' loops sit at the register cap)
+  glds_tile<BN, NT8>(kb, kvstride, smem, tid);
+  glds_tile<BN, NT8>(vb, kvstride, smem + BN * CH, tid);
+  if (ntiles > 1) {
+    glds_tile<BN, NT8>(kb + (size_t)BN * kvstride, kvstride, smem + 2 * BN * CH, tid);
+    glds_tile<BN, NT8>(vb + (size_t)BN * kvstride, kvstride, smem + 3 * BN * CH, tid);
+  }
+  __syncthreads();
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  float m2 = -INFINITY, l = 0.f;
+  f32x16 sacc[2];
+
+  auto qk = [&](const u32x4* Ks, int r, int h) {
+    __builtin_amdgcn_sched_barrier(0);  // keep the operand reads out of the previous phase
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {  // one 32-key half at a time: 32 operand registers, not 64
+      bf16x8 a0[NDS];
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) a0[s] = row_frag(Ks, 32 * kt + r, 2 * s + h);
+      __builtin_amdgcn_sched_barrier(0);
+      sacc[kt] = zero16();
+#pragma unroll
+      for (int s = 0; s < NDS; ++s) sacc[kt] = mfma(a0[s], qf[s], sacc[kt]);
+    }
+  };
+  auto softmax_pv = [&](int t, const u32x4* Vs, int lane, int r, int h) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int kv0 = t * BN;
+    if (causal && kv0 + BN - 1 > q0w) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int lim = qme - kv0 - kt * 32 - 4 * h;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((i & 3) + 8 * (i >> 2) > lim) sacc[kt][i] = -INFINITY;
+      }
+    }
+    float mx = max3(sacc[0][0], sacc[0][1], sacc[0][2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) mx = max3(mx, sacc[0][i], sacc[0][i + 1]);
+    mx = max3(mx, sacc[0][15], sacc[1][0]);
+#pragma unroll
+    for (int i = 1; i < 15; i += 2) mx = max3(mx, sacc[1][i], sacc[1][i + 1]);
+    mx = max3(mx, sacc[1][15], sacc[1][15]);
+    mx = half_max(mx);
+    const float mt = mx * c;
+    if (__builtin_amdgcn_ballot_w64(mt > m2 + DEFER) != 0) {
+      const float mnew = fmaxf(m2, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m2 - mnew);
+      m2 = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], c, -m2));
+        sacc[kt][i] = p;
+        rs += p;
+      }
+    l += rs;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      bf16x8 pb[2], vv[2][NDT];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) vv[s2][dt] = tr_frag(Vs, kt * 32 + 16 * s2, dt * 32, lane);
+      pb[0] = acc_frag(sacc[kt], 0);
+      pb[1] = acc_frag(sacc[kt], 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma(vv[s2][dt], pb[s2], oacc[dt]);
+    }
+  };
+
+  auto stage_next = [&](int t) {  // tile t+2 into the slot tile t-1 left (nobody reads it this round)
+    if (t + 2 < ntiles) {
+      u32x4* nk = kbuf(t + 2);
+      glds_tile<BN, NT8>(kb + (size_t)(t + 2) * BN * kvstride, kvstride, nk, tid);
+      glds_tile<BN, NT8>(vb + (size_t)(t + 2) * BN * kvstride, kvstride, nk + BN * CH, tid);
+    }
+  };
+  // one loop per half (same trip count, one barrier per trip each): loop-invariant operand
+  // addresses of the two orders then live in separate loops instead of all at once
+  // (lane indices re-derived per half behind an optimisation barrier, for the same reason)
+  if (!rot) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int rr = ln & 31, hh = ln >> 5;
+#pragma nounroll
+    for (int t = 0; t < ntiles; ++t) {
+      stage_next(t);
+      if (t < wtiles) {  // wave-uniform
+        const u32x4* Ks = kbuf(t);
+        qk(Ks, rr, hh);
+        softmax_pv(t, Ks + BN * CH, ln, rr, hh);
+      }
+      __syncthreads();
+    }
+  } else {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int rr = ln & 31, hh = ln >> 5;
+    if (wtiles > 0) qk(kbuf(0), rr, hh);
+#pragma nounroll
+    for (int t = 0; t < ntiles; ++t) {
+      stage_next(t);
+      if (t < wtiles) softmax_pv(t, kbuf(t) + BN * CH, ln, rr, hh);
+      if (t + 1 < wtiles) qk(kbuf(t + 1), rr, hh);
+      __syncthreads();
+    }
+  }
+  l = half_sum(l);
+  const float inv = 1.f / l;
+  store_rows_T(oacc, inv, smem + w * 32 * CH, lane, o + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+  if (h == 0) lse2[((size_t)b * Hq + hq) * S + qme] = m2 + log2f(l);
+}
+
 // ------------------------------------------------- backward pass 1, 8-wave workgroup
 // The dQ pass in the forward's 8-wave shape (256 query rows share each K/V tile, two waves
 // per SIMD, kv head fastest in the block order, causal per-wave tile skip, younger half at
@@ -629,11 +819,9 @@ __global__ __launch_bounds__(NT8, 1) void attn_bwd_dq8_kernel(
   const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
   const int ntiles = causal ? (qblk * BM8 + BM8) / BN : S / BN;
   const int wtiles = causal ? (q0w + 31) / BN + 1 : ntiles;
-  Stage<BN, NT8> ks, vs;
-  ks.load(kb, kvstride, tid);
-  vs.load(vb, kvstride, tid);
-  ks.store(smem, tid);
-  vs.store(smem + BN * CH, tid);
+  // K/V tiles by LDS-DMA: no staging registers (the register-staged form spilled in the loop)
+  glds_tile<BN, NT8>(kb, kvstride, smem, tid);
+  glds_tile<BN, NT8>(vb, kvstride, smem + BN * CH, tid);
   __syncthreads();
 
   f32x16 dacc[NDT];
@@ -642,23 +830,33 @@ __global__ __launch_bounds__(NT8, 1) void attn_bwd_dq8_kernel(
 
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
-    const u32x4* Ks = smem + cur * 2 * BN * CH;
+    int boff = cur * 2 * BN * CH;
+    asm volatile("" : "+s"(boff));  // opaque: one set of operand addresses, not one per buffer
+    const u32x4* Ks = smem + boff;
     const u32x4* Vs = Ks + BN * CH;
     const int kv0 = t * BN;
     const bool more = t + 1 < ntiles;
-    if (more) {
-      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
-      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+    if (more) {  // into the buffer tile t-1 left; lands under this tile's MFMAs
+      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+      glds_tile<BN, NT8>(kb + (size_t)(t + 1) * BN * kvstride, kvstride, nk, tid);
+      glds_tile<BN, NT8>(vb + (size_t)(t + 1) * BN * kvstride, kvstride, nk + BN * CH, tid);
     }
     if (t < wtiles) {  // wave-uniform
       const bool diag = causal && kv0 + BN - 1 > q0w;
+      // this lane's row-read chunk XOR (xo: chunk 2s+h of row r sits at (2s) ^ cx), re-derived
+      // per tile behind an optimisation barrier: hoisted, the eight per-k-step addresses were
+      // spilled and their reloads' vmcnt(0) waited for the K/V staging loads every tile
+      int cx = h ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      asm volatile("" : "+v"(cx));
+      const u32x4* Kr = Ks + r * CH;
+      const u32x4* Vr = Vs + r * CH;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         f32x16 sa = zero16(), pa = zero16();
         {
           bf16x8 ka[NDS];
 #pragma unroll
-          for (int s = 0; s < NDS; ++s) ka[s] = row_frag(Ks, kt * 32 + r, 2 * s + h);
+          for (int s = 0; s < NDS; ++s) ka[s] = __builtin_bit_cast(bf16x8, Kr[kt * 32 * CH + ((2 * s) ^ cx)]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int s = 0; s < NDS; ++s) sa = mfma(ka[s], qf[s], sa);
@@ -666,7 +864,7 @@ __global__ __launch_bounds__(NT8, 1) void attn_bwd_dq8_kernel(
         {
           bf16x8 va[NDS];
 #pragma unroll
-          for (int s = 0; s < NDS; ++s) va[s] = row_frag(Vs, kt * 32 + r, 2 * s + h);
+          for (int s = 0; s < NDS; ++s) va[s] = __builtin_bit_cast(bf16x8, Vr[kt * 32 * CH + ((2 * s) ^ cx)]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int s = 0; s < NDS; ++s) pa = mfma(va[s], df[s], pa);
@@ -678,24 +876,19 @@ __global__ __launch_bounds__(NT8, 1) void attn_bwd_dq8_kernel(
           if (diag && (i & 3) + 8 * (i >> 2) > lim) p = 0.f;
           sa[i] = p * (pa[i] - dl);
         }
-        bf16x8 db[2], kk[2][NDT];
+        // dQ^T += K^T dS^T, one 16-key k-step at a time (16 operand registers, not 32: the
+        // kernel is at the 256 of two waves per SIMD)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 kk[NDT];
 #pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) kk[s2][dt] = tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane);
-        db[0] = acc_frag(sa, 0);
-        db[1] = acc_frag(sa, 1);
-        __builtin_amdgcn_sched_barrier(0);
+          for (int dt = 0; dt < NDT; ++dt) kk[dt] = tr_frag(Ks, kt * 32 + 16 * s2, dt * 32, lane);
+          const bf16x8 db = acc_frag(sa, s2);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(kk[s2][dt], db[s2], dacc[dt]);
+          for (int dt = 0; dt < NDT; ++dt) dacc[dt] = mfma(kk[dt], db, dacc[dt]);
+        }
       }
-    }
-    if (more) {
-      u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
-      ks.store(nk, tid);
-      vs.store(nk + BN * CH, tid);
     }
     __syncthreads();
   }
@@ -971,18 +1164,163 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_p_kernel(
   store_rows_T(dka, scale, smem + w * 32 * CH, lane, dk + off, kvstride);
 }
 
+// ------------------------------------------- backward pass 2, 8-wave workgroup (dK, dV)
+// Two waves per SIMD (the 4-wave pass runs one, 390 registers): 8 waves x 32 keys = 256 keys
+// per workgroup share each staged Q / dO tile.  To fit 256 registers a wave keeps only K's
+// fragments (the S = Q.K^T operand) in registers; V's (the dP = dO.V^T operand) are re-read
+// per tile from an LDS-resident image of the workgroup's 256 V rows (64 KB, loaded once), and
+// Q / dO / lse2 / delta arrive by LDS-DMA (no staging registers).  Waves skip the query tiles
+// wholly above their keys.  Block order: key block slowest (heaviest first under the mask),
+// kv head fastest (the blocks reading one (b, kv head)'s Q / dO rows share an XCD at Hkv = 8).
+constexpr int BK8 = 256;
+
+__global__ __launch_bounds__(NT8, 1) void attn_bwd_dkdv8_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
+  __shared__ u32x4 vall[BK8 * CH];           // V rows of the workgroup (64 KB); dK/dV epilogue
+  __shared__ u32x4 qd[2][2 * QT * CH];       // [buf][Q | dO] (32 KB)
+  __shared__ __align__(16) float stat[2][2 * QT];  // [buf][lse2 | delta]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  if (__builtin_amdgcn_readfirstlane(tid) >= NT8 / 2) __builtin_amdgcn_s_setprio(1);
+  int bi = (int)blockIdx.x;
+  const int hk = bi % Hkv;
+  bi /= Hkv;
+  const int b = bi % B, kblk = bi / B, G = Hq / Hkv;
+  const int k0w = kblk * BK8 + w * 32, kme = k0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 kf[NDS];
+  {
+    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
+  }
+  const int qt0 = causal ? (kblk * BK8) / QT : 0;
+  const int nqt = S / QT - qt0;
+  const int ntiles = G * nqt;
+  // this wave's first live query tile of every head: qt0 + w (readfirstlane: provably uniform,
+  // so the branches around the LDS-DMA issue stay scalar)
+  const int wskip = causal ? __builtin_amdgcn_readfirstlane(w) : 0;
+
+  auto fetch = [&](int t, int buf) {  // Q, dO rows + lse2 / delta of tile t by LDS-DMA
+    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
+    const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
+    glds_tile<QT, NT8>(q + off, qstride, qd[buf], tid);
+    glds_tile<QT, NT8>(dout + off, qstride, qd[buf] + QT * CH, tid);
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+      const size_t srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
+      const float* src = (lane < 32 ? lse2 : delta) + srow + (lane & 31);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)stat[buf], 4, 0, 0);
+    }
+  };
+  glds_tile<BK8, NT8>(v + (size_t)b * S * kvstride + (size_t)kblk * BK8 * kvstride + (size_t)hk * D, kvstride,
+                      vall, tid);
+  fetch(0, 0);
+  __syncthreads();
+
+  f32x16 dka[NDT], dva[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    dka[dt] = zero16();
+    dva[dt] = zero16();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) fetch(t + 1, cur ^ 1);  // lands under this tile's MFMAs
+    const int qtl = t % nqt;
+    if (qtl >= wskip) {  // wave-uniform
+      int boff = cur * 2 * QT * CH;
+      asm volatile("" : "+s"(boff));  // opaque: one set of operand addresses, not one per buffer
+      const u32x4* Qs = &qd[0][0] + boff;
+      const u32x4* Ds = Qs + QT * CH;
+      const int q0 = (qt0 + qtl) * QT;
+      // row-read chunk XOR of this lane's rows (r of the Q / dO tiles, 32w + r of V: the same
+      // low bits), re-derived per tile behind an optimisation barrier so the eight per-k-step
+      // addresses are not hoisted (and spilled) across the loop
+      int cx = h ^ (((r & 3) << 2) | ((r >> 2) & 3));
+      asm volatile("" : "+v"(cx));
+      const u32x4* Qr = Qs + r * CH;
+      const u32x4* Dr = Ds + r * CH;
+      const u32x4* Vr = vall + (32 * w + r) * CH;
+      f32x16 sa = zero16(), pa = zero16();
+      {
+        bf16x8 qa[NDS];
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) qa[s] = __builtin_bit_cast(bf16x8, Qr[(2 * s) ^ cx]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) sa = mfma(qa[s], kf[s], sa);
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {  // dP in two k-halves: 32 operand registers
+        bf16x8 da[NDS / 2], vf[NDS / 2];
+#pragma unroll
+        for (int s = 0; s < NDS / 2; ++s) {
+          da[s] = __builtin_bit_cast(bf16x8, Dr[(2 * (4 * half + s)) ^ cx]);
+          vf[s] = __builtin_bit_cast(bf16x8, Vr[(2 * (4 * half + s)) ^ cx]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NDS / 2; ++s) pa = mfma(da[s], vf[s], pa);
+      }
+      const bool diag = causal && k0w + 31 > q0;
+      const float* st = stat[cur];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 L4 = *reinterpret_cast<const float4*>(st + 8 * g4 + 4 * h);
+        const float4 D4 = *reinterpret_cast<const float4*>(st + QT + 8 * g4 + 4 * h);
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
+          if (diag && kme > q0 + 8 * g4 + 4 * h + e) p = 0.f;
+          sa[i] = p;
+          pa[i] = p * (pa[i] - Dv[e]);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {  // one 16-query k-step at a time, dV^T += dO^T P then dK^T += Q^T dS
+#pragma unroll
+        for (int which = 0; which < 2; ++which) {
+          const u32x4* src = which == 0 ? Ds : Qs;
+          bf16x8 tf[NDT];
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) tf[dt] = tr_frag(src, 16 * s2, dt * 32, lane);
+          const bf16x8 op = acc_frag(which == 0 ? sa : pa, s2);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            if (which == 0) dva[dt] = mfma(tf[dt], op, dva[dt]);
+            else dka[dt] = mfma(tf[dt], op, dka[dt]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+  store_rows_T(dva, 1.f, vall + w * 32 * CH, lane, dv + off, kvstride);
+  __syncthreads();
+  store_rows_T(dka, scale, vall + w * 32 * CH, lane, dk + off, kvstride);
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// forward + dQ-pass variant: 8 = the 8-wave kernels where S % 256 == 0 (default), 4 = the 4-wave ones;
+// forward + dQ-pass variant: 8 = the 8-wave kernels where S % 256 == 0 (default), 9 = the same
+// with the ping-pong forward, 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
-// dK/dV pass: 2 = software-pipelined (default), 1 = the plain one; PTO_ATTN_DKDV or
+// dK/dV pass: 1 = the plain 4-wave one (default), 2 = software-pipelined 4-wave (measured
+// slower: profiles/r3_attn_dkdv_ab.json), 3 = 8-wave (S % 256 == 0); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
   if (g_dkdv_variant < 0) {
     const char* e = getenv("PTO_ATTN_DKDV");
-    g_dkdv_variant = e != nullptr ? atoi(e) : 2;
+    g_dkdv_variant = e != nullptr ? atoi(e) : 1;
   }
   return g_dkdv_variant;
 }
@@ -1007,13 +1345,13 @@ extern "C" {
 
 int pto_attn_set_dkdv_variant(int v) {
   const int old = dkdv_variant();
-  if (v == 1 || v == 2) g_dkdv_variant = v;
+  if (v >= 1 && v <= 3) g_dkdv_variant = v;
   return old;
 }
 
 int pto_attn_set_variant(int fwd) {
   const int old = fwd_variant();
-  if (fwd == 4 || fwd == 8) g_fwd_variant = fwd;
+  if (fwd == 4 || fwd == 8 || fwd == 9) g_fwd_variant = fwd;
   return old;
 }
 
@@ -1024,7 +1362,11 @@ int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
   if (check_shapes(B, S, Hq, Hkv, Dh)) return -1;
   if (!aligned16(q) || !aligned16(k) || !aligned16(v) || !aligned16(o) || !aligned16(lse2)) return -2;
   const float c = scale * 1.4426950408889634f;
-  if (fwd_variant() == 8 && S % BM8 == 0)
+  if (fwd_variant() == 9 && S % BM8 == 0)
+    hipLaunchKernelGGL(attn_fwd8p_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
+                       causal);
+  else if (fwd_variant() >= 8 && S % BM8 == 0)
     hipLaunchKernelGGL(attn_fwd8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
                        causal);
@@ -1044,7 +1386,7 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   for (const void* p : ps)
     if (!aligned16(p)) return -2;
   const float c = scale * 1.4426950408889634f;
-  if (fwd_variant() == 8 && S % BM8 == 0)
+  if (fwd_variant() >= 8 && S % BM8 == 0)
     hipLaunchKernelGGL(attn_bwd_dq8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                        (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
@@ -1052,10 +1394,15 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                        (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
-  hipLaunchKernelGGL(dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel : attn_bwd_dkdv_kernel,
-                     dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
-                     (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
+  if (dkdv_variant() == 3 && S % BK8 == 0)
+    hipLaunchKernelGGL(attn_bwd_dkdv8_kernel, dim3((S / BK8) * B * Hkv), dim3(NT8), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
+                       (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
+  else
+    hipLaunchKernelGGL(dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel : attn_bwd_dkdv_kernel,
+                       dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
+                       (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
   return (int)hipGetLastError();
 }
 

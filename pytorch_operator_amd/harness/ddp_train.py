@@ -380,7 +380,7 @@ def main(argv=None) -> int:
            "master_weights": use_master_weights(args, dev) or zero, "zero": 1 if zero else 0}
     if zero:
         res.update(optimizer_state_gb_per_rank=round(opt.state_bytes() / 2 ** 30, 2), zero_buckets=len(opt.buckets),
-                   zero_grad_sinks=opt.sinks, zero_grad_dtypes=sorted({str(b.grad32.dtype).replace("torch.", "") for b in opt.buckets}))
+                   zero_grad_sinks=opt.sinks, zero_grad_dtypes=sorted({str(b.gdt).replace("torch.", "") for b in opt.buckets}))
     res.update(gemm_tuning=tuning.get("mode"))
     if is_llama:
         res.update(attn=args.attn, residual_norm=args.residual_norm, linear_bwd=args.linear_bwd,

@@ -290,7 +290,7 @@ class _LinearTN(torch.autograd.Function):
             dx = F.linear(dy2, transpose2d(w)).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             sink = ctx.sink
-            if sink is not None and sink.view.dtype == x2.dtype and sink.view.shape == w.shape:
+            if sink is not None and sink.dtype == x2.dtype and sink.shape == tuple(w.shape):
                 torch.mm(transpose2d(dy2), transpose2d(x2).t(), out=sink.view)
                 sink.ready()
             else:

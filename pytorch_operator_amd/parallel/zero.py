@@ -47,11 +47,20 @@ _ALIGN = 64  # shard lengths are multiples of this (16-byte aligned fp32 / bf16 
 
 
 class _Sink:
-    """Destination of a weight gradient written in place by a backward GEMM."""
-    __slots__ = ("view", "ready")
+    """Destination of a weight gradient written in place by a backward GEMM: its slot of the
+    bucket (allocated when the bucket's first gradient arrives, see ``_Bucket.grad32``)."""
+    __slots__ = ("bucket", "off", "shape", "dtype", "ready")
 
-    def __init__(self, view: torch.Tensor, ready):
-        self.view, self.ready = view, ready
+    def __init__(self, bucket, off: int, shape, ready):
+        self.bucket, self.off, self.shape, self.ready = bucket, off, shape, ready
+        self.dtype = bucket.gdt
+
+    @property
+    def view(self) -> torch.Tensor:
+        n = 1
+        for d in self.shape:
+            n *= d
+        return self.bucket.grad32[self.off:self.off + n].view(self.shape)
 
 
 class _Bucket:
@@ -66,10 +75,16 @@ class _Bucket:
         self.flat_w = torch.zeros(self.npad, dtype=self.dtype, device=dev)
         # gradient bucket: the reduce dtype; at world 1 (nothing is reduced) the parameters' own
         # dtype, i.e. exactly the .grad autograd would have produced
-        gdt = reduce_dtype if world > 1 else self.dtype
-        self.grad32 = torch.zeros(self.npad, dtype=gdt, device=dev)
-        # world 1: the shard IS the bucket (no reduce-scatter, no copy)
-        self.gshard = self.grad32 if world == 1 else torch.zeros(self.shard, dtype=gdt, device=dev)
+        self.gdt = reduce_dtype if world > 1 else self.dtype
+        self.n = n
+        self.world = world
+        # the full gradient bucket lives only from its first gradient of a backward to the end of
+        # its reduce-scatter (world 1: to the end of step()): allocated at the first arrival, then
+        # released, so it never coexists with the forward's activation peak -- the peak memory of
+        # a step stays that of .grad-based training (the caching allocator recycles the block)
+        self._g: Optional[torch.Tensor] = None
+        self._dev = dev
+        self._gshard = None if world == 1 else torch.zeros(self.shard, dtype=self.gdt, device=dev)
         self.slot: Dict[int, int] = {}
         masters = torch.zeros(self.npad, dtype=torch.float32, device=dev) if self.dtype != torch.float32 else None
         off = 0
@@ -98,6 +113,24 @@ class _Bucket:
 
     def w_shard(self) -> torch.Tensor:
         return self.flat_w[self.lo:self.lo + self.shard]
+
+    @property
+    def grad32(self) -> torch.Tensor:
+        if self._g is None:
+            # every slot is written before use (gradient copy / in-place GEMM, or zeroed by
+            # step() for a parameter without a gradient); only the alignment padding is cleared
+            self._g = torch.empty(self.npad, dtype=self.gdt, device=self._dev)
+            if self.npad > self.n:
+                self._g[self.n:].zero_()
+        return self._g
+
+    @property
+    def gshard(self) -> torch.Tensor:
+        # world 1: the shard IS the bucket (no reduce-scatter, no copy)
+        return self.grad32 if self.world == 1 else self._gshard
+
+    def release_grad(self) -> None:
+        self._g = None
 
 
 class ZeroAdamW:
@@ -147,13 +180,12 @@ class ZeroAdamW:
         self.sinks = 0
         if grad_view:
             for b in self.buckets:
-                if b.grad32.dtype != b.dtype or not b.flat_w.is_cuda:
+                if b.gdt != b.dtype or not b.flat_w.is_cuda:
                     continue
                 b.unscaled = True
                 for p in b.params:
                     if p.dim() == 2:
-                        off = b.slot[id(p)]
-                        p._pto_grad_sink = _Sink(b.grad32[off:off + p.numel()].view(p.shape),
+                        p._pto_grad_sink = _Sink(b, b.slot[id(p)], tuple(p.shape),
                                                  lambda p=p, b=b: self._arrive(b, p))
                         self.sinks += 1
         self._hooked = 0
@@ -252,9 +284,13 @@ class ZeroAdamW:
             if b.rs_work is not None:
                 b.rs_work.wait()
                 b.rs_work = None
+            if self.world > 1:
+                b.release_grad()  # the shard holds what AdamW needs (stream-ordered after the wait)
             keep = self._save_ranges(b, skip.get(id(b), []))
             self._adamw(b)
             self._restore_ranges(b, keep)
+            if self.world == 1:
+                b.release_grad()
             if self.world > 1:
                 src = b.w_shard() if b.flat_w.is_cuda else b.w_shard().clone()
                 b.ag_work = dist.all_gather_into_tensor(b.flat_w, src, group=self.group, async_op=True)

@@ -93,7 +93,7 @@ def _fwd(q, k, v, causal):
     return o, lse2
 
 
-@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("variant", [4, 8, 9])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal):
     """Both forward kernels on scores whose row maximum keeps growing along the keys (large,
@@ -120,29 +120,32 @@ def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal
     assert torch.allclose(lse2, lse * math.log2(math.e), atol=5e-3, rtol=1e-4)
 
 
-@pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 768, 4, 4)])
+@pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 768, 4, 4), (1, 256, 2, 1)])
 def test_flash_forward_variants_agree(fwd_variant, shape):
-    """8-wave vs 4-wave forward on the same inputs (bf16 outputs within rounding)."""
+    """8-wave (plain / ping-pong) vs 4-wave forward on the same inputs (bf16 outputs within
+    rounding; the two 8-wave kernels do the same per-row operations in the same order)."""
     q, k, v = _inputs(*shape, seed=5)
     outs = {}
-    for var in (4, 8):
+    for var in (4, 8, 9):
         fwd_variant(var)
         outs[var] = _fwd(q, k, v, True)
     assert _rel(outs[8][0], outs[4][0]) < 4e-3
     assert torch.allclose(outs[8][1], outs[4][1], atol=1e-3, rtol=1e-5)
+    assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
 
 
-@pytest.mark.parametrize("dkdv", [1, 2])
+@pytest.mark.parametrize("dkdv", [1, 2, 3])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_backward_dkdv_variants(dkdv, causal):
-    """Plain and software-pipelined dK/dV passes (3-deep Q/dO ring, 1-5 tiles per head cover
-    the ring's prologue/epilogue cases) against the fp32 reference gradients."""
+    """The dK/dV passes -- plain 4-wave, software-pipelined 4-wave (3-deep Q/dO ring: 1-5 tiles
+    per head cover its prologue/epilogue), 8-wave (S % 256 == 0; other S fall back) -- and the
+    8-wave dQ pass against the fp32 reference gradients."""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import attention_reference, flash_attention, sdpa_bshd
     lib = _native.load()
     old = lib.pto_attn_set_dkdv_variant(dkdv)
     try:
-        for shape in ((1, 128, 2, 2), (2, 256, 8, 2), (1, 640, 4, 1)):
+        for shape in ((1, 128, 2, 2), (2, 256, 8, 2), (1, 640, 4, 1), (1, 768, 4, 1), (1, 512, 8, 8)):
             q, k, v = _inputs(*shape, seed=9)
             g = torch.Generator(device="cuda").manual_seed(4)
             do = torch.randn(q.shape, device="cuda", generator=g).to(torch.bfloat16)

@@ -380,8 +380,8 @@ def test_zero_grad_view_matches_master_adamw():
     to_bf16_matmul_weights(m2)
     o1 = MasterAdamW(m1.parameters(), lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1)
     o2 = ZeroAdamW(m2, lr=1e-3, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=0.05)
-    assert o2.sinks > 0 and all(b.unscaled for b in o2.buckets if b.grad32.dtype == torch.bfloat16)
-    assert {b.grad32.dtype for b in o2.buckets} == {torch.bfloat16, torch.float32}
+    assert o2.sinks > 0 and all(b.unscaled for b in o2.buckets if b.gdt == torch.bfloat16)
+    assert {b.gdt for b in o2.buckets} == {torch.bfloat16, torch.float32}
     x = torch.randint(0, 256, (2, 65), device="cuda")
     for _ in range(3):
         for m, o in ((m1, o1), (m2, o2)):
