@@ -17,6 +17,7 @@ import hashlib
 import os
 import shutil
 import subprocess
+import tempfile
 import threading
 from pathlib import Path
 
@@ -42,9 +43,17 @@ def _sources():
     return sorted(_SRC_DIR.glob("*.hip")) + sorted(_SRC_DIR.glob("*.h"))
 
 
+# Per-file compiler flags.  attention.hip: MFMAs in VGPR form -- its one-wave-per-SIMD dK/dV
+# kernels need more than the 256 architectural VGPRs, and with the default (AGPR-form)
+# accumulators the compiler moved them between AGPRs and VGPRs every tile (298 v_accvgpr_read +
+# 261 v_accvgpr_write in the kernel against 31 + 22 with VGPR form).
+_FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def _source_digest() -> str:
     h = hashlib.sha256()
     h.update(_ARCH.encode())
+    h.update(repr(sorted(_FILE_FLAGS.items())).encode())
     for p in _sources():
         h.update(p.name.encode())
         h.update(p.read_bytes())
@@ -67,17 +76,36 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if not force and _LIB_PATH.exists() and _STAMP.exists() and _STAMP.read_text() == digest:
         return _LIB_PATH
     _LIB_DIR.mkdir(parents=True, exist_ok=True)
-    hip_srcs = [str(p) for p in sorted(_SRC_DIR.glob("*.hip"))]
+    hip_srcs = sorted(_SRC_DIR.glob("*.hip"))
     tmp = _LIB_PATH.with_suffix(f".so.tmp{os.getpid()}")
-    cmd = [
-        hipcc_path(), f"--offload-arch={_ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-munsafe-fp-atomics", "-I", str(_SRC_DIR), "-o", str(tmp), *hip_srcs,
-    ]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise NativeLibraryError(f"hipcc failed ({res.returncode}):\n{res.stderr[-8000:]}")
+    objdir = Path(tempfile.mkdtemp(prefix="pto_hip_obj_"))
+    base = [hipcc_path(), f"--offload-arch={_ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
+            "-I", str(_SRC_DIR)]
+    try:
+        # one object per source (their own flags), compiled in parallel, then one shared library
+        procs, objs = [], []
+        for src in hip_srcs:
+            obj = objdir / (src.stem + ".o")
+            cmd = base + _FILE_FLAGS.get(src.name, []) + ["-c", str(src), "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)))
+            objs.append(str(obj))
+        errs = []
+        for src, pr in procs:
+            _, err = pr.communicate()
+            if pr.returncode != 0:
+                errs.append(f"{src.name}: hipcc failed ({pr.returncode}):\n{err[-8000:]}")
+        if errs:
+            raise NativeLibraryError("\n".join(errs))
+        cmd = [hipcc_path(), f"--offload-arch={_ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise NativeLibraryError(f"hipcc link failed ({res.returncode}):\n{res.stderr[-8000:]}")
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     os.replace(tmp, _LIB_PATH)
     _STAMP.write_text(digest)
     return _LIB_PATH

@@ -134,11 +134,12 @@ def test_flash_forward_variants_agree(fwd_variant, shape):
     assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
 
 
-@pytest.mark.parametrize("dkdv", [1, 2, 3])
+@pytest.mark.parametrize("dkdv", [1, 2, 3, 4])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_backward_dkdv_variants(dkdv, causal):
     """The dK/dV passes -- plain 4-wave, software-pipelined 4-wave (3-deep Q/dO ring: 1-5 tiles
-    per head cover its prologue/epilogue), 8-wave (S % 256 == 0; other S fall back) -- and the
+    per head cover its prologue/epilogue), 8-wave (S % 256 == 0; other S fall back), lean-register
+    4-wave with LDS-DMA staging and per-wave causal tile skip -- and the
     8-wave dQ pass against the fp32 reference gradients."""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import attention_reference, flash_attention, sdpa_bshd

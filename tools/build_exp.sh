@@ -12,7 +12,8 @@ rm -f $OUT/*.so
 pids=()
 for f in csrc/kernels/*.hip; do
   n=$(basename $f .hip); [ "$n" = mnist_kernels ] && continue
-  [ $OBJ/$n.o -nt $f ] || { $HIPCC $FLAGS -c $f -o $OBJ/$n.o & pids+=($!); }
+  extra=""; [ "$n" = attention ] && extra="${ATTN_FLAGS--mllvm -amdgpu-mfma-vgpr-form=1}"  # as ops/_native.py
+  [ $OBJ/$n.o -nt $f ] || { $HIPCC $FLAGS $extra -c $f -o $OBJ/$n.o & pids+=($!); }
 done
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
