@@ -1452,15 +1452,15 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // with the ping-pong forward, 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
-// dK/dV pass: 1 = the plain 4-wave one (default), 2 = software-pipelined 4-wave (measured
-// slower: profiles/r3_attn_dkdv_ab.json), 3 = 8-wave (S % 256 == 0; slower,
-// profiles/r3_attn_v2_ab.json), 4 = lean-register 4-wave with LDS-DMA staging; PTO_ATTN_DKDV or
+// dK/dV pass: 4 = lean-register 4-wave with LDS-DMA staging (default), 1 = the plain 4-wave
+// one (equal within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-pipelined 4-wave
+// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
   if (g_dkdv_variant < 0) {
     const char* e = getenv("PTO_ATTN_DKDV");
-    g_dkdv_variant = e != nullptr ? atoi(e) : 1;
+    g_dkdv_variant = e != nullptr ? atoi(e) : 4;
   }
   return g_dkdv_variant;
 }
