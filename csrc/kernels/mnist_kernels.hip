@@ -45,6 +45,11 @@ using namespace pto;
 #ifndef PTO_ABL
 #define PTO_ABL 0
 #endif
+// fc1 split-K factor of the training path (A/B): 2 (256 workgroups of 5 waves) or 5 (640 of 2)
+#ifndef PTO_FC1_KS
+#define PTO_FC1_KS 2
+#endif
+static_assert(PTO_FC1_KS == 2 || PTO_FC1_KS == 5, "fc1 split-K: K = 800 over 10 waves of 80");
 
 namespace {
 
@@ -634,13 +639,25 @@ __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
   red[wv][lane] = c0 + c1;
   __syncthreads();
   stamp(dbg, 1);
-  if (tid < 256) {
-    float s = 0.f;
+  if constexpr (640 / KS >= 256) {
+    if (tid < 256) {
+      float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
-    if (orow < B && ocol < 500) {
-      if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
-      else h[((size_t)kz * B + orow) * 500 + ocol] = s;
+      for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
+      if (orow < B && ocol < 500) {
+        if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
+        else h[((size_t)kz * B + orow) * 500 + ocol] = s;
+      }
+    }
+  } else {  // fewer threads than tile outputs (KS = 5: 128): two outputs per thread
+#pragma unroll
+    for (int e = tid; e < 256; e += 640 / KS) {
+      const int le = e >> 2, re = e & 3;
+      const int orw = mt * 16 + (le >> 4) * 4 + re, ocl = nt * 16 + (le & 15);
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) s += red[q][le][re];
+      if (orw < B && ocl < 500) h[((size_t)kz * B + orw) * 500 + ocl] = s;
     }
   }
 }
@@ -683,8 +700,17 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
     float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
     if (hp2 != nullptr) {
-      const float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
-      const float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
+      // partials 1 .. KS-1 of the split-K fc1 follow each other ([KS][B][500]), summed in order
+      float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
+      float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
+#pragma unroll
+      for (int kz = 2; kz < PTO_FC1_KS; ++kz) {
+        const float* hk = hp2 + (size_t)(kz - 1) * B * 500 + (size_t)bc * 500;
+        const float4 r0 = *reinterpret_cast<const float4*>(hk + o0);
+        const float4 r1 = *reinterpret_cast<const float4*>(hk + o1);
+        q0 = make_float4(q0.x + r0.x, q0.y + r0.y, q0.z + r0.z, q0.w + r0.w);
+        q1 = make_float4(q1.x + r1.x, q1.y + r1.y, q1.z + r1.z, q1.w + r1.w);
+      }
       const float4 c0 = *reinterpret_cast<const float4*>(b1 + o0);
       const float4 c1 = *reinterpret_cast<const float4*>(b1 + o1);
       h0 = make_float4(fmaxf(h0.x + q0.x + c0.x, 0.f), fmaxf(h0.y + q0.y + c0.y, 0.f),
@@ -2773,11 +2799,13 @@ int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* 
   return (int)hipGetLastError();
 }
 
-// Split-K fc1: pre-activation halves to parts[2][B][500] (head_kernel finishes h).
+int pto_mnist_fc1_ks() { return PTO_FC1_KS; }
+
+// Split-K fc1: pre-activation partials to parts[KS][B][500] (head_kernel finishes h).
 int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, int* clr, void* stream) {
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)parts)) & 15) return -2;
-  hipLaunchKernelGGL(fc1_fwd_kernel<2>, dim3(32, (B + 15) / 16, 2), dim3(320), 0,
+  hipLaunchKernelGGL(fc1_fwd_kernel<PTO_FC1_KS>, dim3(32, (B + 15) / 16, PTO_FC1_KS), dim3(640 / PTO_FC1_KS), 0,
                      (hipStream_t)stream, x, w, nullptr, parts, B, clr, g_dbg);
   return (int)hipGetLastError();
 }
@@ -3042,6 +3070,7 @@ int pto_mnist_fc1_bwd_head(const float* hp, const float* b1, const float* w2, co
                            const int* lab, const float* a2, const uint8_t* idx2, const float* w1,
                            float grad_scale, float* dz2, float* h_out, float* dh_out,
                            float* dlogits, float* per_sample, int B, void* stream) {
+  if (PTO_FC1_KS != 2) return -1;  // reads the fc1 partials as two halves
   PTO_CHECK_B(B);
   if (lab == nullptr || h_out == nullptr || dh_out == nullptr || dlogits == nullptr ||
       per_sample == nullptr)

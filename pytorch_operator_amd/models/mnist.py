@@ -222,7 +222,8 @@ class FusedMnistTrainer:
         self.xn = torch.empty((B, 784), device=dev)
         self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
         self.per_sample = torch.empty((B, 2), device=dev)
-        self.h_parts = torch.empty(2 * B * 500, device=dev)  # split-K fc1 pre-activations
+        self.fc1_ks = K.fc1_split()
+        self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
         self.w1_next = torch.empty((500, 800), device=dev)  # fused-SGD fc1.weight (tail copies back)
         self.stage = K_stage(self.source, B, dev)
         # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
@@ -295,13 +296,14 @@ class FusedMnistTrainer:
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
         # split-K fc1 (256 workgroups); fc1_bwd_head adds the halves + bias and applies ReLU
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:2 * B * 500].view(2, B, 500),
+        ks = self.fc1_ks
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500),
                         clear=self._pend if _defer else None)
 
     def _head(self, B: int) -> None:
         """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
         K, p = self.K, self._pv
-        hp = self.h_parts[:2 * B * 500].view(2, B, 500)
+        hp = self.h_parts[:self.fc1_ks * B * 500].view(self.fc1_ks, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])

@@ -127,6 +127,7 @@ _SIGNATURES = {
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP, _VP],
+    "pto_mnist_fc1_ks": [],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],

@@ -249,19 +249,26 @@ def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out
 
 
+def fc1_split() -> int:
+    """K split of the training-path fc1 (compile-time ``PTO_FC1_KS`` of the library: 2)."""
+    return int(_native.load().pto_mnist_fc1_ks())
+
+
 def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
                   clear: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Split-K fc1 forward: the two pre-activation halves ``out[z] = x[:, Kz] @ w[:, Kz].T``
-    (K halves of 400) as fp32 [2, B, 500]; ``head(..., h_second=out[1], fc1_bias=b,
-    h_out=h)`` finishes ``h = relu(out[0] + out[1] + b)``.  256 workgroups instead of 128:
-    half the operand bytes per CU on the latency-bound load phase.  ``clear``: int32 device
-    flag set to 0 by the launch (conv12_fwd's deferred-SGD flag)."""
+    """Split-K fc1 forward: the pre-activation partials ``out[z] = x[:, Kz] @ w[:, Kz].T`` over
+    ``fc1_split()`` K slices (2 x 400) as fp32 [KS, B, 500]; ``head(..., h_second=out[1],
+    fc1_bias=b, h_out=h)`` finishes ``h = relu(out[0] + out[1] + ... + b)`` (the partials after
+    ``out[1]`` are read from the same buffer).  256 workgroups instead of 128: half the operand
+    bytes per CU on the latency-bound load phase.  ``clear``: int32 device flag set to 0 by the
+    launch (conv12_fwd's deferred-SGD flag)."""
     lib = _native.load()
     B = x.shape[0]
+    ks = fc1_split()
     _req(x, (B, 800), torch.float32, "x")
     _req(w, (500, 800), torch.float32, "fc1.weight")
-    out = torch.empty((2, B, 500), device=x.device) if out is None else out
-    _req(out, (2, B, 500), torch.float32, "fc1 partials")
+    out = torch.empty((ks, B, 500), device=x.device) if out is None else out
+    _req(out, (ks, B, 500), torch.float32, "fc1 partials")
     rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _ptr(clear), _stream())
     _native.check(rc, "fc1_fwd_parts")
     return out
