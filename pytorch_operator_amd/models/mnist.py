@@ -222,7 +222,7 @@ class FusedMnistTrainer:
         self.xn = torch.empty((B, 784), device=dev)
         self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
         self.per_sample = torch.empty((B, 2), device=dev)
-        self.fc1_ks = K.fc1_split()
+        self.fc1_ks = self.K.fc1_split()
         self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
         self.w1_next = torch.empty((500, 800), device=dev)  # fused-SGD fc1.weight (tail copies back)
         self.stage = K_stage(self.source, B, dev)
