@@ -45,6 +45,11 @@ using namespace pto;
 #ifndef PTO_ABL
 #define PTO_ABL 0
 #endif
+// head_kernel's ten logit sums (A/B): 1 = DPP / permlane all-reduce (six VALU steps, no LDS),
+// 0 = __shfl_xor butterflies (ds_bpermute round trips)
+#ifndef PTO_HEAD_DPP
+#define PTO_HEAD_DPP 0
+#endif
 // fc1 split-K factor of the training path (A/B): 2 (256 workgroups of 5 waves) or 5 (640 of 2)
 #ifndef PTO_FC1_KS
 #define PTO_FC1_KS 2
@@ -159,6 +164,29 @@ __global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
 //   The two K halves meet in LDS; the 2x2 pool window = 2 registers of this
 //   lane x 2 registers of lane^32.
 // ---------------------------------------------------------------------------
+// Sum over the 64 lanes, every lane the same bits: quad xor 1 and 2 and the row half-mirror /
+// mirror (DPP on the add), then v_permlane16_swap / v_permlane32_swap pairs (each step adds
+// two equal-size partial sums, a + b == b + a, so all lanes round identically).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_allsum_dpp(float x) {
+  x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f<0x141>(x);  // row_half_mirror
+  x += dpp_f<0x140>(x);  // row_mirror
+  {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+  }
+  {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+  }
+  return x;
+}
+
 // Value of lane l + 32 for lanes l < 32 (v_permlane32_swap: one VALU op; __shfl_xor(v, 32)
 // lowers to an LDS ds_bpermute round trip).  Lanes >= 32 get an unspecified value.
 __device__ __forceinline__ float from_upper_half(float v) {
@@ -745,11 +773,16 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     for (int q = 0; q < 8; ++q) p = fmaf(hv[q], wv[j][q], p);
     logit[j] = p;
   }
-  // 10 independent butterfly reductions, interleaved
+  if (PTO_HEAD_DPP) {
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1)
+    for (int j = 0; j < 10; ++j) logit[j] = wave_allsum_dpp(logit[j]);
+  } else {
+    // 10 independent butterfly reductions, interleaved
 #pragma unroll
-    for (int j = 0; j < 10; ++j) logit[j] += __shfl_xor(logit[j], o, 64);
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < 10; ++j) logit[j] += __shfl_xor(logit[j], o, 64);
+  }
 #pragma unroll
   for (int j = 0; j < 10; ++j) logit[j] += b2[j];
   float m = logit[0];

@@ -1,10 +1,13 @@
 #!/bin/bash
-# Round 3: fc1 split-K 5 (640 workgroups of 2 waves) vs 2 -- numerics of the variant library,
-# then the same-box bench A/B (tools/gpu_ab_libs2.sh: in-tree vs exp/*.so).
+# Round 3: MNIST variant libraries -- fc1 split-K 5 (640 workgroups of 2 waves) and the head's
+# DPP/permlane logit all-reduce -- numerics of every variant, then the same-box bench A/B
+# (tools/gpu_ab_libs2.sh: in-tree vs exp/*.so).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-PTO_HIP_LIB=pytorch_operator_amd/_lib/exp/ks5.so timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ks5_test.log 2>&1 || { echo "ks5 tests failed"; tail -30 gpurun_out/ks5_test.log; exit 1; }
-tail -1 gpurun_out/ks5_test.log
-REPS=3 timeout -k 10 900 bash tools/gpu_ab_libs2.sh
+for lib in pytorch_operator_amd/_lib/exp/*.so; do
+PTO_HIP_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/var_test.log 2>&1 || { echo "tests failed with $lib"; tail -30 gpurun_out/var_test.log; exit 1; }
+echo "$lib: $(tail -1 gpurun_out/var_test.log)"
+done
+REPS=3 timeout -k 10 1000 bash tools/gpu_ab_libs2.sh
