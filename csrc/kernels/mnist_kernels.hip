@@ -45,12 +45,14 @@ using namespace pto;
 #ifndef PTO_ABL
 #define PTO_ABL 0
 #endif
-// head_kernel's ten logit sums (A/B): 1 = DPP / permlane all-reduce (six VALU steps, no LDS),
-// 0 = __shfl_xor butterflies (ds_bpermute round trips)
+// head_kernel's ten logit sums: 1 = DPP / permlane all-reduce (six VALU steps, no LDS; default:
+// -0.3 to -0.5 us/step, profiles/r3_mnist_ab_dpp_ks5.txt), 0 = __shfl_xor butterflies
+// (ds_bpermute round trips)
 #ifndef PTO_HEAD_DPP
-#define PTO_HEAD_DPP 0
+#define PTO_HEAD_DPP 1
 #endif
-// fc1 split-K factor of the training path (A/B): 2 (256 workgroups of 5 waves) or 5 (640 of 2)
+// fc1 split-K factor of the training path: 2 (256 workgroups of 5 waves; default) or 5 (640 of 2:
+// +0.5 us/step, profiles/r3_mnist_ab_dpp_ks5.txt)
 #ifndef PTO_FC1_KS
 #define PTO_FC1_KS 2
 #endif

@@ -284,7 +284,8 @@ def test_fc1_bwd_head_matches_head_plus_fc1_bwd(lib, B):
 @pytest.mark.parametrize("B", [64, 50])
 def test_fused_schedule_matches_classic(lib, B):
     """The 5-launch schedule (fc1_bwd_head; fc weight grads + SGD in conv_bwd's idle waves at
-    B = 64, in tail_sgd otherwise) trains exactly like the 6-launch classic one."""
+    B = 64, in tail_sgd otherwise) trains like the 6-launch classic one (to rounding: the two
+    heads sum the logits' dot products in different orders -- MFMA K-split vs DPP all-reduce)."""
     from pytorch_operator_amd.models.mnist import FusedMnistTrainer
     from pytorch_operator_amd.ops import mnist as K
     dev = torch.device("cuda")
@@ -301,10 +302,10 @@ def test_fused_schedule_matches_classic(lib, B):
         torch.cuda.synchronize()
         res[sched] = (tr.flat_params.clone(), tr.flat_momentum.clone(), tr.loss(), tr.flat_grads.clone())
     (p0, m0, l0, g0), (p1, m1, l1, g1) = res["classic"], res["fused"]
-    assert _rel(p1, p0) < 1e-6 and _rel(m1, m0) < 1e-5
+    assert _rel(p1, p0) < 1e-5 and _rel(m1, m0) < 1e-4
     assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
     ce = tr.layout.conv_end
-    assert _rel(g1[ce:], g0[ce:]) < 1e-5  # fc grads are still written for inspection
+    assert _rel(g1[ce:], g0[ce:]) < 1e-4  # fc grads are still written for inspection
 
 
 # ---------------------------------------------------------------------------- round 3
