@@ -189,6 +189,18 @@ __device__ __forceinline__ float wave_allsum_dpp(float x) {
   return x;
 }
 
+// Sum over the four 16-lane rows at this lane's row position (= x + shfl_xor 16, then + shfl_xor
+// 32, bit for bit): v_permlane16_swap / v_permlane32_swap pair sums instead of two ds_bpermute
+// round trips.
+__device__ __forceinline__ float sum_lane_rows(float x) {
+  {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
+  }
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
 // Value of lane l + 32 for lanes l < 32 (v_permlane32_swap: one VALU op; __shfl_xor(v, 32)
 // lowers to an LDS ds_bpermute round trip).  Lanes >= 32 get an unspecified value.
 __device__ __forceinline__ float from_upper_half(float v) {
@@ -968,8 +980,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
       }
     }
     if (kt == 0) {
-      dbsum += __shfl_xor(dbsum, 16, 64);
-      dbsum += __shfl_xor(dbsum, 32, 64);
+      dbsum = sum_lane_rows(dbsum);
       if (g == 0 && nv) {
         if (a.gb1 != nullptr) a.gb1[n] = dbsum;
         if (a.sgd) {
@@ -1087,8 +1098,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
       }
     }
     if (nt == 0) {
-      dbsum += __shfl_xor(dbsum, 16, 64);
-      dbsum += __shfl_xor(dbsum, 32, 64);
+      dbsum = sum_lane_rows(dbsum);
       if (g == 0 && i < 10) {
         if (a.gb2 != nullptr) a.gb2[i] = dbsum;
         if (a.sgd) {
@@ -1100,8 +1110,8 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     }
     if (do_stats) {
       for (int bb = lane + 64; bb < B; bb += 64) { ls += a.per_sample[2 * bb]; cs += a.per_sample[2 * bb + 1]; }
-      ls = wave_sum(ls);
-      cs = wave_sum(cs);
+      ls = wave_allsum_dpp(ls);
+      cs = wave_allsum_dpp(cs);
       if (lane == 0) { a.stats[0] = ls * a.loss_scale; a.stats[1] = cs; }
     }
   } else {
@@ -1485,8 +1495,7 @@ __device__ __forceinline__ void fc_tile_run(const FcGrad& fc, int t, int B, int 
   constexpr bool sgd = SGD;
   const bool bias = w1 ? kt == 0 : nt == 0;
   if (bias) {
-    dbsum += __shfl_xor(dbsum, 16, 64);
-    dbsum += __shfl_xor(dbsum, 32, 64);
+    dbsum = sum_lane_rows(dbsum);
   }
   if (w1) {
     const int f = kt * 16 + i;
@@ -1539,8 +1548,8 @@ __device__ __forceinline__ void fc_tile_run(const FcGrad& fc, int t, int B, int 
     if (nt == 1 && fc.per_sample != nullptr && fc.stats != nullptr) {
       float ls = 0.f, cs = 0.f;
       for (int bb = lane; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
-      ls = wave_sum(ls);
-      cs = wave_sum(cs);
+      ls = wave_allsum_dpp(ls);
+      cs = wave_allsum_dpp(cs);
       if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
     }
   }
@@ -2560,8 +2569,7 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
       }
     }
     if (nt == 0) {
-      dbsum += __shfl_xor(dbsum, 16, 64);
-      dbsum += __shfl_xor(dbsum, 32, 64);
+      dbsum = sum_lane_rows(dbsum);
       if (g == 0 && i < 10) {
         sgd_elem(pb, mb, dbsum, hy);
         fc.g_b2[i] = dbsum;
@@ -2571,8 +2579,8 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
     }
     if (do_stats) {
       for (int bb = lane + 64; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
-      ls = wave_sum(ls);
-      cs = wave_sum(cs);
+      ls = wave_allsum_dpp(ls);
+      cs = wave_allsum_dpp(cs);
       if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
     }
     stamp(dbg, 1);
@@ -2627,8 +2635,7 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
       }
     }
     if (kt == 0) {
-      dbsum += __shfl_xor(dbsum, 16, 64);
-      dbsum += __shfl_xor(dbsum, 32, 64);
+      dbsum = sum_lane_rows(dbsum);
       if (g == 0 && nv) {
         sgd_elem(pb, mb, dbsum, hy);
         fc.g_b1[nn] = dbsum;
