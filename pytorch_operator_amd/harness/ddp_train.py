@@ -51,9 +51,10 @@ def parse_args(argv=None):
                    help="ResNet activations/weights layout (NHWC maps to MIOpen's NHWC bf16 kernels)")
     p.add_argument("--bn", choices=["hip", "library"], default="hip",
                    help="ResNet: fused HIP batch-norm(+add)(+ReLU) kernels or PyTorch's BN/add/ReLU ops")
-    p.add_argument("--bn-link", type=int, default=1,
+    p.add_argument("--bn-link", type=int, default=2, choices=[0, 1, 2],
                    help="ResNet: each bottleneck's bn3 backward also sums the next block's residual "
-                        "gradient in-kernel (ops/batchnorm.py GradLink) instead of autograd's add pass (1/0)")
+                        "gradient in-kernel (ops/batchnorm.py GradLink) instead of autograd's add pass (1); "
+                        "2 also sums a stage's downsample-conv input gradient there (link_tap); 0: off")
     p.add_argument("--pool", choices=["hip", "library"], default="hip",
                    help="ResNet stem max-pool: HIP kernels (1-byte taps, gather backward) or PyTorch's op")
     p.add_argument("--conv1x1", choices=["gemm", "library"], default="library",
@@ -109,12 +110,15 @@ def use_zero(args, device, world: int) -> bool:
 def build(args, device, world: int = 1):
     import torch
     if args.model.startswith("resnet"):
-        from ..models.resnet import resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl, set_pool_impl
+        from ..models.resnet import (Bottleneck, resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl,
+                                     set_pool_impl)
         model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
         from ..ops.batchnorm import BatchNormAct2d
         for m in model.modules():
             if isinstance(m, BatchNormAct2d) and m.link_output:
                 m.link_output = bool(args.bn_link)
+            if isinstance(m, Bottleneck):
+                m.tap_downsample = args.bn_link >= 2
         set_pool_impl(model, args.pool)
         set_conv1x1_impl(model, args.conv1x1)
         fmt = torch.channels_last if args.memory_format == "channels_last" else torch.contiguous_format

@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.batchnorm import BatchNormAct2d
+from ..ops.batchnorm import BatchNormAct2d, link_tap
 from ..ops.pool import MaxPool3x3s2
 
 
@@ -60,8 +60,13 @@ class Bottleneck(nn.Module):
         self.bn3 = BatchNormAct2d(planes * self.expansion, relu=True, link_output=True)
         self.downsample = downsample
 
+    tap_downsample = True  # a stage's input gradient from the downsample conv summed in bn3 (link_tap)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            idt = x
+        else:
+            idt = self.downsample(link_tap(x) if self.tap_downsample else x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), idt)

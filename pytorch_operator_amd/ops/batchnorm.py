@@ -14,6 +14,10 @@ consumer's backward hands its residual gradient to the producer through a ``Grad
 (returning no autograd gradient for that input, so the edge only orders the two backwards)
 and the producer's backward kernels load both gradients and add them in fp32.
 
+The first block of a stage uses its input twice through convolutions (conv1 and the
+downsample conv): ``link_tap`` routes the downsample conv's input gradient through the same
+link, so that sum is fused into the producer's backward as well.
+
 ``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and state dict)
 whose forward takes an optional residual and applies the ReLU itself.  Its ``impl``
 (``"hip"`` / ``"library"``) selects the HIP kernels or PyTorch's own ops on a GPU; on CPU, in
@@ -131,6 +135,34 @@ class _BNAct(torch.autograd.Function):
         if dz is not None and dz.dtype != ctx.res_dtype:
             dz = dz.to(ctx.res_dtype)
         return dx, dgamma, dbeta, dz, None, None, None, None, None, None, None, None
+
+
+class _LinkTap(torch.autograd.Function):
+    """Identity whose backward hands the incoming gradient to ``link`` instead of autograd:
+    the second consumer of a linked ``BatchNormAct2d`` output (e.g. a stage's downsample
+    conv next to its conv1) leaves its input gradient for the producer's backward kernels,
+    which add it to the first consumer's in fp32 (no separate gradient-sum pass)."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.link.dz = g
+        return None, None
+
+
+def link_tap(x: torch.Tensor) -> torch.Tensor:
+    """``x`` for a second consumer: if ``x`` is a linked ``batch_norm_act`` output whose link
+    is unclaimed, the gradient flowing back through the result is summed inside the
+    producer's backward; otherwise ``x`` itself (autograd sums the gradients as usual)."""
+    link = getattr(x, "_pto_link", None)
+    if link is None or link.claimed or not torch.is_grad_enabled() or not x.requires_grad:
+        return x
+    link.claimed = True
+    return _LinkTap.apply(x, link)
 
 
 def batch_norm_act(x, weight, bias, running_mean=None, running_var=None, num_batches_tracked=None,

@@ -160,7 +160,9 @@ def test_residual_gradient_summed_in_bn_backward_matches_fp64(dtype):
 
 def test_resnet_blocks_claim_links():
     """In the ResNet every identity bottleneck's residual comes from the previous bn3 through a
-    link (12 of ResNet-50's 16 blocks); downsample blocks keep autograd's path."""
+    link (12 of ResNet-50's 16 blocks), and a stage's first (downsample) block taps the previous
+    bn3's link for its downsample conv's input gradient (3 more); only the last bn3 (feeding the
+    pooling head) has no second consumer."""
     from pytorch_operator_amd.models.resnet import ResNet
     m = ResNet((2, 2, 1, 1), num_classes=10, width=8).cuda().to(memory_format=torch.channels_last)
     x = torch.randn(2, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
@@ -172,6 +174,65 @@ def test_resnet_blocks_claim_links():
     for h in hs:
         h.remove()
     assert len(links) == 6 and all(lk is not None for lk in links)
-    # blocks 2 of layer1 / layer2 take their residual from the previous block's bn3
-    assert [lk.claimed for lk in links] == [True, False, True, False, False, False]
+    # blocks 2 of layer1 / layer2 take their residual from the previous block's bn3; the first
+    # blocks of layer2-4 tap it for the downsample conv
+    assert [lk.claimed for lk in links] == [True, True, True, True, True, False]
     assert all(lk.dz is None for lk in links)
+
+
+def _tap_chain(dtype, tap, seed=1, C=64, shape=(4, 64, 9, 7)):
+    """Stage-entry shape: y1 = relu(bn1(x)) [producer] feeds two 1x1 'convs' -- ha (conv1,
+    through autograd) and hb (downsample, through ``link_tap`` when ``tap``); loss =
+    <relu(bn2(ha(y1))), dy> + <bn3(hb(y1)), dz>."""
+    from pytorch_operator_amd.ops.batchnorm import batch_norm_act, link_tap
+    g = torch.Generator().manual_seed(seed)
+    x1 = torch.randn(shape, generator=g).to(dtype)
+    wa = (torch.randn(C, C, generator=g) / C ** 0.5).to(dtype)
+    wb = (torch.randn(C, C, generator=g) / C ** 0.5).to(dtype)
+    ps = [0.5 + torch.rand(C, generator=g) if i % 2 == 0 else 0.2 * torch.randn(C, generator=g) for i in range(6)]
+    dy = torch.randn(shape, generator=g).to(dtype)
+    dz = torch.randn(shape, generator=g).to(dtype)
+    cl = dict(memory_format=torch.channels_last)
+
+    def h(y, w):
+        return torch.einsum("nchw,dc->ndhw", y, w).contiguous(**cl)
+
+    xg = x1.cuda().contiguous(**cl).requires_grad_(True)
+    p = [t.cuda().requires_grad_(True) for t in ps]
+    y1 = batch_norm_act(xg, p[0], p[1], relu=True, impl="hip", link_output=True)
+    ya = batch_norm_act(h(y1, wa.cuda()), p[2], p[3], relu=True, impl="hip")
+    yb = batch_norm_act(h(link_tap(y1) if tap else y1, wb.cuda()), p[4], p[5], impl="hip")
+    ((ya.float() * dy.cuda().float()).sum() + (yb.float() * dz.cuda().float()).sum()).backward()
+    got = [xg.grad] + [t.grad for t in p]
+
+    xr = x1.double().requires_grad_(True)
+    pr = [t.double().requires_grad_(True) for t in ps]
+    y1r = F.relu(F.batch_norm(xr, None, None, pr[0], pr[1], True, 0.1, 1e-5))
+    yar = F.relu(F.batch_norm(h(y1r, wa.double()), None, None, pr[2], pr[3], True, 0.1, 1e-5))
+    ybr = F.batch_norm(h(y1r, wb.double()), None, None, pr[4], pr[5], True, 0.1, 1e-5)
+    ((yar * dy.double()).sum() + (ybr * dz.double()).sum()).backward()
+    return got, [xr.grad] + [t.grad for t in pr], y1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_downsample_tap_gradient_summed_in_bn_backward_matches_fp64(dtype):
+    """link_tap: the second conv consumer's input gradient reaches the producer BN through its
+    link and is summed in-kernel -- x / gamma / beta gradients match fp64 autograd and are no
+    less accurate than autograd's own sum (the untapped run)."""
+    got, ref, y1 = _tap_chain(dtype, tap=True)
+    assert y1._pto_link.claimed and y1._pto_link.dz is None
+    unfused, _, y1u = _tap_chain(dtype, tap=False)
+    assert not y1u._pto_link.claimed
+
+    def rel(a, r):
+        a, r = a.detach().cpu().double(), r.double()
+        return float((a - r).norm() / r.norm().clamp_min(1e-30))
+
+    for name, a, u, r in zip(["dx", "dg1", "db1", "dg2", "db2", "dg3", "db3"], got, unfused, ref):
+        ea, eu = rel(a, r), rel(u, r)
+        if dtype == torch.float32:
+            assert ea < 2e-5, (name, ea, eu)
+        else:
+            # bf16 rounding of y1, both conv outputs and the gradients: ~3 % vs fp64 on this
+            # chain either way; the fused fp32 sum must be no less accurate than autograd's
+            assert ea < 5e-2 and ea <= 1.05 * eu + 1e-4, (name, ea, eu)
