@@ -23,6 +23,11 @@ constexpr int BN_NT = 256;
 constexpr int FIN_CH = 16;  // finalize blocks: 16 channels x 64 partial groups = 1024 threads
 constexpr int FIN_G = 64;
 constexpr int FIN_NT = FIN_CH * FIN_G;
+#ifndef PTO_BN_FIN_BATCH
+#define PTO_BN_FIN_BATCH 1  // finalize: all of a thread's partials loaded at once (0: one per loop trip)
+#endif
+constexpr int FIN_GMAX = 1024;               // pto_bn_plan's cap on the reduction grid
+constexpr int FIN_IT = FIN_GMAX / FIN_G;     // partials per finalize thread, loaded together
 
 typedef __hip_bfloat16 bf16;
 
@@ -145,8 +150,26 @@ __global__ __launch_bounds__(FIN_NT) void bn_stats_finalize_kernel(
   __shared__ float s_n[FIN_G][FIN_CH], s_m[FIN_G][FIN_CH], s_q[FIN_G][FIN_CH];
   const int pg = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH, c = blockIdx.x * FIN_CH + cl;
   float n = 0.f, m = 0.f, q = 0.f;
+#if !PTO_BN_FIN_BATCH
   if (c < C)
     for (int g = pg; g < G; g += FIN_G) chan(n, m, q, part_n[g], part[(size_t)g * 2 * C + c], part[(size_t)g * 2 * C + C + c]);
+#else
+  {
+    // every partial of this thread in flight at once (G <= FIN_GMAX), then merged in g order
+    float pn[FIN_IT], pm[FIN_IT], pq[FIN_IT];
+    const int cc = c < C ? c : 0;
+#pragma unroll
+    for (int i = 0; i < FIN_IT; ++i) {
+      const int g = pg + FIN_G * i, gg = g < G ? g : 0;
+      pn[i] = part_n[gg];
+      pm[i] = part[(size_t)gg * 2 * C + cc];
+      pq[i] = part[(size_t)gg * 2 * C + C + cc];
+      if (g >= G || c >= C) pn[i] = 0.f;  // chan() skips empty partials
+    }
+#pragma unroll
+    for (int i = 0; i < FIN_IT; ++i) chan(n, m, q, pn[i], pm[i], pq[i]);
+  }
+#endif
   s_n[pg][cl] = n; s_m[pg][cl] = m; s_q[pg][cl] = q;
   __syncthreads();
   for (int w = FIN_G / 2; w >= 1; w >>= 1) {  // fixed-shape tree: deterministic
@@ -176,11 +199,25 @@ __global__ __launch_bounds__(FIN_NT) void bn_stats_finalize_kernel(
 // ---- forward 3: y = (x - mean) * scale + beta [+ z] [ReLU] (centred first: no cancellation
 // of x * scale against mean * scale near the ReLU boundary); the grid stride is a multiple
 // of C/8, so a thread's channels (and its per-channel registers) never change
-template <typename T, bool RELU, bool RES>
+// MOUT: also write the ReLU mask as one byte per 8-channel vector (bit j: stored y > 0), which
+// the backward reads instead of y (1/16 of its bytes)
+template <typename T>
+__device__ __forceinline__ uint32_t pos_bits(const float (&v)[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // the value as stored (bf16: rounded) is > 0; v >= 0 after the ReLU
+    const bool p = sizeof(T) == 2 ? (v[j] > 0.f && rne16(v[j]) != 0u) : v[j] > 0.f;
+    b |= (uint32_t)p << j;
+  }
+  return b;
+}
+
+template <typename T, bool RELU, bool RES, bool MOUT = false>
 __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ z,
                                                          const float* __restrict__ ss,
                                                          const float* __restrict__ mean, T* __restrict__ y,
-                                                         long nvec, int C) {
+                                                         long nvec, int C, uint8_t* __restrict__ mo) {
   const int tpr = C >> 3;
   const long i0 = (long)blockIdx.x * BN_NT + threadIdx.x, stride = (long)gridDim.x * BN_NT;
   const int cv = (int)(i0 % tpr);
@@ -204,6 +241,7 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
         a[u][j] = RELU ? fmaxf(v, 0.f) : v;
       }
       V8<T>::st(y + (i + u * stride) * 8, a[u]);
+      if (MOUT) mo[i + u * stride] = (uint8_t)pos_bits<T>(a[u]);
     }
   }
   for (; i < nvec; i += stride) {
@@ -217,11 +255,13 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_kernel(const T* __restrict__ x
       a[j] = RELU ? fmaxf(v, 0.f) : v;
     }
     V8<T>::st(y + i * 8, a);
+    if (MOUT) mo[i] = (uint8_t)pos_bits<T>(a);
   }
 }
 
 // ReLU mask of the backward: MASK 0 = no ReLU, 1 = recompute (x-mean)*scale+beta > 0 (bitwise
-// the forward's value), 2 = y > 0 (a residual was added before the ReLU).
+// the forward's value), 2 = y > 0 (a residual was added before the ReLU), 3 = the same mask
+// from the forward's bit image (one byte per 8-channel vector, passed in place of y).
 // ADD2: the output has two consumers whose gradients arrive separately (a bottleneck's output
 // feeds the next block's conv1 AND, as the identity, its residual add): g = dy + dy2, summed
 // in fp32 here instead of by an extra elementwise pass over the activation.
@@ -245,6 +285,10 @@ __device__ __forceinline__ void masked_grad(const T* dy, const T* dy2, const T* 
     V8<T>::ld(y + e, yv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+  } else if (MASK == 3) {
+    const uint32_t bits = reinterpret_cast<const uint8_t*>(y)[e >> 3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = (bits >> j) & 1u ? g[j] : 0.f;
   }
 }
 
@@ -306,8 +350,24 @@ __global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_kernel(const float* __
   __shared__ float s_a[FIN_G][FIN_CH], s_b[FIN_G][FIN_CH];
   const int pg = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH, c = blockIdx.x * FIN_CH + cl;
   float a = 0.f, b = 0.f;
+#if !PTO_BN_FIN_BATCH
   if (c < C)
     for (int g = pg; g < G; g += FIN_G) { a += part[(size_t)g * 2 * C + c]; b += part[(size_t)g * 2 * C + C + c]; }
+#else
+  {
+    float pa[FIN_IT], pb[FIN_IT];
+    const int cc = c < C ? c : 0;
+#pragma unroll
+    for (int i = 0; i < FIN_IT; ++i) {
+      const int g = pg + FIN_G * i, gg = g < G ? g : 0;
+      pa[i] = part[(size_t)gg * 2 * C + cc];
+      pb[i] = part[(size_t)gg * 2 * C + C + cc];
+    }
+#pragma unroll
+    for (int i = 0; i < FIN_IT; ++i)
+      if (pg + FIN_G * i < G && c < C) { a += pa[i]; b += pb[i]; }
+  }
+#endif
   s_a[pg][cl] = a; s_b[pg][cl] = b;
   __syncthreads();
   for (int w = FIN_G / 2; w >= 1; w >>= 1) {
@@ -366,7 +426,7 @@ int grid_for(long nvec, int C) {
 template <typename T>
 int fwd_t(const void* x, const void* z, void* y, const float* gamma, const float* beta, float* rm, float* rv,
           long long* nbt, float* mean, float* rstd, float* ss, float* part, long M, int C, int G, int rpb,
-          float momentum, float eps, int relu, hipStream_t s) {
+          float momentum, float eps, int relu, uint8_t* mo, hipStream_t s) {
   const T* xt = static_cast<const T*>(x);
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(G), dim3(BN_NT), 0, s, xt, M, C, rpb, part, part + (size_t)G * 2 * C);
   hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part,
@@ -376,11 +436,13 @@ int fwd_t(const void* x, const void* z, void* y, const float* gamma, const float
   const T* zt = static_cast<const T*>(z);
   T* yt = static_cast<T*>(y);
   if (z != nullptr) {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
+    if (relu && mo != nullptr)
+      hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C, mo);
+    else if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C, mo);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C, mo);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C);
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C, mo);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(gr), dim3(BN_NT), 0, s, xt, zt, ss, mean, yt, nvec, C, mo);
   }
   return (int)hipGetLastError();
 }
@@ -426,7 +488,7 @@ int bwd_t(const void* dy, const void* dy2, const void* x, const void* y, const f
 }
 
 bool shape_ok(long M, int C, int G, int rpb) {
-  if (M <= 0 || C < 8 || C > 2048 || (C & 7) || (BN_NT % (C >> 3)) || G < 1 || rpb < 1) return false;
+  if (M <= 0 || C < 8 || C > 2048 || (C & 7) || (BN_NT % (C >> 3)) || G < 1 || G > FIN_GMAX || rpb < 1) return false;
   const int rpi = BN_NT / (C >> 3);
   return rpb % rpi == 0 && (long)G * rpb >= M && (long)(G - 1) * rpb < M;
 }
@@ -453,22 +515,26 @@ int pto_bn_plan(long M, int C, int* rows_per_block) {
 
 // dtype: 0 fp32, 1 bf16.  part: fp32 workspace of G*(2C+1) floats.  z (residual) may be null;
 // running stats / nbt may be null.  momentum as nn.BatchNorm2d (weight of the new value).
+// mask_out (may be null; residual + ReLU only): M*C/8 bytes, the ReLU mask for mask_mode 3.
 int pto_bn_fwd_train(const void* x, const void* z, void* y, const float* gamma, const float* beta, float* run_mean,
                      float* run_var, long long* nbt, float* mean, float* rstd, float* ss, float* part, long M, int C,
-                     int G, int rows_per_block, float momentum, float eps, int dtype, int relu, void* stream) {
+                     int G, int rows_per_block, float momentum, float eps, int dtype, int relu, void* mask_out,
+                     void* stream) {
   if (!shape_ok(M, C, G, rows_per_block) || !aligned16(x) || !aligned16(z) || !aligned16(y)) return -2;
+  if (mask_out != nullptr && (z == nullptr || !relu)) return -1;
+  uint8_t* mo = static_cast<uint8_t*>(mask_out);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 1)
     return fwd_t<bf16>(x, z, y, gamma, beta, run_mean, run_var, nbt, mean, rstd, ss, part, M, C, G, rows_per_block,
-                       momentum, eps, relu, s);
+                       momentum, eps, relu, mo, s);
   if (dtype == 0)
     return fwd_t<float>(x, z, y, gamma, beta, run_mean, run_var, nbt, mean, rstd, ss, part, M, C, G, rows_per_block,
-                        momentum, eps, relu, s);
+                        momentum, eps, relu, mo, s);
   return -1;
 }
 
 // mask_mode: 0 no ReLU, 1 ReLU (mask recomputed from x), 2 ReLU after a residual add (mask
-// from y).  dz (the residual's gradient = the masked dy) only with mask_mode 2 (may be null).
+// from y), 3 the same from the forward's mask_out bytes (passed as y).  dz (the residual's gradient = the masked dy) only with mask_mode 2 (may be null).
 // dy2 (may be null): a second incoming gradient of the output, summed with dy in-kernel.
 // coef: fp32 workspace of 3C floats.
 int pto_bn_bwd(const void* dy, const void* dy2, const void* x, const void* y, const float* gamma, const float* mean,
@@ -477,16 +543,18 @@ int pto_bn_bwd(const void* dy, const void* dy2, const void* x, const void* y, co
   if (!shape_ok(M, C, G, rows_per_block) || !aligned16(dy) || !aligned16(dy2) || !aligned16(x) || !aligned16(y) ||
       !aligned16(dx) || !aligned16(dz))
     return -2;
-  if (mask_mode == 2 && y == nullptr) return -1;
+  if ((mask_mode == 2 || mask_mode == 3) && y == nullptr) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == 1) {
     if (mask_mode == 0) return bwd_t<bf16, 0>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
     if (mask_mode == 1) return bwd_t<bf16, 1>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
     if (mask_mode == 2) return bwd_t<bf16, 2>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 3) return bwd_t<bf16, 3>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
   } else if (dtype == 0) {
     if (mask_mode == 0) return bwd_t<float, 0>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
     if (mask_mode == 1) return bwd_t<float, 1>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
     if (mask_mode == 2) return bwd_t<float, 2>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
+    if (mask_mode == 3) return bwd_t<float, 3>(dy, dy2, x, y, gamma, mean, rstd, ss, dgamma, dbeta, dx, dz, part, coef, M, C, G, rows_per_block, s);
   }
   return -1;
 }

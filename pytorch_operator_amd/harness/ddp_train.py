@@ -55,6 +55,9 @@ def parse_args(argv=None):
                    help="ResNet: each bottleneck's bn3 backward also sums the next block's residual "
                         "gradient in-kernel (ops/batchnorm.py GradLink) instead of autograd's add pass (1); "
                         "2 also sums a stage's downsample-conv input gradient there (link_tap); 0: off")
+    p.add_argument("--bn-mask", choices=["bits", "output"], default="bits",
+                   help="ResNet: residual+ReLU BN backward masks from a 1-bit forward image, or re-read "
+                        "from the BN output")
     p.add_argument("--pool", choices=["hip", "library"], default="hip",
                    help="ResNet stem max-pool: HIP kernels (1-byte taps, gather backward) or PyTorch's op")
     p.add_argument("--conv1x1", choices=["gemm", "library"], default="library",
@@ -113,7 +116,9 @@ def build(args, device, world: int = 1):
         from ..models.resnet import (Bottleneck, resnet50, resnet_tiny, set_bn_impl, set_conv1x1_impl,
                                      set_pool_impl)
         model = set_bn_impl(resnet50() if args.model == "resnet50" else resnet_tiny(), args.bn)
+        from ..ops import batchnorm as _bnm
         from ..ops.batchnorm import BatchNormAct2d
+        _bnm.MASK_BITS = args.bn_mask == "bits"
         for m in model.modules():
             if isinstance(m, BatchNormAct2d) and m.link_output:
                 m.link_output = bool(args.bn_link)
@@ -397,7 +402,7 @@ def main(argv=None) -> int:
         res.update(gemm_tuning_file=out, gemm_tuned_shapes=len(tunable.get_results()))
     if not is_llama:
         res.update(memory_format=args.memory_format, conv_algo_search=args.conv_algo_search, sgd=args.sgd, bn=args.bn, bn_link=args.bn_link,
-                   pool=args.pool,
+                   bn_mask=args.bn_mask, pool=args.pool,
                    conv1x1=args.conv1x1)
     if args.ckpt_dir:
         train_ckpt.save(args.ckpt_dir, gstep, bare, opt, rank, world)

@@ -177,7 +177,7 @@ _SIGNATURES = {
     "pto_adamw_step_scaled": [_VP, _VP, _VP, _VP, _VP, _L, _I, _F, _F, _F, _F, _F, _I, _F, _VP],
     # batchnorm.hip
     "pto_bn_plan": [_L, _I, ctypes.POINTER(_I)],
-    "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP],
+    "pto_bn_fwd_train": [_VP] * 12 + [_L, _I, _I, _I, _F, _F, _I, _I, _VP, _VP],
     "pto_bn_bwd": [_VP] * 14 + [_L, _I, _I, _I, _I, _I, _VP],
     # attention.hip
     "pto_attn_fwd": [_VP] * 5 + [_I] * 5 + [_F, _I, _VP],

@@ -36,6 +36,7 @@ import torch.nn.functional as F
 from . import _native
 
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+MASK_BITS = True  # residual+ReLU backward masks from the forward's bit image (False: re-read y)
 
 
 def _stream(t: torch.Tensor):
@@ -95,17 +96,22 @@ class _BNAct(torch.autograd.Function):
         f32 = dict(device=x.device, dtype=torch.float32)
         part = torch.empty(G * (2 * C + 1), **f32)
         stats = torch.empty(4 * C, **f32)  # mean | rstd | scale | shift
+        ctx.mask = 0 if not relu else (2 if residual is not None else 1)
+        # ReLU after a residual add: the backward's mask comes from a 1-bit image written here
+        # (M*C/8 bytes) instead of re-reading y in both backward passes
+        bits = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if ctx.mask == 2 and MASK_BITS else None
         _native.check(lib.pto_bn_fwd_train(
             xc.data_ptr(), _ptr(z), y.data_ptr(), weight.data_ptr(), bias.data_ptr(), _ptr(running_mean),
             _ptr(running_var), _ptr(nbt), stats.data_ptr(), stats[C:].data_ptr(), stats[2 * C:].data_ptr(),
-            part.data_ptr(), M, C, G, rpb, float(momentum), float(eps), _DT[x.dtype], int(relu), _stream(x)),
-            "bn_fwd_train")
-        ctx.mask = 0 if not relu else (2 if residual is not None else 1)
+            part.data_ptr(), M, C, G, rpb, float(momentum), float(eps), _DT[x.dtype], int(relu), _ptr(bits),
+            _stream(x)), "bn_fwd_train")
+        if bits is not None:
+            ctx.mask = 3
         ctx.has_res = residual is not None
         ctx.res_dtype = residual.dtype if residual is not None else None
         ctx.plan = (M, C, G, rpb)
         ctx.res_link, ctx.out_link = res_link, out_link
-        ctx.save_for_backward(xc, y if ctx.mask == 2 else None, weight, stats)
+        ctx.save_for_backward(xc, y if ctx.mask == 2 else bits, weight, stats)
         return y
 
     @staticmethod

@@ -236,3 +236,30 @@ def test_downsample_tap_gradient_summed_in_bn_backward_matches_fp64(dtype):
             # bf16 rounding of y1, both conv outputs and the gradients: ~3 % vs fp64 on this
             # chain either way; the fused fp32 sum must be no less accurate than autograd's
             assert ea < 5e-2 and ea <= 1.05 * eu + 1e-4, (name, ea, eu)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
+def test_relu_mask_bits_match_the_output_mask_bitwise(dtype, monkeypatch):
+    """Residual + ReLU: the backward's mask from the forward's 1-bit image (mask mode 3) gives
+    bitwise the gradients of the mask re-read from y (mode 2), including values that round to
+    zero in bf16."""
+    from pytorch_operator_amd.ops import batchnorm as bnm
+    g = torch.Generator().manual_seed(3)
+    N, C, H, W = 4, 64, 9, 7
+    x = torch.randn(N, C, H, W, generator=g).to(dtype)
+    z = torch.randn(N, C, H, W, generator=g).to(dtype)
+    z[:, :, 0, 0] = 0.0
+    w, b = 0.5 + torch.rand(C, generator=g), 0.2 * torch.randn(C, generator=g)
+    dy = torch.randn(N, C, H, W, generator=g).to(dtype)
+    cl = dict(memory_format=torch.channels_last)
+    outs = []
+    for bits in (True, False):
+        monkeypatch.setattr(bnm, "MASK_BITS", bits)
+        xg = x.cuda().contiguous(**cl).requires_grad_(True)
+        zg = z.cuda().contiguous(**cl).requires_grad_(True)
+        p = [t.cuda().requires_grad_(True) for t in (w, b)]
+        y = bnm.batch_norm_act(xg, p[0], p[1], relu=True, residual=zg, impl="hip")
+        y.backward(dy.cuda().contiguous(**cl))
+        outs.append([y.detach(), xg.grad, zg.grad, p[0].grad, p[1].grad])
+    for a, r in zip(*outs):
+        assert torch.equal(a, r)
