@@ -292,13 +292,28 @@ __device__ __forceinline__ void masked_grad(const T* dy, const T* dy2, const T* 
   }
 }
 
-// ---- backward 1: per-block sums of g and g * (x - mean) per channel
-template <typename T, int MASK, bool ADD2>
+#ifndef PTO_BN_GOUT
+#define PTO_BN_GOUT 1  // residual BNs: the reduce pass writes g (= dz), the dx pass reads it back
+#endif
+
+// g as the activation dtype stores it (bf16: round to nearest even)
+template <typename T>
+__device__ __forceinline__ void round_t(float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(rne16(v[j]) << 16);
+  }
+}
+
+// ---- backward 1: per-block sums of g and g * (x - mean) per channel.  GOUT (residual BNs,
+// whose masked g is also the residual's gradient dz): g is rounded to T, summed as rounded and
+// stored to gout, so the dx pass reads that one tensor instead of dy [+ dy2] and the mask again
+template <typename T, int MASK, bool ADD2, bool GOUT = false>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                               const T* __restrict__ x,
                                                               const T* __restrict__ y, const float* __restrict__ ss,
                                                               const float* __restrict__ mean, long M, int C, int rpb,
-                                                              float* __restrict__ part) {
+                                                              float* __restrict__ part, T* __restrict__ gout) {
   __shared__ float s_a[BN_NT * 8], s_b[BN_NT * 8];
   const int tpr = C >> 3, rpi = BN_NT / tpr, tid = threadIdx.x;
   const int slot = tid / tpr, cv = tid - slot * tpr;
@@ -315,6 +330,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       masked_grad<T, MASK, ADD2>(dy, dy2, x, y, (r + u * rpi) * C + cv * 8, sc, sh, mu, g[u], xv[u]);
+    if (GOUT) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        round_t<T>(g[u]);
+        V8<T>::st(gout + (r + u * rpi) * C + cv * 8, g[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -323,6 +345,10 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_kernel(const T* __restric
   for (; r < r1; r += rpi) {
     float g[8], xv[8];
     masked_grad<T, MASK, ADD2>(dy, dy2, x, y, r * C + cv * 8, sc, sh, mu, g, xv);
+    if (GOUT) {
+      round_t<T>(g);
+      V8<T>::st(gout + r * C + cv * 8, g);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) { a[j] += g[j]; b[j] = fmaf(g[j], xv[j] - mu[j], b[j]); }
   }
@@ -415,6 +441,46 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_kernel(const T* __restrict__ 
   }
 }
 
+// ---- backward 3, GOUT form: dx = ca*g + cb*(x - mean) + cc from the reduce pass's stored g
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_dxg_kernel(const T* __restrict__ g_in, const T* __restrict__ x,
+                                                           const float* __restrict__ coef,
+                                                           const float* __restrict__ mean, T* __restrict__ dx,
+                                                           long nvec, int C) {
+  const int tpr = C >> 3;
+  const long i0 = (long)blockIdx.x * BN_NT + threadIdx.x, stride = (long)gridDim.x * BN_NT;
+  const int cv = (int)(i0 % tpr);
+  float ca[8], cb[8], cc[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ch = cv * 8 + j;
+    ca[j] = coef[ch]; cb[j] = coef[C + ch]; cc[j] = coef[2 * C + ch]; mu[j] = mean[ch];
+  }
+  long i = i0;
+  for (; i + stride < nvec; i += 2 * stride) {  // two vectors in flight per thread
+    float g[2][8], xv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      V8<T>::ld(g_in + (i + u * stride) * 8, g[u]);
+      V8<T>::ld(x + (i + u * stride) * 8, xv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[u][j] = fmaf(ca[j], g[u][j], fmaf(cb[j], xv[u][j] - mu[j], cc[j]));
+      V8<T>::st(dx + (i + u * stride) * 8, xv[u]);
+    }
+  }
+  for (; i < nvec; i += stride) {
+    float g[8], xv[8];
+    V8<T>::ld(g_in + i * 8, g);
+    V8<T>::ld(x + i * 8, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = fmaf(ca[j], g[j], fmaf(cb[j], xv[j] - mu[j], cc[j]));
+    V8<T>::st(dx + i * 8, xv);
+  }
+}
+
 int grid_for(long nvec, int C) {
   // ~8 vectors per thread, at most 8 blocks per CU worth; a multiple of nothing in particular:
   // BN_NT is a multiple of C/8, so any grid keeps each thread on one channel group
@@ -463,12 +529,22 @@ template <typename T, int MASK, bool ADD2>
 int bwd_t2(const T* dyt, const T* dy2t, const T* xt, const T* yt, const float* gamma, const float* mean,
            const float* rstd, const float* ss, float* dgamma, float* dbeta, void* dx, void* dz, float* part,
            float* coef, long M, int C, int G, int rpb, hipStream_t s) {
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(G), dim3(BN_NT), 0, s, dyt, dy2t, xt, yt, ss, mean,
-                     M, C, rpb, part);
+  T* dzt = static_cast<T*>(dz);
+  const bool gout = PTO_BN_GOUT && dz != nullptr;
+  if (gout)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2, true>), dim3(G), dim3(BN_NT), 0, s, dyt, dy2t, xt, yt, ss,
+                       mean, M, C, rpb, part, dzt);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(G), dim3(BN_NT), 0, s, dyt, dy2t, xt, yt, ss, mean,
+                       M, C, rpb, part, dzt);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_NT), 0, s, part, G, C, M, gamma,
                      mean, rstd, dgamma, dbeta, coef);
-  bwd_dx_launch<T, MASK, ADD2>(dyt, dy2t, xt, yt, ss, coef, mean, static_cast<T*>(dx), static_cast<T*>(dz),
-                               M * (long)C / 8, C, s);
+  const long nvec = M * (long)C / 8;
+  if (gout)
+    hipLaunchKernelGGL(bn_bwd_dxg_kernel<T>, dim3(grid_for(nvec, C)), dim3(BN_NT), 0, s, dzt, xt, coef, mean,
+                       static_cast<T*>(dx), nvec, C);
+  else
+    bwd_dx_launch<T, MASK, ADD2>(dyt, dy2t, xt, yt, ss, coef, mean, static_cast<T*>(dx), dzt, nvec, C, s);
   return (int)hipGetLastError();
 }
 
