@@ -39,3 +39,20 @@ def test_resnet_tiny_gemm_and_library_conv1x1_agree():
     torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_link_tap_routes_the_gradient_to_the_link():
+    """link_tap: with an unclaimed link the second consumer's gradient lands in link.dz (for the
+    producer's backward) instead of autograd; without one it is the identity."""
+    from pytorch_operator_amd.ops.batchnorm import GradLink, link_tap
+    x = torch.randn(2, 3, requires_grad=True)
+    y = x * 1.0
+    assert link_tap(y) is y  # no link: autograd path
+    y._pto_link = GradLink()
+    t = link_tap(y)
+    assert t is not y and y._pto_link.claimed
+    assert link_tap(y) is y  # claimed once only
+    g = torch.randn(2, 3)
+    (t * g).sum().backward()
+    torch.testing.assert_close(y._pto_link.dz, g)
+    assert x.grad is None or float(x.grad.abs().sum()) == 0.0
