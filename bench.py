@@ -56,18 +56,10 @@ def parse_args(argv=None):
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per hipGraph replay (world 1 only; 0 = auto)")
     p.add_argument("--dataset-size", type=int, default=60000)
-    p.add_argument("--overlap", type=int, default=0, help="side-stream overlap in the step (1/0)")
     p.add_argument("--fuse-conv12", type=int, default=1)
-    p.add_argument("--schedule", choices=["fused", "classic"], default="classic",
-                   help="single-GPU launch schedule (A/B): 5-launch fused or 6-launch classic")
     p.add_argument("--conv-chunk", type=int, default=4, choices=[1, 4],
                    help="conv backward: dW_conv2 per 4-sample chunk (slab 4x smaller) or per sample")
-    p.add_argument("--fc-sgd", default="tail", choices=["fused", "tail", "next"],
-                   help="fc parameters' SGD inside fc1_bwd's weight-gradient tiles, in the tail launch, "
-                        "or deferred into extra blocks of the next step's conv12 launch")
     p.add_argument("--stage", type=int, default=1, help="stage the next batch during fc1_bwd (1/0)")
-    p.add_argument("--store-fc-grads", type=int, default=1,
-                   help="fused fc SGD: also store the fc gradients (1/0)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "rccl", "gloo"],
                    help="collective backend (gloo only to rehearse the multi-rank path on one GPU)")
     p.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -125,6 +117,8 @@ def job_latency(world: int, rank: int, timeout: float, gpus=None, backend: str =
                            "worker_train_seconds": r.get("worker_train_seconds"),
                            "worker_capture_seconds": r.get("worker_capture_seconds"),
                            "pod_topology": r.get("pod_topology"),
+                           "startup_breakdown": r.get("startup_breakdown"),
+                           "allreduce_trial": r.get("allreduce_trial"),
                            "reference_create_to_running_s": 121.0}}
         except Exception as e:  # noqa: BLE001 -- never lose the throughput line over this
             out = {"create_to_first_step_s": None, "create_to_succeeded_s": None,
@@ -188,11 +182,9 @@ def main(argv=None):
                               log=lambda m: print(m, file=sys.stderr) if rank == 0 else None)
         tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
                                seed=1, grad_sync=sync)
-        tr.overlap = bool(args.overlap)
         tr.fuse_conv12 = bool(args.fuse_conv12)
-        tr.schedule = args.schedule
-        tr.conv_chunk, tr.fc_sgd = args.conv_chunk, args.fc_sgd
-        tr.stage_batches, tr.store_fc_grads = bool(args.stage), bool(args.store_fc_grads)
+        tr.conv_chunk = args.conv_chunk
+        tr.stage_batches = bool(args.stage)
         if world > 1:  # DDP constructor semantics: start from rank 0's parameters
             dist.broadcast(tr.flat_params, 0)
         spg = args.steps_per_graph if args.steps_per_graph > 0 else pick_steps_per_graph(args.steps, args.warmup)
@@ -219,9 +211,8 @@ def main(argv=None):
             runner.run(n)
         steps = args.steps - args.steps % runner.steps_per_graph
         xgmi_error = (lambda: xg.xar.error()) if xg is not None else (lambda: 0)
-        mode_desc = (f"{args.mode}(launch={runner.launch},spg={runner.steps_per_graph},overlap={args.overlap},"
-                     f"allreduce={ar_path},schedule={args.schedule},conv_chunk={args.conv_chunk},"
-                     f"fc_sgd={args.fc_sgd},stage={args.stage},store_fc_grads={args.store_fc_grads})")
+        mode_desc = (f"{args.mode}(launch={runner.launch},spg={runner.steps_per_graph},"
+                     f"allreduce={ar_path},conv_chunk={args.conv_chunk},stage={args.stage})")
     else:
         from pytorch_operator_amd.models.mnist import Net
         import torch.nn.functional as F

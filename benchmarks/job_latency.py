@@ -60,23 +60,38 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
             break
         time.sleep(0.02)
     pods = sorted(p["metadata"]["name"] for p in c.rest.list(PODS, "default", f"pytorch-job-name={name}")["items"])
-    first, done, paths = [], [], set()
+    first, done, paths, startups, trials = [], [], set(), {}, []
     for p in pods:
         for line in c.rest.pod_log(p, "default").splitlines():
             if line.startswith('{"event"'):
                 ev = json.loads(line)
                 if ev["event"] == "first_step":
-                    first.append(ev["unix_ns"])
+                    first.append((ev["unix_ns"], ev.get("rank")))
+                elif ev["event"] == "startup":
+                    startups[ev.get("rank")] = ev
                 elif ev["event"] == "train_done":
                     done.append(ev)
                 elif ev["event"] == "grad_allreduce":
                     paths.add(ev.get("path"))
+                    if ev.get("trial") and ev.get("rank") == 0:
+                        trials.append(ev["trial"])
     s = lambda t: None if t is None else round((t - t_create) / 1e9, 3)  # noqa: E731
     # every rank reports the job-wide aggregate (steps * B * world / t): take rank 0's
     rank0 = [d for d in done if d.get("rank") == 0]
+    # where create -> first step goes, for the rank that reached its first step last: the
+    # control plane + kubelet (job POST -> worker process start), then the worker's phases
+    breakdown = None
+    if first:
+        t_last, r_last = max(first)
+        st = startups.get(r_last)
+        if st:
+            m = st["marks_unix_ns"]
+            breakdown = {"rank": r_last, "job_create_to_process_start_s": s(m.get("process_start")),
+                         **st["phases"]}
     return {"replicas": replicas, "result": final,
             "create_to_running_s": s(t_running),
-            "create_to_first_step_s": s(max(first)) if len(first) == replicas else None,
+            "create_to_first_step_s": s(max(first)[0]) if len(first) == replicas else None,
+            "startup_breakdown": breakdown,
             "create_to_succeeded_s": s(t_done),
             "worker_samples_per_sec": rank0[0].get("samples_per_sec") if rank0 else None,
             # steady state inside the pod: per-step ms of the graphed log blocks (p50/p90/p99),
@@ -85,6 +100,7 @@ def run_one(c: LocalCluster, name: str, replicas: int, args, gpu: bool, timeout:
             "worker_train_seconds": rank0[0].get("train_seconds") if rank0 else None,
             "worker_capture_seconds": rank0[0].get("capture_seconds") if rank0 else None,
             "grad_allreduce": sorted(x for x in paths if x) or None,
+            "allreduce_trial": trials[0] if trials else None,
             "accuracy": rank0[0]["accuracy"] if rank0 else None}
 
 

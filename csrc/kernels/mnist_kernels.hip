@@ -25,38 +25,39 @@
 //                      dW_conv2 (MFMA + VALU rows), col2im + un-pool + ReLU mask ->
 //                      dz1 (LDS), dW_conv1 (VALU), per-sample slab rows
 //   G  slab_reduce_sgd deterministic slab reduction + SGD(momentum) on every parameter
-// (A conv1_fwd_pool, B conv2_fwd_pool, sgd_momentum: the unfused / eval building blocks.)
+// (A conv1_fwd_pool, B conv2_fwd_pool, conv_bwd (per-sample slab rows), sgd_momentum: the
+// unfused / eval / fallback building blocks.)
 //
 // All arithmetic is fp32 (the reference's dtype); matrix work uses the exact-fp32
 // MFMA (one rounding per product, same as an fmaf chain).
 //
 // Every kernel takes an optional `dbg` pointer: when non-null, thread 0 of each
 // block records wall_clock64() (100 MHz) at phase boundaries into
-// dbg[block * 16 + phase] (used by tools/phase_profile.py; null in production).
+// dbg[block * 16 + phase] (tools/phase_profile.py, tools/step_timeline.py; null in
+// production).  Each launch gets its own slot of the debug buffer (dbg_next()).
+//
+// Variants measured slower and removed from this file (round-3 A/B records in
+// profiles/r3_*; source at commit f6f36d4): the 5-launch schedule (fc1_bwd_head, fc tiles in
+// conv_bwd's idle waves, tail_sgd), fc SGD fused into fc1_bwd, fc SGD deferred into the next
+// conv12, fc1 split-K 5, nontemporal hand-off stores, shuffle-butterfly head sums.
 #include <atomic>
 
 #include "pto_common.h"
 
 using namespace pto;
 
-// PTO_ABL (timing ablations for tools/build_exp.sh variants only, never numerically valid):
-// bit 0 tail fc SGD, 1 conv1, 2 conv2, 3 conv_bwd4 phase 2, 4 fc1_bwd job 1, 5 head,
-// 6 conv_bwd4 phases 3-4
-#ifndef PTO_ABL
-#define PTO_ABL 0
+// fc1 split-K factor of the training path: 256 workgroups of 5 waves (K = 800 = 2 x 400)
+constexpr int FC1_KS = 2;
+
+// PTO_WT (A/B, tools/build_exp.sh): write-through (sc1) stores for the bytes a launch hands to a
+// later one -- bit 0: the tail's parameters / momentum / reduced conv grads, bit 1: fc1_bwd's
+// dW_fc1, bit 2: conv_bwd4's chunk slab rows
+#ifndef PTO_WT
+#define PTO_WT 0
 #endif
-// head_kernel's ten logit sums: 1 = DPP / permlane all-reduce (six VALU steps, no LDS; default:
-// -0.3 to -0.5 us/step, profiles/r3_mnist_ab_dpp_ks5.txt), 0 = __shfl_xor butterflies
-// (ds_bpermute round trips)
-#ifndef PTO_HEAD_DPP
-#define PTO_HEAD_DPP 1
-#endif
-// fc1 split-K factor of the training path: 2 (256 workgroups of 5 waves; default) or 5 (640 of 2:
-// +0.5 us/step, profiles/r3_mnist_ab_dpp_ks5.txt)
-#ifndef PTO_FC1_KS
-#define PTO_FC1_KS 2
-#endif
-static_assert(PTO_FC1_KS == 2 || PTO_FC1_KS == 5, "fc1 split-K: K = 800 over 10 waves of 80");
+constexpr bool WT_TAIL = (PTO_WT & 1) != 0;
+constexpr bool WT_FC1 = (PTO_WT & 2) != 0;
+constexpr bool WT_SLAB = (PTO_WT & 4) != 0;
 
 namespace {
 
@@ -64,7 +65,7 @@ typedef unsigned long long u64;
 
 __device__ __forceinline__ void stamp(u64* dbg, int phase) {
   if (dbg != nullptr && threadIdx.x == 0) {
-    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     dbg[blk * 16 + phase] = (u64)wall_clock64();
     dbg[blk * 16 + 8 + phase] = (u64)clock64();  // shader clock -> effective GHz per phase
   }
@@ -210,34 +211,14 @@ __device__ __forceinline__ int from_upper_half(int v) {
   return (int)__builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false)[1];
 }
 
-// PTO_NT (A/B): nontemporal stores for the bytes one launch hands to the next on other XCDs
-// (conv-grad slab, dW_fc1, the tail's parameters/momentum), so they stream out of the
-// writing XCD's L2 during the kernel instead of in the end-of-kernel write-back
-#ifndef PTO_NT
-#define PTO_NT 0
-#endif
-__device__ __forceinline__ void st_h(float* p, float v) {
-  if (PTO_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-__device__ __forceinline__ void st_h4(float4* p, float4 v) {
-  if (PTO_NT) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<f4v*>(p));
-  } else {
-    *p = v;
-  }
-}
-
 struct SgdHyper {
   float lr, momentum, dampening, wd, grad_scale;
   int nesterov, first_step;
 };
 
 // torch.optim.SGD on one element (buf = momentum*buf + (1-dampening)*d, or d on the first step).
-// Explicit fmas: every kernel that inlines this (tail, fc1_bwd, conv12's deferred rows, the
-// flush, xgmi_allreduce.hip's sgd4) rounds identically, whatever the contraction choices.
+// Explicit fmas: every kernel that inlines this (the tail, sgd_momentum, xgmi_allreduce.hip's
+// sgd4) rounds identically, whatever the contraction choices.
 __device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const SgdHyper& hy) {
   float d = __builtin_fmaf(hy.wd, pv, gv * hy.grad_scale);
   if (hy.momentum != 0.f) {
@@ -247,30 +228,11 @@ __device__ __forceinline__ void sgd_elem(float& pv, float& mv, float gv, const S
   pv = __builtin_fmaf(-hy.lr, d, pv);
 }
 
-// A deferred SGD(momentum) over a flat float4 range, run by extra blocks of another launch
-// when *pend != 0 (fc_sgd "next": the fc parameters' update of step t rides in step t+1's
-// conv12 launch, whose blocks leave half of every CU's wave slots and LDS free).
-struct SgdRange {
-  float4* p;
-  const float4* g;
-  float4* m;
-  int n4;
-  const int* pend;
-  SgdHyper hy;
-};
-
-__device__ __forceinline__ void sgd_range_block(const SgdRange& r, int blk, int nthreads) {
-  if (*r.pend == 0) return;
-  const int v = blk * nthreads + (int)threadIdx.x;
-  if (v >= r.n4) return;
-  float4 pp = r.p[v], bb = r.m[v];
-  const float4 gg = r.g[v];
-  sgd_elem(pp.x, bb.x, gg.x, r.hy);
-  sgd_elem(pp.y, bb.y, gg.y, r.hy);
-  sgd_elem(pp.z, bb.z, gg.z, r.hy);
-  sgd_elem(pp.w, bb.w, gg.w, r.hy);
-  r.p[v] = pp;
-  r.m[v] = bb;
+__device__ __forceinline__ void sgd4(float4& p, float4& m, const float4& g, const SgdHyper& hy) {
+  sgd_elem(p.x, m.x, g.x, hy);
+  sgd_elem(p.y, m.y, g.y, hy);
+  sgd_elem(p.z, m.z, g.z, hy);
+  sgd_elem(p.w, m.w, g.w, hy);
 }
 
 constexpr int C2_RS = 16;
@@ -518,17 +480,13 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ a1,
     uint8_t* __restrict__ idx1, float* __restrict__ xn_out, int* __restrict__ lab_out,
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, const uint8_t* __restrict__ stg_x,
-    const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, SgdRange sg, u64* dbg) {
+    const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, u64* dbg) {
   __shared__ float img[28 * AB_IRS];
   __shared__ float w1s[520];
   __shared__ __align__(16) float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  if (b >= B) {  // deferred SGD rows of the grid (dispatched after every conv block)
-    sgd_range_block(sg, (b - B) * gridDim.x + cg, AB_NT);
-    return;
-  }
   stamp(dbg, 0);
   const bool pub = cg == 0;
   // conv2 epilogue bias, loaded with the staging loads (no round trip after the last barrier)
@@ -596,18 +554,16 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
-    if (!(PTO_ABL & 2)) {
     conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
-    }
   }
   __syncthreads();
   stamp(dbg, 2);
 
   const int lane = tid & 63, wv = tid >> 6;
   const int pt = wv & 3, i = lane & 15, g = lane >> 4;
-  f32x4 acc = (PTO_ABL & 4) ? zero4() : conv2_block(in_s, w_s, red, wv, lane);
+  f32x4 acc = conv2_block(in_s, w_s, red, wv, lane);
   stamp(dbg, 3);
   if (wv >= 4) return;
   const int co = cg * 16 + i;
@@ -645,12 +601,12 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
 template <int KS>
 __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-    float* __restrict__ h, int B, int* __restrict__ clr, u64* dbg) {
+    float* __restrict__ h, int B, u64* dbg) {
+  static_assert(KS == 1 || KS == 2, "fc1: 10 or 5 waves of 80 K each");
   constexpr int NW = 10 / KS;
   __shared__ f32x4 red[NW][64];
   const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, tid = threadIdx.x;
   stamp(dbg, 0);
-  if (clr != nullptr && (nt | mt | kz | tid) == 0) *clr = 0;  // conv12 consumed the deferred update
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int row = mt * 16 + i, col = nt * 16 + i;
@@ -681,25 +637,13 @@ __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
   red[wv][lane] = c0 + c1;
   __syncthreads();
   stamp(dbg, 1);
-  if constexpr (640 / KS >= 256) {
-    if (tid < 256) {
-      float s = 0.f;
+  if (tid < 256) {
+    float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
-      if (orow < B && ocol < 500) {
-        if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
-        else h[((size_t)kz * B + orow) * 500 + ocol] = s;
-      }
-    }
-  } else {  // fewer threads than tile outputs (KS = 5: 128): two outputs per thread
-#pragma unroll
-    for (int e = tid; e < 256; e += 640 / KS) {
-      const int le = e >> 2, re = e & 3;
-      const int orw = mt * 16 + (le >> 4) * 4 + re, ocl = nt * 16 + (le & 15);
-      float s = 0.f;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) s += red[q][le][re];
-      if (orw < B && ocl < 500) h[((size_t)kz * B + orw) * 500 + ocl] = s;
+    for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
+    if (orow < B && ocol < 500) {
+      if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
+      else h[((size_t)kz * B + orow) * 500 + ocol] = s;
     }
   }
 }
@@ -730,7 +674,6 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
   const int b = blockIdx.x * WPB + wq;
   const bool bvalid = b < B;
   const int bc = bvalid ? b : B - 1;
-  if (PTO_ABL & 32) return;
   const int t = lab[bc];
   // lane owns k = 8 lane + [0, 8): two float4 per row (h, every W2 row), 22 loads per
   // lane, all in flight at once (lane 62 has half a chunk, lane 63 none)
@@ -742,17 +685,9 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
     float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
     if (hp2 != nullptr) {
-      // partials 1 .. KS-1 of the split-K fc1 follow each other ([KS][B][500]), summed in order
-      float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
-      float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
-#pragma unroll
-      for (int kz = 2; kz < PTO_FC1_KS; ++kz) {
-        const float* hk = hp2 + (size_t)(kz - 1) * B * 500 + (size_t)bc * 500;
-        const float4 r0 = *reinterpret_cast<const float4*>(hk + o0);
-        const float4 r1 = *reinterpret_cast<const float4*>(hk + o1);
-        q0 = make_float4(q0.x + r0.x, q0.y + r0.y, q0.z + r0.z, q0.w + r0.w);
-        q1 = make_float4(q1.x + r1.x, q1.y + r1.y, q1.z + r1.z, q1.w + r1.w);
-      }
+      // the second split-K fc1 partial
+      const float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
+      const float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
       const float4 c0 = *reinterpret_cast<const float4*>(b1 + o0);
       const float4 c1 = *reinterpret_cast<const float4*>(b1 + o1);
       h0 = make_float4(fmaxf(h0.x + q0.x + c0.x, 0.f), fmaxf(h0.y + q0.y + c0.y, 0.f),
@@ -787,16 +722,10 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     for (int q = 0; q < 8; ++q) p = fmaf(hv[q], wv[j][q], p);
     logit[j] = p;
   }
-  if (PTO_HEAD_DPP) {
+  // DPP / permlane all-reduce: six VALU steps per sum, no LDS round trips (-0.3 to -0.5 us/step
+  // against __shfl_xor butterflies, profiles/r3_mnist_ab_dpp_ks5.txt)
 #pragma unroll
-    for (int j = 0; j < 10; ++j) logit[j] = wave_allsum_dpp(logit[j]);
-  } else {
-    // 10 independent butterfly reductions, interleaved
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < 10; ++j) logit[j] += __shfl_xor(logit[j], o, 64);
-  }
+  for (int j = 0; j < 10; ++j) logit[j] = wave_allsum_dpp(logit[j]);
 #pragma unroll
   for (int j = 0; j < 10; ++j) logit[j] += b2[j];
   float m = logit[0];
@@ -892,17 +821,11 @@ struct Fc1Bwd {
   const float *dh, *a2;
   const uint8_t* idx2;
   const float *w1, *dlog, *h;
-  float *gw1, *gb1, *gw2, *gb2, *dz2;  // gw1 / gw2 may be null with sgd (not stored)
+  float *gw1, *gb1, *gw2, *gb2, *dz2;
   const float* per_sample;
   float* stats;
   float loss_scale;
   int jobs, B;
-  // fused SGD (sgd != 0): job 1 writes the UPDATED fc1.weight to w1_next -- job 2 of this
-  // launch still reads w1 -- and updates m_w1 / fc1.bias / m_b1 in place; job 3 updates
-  // fc2.weight / fc2.bias (+ momentum) in place (nothing in this launch reads them)
-  int sgd;
-  SgdHyper hy;
-  float *w1_next, *m_w1, *p_b1, *m_b1, *p_w2, *m_w2, *p_b2, *m_b2;
   // next-batch staging (stage_x != null): ceil(B/4) extra blocks copy the uint8 pixels and
   // labels of the batch of step cursor + stage_adv into stage_x / stage_lab and write that
   // step number to stage_tag (conv12_fwd uses the staged batch when its tag matches)
@@ -927,24 +850,11 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   const int blk = blockIdx.x;
   stamp(dbg, 0);
   if (blk < nJ1) {
-    if (PTO_ABL & 16) return;
     const int tile = blk * E_NW + wv;
     const int nt = tile / 50, kt = tile - nt * 50;
     const int n = nt * 16 + i, f = kt * 16 + i;
     const bool nv = n < 500;
     const int nc = nv ? n : 499;
-    // SGD operands of the tile (rows nt*16 + 4g + q, column f) and of the bias (kt == 0),
-    // in flight with the GEMM loads
-    float pw[4], mw[4], pb = 0.f, mb = 0.f;
-    if (a.sgd) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const size_t e = (size_t)min(nt * 16 + g * 4 + q, 499) * 800 + f;
-        pw[q] = a.w1[e];
-        mw[q] = a.m_w1[e];
-      }
-      if (kt == 0) { pb = a.p_b1[nc]; mb = a.m_b1[nc]; }
-    }
     f32x4 c0 = zero4(), c1 = zero4();
     float dbsum = 0.f;
     for (int base = 0; base < B; base += 64) {
@@ -961,34 +871,20 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
         const float x = (bv && nv) ? av[s] : 0.f;
         dbsum += x;
         const float fb = bv ? fv[s] : 0.f;
-        if (s & 1) c1 = mfma16x16x4(x, fb, c1);
-        else c0 = mfma16x16x4(x, fb, c0);
+        // transposed tile (A = a2 columns, B = dh columns): lane (i, g) ends with
+        // dW_fc1[n = 16 nt + i][16 kt + 4 g + r], four consecutive columns -> one 16-B store
+        if (s & 1) c1 = mfma16x16x4(fb, x, c1);
+        else c0 = mfma16x16x4(fb, x, c0);
       }
     }
     const f32x4 c = c0 + c1;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int nn = nt * 16 + g * 4 + r;
-      if (nn < 500) {
-        const size_t e = (size_t)nn * 800 + kt * 16 + i;
-        if (a.gw1 != nullptr) st_h(a.gw1 + e, c[r]);
-        if (a.sgd) {
-          sgd_elem(pw[r], mw[r], c[r], a.hy);
-          a.w1_next[e] = pw[r];
-          a.m_w1[e] = mw[r];
-        }
-      }
+    if (nv) {
+      const unsigned e4 = (unsigned)(n * 200 + kt * 4 + g);  // float4 index of (n, 16 kt + 4 g)
+      st4<WT_FC1>(reinterpret_cast<float4*>(a.gw1), e4, make_float4(c[0], c[1], c[2], c[3]));
     }
     if (kt == 0) {
       dbsum = sum_lane_rows(dbsum);
-      if (g == 0 && nv) {
-        if (a.gb1 != nullptr) a.gb1[n] = dbsum;
-        if (a.sgd) {
-          sgd_elem(pb, mb, dbsum, a.hy);
-          a.p_b1[n] = pb;
-          a.m_b1[n] = mb;
-        }
-      }
+      if (g == 0 && nv) a.gb1[n] = dbsum;
     }
   } else if (blk < nJ1 + nJ2) {
     const int t2 = blk - nJ1;
@@ -1052,16 +948,6 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     const bool do_stats = nt == 1 && a.per_sample != nullptr && a.stats != nullptr;
     float ls = 0.f, cs = 0.f;
     if (do_stats && lane < B) { ls = a.per_sample[2 * lane]; cs = a.per_sample[2 * lane + 1]; }
-    float pw[4], mw[4], pb = 0.f, mb = 0.f;
-    if (a.sgd) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = min(g * 4 + q, 9);
-        pw[q] = a.p_w2[j * 500 + ncl];
-        mw[q] = a.m_w2[j * 500 + ncl];
-      }
-      if (nt == 0) { pb = a.p_b2[jc]; mb = a.m_b2[jc]; }
-    }
     f32x4 c0 = zero4(), c1 = zero4();
     float dbsum = 0.f;
     for (int base = 0; base < B; base += 64) {
@@ -1087,26 +973,12 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = g * 4 + r;
-        if (j < 10) {
-          if (a.gw2 != nullptr) a.gw2[j * 500 + n] = c[r];
-          if (a.sgd) {
-            sgd_elem(pw[r], mw[r], c[r], a.hy);
-            a.p_w2[j * 500 + n] = pw[r];
-            a.m_w2[j * 500 + n] = mw[r];
-          }
-        }
+        if (j < 10) a.gw2[j * 500 + n] = c[r];
       }
     }
     if (nt == 0) {
       dbsum = sum_lane_rows(dbsum);
-      if (g == 0 && i < 10) {
-        if (a.gb2 != nullptr) a.gb2[i] = dbsum;
-        if (a.sgd) {
-          sgd_elem(pb, mb, dbsum, a.hy);
-          a.p_b2[i] = pb;
-          a.m_b2[i] = mb;
-        }
-      }
+      if (g == 0 && i < 10) a.gb2[i] = dbsum;
     }
     if (do_stats) {
       for (int bb = lane + 64; bb < B; bb += 64) { ls += a.per_sample[2 * bb]; cs += a.per_sample[2 * bb + 1]; }
@@ -1130,429 +1002,6 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     if (j4 == 0 && tid == 0) a.stage_tag[0] = (int)step;
   }
   stamp(dbg, 1);
-}
-
-// ---------------------------------------------------------------------------
-// E': fc1 input gradient with the head folded in (the training path).
-//   grid = ceil(B/16) * 50 blocks of 512 threads; block (mt, kt) owns samples
-//   mt*16 .. +16 and pooled features kt*16 .. +16 of dz2.  Every block first rebuilds
-//   the head for its 16 samples -- h = relu(part0 + part1 + b1), logits = h W2^T + b2
-//   (MFMA, K split over the 8 waves), log-softmax / NLL / d(logits) (one wave),
-//   dh = (d(logits) W2) * (h > 0) (MFMA) -- in LDS, then runs the dz2 GEMM of the old
-//   job 2 with dh read from LDS.  The 50 kt-blocks of a sample tile recompute the same
-//   head (bit-identical: same code, same order); the kt == 0 block publishes h, dh,
-//   d(logits) and the per-sample (loss, correct) for the weight-gradient jobs.
-//   Recomputing costs ~1 us of MFMA + 84 KB of L2 reads per block and removes the head
-//   launch (a kernel boundary + its own memory round trip, ~5 us on the step's critical
-//   path).  Block -> (mt, kt) = (blk % MT, blk / MT): with MT = 4 the 8 XCDs
-//   (round-robin block placement) each see one sample tile, so its h rows and W2 are
-//   fetched into that XCD's L2 once.
-// ---------------------------------------------------------------------------
-constexpr int H_NT = 512;
-constexpr int H_NW = H_NT / 64;
-constexpr int H_HS = 514;  // h_s / dh_s row stride (== 2 mod 32: lanes (i, g) -> bank 2i + g)
-constexpr int H_WS = 530;  // w2_s row stride (== 18 mod 32: conflict-free row and column reads)
-constexpr int H_DS = 17;   // dl_s row stride
-
-__global__ __launch_bounds__(H_NT) void fc1_bwd_head_kernel(
-    const float* __restrict__ hp, const float* __restrict__ b1, const float* __restrict__ w2,
-    const float* __restrict__ b2, const int* __restrict__ lab, const float* __restrict__ a2,
-    const uint8_t* __restrict__ idx2, const float* __restrict__ w1, float grad_scale,
-    float* __restrict__ dz2, float* __restrict__ h_out, float* __restrict__ dh_out,
-    float* __restrict__ dlogits, float* __restrict__ per_sample, int B, u64* dbg) {
-  __shared__ float h_s[16 * H_HS];  // h, overwritten in place by dh
-  __shared__ float w2_s[10 * H_WS];
-  __shared__ f32x4 red[H_NW][64];
-  __shared__ float dl_s[16 * H_DS];
-  __shared__ float lg_s[16 * H_DS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int MT = (B + 15) >> 4;
-  const int mt = blockIdx.x % MT, kt = blockIdx.x / MT;
-  const bool pub = kt == 0;
-  stamp(dbg, 0);
-
-  // ---- every global load of the block, issued before the first use
-  // (a) dz2 GEMM B operand: W1[k][f], k = 64 wv + 4 s + g (rows >= 500 clamped, their A is 0)
-  const int f = kt * 16 + i;
-  float bv[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) bv[s] = w1[(size_t)min(64 * wv + 4 * s + g, 499) * 800 + f];
-  // (b) epilogue operands of threads < 256 (ReLU mask + pool argmax)
-  const int l = (tid & 255) >> 2, r = tid & 3;
-  const int bs = mt * 16 + (l >> 4) * 4 + r;
-  const int ff = kt * 16 + (l & 15);
-  const size_t o = (size_t)min(bs, B - 1) * 800 + ff;
-  float a2o = a2[o];
-  int p = idx2[o];
-  // (c) the two split-K halves of the tile's 16 h rows + b1 (16 x 125 float4 each)
-  const float4* hp4 = reinterpret_cast<const float4*>(hp);
-  const float4* b14 = reinterpret_cast<const float4*>(b1);
-  float4 h0[4], h1[4], bb[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int e = min(tid + k * H_NT, 1999);
-    const int row = e / 125, c4 = e - row * 125;
-    const int rr = min(mt * 16 + row, B - 1);
-    h0[k] = hp4[(size_t)rr * 125 + c4];
-    h1[k] = hp4[(size_t)(B + rr) * 125 + c4];
-    bb[k] = b14[c4];
-  }
-  // (d) W2 (10 x 125 float4)
-  const float4* w24 = reinterpret_cast<const float4*>(w2);
-  float4 wq[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) wq[k] = w24[min(tid + k * H_NT, 1249)];
-  // (e) logits epilogue: b2 of this thread's class (tid & 15); softmax threads: their label
-  const float b2v = b2[min(tid & 15, 9)];
-  const int tlab = lab[min(mt * 16 + (tid & 15), B - 1)];
-
-  // ---- h = relu(part0 + part1 + b1) -> LDS (published by the kt == 0 block); W2 -> LDS
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int e = tid + k * H_NT;
-    if (e < 2000) {
-      const int row = e / 125, c4 = e - row * 125;
-      const float4 hv = make_float4(fmaxf(h0[k].x + h1[k].x + bb[k].x, 0.f), fmaxf(h0[k].y + h1[k].y + bb[k].y, 0.f),
-                                    fmaxf(h0[k].z + h1[k].z + bb[k].z, 0.f), fmaxf(h0[k].w + h1[k].w + bb[k].w, 0.f));
-      float2* d = reinterpret_cast<float2*>(h_s + row * H_HS + 4 * c4);
-      d[0] = make_float2(hv.x, hv.y);
-      d[1] = make_float2(hv.z, hv.w);
-      if (pub && mt * 16 + row < B) reinterpret_cast<float4*>(h_out)[(size_t)(mt * 16 + row) * 125 + c4] = hv;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int e = tid + k * H_NT;
-    if (e < 1250) {
-      const int j = e / 125, c4 = e - j * 125;
-      float2* d = reinterpret_cast<float2*>(w2_s + j * H_WS + 4 * c4);
-      d[0] = make_float2(wq[k].x, wq[k].y);
-      d[1] = make_float2(wq[k].z, wq[k].w);
-    }
-  }
-  __syncthreads();
-  stamp(dbg, 1);
-
-  // ---- logits partials: M = 16 samples, N = 16 (10 classes), K = 500 in 125 steps, wave w
-  // takes steps w, w + 8, ...; A = h_s[i][4s + g], B = W2[i][4s + g] (0 for i >= 10); four
-  // independent accumulator chains hide the MFMA dependency latency
-  {
-    const int jr = min(i, 9);
-    const int nst = wv < 5 ? 16 : 15;  // 125 = 15 * 8 + 5
-    float av[16], wb[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int s = min(wv + 8 * q, 124);
-      av[q] = h_s[i * H_HS + 4 * s + g];
-      wb[q] = w2_s[jr * H_WS + 4 * s + g];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 c[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float a = q < nst ? av[q] : 0.f;
-      const float bq = i < 10 ? wb[q] : 0.f;
-      c[q & 3] = mfma16x16x4(a, bq, c[q & 3]);
-    }
-    red[wv][lane] = (c[0] + c[1]) + (c[2] + c[3]);
-  }
-  __syncthreads();
-  // ---- logits = sum of the 8 wave partials + b2 -> LDS (thread t: sample t >> 4, class t & 15)
-  if (tid < 256) {
-    const int row = tid >> 4, j = tid & 15;
-    const int src = (row >> 2) * 16 + j, rr = row & 3;  // C[row][j] = lane (j, row >> 2), reg row & 3
-    float x = red[0][src][rr];
-#pragma unroll
-    for (int q = 1; q < H_NW; ++q) x += red[q][src][rr];
-    lg_s[row * H_DS + j] = x + b2v;
-  }
-  __syncthreads();
-  // ---- log-softmax / NLL / d(logits): one thread per sample, no cross-lane traffic
-  if (tid < 16) {
-    const int row = tid;
-    float x[10];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) x[j] = lg_s[row * H_DS + j];
-    float m = x[0];
-    int pred = 0;
-#pragma unroll
-    for (int j = 1; j < 10; ++j)
-      if (x[j] > m) { m = x[j]; pred = j; }  // first maximum, as torch's argmax
-    float se = 0.f;
-#pragma unroll
-    for (int j = 0; j < 10; ++j) se += __expf(x[j] - m);
-    const float lse = m + __logf(se);
-    const int t = tlab;
-    float lt = 0.f;
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      if (j == t) lt = x[j];
-    const int sample = mt * 16 + row;
-    const bool out = pub && sample < B;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float dl = j < 10 ? (__expf(x[j < 10 ? j : 0] - lse) - (j == t ? 1.f : 0.f)) * grad_scale : 0.f;
-      dl_s[row * H_DS + j] = dl;
-      if (out && j < 10) dlogits[(size_t)sample * 10 + j] = dl;
-    }
-    if (out) {
-      per_sample[2 * sample] = lse - lt;
-      per_sample[2 * sample + 1] = pred == t ? 1.f : 0.f;
-    }
-  }
-  __syncthreads();
-  stamp(dbg, 2);
-  // ---- dh = (d(logits) W2) * (h > 0): M = 16 samples, N = 500 (32 tiles, 4 per wave),
-  // K = 10 classes (3 steps of 4); every LDS operand of the wave's 4 tiles first, then the
-  // 4 tiles' MFMAs interleaved; written over h in place (each element has one owner)
-  {
-    float a3[3], b3[4][3], hq[4][4];
-#pragma unroll
-    for (int s = 0; s < 3; ++s) a3[s] = 4 * s + g < 10 ? dl_s[i * H_DS + 4 * s + g] : 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int kc = min((wv * 4 + u) * 16 + i, 499);
-#pragma unroll
-      for (int s = 0; s < 3; ++s) b3[u][s] = w2_s[min(4 * s + g, 9) * H_WS + kc];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) hq[u][q] = h_s[(g * 4 + q) * H_HS + kc];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int kk = (wv * 4 + u) * 16 + i;
-        const float bq = (4 * s + g < 10 && kk < 500) ? b3[u][s] : 0.f;
-        acc[u] = mfma16x16x4(a3[s], bq, acc[u]);
-      }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int kk = (wv * 4 + u) * 16 + i;
-      if (kk < 500) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int srow = g * 4 + q;
-          const float v = hq[u][q] > 0.f ? acc[u][q] : 0.f;
-          h_s[srow * H_HS + kk] = v;
-          if (pub && mt * 16 + srow < B) dh_out[(size_t)(mt * 16 + srow) * 500 + kk] = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  stamp(dbg, 3);
-  // ---- dz2 GEMM: da2[16 samples, 16 features] = dh . W1[:, f]  (K = 500 over 8 waves)
-  {
-    float av[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) av[s] = h_s[i * H_HS + min(64 * wv + 4 * s + g, 499)];
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 c[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float a = 64 * wv + 4 * s + g < 500 ? av[s] : 0.f;
-      c[s & 3] = mfma16x16x4(a, bv[s], c[s & 3]);
-    }
-    asm volatile("" : "+v"(a2o), "+v"(p));
-    red[wv][lane] = (c[0] + c[1]) + (c[2] + c[3]);
-  }
-  __syncthreads();
-  float v = red[0][l][r];
-#pragma unroll
-  for (int q = 1; q < H_NW; ++q) v += red[q][l][r];
-  if (tid < 256 && bs < B) {
-    const float d = a2o > 0.f ? v : 0.f;
-    const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
-    float* z = dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
-    z[0] = p == 0 ? d : 0.f;
-    z[1] = p == 1 ? d : 0.f;
-    z[8] = p == 2 ? d : 0.f;
-    z[9] = p == 3 ? d : 0.f;
-  }
-  stamp(dbg, 4);
-}
-
-// ---------------------------------------------------------------------------
-// SGD element update + the fc weight-gradient tiles.  The tiles only depend on the
-// head's outputs (dh, d(logits), h) and a2, so they run in waves of whatever launch has
-// idle ones: conv_bwd's waves 9-15 sit out its col2im / dW_conv1 phases (no MFMA work
-// there), which covers all 1632 tiles at B = 64 (<= 7 per block).  Optionally the SGD of
-// each element is applied in the tile's epilogue (single process: the fc gradients never
-// make an HBM round trip before their update; they are still stored for inspection).
-// ---------------------------------------------------------------------------
-struct FcTail {
-  const float *dh, *a2, *dlog, *h, *per_sample;
-  float *p_w1, *m_w1, *g_w1, *p_b1, *m_b1, *g_b1;
-  float *p_w2, *m_w2, *g_w2, *p_b2, *m_b2, *g_b2;
-  float* stats;
-  float loss_scale;
-};
-
-constexpr int FC_NT1 = 1600;  // dW_fc1 tiles: 32 n-tiles x 50 f-tiles of 16 x 16
-constexpr int FC_TILES = FC_NT1 + 32;  // + 32 dW_fc2 n-tiles (10 -> 16 rows)
-
-struct FcGrad {
-  const float *dh, *a2, *dlog, *h, *per_sample;
-  float *p_w1, *m_w1, *g_w1, *p_b1, *m_b1, *g_b1;
-  float *p_w2, *m_w2, *g_w2, *p_b2, *m_b2, *g_b2;
-  float* stats;
-  float loss_scale;
-  SgdHyper hy;
-  int mode;  // 0: off, 1: gradients, 2: gradients + fused SGD
-};
-
-struct FcRegs {
-  float av[16], bv[16], pw[4], mw[4], pb, mb;
-};
-
-// Buffer-descriptor loads (SRSRC, 32-bit lane offset + wave-uniform SGPR offset): one
-// address VGPR for all 16 loads of an operand instead of a 64-bit address each -- with 32
-// loads in flight per lane the flat form needs ~100 VGPRs and spills the host kernel.
-// Out-of-range offsets (rows >= B) read 0 by the descriptor's bounds check.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t fc_rsrc(const float* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
-}
-
-__device__ __forceinline__ float fc_ld(__amdgpu_buffer_rsrc_t r, unsigned voff_bytes, int soff_bytes) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
-}
-
-// Loads of tile t for samples 0 .. 63 (and, when `params`, the parameters and momentum the
-// tile's epilogue updates): independent, unpredicated, all in flight at once.
-__device__ __forceinline__ void fc_tile_load(const FcGrad& fc, int t, int base, int B, int lane, FcRegs& r,
-                                             bool params) {
-  (void)base;
-  const int i = lane & 15, g = lane >> 4;
-  if (t < FC_NT1) {
-    const int nt = t / 50, kt = t - nt * 50;
-    const int nc = min(nt * 16 + i, 499), f = kt * 16 + i;
-    const auto rd = fc_rsrc(fc.dh, (unsigned)B * 2000u), ra = fc_rsrc(fc.a2, (unsigned)B * 3200u);
-    const unsigned vd = (unsigned)(g * 500 + nc) * 4u, va = (unsigned)(g * 800 + f) * 4u;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {  // sample 4 s + g
-      r.av[s] = fc_ld(rd, vd, s * 8000);
-      r.bv[s] = fc_ld(ra, va, s * 12800);
-    }
-    if (params) {
-      const auto rp = fc_rsrc(fc.p_w1, 1600000u), rm = fc_rsrc(fc.m_w1, 1600000u);
-      const unsigned vp = (unsigned)((nt * 16 + g * 4) * 800 + f) * 4u;  // rows >= 500: 0, never stored
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        r.pw[q] = fc_ld(rp, vp, q * 3200);
-        r.mw[q] = fc_ld(rm, vp, q * 3200);
-      }
-      r.pb = fc.p_b1[nc];
-      r.mb = fc.m_b1[nc];
-    }
-  } else {
-    const int nt = t - FC_NT1;
-    const int jc = min(i, 9), ncl = min(nt * 16 + i, 499);
-    const auto rl = fc_rsrc(fc.dlog, (unsigned)B * 40u), rh = fc_rsrc(fc.h, (unsigned)B * 2000u);
-    const unsigned vl = (unsigned)(g * 10 + jc) * 4u, vh = (unsigned)(g * 500 + ncl) * 4u;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      r.av[s] = fc_ld(rl, vl, s * 160);
-      r.bv[s] = fc_ld(rh, vh, s * 8000);
-    }
-    if (params) {
-      const auto rp = fc_rsrc(fc.p_w2, 20000u), rm = fc_rsrc(fc.m_w2, 20000u);
-      const unsigned vp = (unsigned)(g * 4 * 500 + ncl) * 4u;  // class rows >= 10: 0, never stored
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        r.pw[q] = fc_ld(rp, vp, q * 2000);
-        r.mw[q] = fc_ld(rm, vp, q * 2000);
-      }
-      r.pb = fc.p_b2[jc];
-      r.mb = fc.m_b2[jc];
-    }
-  }
-}
-
-// One whole tile by one wave (B <= 64: one K chunk, loaded by fc_tile_load(.., base 0, ..,
-// params = mode == 2)); gradient (+ SGD) epilogue; tile 1601 also writes the step's loss
-// statistics.
-template <bool SGD>
-__device__ __forceinline__ void fc_tile_run(const FcGrad& fc, int t, int B, int lane, FcRegs& r) {
-  const int i = lane & 15, g = lane >> 4;
-  const bool w1 = t < FC_NT1;
-  const int nt = w1 ? t / 50 : t - FC_NT1, kt = w1 ? t - nt * 50 : 0;
-  const bool rowv = w1 ? nt * 16 + i < 500 : i < 10;  // valid A row of this lane
-  f32x4 c0 = zero4(), c1 = zero4();
-  float dbsum = 0.f;
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const bool bvld = 4 * s + g < B;
-    const float a = (bvld && rowv) ? r.av[s] : 0.f;
-    dbsum += a;
-    const float b = bvld ? r.bv[s] : 0.f;
-    if (s & 1) c1 = mfma16x16x4(a, b, c1);
-    else c0 = mfma16x16x4(a, b, c0);
-  }
-  const f32x4 c = c0 + c1;
-  constexpr bool sgd = SGD;
-  const bool bias = w1 ? kt == 0 : nt == 0;
-  if (bias) {
-    dbsum = sum_lane_rows(dbsum);
-  }
-  if (w1) {
-    const int f = kt * 16 + i;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = nt * 16 + g * 4 + q;
-      if (row < 500) {
-        const size_t e = (size_t)row * 800 + f;
-        fc.g_w1[e] = c[q];
-        if (sgd) {
-          sgd_elem(r.pw[q], r.mw[q], c[q], fc.hy);
-          fc.p_w1[e] = r.pw[q];
-          fc.m_w1[e] = r.mw[q];
-        }
-      }
-    }
-    if (bias && g == 0 && rowv) {
-      const int n = nt * 16 + i;
-      fc.g_b1[n] = dbsum;
-      if (sgd) {
-        sgd_elem(r.pb, r.mb, dbsum, fc.hy);
-        fc.p_b1[n] = r.pb;
-        fc.m_b1[n] = r.mb;
-      }
-    }
-  } else {
-    const int n = nt * 16 + i;
-    if (n < 500) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = g * 4 + q;
-        if (j < 10) {
-          fc.g_w2[j * 500 + n] = c[q];
-          if (sgd) {
-            sgd_elem(r.pw[q], r.mw[q], c[q], fc.hy);
-            fc.p_w2[j * 500 + n] = r.pw[q];
-            fc.m_w2[j * 500 + n] = r.mw[q];
-          }
-        }
-      }
-    }
-    if (bias && g == 0 && i < 10) {
-      fc.g_b2[i] = dbsum;
-      if (sgd) {
-        sgd_elem(r.pb, r.mb, dbsum, fc.hy);
-        fc.p_b2[i] = r.pb;
-        fc.m_b2[i] = r.mb;
-      }
-    }
-    if (nt == 1 && fc.per_sample != nullptr && fc.stats != nullptr) {
-      float ls = 0.f, cs = 0.f;
-      for (int bb = lane; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
-      ls = wave_allsum_dpp(ls);
-      cs = wave_allsum_dpp(cs);
-      if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1601,15 +1050,11 @@ constexpr int F_NDZ = 4096 / F_NT;   // dz2 staging: 64 co (50 real) x 64 pos
 constexpr int F_NW2 = (6656 + F_NT - 1) / F_NT;  // W2 slice staging: 52 co x 128 j
 static_assert(F_NT >= 784 && 4096 % F_NT == 0 && 32 % F_NW == 0, "conv_bwd thread mapping");
 
-// FCM = fc tile mode (0: none, 1: gradients, 2: + fused SGD) as a template parameter: the
-// SGD epilogue raises the kernel to 128 VGPRs (the whole register file at 4 waves/SIMD),
-// which modes 0/1 -- the DDP and ranks-sharing-a-GPU paths -- do not pay.
-template <int FCM>
 __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ gw2,
     float* __restrict__ gb2, float* __restrict__ gw1, float* __restrict__ gb1,
-    float* __restrict__ dz1_out, int slab_stride, int B, FcGrad fc, u64* dbg) {
+    float* __restrict__ dz1_out, int slab_stride, int B, u64* dbg) {
   extern __shared__ float lds[];
   float* dz_s = lds + F_OFF_DZ;
   float* dz80_s = lds + F_OFF_D8;
@@ -1625,16 +1070,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   const int lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   stamp(dbg, 0);
-  // fc weight-gradient tiles in the waves the conv phases leave idle: wave 15 - k takes tile
-  // blk + k * (#blocks), k < 7 -- all 1632 tiles when 7 * 4B >= 1632 and B <= 64 (one K
-  // chunk), which the launcher checks (B = 59..64; other batches use fc1_bwd).  The tile
-  // operands are loaded when phase 3 starts (buffer loads: one address VGPR per operand,
-  // so holding them through col2im stays under 100 VGPRs) and the tiles run during phase 4,
-  // where waves 7-15 have no dW_conv1 items.
-  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
-  const int fk = 15 - wv;
-  const int ft0 = blk + nblk * fk;
-  const bool fc_wave = FCM != 0 && fk < 7 && ft0 < FC_TILES;
 
   // ---- phase 1: stage (all loads of a thread are independent and unrolled)
   {
@@ -1800,8 +1235,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 2);
-  FcRegs fr;  // fc tile operands: in flight during col2im, consumed in phase 4
-  if (fc_wave) fc_tile_load(fc, ft0, 0, B, lane, fr, FCM == 2);
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]
 #pragma unroll
@@ -1844,7 +1277,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 3);
-  if (fc_wave) fc_tile_run<FCM == 2>(fc, ft0, B, lane, fr);
 
   // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU.  As an MFMA GEMM this is
   // M = 5 channels padded to 16 (3/4 of every MFMA wasted, ~3 us); here 400 threads =
@@ -1944,9 +1376,6 @@ constexpr int G_OFF_RED = G_OFF_W + 5 * F_Z1;
 static_assert(G_LDS * 4 <= 160 * 1024, "conv_bwd4 LDS budget");
 static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
 
-#ifndef PTO_PIPE
-#define PTO_PIPE 1  // software-pipelined LDS operand reads in conv_bwd4 phase 2 (0: read-all-then-MFMA)
-#endif
 
 // Phase 2 of conv_bwd4 for one wave, software-pipelined: the LDS operand reads of chunk c+1
 // are issued before the MFMAs of chunk c (sched_barrier groups; the compiler's counted
@@ -2137,64 +1566,12 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   //   products, one sample each, summed in sample order after the barrier.
   f32x4 gacc = zero4();
   const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
-#if PTO_PIPE
-  if (PTO_ABL & 8) {
-  } else if (wv < 12) {
+  if (wv < 12) {
     if (own) bwd4_phase2<true, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
     else bwd4_phase2<false, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
     if (wv >= 6) pk_s[tp * 64 + lane] = gacc;
   } else {
     if (own) bwd4_phase2<true, false>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
-#else
-  // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
-  if (own) {
-    const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
-    const float* dzo = dzc_s + r * G_DZN;
-    f32x4 acc[F_TPW];
-#pragma unroll
-    for (int n = 0; n < F_TPW; ++n) acc[n] = zero4();
-    float bv[13], av[F_TPW][13];
-#pragma unroll
-    for (int s = 0; s < 13; ++s) {
-      bv[s] = dzo[(4 * s + g) * G_DZS + pt * 16 + i];
-#pragma unroll
-      for (int n = 0; n < F_TPW; ++n) av[n][s] = w_s[(4 * s + g) * F_WS + (jt0 + n) * 16 + i];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < 13; ++s)
-#pragma unroll
-      for (int n = 0; n < F_TPW; ++n) acc[n] = mfma16x16x4(av[n][s], bv[s], acc[n]);
-#pragma unroll
-    for (int n = 0; n < F_TPW; ++n)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        dcol_s[((jt0 + n) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[n][rr];
-  }
-  if (wv < 12) {
-    const int kh2 = wv / 6;
-    const int jc = min(max(jbase + jt * 16 + i, 0), 124);  // clamped (unstored columns read finite data)
-    const int ci = jc / 25, t = jc - ci * 25;
-    const float* ab = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
-    const float* bb = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
-    float av[32], bv[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {  // k-step u: sample 2 kh2 + u / 16, position 4 (u % 16) + g
-      const int s = u >> 4, uu = u & 15;
-      av[u] = ab[s * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];
-      bv[u] = bb[s * G_DZN + 4 * uu];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 e0 = zero4(), e1 = zero4();
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (u & 1) e1 = mfma16x16x4(av[u], bv[u], e1);
-      else e0 = mfma16x16x4(av[u], bv[u], e0);
-    }
-    gacc = e0 + e1;
-    if (kh2 == 1) pk_s[tp * 64 + lane] = gacc;
-  } else {
-#endif
     const int item = tid - 768;  // (sample s, co 48 + cr, column jl)
     const int s = item >> 6, cr = (item >> 5) & 1, jl = item & 31;
     const int jc = min(max(jbase + jl, 0), 124);
@@ -2222,20 +1599,21 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       float* rp = rowq + (ct * 16 + i) * 500;
       const int j0 = jbase + jt * 16 + 4 * g;
       if (j0 >= 0 && j0 + 3 < 125) {
-        st_h4(reinterpret_cast<float4*>(rp + j0), make_float4(gacc[0], gacc[1], gacc[2], gacc[3]));
+        const float4 v4 = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
+        if constexpr (WT_SLAB) store_wt(buf_rsrc(slab, 0xFFFFFFF0u), (unsigned)((rp + j0) - slab) * 4u, v4);
+        else *reinterpret_cast<float4*>(rp + j0) = v4;
       } else {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          if (j0 + rr >= 0 && j0 + rr < 125) st_h(rp + j0 + rr, gacc[rr]);
+          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
       }
     } else if (wv == 12) {
       const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
       const int j = jbase + (lane & 31);
-      if (j >= 0 && j < 125) st_h(rowq + (48 + (lane >> 5)) * 500 + j, v);
+      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
     }
   }
   if (!own) return;  // block-uniform: padding blocks of the last chunk are done
-  if (PTO_ABL & 64) return;
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
   if (tid < 720) {
@@ -2266,10 +1644,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   __syncthreads();
   stamp(dbg, 3);
-#ifndef PTO_DW1W
-#define PTO_DW1W 1  // phase 4 on 600 threads (one output row each) instead of 400 (3 half rows)
-#endif
-#if PTO_DW1W
   // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU: 600 threads = (channel c, output row
   // y, kernel row kh), each slides a 28-wide register window of input row y + kh across the
   // 24 outputs of dz1 row y: 5 FMAs per LDS read of dz1; 24 row partials meet in LDS.
@@ -2297,36 +1671,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     if (kh == 0) pr[125 + c] = bs;
   }
   static_assert(5 * F_Z1 + NPART * F_RED1 <= 52 * F_WS, "phase-4 partials alias the W2 slice");
-#else
-  constexpr int NPART = 16;
-  if (tid < 400) {
-    const int c = tid / 80, rem = tid - c * 80;
-    const int part = rem / 5, kh = rem - part * 5;
-    const int ry = part & 7, cx = (part >> 3) * 12;
-    const float* zr = dz1_s + c * F_Z1;
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    float bs = 0.f;
-#pragma unroll
-    for (int yy = 0; yy < 3; ++yy) {
-      const int y = ry * 3 + yy;
-      const float* xr = x_s + (y + kh) * F_XR + cx;
-      float xw[16];
-#pragma unroll
-      for (int qq = 0; qq < 16; ++qq) xw[qq] = xr[qq];
-#pragma unroll
-      for (int x = 0; x < 12; ++x) {
-        const float a = zr[y * F_Z1R + cx + x];
-        bs += a;
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
-      }
-    }
-    float* pr = red + part * F_RED1;
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
-    if (kh == 0) pr[125 + c] = bs;
-  }
-#endif
   __syncthreads();
   stamp(dbg, 4);
   // ---- epilogue: sample b's small partials into slab row b
@@ -2335,10 +1679,10 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     float w1sum = 0.f;
 #pragma unroll
     for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
-    if (tid < 125) st_h(rowb + o_gw1 + cig * 125 + tid, w1sum);  // tid = c * 25 + kh * 5 + kw
-    else st_h(rowb + o_gb1 + cig * 5 + (tid - 125), w1sum);
+    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
+    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
   }
-  if (cig == 0 && tid < 50) st_h(rowb + o_gb2 + tid, b2sum);
+  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
   stamp(dbg, 5);
 }
 
@@ -2418,49 +1762,28 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(
 //   (single-process path: the conv grads never make a round trip before the
 //   update).  Also writes the reduced grads (inspection / grad-norm logging) and
 //   advances the device batch cursor.  Blocks past the reduction: plain SGD over a
-//   second, already-reduced range (p2/g2/buf2), then a float4 copy cp_src -> cp_dst (the
-//   fused-SGD schedule: fc1_bwd wrote the updated fc1.weight to a scratch buffer because
-//   its own dz2 job still reads fc1.weight; nothing reads it after fc1_bwd).
+//   second, already-reduced range (p2/g2/buf2: the fc parameters).
 // ---------------------------------------------------------------------------
-constexpr int SR_CP = 2;  // float4s per thread of the copy blocks
 __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ gout,
-    float* __restrict__ p, float* __restrict__ buf, float lr, float momentum, float dampening,
-    float wd, float grad_scale, int nesterov, int first_step, int* __restrict__ step_counter,
+    float* __restrict__ p, float* __restrict__ buf, SgdHyper hy, int* __restrict__ step_counter,
     float* __restrict__ p2, const float* __restrict__ g2, float* __restrict__ buf2, int n2,
-    int red_blocks, const float4* __restrict__ cp_src, float4* __restrict__ cp_dst, int cp_n4,
-    int* __restrict__ pend, u64* dbg) {
+    int red_blocks, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
-  if (pend != nullptr && (blockIdx.x | tid) == 0) *pend = 1;  // fc update deferred to the next conv12
-  const int sgd_blocks = (n2 / 4 + 255) / 256;
-  if ((int)blockIdx.x >= red_blocks + sgd_blocks) {
-    const int v0 = (blockIdx.x - red_blocks - sgd_blocks) * 256 * SR_CP + tid;
-    float4 v[SR_CP];
-#pragma unroll
-    for (int k = 0; k < SR_CP; ++k) v[k] = cp_src[min(v0 + k * 256, cp_n4 - 1)];
-#pragma unroll
-    for (int k = 0; k < SR_CP; ++k)
-      if (v0 + k * 256 < cp_n4) cp_dst[v0 + k * 256] = v[k];
-    return;
-  }
   if ((int)blockIdx.x >= red_blocks) {
-    if (PTO_ABL & 1) return;
     // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
     const int v = (blockIdx.x - red_blocks) * 256 + tid;
     if (v < (n2 >> 2)) {
       float4 pp = reinterpret_cast<float4*>(p2)[v];
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];
       float4 bb = reinterpret_cast<float4*>(buf2)[v];
-      const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-      sgd_elem(pp.x, bb.x, gg.x, hy);
-      sgd_elem(pp.y, bb.y, gg.y, hy);
-      sgd_elem(pp.z, bb.z, gg.z, hy);
-      sgd_elem(pp.w, bb.w, gg.w, hy);
-      st_h4(reinterpret_cast<float4*>(p2) + v, pp);
-      st_h4(reinterpret_cast<float4*>(buf2) + v, bb);
+      sgd4(pp, bb, gg, hy);
+      st4<WT_TAIL>(reinterpret_cast<float4*>(p2), v, pp);
+      st4<WT_TAIL>(reinterpret_cast<float4*>(buf2), v, bb);
     }
+    stamp(dbg, 1);
     return;
   }
   const int col = blockIdx.x * SR_COLS + (tid % SR_COLS);
@@ -2479,199 +1802,12 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     float4 r = red[0][tid];
 #pragma unroll
     for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
-    if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
-    const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-    sgd_elem(pp.x, bb.x, r.x, hy);
-    sgd_elem(pp.y, bb.y, r.y, hy);
-    sgd_elem(pp.z, bb.z, r.z, hy);
-    sgd_elem(pp.w, bb.w, r.w, hy);
-    st_h4(reinterpret_cast<float4*>(p) + col, pp);
-    st_h4(reinterpret_cast<float4*>(buf) + col, bb);
+    if (gout != nullptr) st4<WT_TAIL>(reinterpret_cast<float4*>(gout), col, r);
+    sgd4(pp, bb, r, hy);
+    st4<WT_TAIL>(reinterpret_cast<float4*>(p), col, pp);
+    st4<WT_TAIL>(reinterpret_cast<float4*>(buf), col, bb);
   }
   if (step_counter != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(step_counter, 1);
-  stamp(dbg, 1);
-}
-
-// ---------------------------------------------------------------------------
-// T: the single-process step tail, one launch:
-//   blocks [0, red_blocks)           slab reduction + SGD(momentum) of the conv params
-//                                    (slab_reduce_sgd_kernel's body);
-//   next T_NJ1 blocks (4 waves)      dW_fc1 = dh^T a2 tiles (MFMA, K = B) + db_fc1, each
-//                                    tile's SGD applied in its epilogue -- the fc1 weight
-//                                    gradient never makes an HBM round trip before its
-//                                    update (it is still stored, for inspection);
-//   last T_NJ3 blocks                dW_fc2 = dlogits^T h + db_fc2 with fused SGD, and the
-//                                    step's loss statistics.
-//   Moving the fc weight gradients here (they only depend on the head's outputs) leaves
-//   the fc1_bwd_head launch with just the dz2 critical path.
-// ---------------------------------------------------------------------------
-constexpr int T_NW = 4;
-constexpr int T_NJ1 = 1600 / T_NW;  // dW_fc1 tiles (32 n-tiles x 50 f-tiles)
-constexpr int T_NJ3 = 32 / T_NW;    // dW_fc2 tiles (32 n-tiles)
-
-__global__ __launch_bounds__(256) void tail_sgd_kernel(
-    const float* __restrict__ P, int B, SlabRows sr, int n, int stride, float* __restrict__ gout,
-    float* __restrict__ p, float* __restrict__ buf, SgdHyper hy, FcTail fc,
-    int* __restrict__ step_counter, int red_blocks, u64* dbg) {
-  __shared__ float4 red[SR_SL][SR_COLS];
-  stamp(dbg, 0);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int blk = blockIdx.x;
-  if (blk >= red_blocks + T_NJ1) {
-    // dW_fc2[10, 500] = dlogits^T h (M = 10 -> 16, N = 500 -> 32 tiles, K = B) + db_fc2 + stats
-    const int nt = (blk - red_blocks - T_NJ1) * T_NW + wv;  // 0..31
-    const int jc = min(i, 9);
-    const int nn = nt * 16 + i, ncl = min(nn, 499);
-    float pw[4], mw[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = min(g * 4 + q, 9);
-      pw[q] = fc.p_w2[j * 500 + ncl];
-      mw[q] = fc.m_w2[j * 500 + ncl];
-    }
-    float pb = fc.p_b2[jc], mb = fc.m_b2[jc];
-    const bool do_stats = nt == 1 && fc.per_sample != nullptr && fc.stats != nullptr;
-    float ls = 0.f, cs = 0.f;
-    if (do_stats && lane < B) { ls = fc.per_sample[2 * lane]; cs = fc.per_sample[2 * lane + 1]; }
-    f32x4 c0 = zero4(), c1 = zero4();
-    float dbsum = 0.f;
-    for (int base = 0; base < B; base += 64) {
-      float av[16], hv[16];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int bb = min(base + 4 * s + g, B - 1);
-        av[s] = fc.dlog[(size_t)bb * 10 + jc];
-        hv[s] = fc.h[(size_t)bb * 500 + ncl];
-      }
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const bool bvld = base + 4 * s + g < B;
-        const float a = (bvld && i < 10) ? av[s] : 0.f;
-        dbsum += a;
-        const float hb = bvld ? hv[s] : 0.f;
-        if (s & 1) c1 = mfma16x16x4(a, hb, c1);
-        else c0 = mfma16x16x4(a, hb, c0);
-      }
-    }
-    const f32x4 c = c0 + c1;
-    if (nn < 500) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = g * 4 + q;
-        if (j < 10) {
-          sgd_elem(pw[q], mw[q], c[q], hy);
-          fc.g_w2[j * 500 + nn] = c[q];
-          fc.p_w2[j * 500 + nn] = pw[q];
-          fc.m_w2[j * 500 + nn] = mw[q];
-        }
-      }
-    }
-    if (nt == 0) {
-      dbsum = sum_lane_rows(dbsum);
-      if (g == 0 && i < 10) {
-        sgd_elem(pb, mb, dbsum, hy);
-        fc.g_b2[i] = dbsum;
-        fc.p_b2[i] = pb;
-        fc.m_b2[i] = mb;
-      }
-    }
-    if (do_stats) {
-      for (int bb = lane + 64; bb < B; bb += 64) { ls += fc.per_sample[2 * bb]; cs += fc.per_sample[2 * bb + 1]; }
-      ls = wave_allsum_dpp(ls);
-      cs = wave_allsum_dpp(cs);
-      if (lane == 0) { fc.stats[0] = ls * fc.loss_scale; fc.stats[1] = cs; }
-    }
-    stamp(dbg, 1);
-    return;
-  }
-  if (blk >= red_blocks) {
-    // dW_fc1[500, 800] = dh^T a2 tile (n 16 x f 16, K = B) + fused SGD; db_fc1 (kt == 0)
-    const int tile = (blk - red_blocks) * T_NW + wv;
-    const int nt = tile / 50, kt = tile - nt * 50;
-    const int nn = nt * 16 + i, f = kt * 16 + i;
-    const bool nv = nn < 500;
-    const int nc = nv ? nn : 499;
-    float pw[4], mw[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = min(nt * 16 + g * 4 + q, 499);
-      pw[q] = fc.p_w1[(size_t)row * 800 + f];
-      mw[q] = fc.m_w1[(size_t)row * 800 + f];
-    }
-    float pb = 0.f, mb = 0.f;
-    if (kt == 0) { pb = fc.p_b1[nc]; mb = fc.m_b1[nc]; }
-    f32x4 c0 = zero4(), c1 = zero4();
-    float dbsum = 0.f;
-    for (int base = 0; base < B; base += 64) {
-      float av[16], fv[16];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int bb = min(base + 4 * s + g, B - 1);
-        av[s] = fc.dh[(size_t)bb * 500 + nc];
-        fv[s] = fc.a2[(size_t)bb * 800 + f];
-      }
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const bool bvld = base + 4 * s + g < B;
-        const float a = (bvld && nv) ? av[s] : 0.f;
-        dbsum += a;
-        const float fb = bvld ? fv[s] : 0.f;
-        if (s & 1) c1 = mfma16x16x4(a, fb, c1);
-        else c0 = mfma16x16x4(a, fb, c0);
-      }
-    }
-    const f32x4 c = c0 + c1;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = nt * 16 + g * 4 + q;
-      if (row < 500) {
-        const size_t e = (size_t)row * 800 + f;
-        sgd_elem(pw[q], mw[q], c[q], hy);
-        fc.g_w1[e] = c[q];
-        fc.p_w1[e] = pw[q];
-        fc.m_w1[e] = mw[q];
-      }
-    }
-    if (kt == 0) {
-      dbsum = sum_lane_rows(dbsum);
-      if (g == 0 && nv) {
-        sgd_elem(pb, mb, dbsum, hy);
-        fc.g_b1[nn] = dbsum;
-        fc.p_b1[nn] = pb;
-        fc.m_b1[nn] = mb;
-      }
-    }
-    stamp(dbg, 1);
-    return;
-  }
-  // slab reduction + SGD of the conv params (see slab_reduce_sgd_kernel)
-  const int col = blk * SR_COLS + (tid % SR_COLS);
-  const int slice = tid / SR_COLS;
-  const int n4 = n >> 2;
-  const int cc = min(col, n4 - 1);
-  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bq = pp;
-  if (tid < SR_COLS) {
-    pp = reinterpret_cast<const float4*>(p)[cc];
-    bq = reinterpret_cast<const float4*>(buf)[cc];
-  }
-  red[slice][tid % SR_COLS] = slab_col_sum(reinterpret_cast<const float4*>(P), stride >> 2, cc, sr.of(cc),
-                                           slice, SR_SL);
-  __syncthreads();
-  if (tid < SR_COLS && col < n4) {
-    float4 rr = red[0][tid];
-#pragma unroll
-    for (int q = 1; q < SR_SL; ++q) { rr.x += red[q][tid].x; rr.y += red[q][tid].y; rr.z += red[q][tid].z; rr.w += red[q][tid].w; }
-    if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = rr;
-    sgd_elem(pp.x, bq.x, rr.x, hy);
-    sgd_elem(pp.y, bq.y, rr.y, hy);
-    sgd_elem(pp.z, bq.z, rr.z, hy);
-    sgd_elem(pp.w, bq.w, rr.w, hy);
-    reinterpret_cast<float4*>(p)[col] = pp;
-    reinterpret_cast<float4*>(buf)[col] = bq;
-  }
-  if (step_counter != nullptr && blk == 0 && tid == 0) atomicAdd(step_counter, 1);
   stamp(dbg, 1);
 }
 
@@ -2681,11 +1817,8 @@ __global__ __launch_bounds__(256) void tail_sgd_kernel(
 // p -= lr * (nesterov ? g + momentum*buf : buf)); grad_scale folds the DDP 1/world.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(
-    float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ buf, long n,
-    float lr, float momentum, float dampening, float wd, float grad_scale, int nesterov,
-    int first_step, int* __restrict__ step_counter, const int* __restrict__ cond) {
-  if (cond != nullptr && *cond == 0) return;  // conditional (deferred-update flush)
-  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+    float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ buf, long n, SgdHyper hy,
+    int* __restrict__ step_counter) {
   const long n4 = n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < n4 + 4; v += stride) {
@@ -2697,10 +1830,7 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(
       float4 pp = reinterpret_cast<float4*>(p)[v];
       const float4 gg = reinterpret_cast<const float4*>(gr)[v];
       float4 bb = reinterpret_cast<float4*>(buf)[v];
-      sgd_elem(pp.x, bb.x, gg.x, hy);
-      sgd_elem(pp.y, bb.y, gg.y, hy);
-      sgd_elem(pp.z, bb.z, gg.z, hy);
-      sgd_elem(pp.w, bb.w, gg.w, hy);
+      sgd4(pp, bb, gg, hy);
       reinterpret_cast<float4*>(p)[v] = pp;
       reinterpret_cast<float4*>(buf)[v] = bb;
     } else {
@@ -2722,7 +1852,34 @@ inline BatchSrc make_src(const void* x, int is_u8, const int* labels, const int*
   return s;
 }
 
-u64* g_dbg = nullptr;  // phase-timestamp buffer (tools/phase_profile.py); null in production
+// Phase-timestamp buffer (tools/phase_profile.py, tools/step_timeline.py); null in production.
+// Every launch takes the next of kDbgSlots slots of kDbgSlotU64 words (<= 1024 blocks x 16), so
+// the kernels of one captured step stamp disjoint regions.
+constexpr int kDbgSlots = 16;
+constexpr long kDbgSlotU64 = 1024L * 16;
+u64* g_dbg = nullptr;
+int g_dbg_slot = 0;
+
+u64* dbg_next() {
+  if (g_dbg == nullptr) return nullptr;
+  u64* p = g_dbg + (long)(g_dbg_slot % kDbgSlots) * kDbgSlotU64;
+  ++g_dbg_slot;
+  return p;
+}
+
+template <typename K>
+int set_max_lds(K kernel, int bytes, std::atomic<unsigned>& done) {
+  // > 64 KB of dynamic LDS must be opted into once per device and kernel (thread-safe: several
+  // host threads may drive different GPUs through this library)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
+  if (!(done.load(std::memory_order_acquire) & (1u << dev))) {
+    const hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return (int)e;
+    done.fetch_or(1u << dev, std::memory_order_release);
+  }
+  return 0;
+}
 
 }  // namespace
 
@@ -2733,48 +1890,12 @@ u64* g_dbg = nullptr;  // phase-timestamp buffer (tools/phase_profile.py); null 
 // ===========================================================================
 #define PTO_CHECK_B(B) do { if ((B) <= 0 || (B) > (1 << 20)) return -1; } while (0)
 
-static bool conv_bwd_fc_supported(int B) { return B <= 64 && 7 * 4 * B >= FC_TILES; }
-
-template <int FCM>
-static int conv_bwd_launch_t(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                             const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
-                             float* dz1_out, int slab_stride, int B, const FcGrad& fc, void* stream) {
-  // > 64 KB of dynamic LDS must be opted into once per device and instantiation
-  // (thread-safe: several host threads may drive different GPUs through this library)
-  static std::atomic<unsigned> attr_set{0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
-  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd_kernel<FCM>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             F_LDS * (int)sizeof(float));
-    if (e != hipSuccess) return (int)e;
-    attr_set.fetch_or(1u << dev, std::memory_order_release);
-  }
-  hipLaunchKernelGGL(conv_bwd_kernel<FCM>, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float),
-                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out,
-                     slab_stride, B, fc, g_dbg);
-  return (int)hipGetLastError();
-}
-
-static int conv_bwd_launch(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                           const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
-                           float* dz1_out, int slab_stride, int B, const FcGrad& fc, void* stream) {
-  PTO_CHECK_B(B);
-  if (slab_stride < 0) return -1;
-  // the slab path writes dW_conv2 as float4: row starts and gw2 + 544-float offsets aligned
-  if (slab_stride > 0 && (slab_stride % 4 != 0 || (reinterpret_cast<uintptr_t>(gw2) & 15) != 0)) return -2;
-  switch (fc.mode) {
-    case 0: return conv_bwd_launch_t<0>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
-    case 1: return conv_bwd_launch_t<1>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
-    case 2: return conv_bwd_launch_t<2>(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
-    default: return -1;
-  }
-}
-
 extern "C" {
 
-void pto_set_debug_buffer(void* p) { g_dbg = reinterpret_cast<u64*>(p); }
+void pto_set_debug_buffer(void* p) {
+  g_dbg = reinterpret_cast<u64*>(p);
+  g_dbg_slot = 0;
+}
 
 int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* labels, const int* perm,
                         const int* cursor, int host_offset, int n_total, float scale,
@@ -2787,7 +1908,7 @@ int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* labels, const int* 
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
   const int blocks = (B * 2880 + 255) / 256;
   hipLaunchKernelGGL(conv1_fwd_pool_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     src, w, bias, a1, idx1, B, zero_ptr, zero_n, xn_out, lab_out, g_dbg);
+                     src, w, bias, a1, idx1, B, zero_ptr, zero_n, xn_out, lab_out, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2795,7 +1916,7 @@ int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, floa
                         uint8_t* idx2, int B, void* stream) {
   PTO_CHECK_B(B);
   hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream,
-                     a1, w, bias, a2, idx2, B, g_dbg);
+                     a1, w, bias, a2, idx2, B, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2804,10 +1925,9 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
                          float shift, const float* w1, const float* b1, const float* w2,
                          const float* b2, float* a1, uint8_t* idx1, float* xn_out, int* lab_out,
                          float* a2, uint8_t* idx2, int B, const uint8_t* stg_x, const int* stg_lab,
-                         const int* stg_tag, float* sg_p, const float* sg_g, float* sg_m, int sg_n,
-                         const int* sg_pend, float lr, float momentum, float dampening, float wd,
-                         float grad_scale, int nesterov, int first_step, void* stream) {
+                         const int* stg_tag, void* stream) {
   PTO_CHECK_B(B);
+  if (B > 65535) return -1;  // grid y
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
   if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 1)) return -2;
@@ -2816,19 +1936,8 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
                            !is_u8 || labels == nullptr))
     return -1;
   const BatchSrc src = make_src(x, is_u8, labels, perm, cursor, host_offset, n_total, scale, shift);
-  SgdRange sg{};
-  int rows = 0;
-  if (sg_n > 0) {
-    if (sg_p == nullptr || sg_g == nullptr || sg_m == nullptr || sg_pend == nullptr || (sg_n & 3) ||
-        ((((uintptr_t)sg_p) | ((uintptr_t)sg_g) | ((uintptr_t)sg_m)) & 15))
-      return -1;
-    sg = SgdRange{reinterpret_cast<float4*>(sg_p), reinterpret_cast<const float4*>(sg_g),
-                  reinterpret_cast<float4*>(sg_m), sg_n / 4, sg_pend,
-                  SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step}};
-    rows = (sg.n4 + 4 * AB_NT - 1) / (4 * AB_NT);
-  }
-  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B + rows), dim3(AB_NT), 0, (hipStream_t)stream, src, w1,
-                     b1, w2, b2, a1, idx1, xn_out, lab_out, a2, idx2, B, stg_x, stg_lab, stg_tag, sg, g_dbg);
+  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream, src, w1, b1, w2, b2,
+                     a1, idx1, xn_out, lab_out, a2, idx2, B, stg_x, stg_lab, stg_tag, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2837,18 +1946,18 @@ int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* 
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w)) & 15) return -2;  // float4 loads
   hipLaunchKernelGGL(fc1_fwd_kernel<1>, dim3(32, (B + 15) / 16), dim3(640), 0,
-                     (hipStream_t)stream, x, w, bias, h, B, nullptr, g_dbg);
+                     (hipStream_t)stream, x, w, bias, h, B, dbg_next());
   return (int)hipGetLastError();
 }
 
-int pto_mnist_fc1_ks() { return PTO_FC1_KS; }
+int pto_mnist_fc1_ks() { return FC1_KS; }
 
 // Split-K fc1: pre-activation partials to parts[KS][B][500] (head_kernel finishes h).
-int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, int* clr, void* stream) {
+int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, void* stream) {
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)parts)) & 15) return -2;
-  hipLaunchKernelGGL(fc1_fwd_kernel<PTO_FC1_KS>, dim3(32, (B + 15) / 16, PTO_FC1_KS), dim3(640 / PTO_FC1_KS), 0,
-                     (hipStream_t)stream, x, w, nullptr, parts, B, clr, g_dbg);
+  hipLaunchKernelGGL(fc1_fwd_kernel<FC1_KS>, dim3(32, (B + 15) / 16, FC1_KS), dim3(640 / FC1_KS), 0,
+                     (hipStream_t)stream, x, w, nullptr, parts, B, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2865,11 +1974,11 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
   if (stats == nullptr)
     hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(64), 0, (hipStream_t)stream, h, w2, b2, lab,
                        B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, hp2, b1,
-                       h_out, g_dbg);
+                       h_out, dbg_next());
   else
     hipLaunchKernelGGL(head_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h,
                        w2, b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample,
-                       stats, hp2, b1, h_out, g_dbg);
+                       stats, hp2, b1, h_out, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2877,11 +1986,8 @@ static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
   const int B = a.B;
   PTO_CHECK_B(B);
   if (a.jobs <= 0 || a.jobs > 7) return -1;
-  if (((uintptr_t)a.dh) & 15) return -2;  // float4 dh rows (job 2)
-  if (a.sgd && (a.w1_next == nullptr || a.m_w1 == nullptr || a.p_b1 == nullptr || a.m_b1 == nullptr ||
-                a.p_w2 == nullptr || a.m_w2 == nullptr || a.p_b2 == nullptr || a.m_b2 == nullptr ||
-                a.w1_next == a.w1))
-    return -1;
+  if (a.gw1 == nullptr || a.gb1 == nullptr || a.gw2 == nullptr || a.gb2 == nullptr) return -1;
+  if ((((uintptr_t)a.dh) | ((uintptr_t)a.gw1)) & 15) return -2;  // float4 dh rows (job 2), dW_fc1 stores
   int nst = 0;
   if (a.stage_x != nullptr) {
     if (a.nsrc.perm == nullptr || a.nsrc.cursor == nullptr || a.nsrc.labels == nullptr || !a.nsrc.is_u8 ||
@@ -2892,7 +1998,7 @@ static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
   }
   const int blocks = ((a.jobs & 1) ? E_NJ1 : 0) + ((a.jobs & 2) ? ((B + 15) / 16) * 50 : 0) +
                      ((a.jobs & 4) ? E_NJ3 : 0) + nst;
-  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, a, g_dbg);
+  hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, a, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2904,40 +2010,10 @@ int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, con
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
   a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = jobs; a.B = B;
-  if (gw1 == nullptr || gb1 == nullptr || gw2 == nullptr || gb2 == nullptr) return -1;
   return fc1_bwd_launch(a, stream);
 }
 
-// fc1_bwd with the fc parameters' SGD fused into the weight-gradient jobs (the updated
-// fc1.weight goes to w1_next; the tail copies it back) and the next batch staged.
-// Gradient pointers may be null (not stored).  stage_x null: no staging.
-int pto_mnist_fc1_bwd_sgd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
-                          const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
-                          float* gb2, float* dz2, const float* per_sample, float* stats, float loss_scale,
-                          int B, float* w1_next, float* m_w1, float* p_b1, float* m_b1, float* p_w2,
-                          float* m_w2, float* p_b2, float* m_b2, float lr, float momentum, float dampening,
-                          float wd, float grad_scale, int nesterov, int first_step, const void* nx,
-                          const int* nlabels, const int* nperm, const int* ncursor, int n_total,
-                          int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
-  Fc1Bwd a{};
-  a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
-  a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
-  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
-  a.sgd = 1;
-  a.hy = SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-  a.w1_next = w1_next; a.m_w1 = m_w1; a.p_b1 = p_b1; a.m_b1 = m_b1;
-  a.p_w2 = p_w2; a.m_w2 = m_w2; a.p_b2 = p_b2; a.m_b2 = m_b2;
-  if (stage_x != nullptr) {
-    a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
-    a.stage_adv = stage_adv;
-    a.stage_x = stage_x;
-    a.stage_lab = stage_lab;
-    a.stage_tag = stage_tag;
-  }
-  return fc1_bwd_launch(a, stream);
-}
-
-// fc1_bwd (gradients only, every job) + next-batch staging blocks.
+// fc1_bwd (every job) + next-batch staging blocks.
 int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                             const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                             float* gb2, float* dz2, const float* per_sample, float* stats,
@@ -2948,7 +2024,7 @@ int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
   a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
-  if (gw1 == nullptr || gb1 == nullptr || gw2 == nullptr || gb2 == nullptr || stage_x == nullptr) return -1;
+  if (stage_x == nullptr) return -1;
   a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
   a.stage_adv = stage_adv;
   a.stage_x = stage_x;
@@ -2957,62 +2033,19 @@ int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx
   return fc1_bwd_launch(a, stream);
 }
 
-// Stage the batch of step cursor[0] + adv (uint8 pixels + labels + tag) on its own (first
-// step of a staged schedule, or after anything moved the cursor).
-int pto_mnist_stage_batch(const void* x, const int* labels, const int* perm, const int* cursor, int n_total,
-                          int B, int adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
-  Fc1Bwd a{};
-  a.B = B;
-  a.jobs = 0;
-  a.nsrc = make_src(x, 1, labels, perm, cursor, 0, n_total, 1.f, 0.f);
-  a.stage_adv = adv;
-  a.stage_x = stage_x;
-  a.stage_lab = stage_lab;
-  a.stage_tag = stage_tag;
-  PTO_CHECK_B(B);
-  if (perm == nullptr || cursor == nullptr || labels == nullptr || stage_x == nullptr || stage_lab == nullptr ||
-      stage_tag == nullptr || n_total <= 0 || ((((uintptr_t)x) | ((uintptr_t)stage_x)) & 15))
-    return -1;
-  hipLaunchKernelGGL(fc1_bwd_kernel, dim3((B + 3) / 4), dim3(E_NT), 0, (hipStream_t)stream, a, g_dbg);
-  return (int)hipGetLastError();
-}
-
 int pto_mnist_conv_bwd(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
                        const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
                        float* dz1_out, int slab_stride, int B, void* stream) {
-  FcGrad fc{};
-  fc.mode = 0;
-  return conv_bwd_launch(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, fc, stream);
-}
-
-// conv backward + the fc weight-gradient tiles in its idle waves (fc_mode 1: gradients,
-// 2: gradients + fused SGD with the given hyper-parameters) + the step's loss statistics.
-int pto_mnist_conv_bwd_fc(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                          const float* xn, float* gw2, float* gb2, float* gw1, float* gb1,
-                          int slab_stride, int B, int fc_mode, const float* dh, const float* a2,
-                          const float* dlog, const float* h, const float* per_sample, float* p_w1,
-                          float* m_w1, float* g_w1, float* p_b1, float* m_b1, float* g_b1,
-                          float* p_w2, float* m_w2, float* g_w2, float* p_b2, float* m_b2,
-                          float* g_b2, float* stats, float loss_scale, float lr, float momentum,
-                          float dampening, float wd, float grad_scale, int nesterov, int first_step,
-                          void* stream) {
-  if (fc_mode < 1 || fc_mode > 2) return -1;
-  if (!conv_bwd_fc_supported(B)) return -3;  // every tile needs a wave: B in [59, 64]
-  const float* ins[] = {dh, a2, dlog, h};
-  for (const float* q : ins)
-    if (q == nullptr) return -1;
-  float* grads[] = {g_w1, g_b1, g_w2, g_b2};
-  for (float* q : grads)
-    if (q == nullptr) return -1;
-  if (fc_mode == 2) {
-    float* ps[] = {p_w1, m_w1, p_b1, m_b1, p_w2, m_w2, p_b2, m_b2};
-    for (float* q : ps)
-      if (q == nullptr) return -1;
-  }
-  FcGrad fc{dh, a2, dlog, h, per_sample, p_w1, m_w1, g_w1, p_b1, m_b1, g_b1,
-            p_w2, m_w2, g_w2, p_b2, m_b2, g_b2, stats, loss_scale,
-            SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step}, fc_mode};
-  return conv_bwd_launch(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, nullptr, slab_stride, B, fc, stream);
+  PTO_CHECK_B(B);
+  if (B > 65535 || slab_stride < 0) return -1;
+  // the slab path writes dW_conv2 as float4: row starts and gw2 + 544-float offsets aligned
+  if (slab_stride > 0 && (slab_stride % 4 != 0 || (reinterpret_cast<uintptr_t>(gw2) & 15) != 0)) return -2;
+  static std::atomic<unsigned> attr_set{0};
+  const int rc = set_max_lds(conv_bwd_kernel, F_LDS * (int)sizeof(float), attr_set);
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(conv_bwd_kernel, dim3(4, B), dim3(F_NT), F_LDS * sizeof(float), (hipStream_t)stream, dz2,
+                     w2, a1, idx1, xn, gw2, gb2, gw1, gb1, dz1_out, slab_stride, B, dbg_next());
+  return (int)hipGetLastError();
 }
 
 // Conv-grad slab reduction.  rows_big / [big_lo, big_hi) (floats, multiples of 4): the
@@ -3033,21 +2066,21 @@ int pto_slab_reduce(const float* P, int B, int n, int stride, float* out, int ro
   if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
   const int blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P, sr, n,
-                     stride, out, g_dbg);
+                     stride, out, dbg_next());
   return (int)hipGetLastError();
 }
 
 int pto_sgd_momentum(float* p, const float* g, float* buf, long n, float lr, float momentum,
                      float dampening, float wd, float grad_scale, int nesterov, int first_step,
-                     int* step_counter, const int* cond, void* stream) {
+                     int* step_counter, void* stream) {
   if (n <= 0) return -1;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)buf) & 15) return -2;  // float4 path
   long v = (n >> 2) + 4;
   int blocks = (int)((v + 255) / 256);
   if (blocks > 2048) blocks = 2048;
+  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
   hipLaunchKernelGGL(sgd_momentum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g,
-                     buf, n, lr, momentum, dampening, wd, grad_scale, nesterov, first_step,
-                     step_counter, cond);
+                     buf, n, hy, step_counter);
   return (int)hipGetLastError();
 }
 
@@ -3055,7 +2088,7 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
                         float* buf, float lr, float momentum, float dampening, float wd,
                         float grad_scale, int nesterov, int first_step, int* step_counter,
                         float* p2, const float* g2, float* buf2, int n2, int rows_big, int big_lo,
-                        int big_hi, const float* cp_src, float* cp_dst, int cp_n, int* pend, void* stream) {
+                        int big_hi, void* stream) {
   PTO_CHECK_B(B);
   if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
   if (n2 < 0 || (n2 & 3) || (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)))
@@ -3065,16 +2098,11 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
     return -2;
   SlabRows sr;
   if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
-  if (cp_n < 0 || (cp_n & 3) || (cp_n > 0 && (cp_src == nullptr || cp_dst == nullptr)) ||
-      ((((uintptr_t)cp_src) | ((uintptr_t)cp_dst)) & 15))
-    return -1;
   const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
-  const int cp_n4 = cp_n / 4;
-  const int blocks = red_blocks + (n2 / 4 + 255) / 256 + (cp_n4 + 256 * SR_CP - 1) / (256 * SR_CP);
+  const int blocks = red_blocks + (n2 / 4 + 255) / 256;
+  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
-                     sr, n, stride, gout, p, buf, lr, momentum, dampening, wd, grad_scale,
-                     nesterov, first_step, step_counter, p2, g2, buf2, n2, red_blocks,
-                     reinterpret_cast<const float4*>(cp_src), reinterpret_cast<float4*>(cp_dst), cp_n4, pend, g_dbg);
+                     sr, n, stride, gout, p, buf, hy, step_counter, p2, g2, buf2, n2, red_blocks, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -3091,73 +2119,12 @@ int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, cons
       o_gw1 + 500 > stride || o_gb1 + 20 > stride)
     return -1;
   static std::atomic<unsigned> attr_set{0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return -1;
-  if (!(attr_set.load(std::memory_order_acquire) & (1u << dev))) {
-    const hipError_t e = hipFuncSetAttribute((const void*)conv_bwd4_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             G_LDS * (int)sizeof(float));
-    if (e != hipSuccess) return (int)e;
-    attr_set.fetch_or(1u << dev, std::memory_order_release);
-  }
+  const int rc = set_max_lds(conv_bwd4_kernel, G_LDS * (int)sizeof(float), attr_set);
+  if (rc != 0) return rc;
   const int nb = 4 * ((B + 3) / 4);
   hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
-                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, g_dbg);
+                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
   return (int)hipGetLastError();
 }
-
-// fc1 input gradient with the head folded in (training path): dz2, and from the kt == 0
-// blocks h, dh, d(logits), per-sample (loss, correct).  hp = split-K halves [2][B][500].
-int pto_mnist_fc1_bwd_head(const float* hp, const float* b1, const float* w2, const float* b2,
-                           const int* lab, const float* a2, const uint8_t* idx2, const float* w1,
-                           float grad_scale, float* dz2, float* h_out, float* dh_out,
-                           float* dlogits, float* per_sample, int B, void* stream) {
-  if (PTO_FC1_KS != 2) return -1;  // reads the fc1 partials as two halves
-  PTO_CHECK_B(B);
-  if (lab == nullptr || h_out == nullptr || dh_out == nullptr || dlogits == nullptr ||
-      per_sample == nullptr)
-    return -1;
-  if ((((uintptr_t)hp) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out)) & 15) return -2;
-  const int blocks = ((B + 15) / 16) * 50;
-  hipLaunchKernelGGL(fc1_bwd_head_kernel, dim3(blocks), dim3(H_NT), 0, (hipStream_t)stream, hp, b1,
-                     w2, b2, lab, a2, idx2, w1, grad_scale, dz2, h_out, dh_out, dlogits,
-                     per_sample, B, g_dbg);
-  return (int)hipGetLastError();
-}
-
-// Single-process step tail: conv slab reduction + SGD, dW_fc1 / dW_fc2 (+ biases) with
-// fused SGD, loss statistics, batch-cursor advance -- one launch.
-int pto_mnist_tail_sgd(const float* P, int B, int n, int stride, int rows_big, int big_lo, int big_hi,
-                       float* gout, float* p, float* buf,
-                       float lr, float momentum, float dampening, float wd, float grad_scale,
-                       int nesterov, int first_step, int* step_counter, const float* dh,
-                       const float* a2, const float* dlog, const float* h, const float* per_sample,
-                       float* p_w1, float* m_w1, float* g_w1, float* p_b1, float* m_b1, float* g_b1,
-                       float* p_w2, float* m_w2, float* g_w2, float* p_b2, float* m_b2, float* g_b2,
-                       float* stats, float loss_scale, void* stream) {
-  PTO_CHECK_B(B);
-  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
-  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf)) & 15) return -2;
-  const float* ins[] = {dh, a2, dlog, h};
-  for (const float* q : ins)
-    if (q == nullptr) return -1;
-  float* outs[] = {p_w1, m_w1, g_w1, p_b1, m_b1, g_b1, p_w2, m_w2, g_w2, p_b2, m_b2, g_b2};
-  for (float* q : outs)
-    if (q == nullptr) return -1;
-  SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-  FcTail fc{dh, a2, dlog, h, per_sample, p_w1, m_w1, g_w1, p_b1, m_b1, g_b1,
-            p_w2, m_w2, g_w2, p_b2, m_b2, g_b2, stats, loss_scale};
-  SlabRows sr;
-  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
-  const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
-  hipLaunchKernelGGL(tail_sgd_kernel, dim3(red_blocks + T_NJ1 + T_NJ3), dim3(256), 0,
-                     (hipStream_t)stream, P, B, sr, n, stride, gout, p, buf, hy, fc, step_counter,
-                     red_blocks, g_dbg);
-  return (int)hipGetLastError();
-}
-
-int pto_conv_bwd_fc_supported(int B) { return conv_bwd_fc_supported(B) ? 1 : 0; }
-
-int pto_conv_bwd_lds_bytes() { return F_LDS * (int)sizeof(float); }
 
 }  // extern "C"

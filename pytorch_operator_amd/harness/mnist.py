@@ -15,10 +15,12 @@ MI355X-native differences:
 
 * ``--backend rccl`` (alias of nccl: RCCL over xGMI); ``mpi`` fails clearly;
 * on a GPU the step runs the fused gfx950 kernels (``--kernels hip``, default) on an
-  HBM-resident uint8 dataset, replayed as hipGraphs; DDP gradients go through the
-  xGMI peer-memory all-reduce fused with SGD when its start-up self-test passes
-  (``parallel/xgmi.py``), else two flat-bucket RCCL all-reduces.  ``--kernels torch`` is the plain
-  PyTorch path (also used on CPU with gloo);
+  HBM-resident uint8 dataset, replayed as hipGraphs; DDP gradients go through whichever of
+  the xGMI peer-memory all-reduce fused with SGD (``parallel/xgmi.py``, after its start-up
+  self-test), two stream-launched flat-bucket RCCL all-reduces, or one hipGraph per step with
+  the RCCL collectives captured wins a timed start-up race (``parallel/autotune.py``, the same
+  race ``bench.py`` runs).  ``--kernels torch`` is the plain PyTorch path (also used on CPU with
+  gloo);
 * data: real MNIST IDX files from ``--data-dir`` if present, else the synthetic set
   (no network); by default every rank iterates the full dataset like the reference
   (quirk Q8: no DistributedSampler); ``--shard`` gives each rank a disjoint slice like a
@@ -34,6 +36,9 @@ import math
 import os
 import sys
 import time
+from typing import Optional
+
+_T_MODULE = time.time_ns()  # worker entry when run as ``python -m pytorch_operator_amd.harness.mnist``
 
 
 def parse_args(argv=None):
@@ -65,8 +70,12 @@ def parse_args(argv=None):
                    help="HIP path: replay log-interval hipGraphs, or launch the captured one-step kernel "
                         "list from C++ onto the stream (no per-replay graph-launch gap)")
     p.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"], default="auto",
-                   help="HIP path, world>1: xGMI peer-memory all-reduce fused with SGD (self-tested, "
-                        "RCCL fallback) or RCCL bucket all-reduce")
+                   help="HIP path, world>1: auto = time the xGMI peer-memory all-reduce fused with SGD "
+                        "(self-tested) against RCCL at start-up and keep the faster (parallel/autotune.py); "
+                        "xgmi / rccl force one")
+    p.add_argument("--race-steps", type=int, default=40,
+                   help="training steps each candidate of the --allreduce auto race runs (the state is "
+                        "restored afterwards: the race does not change the trajectory)")
     p.add_argument("--xgmi-timeout", type=float, default=5.0,
                    help="bounded wait (s) inside the xGMI exchange before it flags an error; an error "
                         "ends the worker with the retryable exit code 138")
@@ -121,17 +130,51 @@ def _epoch_perm(n: int, seed: int, epoch: int, rank: int, shard: bool, device):
     return torch.randperm(n, generator=g).to(torch.int32).to(device)
 
 
-def run(args) -> dict:
+def _proc_start_ns() -> Optional[int]:
+    """Wall-clock start of this process (Linux: /proc/self/stat starttime + boot time)."""
+    try:
+        with open("/proc/self/stat") as f:
+            ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/stat") as f:
+            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
+        return int((btime + ticks / os.sysconf("SC_CLK_TCK")) * 1e9)
+    except (OSError, ValueError, StopIteration, IndexError):
+        return None
+
+
+class _Startup:
+    """Wall-clock milestones from process start to the first optimizer step (the pieces of
+    BASELINE's create-to-first-step latency that run inside the pod); emitted as one
+    ``startup`` event with absolute ``unix_ns`` stamps and per-phase seconds."""
+
+    def __init__(self, t_main_ns: Optional[int]):
+        self.marks = [("process_start", _proc_start_ns()), ("worker_main", t_main_ns)]
+
+    def mark(self, name: str) -> None:
+        self.marks.append((name, time.time_ns()))
+
+    def record(self) -> dict:
+        marks = [(k, t) for k, t in self.marks if t is not None]
+        phases = {f"{k}_s": round((t - marks[i - 1][1]) / 1e9, 4) for i, (k, t) in enumerate(marks) if i}
+        return {"marks_unix_ns": dict(marks), "phases": phases}
+
+
+def run(args, t_main_ns: Optional[int] = None) -> dict:
+    startup = _Startup(t_main_ns)
     import torch
     import torch.nn.functional as F
     from ..parallel.dist import init_from_env
+    startup.mark("import_torch")
 
     use_cuda = not args.no_cuda and torch.cuda.is_available()
     if use_cuda:
         print("Using CUDA")  # reference wording; the device is an MI355X over HIP
+        torch.cuda.init()
+        startup.mark("hip_init")
     torch.manual_seed(args.seed)
     env = init_from_env(args.backend, use_gpu=use_cuda)
     rank, world, device = env.rank, env.world_size, env.device
+    startup.mark("process_group")
     emit = _Emitter(rank, args.metrics_file)
     if world > 1:
         print(f"Using distributed PyTorch with {args.backend} backend")
@@ -143,7 +186,12 @@ def run(args) -> dict:
 
     from ..utils.tb_writer import SummaryWriter
     writer = SummaryWriter(args.dir)
+    if kernels == "hip":
+        from ..ops import _native
+        _native.load()
+        startup.mark("hip_library")
     (xtr, ytr), (xte, yte), data_source = _datasets(args, rank, world, device)
+    startup.mark("dataset")
     n = xtr.shape[0]
     B = args.batch_size
     steps_per_epoch = math.ceil(n / B)
@@ -153,9 +201,9 @@ def run(args) -> dict:
          n_train=int(n), steps_per_epoch=steps_per_epoch)
 
     if kernels == "hip":
-        result = _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch)
+        result = _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup)
     else:
-        result = _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch)
+        result = _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup)
     writer.close()
     emit("train_done", **result)
     if world > 1:
@@ -277,7 +325,7 @@ def _log_test(acc, epoch, writer):
     writer.flush()
 
 
-def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> dict:
+def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup) -> dict:
     import torch
     import torch.distributed as dist
     from ..models.mnist import FusedMnistTrainer
@@ -290,16 +338,22 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
     perm = _epoch_perm(n, args.seed, 1, rank, args.shard, dev)
     cursor = torch.zeros(1, dtype=torch.int32, device=dev)
     src = K.BatchSource(xtr, ytr, perm=perm, cursor=cursor)
-    sync = None
+    sync = xg = rccl = None
+    race = False
     if world > 1:
         from ..models.mnist import flat_layout
         from ..parallel.xgmi import try_xgmi
-        sync = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
-                        timeout_s=args.xgmi_timeout) if args.allreduce != "rccl" else None
-        sync = sync or FlatGradAllReduce()
-        emit("grad_allreduce", path="xgmi" if getattr(sync, "fused_sgd", False) else "rccl")
+        rccl = FlatGradAllReduce()
+        xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
+                      timeout_s=args.xgmi_timeout) if args.allreduce != "rccl" else None
+        sync = xg or rccl
+        race = xg is not None and args.allreduce == "auto" and not args.no_graph
+        if not race:
+            emit("grad_allreduce", path="xgmi" if xg is not None else "rccl")
+        startup.mark("grad_sync")
     tr = FusedMnistTrainer(batch_size=B, source=src, lr=args.lr, momentum=args.momentum,
                            device=dev, seed=args.seed, grad_sync=sync)
+    startup.mark("trainer")
     trace = _Trace(args.trace)
     start_epoch = 1
     ck = _load_ckpt(args) if rank == 0 else None
@@ -337,6 +391,8 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
         tr.train_step()
         if steps_done == 0:
             torch.cuda.synchronize(dev)
+            startup.mark("first_step")
+            emit("startup", **startup.record())
             emit("first_step")
         _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer)
         if runner is None and not args.no_graph:
@@ -346,10 +402,23 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> 
             torch.cuda.synchronize(dev)
             t_cap0 = time.perf_counter()
             saved = (tr.flat_params.clone(), tr.flat_momentum.clone())
-            whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
-            runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1, launch=args.launch)
+            if race:
+                # the start-up race of bench.py: every candidate runs real DDP steps, the
+                # fastest (MAX over ranks) is kept; the snapshot restore below undoes the steps
+                from ..parallel.autotune import choose_grad_sync
+                runner, path, trial = choose_grad_sync(tr, rccl, xg, spg=log_iv, trial_steps=args.race_steps,
+                                                       launch=args.launch)
+                sync = runner.sync
+                emit("grad_allreduce", path=path, trial=trial)
+            else:
+                whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
+                runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1, launch=args.launch)
             tr.flat_params.copy_(saved[0])
             tr.flat_momentum.copy_(saved[1])
+            if xg is not None and not getattr(sync, "fused_sgd", False):
+                # step 0 ran the fused xGMI exchange (each rank kept only its momentum shard);
+                # the RCCL step needs every rank's whole buffer
+                xg.xar.gather_sharded_(tr.flat_momentum)
             cursor.fill_(1)
             torch.cuda.synchronize(dev)
             t_capture = time.perf_counter() - t_cap0
@@ -404,7 +473,7 @@ def _evaluate_hip(tr, K, xte, yte, batch_size):
     return tr.evaluate(src, batch_size=min(batch_size, xte.shape[0]))
 
 
-def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -> dict:
+def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup) -> dict:
     import torch
     import torch.nn.functional as F
     from ..models.mnist import Net
@@ -443,6 +512,8 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -
             loss.backward()
             opt.step()
             if steps_done == 0 and batch_idx == 0:
+                startup.mark("first_step")
+                emit("startup", **startup.record())
                 emit("first_step")
             if batch_idx % args.log_interval == 0:
                 _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss.item(), writer)
@@ -470,9 +541,9 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch) -
             "test_loss": round(test_loss, 5), "accuracy": round(acc, 5)}
 
 
-def main(argv=None) -> int:
+def main(argv=None, t_main_ns: Optional[int] = None) -> int:
     args = parse_args(argv)
-    run(args)
+    run(args, t_main_ns if t_main_ns is not None else _T_MODULE)
     return 0
 
 

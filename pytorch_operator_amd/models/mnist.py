@@ -129,12 +129,7 @@ class FusedMnistTrainer:
         self._fm = torch.zeros(L, device=dev)
         self._pv = _views(self._fp, self.layout)
         self.grads = _views(self.flat_grads, self.layout)
-        # fc_sgd "next": device flag "an fc update is pending" (set by the tail, applied and
-        # cleared by the next step's conv12 / fc1_fwd launches, or by flush_deferred())
-        self._pend = torch.zeros(1, device=dev, dtype=torch.int32)
-        self._defer_used = False
-        self._defer_first = False
-        # device batch cursor: advanced by the SGD launch, read by conv1_fwd/head/conv_bwd
+        # device batch cursor: advanced by the SGD launch, read by conv12_fwd / fc1_bwd's staging
         self.cursor = source.cursor if (source is not None and source.cursor is not None) \
             else torch.zeros(1, device=dev, dtype=torch.int32)
         self.load_state_dict(reference_init(seed))
@@ -147,67 +142,27 @@ class FusedMnistTrainer:
         self.source = source
         self._alloc(self.B)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        # schedule knobs (measured on MI355X, see profiles/): conv1+conv2 as one launch
-        # recomputes conv1 4x per sample and loses to two launches; side-stream overlap
-        self.fuse_conv12 = True
-        self.overlap = False
-        # "classic": 6 launches -- conv12_fwd, fc1_fwd<2>, head, fc1_bwd (dz2 beside the fc
-        # weight grads), conv_bwd, slab_reduce_sgd; "fused": 5 launches (head folded into
-        # fc1_bwd_head, fc weight grads + SGD in conv_bwd's idle waves).  Measured on MI355X
-        # (profiles/r2_schedule_ab.md): classic 42.0 us/step, fused 42.75 -- the fold saves
-        # 1.3 us but the fc weight gradients cost more anywhere else than beside dz2.
-        self.schedule = "classic"
-        # round-3 step pieces (A/B knobs, measured in profiles/r3_*):
+        # step knobs (defaults measured on MI355X, docs/kernels.md):
+        #   fuse_conv12: conv1 + conv2 forward as one launch (False: the two standalone kernels)
         #   conv_chunk 4: conv_bwd4 sums dW_conv2 over 4-sample chunks -> the slab the tail
-        #                 reduces is 4x smaller (1: the per-sample conv_bwd of round 2)
-        #   fc_sgd "tail": the tail launch streams fc params / grads / momentum (its span is
-        #                 latency-bound: measured cheaper than "fused", where fc1_bwd's
-        #                 weight-gradient tiles apply the SGD -- updated fc1.weight via w1_next,
-        #                 copied back by the tail -- and become fc1_bwd's critical path)
-        #   stage: fc1_bwd stages the next step's batch; conv12 reads it with one load
-        #   store_fc_grads: also store the fc gradients in the fused-SGD path (inspection)
-        #   fc_sgd "next": the tail leaves the fc update pending; extra grid rows of the next
-        #                 step's conv12 launch apply it (conv12 leaves half of every CU idle).
-        #                 Parameters, momentum and state are flushed on every public access.
+        #                 reduces is 4x smaller (1: the per-sample conv_bwd, the fallback)
+        #   stage_batches: fc1_bwd stages the next step's batch; conv12 reads it with one load
+        self.fuse_conv12 = True
         self.conv_chunk = 4
-        self.fc_sgd = "tail"
         self.stage_batches = True
-        self.store_fc_grads = True
 
     # ---------------------------------------------------------------- state
     @property
     def flat_params(self) -> torch.Tensor:
-        self.flush_deferred()
         return self._fp
 
     @property
     def flat_momentum(self) -> torch.Tensor:
-        self.flush_deferred()
         return self._fm
 
     @property
     def params(self) -> Dict[str, torch.Tensor]:
-        self.flush_deferred()
         return self._pv
-
-    def flush_deferred(self) -> None:
-        """Apply a pending fc_sgd="next" update (conditional on the device flag; no-op when
-        no deferred step ever ran).  Stream-ordered, so callers just use the tensors."""
-        if not self._defer_used:
-            return
-        ce = self.layout.conv_end
-        self.K.sgd_momentum_(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:], lr=self.lr,
-                             momentum=self.momentum, dampening=self.dampening,
-                             weight_decay=self.weight_decay, nesterov=self.nesterov,
-                             first_step=self._defer_first, cond=self._pend)
-        self._pend.zero_()
-        self._defer_first = False
-
-    def _deferred_arg(self) -> dict:
-        ce = self.layout.conv_end
-        return dict(params=self._fp[ce:], grads=self.flat_grads[ce:], buf=self._fm[ce:], pend=self._pend,
-                    lr=self.lr, momentum=self.momentum, dampening=self.dampening,
-                    weight_decay=self.weight_decay, nesterov=self.nesterov, first_step=self._defer_first)
 
     def _alloc(self, B: int):
         dev = self.device
@@ -224,7 +179,6 @@ class FusedMnistTrainer:
         self.per_sample = torch.empty((B, 2), device=dev)
         self.fc1_ks = self.K.fc1_split()
         self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
-        self.w1_next = torch.empty((500, 800), device=dev)  # fused-SGD fc1.weight (tail copies back)
         self.stage = K_stage(self.source, B, dev)
         # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
         # (conv_bwd4) per-4-sample-chunk rows for conv2.weight
@@ -252,36 +206,25 @@ class FusedMnistTrainer:
 
     # ---------------------------------------------------------------- step
     #
-    # Launch schedules of one single-process step (one hipGraph; ``self.schedule``):
+    # One single-process step is six launches (one hipGraph, or the captured kernel list
+    # launched from C++ -- parallel/graphed_step.py):
     #
-    #   classic: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd -> slab_reduce_sgd
-    #   fused:   conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head -> conv_bwd(+fc) -> slab_reduce_sgd
+    #   conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd (+ next-batch staging) -> conv_bwd4
+    #   -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor advance)
     #
-    # fc1_bwd_head rebuilds the head (h, log-softmax/NLL, dh) per 16-sample tile and computes
-    # dz2, the critical path into the conv backward; conv_bwd's idle waves compute the fc
-    # weight gradients and apply their SGD; the tail reduces the per-sample conv gradients
-    # and updates the conv parameters.  DDP (xGMI) uses the same launches with the fc
-    # gradients only written (the exchange kernel updates every parameter).  Batches other
-    # than 59..64 compute the fc gradients in their own launch (fc1_bwd / tail_sgd).
-    def _side_stream(self) -> torch.cuda.Stream:
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        return self._side
-
-    def _stage_for(self, source) -> object:
-        return self.stage if (self.stage_batches and self.stage is not None and
-                              (source is None or source is self.source)) else None
-
+    # DDP: with the xGMI kernel the tail launch is the cross-GPU exchange + SGD
+    # (parallel/xgmi.py); with RCCL the fc / conv buckets are all-reduced between the pieces.
     def invalidate_stage(self) -> None:
         """Drop the staged next batch (call after changing the source's perm in place)."""
         if self.stage is not None:
             self.stage.invalidate()
 
-    def forward(self, source=None, B: Optional[int] = None, _defer: bool = False) -> None:
-        """conv12_fwd + split-K fc1 (the head runs inside fc1_bwd_head).  ``_defer``
-        (fc_sgd "next" steps): conv12 applies the pending fc update instead of a flush."""
-        if not _defer:
-            self.flush_deferred()
+    def _stage_for(self, source) -> object:
+        return self.stage if (self.stage_batches and self.stage is not None and
+                              (source is None or source is self.source)) else None
+
+    def forward(self, source=None, B: Optional[int] = None) -> None:
+        """conv12_fwd (or conv1_fwd + conv2_fwd) + split-K fc1 (the head finishes h)."""
         K, p = self.K, self._pv
         src = source or self.source
         B = self.B if B is None else B
@@ -289,16 +232,14 @@ class FusedMnistTrainer:
             K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
                          p["conv2.bias"], B, a1=self.a1[:B], idx1=self.idx1[:B], xn=self.xn[:B],
                          lab=self.lab[:B], a2=self.a2[:B], idx2=self.idx2[:B],
-                         stage=self._stage_for(source), deferred=self._deferred_arg() if _defer else None)
+                         stage=self._stage_for(source))
         else:
             K.conv1_fwd(src, p["conv1.weight"], p["conv1.bias"], B, out=self.a1[:B],
                         idx=self.idx1[:B], xn=self.xn[:B], lab=self.lab[:B])
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
-        # split-K fc1 (256 workgroups); fc1_bwd_head adds the halves + bias and applies ReLU
         ks = self.fc1_ks
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500),
-                        clear=self._pend if _defer else None)
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500))
 
     def _head(self, B: int) -> None:
         """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
@@ -308,41 +249,15 @@ class FusedMnistTrainer:
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
-    def _fc1_bwd_head(self, B: int) -> None:
-        K, p = self.K, self._pv
-        K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"],
-                       p["fc2.bias"], self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"],
-                       grad_scale=1.0 / B, dz2=self.dz2[:B], h_out=self.h1[:B], dh=self.dh[:B],
-                       dlogits=self.dlogits[:B], per_sample=self.per_sample[:B])
-
-    def _fc1_bwd(self, B: int, jobs: int, stage_adv: Optional[int] = None) -> None:
+    def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None) -> None:
         """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv."""
         K, p, g = self.K, self._pv, self.grads
-        st = self._stage_for(None) if stage_adv is not None and jobs == K.FC1_BWD_ALL else None
+        st = self._stage_for(None) if stage_adv is not None else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
                   dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
-                  loss_scale=1.0 / B, jobs=jobs, src=self.source if st is not None else None, stage=st,
-                  stage_adv=stage_adv or 0)
-
-    def _conv_bwd_fc(self, B: int, sgd: bool) -> None:
-        """conv backward + fc weight grads (+ their SGD when ``sgd``) in one launch."""
-        K, p = self.K, self._pv
-        fp, fm, fg = self._fc_dicts()
-        self._last_big = None  # per-sample slab rows
-        K.conv_bwd_fc(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
-                      self.conv_slab, self.slab_views, dh=self.dh[:B], a2=self.a2[:B],
-                      dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
-                      fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
-                      fc_params=fp if sgd else None, fc_bufs=fm if sgd else None, lr=self.lr,
-                      momentum=self.momentum, dampening=self.dampening,
-                      weight_decay=self.weight_decay, nesterov=self.nesterov,
-                      first_step=self._first_step)
-
-    def _fc_in_conv(self, B: int) -> bool:
-        if getattr(self, "_fc_in_conv_B", None) != B:
-            self._fc_in_conv_B, self._fc_in_conv_ok = B, self.K.conv_bwd_fc_supported(B)
-        return self._fc_in_conv_ok
+                  loss_scale=1.0 / B, jobs=K.FC1_BWD_ALL, src=self.source if st is not None else None,
+                  stage=st, stage_adv=stage_adv or 0)
 
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self._pv
@@ -361,19 +276,6 @@ class FusedMnistTrainer:
         """Chunk-row geometry of the slab the last conv backward wrote (None: per-sample rows)."""
         return getattr(self, "_last_big", None)
 
-    def _fc1_bwd_sgd(self, B: int, advance_cursor: bool) -> None:
-        """fc1_bwd with the fc SGD fused in (updated fc1.weight -> w1_next) + next-batch staging."""
-        K, p = self.K, self._pv
-        fp, fm, fg = self._fc_dicts()
-        st = self._stage_for(None)
-        K.fc1_bwd_sgd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
-                      self.h1[:B], dz2=self.dz2[:B], w1_next=self.w1_next, params=fp, bufs=fm,
-                      grads=fg if self.store_fc_grads else None, per_sample=self.per_sample[:B],
-                      stats=self.stats, loss_scale=1.0 / B, lr=self.lr, momentum=self.momentum,
-                      dampening=self.dampening, weight_decay=self.weight_decay, nesterov=self.nesterov,
-                      first_step=self._first_step, src=self.source if st is not None else None, stage=st,
-                      stage_adv=1 if advance_cursor else 0)
-
     def _sgd(self, lo: int, hi: int, grad_scale: float, advance_cursor: bool) -> None:
         self.K.sgd_momentum_(self._fp[lo:hi], self.flat_grads[lo:hi],
                              self._fm[lo:hi], lr=self.lr, momentum=self.momentum,
@@ -386,12 +288,8 @@ class FusedMnistTrainer:
         """Forward + loss + fc backward (the fc bucket and dz2 are complete after this)."""
         B = self.B if B is None else B
         self.forward(source, B)
-        if self.schedule == "classic":
-            self._head(B)
-            self._fc1_bwd(B, self.K.FC1_BWD_ALL)
-        else:
-            self._fc1_bwd_head(B)
-            self._fc1_bwd(B, self.K.FC1_BWD_WGRAD | self.K.FC1_BWD_FC2)
+        self._head(B)
+        self._fc1_bwd(B)
 
     def backward_conv(self, source=None, B: Optional[int] = None) -> None:
         """conv backward + deterministic slab reduction into the conv bucket."""
@@ -409,126 +307,49 @@ class FusedMnistTrainer:
             self.grad_sync.conv_ready(self.conv_bucket())
 
     def optimizer_step(self, advance_cursor: bool = True, grad_scale: Optional[float] = None) -> None:
-        self.flush_deferred()
         if grad_scale is None:
             grad_scale = self.grad_sync.finish() if self.grad_sync is not None else 1.0
         self._sgd(0, self.layout.total, grad_scale, advance_cursor)
         self._first_step = False
 
-    def _fc_dicts(self):
-        names = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
-        mom = _views(self._fm, self.layout)
-        return ({k: self._pv[k] for k in names}, {k: mom[k] for k in names},
-                {k: self.grads[k] for k in names})
-
-    def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True,
-                   overlap: Optional[bool] = None):
+    def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True):
         """One full training step (forward, backward, [all-reduce], SGD)."""
-        overlap = self.overlap if overlap is None else overlap
-        defer = (self.fc_sgd == "next" and self.grad_sync is None and not overlap and
-                 self.schedule == "classic" and self.fuse_conv12)
-        if not defer:
-            self.flush_deferred()
+        B = self.B if B is None else B
         if getattr(self.grad_sync, "fused_sgd", False):
             # xGMI path: one kernel reduces the per-sample conv-grad slabs, does the
             # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
             # updated parameters (parallel/xgmi.py).  flat_grads[:conv_end] is not written.
-            B_ = self.B if B is None else B
-            self.forward(source, B_)
-            if self.schedule == "classic":
-                self._head(B_)
-                self._fc1_bwd(B_, self.K.FC1_BWD_ALL)
-                self._conv_bwd(B_)
-            else:
-                self._fc1_bwd_head(B_)
-                if self._fc_in_conv(B_):
-                    self._conv_bwd_fc(B_, sgd=False)
-                else:
-                    self._fc1_bwd(B_, self.K.FC1_BWD_WGRAD | self.K.FC1_BWD_FC2)
-                    self._conv_bwd(B_)
+            self.forward(source, B)
+            self._head(B)
+            self._fc1_bwd(B)
+            self._conv_bwd(B)
             self.grad_sync.xar.allreduce_sgd_(
                 self.flat_grads, self._fp, self._fm, lr=self.lr,
                 momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
                 nesterov=self.nesterov, first_step=self._first_step,
                 step_counter=self.cursor if advance_cursor else None,
-                slab=self.conv_slab, slab_rows=B_, conv_n=self.layout.conv_end,
-                slab_big=self._slab_big(B_))
+                slab=self.conv_slab, slab_rows=B, conv_n=self.layout.conv_end,
+                slab_big=self._slab_big(B))
             self._first_step = False
             return
         if self.grad_sync is not None:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return
+        # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
         K = self.K
-        B = self.B if B is None else B
         ce = self.layout.conv_end
-        if not overlap and self.schedule == "classic":
-            # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd -> tail
-            self.forward(source, B, _defer=defer)
-            self._head(B)
-            fused_sgd = self.fc_sgd == "fused"
-            if fused_sgd:
-                self._fc1_bwd_sgd(B, advance_cursor)
-            else:
-                self._fc1_bwd(B, K.FC1_BWD_ALL, stage_adv=1 if advance_cursor else 0)
-            self._conv_bwd(B)
-            w1 = self._pv["fc1.weight"]
-            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
-                               self._fm[:ce], lr=self.lr, momentum=self.momentum,
-                               dampening=self.dampening, weight_decay=self.weight_decay,
-                               nesterov=self.nesterov, first_step=self._first_step,
-                               step_counter=self.cursor if advance_cursor else None,
-                               extra=None if (fused_sgd or defer) else
-                               (self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
-                               big=self._slab_big(B), copy=(self.w1_next, w1) if fused_sgd else None,
-                               set_pend=self._pend if defer else None)
-            if defer:
-                self._defer_used, self._defer_first = True, self._first_step
-            self._first_step = False
-            return
-        if not overlap and self._fc_in_conv(B):
-            self.forward(source, B)
-            self._fc1_bwd_head(B)
-            self._conv_bwd_fc(B, sgd=True)
-            K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
-                               self._fm[:ce], lr=self.lr, momentum=self.momentum,
-                               dampening=self.dampening, weight_decay=self.weight_decay,
-                               nesterov=self.nesterov, first_step=self._first_step,
-                               step_counter=self.cursor if advance_cursor else None)
-            self._first_step = False
-            return
-        if not overlap:
-            self.forward(source, B)
-            self._fc1_bwd_head(B)
-            self._conv_bwd(B)
-            fp, fm, fg = self._fc_dicts()
-            K.tail_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
-                        self._fm[:ce], big=self._slab_big(B), dh=self.dh[:B], a2=self.a2[:B],
-                        dlogits=self.dlogits[:B], h=self.h1[:B], per_sample=self.per_sample[:B],
-                        fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=self.stats, loss_scale=1.0 / B,
-                        lr=self.lr, momentum=self.momentum, dampening=self.dampening,
-                        weight_decay=self.weight_decay, nesterov=self.nesterov,
-                        first_step=self._first_step,
-                        step_counter=self.cursor if advance_cursor else None)
-            self._first_step = False
-            return
-        # side-stream variant (measured slower on MI355X, kept for A/B): fc weight grads and
-        # their SGD beside the conv backward
-        main = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
         self.forward(source, B)
-        self._fc1_bwd_head(B)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)
-            self._sgd(ce, self.layout.total, 1.0, False)
+        self._head(B)
+        self._fc1_bwd(B, stage_adv=1 if advance_cursor else 0)
         self._conv_bwd(B)
         K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
                            self._fm[:ce], lr=self.lr, momentum=self.momentum,
                            dampening=self.dampening, weight_decay=self.weight_decay,
                            nesterov=self.nesterov, first_step=self._first_step,
-                           step_counter=self.cursor if advance_cursor else None, big=self._slab_big(B))
-        main.wait_stream(side)
+                           step_counter=self.cursor if advance_cursor else None,
+                           extra=(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
+                           big=self._slab_big(B))
         self._first_step = False
 
     def loss(self) -> float:
@@ -546,7 +367,6 @@ class FusedMnistTrainer:
             raise ValueError("graph capture needs a BatchSource with a device cursor")
         if self._first_step:
             self.train_step()
-            self.flush_deferred()  # a deferred first-step update must not be baked into the graph
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):

@@ -120,29 +120,19 @@ _SIGNATURES = {
     "pto_mnist_conv1_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F, _VP, _VP, _VP, _VP, _I, _VP,
                             _I, _VP, _VP, _VP],
     "pto_mnist_conv2_fwd": [_VP, _VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_conv12_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F] + [_VP] * 10 + [_I, _VP, _VP, _VP]
-                            + [_VP, _VP, _VP, _I, _VP] + [_F] * 5 + [_I, _I, _VP],
+    "pto_mnist_conv12_fwd": [_VP, _I, _VP, _VP, _VP, _I, _I, _F, _F] + [_VP] * 10 + [_I, _VP, _VP, _VP, _VP],
     "pto_slab_reduce_sgd": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
-                            _VP, _VP, _VP, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP],
+                            _VP, _VP, _VP, _I, _I, _I, _I, _VP],
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
-    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP, _VP],
+    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_ks": [],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
-    "pto_mnist_fc1_bwd_sgd": [_VP] * 13 + [_F, _I] + [_VP] * 8 + [_F] * 5 + [_I, _I] + [_VP] * 4
-                             + [_I, _I, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
-    "pto_mnist_stage_batch": [_VP, _VP, _VP, _VP, _I, _I, _I, _VP, _VP, _VP, _VP],
-    "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _VP],
-    "pto_conv_bwd_lds_bytes": [],
-    "pto_conv_bwd_fc_supported": [_I],
-    "pto_mnist_conv_bwd_fc": [_VP] * 9 + [_I, _I, _I] + [_VP] * 18 + [_F] * 6 + [_I, _I, _VP],
-    "pto_mnist_fc1_bwd_head": [_VP] * 8 + [_F] + [_VP] * 5 + [_I, _VP],
-    "pto_mnist_tail_sgd": [_VP, _I, _I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP]
-                          + [_VP] * 18 + [_F, _VP],
+    "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     # xgmi_allreduce.hip
     "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],
     "pto_xar_open": [_VP, _VP],

@@ -151,8 +151,8 @@ def conv2_fwd(a1: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
 
 class BatchStage:
     """Device staging slot for the NEXT step's batch (uint8 pixels [B, 784], int32 labels,
-    and the step number they belong to).  ``fc1_bwd_sgd`` fills it during step t for step
-    t + 1; ``conv12_fwd(..., stage=)`` then reads the batch with one load instead of the
+    and the step number they belong to).  ``fc1_bwd(..., stage=)`` fills it during step t for
+    step t + 1; ``conv12_fwd(..., stage=)`` then reads the batch with one load instead of the
     cursor -> permutation -> pixel chain, and falls back to the gather on its own whenever the
     tag is not the current cursor (first step, or the cursor was moved from the host)."""
 
@@ -173,13 +173,9 @@ class BatchStage:
 
 def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
                b2: torch.Tensor, B: int, a1=None, idx1=None, xn=None, lab=None, a2=None,
-               idx2=None, stage: Optional[BatchStage] = None, deferred: Optional[dict] = None):
+               idx2=None, stage: Optional[BatchStage] = None):
     """conv1+pool+conv2+pool fused (one launch): returns (a1, idx1, xn, lab, a2, idx2).
-    ``stage``: take the batch from a ``BatchStage`` when its tag matches the cursor.
-    ``deferred``: dict(params, grads, buf, pend, lr, momentum, dampening, weight_decay,
-    nesterov, grad_scale, first_step) -- extra grid rows apply SGD(momentum) to the flat
-    range when the int32 device flag ``pend`` is non-zero (an update deferred from the
-    previous step; ``fc1_fwd_parts(clear=pend)`` clears the flag after this launch)."""
+    ``stage``: take the batch from a ``BatchStage`` when its tag matches the cursor."""
     lib = _native.load()
     src.check_batch(B)
     _req(w1, (20, 1, 5, 5), torch.float32, "conv1.weight")
@@ -208,27 +204,12 @@ def conv12_fwd(src: BatchSource, w1: torch.Tensor, b1: torch.Tensor, w2: torch.T
             raise ValueError("a staged batch needs a uint8 source with labels, perm and a device cursor")
         if stage.B < B:
             raise ValueError("stage holds fewer samples than B")
-    d = deferred or {}
-    sg_n = 0
-    if deferred is not None:
-        sg_n = d["params"].numel()
-        for t, nm in ((d["params"], "params"), (d["grads"], "grads"), (d["buf"], "buf")):
-            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != sg_n or t.data_ptr() % 16:
-                raise ValueError(f"deferred {nm} must be 16-byte aligned contiguous fp32 with {sg_n} elements")
-        if sg_n % 4:
-            raise ValueError("deferred range must be a multiple of 4 elements")
-        if d["pend"].dtype != torch.int32:
-            raise ValueError("deferred pend flag must be int32")
     rc = lib.pto_mnist_conv12_fwd(
         src.x.data_ptr(), int(src.is_u8), _ptr(src.labels), _ptr(src.perm), _ptr(src.cursor),
         src.host_offset, src.n_total, src.scale, src.shift, w1.data_ptr(), b1.data_ptr(),
         w2.data_ptr(), b2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(), _ptr(lab),
         a2.data_ptr(), idx2.data_ptr(), B, _ptr(stage.x if stage else None),
-        _ptr(stage.lab if stage else None), _ptr(stage.tag if stage else None),
-        _ptr(d.get("params")), _ptr(d.get("grads")), _ptr(d.get("buf")), sg_n, _ptr(d.get("pend")),
-        float(d.get("lr", 0.0)), float(d.get("momentum", 0.0)), float(d.get("dampening", 0.0)),
-        float(d.get("weight_decay", 0.0)), float(d.get("grad_scale", 1.0)), int(d.get("nesterov", False)),
-        int(d.get("first_step", False)), _stream())
+        _ptr(stage.lab if stage else None), _ptr(stage.tag if stage else None), _stream())
     _native.check(rc, "conv12_fwd")
     return a1, idx1, xn, lab, a2, idx2
 
@@ -249,19 +230,19 @@ def fc1_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
     return out
 
 
+FC1_KS = 2  # K split of the training-path fc1 (FC1_KS of mnist_kernels.hip)
+
+
 def fc1_split() -> int:
-    """K split of the training-path fc1 (compile-time ``PTO_FC1_KS`` of the library: 2)."""
-    return int(_native.load().pto_mnist_fc1_ks())
+    """K split of the training-path fc1: 2 (256 workgroups)."""
+    return FC1_KS
 
 
-def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  clear: Optional[torch.Tensor] = None) -> torch.Tensor:
+def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Split-K fc1 forward: the pre-activation partials ``out[z] = x[:, Kz] @ w[:, Kz].T`` over
-    ``fc1_split()`` K slices (2 x 400) as fp32 [KS, B, 500]; ``head(..., h_second=out[1],
-    fc1_bias=b, h_out=h)`` finishes ``h = relu(out[0] + out[1] + ... + b)`` (the partials after
-    ``out[1]`` are read from the same buffer).  256 workgroups instead of 128: half the operand
-    bytes per CU on the latency-bound load phase.  ``clear``: int32 device flag set to 0 by the
-    launch (conv12_fwd's deferred-SGD flag)."""
+    2 K slices (2 x 400) as fp32 [2, B, 500]; ``head(..., h_second=out[1], fc1_bias=b,
+    h_out=h)`` finishes ``h = relu(out[0] + out[1] + b)``.  256 workgroups instead of 128: half
+    the operand bytes per CU on the latency-bound load phase."""
     lib = _native.load()
     B = x.shape[0]
     ks = fc1_split()
@@ -269,7 +250,7 @@ def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
     _req(w, (500, 800), torch.float32, "fc1.weight")
     out = torch.empty((ks, B, 500), device=x.device) if out is None else out
     _req(out, (ks, B, 500), torch.float32, "fc1 partials")
-    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _ptr(clear), _stream())
+    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _stream())
     _native.check(rc, "fc1_fwd_parts")
     return out
 
@@ -381,157 +362,6 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     return dz2
 
 
-def fc1_bwd_sgd(dh, a2, idx2, w1, dlogits, h, *, dz2, w1_next, params: dict, bufs: dict,
-                grads: Optional[dict] = None, per_sample=None, stats=None, loss_scale: float = 1.0,
-                lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-                src: Optional[BatchSource] = None, stage: Optional[BatchStage] = None,
-                stage_adv: int = 1):
-    """fc1_bwd (dz2, dW_fc1, db_fc1, dW_fc2, db_fc2, loss statistics) with the SGD(momentum)
-    of every fc parameter fused into the weight-gradient tiles: the updated fc1.weight is
-    written to ``w1_next`` (this launch's dz2 job still reads ``w1``; copy it back after the
-    launch -- ``slab_reduce_sgd_(copy=...)`` does), fc1.bias / fc2.* and all fc momentum
-    buffers are updated in place.  ``params`` / ``bufs`` / ``grads``: dicts of the fc1/fc2
-    weight/bias tensors (``grads`` optional: stored when given).  With ``src`` + ``stage``,
-    ceil(B/4) extra blocks stage the batch of step ``cursor + stage_adv``."""
-    lib = _native.load()
-    B = dh.shape[0]
-    _req(dh, (B, 500), torch.float32, "dh")
-    _req(a2, (B, 800), torch.float32, "a2")
-    _req(idx2, (B, 800), torch.uint8, "idx2")
-    _req(w1, (500, 800), torch.float32, "fc1.weight")
-    _req(w1_next, (500, 800), torch.float32, "fc1.weight (next)")
-    if w1_next.data_ptr() == w1.data_ptr():
-        raise ValueError("w1_next must not alias w1")
-    _req(dlogits, (B, 10), torch.float32, "dlogits")
-    _req(h, (B, 500), torch.float32, "h1")
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
-    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
-    for k, shp in shapes.items():
-        _req(bufs[k], shp, torch.float32, f"{k} momentum")
-        if k != "fc1.weight":
-            _req(params[k], shp, torch.float32, f"{k} param")
-        if grads is not None:
-            _req(grads[k], shp, torch.float32, f"{k} grad")
-    if per_sample is not None:
-        _req(per_sample, (B, 2), torch.float32, "per_sample")
-    g = (lambda k: _ptr(grads[k])) if grads is not None else (lambda k: None)
-    if stage is not None:
-        if src is None or not BatchStage.supported(src):
-            raise ValueError("staging needs a uint8 BatchSource with labels, perm and a device cursor")
-        if stage.B < B:
-            raise ValueError("stage holds fewer samples than B")
-        if src.x.data_ptr() % 16:
-            raise ValueError("source pixels must be 16-byte aligned")
-    st = stage is not None
-    rc = lib.pto_mnist_fc1_bwd_sgd(
-        dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
-        g("fc1.weight"), g("fc1.bias"), g("fc2.weight"), g("fc2.bias"), dz2.data_ptr(), _ptr(per_sample),
-        _ptr(stats), float(loss_scale), B, w1_next.data_ptr(), bufs["fc1.weight"].data_ptr(),
-        params["fc1.bias"].data_ptr(), bufs["fc1.bias"].data_ptr(), params["fc2.weight"].data_ptr(),
-        bufs["fc2.weight"].data_ptr(), params["fc2.bias"].data_ptr(), bufs["fc2.bias"].data_ptr(),
-        float(lr), float(momentum), float(dampening), float(weight_decay), float(grad_scale), int(nesterov),
-        int(first_step), _ptr(src.x) if st else None, _ptr(src.labels) if st else None,
-        _ptr(src.perm) if st else None, _ptr(src.cursor) if st else None, src.n_total if st else 0,
-        int(stage_adv), _ptr(stage.x) if st else None, _ptr(stage.lab) if st else None,
-        _ptr(stage.tag) if st else None, _stream())
-    _native.check(rc, "fc1_bwd_sgd")
-    return dz2
-
-
-def stage_batch(src: BatchSource, stage: BatchStage, B: int, adv: int = 0) -> None:
-    """Gather the batch of step ``cursor + adv`` into ``stage`` (one small launch)."""
-    lib = _native.load()
-    if not BatchStage.supported(src):
-        raise ValueError("staging needs a uint8 BatchSource with labels, perm and a device cursor")
-    if stage.B < B or src.x.data_ptr() % 16:
-        raise ValueError("stage too small or unaligned source")
-    rc = lib.pto_mnist_stage_batch(src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(),
-                                   src.cursor.data_ptr(), src.n_total, int(B), int(adv), stage.x.data_ptr(),
-                                   stage.lab.data_ptr(), stage.tag.data_ptr(), _stream())
-    _native.check(rc, "stage_batch")
-
-
-def fc1_bwd_head(hp: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-                 lab: torch.Tensor, a2: torch.Tensor, idx2: torch.Tensor, w1: torch.Tensor, *,
-                 grad_scale: float, dz2: torch.Tensor, h_out: torch.Tensor, dh: torch.Tensor,
-                 dlogits: torch.Tensor, per_sample: torch.Tensor) -> torch.Tensor:
-    """fc1 input gradient with the head folded in (one launch).
-
-    From the split-K fc1 halves ``hp`` ([2, B, 500], ``fc1_fwd_parts``) every block rebuilds
-    h = relu(hp[0] + hp[1] + b1), logits, log-softmax, NLL and dh for its 16 samples, then
-    computes dz2 = unpool(relu'(dh . W1)).  Also writes h_out, dh, dlogits (scaled by
-    ``grad_scale``) and per_sample (loss, correct) for the weight-gradient launches.
-    """
-    lib = _native.load()
-    B = a2.shape[0]
-    _req(hp, (2, B, 500), torch.float32, "fc1 partials")
-    _req(b1, (500,), torch.float32, "fc1.bias")
-    _req(w2, (10, 500), torch.float32, "fc2.weight")
-    _req(b2, (10,), torch.float32, "fc2.bias")
-    _req(lab, (B,), torch.int32, "lab")
-    _req(a2, (B, 800), torch.float32, "a2")
-    _req(idx2, (B, 800), torch.uint8, "idx2")
-    _req(w1, (500, 800), torch.float32, "fc1.weight")
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
-    _req(h_out, (B, 500), torch.float32, "h_out")
-    _req(dh, (B, 500), torch.float32, "dh")
-    _req(dlogits, (B, 10), torch.float32, "dlogits")
-    _req(per_sample, (B, 2), torch.float32, "per_sample")
-    rc = lib.pto_mnist_fc1_bwd_head(hp.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-                                    lab.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
-                                    float(grad_scale), dz2.data_ptr(), h_out.data_ptr(),
-                                    dh.data_ptr(), dlogits.data_ptr(), per_sample.data_ptr(), B,
-                                    _stream())
-    _native.check(rc, "fc1_bwd_head")
-    return dz2
-
-
-def tail_sgd_(slab: torch.Tensor, B: int, conv_grads: torch.Tensor, conv_params: torch.Tensor,
-              conv_buf: torch.Tensor, *, dh, a2, dlogits, h, per_sample, fc_params: dict,
-              fc_bufs: dict, fc_grads: dict, stats: Optional[torch.Tensor], loss_scale: float,
-              lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-              nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-              step_counter: Optional[torch.Tensor] = None, big: Optional[tuple] = None) -> None:
-    """Single-process step tail (one launch): conv grads = sum of the slab rows + SGD on the
-    conv params; dW_fc1 = dh^T a2, db_fc1, dW_fc2 = dlogits^T h, db_fc2, each with its SGD
-    applied in the epilogue (grads also stored); loss statistics; cursor advance.
-    ``fc_params`` / ``fc_bufs`` / ``fc_grads``: dicts of the fc1/fc2 weight/bias tensors."""
-    lib = _native.load()
-    n = conv_params.numel()
-    for t, nm in ((conv_grads, "conv grads"), (conv_params, "conv params"), (conv_buf, "conv momentum")):
-        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
-            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
-    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
-            slab.shape[1] < n or slab.shape[0] < B:
-        raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
-    _req(dh, (B, 500), torch.float32, "dh")
-    _req(a2, (B, 800), torch.float32, "a2")
-    _req(dlogits, (B, 10), torch.float32, "dlogits")
-    _req(h, (B, 500), torch.float32, "h")
-    _req(per_sample, (B, 2), torch.float32, "per_sample")
-    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
-    ptrs = []
-    for k, shp in shapes.items():
-        for d, nm in ((fc_params, "param"), (fc_bufs, "momentum"), (fc_grads, "grad")):
-            _req(d[k], shp, torch.float32, f"{k} {nm}")
-            ptrs.append(d[k].data_ptr())
-    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
-        raise ValueError("stats must be fp32 with >= 2 elements")
-    if step_counter is not None and (step_counter.dtype != torch.int32 or not step_counter.is_cuda):
-        raise ValueError("step_counter must be int32 CUDA")
-    rb, lo, hi = big if big is not None else (B, 0, 0)
-    rc = lib.pto_mnist_tail_sgd(slab.data_ptr(), B, n, slab.shape[1], int(rb), int(lo), int(hi),
-                                conv_grads.data_ptr(),
-                                conv_params.data_ptr(), conv_buf.data_ptr(), float(lr),
-                                float(momentum), float(dampening), float(weight_decay),
-                                float(grad_scale), int(nesterov), int(first_step),
-                                _ptr(step_counter), dh.data_ptr(), a2.data_ptr(), dlogits.data_ptr(),
-                                h.data_ptr(), per_sample.data_ptr(), *ptrs, _ptr(stats),
-                                float(loss_scale), _stream())
-    _native.check(rc, "tail_sgd")
-
-
 def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
              slab: Optional[torch.Tensor] = None):
     """conv2 weight/bias grads, dz1 (internal), conv1 weight/bias grads.
@@ -604,61 +434,6 @@ def conv_bwd4_rows(B: int, offsets: dict) -> tuple:
     return ((B + 3) // 4, lo, lo + 25000)
 
 
-def conv_bwd_fc_supported(B: int) -> bool:
-    """Whether conv_bwd can carry every fc weight-gradient tile in its idle waves (B 59..64)."""
-    return bool(_native.load().pto_conv_bwd_fc_supported(int(B)))
-
-
-def conv_bwd_fc(dz2, w2, a1, idx1, xn, slab: torch.Tensor, slab_views: dict, *, dh, a2, dlogits, h,
-                per_sample, fc_grads: dict, stats: Optional[torch.Tensor], loss_scale: float,
-                fc_params: Optional[dict] = None, fc_bufs: Optional[dict] = None, lr: float = 0.0,
-                momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False) -> None:
-    """conv_bwd (per-sample slab rows) + the fc weight gradients dW_fc1 = dh^T a2, db_fc1,
-    dW_fc2 = dlogits^T h, db_fc2 and the loss statistics, computed in the conv kernel's idle
-    waves (one launch).  With ``fc_params``/``fc_bufs`` the SGD(momentum) update of the fc
-    parameters is applied in the same epilogue (the gradients are still written)."""
-    lib = _native.load()
-    B = dz2.shape[0]
-    if not conv_bwd_fc_supported(B):
-        raise ValueError(f"conv_bwd_fc needs B in 59..64 (got {B}); use conv_bwd + fc1_bwd")
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
-    _req(w2, (50, 20, 5, 5), torch.float32, "conv2.weight")
-    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
-    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
-    _req(xn, (B, 784), torch.float32, "xn")
-    _req(dh, (B, 500), torch.float32, "dh")
-    _req(a2, (B, 800), torch.float32, "a2")
-    _req(dlogits, (B, 10), torch.float32, "dlogits")
-    _req(h, (B, 500), torch.float32, "h")
-    _req(per_sample, (B, 2), torch.float32, "per_sample")
-    if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
-        raise ValueError("slab must be contiguous fp32 [>=B, S]")
-    lo, hi = slab.data_ptr(), slab.data_ptr() + slab.shape[1] * 4
-    sv = [slab_views[k] for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
-    for t in sv:
-        if not (lo <= t.data_ptr() and t.data_ptr() + t.numel() * 4 <= hi):
-            raise ValueError("slab views must lie inside slab[0]")
-    shapes = {"fc1.weight": (500, 800), "fc1.bias": (500,), "fc2.weight": (10, 500), "fc2.bias": (10,)}
-    sgd = fc_params is not None
-    ptrs = []
-    for k, shp in shapes.items():
-        _req(fc_grads[k], shp, torch.float32, f"{k} grad")
-        if sgd:
-            _req(fc_params[k], shp, torch.float32, f"{k} param")
-            _req(fc_bufs[k], shp, torch.float32, f"{k} momentum")
-        ptrs += [_ptr(fc_params[k]) if sgd else None, _ptr(fc_bufs[k]) if sgd else None, fc_grads[k].data_ptr()]
-    if stats is not None and (stats.dtype != torch.float32 or stats.numel() < 2):
-        raise ValueError("stats must be fp32 with >= 2 elements")
-    rc = lib.pto_mnist_conv_bwd_fc(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
-                                   *[t.data_ptr() for t in sv], slab.shape[1], B, 2 if sgd else 1,
-                                   dh.data_ptr(), a2.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
-                                   per_sample.data_ptr(), *ptrs, _ptr(stats), float(loss_scale), float(lr),
-                                   float(momentum), float(dampening), float(weight_decay), float(grad_scale),
-                                   int(nesterov), int(first_step), _stream())
-    _native.check(rc, "conv_bwd_fc")
-
-
 def slab_reduce(slab: torch.Tensor, B: int, out: torch.Tensor, big: Optional[tuple] = None) -> torch.Tensor:
     """out[o] = sum_{b<B} slab[b, o] for o < out.numel() (deterministic order).
     ``big = (rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows
@@ -683,15 +458,12 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                      dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                      grad_scale: float = 1.0, first_step: bool = False,
                      step_counter: Optional[torch.Tensor] = None,
-                     extra: Optional[tuple] = None, big: Optional[tuple] = None,
-                     copy: Optional[tuple] = None, set_pend: Optional[torch.Tensor] = None) -> None:
+                     extra: Optional[tuple] = None, big: Optional[tuple] = None) -> None:
     """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch).
 
     ``extra=(params2, grads2, buf2)``: also apply the same SGD to a second,
     already-reduced range in the same launch (e.g. the fc parameters).
     ``big=(rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows.
-    ``copy=(src, dst)``: also copy ``src`` into ``dst`` (equal-size contiguous fp32).
-    ``set_pend``: int32 device flag set to 1 (a deferred update is pending, see conv12_fwd).
     """
     lib = _native.load()
     n = params.numel()
@@ -710,20 +482,11 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
             if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n2:
                 raise ValueError(f"{nm} must be contiguous fp32 with {n2} elements")
     rb, lo, hi = big if big is not None else (B, 0, 0)
-    cs = cd = None
-    cn = 0
-    if copy is not None:
-        cs, cd = copy
-        if cs.dtype != torch.float32 or cd.dtype != torch.float32 or not cs.is_contiguous() or \
-                not cd.is_contiguous() or cs.numel() != cd.numel():
-            raise ValueError("copy=(src, dst) must be equal-size contiguous fp32 tensors")
-        cn = cs.numel()
     rc = lib.pto_slab_reduce_sgd(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
                                  params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
                                  float(dampening), float(weight_decay), float(grad_scale),
                                  int(nesterov), int(first_step), _ptr(step_counter), _ptr(p2),
-                                 _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi), _ptr(cs), _ptr(cd),
-                                 int(cn), _ptr(set_pend), _stream())
+                                 _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi), _stream())
     _native.check(rc, "slab_reduce_sgd")
 
 
@@ -735,9 +498,8 @@ def set_debug_buffer(buf: Optional[torch.Tensor]) -> None:
 def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, *, lr: float,
                   momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
                   nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-                  step_counter: Optional[torch.Tensor] = None, cond: Optional[torch.Tensor] = None) -> None:
-    """In-place fused SGD(momentum) over flat fp32 buffers (torch.optim.SGD math).
-    ``cond``: int32 device flag; the update is skipped when it is 0."""
+                  step_counter: Optional[torch.Tensor] = None) -> None:
+    """In-place fused SGD(momentum) over flat fp32 buffers (torch.optim.SGD math)."""
     lib = _native.load()
     n = params.numel()
     for t, nm in ((params, "params"), (grads, "grads"), (buf, "momentum_buffer")):
@@ -748,5 +510,5 @@ def sgd_momentum_(params: torch.Tensor, grads: torch.Tensor, buf: torch.Tensor, 
     rc = lib.pto_sgd_momentum(params.data_ptr(), grads.data_ptr(), buf.data_ptr(), n, float(lr),
                               float(momentum), float(dampening), float(weight_decay),
                               float(grad_scale), int(nesterov), int(first_step),
-                              _ptr(step_counter), _ptr(cond), _stream())
+                              _ptr(step_counter), _stream())
     _native.check(rc, "sgd_momentum")

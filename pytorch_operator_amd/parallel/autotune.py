@@ -1,28 +1,59 @@
-"""Pick the faster DDP gradient path on the actual hardware, at start-up.
+"""Pick the fastest DDP gradient path on the actual hardware, at start-up.
 
-The xGMI peer-memory kernel (``parallel.xgmi``) is expected to beat RCCL for this 1.7 MB
-gradient on a fully connected 8x MI355X node, but that is a property of the fabric the
-job lands on, so it is measured rather than assumed: both paths run a short graph-replayed
-trial inside the warm-up, every rank reports its time, and all ranks adopt the path with
-the lower MAX-over-ranks time.  Both trials are real DDP steps (replicas stay identical);
-when RCCL wins after the xGMI trial, the sharded momentum is reassembled first.
+The reference synchronises gradients with DDP's bucketed all-reduce
+(examples/mnist/mnist.py:135-138).  Here three ways to run the same DDP step race:
+
+``rccl``        two flat-bucket RCCL all-reduces between the three pieces of the step (fc bucket
+                overlapping the conv backward), each piece's kernels launched from C++ straight
+                onto the stream (``launch="stream"``; ``"graph"`` replays hipGraphs instead);
+``rccl-graph``  the whole step with its RCCL collectives captured into ONE hipGraph per step
+                (``GraphedStep(mode="graph-comm")``; RCCL only -- gloo collectives are not
+                capturable, so with gloo this candidate is reported as skipped);
+``xgmi``        the peer-memory exchange kernel fused with SGD (``parallel.xgmi``), one whole
+                step per kernel list.
+
+Whether the xGMI kernel beats RCCL for this 1.7 MB gradient is a property of the fabric the job
+lands on, so it is measured rather than assumed: every candidate runs ``trial_steps`` real DDP
+steps (replicas stay identical), each trial is timed as the MAX over ranks, and every rank adopts
+the lowest time (identical numbers on every rank, so an identical choice; an all-reduce checks
+it).  The same procedure runs in ``bench.py`` and in the operator-deployed worker
+(``harness/mnist.py --allreduce auto``).
+
+``PTO_RACE_DELAY_MS="<candidate>:<ms>"`` (fault injection for tests) adds ``ms`` per step of host
+sleep inside that candidate's timed trial.
 """
 from __future__ import annotations
 
+import os
 import time
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 from .graphed_step import GraphedStep
 
+CANDIDATES = ("rccl", "rccl-graph", "xgmi")
 
-def _timed(runner: GraphedStep, steps: int, device) -> float:
+
+def _delay_ms(name: str) -> float:
+    spec = os.environ.get("PTO_RACE_DELAY_MS", "")
+    for part in spec.split(","):
+        if ":" in part:
+            k, v = part.split(":", 1)
+            if k.strip() == name:
+                return float(v)
+    return 0.0
+
+
+def _timed(runner: GraphedStep, steps: int, device, name: str) -> float:
     torch.cuda.synchronize(device)
     dist.barrier()
     t0 = time.perf_counter()
     runner.warm(steps)
+    delay = _delay_ms(name)
+    if delay > 0:
+        time.sleep(delay * steps / 1e3)
     torch.cuda.synchronize(device)
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -31,30 +62,65 @@ def _timed(runner: GraphedStep, steps: int, device) -> float:
 
 def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 10,
                      trial_steps: int = 60, force: Optional[str] = None,
-                     launch: str = "graph") -> Tuple[GraphedStep, str, dict]:
-    """Returns (runner, "xgmi" | "rccl", per-step times of both trials + ``steps``: the
-    training steps taken here).  ``force`` overrides the measured decision (tests use it to
-    cover both hand-overs).  ``spg``: whole steps per replay of the returned xGMI runner's
-    timed graph; the trials replay one-step graphs, so any ``trial_steps`` works."""
+                     launch: str = "stream") -> Tuple[GraphedStep, str, Dict]:
+    """Returns (runner, path, record).  ``path`` is one of ``CANDIDATES``; ``record`` holds
+    every candidate's per-step trial time in ms (None when skipped, with the reason), the RCCL
+    runner's launch form and ``steps``: the training steps taken here.  ``force`` overrides the
+    measured decision (tests cover every hand-over with it).  ``spg``: whole steps per replay of
+    a returned graph-replayed xGMI runner.  ``mode="eager"`` races eager launches instead."""
     trial = max(1, int(trial_steps))
-    # the RCCL step keeps momentum for every parameter: make it whole if fused xGMI steps
-    # ran before (a no-op when it already is)
+    dev = tr.device
+    eager = mode == "eager"
+    times: Dict[str, Optional[float]] = {}
+    runners: Dict[str, GraphedStep] = {}
+    skipped: Dict[str, str] = {}
+    steps = 0
+    # the RCCL steps keep momentum for every parameter: make it whole if fused xGMI steps ran
+    # before (a no-op when it already is)
     xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
     tr.grad_sync = rccl_sync
-    r_rccl = GraphedStep(tr, mode=mode, steps_per_graph=1 if mode == "graph" else spg)
-    t_rccl = _timed(r_rccl, trial, tr.device)
+    r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=1, launch=launch)
+    runners["rccl"] = r
+    times["rccl"] = _timed(r, trial, dev, "rccl")
+    steps += r.internal_steps + trial
+    if eager:
+        skipped["rccl-graph"] = "eager race"
+    elif dist.get_backend() != "nccl":
+        skipped["rccl-graph"] = f"{dist.get_backend()} collectives are not capturable"
+    else:
+        r = GraphedStep(tr, mode="graph-comm")
+        runners["rccl-graph"] = r
+        times["rccl-graph"] = _timed(r, trial, dev, "rccl-graph")
+        steps += r.internal_steps + trial
     tr.grad_sync = xgmi_sync
-    r_xgmi = GraphedStep(tr, mode="graph", steps_per_graph=spg, launch=launch)
-    t_xgmi = _timed(r_xgmi, trial, tr.device)
-    if xgmi_sync.xar.error():
-        t_xgmi = float("inf")
-    want = (t_xgmi < t_rccl) if force is None else (force == "xgmi")
-    flag = torch.tensor([1 if want else 0], dtype=torch.int32, device=tr.device)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # unanimous or RCCL
-    times = {"rccl_ms_per_step": round(t_rccl / trial * 1e3, 4), "xgmi_ms_per_step": round(t_xgmi / trial * 1e3, 4),
-             "steps": r_rccl.internal_steps + r_xgmi.internal_steps + 2 * trial}
-    if flag.item():
-        return r_xgmi, "xgmi", times
-    xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
-    tr.grad_sync = rccl_sync
-    return r_rccl, "rccl", times
+    r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
+    runners["xgmi"] = r
+    t = _timed(r, trial, dev, "xgmi")
+    steps += r.internal_steps + trial
+    times["xgmi"] = float("inf") if xgmi_sync.xar.error() else t
+    if force is not None:
+        if force not in runners:
+            raise ValueError(f"force={force!r}: candidate not available ({skipped.get(force, 'unknown')})")
+        pick = force
+    else:
+        pick = min(times, key=lambda k: (times[k], CANDIDATES.index(k)))
+    # identical MAX-over-ranks numbers give an identical pick everywhere; check it anyway
+    idx = torch.tensor([CANDIDATES.index(pick)], dtype=torch.int32, device=dev)
+    lo, hi = idx.clone(), idx.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    if int(lo.item()) != int(hi.item()):
+        pick = "rccl"  # ranks disagree (cannot happen with shared numbers): the safe path
+    if pick != "xgmi":
+        xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+        tr.grad_sync = rccl_sync
+    record = {f"{k.replace('-', '_')}_ms_per_step": (round(v / trial * 1e3, 4) if v != float("inf") else None)
+              for k, v in times.items()}
+    for k, why in skipped.items():
+        record[f"{k.replace('-', '_')}_ms_per_step"] = None
+        record[f"{k.replace('-', '_')}_skipped"] = why
+    if times["xgmi"] == float("inf"):
+        record["xgmi_error"] = int(xgmi_sync.xar.error())
+    record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,
+                   "steps": steps})
+    return runners[pick], pick, record

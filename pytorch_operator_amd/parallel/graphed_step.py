@@ -130,7 +130,6 @@ class GraphedStep:
         tr = trainer
         if tr._first_step:
             tr.train_step()  # momentum initialisation happens outside any graph
-            tr.flush_deferred()  # and a deferred (fc_sgd="next") first-step update too
             self.internal_steps += 1
         torch.cuda.synchronize(tr.device)
         whole_step = self.world == 1 or getattr(tr.grad_sync, "fused_sgd", False)

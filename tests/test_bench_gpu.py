@@ -27,15 +27,23 @@ def _port():
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("allreduce", ["xgmi", "auto"])
+@pytest.mark.parametrize("allreduce", ["xgmi", "auto", "auto-slow-xgmi"])
 def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
+    """``auto-slow-xgmi``: PTO_RACE_DELAY_MS makes the xGMI candidate slow, so the race must
+    pick RCCL, and the timed runner must then be the stream-launched RCCL step."""
     out = tmp_path / "bench.json"
+    env = dict(os.environ, PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1")
+    if allreduce == "auto-slow-xgmi":
+        env["PTO_RACE_DELAY_MS"] = "xgmi:5"
+        allreduce = "auto"
+        slow_xgmi = True
+    else:
+        slow_xgmi = False
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
            "--gpus", "2", "--backend", "gloo", "--allreduce", allreduce, "--steps", "20", "--warmup", "5",
            "--job-gpus", "0,0", "--job-timeout", "200", "--json-out", str(out)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=ROOT,
-                       env=dict(os.environ, PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=ROOT, env=env)
     assert r.returncode == 0 and out.exists(), r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads(out.read_text())
     assert line["n_gpus"] == 2 and line["steps"] == 20 and line["warmup"] == 5
@@ -45,8 +53,19 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
     if allreduce == "xgmi":
         assert line["config"]["grad_allreduce"] == "xgmi", line
     else:
-        assert line["config"]["grad_allreduce"] in ("xgmi", "rccl"), line
-        assert line["config"]["allreduce_trial"] is not None, line
+        trial = line["config"]["allreduce_trial"]
+        assert trial is not None, line
+        # every candidate reported: RCCL stream-launched (not the 3-hipGraph form), xGMI timed,
+        # the captured one-graph RCCL step skipped on gloo (its collectives are not capturable)
+        assert trial["rccl_launch"] == "stream", trial
+        assert trial["rccl_ms_per_step"] > 0 and trial["xgmi_ms_per_step"] > 0, trial
+        assert trial["rccl_graph_ms_per_step"] is None and "gloo" in trial["rccl_graph_skipped"], trial
+        assert line["config"]["grad_allreduce"] == trial["picked"], line
+        if slow_xgmi:
+            assert trial["picked"] == "rccl" and trial["xgmi_ms_per_step"] > trial["rccl_ms_per_step"], trial
+            assert "launch=stream" in line["config"]["exec"], line
+        # the operator-deployed pods ran the same race
+        assert line["job"]["allreduce_trial"] is not None, line["job"]
     assert line["value"] > 0 and line["ms_per_step"] > 0
     job = line["job"]
     assert job.get("result") == "Succeeded" and job.get("replicas") == 2, job
@@ -54,3 +73,10 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
     sm = job.get("worker_step_ms")
     assert sm and sm["n"] > 0 and 0 < sm["p50"] <= sm["p90"], job
     assert job["worker_capture_seconds"] is not None and job["worker_train_seconds"] > 0, job
+    # create -> first step of the two-pod job, and where it went
+    assert line["create_to_first_step_s"] is not None and line["create_to_first_step_s"] > 0, line
+    bd = job["startup_breakdown"]
+    assert bd and bd["job_create_to_process_start_s"] > 0 and bd["first_step_s"] > 0, bd
+    (tmp_path / "job.json").write_text(json.dumps(job))
+    print(json.dumps({"world2_shared_gpu": {"create_to_first_step_s": line.get("create_to_first_step_s"),
+                                             "startup_breakdown": bd, "allreduce": allreduce}}))

@@ -85,8 +85,15 @@ def test_mnist_worker_single_process_reference_output(tmp_path):
     assert "Train Epoch: 1 [320/1280 (25%)]\tloss=" in out
     assert "\naccuracy=" in out
     ev = _events(out)
-    assert [e["event"] for e in ev] == ["start", "first_step", "train_done"]
+    assert [e["event"] for e in ev] == ["start", "startup", "first_step", "train_done"]
     assert ev[0]["kernels"] == "torch" and ev[-1]["steps"] == 20
+    # create-to-first-step breakdown: every in-pod phase, in order, summing to the wall clock
+    st = ev[1]
+    marks = st["marks_unix_ns"]
+    assert list(marks) == ["process_start", "worker_main", "import_torch", "process_group", "dataset",
+                           "first_step"], marks
+    assert list(marks.values()) == sorted(marks.values())
+    assert abs(sum(st["phases"].values()) - (marks["first_step"] - marks["process_start"]) / 1e9) < 1e-3
     sd = torch.load(tmp_path / "mnist_cnn.pt", weights_only=True)
     assert sd["fc1.weight"].shape == (500, 800)
     scal = [json.loads(x) for x in open(tmp_path / "tb" / "scalars.jsonl")]

@@ -243,71 +243,6 @@ def test_conv12_fused_matches_separate_kernels(lib, B):
     assert torch.equal(lab.cpu(), y[rows])
 
 
-@pytest.mark.parametrize("B", [64, 50, 130])
-def test_fc1_bwd_head_matches_head_plus_fc1_bwd(lib, B):
-    """The head folded into fc1_bwd_head (recomputed per 16-sample tile, MFMA logits and dh)
-    against the standalone head kernel + fc1_bwd job 2 on the same split-K fc1 halves."""
-    from pytorch_operator_amd.models.mnist import reference_init
-    from pytorch_operator_amd.ops import mnist as K
-    dev = torch.device("cuda")
-    p = {k: v.to(dev) for k, v in reference_init(9).items()}
-    x, y = _data(B, seed=500 + B)
-    src = K.BatchSource(x.to(dev), y.to(dev))
-    f = K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"], p["conv2.bias"], B)
-    lab, a2, idx2 = f[3], f[4], f[5]
-    hp = K.fc1_fwd_parts(a2, p["fc1.weight"])
-    # reference: head + fc1_bwd job 2
-    h_ref = torch.empty(B, 500, device=dev)
-    ps_ref = torch.empty(B, 2, device=dev)
-    dl_ref, dh_ref, _ = K.head(hp[0], p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B,
-                               per_sample=ps_ref, h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=h_ref)
-    g = {k: torch.empty_like(v) for k, v in p.items()}
-    dz_ref = K.fc1_bwd(dh_ref, a2, idx2, p["fc1.weight"], dl_ref, h_ref, g["fc1.weight"], g["fc1.bias"],
-                       g["fc2.weight"], g["fc2.bias"], jobs=K.FC1_BWD_DGRAD)
-    # folded
-    dz2 = torch.full((B, 50, 8, 8), float("nan"), device=dev)
-    h = torch.full((B, 500), float("nan"), device=dev)
-    dh = torch.full((B, 500), float("nan"), device=dev)
-    dl = torch.full((B, 10), float("nan"), device=dev)
-    ps = torch.full((B, 2), float("nan"), device=dev)
-    K.fc1_bwd_head(hp, p["fc1.bias"], p["fc2.weight"], p["fc2.bias"], lab, a2, idx2, p["fc1.weight"],
-                   grad_scale=1.0 / B, dz2=dz2, h_out=h, dh=dh, dlogits=dl, per_sample=ps)
-    torch.cuda.synchronize()
-    assert torch.equal(h, h_ref)
-    assert _rel(dl, dl_ref) < 1e-5
-    assert _rel(dh, dh_ref) < 1e-5
-    assert _rel(ps[:, 0], ps_ref[:, 0]) < 1e-5 and torch.equal(ps[:, 1], ps_ref[:, 1])
-    assert _rel(dz2, dz_ref) < 1e-5
-    assert torch.isfinite(dz2).all()
-
-
-@pytest.mark.parametrize("B", [64, 50])
-def test_fused_schedule_matches_classic(lib, B):
-    """The 5-launch schedule (fc1_bwd_head; fc weight grads + SGD in conv_bwd's idle waves at
-    B = 64, in tail_sgd otherwise) trains like the 6-launch classic one (to rounding: the two
-    heads sum the logits' dot products in different orders -- MFMA K-split vs DPP all-reduce)."""
-    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
-    from pytorch_operator_amd.ops import mnist as K
-    dev = torch.device("cuda")
-    x, y = _data(4 * B, seed=700 + B)
-    perm = torch.arange(4 * B, dtype=torch.int32, device=dev)
-    res = {}
-    for sched in ("classic", "fused"):
-        cur = torch.zeros(1, dtype=torch.int32, device=dev)
-        src = K.BatchSource(x.to(dev), y.to(dev), perm=perm, cursor=cur)
-        tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.05, momentum=0.5, seed=3)
-        tr.schedule = sched
-        for _ in range(3):
-            tr.train_step()
-        torch.cuda.synchronize()
-        res[sched] = (tr.flat_params.clone(), tr.flat_momentum.clone(), tr.loss(), tr.flat_grads.clone())
-    (p0, m0, l0, g0), (p1, m1, l1, g1) = res["classic"], res["fused"]
-    assert _rel(p1, p0) < 1e-5 and _rel(m1, m0) < 1e-4
-    assert abs(l1 - l0) < 1e-5 * max(1.0, abs(l0))
-    ce = tr.layout.conv_end
-    assert _rel(g1[ce:], g0[ce:]) < 1e-4  # fc grads are still written for inspection
-
-
 # ---------------------------------------------------------------------------- round 3
 @pytest.mark.parametrize("B", [64, 37, 13, 1])
 def test_conv_bwd4_chunked_slab_matches_autograd(lib, B):
@@ -363,45 +298,6 @@ def test_conv_bwd4_chunked_slab_matches_autograd(lib, B):
     assert torch.equal(got, got2)
 
 
-@pytest.mark.parametrize("B", [64, 50])
-def test_fc1_bwd_fused_sgd_matches_grads_plus_sgd(lib, B):
-    """fc1_bwd_sgd: dz2 and the fc gradients equal fc1_bwd's; the fused update equals
-    torch.optim.SGD semantics applied to those gradients; fc1.weight goes to w1_next only."""
-    from pytorch_operator_amd.models.mnist import reference_init
-    from pytorch_operator_amd.ops import mnist as K
-    dev = torch.device("cuda")
-    p = {k: v.to(dev).contiguous() for k, v in reference_init(12).items()}
-    x, y = _data(B, seed=1200 + B)
-    src = K.BatchSource(x.to(dev), y.to(dev))
-    f = K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"], p["conv2.bias"], B)
-    lab, a2, idx2 = f[3], f[4], f[5]
-    h = K.fc1_fwd(a2, p["fc1.weight"], p["fc1.bias"])
-    dl, dh, _ = K.head(h, p["fc2.weight"], p["fc2.bias"], lab, grad_scale=1.0 / B)
-    names = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
-    g_ref = {k: torch.empty_like(p[k]) for k in names}
-    dz_ref = K.fc1_bwd(dh, a2, idx2, p["fc1.weight"], dl, h, *[g_ref[k] for k in names])
-    g = torch.Generator().manual_seed(B)
-    mom = {k: torch.randn(p[k].shape, generator=g).to(dev) for k in names}
-    params = {k: p[k].clone() for k in names}
-    bufs = {k: mom[k].clone() for k in names}
-    grads = {k: torch.full_like(p[k], float("nan")) for k in names}
-    w1n = torch.full_like(p["fc1.weight"], float("nan"))
-    dz2 = torch.full((B, 50, 8, 8), float("nan"), device=dev)
-    lr, m = 0.05, 0.5
-    K.fc1_bwd_sgd(dh, a2, idx2, params["fc1.weight"], dl, h, dz2=dz2, w1_next=w1n, params=params, bufs=bufs,
-                  grads=grads, lr=lr, momentum=m)
-    torch.cuda.synchronize()
-    assert torch.equal(dz2, dz_ref)
-    for k in names:
-        assert torch.equal(grads[k], g_ref[k]), k
-        m_ref = m * mom[k] + g_ref[k]
-        p_ref = p[k] - lr * m_ref
-        assert _rel(bufs[k], m_ref) < 1e-6, k
-        got = w1n if k == "fc1.weight" else params[k]
-        assert _rel(got, p_ref) < 1e-6, k
-    assert torch.equal(params["fc1.weight"], p["fc1.weight"])  # read-only in this launch
-
-
 def _stage_trainer(x, y, perm, B=64, seed=9, **knobs):
     from pytorch_operator_amd.models.mnist import FusedMnistTrainer
     from pytorch_operator_amd.ops import mnist as K
@@ -440,14 +336,13 @@ def test_staged_batches_are_bit_identical_to_gathered(lib):
 
 @pytest.mark.parametrize("B", [64, 37])
 def test_round3_step_matches_round2_step(lib, B):
-    """chunked conv backward + fc SGD fused into fc1_bwd + staged batches vs the round-2
-    step (per-sample slab, SGD in the tail, gathered batches): same training trajectory up to
-    summation order; fc gradients stored identically."""
+    """chunked conv backward + staged batches vs the round-2 step (per-sample slab, gathered
+    batches): same training trajectory up to summation order; fc gradients stored identically."""
     n = 8 * B
     x, y = _data(n, seed=300 + B, n_total=n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(5)).to(torch.int32)
     new = _stage_trainer(x, y, perm, B=B)
-    old = _stage_trainer(x, y, perm, B=B, conv_chunk=1, fc_sgd="tail", stage_batches=False)
+    old = _stage_trainer(x, y, perm, B=B, conv_chunk=1, stage_batches=False)
     for _ in range(5):
         new.train_step()
         old.train_step()
@@ -459,42 +354,3 @@ def test_round3_step_matches_round2_step(lib, B):
     ce = new.layout.conv_end
     assert _rel(new.flat_grads[ce:], old.flat_grads[ce:]) < 1e-5
     assert _rel(new.flat_grads[:ce], old.flat_grads[:ce]) < 1e-5
-
-
-@pytest.mark.parametrize("dampening", [0.0, 0.3])
-def test_deferred_fc_sgd_is_bit_identical_to_tail(lib, dampening):
-    """fc_sgd="next" (the tail leaves the fc update pending; the next conv12 launch's extra
-    grid rows apply it, fc1_fwd clears the flag) trains bit-identically to the tail SGD:
-    eager steps, a mid-run public read (flush), a graph captured after the eager first step
-    (dampening != 0 exercises the first-step buffer rule), state_dict and momentum."""
-    n = 640
-    x, y = _data(n, seed=91, n_total=n)
-    perm = torch.randperm(n, generator=torch.Generator().manual_seed(4)).to(torch.int32)
-    a = _stage_trainer(x, y, perm, fc_sgd="next")
-    b = _stage_trainer(x, y, perm, fc_sgd="tail")
-    for tr in (a, b):
-        tr.dampening = dampening
-        tr._first_step = dampening != 0.0
-        for _ in range(2):
-            tr.train_step()
-    torch.cuda.synchronize()
-    assert a._defer_used and int(a._pend.item()) == 1
-    assert torch.equal(a.flat_params, b.flat_params)  # the read flushes the pending update
-    assert int(a._pend.item()) == 0
-    for tr in (a, b):
-        tr.train_step()
-        tr.train_step()
-        g = tr.capture(1)
-        for _ in range(3):
-            g.replay()
-    torch.cuda.synchronize()
-    assert int(a.cursor.item()) == int(b.cursor.item()) == 7
-    assert torch.equal(a.flat_params, b.flat_params)
-    assert torch.equal(a.flat_momentum, b.flat_momentum)
-    sa, sb = a.state_dict(), b.state_dict()
-    assert all(torch.equal(sa[k], sb[k]) for k in sb)
-    # a flush with nothing pending is a no-op
-    before = a._fp.clone()
-    a.flush_deferred()
-    torch.cuda.synchronize()
-    assert torch.equal(a._fp, before)

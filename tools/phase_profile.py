@@ -19,15 +19,6 @@ from pytorch_operator_amd.models.mnist import FusedMnistTrainer  # noqa: E402
 from pytorch_operator_amd.ops import mnist as K  # noqa: E402
 
 
-def tail(tr, B):
-    fp, fm, fg = tr._fc_dicts()
-    ce = tr.layout.conv_end
-    K.tail_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce], tr.flat_momentum[:ce],
-                dh=tr.dh[:B], a2=tr.a2[:B], dlogits=tr.dlogits[:B], h=tr.h1[:B],
-                per_sample=tr.per_sample[:B], fc_params=fp, fc_bufs=fm, fc_grads=fg, stats=tr.stats,
-                loss_scale=1.0 / B, lr=0.0, momentum=0.5)
-
-
 def main():
     dev = torch.device("cuda")
     ds = make_synthetic_mnist(6400, device=dev)
@@ -39,49 +30,36 @@ def main():
         tr.train_step()
     torch.cuda.synchronize()
     dbg = torch.zeros(1 << 16, dtype=torch.int64, device=dev)
-    p, g = tr.params, tr.grads
+    p = tr.params
+    lay = tr.layout
+    ce = lay.conv_end
     launches = [
         ("conv12_fwd", lambda: K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"],
                                             p["conv2.weight"], p["conv2.bias"], B, a1=tr.a1,
                                             idx1=tr.idx1, xn=tr.xn, lab=tr.lab, a2=tr.a2,
                                             idx2=tr.idx2)),
-        ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
-        ("head", lambda: K.head(tr.h1, p["fc2.weight"], p["fc2.bias"], tr.lab, grad_scale=1.0 / B,
-                                per_sample=tr.per_sample, dlogits=tr.dlogits, dh=tr.dh)),
-        ("fc1_parts", lambda: K.fc1_fwd_parts(tr.a2, p["fc1.weight"],
-                                              out=tr.h_parts[:2 * B * 500].view(2, B, 500))),
-        ("head_parts", lambda: K.head(tr.h_parts[:B * 500].view(B, 500), p["fc2.weight"], p["fc2.bias"],
-                                      tr.lab, grad_scale=1.0 / B, per_sample=tr.per_sample,
-                                      dlogits=tr.dlogits, dh=tr.dh,
-                                      h_second=tr.h_parts[B * 500:2 * B * 500].view(B, 500),
-                                      fc1_bias=p["fc1.bias"], h_out=tr.h1)),
-        ("fc1_bwd_w", lambda: tr._fc1_bwd(B, K.FC1_BWD_WGRAD | K.FC1_BWD_FC2)),
-        ("fc1_bwd_d", lambda: tr._fc1_bwd(B, K.FC1_BWD_DGRAD)),
-        ("fc1_bwd_head", lambda: tr._fc1_bwd_head(B)),
-        ("conv_bwd", lambda: tr._conv_bwd(B)),
-        ("conv_bwd_fc", lambda: tr._conv_bwd_fc(B, sgd=False)),
-        ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(),
-                                                    tr.flat_params[:tr.layout.conv_end],
-                                                    tr.flat_momentum[:tr.layout.conv_end],
-                                                    lr=0.0, momentum=0.5)),
-        ("tail_sgd", lambda: tail(tr, B)),
-    ]
-    fp, fm, fg = tr._fc_dicts()
-    lay = tr.layout
-    launches += [
-        ("conv_bwd4", lambda: K.conv_bwd4(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn, tr.conv_slab,
-                                          lay.offsets, B)),
-        ("fc1_bwd_sgd", lambda: K.fc1_bwd_sgd(tr.dh, tr.a2, tr.idx2, p["fc1.weight"], tr.dlogits, tr.h1,
-                                              dz2=tr.dz2, w1_next=tr.w1_next, params=fp, bufs=fm, grads=fg,
-                                              per_sample=tr.per_sample, stats=tr.stats, lr=0.0, momentum=0.5,
-                                              src=src, stage=tr.stage, stage_adv=0)),
-        ("tail4_copy", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:lay.conv_end],
-                                                  tr.flat_momentum[:lay.conv_end], lr=0.0, momentum=0.5,
-                                                  big=K.conv_bwd4_rows(B, lay.offsets),
-                                                  copy=(p["fc1.weight"].reshape(-1), tr.w1_next.reshape(-1)))),
         ("conv12_staged", lambda: K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"], p["conv2.weight"],
                                                p["conv2.bias"], B, a1=tr.a1, idx1=tr.idx1, xn=tr.xn, lab=tr.lab,
                                                a2=tr.a2, idx2=tr.idx2, stage=tr.stage)),
+        ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
+        ("fc1_parts", lambda: K.fc1_fwd_parts(tr.a2, p["fc1.weight"],
+                                              out=tr.h_parts[:2 * B * 500].view(2, B, 500))),
+        ("head_parts", lambda: tr._head(B)),
+        ("fc1_bwd", lambda: tr._fc1_bwd(B, stage_adv=0)),
+        ("conv_bwd", lambda: K.conv_bwd(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn,
+                                        tr.slab_views["conv2.weight"], tr.slab_views["conv2.bias"],
+                                        tr.slab_views["conv1.weight"], tr.slab_views["conv1.bias"],
+                                        slab=tr.conv_slab)),
+        ("conv_bwd4", lambda: K.conv_bwd4(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn, tr.conv_slab,
+                                          lay.offsets, B)),
+        ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
+                                                    tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
+                                                    big=K.conv_bwd4_rows(B, lay.offsets))),
+        ("tail", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
+                                            tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
+                                            big=K.conv_bwd4_rows(B, lay.offsets),
+                                            extra=(tr.flat_params[ce:], tr.flat_grads[ce:],
+                                                   tr.flat_momentum[ce:]))),
     ]
     reps = 20
     for name, fn in launches:

@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""In-situ timeline of the stream-launched MNIST training step (what the bench times).
+
+Every kernel launcher hands its launch the next slot of the debug buffer (mnist_kernels.hip
+``dbg_next``), so capturing two whole steps gives each of their launches its own slot.  The
+captured kernel list is then launched straight onto the stream (``GraphedStep``'s
+``launch="stream"`` path) for ``--steps`` steps; the stamps left behind are those of the last
+two steps.  Per kernel this prints, on the 100 MHz wall clock every CU shares:
+
+  start   first block's first stamp, relative to the first kernel of the pair
+  span    first block start -> last block's last stamp (the kernel as its waves see it)
+  p50end  median block end (tail imbalance = span - p50end)
+  gap     this kernel's first block start - the previous kernel's last block end: the
+          dependent-launch boundary as the GPU sees it (dispatch, cache maintenance, ramp)
+
+    python tools/step_timeline.py [--steps 400] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from pytorch_operator_amd.data.synthetic import make_synthetic_mnist  # noqa: E402
+from pytorch_operator_amd.models.mnist import FusedMnistTrainer  # noqa: E402
+from pytorch_operator_amd.ops import mnist as K  # noqa: E402
+from pytorch_operator_amd.parallel.graphed_step import NativeGraph  # noqa: E402
+
+SLOT_U64 = 1024 * 16  # mnist_kernels.hip kDbgSlotU64
+NAMES = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]
+# block ranges of the launches that run several jobs (B = 64): name -> [(first, end, job)]
+GROUPS = {"fc1_bwd": [(0, 200, "dW_fc1"), (200, 400, "dz2"), (400, 404, "fc2+stats"), (404, 420, "stage")],
+          "tail": [(0, 201, "conv reduce+sgd"), (201, 598, "fc sgd")]}
+
+
+def analyse(dbg: torch.Tensor, nslots: int):
+    out = []
+    d_all = dbg.view(-1, 16).cpu()
+    for k in range(nslots):
+        d = d_all[k * 1024:(k + 1) * 1024]
+        used = d[:, 0] > 0
+        w = d[used][:, :8].double()
+        valid = w > 0
+        last = (w * valid).max(1).values
+        idx = torch.nonzero(used).flatten()
+        out.append({"blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
+                    "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist()))})
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--reps", type=int, default=5, help="timelines sampled (each after --steps steps)")
+    args = ap.parse_args(argv)
+    dev = torch.device("cuda")
+    ds = make_synthetic_mnist(60000, seed=1, device=dev)
+    cur = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cur)
+    tr = FusedMnistTrainer(batch_size=64, source=src, lr=0.01, momentum=0.5, device=dev, seed=1)
+    for _ in range(3):
+        tr.train_step()
+    torch.cuda.synchronize()
+    dbg = torch.zeros(16 * SLOT_U64, dtype=torch.int64, device=dev)
+    K.set_debug_buffer(dbg)
+
+    def two_steps():
+        tr.train_step()
+        tr.train_step()
+    g = NativeGraph(two_steps, dev)
+    K.set_debug_buffer(None)  # later launches (none) would not stamp; the captured ones keep dbg
+    if not g.stream_ok:
+        raise SystemExit("captured step holds non-kernel nodes")
+    nk = g.nodes
+    samples = []
+    for _ in range(args.reps):
+        dbg.zero_()
+        g.replay_stream(args.steps // 2)
+        torch.cuda.synchronize()
+        samples.append(analyse(dbg, nk))
+    # per-kernel medians over the samples
+    rows = []
+    per = nk // 2
+    for k in range(nk):
+        vals = {key: sorted(s[k][key] - s[0]["start"] for s in samples) for key in ("start", "end", "p50end")}
+        med = {key: v[len(v) // 2] / 100.0 for key, v in vals.items()}
+        gaps = sorted((s[k]["start"] - s[k - 1]["end"]) / 100.0 for s in samples) if k else [float("nan")]
+        rows.append({"kernel": NAMES[k % per] if per == len(NAMES) else f"k{k}", "step": k // per,
+                     "blocks": samples[0][k]["blocks"], "start_us": round(med["start"], 2),
+                     "span_us": round(med["end"] - med["start"], 2),
+                     "p50_block_end_us": round(med["p50end"] - med["start"], 2),
+                     "gap_from_prev_us": round(gaps[len(gaps) // 2], 2)})
+    for r, k in zip(rows, range(nk)):
+        if r["kernel"] in GROUPS:
+            r["jobs"] = {}
+            for lo, hi, job in GROUPS[r["kernel"]]:
+                ends = sorted(max((e for b, e in s[k]["block_end"].items() if lo <= b < hi), default=0.0)
+                              - s[k]["start"] for s in samples)
+                r["jobs"][job] = round(ends[len(ends) // 2] / 100.0, 2)
+    period = sorted((s[per]["start"] - s[0]["start"]) / 100.0 for s in samples)
+    res = {"step_period_us": round(period[len(period) // 2], 2), "kernels": rows,
+           "sum_span_us": round(sum(r["span_us"] for r in rows[per:]), 2),
+           "sum_gap_us": round(sum(r["gap_from_prev_us"] for r in rows[1:per + 1]), 2)}
+    print(f"step period (kernel 0 of step t -> kernel 0 of step t+1): {res['step_period_us']} us")
+    print(f"{'kernel':12s} {'step':>4s} {'blocks':>6s} {'start':>8s} {'span':>7s} {'p50end':>7s} {'gap':>6s}")
+    for r in rows:
+        print(f"{r['kernel']:12s} {r['step']:4d} {r['blocks']:6d} {r['start_us']:8.2f} {r['span_us']:7.2f} "
+              f"{r['p50_block_end_us']:7.2f} {r['gap_from_prev_us']:6.2f}" +
+              ("   last block end by job: " + ", ".join(f"{j} {v}" for j, v in r["jobs"].items())
+               if r.get("jobs") else ""))
+    print(f"one step: sum of spans {res['sum_span_us']} us + sum of gaps {res['sum_gap_us']} us")
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
