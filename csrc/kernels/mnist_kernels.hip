@@ -58,6 +58,14 @@ constexpr int FC1_KS = 2;
 constexpr bool WT_TAIL = (PTO_WT & 1) != 0;
 constexpr bool WT_FC1 = (PTO_WT & 2) != 0;
 constexpr bool WT_SLAB = (PTO_WT & 4) != 0;
+constexpr bool WT_TAIL_FC = (PTO_WT & 8) != 0;  // only the tail's fc-parameter SGD stores
+// PTO_FB (A/B): fc1_bwd block layout -- bit 0: the dz2 job (the launch's critical path into the
+// conv backward) takes the first block ids, so it is dispatched first onto idle CUs; bit 1: its
+// blocks are ordered so the four sample tiles of one feature tile share an XCD (round-robin
+// placement: blocks b and b + 8 share one) and read that W1 column slab into one L2
+#ifndef PTO_FB
+#define PTO_FB 0
+#endif
 
 namespace {
 
@@ -847,8 +855,22 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   const int nJ1 = (a.jobs & 1) ? E_NJ1 : 0;
   const int nJ2 = (a.jobs & 2) ? ((B + 15) / 16) * 50 : 0;
   const int nJ3 = (a.jobs & 4) ? E_NJ3 : 0;
-  const int blk = blockIdx.x;
+  int blk = blockIdx.x;
   stamp(dbg, 0);
+  int t2x = -1;  // dz2 tile (mt * 50 + kt) when this block runs the dz2 job
+  if (PTO_FB & 1) {
+    // physical ids [0, nJ2): dz2, then [nJ2, nJ2 + nJ1): dW_fc1, then fc2 + staging as before
+    if (blk < nJ2) {
+      t2x = blk;
+      if ((PTO_FB & 2) && nJ2 == 200) {
+        const int s = (blk & 7) * 25 + (blk >> 3);  // blocks grouped by XCD: 25 per XCD
+        t2x = (s & 3) * 50 + (s >> 2);              // 4 consecutive slots = the 4 mt of one kt
+      }
+      blk = nJ1 + t2x;
+    } else if (blk < nJ2 + nJ1) {
+      blk -= nJ2;
+    }
+  }
   if (blk < nJ1) {
     const int tile = blk * E_NW + wv;
     const int nt = tile / 50, kt = tile - nt * 50;
@@ -1780,8 +1802,8 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];
       float4 bb = reinterpret_cast<float4*>(buf2)[v];
       sgd4(pp, bb, gg, hy);
-      st4<WT_TAIL>(reinterpret_cast<float4*>(p2), v, pp);
-      st4<WT_TAIL>(reinterpret_cast<float4*>(buf2), v, bb);
+      st4<WT_TAIL || WT_TAIL_FC>(reinterpret_cast<float4*>(p2), v, pp);
+      st4<WT_TAIL || WT_TAIL_FC>(reinterpret_cast<float4*>(buf2), v, bb);
     }
     stamp(dbg, 1);
     return;

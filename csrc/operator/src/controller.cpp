@@ -459,7 +459,6 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
     }
     if (!e2.not_found()) events_.record(job, {"Normal", "SuccessfulDeleteService", "Deleted service: " + d.name});
   }
-  M.inc("pytorch_operator_jobs_restarted_total", r.metrics.restarted);
   if (!r.error.empty()) return r.error;
   if (r.delete_job) {
     ApiError e2;
@@ -470,11 +469,13 @@ std::string PyTorchController::apply(Json& job, ReconcileResult& r) {
     std::string e = write_status(job, r.status);
     if (!e.empty()) return e;
   }
-  // a job's Succeeded / Failed transition is counted once it is persisted: a status write that
-  // loses a resourceVersion race requeues the key, and the retry (which still sees the old
-  // status in the cache) would otherwise count the same transition again
+  // a job's Succeeded / Failed / Restarting transition is counted once it is persisted: a status
+  // write that loses a resourceVersion race requeues the key, and the retry (which still sees the
+  // old status in the cache) would otherwise count the same transition again.  Failed and
+  // restarted move together, as status.go:128-129 increments them
   M.inc("pytorch_operator_jobs_successful_total", r.metrics.successful);
   M.inc("pytorch_operator_jobs_failed_total", r.metrics.failed);
+  M.inc("pytorch_operator_jobs_restarted_total", r.metrics.restarted);
   for (double d : r.requeue_after_s) queue_.add_after(key, d);
   if (r.requeue_rate_limited) queue_.add_rate_limited(key);
   return "";

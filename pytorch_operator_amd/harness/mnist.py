@@ -86,12 +86,19 @@ def parse_args(argv=None):
                    help="continue from --checkpoint-dir if a checkpoint exists (e.g. after an ExitCode restart)")
     p.add_argument("--trace", action="store_true", help="roctx ranges around epochs, step blocks and eval")
     p.add_argument("--metrics-file", default=None, help="append the JSON milestone lines here too")
+    p.add_argument("--metrics-port", type=int, default=int(os.environ.get("PTO_WORKER_METRICS_PORT", "-1")),
+                   help="serve Prometheus /metrics on this port (0: any free port, -1: off; "
+                        "docs/monitoring.md; env PTO_WORKER_METRICS_PORT)")
     return p.parse_args(argv)
 
 
 class _Emitter:
-    def __init__(self, rank: int, path):
-        self.rank, self.path = rank, path
+    """JSON milestone lines (stdout + ``--metrics-file``), mirrored into the worker's Prometheus
+    endpoint when ``--metrics-port`` is on (``wm``)."""
+
+    def __init__(self, rank: int, path, wm=None):
+        self.rank, self.path, self.wm = rank, path, wm
+        self.info = {"rank": rank}
 
     def __call__(self, event: str, **kw):
         rec = {"event": event, "rank": self.rank, "unix_ns": time.time_ns(), **kw}
@@ -100,6 +107,19 @@ class _Emitter:
         if self.path:
             with open(self.path, "a") as f:
                 f.write(line + "\n")
+        if self.wm is not None:
+            if event == "first_step":
+                self.wm.set("pto_worker_first_step_unix_seconds", rec["unix_ns"] / 1e9)
+            elif event == "startup":
+                for k, v in kw["phases"].items():
+                    self.wm.set("pto_worker_startup_phase_seconds", v, phase=k[:-2] if k.endswith("_s") else k)
+            elif event == "grad_allreduce":
+                self.info["grad_allreduce"] = kw.get("path", "")
+                self.wm.set("pto_worker_info", 1, replace=True, **self.info)
+            elif event == "xgmi_error":
+                self.wm.set("pto_worker_grad_exchange_errors", kw.get("code", 1))
+            elif event == "train_done" and kw.get("accuracy") is not None:
+                self.wm.set("pto_worker_accuracy", kw["accuracy"])
 
 
 def _datasets(args, rank: int, world: int, device):
@@ -175,7 +195,14 @@ def run(args, t_main_ns: Optional[int] = None) -> dict:
     env = init_from_env(args.backend, use_gpu=use_cuda)
     rank, world, device = env.rank, env.world_size, env.device
     startup.mark("process_group")
-    emit = _Emitter(rank, args.metrics_file)
+    wm = None
+    if args.metrics_port >= 0:
+        from ..utils.worker_metrics import WorkerMetrics
+        wm = WorkerMetrics()
+        port = wm.serve(args.metrics_port)
+    emit = _Emitter(rank, args.metrics_file, wm)
+    if wm is not None:
+        emit("metrics_endpoint", port=port)
     if world > 1:
         print(f"Using distributed PyTorch with {args.backend} backend")
     kernels = args.kernels
@@ -199,6 +226,9 @@ def run(args, t_main_ns: Optional[int] = None) -> dict:
         steps_per_epoch = min(steps_per_epoch, args.max_steps)
     emit("start", world_size=world, backend=env.backend, kernels=kernels, data=data_source,
          n_train=int(n), steps_per_epoch=steps_per_epoch)
+    if wm is not None:
+        emit.info.update(world_size=world, backend=env.backend, kernels=kernels)
+        wm.set("pto_worker_info", 1, replace=True, **emit.info)
 
     if kernels == "hip":
         result = _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup)
@@ -313,10 +343,12 @@ def _percentiles(samples_ms):
     return {"p50": pick(0.5), "p90": pick(0.9), "p99": pick(0.99), "n": len(xs)}
 
 
-def _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss, writer):
+def _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss, writer, wm=None):
     print("Train Epoch: {} [{}/{} ({:.0f}%)]\tloss={:.4f}".format(
         epoch, batch_idx * B, n, 100.0 * batch_idx / steps_per_epoch, loss), flush=True)
     writer.add_scalar("loss", loss, epoch * steps_per_epoch + batch_idx)
+    if wm is not None:
+        wm.set("pto_worker_loss", loss)
 
 
 def _log_test(acc, epoch, writer):
@@ -394,7 +426,9 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, sta
             startup.mark("first_step")
             emit("startup", **startup.record())
             emit("first_step")
-        _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer)
+        _log_train(epoch, 0, B, n, steps_per_epoch, tr.loss(), writer, emit.wm)
+        if emit.wm is not None:
+            emit.wm.inc("pto_worker_steps_total")
         if runner is None and not args.no_graph:
             # capturing runs warm-up steps: snapshot the state, capture, restore, so the
             # trajectory is exactly the eager one (a log block = one graph replay).  The
@@ -443,8 +477,14 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, sta
                 e1.record()
                 events.append((e0, e1, chunk))
                 b += chunk
+                if emit.wm is not None:
+                    emit.wm.inc("pto_worker_steps_total", chunk)
                 if (b - 1) % log_iv == 0:
-                    _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer)
+                    _log_train(epoch, b - 1, B, n, steps_per_epoch, tr.loss(), writer, emit.wm)
+                    if emit.wm is not None:  # tr.loss() synchronised: the interval's events are done
+                        sec = e0.elapsed_time(e1) / 1e3 / chunk
+                        emit.wm.set("pto_worker_step_seconds", sec)
+                        emit.wm.set("pto_worker_samples_per_second", B * world / sec)
                     _xgmi_guard(sync, emit, f"epoch {epoch} batch {b - 1}")
         torch.cuda.synchronize(dev)
         _xgmi_guard(sync, emit, f"end of epoch {epoch}")
@@ -515,8 +555,10 @@ def _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, s
                 startup.mark("first_step")
                 emit("startup", **startup.record())
                 emit("first_step")
+            if emit.wm is not None:
+                emit.wm.inc("pto_worker_steps_total")
             if batch_idx % args.log_interval == 0:
-                _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss.item(), writer)
+                _log_train(epoch, batch_idx, B, n, steps_per_epoch, loss.item(), writer, emit.wm)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         t_train += time.perf_counter() - t0

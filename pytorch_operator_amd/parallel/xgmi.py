@@ -55,10 +55,12 @@ class XgmiAllReduce:
         self.n = int(n)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         if nblk <= 0:
-            # one workgroup per CU when every rank owns its GPU (the kernel's phase 1 reads
-            # the 6.5 MB per-sample slab: 256 x 25 KB beats 128 x 51 KB, emulated W=2:
-            # 16.7 vs 18.2 us/launch); 128 when ranks share a device (1-GPU rehearsals),
-            # where every rank's blocks must be resident at once
+            # one workgroup per CU when every rank owns its GPU (the kernel's phase 1 reduces
+            # the conv backward's slab -- 1.6 MB of 4-sample chunk rows + per-sample rows of the
+            # small conv grads at B = 64 -- across more CUs: 256 workgroups measured faster than
+            # 128 on the emulated W=2 exchange, 16.7 vs 18.2 us/launch, when the slab was the
+            # round-2 6.5 MB per-sample form); 128 when ranks share a device (1-GPU
+            # rehearsals), where every rank's blocks must be resident at once
             where = (socket.gethostname(), self.device.index)
             peers = [None] * self.world
             dist.all_gather_object(peers, where, group=group)

@@ -145,6 +145,9 @@ class ZeroAdamW:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.t = 0
+        # per-parameter AdamW step counts (bias correction), as MasterAdamW's st["step"]: at world 1
+        # a parameter that gets no gradient skips the step and its count stays behind
+        self.pstep: Dict[int, int] = {}
         if reduce_dtype not in (torch.float32, torch.bfloat16):
             raise TypeError("reduce_dtype: float32 or bfloat16")
         self.reduce_dtype = reduce_dtype
@@ -258,7 +261,7 @@ class ZeroAdamW:
             with torch.enable_grad():
                 loss = closure()
         self.t += 1
-        skip: Dict[int, List[tuple]] = {}
+        skip: Dict[int, set] = {}
         for b in self.buckets:
             if b.pending >= 0:
                 # some parameter of this bucket got no gradient through the hook this step.  Only
@@ -274,7 +277,7 @@ class ZeroAdamW:
                     if p.grad is None:
                         b.grad32[off:off + p.numel()].zero_()
                         if self.world == 1:
-                            skip.setdefault(id(b), []).append((off, p.numel()))
+                            skip.setdefault(id(b), set()).add(id(p))
                     else:
                         self._deposit(b.grad32[off:off + p.numel()], p.grad.reshape(-1), b.unscaled)
                         p.grad = None
@@ -286,9 +289,20 @@ class ZeroAdamW:
                 b.rs_work = None
             if self.world > 1:
                 b.release_grad()  # the shard holds what AdamW needs (stream-ordered after the wait)
-            keep = self._save_ranges(b, skip.get(id(b), []))
-            self._adamw(b)
-            self._restore_ranges(b, keep)
+            # parameters grouped by their step count after this step (world > 1: every parameter
+            # steps -- a missing gradient is a zero contribution, DDP's semantics); each group is
+            # one AdamW pass over the bucket with the other ranges saved and restored around it
+            skipped = skip.get(id(b), set())
+            groups: Dict[int, List[nn.Parameter]] = {}
+            for p in b.params:
+                if id(p) not in skipped:
+                    t = self.pstep[id(p)] = self.pstep.get(id(p), self.t - 1) + 1
+                    groups.setdefault(t, []).append(p)
+            for t, members in groups.items():
+                ids = {id(p) for p in members}
+                keep = self._save_ranges(b, [(b.slot[id(p)], p.numel()) for p in b.params if id(p) not in ids])
+                self._adamw(b, t)
+                self._restore_ranges(b, keep)
             if self.world == 1:
                 b.release_grad()
             if self.world > 1:
@@ -318,7 +332,7 @@ class ZeroAdamW:
             if ms is not None:
                 b.master[sl].copy_(ms)
 
-    def _adamw(self, b: _Bucket) -> None:
+    def _adamw(self, b: _Bucket, t: int) -> None:
         b1, b2 = self.betas
         w = b.w_shard()
         master = b.master if b.master is not None else w
@@ -329,10 +343,10 @@ class ZeroAdamW:
             _native.check(_native.load().pto_adamw_step_scaled(
                 master.data_ptr(), b.exp_avg.data_ptr(), b.exp_avg_sq.data_ptr(), b.gshard.data_ptr(), out,
                 b.shard, 1 if b.gshard.dtype == torch.bfloat16 else 0, self.lr, b1, b2, self.eps,
-                self.weight_decay, self.t, 1.0 / self.world if b.unscaled else 1.0, stream), "adamw_step")
+                self.weight_decay, t, 1.0 / self.world if b.unscaled else 1.0, stream), "adamw_step")
         else:
             from ..ops.optim import MasterAdamW
-            st = {"step": self.t, "exp_avg": b.exp_avg, "exp_avg_sq": b.exp_avg_sq}
+            st = {"step": t, "exp_avg": b.exp_avg, "exp_avg_sq": b.exp_avg_sq}
             MasterAdamW._step_reference(w, b.gshard, master, st, self.lr, b1, b2, self.eps, self.weight_decay)
 
     def _wait_weights(self, buckets) -> None:
@@ -351,7 +365,8 @@ class ZeroAdamW:
         (the weights themselves are in the model's state_dict)."""
         return {"t": self.t, "world": self.world, "rank": self.rank,
                 "buckets": [{"npad": b.npad, "master": b.master, "exp_avg": b.exp_avg,
-                             "exp_avg_sq": b.exp_avg_sq} for b in self.buckets]}
+                             "exp_avg_sq": b.exp_avg_sq,
+                             "pstep": [self.pstep.get(id(p), self.t) for p in b.params]} for b in self.buckets]}
 
     @torch.no_grad()
     def load_shard_state_dict(self, sd: dict) -> None:
@@ -364,6 +379,8 @@ class ZeroAdamW:
                 b.master.copy_(s["master"])
             b.exp_avg.copy_(s["exp_avg"])
             b.exp_avg_sq.copy_(s["exp_avg_sq"])
+            for p, n in zip(b.params, s.get("pstep") or [int(sd["t"])] * len(b.params)):
+                self.pstep[id(p)] = int(n)
         self.t = int(sd["t"])
 
     # ------------------------------------------------------------------ inspection

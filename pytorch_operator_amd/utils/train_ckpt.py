@@ -104,16 +104,30 @@ def save(dirpath: str, step: int, model, opt, rank: int, world: int, keep: int =
         _atomic_save(_cpu(opt.shard_state_dict()), os.path.join(path, f"optim_rank{rank}.pt"))
     _barrier(world)  # every rank's files of step_<N> are complete
     if rank == 0:
+        # the pointer file lists the last `keep` COMPLETE checkpoints (newest last); everything
+        # else under step_* is pruned -- including a higher-numbered directory a crashed save left
+        # behind, which must never displace the fallback checkpoint
+        prev = []
+        meta_path = os.path.join(dirpath, "meta.json")
+        if os.path.exists(meta_path):
+            try:
+                with open(meta_path) as f:
+                    old = json.load(f)
+                prev = old.get("complete") or ([old["subdir"]] if old.get("subdir") else [])
+            except (OSError, ValueError):
+                prev = []
+        older = [d for d in prev if d != sub and os.path.isdir(os.path.join(dirpath, d))]
+        complete = (older[-(keep - 1):] if keep > 1 else []) + [sub]
         tmp = os.path.join(dirpath, "meta.json.tmp")
         with open(tmp, "w") as f:
-            json.dump({"step": int(step), "world": int(world), "sharded": sharded, "subdir": sub}, f)
+            json.dump({"step": int(step), "world": int(world), "sharded": sharded, "subdir": sub,
+                       "complete": complete}, f)
             f.flush()
             os.fsync(f.fileno())
-        os.replace(tmp, os.path.join(dirpath, "meta.json"))
-        # prune: never the directory the pointer names, keep the newest `keep`
-        dirs = [d for d in _step_dirs(dirpath) if d[1] != sub]
-        for _, name in dirs[:max(0, len(dirs) - (keep - 1))]:
-            shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
+        os.replace(tmp, meta_path)
+        for _, name in _step_dirs(dirpath):
+            if name not in complete:
+                shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
     _barrier(world)
 
 

@@ -58,12 +58,14 @@ class Configuration:
         if st.get("token"):
             self.token = st["token"]
         if st.get("clientCertificateData") and st.get("clientKeyData"):
-            # one pair of files per Configuration, rewritten in place on refresh and removed at
-            # exit (the key is a secret: never leave one temp file per request behind)
+            # one pair of files per Configuration inside a private (0700) directory, rewritten on
+            # refresh and removed at exit (the key is a secret: never leave one temp file per
+            # request behind, and never write it where another local user can pre-create names)
             if self._exec_files is None:
-                self._exec_files = (_new_private_file(".crt"), _new_private_file(".key"))
+                d = tempfile.mkdtemp(prefix="pytorchjob-exec-")  # mode 0700
+                self._exec_files = (os.path.join(d, "client.crt"), os.path.join(d, "client.key"))
                 import atexit
-                atexit.register(_remove_files, self._exec_files)
+                atexit.register(_remove_files, self._exec_files, d)
             _write_private(self._exec_files[0], st["clientCertificateData"])
             _write_private(self._exec_files[1], st["clientKeyData"])
             self.cert_file, self.key_file = self._exec_files
@@ -92,24 +94,31 @@ def _parse_rfc3339(s: str) -> float:
     return float(calendar.timegm(time.strptime(s, "%Y-%m-%dT%H:%M:%S")))
 
 
-def _new_private_file(suffix: str) -> str:
-    fd, path = tempfile.mkstemp(suffix=suffix, prefix="pytorchjob-exec-")  # mode 0600
-    os.close(fd)
-    return path
-
-
 def _write_private(path: str, text: str) -> None:
-    tmp = path + ".tmp"
-    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
-    with os.fdopen(fd, "w") as f:
-        f.write(text)
-    os.replace(tmp, path)
+    """Atomically replace ``path`` (in a private directory) with a new 0600 file: the temp file
+    is created with O_EXCL by mkstemp in the same directory, never at a guessable name."""
+    fd, tmp = tempfile.mkstemp(dir=os.path.dirname(path), prefix=".tmp-")
+    try:
+        with os.fdopen(fd, "w") as f:
+            f.write(text)
+        os.replace(tmp, path)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
 
 
-def _remove_files(paths) -> None:
+def _remove_files(paths, directory: Optional[str] = None) -> None:
     for p in paths:
         try:
             os.unlink(p)
+        except OSError:
+            pass
+    if directory:
+        try:
+            os.rmdir(directory)
         except OSError:
             pass
 

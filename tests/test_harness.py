@@ -367,6 +367,50 @@ def test_zero_adamw_unused_parameter_matches_master_adamw():
     assert not torch.equal(m2.a.weight, m1.a.weight * 0)  # the used parameters did move
 
 
+def test_zero_adamw_parameter_skipping_a_step_keeps_its_own_step_count():
+    """a parameter that gets no gradient in one step and then trains again uses its
+    own AdamW step count for the bias correction afterwards (MasterAdamW's st["step"]), not the
+    optimizer's global count."""
+    import copy
+    import torch.nn as nn
+    from pytorch_operator_amd.ops.optim import MasterAdamW
+    from pytorch_operator_amd.parallel.zero import ZeroAdamW
+
+    class Gated(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(8, 8)
+            self.side = nn.Linear(8, 8)  # same bucket; skipped on odd steps
+            self.b = nn.Linear(8, 4)
+
+        def forward(self, x, use_side):
+            h = torch.relu(self.a(x))
+            if use_side:
+                h = h + self.side(h)
+            return self.b(h)
+
+    torch.manual_seed(3)
+    m1 = Gated()
+    m2 = copy.deepcopy(m1)
+    o1 = MasterAdamW(m1.parameters(), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1)
+    o2 = ZeroAdamW(m2, lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=1.0)
+    assert len(o2.buckets) == 1
+    x = torch.randn(5, 8)
+    for step in range(5):
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad(set_to_none=True)
+            m(x, step % 2 == 0).square().mean().backward()
+            o.step()
+    assert o2.pstep[id(m2.side.weight)] == 3 and o2.pstep[id(m2.a.weight)] == 5
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(a, b, rtol=0, atol=1e-6), n
+    # the per-parameter counts survive a shard checkpoint round trip
+    sd = o2.shard_state_dict()
+    o3 = ZeroAdamW(copy.deepcopy(m2), lr=1e-2, betas=(0.9, 0.95), weight_decay=0.1, bucket_mb=1.0)
+    o3.load_shard_state_dict(sd)
+    assert sorted(o3.pstep.values()) == sorted(o2.pstep.values())
+
+
 def test_zero_adamw_hook_without_gradient():
     """Autograd runs post-accumulate hooks even when a backward returns None for a leaf -- what
     linear_tn does for a weight whose gradient sink it wrote in place.  ZeroAdamW must treat
@@ -508,3 +552,21 @@ def test_train_ckpt_interrupted_save_keeps_previous_checkpoint(tmp_path):
     assert sorted(os.listdir(d)) == ["meta.json", "step_11", "step_12"]
     assert train_ckpt.load(d, m2, opt2, rank=0, world=1, device="cpu") == 12
     assert torch.equal(m2.weight, m.weight)
+
+
+def test_train_ckpt_resume_after_crash_keeps_the_fallback(tmp_path):
+    """resume from step_5 with a dead (incomplete) step_9 left behind, then save 6:
+    the complete step_5 stays as the fallback and the partial step_9 is pruned."""
+    import torch.nn as nn
+    from pytorch_operator_amd.utils import train_ckpt
+    torch.manual_seed(0)
+    m = nn.Linear(4, 3)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+    d = str(tmp_path / "ck")
+    train_ckpt.save(d, 5, m, opt, rank=0, world=1, keep=2)
+    os.makedirs(os.path.join(d, "step_9"))  # crashed save: files partly written, pointer never moved
+    assert train_ckpt.load(d, m, opt, rank=0, world=1, device="cpu") == 5
+    train_ckpt.save(d, 6, m, opt, rank=0, world=1, keep=2)
+    assert sorted(os.listdir(d)) == ["meta.json", "step_5", "step_6"]
+    with open(os.path.join(d, "meta.json")) as f:
+        assert json.load(f)["complete"] == ["step_5", "step_6"]

@@ -204,6 +204,12 @@ def test_sanitized_operator_concurrent_jobs_with_churn(tmp_path, san):
                         done[n] = t
             time.sleep(0.3)
         assert done == want, (done, open(c.operator_log).read()[-4000:])
+        # the failed and restarted counters move together (status.go:128-129), each
+        # persisted transition counted once under --threadiness=4 status-write conflicts; the
+        # two Never-policy jobs are the only failures that are not restarts
+        failed = c.metric_value("pytorch_operator_jobs_failed_total")
+        restarted = c.metric_value("pytorch_operator_jobs_restarted_total")
+        assert restarted >= 3 and failed == restarted + 2, (failed, restarted)
         for n in want:
             c.rest.delete(PYTORCHJOBS, n, "default")
         time.sleep(1.0)

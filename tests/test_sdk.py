@@ -169,9 +169,13 @@ def test_sdk_is_a_standalone_distribution(cluster, tmp_path):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import shutil
     target = tmp_path / "site"
+    src = tmp_path / "sdk_src"  # a copy: pip's build/ directory must not land in the repository
+    shutil.copytree(os.path.join(root, "sdk", "python"), src,
+                    ignore=shutil.ignore_patterns("build", "*.egg-info", "__pycache__"))
     r = subprocess.run([sys.executable, "-m", "pip", "install", "--no-deps", "--no-build-isolation",
-                        "--no-index", "--target", str(target), os.path.join(root, "sdk", "python")],
+                        "--no-index", "--target", str(target), str(src)],
                        capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     dist = [p.name for p in target.iterdir() if p.name.endswith(".dist-info")]

@@ -274,6 +274,11 @@ def test_sdk_cert_only_exec_plugin_runs_once_and_reuses_one_key_file(pki, tmp_pa
     cfg.refresh_credentials(force=True)  # a forced refresh rewrites the same two files
     assert (cfg.cert_file, cfg.key_file) == first and counter.read_text() == "xx"
     assert open(cfg.key_file).read() == open(key).read()
+    # the pair lives in a private 0700 directory (no predictable names in the shared
+    # temp dir that another local user could pre-create), rewritten through mkstemp temp files
+    d = os.path.dirname(cfg.key_file)
+    assert os.path.dirname(cfg.cert_file) == d and os.stat(d).st_mode & 0o777 == 0o700
+    assert sorted(os.listdir(d)) == ["client.crt", "client.key"]
 
 
 def test_operator_kills_a_hanging_exec_plugin(pki, tmp_path):

@@ -11,7 +11,10 @@ export PYTHONUNBUFFERED=1
 libs="in-tree $(ls pytorch_operator_amd/_lib/exp/*.so 2>/dev/null)"
 for lib in $libs; do
   tag=$(basename $lib .so); L=$lib; [ "$lib" = in-tree ] && L=""
-  PTO_HIP_LIB=$L timeout -k 10 120 python tools/step_timeline.py --json $O/timeline_$tag.json > $O/timeline_$tag.txt 2>&1 || { cat $O/timeline_$tag.txt; exit 1; }
+  PTO_HIP_LIB=$L timeout -k 10 200 python -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
+    -k "fused_step or round3 or staged or stream_launch" > $O/pytest_$tag.log 2>&1 || { tail -30 $O/pytest_$tag.log; exit 1; }
+  FB=""; case $tag in *fb*) FB=1;; esac
+  PTO_TIMELINE_FB=$FB PTO_HIP_LIB=$L timeout -k 10 120 python tools/step_timeline.py --json $O/timeline_$tag.json > $O/timeline_$tag.txt 2>&1 || { cat $O/timeline_$tag.txt; exit 1; }
   echo "== $tag"; grep -E "period|one step" $O/timeline_$tag.txt
 done
 for rep in $(seq 1 $REPS); do

@@ -34,6 +34,8 @@ NAMES = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]
 # block ranges of the launches that run several jobs (B = 64): name -> [(first, end, job)]
 GROUPS = {"fc1_bwd": [(0, 200, "dW_fc1"), (200, 400, "dz2"), (400, 404, "fc2+stats"), (404, 420, "stage")],
           "tail": [(0, 201, "conv reduce+sgd"), (201, 598, "fc sgd")]}
+if os.environ.get("PTO_TIMELINE_FB"):  # library built with PTO_FB & 1: the dz2 job takes ids 0..199
+    GROUPS["fc1_bwd"] = [(0, 200, "dz2"), (200, 400, "dW_fc1"), (400, 404, "fc2+stats"), (404, 420, "stage")]
 
 
 def analyse(dbg: torch.Tensor, nslots: int):
@@ -46,8 +48,13 @@ def analyse(dbg: torch.Tensor, nslots: int):
         valid = w > 0
         last = (w * valid).max(1).values
         idx = torch.nonzero(used).flatten()
+        both = valid[:, 1:] & valid[:, :-1]
+        dph = (w[:, 1:] - w[:, :-1]) * both
+        phases = (dph.sum(0) / both.sum(0).clamp_min(1) / 100.0).tolist()
+        nph = int(both.any(0).sum())
         out.append({"blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
-                    "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist()))})
+                    "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist())),
+                    "phases": phases[:nph]})
     return out
 
 
@@ -93,7 +100,9 @@ def main(argv=None):
                      "blocks": samples[0][k]["blocks"], "start_us": round(med["start"], 2),
                      "span_us": round(med["end"] - med["start"], 2),
                      "p50_block_end_us": round(med["p50end"] - med["start"], 2),
-                     "gap_from_prev_us": round(gaps[len(gaps) // 2], 2)})
+                     "gap_from_prev_us": round(gaps[len(gaps) // 2], 2),
+                     "phase_means_us": [round(sum(x["phases"][j] for x in (s_[k] for s_ in samples)) / len(samples), 2)
+                                        for j in range(len(samples[0][k]["phases"]))]})
     for r, k in zip(rows, range(nk)):
         if r["kernel"] in GROUPS:
             r["jobs"] = {}
@@ -113,6 +122,8 @@ def main(argv=None):
               ("   last block end by job: " + ", ".join(f"{j} {v}" for j, v in r["jobs"].items())
                if r.get("jobs") else ""))
     print(f"one step: sum of spans {res['sum_span_us']} us + sum of gaps {res['sum_gap_us']} us")
+    print("mean block phase times (us, stamp k -> k+1): " +
+          "; ".join(f"{r['kernel']} {r['phase_means_us']}" for r in rows[per:]))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
