@@ -49,24 +49,6 @@ using namespace pto;
 // fc1 split-K factor of the training path: 256 workgroups of 5 waves (K = 800 = 2 x 400)
 constexpr int FC1_KS = 2;
 
-// PTO_WT (A/B, tools/build_exp.sh): write-through (sc1) stores for the bytes a launch hands to a
-// later one -- bit 0: the tail's parameters / momentum / reduced conv grads, bit 1: fc1_bwd's
-// dW_fc1, bit 2: conv_bwd4's chunk slab rows
-#ifndef PTO_WT
-#define PTO_WT 0
-#endif
-constexpr bool WT_TAIL = (PTO_WT & 1) != 0;
-constexpr bool WT_FC1 = (PTO_WT & 2) != 0;
-constexpr bool WT_SLAB = (PTO_WT & 4) != 0;
-constexpr bool WT_TAIL_FC = (PTO_WT & 8) != 0;  // only the tail's fc-parameter SGD stores
-// PTO_FB (A/B): fc1_bwd block layout -- bit 0: the dz2 job (the launch's critical path into the
-// conv backward) takes the first block ids, so it is dispatched first onto idle CUs; bit 1: its
-// blocks are ordered so the four sample tiles of one feature tile share an XCD (round-robin
-// placement: blocks b and b + 8 share one) and read that W1 column slab into one L2
-#ifndef PTO_FB
-#define PTO_FB 0
-#endif
-
 namespace {
 
 typedef unsigned long long u64;
@@ -801,6 +783,202 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// D2: fc1 forward + head in ONE launch (the training path; replaces fc1_fwd<2> + head<1> and
+// their dependent launch boundary).  The 256 blocks are fc1_fwd_kernel<2>'s: each writes its
+// 16 x 16 pre-activation partial with write-through (sc1) 16-B stores, waits for them, and one
+// lane adds 1 to its sample tile's arrival counter (agent-scope atomic).  The block whose add
+// returns 63 -- the tile's 64th arrival (32 feature tiles x 2 K halves) -- runs the head for
+// the tile's 16 samples, reading the partials with sc1 loads: MI355X_MICROARCH.md's cross-CU
+// hand-off table, row 1 (no fence; every other block just exits).  It resets the counter for
+// the next launch.  The head itself is on MFMA:
+//   logits[16 x 16] = relu(P0 + P1 + b1) . W2^T   K = 500 in 32 chunks of 16, chunk c on wave
+//                     c % 5; inside a chunk lane (i, g) takes k = 16c + 4g + e in MFMA step e
+//                     (the same K permutation on both operands), so every operand is a float4
+//   softmax / NLL / argmax on wave 0, one 16-lane row per 4 samples (lane i = class i)
+//   dh^T[k][s] = W2^T . dl^T per chunk (K = 10 classes padded to 12: 3 MFMAs); lane (i, g) ends
+//                with dh[sample i][16c + 4g + r], the k its h registers hold: ReLU mask + float4
+// Deterministic: the head's result does not depend on which block arrived last.
+// ---------------------------------------------------------------------------
+struct FcHead {
+  const float *x, *w1, *b1, *w2, *b2;
+  const int* lab;
+  float* parts;  // [2][B][500] pre-activation partials (scratch)
+  int* cnt;      // [ceil(B / 16)] arrival counters, 0 between launches
+  float *h_out, *dh, *dlogits, *per_sample;
+  float grad_scale;
+  int B;
+};
+constexpr int FH_NW = 5;                     // waves per block (fc1_fwd_kernel<2>)
+constexpr int FH_ARRIVALS = 32 * 2;          // blocks per sample tile
+constexpr int FH_CPW = (32 + FH_NW - 1) / FH_NW;  // K chunks per wave in the head (7)
+
+__global__ __launch_bounds__(64 * FH_NW) void fc1_head_kernel(FcHead a, u64* dbg) {
+  __shared__ f32x4 red[FH_NW][64];
+  __shared__ float dl_s[16][17];
+  __shared__ int last_s;
+  const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, tid = threadIdx.x;
+  stamp(dbg, 0);
+  const int B = a.B;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t P = buf_rsrc(a.parts, (unsigned)(2 * B * 500 * 4));
+  {  // ---- fc1 partial: as fc1_fwd_kernel<2>
+    const int row = mt * 16 + i, col = nt * 16 + i;
+    const bool rv = row < B, cv = col < 500;
+    const int k0 = (kz * FH_NW + wv) * 80 + g * 4;
+    const float4* xa = reinterpret_cast<const float4*>(a.x + (size_t)(rv ? row : B - 1) * 800 + k0);
+    const float4* wb = reinterpret_cast<const float4*>(a.w1 + (size_t)(cv ? col : 499) * 800 + k0);
+    float4 av[5], bv[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) { av[s] = xa[4 * s]; bv[s] = wb[4 * s]; }
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const float* ae = &av[s].x;
+      const float* be = &bv[s].x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = rv ? ae[e] : 0.f;
+        const float y = cv ? be[e] : 0.f;
+        if (e & 1) c1 = mfma16x16x4(x, y, c1);
+        else c0 = mfma16x16x4(x, y, c0);
+      }
+    }
+    red[wv][lane] = c0 + c1;
+    __syncthreads();
+    if (tid < 64) {  // thread = (tile row, 4 consecutive columns): one 16-B sc1 store
+      const int tr = tid >> 2, cg = tid & 3;
+      const int orow = mt * 16 + tr, ocol = nt * 16 + 4 * cg;
+      float sv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < FH_NW; ++q) acc += red[q][(tr >> 2) * 16 + 4 * cg + e][tr & 3];
+        sv[e] = acc;
+      }
+      if (orow < B && ocol < 500)
+        store_sc1(P, (unsigned)((((size_t)kz * B + orow) * 500 + ocol) * 4),
+                  make_float4(sv[0], sv[1], sv[2], sv[3]));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0)
+      last_s = __hip_atomic_fetch_add(a.cnt + mt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               FH_ARRIVALS - 1;
+    __syncthreads();
+    stamp(dbg, 1);
+    if (!last_s) return;  // block-uniform
+  }
+  if (tid == 0) __hip_atomic_store(a.cnt + mt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ---- head for samples mt * 16 + [0, 16): every load first (partials sc1, parameters plain),
+  // all unconditional from clamped addresses; padding is zeroed by multiplying the W2 operands
+  // by a 0/1 mask (every value is finite), so no load sits behind a branch.  Rows >= B compute
+  // row B - 1's values and store nothing.
+  const int srow = mt * 16 + i;
+  const bool rv = srow < B;
+  const int rc = rv ? srow : B - 1;
+  float4 hv[FH_CPW], wl[FH_CPW];
+  float wt[FH_CPW][3];
+#pragma unroll
+  for (int u = 0; u < FH_CPW; ++u) {
+    const int c = wv + FH_NW * u;
+    const int kb = 16 * c + 4 * g;
+    const bool kv = c < 32 && kb < 500;
+    const int kc = kv ? kb : 496;
+    const float4 p0 = load_sc1(P, (unsigned)(((size_t)rc * 500 + kc) * 4));
+    const float4 p1 = load_sc1(P, (unsigned)((((size_t)B + rc) * 500 + kc) * 4));
+    const float4 b1 = *reinterpret_cast<const float4*>(a.b1 + kc);
+    const float4 w = *reinterpret_cast<const float4*>(a.w2 + (i < 10 ? i : 9) * 500 + kc);
+    hv[u] = make_float4(fmaxf(p0.x + p1.x + b1.x, 0.f), fmaxf(p0.y + p1.y + b1.y, 0.f),
+                        fmaxf(p0.z + p1.z + b1.z, 0.f), fmaxf(p0.w + p1.w + b1.w, 0.f));
+    const float wm = (kv && i < 10) ? 1.f : 0.f;
+    wl[u] = make_float4(w.x * wm, w.y * wm, w.z * wm, w.w * wm);
+    const int kd = min(16 * c + i, 499);  // dh pass: A[k row i][class 4s + g] = W2[4s + g][16c + i]
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int j = 4 * s + g;
+      const float v = a.w2[(j < 10 ? j : 9) * 500 + kd];
+      wt[u][s] = v * ((j < 10 && c < 32 && 16 * c + i < 500) ? 1.f : 0.f);
+    }
+  }
+  int tl[4];  // labels of samples 4g + r (wave 0's softmax)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tl[r] = a.lab[min(mt * 16 + 4 * g + r, B - 1)];
+  const float bias = a.b2[i < 10 ? i : 0];
+  f32x4 acc0 = zero4(), acc1 = zero4();  // two chains: C[sample 4g + r][class i]
+#pragma unroll
+  for (int u = 0; u < FH_CPW; ++u) {
+    const float* hx = &hv[u].x;
+    const float* wx = &wl[u].x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e & 1) acc1 = mfma16x16x4(hx[e], wx[e], acc1);
+      else acc0 = mfma16x16x4(hx[e], wx[e], acc0);
+    }
+  }
+  red[wv][lane] = acc0 + acc1;
+  __syncthreads();
+  stamp(dbg, 2);
+  if (wv == 0) {
+    f32x4 L = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < FH_NW; ++q) L += red[q][lane];
+    const bool cls = i < 10;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ts = 4 * g + r, b = mt * 16 + ts;
+      const bool bv = b < B;
+      const int t = tl[r];
+      const float l = L[r] + bias;
+      float m = cls ? l : -INFINITY;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+      float se = cls ? __expf(l - m) : 0.f;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) se += __shfl_xor(se, o, 16);
+      const float lse = m + __logf(se);
+      int pred = (cls && l == m) ? i : 16;  // first maximum
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) pred = min(pred, __shfl_xor(pred, o, 16));
+      const float lt = __shfl(l, t, 16);
+      const float dl = cls ? (__expf(l - lse) - (i == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+      dl_s[ts][i] = dl;
+      if (bv) {
+        if (cls) a.dlogits[(size_t)b * 10 + i] = dl;
+        if (i == 0) {
+          a.per_sample[2 * b] = lse - lt;
+          a.per_sample[2 * b + 1] = pred == t ? 1.f : 0.f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- dh = (dl . W2) * (h > 0), and h itself, for this wave's chunks
+  float dlr[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) dlr[s] = dl_s[i][min(4 * s + g, 15)];  // B[class 4s + g][sample i]
+#pragma unroll
+  for (int u = 0; u < FH_CPW; ++u) {
+    const int c = wv + FH_NW * u;
+    const int kb = 16 * c + 4 * g;
+    if (c < 32) {  // wave-uniform
+      f32x4 d = zero4();
+#pragma unroll
+      for (int s = 0; s < 3; ++s) d = mfma16x16x4(wt[u][s], dlr[s], d);
+      if (rv && kb < 500) {
+        const float4 h = hv[u];
+        *reinterpret_cast<float4*>(a.h_out + (size_t)srow * 500 + kb) = h;
+        *reinterpret_cast<float4*>(a.dh + (size_t)srow * 500 + kb) =
+            make_float4(h.x > 0.f ? d[0] : 0.f, h.y > 0.f ? d[1] : 0.f, h.z > 0.f ? d[2] : 0.f,
+                        h.w > 0.f ? d[3] : 0.f);
+      }
+    }
+  }
+  stamp(dbg, 3);
+}
+
+// ---------------------------------------------------------------------------
 // E: fc1 backward, three independent jobs in one launch (blockDim 512 = 8 waves):
 //   job 1 (200 blocks x 8 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B,
 //          64 samples per register-preloaded chunk), db_fc1 from the kt==0 tiles.
@@ -825,7 +1003,28 @@ __device__ __forceinline__ int batch_row_at(const BatchSrc& s, long long step, i
   return s.perm[i];
 }
 
+// DDP over xGMI (parallel/xgmi.py): fc1_bwd pushes each dW_fc1 tile straight into the receive
+// buffer of the rank that owns it (xgmi_allreduce.hip layout: recv[sender][shard] behind a 64 KB
+// header, element v of the flat gradient owned by rank v / shard4), so the exchange kernel's
+// phase 1 no longer re-reads and re-sends 93.9 % of the gradient bytes.  Write-through system-
+// scope stores (visible over the fabric whatever the IPC mapping's cache type), drained by every
+// pushing wave before it ends; the exchange raises its flags in a later launch of this stream.
+struct XPush {
+  char* base[8];  // every rank's exchange buffer (IPC-mapped); null: no push
+  int rank, world;
+  long shard4;    // float4s per owner shard
+  long w1_f4;     // flat float4 index of fc1.weight's first element
+};
+constexpr long kXarHdrBytes = 64 * 1024;  // xgmi_allreduce.hip kHdrBytes
+
+__device__ __forceinline__ void push_wt4(char* dst, float4 v) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v x = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(dst), "v"(x) : "memory");
+}
+
 struct Fc1Bwd {
+  XPush xp;
   const float *dh, *a2;
   const uint8_t* idx2;
   const float *w1, *dlog, *h;
@@ -857,19 +1056,20 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   const int nJ3 = (a.jobs & 4) ? E_NJ3 : 0;
   int blk = blockIdx.x;
   stamp(dbg, 0);
-  int t2x = -1;  // dz2 tile (mt * 50 + kt) when this block runs the dz2 job
-  if (PTO_FB & 1) {
-    // physical ids [0, nJ2): dz2, then [nJ2, nJ2 + nJ1): dW_fc1, then fc2 + staging as before
-    if (blk < nJ2) {
-      t2x = blk;
-      if ((PTO_FB & 2) && nJ2 == 200) {
-        const int s = (blk & 7) * 25 + (blk >> 3);  // blocks grouped by XCD: 25 per XCD
-        t2x = (s & 3) * 50 + (s >> 2);              // 4 consecutive slots = the 4 mt of one kt
-      }
-      blk = nJ1 + t2x;
-    } else if (blk < nJ2 + nJ1) {
-      blk -= nJ2;
+  // Block layout (round-4 A/B, profiles/r4_fb_ab.txt: -0.8 us per step): physical ids
+  // [0, nJ2) run the dz2 job -- the launch's critical path into the conv backward -- so it is
+  // dispatched first onto idle CUs, ordered so the four sample tiles of one feature tile share an
+  // XCD (round-robin placement: blocks b and b + 8 share one) and read that W1 column slab into
+  // one L2; then [nJ2, nJ2 + nJ1) dW_fc1, then fc2 + staging
+  if (blk < nJ2) {
+    int t2x = blk;  // dz2 tile mt * 50 + kt
+    if (nJ2 == 200) {
+      const int s = (blk & 7) * 25 + (blk >> 3);  // blocks grouped by XCD: 25 per XCD
+      t2x = (s & 3) * 50 + (s >> 2);              // 4 consecutive slots = the 4 mt of one kt
     }
+    blk = nJ1 + t2x;
+  } else if (blk < nJ2 + nJ1) {
+    blk -= nJ2;
   }
   if (blk < nJ1) {
     const int tile = blk * E_NW + wv;
@@ -902,8 +1102,18 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     const f32x4 c = c0 + c1;
     if (nv) {
       const unsigned e4 = (unsigned)(n * 200 + kt * 4 + g);  // float4 index of (n, 16 kt + 4 g)
-      st4<WT_FC1>(reinterpret_cast<float4*>(a.gw1), e4, make_float4(c[0], c[1], c[2], c[3]));
+      const float4 v4 = make_float4(c[0], c[1], c[2], c[3]);
+      reinterpret_cast<float4*>(a.gw1)[e4] = v4;
+      if (a.xp.base[0] != nullptr) {  // DDP over xGMI: also straight to the owner's receive buffer
+        const long v = a.xp.w1_f4 + (long)e4;
+        const int q = (int)(v / a.xp.shard4);
+        char* b = a.xp.base[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) b = q == k ? a.xp.base[k] : b;
+        push_wt4(b + kXarHdrBytes + (((long)a.xp.rank * a.xp.shard4 + (v - (long)q * a.xp.shard4)) << 4), v4);
+      }
     }
+    if (a.xp.base[0] != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (kt == 0) {
       dbsum = sum_lane_rows(dbsum);
       if (g == 0 && nv) a.gb1[n] = dbsum;
@@ -1622,8 +1832,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       const int j0 = jbase + jt * 16 + 4 * g;
       if (j0 >= 0 && j0 + 3 < 125) {
         const float4 v4 = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
-        if constexpr (WT_SLAB) store_wt(buf_rsrc(slab, 0xFFFFFFF0u), (unsigned)((rp + j0) - slab) * 4u, v4);
-        else *reinterpret_cast<float4*>(rp + j0) = v4;
+        *reinterpret_cast<float4*>(rp + j0) = v4;
       } else {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
@@ -1802,8 +2011,8 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];
       float4 bb = reinterpret_cast<float4*>(buf2)[v];
       sgd4(pp, bb, gg, hy);
-      st4<WT_TAIL || WT_TAIL_FC>(reinterpret_cast<float4*>(p2), v, pp);
-      st4<WT_TAIL || WT_TAIL_FC>(reinterpret_cast<float4*>(buf2), v, bb);
+      reinterpret_cast<float4*>(p2)[v] = pp;
+      reinterpret_cast<float4*>(buf2)[v] = bb;
     }
     stamp(dbg, 1);
     return;
@@ -1824,10 +2033,10 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     float4 r = red[0][tid];
 #pragma unroll
     for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
-    if (gout != nullptr) st4<WT_TAIL>(reinterpret_cast<float4*>(gout), col, r);
+    if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
     sgd4(pp, bb, r, hy);
-    st4<WT_TAIL>(reinterpret_cast<float4*>(p), col, pp);
-    st4<WT_TAIL>(reinterpret_cast<float4*>(buf), col, bb);
+    reinterpret_cast<float4*>(p)[col] = pp;
+    reinterpret_cast<float4*>(buf)[col] = bb;
   }
   if (step_counter != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(step_counter, 1);
   stamp(dbg, 1);
@@ -2004,12 +2213,36 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
   return (int)hipGetLastError();
 }
 
+// fc1 forward + head in one launch (fc1_head_kernel): parts [2][B][500] scratch, cnt
+// [ceil(B / 16)] int32 zeros (the kernel leaves them 0); writes h_out, dh, dlogits, per_sample.
+int pto_mnist_fc1_head(const float* x, const float* w1, const float* b1, const float* w2,
+                       const float* b2, const int* lab, int B, float grad_scale, float* parts,
+                       int* cnt, float* h_out, float* dh, float* dlogits, float* per_sample,
+                       void* stream) {
+  if (B <= 0 || B > (1 << 19)) return -1;  // parts bytes < 2^31 (32-bit buffer offsets)
+  if (lab == nullptr || cnt == nullptr || dlogits == nullptr || per_sample == nullptr) return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)w1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)parts) |
+       ((uintptr_t)h_out) | ((uintptr_t)dh)) & 15)
+    return -2;  // float4 rows
+  const FcHead a{x, w1, b1, w2, b2, lab, parts, cnt, h_out, dh, dlogits, per_sample, grad_scale, B};
+  hipLaunchKernelGGL(fc1_head_kernel, dim3(32, (B + 15) / 16, 2), dim3(64 * FH_NW), 0,
+                     (hipStream_t)stream, a, dbg_next());
+  return (int)hipGetLastError();
+}
+
 static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
   const int B = a.B;
   PTO_CHECK_B(B);
   if (a.jobs <= 0 || a.jobs > 7) return -1;
   if (a.gw1 == nullptr || a.gb1 == nullptr || a.gw2 == nullptr || a.gb2 == nullptr) return -1;
   if ((((uintptr_t)a.dh) | ((uintptr_t)a.gw1)) & 15) return -2;  // float4 dh rows (job 2), dW_fc1 stores
+  if (a.xp.base[0] != nullptr) {
+    if (a.xp.world < 2 || a.xp.world > 8 || a.xp.rank < 0 || a.xp.rank >= a.xp.world || a.xp.shard4 <= 0 ||
+        a.xp.w1_f4 < 0 || a.xp.w1_f4 + 100000 > a.xp.shard4 * a.xp.world)
+      return -1;
+    for (int q = 0; q < a.xp.world; ++q)
+      if (a.xp.base[q] == nullptr) return -1;
+  }
   int nst = 0;
   if (a.stage_x != nullptr) {
     if (a.nsrc.perm == nullptr || a.nsrc.cursor == nullptr || a.nsrc.labels == nullptr || !a.nsrc.is_u8 ||
@@ -2022,6 +2255,23 @@ static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
                      ((a.jobs & 4) ? E_NJ3 : 0) + nst;
   hipLaunchKernelGGL(fc1_bwd_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, a, dbg_next());
   return (int)hipGetLastError();
+}
+
+// fc1_bwd that also pushes dW_fc1 into the xGMI owners' receive buffers (xp_bases: `world`
+// device addresses in rank order, pto_xar_push_info), every job.
+int pto_mnist_fc1_bwd_push(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
+                           const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
+                           float* gb2, float* dz2, const float* per_sample, float* stats,
+                           float loss_scale, int B, void* const* xp_bases, int xp_rank, int xp_world,
+                           long xp_shard4, long xp_w1_f4, void* stream) {
+  Fc1Bwd a{};
+  if (xp_bases == nullptr || xp_world < 2 || xp_world > 8) return -1;
+  for (int q = 0; q < xp_world; ++q) a.xp.base[q] = static_cast<char*>(xp_bases[q]);
+  a.xp.rank = xp_rank; a.xp.world = xp_world; a.xp.shard4 = xp_shard4; a.xp.w1_f4 = xp_w1_f4;
+  a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
+  a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
+  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
+  return fc1_bwd_launch(a, stream);
 }
 
 int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,

@@ -32,20 +32,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
 
-// 16-byte store with the sc1 cache policy (write-through): the bytes leave the XCD's L2 with the
-// store instead of in the end-of-kernel L2 write-back that the next dependent launch waits
-// behind (MI355X_MICROARCH.md: the boundary grows by dirty bytes / ~6 TB/s).  Full 16-B stores
-// only: narrow write-through stores cost one fabric write each.
-__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float4 v) {
+// 16-B vector store / load with the sc1 cache policy (aux bit 4): the store writes through and
+// drops the line from this XCD's L2, the load bypasses L1 (MI355X_MICROARCH.md's cross-CU
+// hand-off table, row 1: producer sc1 stores + vmcnt(0) + agent atomic add, consumer sc1 loads)
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float4 v) {
   const u32x4 d = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
   __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, 16);
 }
-
-// float4 store to p[i], write-through when WT
-template <bool WT>
-__device__ __forceinline__ void st4(float4* p, unsigned i, float4 v) {
-  if constexpr (WT) store_wt(buf_rsrc(p, 0xFFFFFFF0u), i * 16u, v);
-  else p[i] = v;
+__device__ __forceinline__ float4 load_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16);
+  return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

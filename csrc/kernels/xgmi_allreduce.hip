@@ -53,7 +53,9 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxWorld = 8;
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;  // threads per exchange workgroup (the one-GPU-per-rank kernel)
+constexpr int kEmuThreads = 64;  // emulation of W x nblk > 1024 workgroups on one GPU: one wave each,
+                                 // so every emulated rank's workgroups fit on the device at once
 constexpr int kMaxBlocks = 256;
 constexpr size_t kHdrBytes = 64 * 1024;  // flag1 + flag2 + stepc (<= 2*8*256*4 + 1 KB)
 
@@ -75,6 +77,10 @@ struct XarArgs {
   const float* slab;
   int slab_rows, slab_rows_big;
   long slab_stride, conv4, big_lo4, big_hi4;
+  // [skip_lo4, skip_hi4): gradient float4s an earlier launch of this step already pushed into
+  // their owners' receive buffers (fc1_bwd's dW_fc1 tiles, mnist_kernels.hip XPush); phase 1
+  // produces and pushes only the rest
+  long skip_lo4, skip_hi4;
   int* err;
   long long timeout_ticks;  // wall_clock64 ticks (100 MHz)
   unsigned long long* stamps;  // optional: 4 wall_clock64 stamps per (rank, block)
@@ -192,13 +198,14 @@ __device__ __forceinline__ void deposit(const XarArgs& a, long v, f4 g, bool deg
   push4(recv_buf(peer(a, q)) + (long)a.rank * a.shard4 + pos, g);
 }
 
-// Wait until every flag in `f[idx]` (idx = tid, tid + kThreads, ... < nf) is >= target.
+// Wait until every flag in `f[idx]` (idx = tid, tid + NT, ... < nf) is >= target.
 // All of a thread's flags are loaded back to back (one local round trip per poll), the
 // block leaves together.  False (error flagged) on timeout.
+template <int NT>
 __device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long deadline, int* err) {
   for (;;) {
     int pending = 0;
-    for (int i = threadIdx.x; i < nf; i += kThreads) pending |= load_sys(f + i) < target;
+    for (int i = threadIdx.x; i < nf; i += NT) pending |= load_sys(f + i) < target;
     if (!__syncthreads_or(pending)) return true;
     if ((long long)wall_clock64() > deadline) {
       if (threadIdx.x == 0) atomicOr(err, 1);
@@ -211,7 +218,9 @@ __device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long
 constexpr int kP2 = 2;  // phase-2 elements per thread per batch
 constexpr int kP3 = 4;  // phase-3 float4s per thread per batch
 
+template <int NT>
 __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
+  constexpr int kThreads = NT;
   __shared__ unsigned s_step;
   __shared__ int s_degraded;
   __shared__ f4 part[kThreads];
@@ -232,18 +241,26 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   // ---- phase 1: produce my gradient slice and push it to the owners
   {
     const long c4 = a.slab != nullptr ? a.conv4 : 0;
-    const long rest = a.npad4 - c4;
+    // the copied segment: logical index L -> flat float4 v = c4 + L, stepping over the
+    // pre-pushed range [skip_lo4, skip_hi4) (host-checked: skip_lo4 >= c4)
+    const long skip = a.skip_hi4 - a.skip_lo4;
+    const long rest = a.npad4 - c4 - skip;
     const long per = (rest + a.nblk - 1) / a.nblk;
-    const long lo4 = c4 + (long)b * per, hi4 = min(lo4 + per, a.npad4);
+    const long lo4 = (long)b * per, hi4 = min(lo4 + per, rest);
+    auto vmap = [&](long L) {
+      const long v = c4 + L;
+      return v >= a.skip_lo4 ? v + skip : v;
+    };
     // first batch of the copied segment: loads in flight while the slab rows are summed
     f4 g0, g1, g2, g3;
     // unconditional loads from clamped addresses, then selects (a predicated load becomes
     // a branch + a wait per element)
     const f4* gin = reinterpret_cast<const f4*>(a.in);
     const long vmax = a.n4 - 1;
-    auto ld = [&](long v) {
+    auto ld = [&](long L) {
+      const long v = vmap(L);
       const f4 x = gin[v < vmax ? v : vmax];
-      return (v < hi4 && v < a.n4) ? x : zero4;
+      return (L < hi4 && v < a.n4) ? x : zero4;
     };
     auto load_batch = [&](long v0) {
       g0 = ld(v0);
@@ -280,10 +297,17 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     }
     for (long v0 = lo4 + tid; v0 < hi4; v0 += 4 * kThreads) {
       if (v0 != lo4 + tid) load_batch(v0);
-      deposit(a, v0, g0, degraded);
-      if (v0 + kThreads < hi4) deposit(a, v0 + kThreads, g1, degraded);
-      if (v0 + 2 * kThreads < hi4) deposit(a, v0 + 2 * kThreads, g2, degraded);
-      if (v0 + 3 * kThreads < hi4) deposit(a, v0 + 3 * kThreads, g3, degraded);
+      deposit(a, vmap(v0), g0, degraded);
+      if (v0 + kThreads < hi4) deposit(a, vmap(v0 + kThreads), g1, degraded);
+      if (v0 + 2 * kThreads < hi4) deposit(a, vmap(v0 + 2 * kThreads), g2, degraded);
+      if (v0 + 3 * kThreads < hi4) deposit(a, vmap(v0 + 3 * kThreads), g3, degraded);
+    }
+    if (degraded && skip > 0) {
+      // rank-local fallback: the pre-pushed range still needs its local SGD step (the
+      // pushing launch also stored it to `in`); block b takes its share of it
+      const long sper = (skip + a.nblk - 1) / a.nblk;
+      const long s0 = a.skip_lo4 + (long)b * sper, s1 = min(s0 + sper, a.skip_hi4);
+      for (long v = s0 + tid; v < s1; v += kThreads) deposit(a, v, grad4(a, v), true);
     }
     if (degraded) {
       if (a.step_counter != nullptr && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
@@ -312,7 +336,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     };
     load_pb(tid);  // in flight while waiting
     // every sender block's flag (or timed out: go on, the error is set); block-uniform
-    wait_flags(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err);
+    wait_flags<NT>(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err);
     acquire_fence(a);
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
       // every sender's contribution in flight at once (clamped addresses, no predicated
@@ -396,13 +420,27 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   if (st != nullptr && tid == 0) st[3] = wall_clock64();
 }
 
-__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body<kThreads>(a, blockIdx.x); }
 
 // Emulation of `world` ranks on ONE device in one launch (blockIdx.y = rank): all blocks
 // of all ranks are co-resident, so the protocol (and its latency floor over local HBM)
-// can be tested at any world size on a single GPU.
-__global__ __launch_bounds__(kThreads) void xar_kernel_emu(const XarArgs* __restrict__ all) {
-  xar_body(all[blockIdx.y], blockIdx.x);
+// can be tested at any world size on a single GPU.  NT = kEmuThreads when the emulated
+// grid (W x nblk workgroups) would not fit the device with 256-thread workgroups (W = 8 x
+// 256: the production geometry); same chunking, flags and phases, fewer lanes per chunk.
+template <int NT>
+__global__ __launch_bounds__(NT) void xar_kernel_emu(const XarArgs* __restrict__ all) {
+  xar_body<NT>(all[blockIdx.y], blockIdx.x);
+}
+
+// Emulated producer push (what fc1_bwd does with XPush): every emulated rank (blockIdx.y)
+// pushes its gradient float4s [skip_lo4, skip_hi4) into their owners' receive buffers, then
+// waits for the stores (the exchange launch that follows skips that range).
+__global__ __launch_bounds__(kThreads) void xar_emu_prepush(const XarArgs* __restrict__ all) {
+  const XarArgs& a = all[blockIdx.y];
+  for (long v = a.skip_lo4 + (long)blockIdx.x * kThreads + threadIdx.x; v < a.skip_hi4;
+       v += (long)gridDim.x * kThreads)
+    deposit(a, v, grad4(a, v), false);
+  __builtin_amdgcn_s_waitcnt(0);
 }
 
 struct XarCtx {
@@ -477,6 +515,18 @@ int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void
 }
 
 int pto_xar_alloc_kind(void* ctx) { return static_cast<XarCtx*>(ctx)->alloc_kind; }
+
+// What a producer kernel needs to push gradient float4s straight into their owners' receive
+// buffers (mnist_kernels.hip XPush): every rank's buffer base (world entries), this rank, the
+// world size and the float4s per owner shard.
+int pto_xar_push_info(void* ctx, void** bases, int* rank, int* world, long* shard4) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  for (int q = 0; q < c->world; ++q) bases[q] = c->base[q];
+  *rank = c->rank;
+  *world = c->world;
+  *shard4 = (c->npad >> 2) / c->world;
+  return 0;
+}
 long pto_xar_npad(void* ctx) { return static_cast<XarCtx*>(ctx)->npad; }
 
 // Map every peer's buffer (handles: world x 64 bytes, in rank order).
@@ -533,10 +583,16 @@ int pto_xar_allreduce(void* ctx, const float* in, float* out, float scale, void*
 int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
                           float dampening, float wd, float scale, int nesterov, int first_step,
                           int* step_counter, const float* slab, int slab_rows, long slab_stride,
-                          long conv_n, int slab_rows_big, long big_lo, long big_hi, void* stream) {
+                          long conv_n, int slab_rows_big, long big_lo, long big_hi, long skip_lo, long skip_hi,
+                          void* stream) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
   XarArgs a{};
   a.mode = 1;
+  if (skip_lo < 0 || skip_hi < skip_lo || skip_hi > c->n || (skip_lo & 3) || (skip_hi & 3) ||
+      (skip_hi > skip_lo && skip_lo < (slab != nullptr ? conv_n : 0)))
+    return -1;
+  a.skip_lo4 = skip_lo >> 2;
+  a.skip_hi4 = skip_hi >> 2;
   a.in = grads;
   a.p = p;
   a.mbuf = mbuf;
@@ -568,6 +624,9 @@ int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, 
 }
 
 // ---- single-device emulation of `world` ranks (tests / latency floor) -------------------
+// Emulated workgroup size: 256 threads while W x nblk <= 1024 (4 per CU), else one wave.
+static int emu_threads(int world, int nblk) { return world * nblk <= 1024 ? kThreads : kEmuThreads; }
+
 struct XarEmu {
   int world, nblk;
   long n, npad;
@@ -621,9 +680,12 @@ void pto_xar_emu_stamps(void* ctx, unsigned long long* buf) { static_cast<XarEmu
 int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* dst, const long long* mbuf,
                     const long long* slab, int slab_rows, long slab_stride, long conv_n, int slab_rows_big,
                     long big_lo, long big_hi, float lr, float momentum, float dampening, float wd,
-                    int nesterov, int first_step) {
+                    int nesterov, int first_step, long skip_lo, long skip_hi) {
   XarEmu* e = static_cast<XarEmu*>(ctx);
   XarArgs h[kMaxWorld];
+  if (skip_lo < 0 || skip_hi < skip_lo || skip_hi > e->n || (skip_lo & 3) || (skip_hi & 3) ||
+      (skip_hi > skip_lo && skip_lo < (slab != nullptr ? conv_n : 0)))
+    return -1;
   for (int r = 0; r < e->world; ++r) {
     XarArgs a{};
     for (int q = 0; q < kMaxWorld; ++q) a.base[q] = q < e->world ? e->base[q] : nullptr;
@@ -662,8 +724,10 @@ int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* d
       a.big_hi4 = big_hi >> 2;
       a.slab_stride = slab_stride;
       a.conv4 = conv_n >> 2;
-      if ((a.conv4 + e->nblk - 1) / e->nblk > kThreads) return -1;
+      if ((a.conv4 + e->nblk - 1) / e->nblk > emu_threads(e->world, e->nblk)) return -1;
     }
+    a.skip_lo4 = skip_lo >> 2;
+    a.skip_hi4 = skip_hi >> 2;
     a.err = e->err + r;
     a.timeout_ticks = e->timeout_ticks;
     a.stamps = e->stamps;
@@ -674,10 +738,26 @@ int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* d
   return 0;
 }
 
+int pto_xar_emu_threads(void* ctx) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  return emu_threads(e->world, e->nblk);
+}
+
 int pto_xar_emu_launch(void* ctx, void* stream) {
   XarEmu* e = static_cast<XarEmu*>(ctx);
-  hipLaunchKernelGGL(xar_kernel_emu, dim3(e->nblk, e->world), dim3(kThreads), 0, (hipStream_t)stream,
-                     e->d_args);
+  if (emu_threads(e->world, e->nblk) == kThreads)
+    hipLaunchKernelGGL(xar_kernel_emu<kThreads>, dim3(e->nblk, e->world), dim3(kThreads), 0, (hipStream_t)stream,
+                       e->d_args);
+  else
+    hipLaunchKernelGGL(xar_kernel_emu<kEmuThreads>, dim3(e->nblk, e->world), dim3(kEmuThreads), 0,
+                       (hipStream_t)stream, e->d_args);
+  return (int)hipGetLastError();
+}
+
+// The emulated producer push of the configured skip range (call before pto_xar_emu_launch).
+int pto_xar_emu_prepush(void* ctx, void* stream) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  hipLaunchKernelGGL(xar_emu_prepush, dim3(e->nblk, e->world), dim3(kThreads), 0, (hipStream_t)stream, e->d_args);
   return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@ pre-allocated workspaces, and a whole step can be captured into one hipGraph.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -147,7 +148,10 @@ class FusedMnistTrainer:
         #   conv_chunk 4: conv_bwd4 sums dW_conv2 over 4-sample chunks -> the slab the tail
         #                 reduces is 4x smaller (1: the per-sample conv_bwd, the fallback)
         #   stage_batches: fc1_bwd stages the next step's batch; conv12 reads it with one load
+        #   fuse_head: fc1 forward + head as one launch (fc1_head_kernel: the last-arriving
+        #              block of each 16-sample tile runs its head; False: fc1_fwd<2> + head)
         self.fuse_conv12 = True
+        self.fuse_head = os.environ.get("PTO_MNIST_FUSE_HEAD", "1") != "0"
         self.conv_chunk = 4
         self.stage_batches = True
 
@@ -179,6 +183,7 @@ class FusedMnistTrainer:
         self.per_sample = torch.empty((B, 2), device=dev)
         self.fc1_ks = self.K.fc1_split()
         self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
+        self.fc1_cnt = torch.zeros((B + 15) // 16, device=dev, dtype=torch.int32)  # fc1_head arrivals
         self.stage = K_stage(self.source, B, dev)
         # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
         # (conv_bwd4) per-4-sample-chunk rows for conv2.weight
@@ -206,11 +211,12 @@ class FusedMnistTrainer:
 
     # ---------------------------------------------------------------- step
     #
-    # One single-process step is six launches (one hipGraph, or the captured kernel list
+    # One single-process step is five launches (one hipGraph, or the captured kernel list
     # launched from C++ -- parallel/graphed_step.py):
     #
-    #   conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd (+ next-batch staging) -> conv_bwd4
-    #   -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor advance)
+    #   conv12_fwd -> fc1_head (fc1 forward + head) -> fc1_bwd (+ next-batch staging)
+    #   -> conv_bwd4 -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor
+    #   advance)
     #
     # DDP: with the xGMI kernel the tail launch is the cross-GPU exchange + SGD
     # (parallel/xgmi.py); with RCCL the fc / conv buckets are all-reduced between the pieces.
@@ -224,7 +230,8 @@ class FusedMnistTrainer:
                               (source is None or source is self.source)) else None
 
     def forward(self, source=None, B: Optional[int] = None) -> None:
-        """conv12_fwd (or conv1_fwd + conv2_fwd) + split-K fc1 (the head finishes h)."""
+        """conv12_fwd (or conv1_fwd + conv2_fwd) + fc1 and the head in one launch (``fuse_head``;
+        otherwise the split-K fc1 partials, which ``_head`` finishes)."""
         K, p = self.K, self._pv
         src = source or self.source
         B = self.B if B is None else B
@@ -239,25 +246,36 @@ class FusedMnistTrainer:
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
         ks = self.fc1_ks
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500))
+        hp = self.h_parts[:ks * B * 500].view(ks, B, 500)
+        if self.fuse_head:
+            K.fc1_head(self.a2[:B], p["fc1.weight"], p["fc1.bias"], p["fc2.weight"], p["fc2.bias"],
+                       self.lab[:B], grad_scale=1.0 / B, parts=hp, counters=self.fc1_cnt,
+                       h_out=self.h1[:B], dh=self.dh[:B], dlogits=self.dlogits[:B],
+                       per_sample=self.per_sample[:B])
+            return
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=hp)
 
     def _head(self, B: int) -> None:
-        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
+        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch; a
+        no-op with ``fuse_head``: forward ran it)."""
+        if self.fuse_head:
+            return
         K, p = self.K, self._pv
         hp = self.h_parts[:self.fc1_ks * B * 500].view(self.fc1_ks, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
-    def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None) -> None:
-        """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv."""
+    def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None, xpush: Optional[tuple] = None) -> None:
+        """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv;
+        with ``xpush``, also push dW_fc1 to its xGMI owners (ops.mnist.fc1_bwd)."""
         K, p, g = self.K, self._pv, self.grads
-        st = self._stage_for(None) if stage_adv is not None else None
+        st = self._stage_for(None) if stage_adv is not None and xpush is None else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
                   dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
                   loss_scale=1.0 / B, jobs=K.FC1_BWD_ALL, src=self.source if st is not None else None,
-                  stage=st, stage_adv=stage_adv or 0)
+                  stage=st, stage_adv=stage_adv or 0, xpush=xpush)
 
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self._pv
@@ -319,9 +337,14 @@ class FusedMnistTrainer:
             # xGMI path: one kernel reduces the per-sample conv-grad slabs, does the
             # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
             # updated parameters (parallel/xgmi.py).  flat_grads[:conv_end] is not written.
+            # fc1_bwd pushes dW_fc1 (93.9 % of the gradient) into its owners' receive buffers
+            # itself; the exchange produces and pushes only the rest
+            xar = self.grad_sync.xar
+            w1o = self.layout.offsets["fc1.weight"]
+            push = getattr(self.grad_sync, "push_fc1", True)
             self.forward(source, B)
             self._head(B)
-            self._fc1_bwd(B)
+            self._fc1_bwd(B, xpush=(*xar.push_info(), w1o) if push else None)
             self._conv_bwd(B)
             self.grad_sync.xar.allreduce_sgd_(
                 self.flat_grads, self._fp, self._fm, lr=self.lr,
@@ -329,14 +352,14 @@ class FusedMnistTrainer:
                 nesterov=self.nesterov, first_step=self._first_step,
                 step_counter=self.cursor if advance_cursor else None,
                 slab=self.conv_slab, slab_rows=B, conv_n=self.layout.conv_end,
-                slab_big=self._slab_big(B))
+                slab_big=self._slab_big(B), skip=(w1o, w1o + 400000) if push else None)
             self._first_step = False
             return
         if self.grad_sync is not None:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return
-        # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
+        # 5 launches: conv12_fwd -> fc1_head -> fc1_bwd -> conv_bwd4 -> tail
         K = self.K
         ce = self.layout.conv_end
         self.forward(source, B)

@@ -126,12 +126,14 @@ _SIGNATURES = {
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
+    "pto_mnist_fc1_head": [_VP, _VP, _VP, _VP, _VP, _VP, _I, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_ks": [],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     # xgmi_allreduce.hip
     "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],
@@ -140,12 +142,15 @@ _SIGNATURES = {
     "pto_xar_alloc_kind": [_VP],
     "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],
     "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _I, _L, _L,
-                              _I, _L, _L, _VP],
+                              _I, _L, _L, _L, _L, _VP],
+    "pto_xar_push_info": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_L)],
     "pto_xar_destroy": [_VP],
     "pto_xar_emu_create": [_I, _L, _I, ctypes.c_double, _I, _I, ctypes.POINTER(_VP)],
-    "pto_xar_emu_set": [_VP, _I, _VP, _VP, _VP, _VP, _I, _L, _L, _I, _L, _L, _F, _F, _F, _F, _I, _I],
+    "pto_xar_emu_set": [_VP, _I, _VP, _VP, _VP, _VP, _I, _L, _L, _I, _L, _L, _F, _F, _F, _F, _I, _I, _L, _L],
+    "pto_xar_emu_prepush": [_VP, _VP],
     "pto_xar_emu_launch": [_VP, _VP],
     "pto_xar_emu_error": [_VP],
+    "pto_xar_emu_threads": [_VP],
     "pto_xar_emu_destroy": [_VP],
     # rmsnorm.hip
     "pto_rmsnorm_fwd": [_VP, _VP, _VP, _VP, _L, _I, _F, _I, _VP],
@@ -206,18 +211,17 @@ def load(build_if_missing: bool = True):
         if not path.exists():
             raise NativeLibraryError(f"{path} missing; run pytorch_operator_amd.ops.build()")
         lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
-        for name, argtypes in _SIGNATURES.items():
-            fn = getattr(lib, name)
-            fn.argtypes = argtypes
-            fn.restype = ctypes.c_int
-        for name, argtypes in _LONG_FNS.items():
-            fn = getattr(lib, name)
-            fn.argtypes = argtypes
-            fn.restype = ctypes.c_long
-        for name, argtypes in _VOID_FNS.items():
-            fn = getattr(lib, name)
-            fn.argtypes = argtypes
-            fn.restype = None
+        variant = path != _LIB_PATH  # an A/B build may predate entry points it never exercises
+        for table, restype in ((_SIGNATURES, ctypes.c_int), (_LONG_FNS, ctypes.c_long), (_VOID_FNS, None)):
+            for name, argtypes in table.items():
+                try:
+                    fn = getattr(lib, name)
+                except AttributeError:
+                    if variant:
+                        continue
+                    raise
+                fn.argtypes = argtypes
+                fn.restype = restype
         _lib = lib
         return lib
 

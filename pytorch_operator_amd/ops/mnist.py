@@ -255,6 +255,40 @@ def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
     return out
 
 
+def fc1_head(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+             lab: torch.Tensor, *, grad_scale: float, parts: torch.Tensor, counters: torch.Tensor,
+             h_out: torch.Tensor, dh: torch.Tensor, dlogits: torch.Tensor, per_sample: torch.Tensor) -> None:
+    """fc1 forward + head in ONE launch (the training path; ``fc1_fwd_parts`` + ``head``).
+
+    ``h_out = relu(x @ w1.T + b1)``, fc2 + log-softmax + NLL per sample into ``per_sample``
+    [B,2] (loss, correct), ``dlogits`` [B,10] (scaled by ``grad_scale``) and ``dh`` [B,500]
+    (ReLU-masked).  ``parts`` (fp32 [2,B,500]) is scratch for the split-K partials;
+    ``counters`` (int32 [>= ceil(B/16)], zero) are the per-sample-tile arrival counters: the
+    last-arriving block of a tile runs that tile's head and leaves its counter at 0 again
+    (mnist_kernels.hip fc1_head_kernel).
+    """
+    lib = _native.load()
+    B = x.shape[0]
+    _req(x, (B, 800), torch.float32, "x")
+    _req(w1, (500, 800), torch.float32, "fc1.weight")
+    _req(b1, (500,), torch.float32, "fc1.bias")
+    _req(w2, (10, 500), torch.float32, "fc2.weight")
+    _req(b2, (10,), torch.float32, "fc2.bias")
+    _req(lab, (B,), torch.int32, "lab")
+    _req(parts, (2, B, 500), torch.float32, "fc1 partials")
+    if counters.dtype != torch.int32 or counters.numel() < (B + 15) // 16 or not counters.is_contiguous():
+        raise ValueError("counters: contiguous int32 with >= ceil(B/16) elements")
+    _req(h_out, (B, 500), torch.float32, "h_out")
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    rc = lib.pto_mnist_fc1_head(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                lab.data_ptr(), B, float(grad_scale), parts.data_ptr(),
+                                counters.data_ptr(), h_out.data_ptr(), dh.data_ptr(), dlogits.data_ptr(),
+                                per_sample.data_ptr(), _stream())
+    _native.check(rc, "fc1_head")
+
+
 def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *,
          grad_scale: float = 0.0, loss_scale: float = 1.0, want_grad: bool = True,
          want_logp: bool = False, stats: Optional[torch.Tensor] = None,
@@ -315,7 +349,8 @@ FC1_BWD_ALL = 7
 
 def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_sample=None,
             stats=None, loss_scale: float = 1.0, jobs: int = FC1_BWD_ALL,
-            src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None, stage_adv: int = 1):
+            src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None, stage_adv: int = 1,
+            xpush: Optional[tuple] = None):
     """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked).
 
     ``jobs`` selects which of the three independent parts to launch (so the weight
@@ -324,6 +359,9 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     ``stats[0] = sum(loss)*loss_scale`` and ``stats[1] = #correct``.
     With ``src`` + ``stage`` (all jobs), ceil(B/4) extra blocks stage the batch of step
     ``cursor + stage_adv`` for the next conv12_fwd.
+    ``xpush = (bases, rank, world, shard4, w1_offset)`` (DDP over xGMI, all jobs): dW_fc1 is also
+    pushed into the owning ranks' receive buffers (``XgmiAllReduce.push_info``; ``w1_offset`` =
+    float offset of fc1.weight in the flat gradient); the exchange then skips that range.
     """
     lib = _native.load()
     B = dh.shape[0]
@@ -353,6 +391,19 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
             src.cursor.data_ptr(), src.n_total, int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(),
             stage.tag.data_ptr(), _stream())
         _native.check(rc, "fc1_bwd(stage)")
+        return dz2
+    if xpush is not None:
+        if stage is not None or jobs != FC1_BWD_ALL:
+            raise ValueError("xpush runs every job and no staging")
+        bases, rank, world, shard4, w1_off = xpush
+        if w1_off % 4:
+            raise ValueError("fc1.weight must start on a float4 boundary of the flat gradient")
+        rc = lib.pto_mnist_fc1_bwd_push(
+            dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
+            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
+            _ptr(stats), float(loss_scale), B, bases, int(rank), int(world), int(shard4), int(w1_off) // 4,
+            _stream())
+        _native.check(rc, "fc1_bwd(xpush)")
         return dz2
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),

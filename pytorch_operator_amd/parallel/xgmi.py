@@ -100,13 +100,16 @@ class XgmiAllReduce:
                        nesterov: bool = False, first_step: bool = False,
                        step_counter: Optional[torch.Tensor] = None,
                        slab: Optional[torch.Tensor] = None, slab_rows: int = 0, conv_n: int = 0,
-                       slab_big: Optional[tuple] = None) -> None:
+                       slab_big: Optional[tuple] = None, skip: Optional[tuple] = None) -> None:
         """SGD with the mean gradient over ranks.  With ``slab`` ([rows, stride] fp32), the
         first ``conv_n`` gradient entries are the sum of its first ``slab_rows`` rows
         (fused deterministic reduction of the conv backward's partials); ``grads`` then
         only needs to hold the entries after ``conv_n``.  ``slab_big = (rows, lo, hi)``: the
         entries [lo, hi) (conv2.weight, written per 4-sample chunk by conv_bwd4) sum only
-        their first ``rows`` rows."""
+        their first ``rows`` rows.  ``skip = (lo, hi)``: gradient entries [lo, hi) a producer
+        launch of this step already pushed into their owners' receive buffers (fc1_bwd with
+        ``xpush``, ``push_info``); they must still be in ``grads`` (the degraded fallback's
+        local SGD reads them)."""
         for t in (grads, params, momentum_buf):
             self._check(t)
         sc = step_counter.data_ptr() if step_counter is not None else None
@@ -121,7 +124,18 @@ class XgmiAllReduce:
             self._ctx, grads.data_ptr(), params.data_ptr(), momentum_buf.data_ptr(), lr, momentum,
             dampening, weight_decay, 1.0 / self.world, int(nesterov), int(first_step), sc,
             sp, int(slab_rows), int(stride), int(conv_n), int(big_rows), int(big_lo), int(big_hi),
-            self._stream()), "pto_xar_allreduce_sgd")
+            int(skip[0]) if skip else 0, int(skip[1]) if skip else 0, self._stream()), "pto_xar_allreduce_sgd")
+
+    def push_info(self):
+        """(bases, rank, world, shard4) for a producer kernel that pushes gradient float4s into
+        their owners' receive buffers itself (``ops.mnist.fc1_bwd(xpush=...)``)."""
+        if getattr(self, "_push_info", None) is None:
+            bases = (ctypes.c_void_p * 8)()
+            rank, world, shard4 = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+            _native.check(self.lib.pto_xar_push_info(self._ctx, bases, ctypes.byref(rank), ctypes.byref(world),
+                                                     ctypes.byref(shard4)), "pto_xar_push_info")
+            self._push_info = (bases, rank.value, world.value, shard4.value)
+        return self._push_info
 
     def gather_sharded_(self, t: torch.Tensor) -> None:
         """Reassemble a tensor each rank only kept for its own shard (e.g. the momentum
@@ -221,6 +235,9 @@ class XgmiEmulation:
             raise XgmiUnavailable(f"pto_xar_emu_create failed ({rc})")
         self.npad = int(self.lib.pto_xar_emu_npad(self._ctx))
         self.nblk = nblk
+        # threads per emulated workgroup: 256 as on a node, or one wave when W x nblk > 1024
+        # (W = 8 x 256, the production geometry, fits the device only with 1-wave workgroups)
+        self.threads = int(self.lib.pto_xar_emu_threads(self._ctx))
         self.stamps = None
 
     def enable_stamps(self) -> torch.Tensor:
@@ -238,7 +255,10 @@ class XgmiEmulation:
 
     def configure(self, mode: int, inputs, dst, mbuf=None, slab=None, slab_rows: int = 0, conv_n: int = 0,
                   lr: float = 0.0, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                  nesterov: bool = False, first_step: bool = False, slab_big: Optional[tuple] = None) -> None:
+                  nesterov: bool = False, first_step: bool = False, slab_big: Optional[tuple] = None,
+                  skip: Optional[tuple] = None) -> None:
+        """``skip = (lo, hi)``: gradient entries a producer pushes itself (``prepush`` emulates
+        fc1_bwd's dW_fc1 push); the exchange's phase 1 skips them."""
         for t in list(inputs) + list(dst) + list(mbuf or []):
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == self.n
                     and t.data_ptr() % 16 == 0):
@@ -249,7 +269,12 @@ class XgmiEmulation:
         _native.check(self.lib.pto_xar_emu_set(
             self._ctx, int(mode), self._ptrs(inputs), self._ptrs(dst), self._ptrs(mbuf), self._ptrs(slab),
             int(slab_rows), int(stride), int(conv_n), int(big_rows), int(big_lo), int(big_hi), lr, momentum,
-            dampening, weight_decay, int(nesterov), int(first_step)), "pto_xar_emu_set")
+            dampening, weight_decay, int(nesterov), int(first_step), int(skip[0]) if skip else 0,
+            int(skip[1]) if skip else 0), "pto_xar_emu_set")
+
+    def prepush(self) -> None:
+        _native.check(self.lib.pto_xar_emu_prepush(
+            self._ctx, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "pto_xar_emu_prepush")
 
     def launch(self) -> None:
         _native.check(self.lib.pto_xar_emu_launch(
@@ -272,9 +297,12 @@ class XgmiEmulation:
 
 class XgmiGradSync:
     """``grad_sync`` for ``FusedMnistTrainer``: the all-reduce and SGD are one kernel,
-    issued from the trainer's step tail (capturable, so the step graph holds everything)."""
+    issued from the trainer's step tail (capturable, so the step graph holds everything).
+    ``push_fc1``: fc1_bwd pushes dW_fc1 into its owners' receive buffers itself and the
+    exchange skips it (default; ``PTO_XGMI_PUSH_FC1=0`` turns it off for A/B)."""
 
     fused_sgd = True
+    push_fc1 = os.environ.get("PTO_XGMI_PUSH_FC1", "1") != "0"
 
     def __init__(self, xar: XgmiAllReduce):
         self.xar = xar

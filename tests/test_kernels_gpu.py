@@ -354,3 +354,68 @@ def test_round3_step_matches_round2_step(lib, B):
     ce = new.layout.conv_end
     assert _rel(new.flat_grads[ce:], old.flat_grads[ce:]) < 1e-5
     assert _rel(new.flat_grads[:ce], old.flat_grads[:ce]) < 1e-5
+
+
+@pytest.mark.parametrize("B", [64, 50, 16, 1, 130])
+def test_fc1_head_fused_matches_split_launches(lib, B):
+    """fc1_head (fc1 forward + head in one launch, last-arriving block per 16-sample tile) vs
+    fc1_fwd_parts + head: h identical (same partial sums), the rest to fp32 rounding; the
+    arrival counters are 0 after every launch, across repeated launches."""
+    from pytorch_operator_amd.models.mnist import reference_init
+    from pytorch_operator_amd.ops import mnist as K
+    dev = torch.device("cuda")
+    sd = {k: v.to(dev).contiguous() for k, v in reference_init(7).items()}
+    g = torch.Generator().manual_seed(B)
+    a2 = torch.relu(torch.randn(B, 800, generator=g)).to(dev)
+    lab = torch.randint(0, 10, (B,), generator=g, dtype=torch.int32).to(dev)
+    parts = K.fc1_fwd_parts(a2, sd["fc1.weight"])
+    ref_ps = torch.zeros(B, 2, device=dev)
+    ref_dl = torch.zeros(B, 10, device=dev)
+    ref_dh = torch.zeros(B, 500, device=dev)
+    ref_h = torch.zeros(B, 500, device=dev)
+    K.head(parts[0], sd["fc2.weight"], sd["fc2.bias"], lab, grad_scale=1.0 / B, per_sample=ref_ps,
+           dlogits=ref_dl, dh=ref_dh, h_second=parts[1], fc1_bias=sd["fc1.bias"], h_out=ref_h)
+    cnt = torch.zeros((B + 15) // 16, dtype=torch.int32, device=dev)
+    scratch = torch.full((2, B, 500), float("nan"), device=dev)
+    outs = [torch.full(s, float("nan"), device=dev) for s in ((B, 500), (B, 500), (B, 10), (B, 2))]
+    for _ in range(3):
+        K.fc1_head(a2, sd["fc1.weight"], sd["fc1.bias"], sd["fc2.weight"], sd["fc2.bias"], lab,
+                   grad_scale=1.0 / B, parts=scratch, counters=cnt, h_out=outs[0], dh=outs[1],
+                   dlogits=outs[2], per_sample=outs[3])
+        torch.cuda.synchronize()
+        assert int(cnt.abs().sum()) == 0
+    h, dh, dl, ps = outs
+    assert torch.equal(h, ref_h)
+    assert _rel(dl, ref_dl) < 1e-5
+    assert _rel(dh, ref_dh) < 1e-5
+    assert _rel(ps[:, 0], ref_ps[:, 0]) < 1e-5
+    assert torch.equal(ps[:, 1], ref_ps[:, 1])
+    # against torch fp32 directly
+    rh = torch.relu(a2.cpu() @ sd["fc1.weight"].cpu().T + sd["fc1.bias"].cpu())
+    logits = rh @ sd["fc2.weight"].cpu().T + sd["fc2.bias"].cpu()
+    lp = torch.log_softmax(logits, 1)
+    assert _rel(ps[:, 0], -lp.gather(1, lab.cpu().long()[:, None])[:, 0]) < 1e-5
+    d = (lp.exp() - F.one_hot(lab.cpu().long(), 10).float()) / B
+    assert _rel(dl, d) < 1e-5
+    assert _rel(dh, (d @ sd["fc2.weight"].cpu()) * (rh > 0)) < 1e-5
+
+
+@pytest.mark.parametrize("B", [64, 37])
+def test_fused_head_step_matches_unfused_step(lib, B, monkeypatch):
+    """The 5-launch step (fc1_head) and the 6-launch step (fc1_fwd<2> + head) train the same
+    trajectory up to fp32 summation order."""
+    n = 8 * B
+    x, y = _data(n, seed=400 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(6)).to(torch.int32)
+    new = _stage_trainer(x, y, perm, B=B)
+    monkeypatch.setenv("PTO_MNIST_FUSE_HEAD", "0")
+    old = _stage_trainer(x, y, perm, B=B)
+    assert new.fuse_head and not old.fuse_head
+    for _ in range(5):
+        new.train_step()
+        old.train_step()
+    torch.cuda.synchronize()
+    assert _rel(new.flat_params, old.flat_params) < 1e-6
+    assert _rel(new.flat_momentum, old.flat_momentum) < 1e-5
+    assert abs(new.loss() - old.loss()) < 1e-5 * max(1.0, abs(old.loss()))
+    assert float(new.stats[1]) == float(old.stats[1])

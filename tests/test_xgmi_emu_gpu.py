@@ -43,9 +43,13 @@ def test_mean_allreduce(world, n):
         emu.close()
 
 
-@pytest.mark.parametrize("world,nblk,chunked", [(2, 128, False), (4, 128, False), (8, 128, False),
-                                                (2, 256, False), (2, 256, True), (8, 128, True)])
-def test_fused_sgd_with_slab(world, nblk, chunked):
+@pytest.mark.parametrize("world,nblk,chunked,prepush", [
+    (2, 128, False, False), (4, 128, False, False), (8, 128, False, False), (2, 256, False, False),
+    (2, 256, True, False), (8, 128, True, False),
+    # round 4: fc1_bwd pushes dW_fc1 itself (emulated by prepush), the exchange skips that range;
+    # W = 8 x 256 is the production geometry (emulated with one-wave workgroups)
+    (2, 256, True, True), (8, 128, True, True), (8, 256, True, True), (8, 256, True, False)])
+def test_fused_sgd_with_slab(world, nblk, chunked, prepush):
     from pytorch_operator_amd.models.mnist import flat_layout
     dev = torch.device("cuda", 0)
     L = flat_layout().total
@@ -53,6 +57,9 @@ def test_fused_sgd_with_slab(world, nblk, chunked):
     B, lr, mom = 64, 0.01, 0.5
     g = torch.Generator(device="cpu").manual_seed(100 + world)
     emu = _emu(world, L, nblk)  # nblk 256: the one-GPU-per-rank default (parallel/xgmi.py)
+    w1o = flat_layout().offsets["fc1.weight"]
+    if world * nblk > 1024:
+        assert emu.threads == 64  # the production grid fits one GPU only with one-wave workgroups
     try:
         p0 = torch.randn(L, generator=g).to(dev)
         ps = [p0.clone() for _ in range(world)]
@@ -65,7 +72,9 @@ def test_fused_sgd_with_slab(world, nblk, chunked):
             lo = flat_layout().offsets["conv2.weight"]
             big = (B // 4, lo, lo + 25000) if chunked else None
             emu.configure(1, grads, ps, ms, slab=slabs, slab_rows=B, conv_n=ce, lr=lr, momentum=mom,
-                          first_step=step == 0, slab_big=big)
+                          first_step=step == 0, slab_big=big, skip=(w1o, w1o + 400000) if prepush else None)
+            if prepush:
+                emu.prepush()
             emu.launch()
             torch.cuda.synchronize()
             mean = torch.zeros(L, device=dev)
@@ -124,3 +133,42 @@ def test_exchange_latency_floor(world, record_property):
         assert us < 1000
     finally:
         emu.close()
+
+
+@pytest.mark.parametrize("world,nblk", [(2, 256), (8, 128), (8, 256)])
+def test_producer_push_is_bit_identical(world, nblk):
+    """fc1_bwd's own dW_fc1 push (emulated: prepush, the exchange skipping that range) lands
+    the same bytes in the same receive slots as the exchange's own push: parameters and
+    momentum bit-identical to the no-push exchange over several steps."""
+    from pytorch_operator_amd.models.mnist import flat_layout
+    dev = torch.device("cuda", 0)
+    lay = flat_layout()
+    L, ce, B = lay.total, lay.conv_end, 64
+    w1o, lo = lay.offsets["fc1.weight"], lay.offsets["conv2.weight"]
+
+    def run(prepush):
+        g = torch.Generator(device="cpu").manual_seed(500 + world)
+        emu = _emu(world, L, nblk)
+        try:
+            p0 = torch.randn(L, generator=g).to(dev)
+            ps = [p0.clone() for _ in range(world)]
+            ms = [torch.zeros(L, device=dev) for _ in range(world)]
+            for step in range(3):
+                grads = [torch.randn(L, generator=g).to(dev) for _ in range(world)]
+                slabs = [torch.randn(B, ce, generator=g).to(dev) for _ in range(world)]
+                emu.configure(1, grads, ps, ms, slab=slabs, slab_rows=B, conv_n=ce, lr=0.01, momentum=0.5,
+                              first_step=step == 0, slab_big=(B // 4, lo, lo + 25000),
+                              skip=(w1o, w1o + 400000) if prepush else None)
+                if prepush:
+                    emu.prepush()
+                emu.launch()
+            torch.cuda.synchronize()
+            assert emu.error() == 0
+            return ps, ms
+        finally:
+            emu.close()
+    pa, ma = run(False)
+    pb, mb = run(True)
+    for r in range(world):
+        assert torch.equal(pa[r], pb[r]), r
+        assert torch.equal(ma[r], mb[r]), r

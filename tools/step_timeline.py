@@ -30,12 +30,12 @@ from pytorch_operator_amd.ops import mnist as K  # noqa: E402
 from pytorch_operator_amd.parallel.graphed_step import NativeGraph  # noqa: E402
 
 SLOT_U64 = 1024 * 16  # mnist_kernels.hip kDbgSlotU64
-NAMES = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]
+NAMES = ["conv12_fwd", "fc1_head", "fc1_bwd", "conv_bwd4", "tail"]
+NAMES_UNFUSED = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]  # PTO_MNIST_FUSE_HEAD=0
 # block ranges of the launches that run several jobs (B = 64): name -> [(first, end, job)]
-GROUPS = {"fc1_bwd": [(0, 200, "dW_fc1"), (200, 400, "dz2"), (400, 404, "fc2+stats"), (404, 420, "stage")],
+# (fc1_bwd: the dz2 job takes the first ids, mnist_kernels.hip fc1_bwd_kernel's block layout)
+GROUPS = {"fc1_bwd": [(0, 200, "dz2"), (200, 400, "dW_fc1"), (400, 404, "fc2+stats"), (404, 420, "stage")],
           "tail": [(0, 201, "conv reduce+sgd"), (201, 598, "fc sgd")]}
-if os.environ.get("PTO_TIMELINE_FB"):  # library built with PTO_FB & 1: the dz2 job takes ids 0..199
-    GROUPS["fc1_bwd"] = [(0, 200, "dz2"), (200, 400, "dW_fc1"), (400, 404, "fc2+stats"), (404, 420, "stage")]
 
 
 def analyse(dbg: torch.Tensor, nslots: int):
@@ -92,11 +92,12 @@ def main(argv=None):
     # per-kernel medians over the samples
     rows = []
     per = nk // 2
+    names = NAMES if per == len(NAMES) else NAMES_UNFUSED
     for k in range(nk):
         vals = {key: sorted(s[k][key] - s[0]["start"] for s in samples) for key in ("start", "end", "p50end")}
         med = {key: v[len(v) // 2] / 100.0 for key, v in vals.items()}
         gaps = sorted((s[k]["start"] - s[k - 1]["end"]) / 100.0 for s in samples) if k else [float("nan")]
-        rows.append({"kernel": NAMES[k % per] if per == len(NAMES) else f"k{k}", "step": k // per,
+        rows.append({"kernel": names[k % per] if per == len(names) else f"k{k}", "step": k // per,
                      "blocks": samples[0][k]["blocks"], "start_us": round(med["start"], 2),
                      "span_us": round(med["end"] - med["start"], 2),
                      "p50_block_end_us": round(med["p50end"] - med["start"], 2),

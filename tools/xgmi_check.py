@@ -104,12 +104,20 @@ def main(argv=None) -> int:
 
     ta = trainer(XgmiGradSync(xar))
     tb = trainer(FlatGradAllReduce())
+    # the exchange pushing dW_fc1 itself (fc1_bwd's producer push off): must be bit-identical
+    nopush = XgmiGradSync(xar)
+    nopush.push_fc1 = False
+    tc = trainer(nopush)
+    res["push_fc1"] = bool(getattr(ta.grad_sync, "push_fc1", False))
     for _ in range(a.steps):
         ta.train_step()
         tb.train_step()
+        tc.train_step()
     torch.cuda.synchronize(dev)
     res["max_diff_vs_rccl_path"] = float((ta.flat_params - tb.flat_params).abs().max())
     res["eager_match"] = res["max_diff_vs_rccl_path"] < 1e-4
+    res["push_bit_identical"] = bool(torch.equal(ta.flat_params, tc.flat_params)) and bool(
+        torch.equal(ta.flat_momentum, tc.flat_momentum))
 
     runner = GraphedStep(ta, mode="graph", steps_per_graph=4)
     runner.run(8)
@@ -135,7 +143,7 @@ def main(argv=None) -> int:
     if a.bench:
         res["exchange_us"] = _bench_exchange(xar, ta, dev)
     res["kernel_error"] = xar.error()
-    ok = res["self_test"] and res["eager_match"] and res["graph_in_sync"] and res["finite"] \
+    ok = res["self_test"] and res["eager_match"] and res["push_bit_identical"] and res["graph_in_sync"] and res["finite"] \
         and res["kernel_error"] == 0 and res["handover_rccl_in_sync"] and res["handover_xgmi_in_sync"]
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)

@@ -30,8 +30,11 @@ def main() -> int:
     nblks = [int(b) for b in os.environ.get("XAR_NBLK", "128").split(",")]
     fences = [int(f) for f in os.environ.get("XAR_FENCE", "-1").split(",")]
     slab_modes = os.environ.get("XAR_SLAB", "chunk").split(",")
+    # XAR_PUSH=1: fc1_bwd pushes dW_fc1 itself (round 4; emulated by a prepush launch, timed apart)
+    pushes = [int(x) for x in os.environ.get("XAR_PUSH", "0,1").split(",")]
+    w1o = flat_layout().offsets["fc1.weight"]
     lo = flat_layout().offsets["conv2.weight"]
-    for kind, fence, sm in [(k, f, m) for k in kinds for f in fences for m in slab_modes]:
+    for kind, fence, sm, push in [(k, f, m, q) for k in kinds for f in fences for m in slab_modes for q in pushes]:
         for world in worlds:
             for nblk in nblks:
                 emu = XgmiEmulation(world, L, nblk=nblk, alloc_kind=kind, fence=fence)
@@ -40,31 +43,45 @@ def main() -> int:
                 grads = [torch.randn(L, device=dev) for _ in range(world)]
                 slabs = [torch.randn(B, ce, device=dev) for _ in range(world)]
                 cfg = dict(slab=slabs, slab_rows=B, conv_n=ce, lr=0.0, momentum=0.5,
-                           slab_big=((B + 3) // 4, lo, lo + 25000) if sm == "chunk" else None)
+                           slab_big=((B + 3) // 4, lo, lo + 25000) if sm == "chunk" else None,
+                           skip=(w1o, w1o + 400000) if push else None)
                 emu.configure(1, grads, ps, ms, **cfg)
+                if push:
+                    emu.prepush()
                 emu.launch()
                 torch.cuda.synchronize()
-                graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    for _ in range(50):
-                        emu.launch()
-                best = float("inf")
-                for _ in range(5):
-                    torch.cuda.synchronize()
-                    t0 = time.perf_counter()
-                    graph.replay()
-                    torch.cuda.synchronize()
-                    best = min(best, time.perf_counter() - t0)
+
+                def timed(fn):
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        for _ in range(50):
+                            fn()
+                    best = float("inf")
+                    for _ in range(5):
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        graph.replay()
+                        torch.cuda.synchronize()
+                        best = min(best, time.perf_counter() - t0)
+                    return best
+                # the exchange alone (with push: after a prepush, which is what fc1_bwd did)
+                best = timed((lambda: (emu.prepush(), emu.launch())) if push else emu.launch)
+                pre = timed(emu.prepush) if push else 0.0
+                best -= pre
                 st = emu.enable_stamps()
                 emu.configure(1, grads, ps, ms, **cfg)
                 for _ in range(3):
+                    if push:
+                        emu.prepush()
                     emu.launch()
                 torch.cuda.synchronize()
                 s = st.view(world, nblk, 4).double().cpu() / 100.0  # us (100 MHz)
                 t0 = s[..., 0].min()
                 ph = s[..., 1:] - s[..., :-1]
-                res = {"alloc_kind": kind, "fence": fence, "slab": sm, "world": world, "nblk": nblk,
+                res = {"alloc_kind": kind, "fence": fence, "slab": sm, "push_fc1": push, "world": world,
+                       "nblk": nblk, "threads": emu.threads,
                        "us_per_launch": round(best / 50 * 1e6, 2),
+                       "prepush_us_per_launch": round(pre / 50 * 1e6, 2),
                        "span_us": round(float(s[..., 3].max() - t0), 2),
                        "start_skew_us": round(float(s[..., 0].max() - t0), 2),
                        "phase_mean_us": [round(float(x), 2) for x in ph.mean((0, 1))],
