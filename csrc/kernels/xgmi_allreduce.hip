@@ -146,11 +146,15 @@ __device__ __forceinline__ void store_sys(unsigned* p, unsigned v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Error word bits: which bounded wait timed out first (host reads it with pto_xar_error)
+constexpr int kErrPushWait = 1;    // phase 2: the senders' flag1 (their pushes to this owner)
+constexpr int kErrGatherWait = 2;  // phase 3: an owner's flag2 (its updated shard)
+
 // Poll one local flag until >= target; false (error flagged) on timeout.
-__device__ bool wait_flag(const unsigned* p, unsigned target, long long deadline, int* err) {
+__device__ bool wait_flag(const unsigned* p, unsigned target, long long deadline, int* err, int code) {
   while (load_sys(p) < target) {
     if ((long long)wall_clock64() > deadline) {
-      atomicOr(err, 1);
+      atomicOr(err, code);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -202,13 +206,13 @@ __device__ __forceinline__ void deposit(const XarArgs& a, long v, f4 g, bool deg
 // All of a thread's flags are loaded back to back (one local round trip per poll), the
 // block leaves together.  False (error flagged) on timeout.
 template <int NT>
-__device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long deadline, int* err) {
+__device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long deadline, int* err, int code) {
   for (;;) {
     int pending = 0;
     for (int i = threadIdx.x; i < nf; i += NT) pending |= load_sys(f + i) < target;
     if (!__syncthreads_or(pending)) return true;
     if ((long long)wall_clock64() > deadline) {
-      if (threadIdx.x == 0) atomicOr(err, 1);
+      if (threadIdx.x == 0) atomicOr(err, code);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -336,7 +340,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     };
     load_pb(tid);  // in flight while waiting
     // every sender block's flag (or timed out: go on, the error is set); block-uniform
-    wait_flags<NT>(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err);
+    wait_flags<NT>(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err, kErrPushWait);
     acquire_fence(a);
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
       // every sender's contribution in flight at once (clamped addresses, no predicated
@@ -392,7 +396,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   // ---- phase 3: collect chunk b of every other shard
   {
     int ok = 1;
-    if (tid < a.world && tid != a.rank) ok = wait_flag(flag2(mine, a.nblk, tid, b), s, deadline, a.err);
+    if (tid < a.world && tid != a.rank) ok = wait_flag(flag2(mine, a.nblk, tid, b), s, deadline, a.err, kErrGatherWait);
     (void)__syncthreads_and(ok);
     acquire_fence(a);
     f4* dst = reinterpret_cast<f4*>(a.mode == 0 ? a.out : a.p);

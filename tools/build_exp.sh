@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build -D experiment variants of libpto_hip.so for same-box A/B (tools/gpu_ab_libs.sh loads
+# Build -D experiment variants of libpto_hip.so for same-box A/B (tools/gpu/ab_libs.sh loads
 # every pytorch_operator_amd/_lib/exp/*.so through PTO_HIP_LIB).
 #   tools/build_exp.sh name1 "-DFOO=0" name2 "-DFOO=0 -DBAR=1" ...
 set -e

@@ -1,10 +1,12 @@
 #!/bin/bash
-# Round-end readiness on one MI355X: every GPU test, smoke(), the driver's bench line, and a
-# rocprofv3 kernel-stats profile of the default bench path (stream launch).
+# Round-end readiness on one MI355X: the GPU tests (PYTEST_SEL, default all of tests/), smoke(),
+# the driver's bench line, and (unless SKIP_PROF) a rocprofv3 kernel-stats table of the bench.
+#   bash tools/gpu/check.sh [OUT_DIR]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/final; mkdir -p $O
+O=${1:-gpurun_out/check}; mkdir -p $O
+export PYTHONUNBUFFERED=1
 ( while sleep 30; do echo "hb $(date +%T)"; done ) & HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 900 python -u -m pytest ${PYTEST_SEL:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $O/pytest_gpu.log; exit 1; }
@@ -14,6 +16,4 @@ tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_20_5.log 2>&1 || { echo "bench failed"; tail -30 $O/bench_20_5.log; exit 1; }
 tail -1 $O/bench_20_5.log
 [ -n "$SKIP_PROF" ] && exit 0
-timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d /tmp/fprof -o run --output-format csv -- python3 bench.py --steps 2000 --warmup 50 --job-latency 0 > $O/prof_bench.log 2>&1 || { echo "prof failed"; tail -10 $O/prof_bench.log; exit 1; }
-f=$(find /tmp/fprof -name "*kernel_stats.csv" | head -1)
-python3 tools/kstats_md.py "$f" --top 12 --steps 2050 > $O/kernel_stats.md && cat $O/kernel_stats.md
+bash tools/gpu/profile.sh $O/prof 2050 python3 bench.py --steps 2000 --warmup 50 --job-latency 0

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Break a short timed region (bench.py --steps 20 --warmup 5) into host launch latency,
 GPU busy time, inter-kernel gaps and the host's synchronize tail, from a rocprofv3
-``--kernel-trace --hip-runtime-trace --output-format csv`` run (tools/gpu_k20_trace.sh).
+``--kernel-trace --hip-runtime-trace --output-format csv`` run (tools/gpu/profile.sh with --hip-runtime-trace added).
 
 The timed region is the last run of hipGraphLaunch calls followed by a synchronize."""
 import csv

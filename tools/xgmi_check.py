@@ -118,6 +118,7 @@ def main(argv=None) -> int:
     res["eager_match"] = res["max_diff_vs_rccl_path"] < 1e-4
     res["push_bit_identical"] = bool(torch.equal(ta.flat_params, tc.flat_params)) and bool(
         torch.equal(ta.flat_momentum, tc.flat_momentum))
+    res["error_after"] = {"eager": xar.error()}
 
     runner = GraphedStep(ta, mode="graph", steps_per_graph=4)
     runner.run(8)
@@ -125,6 +126,7 @@ def main(argv=None) -> int:
     ref = ta.flat_params.clone()
     dist.broadcast(ref, 0)
     res["graph_in_sync"] = bool(torch.equal(ref, ta.flat_params))
+    res["error_after"]["graph"] = xar.error()
     res["finite"] = bool(torch.isfinite(ta.flat_params).all())
     # autotune hand-over in both directions keeps the replicas identical
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
@@ -140,6 +142,7 @@ def main(argv=None) -> int:
         res[f"handover_{force}_in_sync"] = bool(torch.equal(ref, ta.flat_params)) and (
             force == "xgmi" or bool(torch.equal(mref, ta.flat_momentum)))
         res[f"handover_{force}_times"] = times
+        res["error_after"][f"handover_{force}"] = xar.error()
     if a.bench:
         res["exchange_us"] = _bench_exchange(xar, ta, dev)
     res["kernel_error"] = xar.error()
