@@ -1576,6 +1576,52 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   stamp(dbg, 5);
 }
 
+// slab reduction helpers (the tail, and conv_bwd4's fused tail)
+constexpr int SR_COLS = 32;
+constexpr int SR_CH = 8;
+constexpr int SR_SL = 256 / SR_COLS;
+
+__device__ __forceinline__ void add4(float4& a, const float4& v) {
+  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+}
+
+// Rows [slice * per, min(rows, (slice + 1) * per)) of float4 column cc summed in row order,
+// per = ceil(rows / nsl).  Every load is issued before the first add (clamped addresses).
+// ld(row, cc) loads one float4 of the slab (plain, or sc1 for an in-launch hand-off).
+template <typename LD>
+__device__ __forceinline__ float4 slab_col_sum_ld(LD ld, int cc, int rows, int slice, int nsl) {
+  const int per = (rows + nsl - 1) / nsl;
+  const int b0 = slice * per, b1 = min(rows, b0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (per <= 2) {  // chunked conv2.weight rows: 16 rows / 8 slices at B = 64
+    const float4 v0 = ld(min(b0, rows - 1), cc);
+    const float4 v1 = ld(min(b0 + 1, rows - 1), cc);
+    if (b0 < b1) add4(acc, v0);
+    if (b0 + 1 < b1) add4(acc, v1);
+    return acc;
+  }
+  for (int base = b0; base < b1; base += SR_CH) {
+    float4 v[SR_CH];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k) v[k] = ld(min(base + k, rows - 1), cc);
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k)
+      if (base + k < b1) add4(acc, v[k]);
+  }
+  return acc;
+}
+__device__ __forceinline__ float4 slab_col_sum(const float4* __restrict__ P4, long s4, int cc, int rows,
+                                               int slice, int nsl) {
+  return slab_col_sum_ld([=](int r, int c) { return P4[(size_t)r * s4 + c]; }, cc, rows, slice, nsl);
+}
+
+struct SlabRows {
+  int rows;      // rows of every column outside [big_lo4, big_hi4)
+  int rows_big;  // rows of the columns inside
+  int big_lo4, big_hi4;
+  __device__ __forceinline__ int of(int c4) const { return (c4 >= big_lo4 && c4 < big_hi4) ? rows_big : rows; }
+};
+
 // ---------------------------------------------------------------------------
 // F4: conv backward with dW_conv2 summed over 4-sample chunks (the training path).
 //   grid = (4 input-channel groups, 4 * ceil(B / 4)); block (cig, b): chunk q = b / 4,
@@ -1677,10 +1723,36 @@ __device__ __forceinline__ void bwd4_phase2(const float* dzc_s, const float* w_s
 }
 static_assert(F_TPW == 2, "bwd4_phase2 holds two 2a tiles per wave");
 
+// Fused tail (TAIL = true; the step's last launch then is this one): besides its own work every
+// block updates its 1/256 share of the fc parameters (SGD on the fc grads fc1_bwd finished),
+// stores its slab rows write-through (sc1), and after every store has landed adds 1 to an
+// arrival counter (agent-scope atomic; MI355X_MICROARCH.md's cross-CU hand-off, row 1).  The last
+// `reducers` blocks to arrive wait (bounded) for the rest, then each reduces its share of the
+// slab columns with sc1 loads in slab_reduce_sgd_kernel's exact summation order and applies SGD
+// to those conv parameters; the very last arrival advances the step cursor.  Bit-identical to
+// conv_bwd4 + slab_reduce_sgd, one dependent launch boundary less.
+struct Bwd4Tail {
+  SlabRows sr;
+  int n;                 // conv-segment floats (slab columns reduced)
+  unsigned slab_bytes;   // B x stride x 4 (< 2^31: 32-bit buffer offsets)
+  float *gout, *p, *buf;  // reduced conv grads, conv parameters, momentum
+  SgdHyper hy;
+  int* step_counter;
+  float* p2;              // fc parameters / grads / momentum
+  const float* g2;
+  float* buf2;
+  int n2;
+  unsigned* cnt;          // arrival counter (monotonic: a launch of T blocks adds T)
+  int* err;               // set when a reducer's bounded wait timed out
+  int reducers;
+  long long timeout_ticks;
+};
+
+template <bool TAIL>
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
-    int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, u64* dbg) {
+    int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, Bwd4Tail t, u64* dbg) {
   extern __shared__ float lds[];
   float* dzc_s = lds + G_OFF_DZ;
   float* w_s = lds + G_OFF_W;
@@ -1705,6 +1777,16 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   const int jbase = 32 * r - cig;
   const int c0 = max(jbase, 0) / 25;  // first of the <= 2 input channels those columns touch
   stamp(dbg, 0);
+  // slab stores: plain, or write-through (sc1) when the fused tail reads them in this launch
+  const __amdgpu_buffer_rsrc_t S = buf_rsrc(slab, TAIL ? t.slab_bytes : 0u);
+  auto st1 = [&](float* q, float v) {
+    if constexpr (TAIL) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), S, (int)((q - slab) * 4), 0, 16);
+    else *q = v;
+  };
+  auto st4 = [&](float* q, float4 v) {
+    if constexpr (TAIL) store_sc1(S, (unsigned)((q - slab) * 4), v);
+    else *reinterpret_cast<float4*>(q) = v;
+  };
 
   // ---- phase 1: stage.  Group 1: the own sample's dz2 and the W2 slice; group 2: the chunk's
   // other three samples, the 2b im2col source, the own a1 / idx1 / xn (measured: keeping group
@@ -1789,6 +1871,20 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   stage_g2();
   __syncthreads();
   stamp(dbg, 1);
+  // fused tail: this block's share of the fc SGD, loads in flight under phase 2
+  float4 fp = make_float4(0.f, 0.f, 0.f, 0.f), fg = fp, fm = fp;
+  int fv = -1;
+  if constexpr (TAIL) {
+    const int bl = blockIdx.y * gridDim.x + blockIdx.x, nbl = gridDim.x * gridDim.y;
+    const int n24 = t.n2 >> 2, per = (n24 + nbl - 1) / nbl;  // <= F_NT (host-checked)
+    const int v = bl * per + tid;
+    if (tid < per && v < n24) {
+      fv = v;
+      fp = reinterpret_cast<const float4*>(t.p2)[v];
+      fg = reinterpret_cast<const float4*>(t.g2)[v];
+      fm = reinterpret_cast<const float4*>(t.buf2)[v];
+    }
+  }
 
   // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
   // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
@@ -1831,20 +1927,27 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       float* rp = rowq + (ct * 16 + i) * 500;
       const int j0 = jbase + jt * 16 + 4 * g;
       if (j0 >= 0 && j0 + 3 < 125) {
-        const float4 v4 = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
-        *reinterpret_cast<float4*>(rp + j0) = v4;
+        st4(rp + j0, make_float4(gacc[0], gacc[1], gacc[2], gacc[3]));
       } else {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
+          if (j0 + rr >= 0 && j0 + rr < 125) st1(rp + j0 + rr, gacc[rr]);
       }
     } else if (wv == 12) {
       const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
       const int j = jbase + (lane & 31);
-      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
+      if (j >= 0 && j < 125) st1(rowq + (48 + (lane >> 5)) * 500 + j, v);
     }
   }
-  if (!own) return;  // block-uniform: padding blocks of the last chunk are done
+  if constexpr (TAIL) {
+    if (fv >= 0) {  // fc SGD: nothing in this launch reads the fc parameters
+      sgd4(fp, fm, fg, t.hy);
+      reinterpret_cast<float4*>(t.p2)[fv] = fp;
+      reinterpret_cast<float4*>(t.buf2)[fv] = fm;
+    }
+  }
+  if (!TAIL && !own) return;  // block-uniform: padding blocks of the last chunk are done
+  if (own) {
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
   if (tid < 720) {
@@ -1910,11 +2013,66 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     float w1sum = 0.f;
 #pragma unroll
     for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
-    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
-    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
+    if (tid < 125) st1(rowb + o_gw1 + cig * 125 + tid, w1sum);  // tid = c * 25 + kh * 5 + kw
+    else st1(rowb + o_gb1 + cig * 5 + (tid - 125), w1sum);
   }
-  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
+  if (cig == 0 && tid < 50) st1(rowb + o_gb2 + tid, b2sum);
+  }  // own
   stamp(dbg, 5);
+  if constexpr (TAIL) {
+    // ---- arrival: every wave's slab stores have landed, then one add per block
+    __shared__ unsigned s_arr;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_arr = __hip_atomic_fetch_add(t.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned total = gridDim.x * gridDim.y;
+    const unsigned k = s_arr % total, base = s_arr - k;
+    if (k == total - 1 && t.step_counter != nullptr && tid == 0) atomicAdd(t.step_counter, 1);
+    if ((int)k < (int)total - t.reducers) return;  // block-uniform
+    const int r = (int)k - ((int)total - t.reducers);
+    // ---- reducer r: wait (bounded) for every block of this launch, then reduce its columns
+    if (tid == 0) {
+      const long long deadline = (long long)wall_clock64() + t.timeout_ticks;
+      while ((int)(__hip_atomic_load(t.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base) < (int)total) {
+        if ((long long)wall_clock64() > deadline) {
+          atomicOr(t.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    stamp(dbg, 6);
+    constexpr int RC = F_NT / SR_SL;  // columns per pass (128), SR_SL row slices each
+    float4* rd = reinterpret_cast<float4*>(lds);  // [SR_SL][RC]: phase buffers are dead
+    const int n4 = t.n >> 2, per = (n4 + t.reducers - 1) / t.reducers;
+    const int c_lo = r * per, c_hi = min(n4, c_lo + per);
+    const long s4 = stride >> 2;
+    auto ld = [&](int row, int c) { return load_sc1(S, (unsigned)(((long)row * s4 + c) * 16)); };
+    const int slice = tid / RC, ci = tid - slice * RC;
+    for (int cb = c_lo; cb < c_hi; cb += RC) {
+      const int col = cb + ci, cc = min(col, n4 - 1);
+      float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bb = pp;
+      if (tid < RC) {
+        pp = reinterpret_cast<const float4*>(t.p)[cc];
+        bb = reinterpret_cast<const float4*>(t.buf)[cc];
+      }
+      rd[slice * RC + ci] = slab_col_sum_ld(ld, cc, t.sr.of(cc), slice, SR_SL);
+      __syncthreads();
+      if (tid < RC && col < c_hi) {
+        float4 acc = rd[tid];
+#pragma unroll
+        for (int q = 1; q < SR_SL; ++q) add4(acc, rd[q * RC + tid]);
+        if (t.gout != nullptr) reinterpret_cast<float4*>(t.gout)[col] = acc;
+        sgd4(pp, bb, acc, t.hy);
+        reinterpret_cast<float4*>(t.p)[col] = pp;
+        reinterpret_cast<float4*>(t.buf)[col] = bb;
+      }
+      __syncthreads();
+    }
+    stamp(dbg, 7);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1927,46 +2085,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
 // Slab reduction geometry: SR_COLS float4 columns per workgroup x SR_SL row slices, SR_CH
 // loads in flight per thread.  32 columns (200 reduction workgroups at B = 64, 32 KB each)
 // beat 64 (100 x 64 KB): 0.25 us off the load phase.
-constexpr int SR_COLS = 32;
-constexpr int SR_CH = 8;
-constexpr int SR_SL = 256 / SR_COLS;
-
-__device__ __forceinline__ void add4(float4& a, const float4& v) {
-  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-}
-
-// Rows [slice * per, min(rows, (slice + 1) * per)) of float4 column cc summed in row order,
-// per = ceil(rows / nsl).  Every load is issued before the first add (clamped addresses).
-__device__ __forceinline__ float4 slab_col_sum(const float4* __restrict__ P4, long s4, int cc, int rows,
-                                               int slice, int nsl) {
-  const int per = (rows + nsl - 1) / nsl;
-  const int b0 = slice * per, b1 = min(rows, b0 + per);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (per <= 2) {  // chunked conv2.weight rows: 16 rows / 8 slices at B = 64
-    const float4 v0 = P4[(size_t)min(b0, rows - 1) * s4 + cc];
-    const float4 v1 = P4[(size_t)min(b0 + 1, rows - 1) * s4 + cc];
-    if (b0 < b1) add4(acc, v0);
-    if (b0 + 1 < b1) add4(acc, v1);
-    return acc;
-  }
-  for (int base = b0; base < b1; base += SR_CH) {
-    float4 v[SR_CH];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, rows - 1) * s4 + cc];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k)
-      if (base + k < b1) add4(acc, v[k]);
-  }
-  return acc;
-}
-
-struct SlabRows {
-  int rows;      // rows of every column outside [big_lo4, big_hi4)
-  int rows_big;  // rows of the columns inside
-  int big_lo4, big_hi4;
-  __device__ __forceinline__ int of(int c4) const { return (c4 >= big_lo4 && c4 < big_hi4) ? rows_big : rows; }
-};
-
 __global__ __launch_bounds__(256) void slab_reduce_kernel(
     const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ out, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
@@ -2391,11 +2509,65 @@ int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, cons
       o_gw1 + 500 > stride || o_gb1 + 20 > stride)
     return -1;
   static std::atomic<unsigned> attr_set{0};
-  const int rc = set_max_lds(conv_bwd4_kernel, G_LDS * (int)sizeof(float), attr_set);
+  const int rc = set_max_lds(conv_bwd4_kernel<false>, G_LDS * (int)sizeof(float), attr_set);
   if (rc != 0) return rc;
   const int nb = 4 * ((B + 3) / 4);
-  hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
-                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
+  hipLaunchKernelGGL(conv_bwd4_kernel<false>, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float),
+                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B,
+                     Bwd4Tail{}, dbg_next());
+  return (int)hipGetLastError();
+}
+
+// conv_bwd4 + the step's tail in one launch (conv_bwd4_kernel<true>): as pto_mnist_conv_bwd4,
+// then the conv slab reduction (n floats, rows_big chunk rows for [big_lo, big_hi)) into gout +
+// SGD of p/buf, SGD of the fc range p2/g2/buf2 (n2 floats), cursor advance -- what
+// pto_slab_reduce_sgd does after it.  cnt: one uint32 (any start value, never reset); err: int32,
+// set when a reducer timed out.
+int pto_mnist_conv_bwd4_tail(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
+                             const float* xn, float* slab, int stride, int o_gw2, int o_gb2, int o_gw1,
+                             int o_gb1, int B, int n, float* gout, float* p, float* buf, float lr,
+                             float momentum, float dampening, float wd, float grad_scale, int nesterov,
+                             int first_step, int* step_counter, float* p2, const float* g2, float* buf2,
+                             int n2, int rows_big, int big_lo, int big_hi, unsigned* cnt, int* err,
+                             int reducers, double timeout_s, void* stream) {
+  PTO_CHECK_B(B);
+  if (4 * ((B + 3) / 4) > 65535) return -1;
+  if ((stride & 3) || (o_gw2 & 3) || (((uintptr_t)slab) & 15) || (((uintptr_t)dz2) & 15)) return -2;
+  if (o_gw2 < 0 || o_gb2 < 0 || o_gw1 < 0 || o_gb1 < 0 || o_gw2 + 25000 > stride || o_gb2 + 50 > stride ||
+      o_gw1 + 500 > stride || o_gb1 + 20 > stride)
+    return -1;
+  if (n <= 0 || (n & 3) || stride < n || n2 < 0 || (n2 & 3) || cnt == nullptr || err == nullptr) return -1;
+  if (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)) return -1;
+  if ((((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) | ((uintptr_t)p2) | ((uintptr_t)g2) |
+       ((uintptr_t)buf2)) & 15)
+    return -2;
+  const int nb = 4 * ((B + 3) / 4), total = 4 * nb;
+  if ((double)B * stride * 4 >= 2147483648.0) return -1;  // 32-bit buffer offsets
+  if ((n2 / 4 + total - 1) / total > F_NT) return -1;    // one fc float4 per thread
+  if (reducers < 1 || reducers > total) return -1;
+  Bwd4Tail t{};
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, t.sr)) return -1;
+  t.n = n;
+  t.slab_bytes = (unsigned)((long)B * stride * 4);
+  t.gout = gout;
+  t.p = p;
+  t.buf = buf;
+  t.hy = SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  t.step_counter = step_counter;
+  t.p2 = p2;
+  t.g2 = g2;
+  t.buf2 = buf2;
+  t.n2 = n2;
+  t.cnt = cnt;
+  t.err = err;
+  t.reducers = reducers;
+  t.timeout_ticks = (long long)(timeout_s * 1e8);  // wall_clock64: 100 MHz
+  static std::atomic<unsigned> attr_set{0};
+  const int rc = set_max_lds(conv_bwd4_kernel<true>, G_LDS * (int)sizeof(float), attr_set);
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(conv_bwd4_kernel<true>, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float),
+                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B,
+                     t, dbg_next());
   return (int)hipGetLastError();
 }
 

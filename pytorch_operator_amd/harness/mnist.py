@@ -133,8 +133,12 @@ def _datasets(args, rank: int, world: int, device):
     source = "mnist-idx"
     if train is None or test is None:
         source = "synthetic"
-        tr = make_synthetic_mnist(args.dataset_size, seed=args.seed)
-        te = make_synthetic_mnist(args.test_size, seed=args.seed + 7919)
+        # on a GPU the set is drawn on the device (ms, not the ~1-2 s of single-threaded CPU
+        # warps: the biggest piece of a pod's start-up, profiles/r4_startup.md)
+        gpu = device is not None and torch.device(device).type == "cuda"
+        tr = make_synthetic_mnist(args.dataset_size, seed=args.seed, device=device if gpu else None, on_device=gpu)
+        te = make_synthetic_mnist(args.test_size, seed=args.seed + 7919, device=device if gpu else None,
+                                  on_device=gpu)
         train, test = (tr.images, tr.labels), (te.images, te.labels)
     xtr, ytr = train
     if args.shard and world > 1:
@@ -151,14 +155,18 @@ def _epoch_perm(n: int, seed: int, epoch: int, rank: int, shard: bool, device):
 
 
 def _proc_start_ns() -> Optional[int]:
-    """Wall-clock start of this process (Linux: /proc/self/stat starttime + boot time)."""
+    """Wall-clock start of this process: now minus its age, the age from /proc/self/stat's
+    starttime against /proc/uptime (both since boot, 10 ms ticks).  /proc/stat's integer
+    ``btime`` is not used: its truncation put the start up to 1 s late."""
     try:
+        now = time.time_ns()
         with open("/proc/self/stat") as f:
             ticks = int(f.read().rsplit(")", 1)[1].split()[19])
-        with open("/proc/stat") as f:
-            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
-        return int((btime + ticks / os.sysconf("SC_CLK_TCK")) * 1e9)
-    except (OSError, ValueError, StopIteration, IndexError):
+        with open("/proc/uptime") as f:
+            up = float(f.read().split()[0])
+        age = up - ticks / os.sysconf("SC_CLK_TCK")
+        return int(now - max(age, 0.0) * 1e9)
+    except (OSError, ValueError, IndexError):
         return None
 
 

@@ -152,6 +152,10 @@ class FusedMnistTrainer:
         #              block of each 16-sample tile runs its head; False: fc1_fwd<2> + head)
         self.fuse_conv12 = True
         self.fuse_head = os.environ.get("PTO_MNIST_FUSE_HEAD", "1") != "0"
+        #   fuse_tail: conv_bwd4 + the tail (slab reduction + SGD of every parameter + cursor)
+        #              as one launch: the last `tail_reducers` workgroups reduce the slab
+        self.fuse_tail = os.environ.get("PTO_MNIST_FUSE_TAIL", "0") != "0"
+        self.tail_reducers = int(os.environ.get("PTO_MNIST_TAIL_REDUCERS", "16"))
         self.conv_chunk = 4
         self.stage_batches = True
 
@@ -184,6 +188,8 @@ class FusedMnistTrainer:
         self.fc1_ks = self.K.fc1_split()
         self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
         self.fc1_cnt = torch.zeros((B + 15) // 16, device=dev, dtype=torch.int32)  # fc1_head arrivals
+        self.tail_cnt = torch.zeros(1, device=dev, dtype=torch.int32)  # conv_bwd4_tail arrivals
+        self.tail_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stage = K_stage(self.source, B, dev)
         # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
         # (conv_bwd4) per-4-sample-chunk rows for conv2.weight
@@ -365,6 +371,19 @@ class FusedMnistTrainer:
         self.forward(source, B)
         self._head(B)
         self._fc1_bwd(B, stage_adv=1 if advance_cursor else 0)
+        if self.fuse_tail and self.conv_chunk == 4:
+            p = self._pv
+            K.conv_bwd4_tail(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
+                             self.conv_slab, self.layout.offsets, B, grads=self.conv_bucket(),
+                             params=self._fp[:ce], buf=self._fm[:ce], lr=self.lr, momentum=self.momentum,
+                             dampening=self.dampening, weight_decay=self.weight_decay,
+                             nesterov=self.nesterov, first_step=self._first_step,
+                             step_counter=self.cursor if advance_cursor else None,
+                             extra=(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
+                             counter=self.tail_cnt, err=self.tail_err, reducers=self.tail_reducers)
+            self._last_big = K.conv_bwd4_rows(B, self.layout.offsets)
+            self._first_step = False
+            return
         self._conv_bwd(B)
         K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
                            self._fm[:ce], lr=self.lr, momentum=self.momentum,

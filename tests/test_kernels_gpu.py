@@ -419,3 +419,47 @@ def test_fused_head_step_matches_unfused_step(lib, B, monkeypatch):
     assert _rel(new.flat_momentum, old.flat_momentum) < 1e-5
     assert abs(new.loss() - old.loss()) < 1e-5 * max(1.0, abs(old.loss()))
     assert float(new.stats[1]) == float(old.stats[1])
+
+
+def test_on_device_synthetic_dataset_is_deterministic_and_mnist_like(lib):
+    """The worker's start-up draws its synthetic set on the GPU: same seed -> same bytes, and
+    the same shape / value statistics as the CPU recipe (a different random stream)."""
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    dev = torch.device("cuda")
+    a = make_synthetic_mnist(20000, seed=4, device=dev, on_device=True)
+    b = make_synthetic_mnist(20000, seed=4, device=dev, on_device=True)
+    c = make_synthetic_mnist(20000, seed=4)
+    assert a.images.device.type == "cuda" and a.images.dtype == torch.uint8 and a.images.shape == (20000, 784)
+    assert torch.equal(a.images, b.images) and torch.equal(a.labels, b.labels)
+    assert not torch.equal(a.images.cpu(), c.images)
+    ma, mc = float(a.images.float().mean()), float(c.images.float().mean())
+    assert abs(ma - mc) < 0.05 * mc, (ma, mc)
+    counts = torch.bincount(a.labels.long().cpu(), minlength=10)
+    assert int(counts.min()) > 1700 and sorted(a.perm.cpu().tolist()) == list(range(20000))
+
+
+@pytest.mark.parametrize("B", [64, 37, 13])
+def test_fused_tail_step_is_bit_identical(lib, B, monkeypatch):
+    """conv_bwd4 + tail in one launch (the last workgroups reduce the slab after an in-launch
+    hand-off) trains bit-identically to conv_bwd4 + slab_reduce_sgd: same summation order;
+    the cursor advances once per step and no reducer wait times out."""
+    n = 8 * B
+    x, y = _data(n, seed=500 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(torch.int32)
+    monkeypatch.setenv("PTO_MNIST_FUSE_TAIL", "1")
+    new = _stage_trainer(x, y, perm, B=B)
+    monkeypatch.setenv("PTO_MNIST_FUSE_TAIL", "0")
+    old = _stage_trainer(x, y, perm, B=B)
+    assert new.fuse_tail and not old.fuse_tail
+    for i in range(6):
+        adv = i != 3
+        new.train_step(advance_cursor=adv)
+        old.train_step(advance_cursor=adv)
+    torch.cuda.synchronize()
+    assert int(new.tail_err.item()) == 0
+    assert int(new.cursor.item()) == int(old.cursor.item()) == 5
+    assert torch.equal(new.flat_params, old.flat_params)
+    assert torch.equal(new.flat_momentum, old.flat_momentum)
+    assert torch.equal(new.flat_grads, old.flat_grads)
+    # the arrival counter advanced by one launch's workgroups per step
+    assert int(new.tail_cnt.item()) == 6 * 4 * 4 * ((B + 3) // 4)

@@ -6,7 +6,8 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4s5; mkdir -p $O
 export PYTHONUNBUFFERED=1
-AB_ENVS="unfused:PTO_MNIST_FUSE_HEAD=0" bash tools/gpu/ab_libs.sh $O 2 || exit 1
+timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "fused_tail or on_device" > $O/pytest_tail.log 2>&1; rc=$?; tail -8 $O/pytest_tail.log; [ $rc -ne 0 ] && exit $rc
+AB_ENVS="unfused:PTO_MNIST_FUSE_HEAD=0 tail:PTO_MNIST_FUSE_TAIL=1 tail32:PTO_MNIST_FUSE_TAIL=1,PTO_MNIST_TAIL_REDUCERS=32" bash tools/gpu/ab_libs.sh $O 2 || exit 1
 port=29521
 for v in "default:" "nopush:PTO_XGMI_PUSH_FC1=0" "unfused:PTO_MNIST_FUSE_HEAD=0"; do
   tag=${v%%:*}; E=${v#*:}
