@@ -783,202 +783,6 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// D2: fc1 forward + head in ONE launch (the training path; replaces fc1_fwd<2> + head<1> and
-// their dependent launch boundary).  The 256 blocks are fc1_fwd_kernel<2>'s: each writes its
-// 16 x 16 pre-activation partial with write-through (sc1) 16-B stores, waits for them, and one
-// lane adds 1 to its sample tile's arrival counter (agent-scope atomic).  The block whose add
-// returns 63 -- the tile's 64th arrival (32 feature tiles x 2 K halves) -- runs the head for
-// the tile's 16 samples, reading the partials with sc1 loads: MI355X_MICROARCH.md's cross-CU
-// hand-off table, row 1 (no fence; every other block just exits).  It resets the counter for
-// the next launch.  The head itself is on MFMA:
-//   logits[16 x 16] = relu(P0 + P1 + b1) . W2^T   K = 500 in 32 chunks of 16, chunk c on wave
-//                     c % 5; inside a chunk lane (i, g) takes k = 16c + 4g + e in MFMA step e
-//                     (the same K permutation on both operands), so every operand is a float4
-//   softmax / NLL / argmax on wave 0, one 16-lane row per 4 samples (lane i = class i)
-//   dh^T[k][s] = W2^T . dl^T per chunk (K = 10 classes padded to 12: 3 MFMAs); lane (i, g) ends
-//                with dh[sample i][16c + 4g + r], the k its h registers hold: ReLU mask + float4
-// Deterministic: the head's result does not depend on which block arrived last.
-// ---------------------------------------------------------------------------
-struct FcHead {
-  const float *x, *w1, *b1, *w2, *b2;
-  const int* lab;
-  float* parts;  // [2][B][500] pre-activation partials (scratch)
-  int* cnt;      // [ceil(B / 16)] arrival counters, 0 between launches
-  float *h_out, *dh, *dlogits, *per_sample;
-  float grad_scale;
-  int B;
-};
-constexpr int FH_NW = 5;                     // waves per block (fc1_fwd_kernel<2>)
-constexpr int FH_ARRIVALS = 32 * 2;          // blocks per sample tile
-constexpr int FH_CPW = (32 + FH_NW - 1) / FH_NW;  // K chunks per wave in the head (7)
-
-__global__ __launch_bounds__(64 * FH_NW) void fc1_head_kernel(FcHead a, u64* dbg) {
-  __shared__ f32x4 red[FH_NW][64];
-  __shared__ float dl_s[16][17];
-  __shared__ int last_s;
-  const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, tid = threadIdx.x;
-  stamp(dbg, 0);
-  const int B = a.B;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const __amdgpu_buffer_rsrc_t P = buf_rsrc(a.parts, (unsigned)(2 * B * 500 * 4));
-  {  // ---- fc1 partial: as fc1_fwd_kernel<2>
-    const int row = mt * 16 + i, col = nt * 16 + i;
-    const bool rv = row < B, cv = col < 500;
-    const int k0 = (kz * FH_NW + wv) * 80 + g * 4;
-    const float4* xa = reinterpret_cast<const float4*>(a.x + (size_t)(rv ? row : B - 1) * 800 + k0);
-    const float4* wb = reinterpret_cast<const float4*>(a.w1 + (size_t)(cv ? col : 499) * 800 + k0);
-    float4 av[5], bv[5];
-#pragma unroll
-    for (int s = 0; s < 5; ++s) { av[s] = xa[4 * s]; bv[s] = wb[4 * s]; }
-    f32x4 c0 = zero4(), c1 = zero4();
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const float* ae = &av[s].x;
-      const float* be = &bv[s].x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = rv ? ae[e] : 0.f;
-        const float y = cv ? be[e] : 0.f;
-        if (e & 1) c1 = mfma16x16x4(x, y, c1);
-        else c0 = mfma16x16x4(x, y, c0);
-      }
-    }
-    red[wv][lane] = c0 + c1;
-    __syncthreads();
-    if (tid < 64) {  // thread = (tile row, 4 consecutive columns): one 16-B sc1 store
-      const int tr = tid >> 2, cg = tid & 3;
-      const int orow = mt * 16 + tr, ocol = nt * 16 + 4 * cg;
-      float sv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float acc = 0.f;
-#pragma unroll
-        for (int q = 0; q < FH_NW; ++q) acc += red[q][(tr >> 2) * 16 + 4 * cg + e][tr & 3];
-        sv[e] = acc;
-      }
-      if (orow < B && ocol < 500)
-        store_sc1(P, (unsigned)((((size_t)kz * B + orow) * 500 + ocol) * 4),
-                  make_float4(sv[0], sv[1], sv[2], sv[3]));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (tid == 0)
-      last_s = __hip_atomic_fetch_add(a.cnt + mt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               FH_ARRIVALS - 1;
-    __syncthreads();
-    stamp(dbg, 1);
-    if (!last_s) return;  // block-uniform
-  }
-  if (tid == 0) __hip_atomic_store(a.cnt + mt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // ---- head for samples mt * 16 + [0, 16): every load first (partials sc1, parameters plain),
-  // all unconditional from clamped addresses; padding is zeroed by multiplying the W2 operands
-  // by a 0/1 mask (every value is finite), so no load sits behind a branch.  Rows >= B compute
-  // row B - 1's values and store nothing.
-  const int srow = mt * 16 + i;
-  const bool rv = srow < B;
-  const int rc = rv ? srow : B - 1;
-  float4 hv[FH_CPW], wl[FH_CPW];
-  float wt[FH_CPW][3];
-#pragma unroll
-  for (int u = 0; u < FH_CPW; ++u) {
-    const int c = wv + FH_NW * u;
-    const int kb = 16 * c + 4 * g;
-    const bool kv = c < 32 && kb < 500;
-    const int kc = kv ? kb : 496;
-    const float4 p0 = load_sc1(P, (unsigned)(((size_t)rc * 500 + kc) * 4));
-    const float4 p1 = load_sc1(P, (unsigned)((((size_t)B + rc) * 500 + kc) * 4));
-    const float4 b1 = *reinterpret_cast<const float4*>(a.b1 + kc);
-    const float4 w = *reinterpret_cast<const float4*>(a.w2 + (i < 10 ? i : 9) * 500 + kc);
-    hv[u] = make_float4(fmaxf(p0.x + p1.x + b1.x, 0.f), fmaxf(p0.y + p1.y + b1.y, 0.f),
-                        fmaxf(p0.z + p1.z + b1.z, 0.f), fmaxf(p0.w + p1.w + b1.w, 0.f));
-    const float wm = (kv && i < 10) ? 1.f : 0.f;
-    wl[u] = make_float4(w.x * wm, w.y * wm, w.z * wm, w.w * wm);
-    const int kd = min(16 * c + i, 499);  // dh pass: A[k row i][class 4s + g] = W2[4s + g][16c + i]
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int j = 4 * s + g;
-      const float v = a.w2[(j < 10 ? j : 9) * 500 + kd];
-      wt[u][s] = v * ((j < 10 && c < 32 && 16 * c + i < 500) ? 1.f : 0.f);
-    }
-  }
-  int tl[4];  // labels of samples 4g + r (wave 0's softmax)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) tl[r] = a.lab[min(mt * 16 + 4 * g + r, B - 1)];
-  const float bias = a.b2[i < 10 ? i : 0];
-  f32x4 acc0 = zero4(), acc1 = zero4();  // two chains: C[sample 4g + r][class i]
-#pragma unroll
-  for (int u = 0; u < FH_CPW; ++u) {
-    const float* hx = &hv[u].x;
-    const float* wx = &wl[u].x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (e & 1) acc1 = mfma16x16x4(hx[e], wx[e], acc1);
-      else acc0 = mfma16x16x4(hx[e], wx[e], acc0);
-    }
-  }
-  red[wv][lane] = acc0 + acc1;
-  __syncthreads();
-  stamp(dbg, 2);
-  if (wv == 0) {
-    f32x4 L = red[0][lane];
-#pragma unroll
-    for (int q = 1; q < FH_NW; ++q) L += red[q][lane];
-    const bool cls = i < 10;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int ts = 4 * g + r, b = mt * 16 + ts;
-      const bool bv = b < B;
-      const int t = tl[r];
-      const float l = L[r] + bias;
-      float m = cls ? l : -INFINITY;
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
-      float se = cls ? __expf(l - m) : 0.f;
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) se += __shfl_xor(se, o, 16);
-      const float lse = m + __logf(se);
-      int pred = (cls && l == m) ? i : 16;  // first maximum
-#pragma unroll
-      for (int o = 8; o >= 1; o >>= 1) pred = min(pred, __shfl_xor(pred, o, 16));
-      const float lt = __shfl(l, t, 16);
-      const float dl = cls ? (__expf(l - lse) - (i == t ? 1.f : 0.f)) * a.grad_scale : 0.f;
-      dl_s[ts][i] = dl;
-      if (bv) {
-        if (cls) a.dlogits[(size_t)b * 10 + i] = dl;
-        if (i == 0) {
-          a.per_sample[2 * b] = lse - lt;
-          a.per_sample[2 * b + 1] = pred == t ? 1.f : 0.f;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // ---- dh = (dl . W2) * (h > 0), and h itself, for this wave's chunks
-  float dlr[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) dlr[s] = dl_s[i][min(4 * s + g, 15)];  // B[class 4s + g][sample i]
-#pragma unroll
-  for (int u = 0; u < FH_CPW; ++u) {
-    const int c = wv + FH_NW * u;
-    const int kb = 16 * c + 4 * g;
-    if (c < 32) {  // wave-uniform
-      f32x4 d = zero4();
-#pragma unroll
-      for (int s = 0; s < 3; ++s) d = mfma16x16x4(wt[u][s], dlr[s], d);
-      if (rv && kb < 500) {
-        const float4 h = hv[u];
-        *reinterpret_cast<float4*>(a.h_out + (size_t)srow * 500 + kb) = h;
-        *reinterpret_cast<float4*>(a.dh + (size_t)srow * 500 + kb) =
-            make_float4(h.x > 0.f ? d[0] : 0.f, h.y > 0.f ? d[1] : 0.f, h.z > 0.f ? d[2] : 0.f,
-                        h.w > 0.f ? d[3] : 0.f);
-      }
-    }
-  }
-  stamp(dbg, 3);
-}
-
-// ---------------------------------------------------------------------------
 // E: fc1 backward, three independent jobs in one launch (blockDim 512 = 8 waves):
 //   job 1 (200 blocks x 8 waves = 1600 tiles): dW_fc1[500,800] = dh^T . a2 (K = B,
 //          64 samples per register-preloaded chunk), db_fc1 from the kt==0 tiles.
@@ -1576,52 +1380,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd_kernel(
   stamp(dbg, 5);
 }
 
-// slab reduction helpers (the tail, and conv_bwd4's fused tail)
-constexpr int SR_COLS = 32;
-constexpr int SR_CH = 8;
-constexpr int SR_SL = 256 / SR_COLS;
-
-__device__ __forceinline__ void add4(float4& a, const float4& v) {
-  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-}
-
-// Rows [slice * per, min(rows, (slice + 1) * per)) of float4 column cc summed in row order,
-// per = ceil(rows / nsl).  Every load is issued before the first add (clamped addresses).
-// ld(row, cc) loads one float4 of the slab (plain, or sc1 for an in-launch hand-off).
-template <typename LD>
-__device__ __forceinline__ float4 slab_col_sum_ld(LD ld, int cc, int rows, int slice, int nsl) {
-  const int per = (rows + nsl - 1) / nsl;
-  const int b0 = slice * per, b1 = min(rows, b0 + per);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (per <= 2) {  // chunked conv2.weight rows: 16 rows / 8 slices at B = 64
-    const float4 v0 = ld(min(b0, rows - 1), cc);
-    const float4 v1 = ld(min(b0 + 1, rows - 1), cc);
-    if (b0 < b1) add4(acc, v0);
-    if (b0 + 1 < b1) add4(acc, v1);
-    return acc;
-  }
-  for (int base = b0; base < b1; base += SR_CH) {
-    float4 v[SR_CH];
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k) v[k] = ld(min(base + k, rows - 1), cc);
-#pragma unroll
-    for (int k = 0; k < SR_CH; ++k)
-      if (base + k < b1) add4(acc, v[k]);
-  }
-  return acc;
-}
-__device__ __forceinline__ float4 slab_col_sum(const float4* __restrict__ P4, long s4, int cc, int rows,
-                                               int slice, int nsl) {
-  return slab_col_sum_ld([=](int r, int c) { return P4[(size_t)r * s4 + c]; }, cc, rows, slice, nsl);
-}
-
-struct SlabRows {
-  int rows;      // rows of every column outside [big_lo4, big_hi4)
-  int rows_big;  // rows of the columns inside
-  int big_lo4, big_hi4;
-  __device__ __forceinline__ int of(int c4) const { return (c4 >= big_lo4 && c4 < big_hi4) ? rows_big : rows; }
-};
-
 // ---------------------------------------------------------------------------
 // F4: conv backward with dW_conv2 summed over 4-sample chunks (the training path).
 //   grid = (4 input-channel groups, 4 * ceil(B / 4)); block (cig, b): chunk q = b / 4,
@@ -1723,36 +1481,10 @@ __device__ __forceinline__ void bwd4_phase2(const float* dzc_s, const float* w_s
 }
 static_assert(F_TPW == 2, "bwd4_phase2 holds two 2a tiles per wave");
 
-// Fused tail (TAIL = true; the step's last launch then is this one): besides its own work every
-// block updates its 1/256 share of the fc parameters (SGD on the fc grads fc1_bwd finished),
-// stores its slab rows write-through (sc1), and after every store has landed adds 1 to an
-// arrival counter (agent-scope atomic; MI355X_MICROARCH.md's cross-CU hand-off, row 1).  The last
-// `reducers` blocks to arrive wait (bounded) for the rest, then each reduces its share of the
-// slab columns with sc1 loads in slab_reduce_sgd_kernel's exact summation order and applies SGD
-// to those conv parameters; the very last arrival advances the step cursor.  Bit-identical to
-// conv_bwd4 + slab_reduce_sgd, one dependent launch boundary less.
-struct Bwd4Tail {
-  SlabRows sr;
-  int n;                 // conv-segment floats (slab columns reduced)
-  unsigned slab_bytes;   // B x stride x 4 (< 2^31: 32-bit buffer offsets)
-  float *gout, *p, *buf;  // reduced conv grads, conv parameters, momentum
-  SgdHyper hy;
-  int* step_counter;
-  float* p2;              // fc parameters / grads / momentum
-  const float* g2;
-  float* buf2;
-  int n2;
-  unsigned* cnt;          // arrival counter (monotonic: a launch of T blocks adds T)
-  int* err;               // set when a reducer's bounded wait timed out
-  int reducers;
-  long long timeout_ticks;
-};
-
-template <bool TAIL>
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
-    int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, Bwd4Tail t, u64* dbg) {
+    int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, u64* dbg) {
   extern __shared__ float lds[];
   float* dzc_s = lds + G_OFF_DZ;
   float* w_s = lds + G_OFF_W;
@@ -1777,16 +1509,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   const int jbase = 32 * r - cig;
   const int c0 = max(jbase, 0) / 25;  // first of the <= 2 input channels those columns touch
   stamp(dbg, 0);
-  // slab stores: plain, or write-through (sc1) when the fused tail reads them in this launch
-  const __amdgpu_buffer_rsrc_t S = buf_rsrc(slab, TAIL ? t.slab_bytes : 0u);
-  auto st1 = [&](float* q, float v) {
-    if constexpr (TAIL) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), S, (int)((q - slab) * 4), 0, 16);
-    else *q = v;
-  };
-  auto st4 = [&](float* q, float4 v) {
-    if constexpr (TAIL) store_sc1(S, (unsigned)((q - slab) * 4), v);
-    else *reinterpret_cast<float4*>(q) = v;
-  };
 
   // ---- phase 1: stage.  Group 1: the own sample's dz2 and the W2 slice; group 2: the chunk's
   // other three samples, the 2b im2col source, the own a1 / idx1 / xn (measured: keeping group
@@ -1871,20 +1593,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   stage_g2();
   __syncthreads();
   stamp(dbg, 1);
-  // fused tail: this block's share of the fc SGD, loads in flight under phase 2
-  float4 fp = make_float4(0.f, 0.f, 0.f, 0.f), fg = fp, fm = fp;
-  int fv = -1;
-  if constexpr (TAIL) {
-    const int bl = blockIdx.y * gridDim.x + blockIdx.x, nbl = gridDim.x * gridDim.y;
-    const int n24 = t.n2 >> 2, per = (n24 + nbl - 1) / nbl;  // <= F_NT (host-checked)
-    const int v = bl * per + tid;
-    if (tid < per && v < n24) {
-      fv = v;
-      fp = reinterpret_cast<const float4*>(t.p2)[v];
-      fg = reinterpret_cast<const float4*>(t.g2)[v];
-      fm = reinterpret_cast<const float4*>(t.buf2)[v];
-    }
-  }
 
   // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
   // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
@@ -1927,27 +1635,19 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       float* rp = rowq + (ct * 16 + i) * 500;
       const int j0 = jbase + jt * 16 + 4 * g;
       if (j0 >= 0 && j0 + 3 < 125) {
-        st4(rp + j0, make_float4(gacc[0], gacc[1], gacc[2], gacc[3]));
+        *reinterpret_cast<float4*>(rp + j0) = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
       } else {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          if (j0 + rr >= 0 && j0 + rr < 125) st1(rp + j0 + rr, gacc[rr]);
+          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
       }
     } else if (wv == 12) {
       const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
       const int j = jbase + (lane & 31);
-      if (j >= 0 && j < 125) st1(rowq + (48 + (lane >> 5)) * 500 + j, v);
+      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
     }
   }
-  if constexpr (TAIL) {
-    if (fv >= 0) {  // fc SGD: nothing in this launch reads the fc parameters
-      sgd4(fp, fm, fg, t.hy);
-      reinterpret_cast<float4*>(t.p2)[fv] = fp;
-      reinterpret_cast<float4*>(t.buf2)[fv] = fm;
-    }
-  }
-  if (!TAIL && !own) return;  // block-uniform: padding blocks of the last chunk are done
-  if (own) {
+  if (!own) return;  // block-uniform: padding blocks of the last chunk are done
 
   // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
   if (tid < 720) {
@@ -2013,66 +1713,11 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     float w1sum = 0.f;
 #pragma unroll
     for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
-    if (tid < 125) st1(rowb + o_gw1 + cig * 125 + tid, w1sum);  // tid = c * 25 + kh * 5 + kw
-    else st1(rowb + o_gb1 + cig * 5 + (tid - 125), w1sum);
+    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
+    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
   }
-  if (cig == 0 && tid < 50) st1(rowb + o_gb2 + tid, b2sum);
-  }  // own
+  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
   stamp(dbg, 5);
-  if constexpr (TAIL) {
-    // ---- arrival: every wave's slab stores have landed, then one add per block
-    __shared__ unsigned s_arr;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) s_arr = __hip_atomic_fetch_add(t.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const unsigned total = gridDim.x * gridDim.y;
-    const unsigned k = s_arr % total, base = s_arr - k;
-    if (k == total - 1 && t.step_counter != nullptr && tid == 0) atomicAdd(t.step_counter, 1);
-    if ((int)k < (int)total - t.reducers) return;  // block-uniform
-    const int r = (int)k - ((int)total - t.reducers);
-    // ---- reducer r: wait (bounded) for every block of this launch, then reduce its columns
-    if (tid == 0) {
-      const long long deadline = (long long)wall_clock64() + t.timeout_ticks;
-      while ((int)(__hip_atomic_load(t.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base) < (int)total) {
-        if ((long long)wall_clock64() > deadline) {
-          atomicOr(t.err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    __syncthreads();
-    stamp(dbg, 6);
-    constexpr int RC = F_NT / SR_SL;  // columns per pass (128), SR_SL row slices each
-    float4* rd = reinterpret_cast<float4*>(lds);  // [SR_SL][RC]: phase buffers are dead
-    const int n4 = t.n >> 2, per = (n4 + t.reducers - 1) / t.reducers;
-    const int c_lo = r * per, c_hi = min(n4, c_lo + per);
-    const long s4 = stride >> 2;
-    auto ld = [&](int row, int c) { return load_sc1(S, (unsigned)(((long)row * s4 + c) * 16)); };
-    const int slice = tid / RC, ci = tid - slice * RC;
-    for (int cb = c_lo; cb < c_hi; cb += RC) {
-      const int col = cb + ci, cc = min(col, n4 - 1);
-      float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bb = pp;
-      if (tid < RC) {
-        pp = reinterpret_cast<const float4*>(t.p)[cc];
-        bb = reinterpret_cast<const float4*>(t.buf)[cc];
-      }
-      rd[slice * RC + ci] = slab_col_sum_ld(ld, cc, t.sr.of(cc), slice, SR_SL);
-      __syncthreads();
-      if (tid < RC && col < c_hi) {
-        float4 acc = rd[tid];
-#pragma unroll
-        for (int q = 1; q < SR_SL; ++q) add4(acc, rd[q * RC + tid]);
-        if (t.gout != nullptr) reinterpret_cast<float4*>(t.gout)[col] = acc;
-        sgd4(pp, bb, acc, t.hy);
-        reinterpret_cast<float4*>(t.p)[col] = pp;
-        reinterpret_cast<float4*>(t.buf)[col] = bb;
-      }
-      __syncthreads();
-    }
-    stamp(dbg, 7);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2085,6 +1730,46 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
 // Slab reduction geometry: SR_COLS float4 columns per workgroup x SR_SL row slices, SR_CH
 // loads in flight per thread.  32 columns (200 reduction workgroups at B = 64, 32 KB each)
 // beat 64 (100 x 64 KB): 0.25 us off the load phase.
+constexpr int SR_COLS = 32;
+constexpr int SR_CH = 8;
+constexpr int SR_SL = 256 / SR_COLS;
+
+__device__ __forceinline__ void add4(float4& a, const float4& v) {
+  a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+}
+
+// Rows [slice * per, min(rows, (slice + 1) * per)) of float4 column cc summed in row order,
+// per = ceil(rows / nsl).  Every load is issued before the first add (clamped addresses).
+__device__ __forceinline__ float4 slab_col_sum(const float4* __restrict__ P4, long s4, int cc, int rows,
+                                               int slice, int nsl) {
+  const int per = (rows + nsl - 1) / nsl;
+  const int b0 = slice * per, b1 = min(rows, b0 + per);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (per <= 2) {  // chunked conv2.weight rows: 16 rows / 8 slices at B = 64
+    const float4 v0 = P4[(size_t)min(b0, rows - 1) * s4 + cc];
+    const float4 v1 = P4[(size_t)min(b0 + 1, rows - 1) * s4 + cc];
+    if (b0 < b1) add4(acc, v0);
+    if (b0 + 1 < b1) add4(acc, v1);
+    return acc;
+  }
+  for (int base = b0; base < b1; base += SR_CH) {
+    float4 v[SR_CH];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k) v[k] = P4[(size_t)min(base + k, rows - 1) * s4 + cc];
+#pragma unroll
+    for (int k = 0; k < SR_CH; ++k)
+      if (base + k < b1) add4(acc, v[k]);
+  }
+  return acc;
+}
+
+struct SlabRows {
+  int rows;      // rows of every column outside [big_lo4, big_hi4)
+  int rows_big;  // rows of the columns inside
+  int big_lo4, big_hi4;
+  __device__ __forceinline__ int of(int c4) const { return (c4 >= big_lo4 && c4 < big_hi4) ? rows_big : rows; }
+};
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(
     const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ out, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
@@ -2331,23 +2016,6 @@ int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* 
   return (int)hipGetLastError();
 }
 
-// fc1 forward + head in one launch (fc1_head_kernel): parts [2][B][500] scratch, cnt
-// [ceil(B / 16)] int32 zeros (the kernel leaves them 0); writes h_out, dh, dlogits, per_sample.
-int pto_mnist_fc1_head(const float* x, const float* w1, const float* b1, const float* w2,
-                       const float* b2, const int* lab, int B, float grad_scale, float* parts,
-                       int* cnt, float* h_out, float* dh, float* dlogits, float* per_sample,
-                       void* stream) {
-  if (B <= 0 || B > (1 << 19)) return -1;  // parts bytes < 2^31 (32-bit buffer offsets)
-  if (lab == nullptr || cnt == nullptr || dlogits == nullptr || per_sample == nullptr) return -1;
-  if ((((uintptr_t)x) | ((uintptr_t)w1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)parts) |
-       ((uintptr_t)h_out) | ((uintptr_t)dh)) & 15)
-    return -2;  // float4 rows
-  const FcHead a{x, w1, b1, w2, b2, lab, parts, cnt, h_out, dh, dlogits, per_sample, grad_scale, B};
-  hipLaunchKernelGGL(fc1_head_kernel, dim3(32, (B + 15) / 16, 2), dim3(64 * FH_NW), 0,
-                     (hipStream_t)stream, a, dbg_next());
-  return (int)hipGetLastError();
-}
-
 static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
   const int B = a.B;
   PTO_CHECK_B(B);
@@ -2509,65 +2177,11 @@ int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, cons
       o_gw1 + 500 > stride || o_gb1 + 20 > stride)
     return -1;
   static std::atomic<unsigned> attr_set{0};
-  const int rc = set_max_lds(conv_bwd4_kernel<false>, G_LDS * (int)sizeof(float), attr_set);
+  const int rc = set_max_lds(conv_bwd4_kernel, G_LDS * (int)sizeof(float), attr_set);
   if (rc != 0) return rc;
   const int nb = 4 * ((B + 3) / 4);
-  hipLaunchKernelGGL(conv_bwd4_kernel<false>, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float),
-                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B,
-                     Bwd4Tail{}, dbg_next());
-  return (int)hipGetLastError();
-}
-
-// conv_bwd4 + the step's tail in one launch (conv_bwd4_kernel<true>): as pto_mnist_conv_bwd4,
-// then the conv slab reduction (n floats, rows_big chunk rows for [big_lo, big_hi)) into gout +
-// SGD of p/buf, SGD of the fc range p2/g2/buf2 (n2 floats), cursor advance -- what
-// pto_slab_reduce_sgd does after it.  cnt: one uint32 (any start value, never reset); err: int32,
-// set when a reducer timed out.
-int pto_mnist_conv_bwd4_tail(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                             const float* xn, float* slab, int stride, int o_gw2, int o_gb2, int o_gw1,
-                             int o_gb1, int B, int n, float* gout, float* p, float* buf, float lr,
-                             float momentum, float dampening, float wd, float grad_scale, int nesterov,
-                             int first_step, int* step_counter, float* p2, const float* g2, float* buf2,
-                             int n2, int rows_big, int big_lo, int big_hi, unsigned* cnt, int* err,
-                             int reducers, double timeout_s, void* stream) {
-  PTO_CHECK_B(B);
-  if (4 * ((B + 3) / 4) > 65535) return -1;
-  if ((stride & 3) || (o_gw2 & 3) || (((uintptr_t)slab) & 15) || (((uintptr_t)dz2) & 15)) return -2;
-  if (o_gw2 < 0 || o_gb2 < 0 || o_gw1 < 0 || o_gb1 < 0 || o_gw2 + 25000 > stride || o_gb2 + 50 > stride ||
-      o_gw1 + 500 > stride || o_gb1 + 20 > stride)
-    return -1;
-  if (n <= 0 || (n & 3) || stride < n || n2 < 0 || (n2 & 3) || cnt == nullptr || err == nullptr) return -1;
-  if (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)) return -1;
-  if ((((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) | ((uintptr_t)p2) | ((uintptr_t)g2) |
-       ((uintptr_t)buf2)) & 15)
-    return -2;
-  const int nb = 4 * ((B + 3) / 4), total = 4 * nb;
-  if ((double)B * stride * 4 >= 2147483648.0) return -1;  // 32-bit buffer offsets
-  if ((n2 / 4 + total - 1) / total > F_NT) return -1;    // one fc float4 per thread
-  if (reducers < 1 || reducers > total) return -1;
-  Bwd4Tail t{};
-  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, t.sr)) return -1;
-  t.n = n;
-  t.slab_bytes = (unsigned)((long)B * stride * 4);
-  t.gout = gout;
-  t.p = p;
-  t.buf = buf;
-  t.hy = SgdHyper{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-  t.step_counter = step_counter;
-  t.p2 = p2;
-  t.g2 = g2;
-  t.buf2 = buf2;
-  t.n2 = n2;
-  t.cnt = cnt;
-  t.err = err;
-  t.reducers = reducers;
-  t.timeout_ticks = (long long)(timeout_s * 1e8);  // wall_clock64: 100 MHz
-  static std::atomic<unsigned> attr_set{0};
-  const int rc = set_max_lds(conv_bwd4_kernel<true>, G_LDS * (int)sizeof(float), attr_set);
-  if (rc != 0) return rc;
-  hipLaunchKernelGGL(conv_bwd4_kernel<true>, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float),
-                     (hipStream_t)stream, dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B,
-                     t, dbg_next());
+  hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
+                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
   return (int)hipGetLastError();
 }
 

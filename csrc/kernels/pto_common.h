@@ -24,26 +24,6 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// Raw buffer descriptor over [base, base + bytes) (32-bit lane offsets; out-of-range stores are
-// dropped and loads return 0 by the descriptor's bounds check).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-}
-
-// 16-B vector store / load with the sc1 cache policy (aux bit 4): the store writes through and
-// drops the line from this XCD's L2, the load bypasses L1 (MI355X_MICROARCH.md's cross-CU
-// hand-off table, row 1: producer sc1 stores + vmcnt(0) + agent atomic add, consumer sc1 loads)
-__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float4 v) {
-  const u32x4 d = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-  __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, 16);
-}
-__device__ __forceinline__ float4 load_sc1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
-  const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16);
-  return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -23,8 +23,10 @@
 //            (the conv segment reduced from the per-sample slabs in fixed row order, the
 //            rest copied) and stores every element into its OWNER's recv[my rank][.];
 //            fence; flag1[my rank][b] := s on every rank.
-//   phase 2  (owner) wait until flag1[*][*] >= s (local, lanes in parallel); chunk b of
-//            my shard = sum over senders in rank order (deterministic), scale 1/W; SGD on
+//   phase 2  (owner) wait until flag1[q][j] >= s for every sender q and every sender block j
+//            whose phase-1 slice lands in chunk b of my shard (push_sources; local, lanes in
+//            parallel; a chunk fed only by the producer's pre-push waits on block b's flag);
+//            chunk b of my shard = sum over senders in rank order (deterministic), scale 1/W; SGD on
 //            it (mode 1, ZeRO-1: each parameter is updated by exactly one rank) or the mean
 //            (mode 0); store the result locally and into every peer's gath[.]; fence;
 //            flag2[my rank][b] := s on every rank.
@@ -202,20 +204,62 @@ __device__ __forceinline__ void deposit(const XarArgs& a, long v, f4 g, bool deg
   push4(recv_buf(peer(a, q)) + (long)a.rank * a.shard4 + pos, g);
 }
 
-// Wait until every flag in `f[idx]` (idx = tid, tid + NT, ... < nf) is >= target.
-// All of a thread's flags are loaded back to back (one local round trip per poll), the
-// block leaves together.  False (error flagged) on timeout.
+// Wait until flag1[q][j] >= target for every sender q and every sender block j in the (at
+// most 3) ranges [lo[k], hi[k]); flags are [q][nblk] contiguous.  All of a thread's flags are
+// loaded back to back (one local round trip per poll), the block leaves together.  False (error
+// flagged) on timeout.
 template <int NT>
-__device__ bool wait_flags(const unsigned* f, int nf, unsigned target, long long deadline, int* err, int code) {
+__device__ bool wait_flag_ranges(const unsigned* f, int nblk, int world, const int (&lo)[3], const int (&hi)[3],
+                                 unsigned target, long long deadline, int* err, int code) {
+  const int n0 = hi[0] - lo[0], n1 = hi[1] - lo[1], n = n0 + n1 + (hi[2] - lo[2]);
   for (;;) {
     int pending = 0;
-    for (int i = threadIdx.x; i < nf; i += NT) pending |= load_sys(f + i) < target;
+    for (int i = threadIdx.x; i < world * n; i += NT) {
+      const int q = i / n, j = i - q * n;
+      const int blk = j < n0 ? lo[0] + j : (j < n0 + n1 ? lo[1] + j - n0 : lo[2] + j - n0 - n1);
+      pending |= load_sys(f + q * nblk + blk) < target;
+    }
     if (!__syncthreads_or(pending)) return true;
     if ((long long)wall_clock64() > deadline) {
       if (threadIdx.x == 0) atomicOr(err, code);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Sender blocks whose phase-1 pushes land in chunk b of my shard -- the same block indices on
+// every sender (every rank partitions its gradient identically): the conv columns of the chunk
+// (slab reduction, per_c columns per block) and its copied elements before / after the
+// pre-pushed range (per logical elements per block).  A chunk wholly inside the pre-pushed
+// range needs no phase-1 data; it waits on sender block b's flag alone, which proves that
+// sender's exchange launch began, so its producer launch (and its pre-push) had finished.
+__device__ __forceinline__ void push_sources(const XarArgs& a, int b, int (&lo)[3], int (&hi)[3]) {
+  const long c4 = a.slab != nullptr ? a.conv4 : 0;
+  const long skip = a.skip_hi4 - a.skip_lo4;
+  const long rest = a.npad4 - c4 - skip;
+  const long per = (rest + a.nblk - 1) / a.nblk;
+  const long per_c = c4 > 0 ? (c4 + a.nblk - 1) / a.nblk : 1;
+  const long f_lo = (long)a.rank * a.shard4 + (long)b * a.chunk4, f_hi = f_lo + a.chunk4;
+  for (int k = 0; k < 3; ++k) lo[k] = hi[k] = 0;
+  if (f_lo < c4) {  // conv columns
+    lo[0] = (int)(f_lo / per_c);
+    hi[0] = (int)((min(f_hi, c4) - 1) / per_c) + 1;
+  }
+  const long sk_lo = max(a.skip_lo4, c4), sk_hi = max(a.skip_hi4, c4);
+  const long a_lo = max(f_lo, c4), a_hi = min(f_hi, sk_lo);  // before the pre-pushed range
+  if (a_lo < a_hi) {
+    lo[1] = (int)((a_lo - c4) / per);
+    hi[1] = (int)((a_hi - 1 - c4) / per) + 1;
+  }
+  const long b_lo = max(f_lo, sk_hi), b_hi = f_hi;  // after it
+  if (b_lo < b_hi) {
+    lo[2] = (int)((b_lo - c4 - skip) / per);
+    hi[2] = (int)((b_hi - 1 - c4 - skip) / per) + 1;
+  }
+  if (lo[0] == hi[0] && lo[1] == hi[1] && lo[2] == hi[2]) {
+    lo[0] = b;
+    hi[0] = b + 1;
   }
 }
 
@@ -339,8 +383,13 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       }
     };
     load_pb(tid);  // in flight while waiting
-    // every sender block's flag (or timed out: go on, the error is set); block-uniform
-    wait_flags<NT>(reinterpret_cast<const unsigned*>(mine), a.world * a.nblk, s, deadline, a.err, kErrPushWait);
+    // the flags of the sender blocks that feed this chunk (or timed out: go on, the error is
+    // set); block-uniform.  Not every sender block's: chunks fed only by the producer's
+    // pre-push start as soon as the matching sender block is in its exchange
+    int src_lo[3], src_hi[3];
+    push_sources(a, b, src_lo, src_hi);
+    wait_flag_ranges<NT>(reinterpret_cast<const unsigned*>(mine), a.nblk, a.world, src_lo, src_hi, s, deadline,
+                         a.err, kErrPushWait);
     acquire_fence(a);
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
       // every sender's contribution in flight at once (clamped addresses, no predicated

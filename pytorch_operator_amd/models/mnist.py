@@ -12,7 +12,6 @@ pre-allocated workspaces, and a whole step can be captured into one hipGraph.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -148,14 +147,7 @@ class FusedMnistTrainer:
         #   conv_chunk 4: conv_bwd4 sums dW_conv2 over 4-sample chunks -> the slab the tail
         #                 reduces is 4x smaller (1: the per-sample conv_bwd, the fallback)
         #   stage_batches: fc1_bwd stages the next step's batch; conv12 reads it with one load
-        #   fuse_head: fc1 forward + head as one launch (fc1_head_kernel: the last-arriving
-        #              block of each 16-sample tile runs its head; False: fc1_fwd<2> + head)
         self.fuse_conv12 = True
-        self.fuse_head = os.environ.get("PTO_MNIST_FUSE_HEAD", "1") != "0"
-        #   fuse_tail: conv_bwd4 + the tail (slab reduction + SGD of every parameter + cursor)
-        #              as one launch: the last `tail_reducers` workgroups reduce the slab
-        self.fuse_tail = os.environ.get("PTO_MNIST_FUSE_TAIL", "0") != "0"
-        self.tail_reducers = int(os.environ.get("PTO_MNIST_TAIL_REDUCERS", "16"))
         self.conv_chunk = 4
         self.stage_batches = True
 
@@ -187,9 +179,6 @@ class FusedMnistTrainer:
         self.per_sample = torch.empty((B, 2), device=dev)
         self.fc1_ks = self.K.fc1_split()
         self.h_parts = torch.empty(self.fc1_ks * B * 500, device=dev)  # split-K fc1 pre-activations
-        self.fc1_cnt = torch.zeros((B + 15) // 16, device=dev, dtype=torch.int32)  # fc1_head arrivals
-        self.tail_cnt = torch.zeros(1, device=dev, dtype=torch.int32)  # conv_bwd4_tail arrivals
-        self.tail_err = torch.zeros(1, device=dev, dtype=torch.int32)
         self.stage = K_stage(self.source, B, dev)
         # conv-grad slabs in the flat conv-segment layout (pads stay 0): per-sample rows, or
         # (conv_bwd4) per-4-sample-chunk rows for conv2.weight
@@ -217,12 +206,15 @@ class FusedMnistTrainer:
 
     # ---------------------------------------------------------------- step
     #
-    # One single-process step is five launches (one hipGraph, or the captured kernel list
+    # One single-process step is six launches (one hipGraph, or the captured kernel list
     # launched from C++ -- parallel/graphed_step.py):
     #
-    #   conv12_fwd -> fc1_head (fc1 forward + head) -> fc1_bwd (+ next-batch staging)
-    #   -> conv_bwd4 -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor
-    #   advance)
+    #   conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd (+ next-batch staging) -> conv_bwd4
+    #   -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor advance)
+    #
+    # Fusing a pair across an in-launch hand-off (last-arriving workgroups continue, write-through
+    # stores + an arrival counter) measured slower than the launch boundary it removes: fc1 + head
+    # +5.3 us, conv_bwd4 + tail +7.3 to +10.8 us per step (profiles/r4_inlaunch_handoff_ab.txt).
     #
     # DDP: with the xGMI kernel the tail launch is the cross-GPU exchange + SGD
     # (parallel/xgmi.py); with RCCL the fc / conv buckets are all-reduced between the pieces.
@@ -236,8 +228,7 @@ class FusedMnistTrainer:
                               (source is None or source is self.source)) else None
 
     def forward(self, source=None, B: Optional[int] = None) -> None:
-        """conv12_fwd (or conv1_fwd + conv2_fwd) + fc1 and the head in one launch (``fuse_head``;
-        otherwise the split-K fc1 partials, which ``_head`` finishes)."""
+        """conv12_fwd (or conv1_fwd + conv2_fwd) + split-K fc1 (the head finishes h)."""
         K, p = self.K, self._pv
         src = source or self.source
         B = self.B if B is None else B
@@ -252,20 +243,10 @@ class FusedMnistTrainer:
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
         ks = self.fc1_ks
-        hp = self.h_parts[:ks * B * 500].view(ks, B, 500)
-        if self.fuse_head:
-            K.fc1_head(self.a2[:B], p["fc1.weight"], p["fc1.bias"], p["fc2.weight"], p["fc2.bias"],
-                       self.lab[:B], grad_scale=1.0 / B, parts=hp, counters=self.fc1_cnt,
-                       h_out=self.h1[:B], dh=self.dh[:B], dlogits=self.dlogits[:B],
-                       per_sample=self.per_sample[:B])
-            return
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=hp)
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500))
 
     def _head(self, B: int) -> None:
-        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch; a
-        no-op with ``fuse_head``: forward ran it)."""
-        if self.fuse_head:
-            return
+        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
         K, p = self.K, self._pv
         hp = self.h_parts[:self.fc1_ks * B * 500].view(self.fc1_ks, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
@@ -365,25 +346,12 @@ class FusedMnistTrainer:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return
-        # 5 launches: conv12_fwd -> fc1_head -> fc1_bwd -> conv_bwd4 -> tail
+        # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
         K = self.K
         ce = self.layout.conv_end
         self.forward(source, B)
         self._head(B)
         self._fc1_bwd(B, stage_adv=1 if advance_cursor else 0)
-        if self.fuse_tail and self.conv_chunk == 4:
-            p = self._pv
-            K.conv_bwd4_tail(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
-                             self.conv_slab, self.layout.offsets, B, grads=self.conv_bucket(),
-                             params=self._fp[:ce], buf=self._fm[:ce], lr=self.lr, momentum=self.momentum,
-                             dampening=self.dampening, weight_decay=self.weight_decay,
-                             nesterov=self.nesterov, first_step=self._first_step,
-                             step_counter=self.cursor if advance_cursor else None,
-                             extra=(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
-                             counter=self.tail_cnt, err=self.tail_err, reducers=self.tail_reducers)
-            self._last_big = K.conv_bwd4_rows(B, self.layout.offsets)
-            self._first_step = False
-            return
         self._conv_bwd(B)
         K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
                            self._fm[:ce], lr=self.lr, momentum=self.momentum,

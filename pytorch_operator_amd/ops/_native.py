@@ -126,14 +126,11 @@ _SIGNATURES = {
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
-    "pto_mnist_fc1_head": [_VP, _VP, _VP, _VP, _VP, _VP, _I, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_ks": [],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
-    "pto_mnist_conv_bwd4_tail": [_VP] * 6 + [_I] * 7 + [_VP] * 3 + [_F] * 5 + [_I, _I, _VP, _VP, _VP, _VP] +
-                                [_I] * 4 + [_VP, _VP, _I, ctypes.c_double, _VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],

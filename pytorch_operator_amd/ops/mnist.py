@@ -255,40 +255,6 @@ def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] 
     return out
 
 
-def fc1_head(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
-             lab: torch.Tensor, *, grad_scale: float, parts: torch.Tensor, counters: torch.Tensor,
-             h_out: torch.Tensor, dh: torch.Tensor, dlogits: torch.Tensor, per_sample: torch.Tensor) -> None:
-    """fc1 forward + head in ONE launch (the training path; ``fc1_fwd_parts`` + ``head``).
-
-    ``h_out = relu(x @ w1.T + b1)``, fc2 + log-softmax + NLL per sample into ``per_sample``
-    [B,2] (loss, correct), ``dlogits`` [B,10] (scaled by ``grad_scale``) and ``dh`` [B,500]
-    (ReLU-masked).  ``parts`` (fp32 [2,B,500]) is scratch for the split-K partials;
-    ``counters`` (int32 [>= ceil(B/16)], zero) are the per-sample-tile arrival counters: the
-    last-arriving block of a tile runs that tile's head and leaves its counter at 0 again
-    (mnist_kernels.hip fc1_head_kernel).
-    """
-    lib = _native.load()
-    B = x.shape[0]
-    _req(x, (B, 800), torch.float32, "x")
-    _req(w1, (500, 800), torch.float32, "fc1.weight")
-    _req(b1, (500,), torch.float32, "fc1.bias")
-    _req(w2, (10, 500), torch.float32, "fc2.weight")
-    _req(b2, (10,), torch.float32, "fc2.bias")
-    _req(lab, (B,), torch.int32, "lab")
-    _req(parts, (2, B, 500), torch.float32, "fc1 partials")
-    if counters.dtype != torch.int32 or counters.numel() < (B + 15) // 16 or not counters.is_contiguous():
-        raise ValueError("counters: contiguous int32 with >= ceil(B/16) elements")
-    _req(h_out, (B, 500), torch.float32, "h_out")
-    _req(dh, (B, 500), torch.float32, "dh")
-    _req(dlogits, (B, 10), torch.float32, "dlogits")
-    _req(per_sample, (B, 2), torch.float32, "per_sample")
-    rc = lib.pto_mnist_fc1_head(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-                                lab.data_ptr(), B, float(grad_scale), parts.data_ptr(),
-                                counters.data_ptr(), h_out.data_ptr(), dh.data_ptr(), dlogits.data_ptr(),
-                                per_sample.data_ptr(), _stream())
-    _native.check(rc, "fc1_head")
-
-
 def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *,
          grad_scale: float = 0.0, loss_scale: float = 1.0, want_grad: bool = True,
          want_logp: bool = False, stats: Optional[torch.Tensor] = None,
@@ -477,52 +443,6 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     rc = lib.pto_mnist_conv_bwd4(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
                                  slab.data_ptr(), slab.shape[1], *o, B, _stream())
     _native.check(rc, "conv_bwd4")
-
-
-def conv_bwd4_tail(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: int, *,
-                   grads: torch.Tensor, params: torch.Tensor, buf: torch.Tensor, lr: float,
-                   momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
-                   nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
-                   step_counter: Optional[torch.Tensor] = None, extra: Optional[tuple] = None,
-                   counter: torch.Tensor, err: torch.Tensor, reducers: int = 16,
-                   timeout_s: float = 0.1) -> None:
-    """``conv_bwd4`` + ``slab_reduce_sgd_(slab, B, grads, params, buf, ..., extra=extra,
-    big=conv_bwd4_rows(B, offsets))`` in ONE launch (mnist_kernels.hip conv_bwd4_kernel<true>):
-    the last ``reducers`` workgroups to finish reduce the slab (same summation order: bit-identical)
-    after an in-launch hand-off.  ``counter``: uint32-as-int32 [1], any value, advanced by the
-    launch; ``err``: int32 [1], set to 1 if a reducer's bounded wait (``timeout_s``) expired."""
-    lib = _native.load()
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
-    _req(w2, CONV2_W, torch.float32, "conv2.weight")
-    _req(a1, (B, 20, 12, 12), torch.float32, "a1")
-    _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
-    _req(xn, (B, 784), torch.float32, "xn")
-    if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
-        raise ValueError("slab must be contiguous fp32 [>=B, S]")
-    n = params.numel()
-    for t, nm in ((grads, "grads"), (params, "params"), (buf, "momentum_buffer")):
-        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
-            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
-    p2 = g2 = b2 = None
-    n2 = 0
-    if extra is not None:
-        p2, g2, b2 = extra
-        n2 = p2.numel()
-        for t, nm in ((p2, "params2"), (g2, "grads2"), (b2, "buf2")):
-            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n2:
-                raise ValueError(f"{nm} must be contiguous fp32 with {n2} elements")
-    for t, nm in ((counter, "counter"), (err, "err")):
-        if t.dtype != torch.int32 or not t.is_cuda or t.numel() < 1:
-            raise ValueError(f"{nm} must be an int32 CUDA tensor")
-    o = [int(offsets[k]) for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
-    rb, lo, hi = conv_bwd4_rows(B, offsets)
-    rc = lib.pto_mnist_conv_bwd4_tail(
-        dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(), slab.data_ptr(),
-        slab.shape[1], *o, B, n, grads.data_ptr(), params.data_ptr(), buf.data_ptr(), float(lr),
-        float(momentum), float(dampening), float(weight_decay), float(grad_scale), int(nesterov),
-        int(first_step), _ptr(step_counter), _ptr(p2), _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi),
-        counter.data_ptr(), err.data_ptr(), int(reducers), float(timeout_s), _stream())
-    _native.check(rc, "conv_bwd4_tail")
 
 
 def conv_bwd4_rows(B: int, offsets: dict) -> tuple:

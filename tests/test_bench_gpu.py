@@ -78,5 +78,9 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
     bd = job["startup_breakdown"]
     assert bd and bd["job_create_to_process_start_s"] > 0 and bd["first_step_s"] > 0, bd
     (tmp_path / "job.json").write_text(json.dumps(job))
+    rec = os.environ.get("PTO_TEST_RECORD_DIR")  # keep the line (profiles/ records the world-2 latency)
+    if rec:
+        Path(rec).mkdir(parents=True, exist_ok=True)
+        (Path(rec) / f"bench_w2_{'slow-xgmi' if slow_xgmi else allreduce}.json").write_text(json.dumps(line))
     print(json.dumps({"world2_shared_gpu": {"create_to_first_step_s": line.get("create_to_first_step_s"),
                                              "startup_breakdown": bd, "allreduce": allreduce}}))

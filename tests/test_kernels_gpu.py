@@ -356,71 +356,6 @@ def test_round3_step_matches_round2_step(lib, B):
     assert _rel(new.flat_grads[:ce], old.flat_grads[:ce]) < 1e-5
 
 
-@pytest.mark.parametrize("B", [64, 50, 16, 1, 130])
-def test_fc1_head_fused_matches_split_launches(lib, B):
-    """fc1_head (fc1 forward + head in one launch, last-arriving block per 16-sample tile) vs
-    fc1_fwd_parts + head: h identical (same partial sums), the rest to fp32 rounding; the
-    arrival counters are 0 after every launch, across repeated launches."""
-    from pytorch_operator_amd.models.mnist import reference_init
-    from pytorch_operator_amd.ops import mnist as K
-    dev = torch.device("cuda")
-    sd = {k: v.to(dev).contiguous() for k, v in reference_init(7).items()}
-    g = torch.Generator().manual_seed(B)
-    a2 = torch.relu(torch.randn(B, 800, generator=g)).to(dev)
-    lab = torch.randint(0, 10, (B,), generator=g, dtype=torch.int32).to(dev)
-    parts = K.fc1_fwd_parts(a2, sd["fc1.weight"])
-    ref_ps = torch.zeros(B, 2, device=dev)
-    ref_dl = torch.zeros(B, 10, device=dev)
-    ref_dh = torch.zeros(B, 500, device=dev)
-    ref_h = torch.zeros(B, 500, device=dev)
-    K.head(parts[0], sd["fc2.weight"], sd["fc2.bias"], lab, grad_scale=1.0 / B, per_sample=ref_ps,
-           dlogits=ref_dl, dh=ref_dh, h_second=parts[1], fc1_bias=sd["fc1.bias"], h_out=ref_h)
-    cnt = torch.zeros((B + 15) // 16, dtype=torch.int32, device=dev)
-    scratch = torch.full((2, B, 500), float("nan"), device=dev)
-    outs = [torch.full(s, float("nan"), device=dev) for s in ((B, 500), (B, 500), (B, 10), (B, 2))]
-    for _ in range(3):
-        K.fc1_head(a2, sd["fc1.weight"], sd["fc1.bias"], sd["fc2.weight"], sd["fc2.bias"], lab,
-                   grad_scale=1.0 / B, parts=scratch, counters=cnt, h_out=outs[0], dh=outs[1],
-                   dlogits=outs[2], per_sample=outs[3])
-        torch.cuda.synchronize()
-        assert int(cnt.abs().sum()) == 0
-    h, dh, dl, ps = outs
-    assert torch.equal(h, ref_h)
-    assert _rel(dl, ref_dl) < 1e-5
-    assert _rel(dh, ref_dh) < 1e-5
-    assert _rel(ps[:, 0], ref_ps[:, 0]) < 1e-5
-    assert torch.equal(ps[:, 1], ref_ps[:, 1])
-    # against torch fp32 directly
-    rh = torch.relu(a2.cpu() @ sd["fc1.weight"].cpu().T + sd["fc1.bias"].cpu())
-    logits = rh @ sd["fc2.weight"].cpu().T + sd["fc2.bias"].cpu()
-    lp = torch.log_softmax(logits, 1)
-    assert _rel(ps[:, 0], -lp.gather(1, lab.cpu().long()[:, None])[:, 0]) < 1e-5
-    d = (lp.exp() - F.one_hot(lab.cpu().long(), 10).float()) / B
-    assert _rel(dl, d) < 1e-5
-    assert _rel(dh, (d @ sd["fc2.weight"].cpu()) * (rh > 0)) < 1e-5
-
-
-@pytest.mark.parametrize("B", [64, 37])
-def test_fused_head_step_matches_unfused_step(lib, B, monkeypatch):
-    """The 5-launch step (fc1_head) and the 6-launch step (fc1_fwd<2> + head) train the same
-    trajectory up to fp32 summation order."""
-    n = 8 * B
-    x, y = _data(n, seed=400 + B, n_total=n)
-    perm = torch.randperm(n, generator=torch.Generator().manual_seed(6)).to(torch.int32)
-    new = _stage_trainer(x, y, perm, B=B)
-    monkeypatch.setenv("PTO_MNIST_FUSE_HEAD", "0")
-    old = _stage_trainer(x, y, perm, B=B)
-    assert new.fuse_head and not old.fuse_head
-    for _ in range(5):
-        new.train_step()
-        old.train_step()
-    torch.cuda.synchronize()
-    assert _rel(new.flat_params, old.flat_params) < 1e-6
-    assert _rel(new.flat_momentum, old.flat_momentum) < 1e-5
-    assert abs(new.loss() - old.loss()) < 1e-5 * max(1.0, abs(old.loss()))
-    assert float(new.stats[1]) == float(old.stats[1])
-
-
 def test_on_device_synthetic_dataset_is_deterministic_and_mnist_like(lib):
     """The worker's start-up draws its synthetic set on the GPU: same seed -> same bytes, and
     the same shape / value statistics as the CPU recipe (a different random stream)."""
@@ -436,30 +371,3 @@ def test_on_device_synthetic_dataset_is_deterministic_and_mnist_like(lib):
     assert abs(ma - mc) < 0.05 * mc, (ma, mc)
     counts = torch.bincount(a.labels.long().cpu(), minlength=10)
     assert int(counts.min()) > 1700 and sorted(a.perm.cpu().tolist()) == list(range(20000))
-
-
-@pytest.mark.parametrize("B", [64, 37, 13])
-def test_fused_tail_step_is_bit_identical(lib, B, monkeypatch):
-    """conv_bwd4 + tail in one launch (the last workgroups reduce the slab after an in-launch
-    hand-off) trains bit-identically to conv_bwd4 + slab_reduce_sgd: same summation order;
-    the cursor advances once per step and no reducer wait times out."""
-    n = 8 * B
-    x, y = _data(n, seed=500 + B, n_total=n)
-    perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(torch.int32)
-    monkeypatch.setenv("PTO_MNIST_FUSE_TAIL", "1")
-    new = _stage_trainer(x, y, perm, B=B)
-    monkeypatch.setenv("PTO_MNIST_FUSE_TAIL", "0")
-    old = _stage_trainer(x, y, perm, B=B)
-    assert new.fuse_tail and not old.fuse_tail
-    for i in range(6):
-        adv = i != 3
-        new.train_step(advance_cursor=adv)
-        old.train_step(advance_cursor=adv)
-    torch.cuda.synchronize()
-    assert int(new.tail_err.item()) == 0
-    assert int(new.cursor.item()) == int(old.cursor.item()) == 5
-    assert torch.equal(new.flat_params, old.flat_params)
-    assert torch.equal(new.flat_momentum, old.flat_momentum)
-    assert torch.equal(new.flat_grads, old.flat_grads)
-    # the arrival counter advanced by one launch's workgroups per step
-    assert int(new.tail_cnt.item()) == 6 * 4 * 4 * ((B + 3) // 4)

@@ -30,9 +30,7 @@ from pytorch_operator_amd.ops import mnist as K  # noqa: E402
 from pytorch_operator_amd.parallel.graphed_step import NativeGraph  # noqa: E402
 
 SLOT_U64 = 1024 * 16  # mnist_kernels.hip kDbgSlotU64
-NAMES = ["conv12_fwd", "fc1_head", "fc1_bwd", "conv_bwd4", "tail"]
-NAMES_UNFUSED = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]  # PTO_MNIST_FUSE_HEAD=0
-NAMES_TAIL = ["conv12_fwd", "fc1_head", "fc1_bwd", "conv_bwd4_tail"]  # PTO_MNIST_FUSE_TAIL=1
+NAMES = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]
 # block ranges of the launches that run several jobs (B = 64): name -> [(first, end, job)]
 # (fc1_bwd: the dz2 job takes the first ids, mnist_kernels.hip fc1_bwd_kernel's block layout)
 GROUPS = {"fc1_bwd": [(0, 200, "dz2"), (200, 400, "dW_fc1"), (400, 404, "fc2+stats"), (404, 420, "stage")],
@@ -93,7 +91,7 @@ def main(argv=None):
     # per-kernel medians over the samples
     rows = []
     per = nk // 2
-    names = {len(NAMES): NAMES, len(NAMES_UNFUSED): NAMES_UNFUSED, len(NAMES_TAIL): NAMES_TAIL}.get(per, NAMES)
+    names = NAMES
     for k in range(nk):
         vals = {key: sorted(s[k][key] - s[0]["start"] for s in samples) for key in ("start", "end", "p50end")}
         med = {key: v[len(v) // 2] / 100.0 for key, v in vals.items()}
