@@ -1481,6 +1481,69 @@ __device__ __forceinline__ void bwd4_phase2(const float* dzc_s, const float* w_s
 }
 static_assert(F_TPW == 2, "bwd4_phase2 holds two 2a tiles per wave");
 
+#ifndef PTO_BWD4_SPLIT
+#define PTO_BWD4_SPLIT 0
+#endif
+// PTO_BWD4_SPLIT (round-4 A/B): after staging, waves 0-7 run 2a (four dcolT tiles each) and then
+// the VALU phases 3-4 + epilogue while waves 8-15 run all of 2b: the VALU work overlaps the 2b
+// MFMAs on the same SIMDs (waves w and w + 4 share one) instead of following them behind a
+// block barrier.  The two groups synchronise through LDS arrival counters.  Same per-tile
+// operation order as the barrier form: bit-identical.
+__device__ __forceinline__ void wave_group_sync(unsigned* ctr, unsigned target) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
+
+// 2a for wave w of 8: dcolT tiles jt0 .. jt0 + 3 (jt0 = 4 (w >> 2)) x position tile w & 3
+__device__ __forceinline__ void bwd4_2a4(const float* dzc_s, const float* w_s, float* dcol_s, int r, int w,
+                                         int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int pt = w & 3, jt0 = (w >> 2) * 4;
+  const float* qa_b = dzc_s + r * G_DZN + g * G_DZS + pt * 16 + i;
+  const float* qa_a = w_s + g * F_WS + jt0 * 16 + i;
+  float ya[13], xa[4][13];
+#pragma unroll
+  for (int s = 0; s < 13; ++s) {
+    ya[s] = qa_b[4 * s * G_DZS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) xa[t][s] = qa_a[4 * s * F_WS + 16 * t];
+  }
+  f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+  for (int s = 0; s < 13; ++s)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = mfma16x16x4(xa[t][s], ya[s], acc[t]);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) dcol_s[((jt0 + t) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[t][rr];
+}
+
+// 2b, one K half (samples 2 kh2, 2 kh2 + 1 of the chunk) of dW_conv2 tile pair tp
+__device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s, int tp, int kh2, int lane,
+                                         int jbase, int c0) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ct = tp >> 1, jt = tp & 1;
+  const int jc = min(max(jbase + jt * 16 + i, 0), 124);
+  const int ci = jc / 25, t = jc - ci * 25;
+  const float* qb_a = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
+  const float* qb_b = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
+  float xb[32], yb[32];
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {
+    const int s_ = u >> 4, uu = u & 15;
+    xb[u] = qb_a[s_ * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];
+    yb[u] = qb_b[s_ * G_DZN + 4 * uu];
+  }
+  f32x4 e0 = zero4(), e1 = zero4();
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {
+    if (u & 1) e1 = mfma16x16x4(xb[u], yb[u], e1);
+    else e0 = mfma16x16x4(xb[u], yb[u], e0);
+  }
+  return e0 + e1;
+}
+
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
@@ -1590,9 +1653,136 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     }
     if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv1;
   };
+#if PTO_BWD4_SPLIT
+  __shared__ unsigned s_grp[2];  // group arrival counters (waves 0-7, waves 8-15)
+  if (tid == 0) {
+    s_grp[0] = 0u;
+    s_grp[1] = 0u;
+  }
+#endif
   stage_g2();
   __syncthreads();
   stamp(dbg, 1);
+#if PTO_BWD4_SPLIT
+  if (wv >= 8) {  // ---- group B: all of 2b, then its slab rows
+    const int w8 = wv - 8;
+    const int tpb = w8 < 4 ? w8 : 4 + ((w8 - 4) >> 1), khb = (w8 - 4) & 1;
+    f32x4 gacc;
+    if (w8 < 4) {
+      const f32x4 h0 = bwd4_2b(dzc_s, a1c_s, tpb, 0, lane, jbase, c0);
+      gacc = h0 + bwd4_2b(dzc_s, a1c_s, tpb, 1, lane, jbase, c0);  // K half 0 + K half 1
+    } else {
+      gacc = bwd4_2b(dzc_s, a1c_s, tpb, khb, lane, jbase, c0);
+      if (khb) pk_s[tpb * 64 + lane] = gacc;
+      const int item = tid - 768;  // co 48 / 49 on the VALU, as the barrier form
+      const int sm = item >> 6, cr = (item >> 5) & 1, jl = item & 31;
+      const int jc = min(max(jbase + jl, 0), 124);
+      const int ci = jc / 25, t = jc - ci * 25;
+      const float* ar = a1c_s + sm * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5);
+      const float* dr = dzc_s + sm * G_DZN + (48 + cr) * G_DZS;
+      float accv = 0.f;
+#pragma unroll 16
+      for (int pos = 0; pos < 64; ++pos) accv = fmaf(dr[pos], ar[(pos >> 3) * F_A1R + (pos & 7)], accv);
+      pv_s[item] = accv;
+    }
+    wave_group_sync(&s_grp[1], 8u);
+    float* rowq = slab + (size_t)q * stride + o_gw2 + cig * 125;
+    if (w8 < 4 || khb == 0) {
+      if (w8 >= 4) gacc += pk_s[tpb * 64 + lane];
+      const int ctb = tpb >> 1, jtb = tpb & 1;
+      float* rp = rowq + (ctb * 16 + i) * 500;
+      const int j0 = jbase + jtb * 16 + 4 * g;
+      if (j0 >= 0 && j0 + 3 < 125) {
+        *reinterpret_cast<float4*>(rp + j0) = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
+      }
+    } else if (w8 == 5) {
+      const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
+      const int j = jbase + (lane & 31);
+      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
+    }
+    return;
+  }
+  // ---- group A (waves 0-7): 2a, col2im, dW_conv1, the own sample's slab row
+  if (!own) return;
+  bwd4_2a4(dzc_s, w_s, dcol_s, r, wv, lane);
+  float b2sum = 0.f;
+  if (cig == 0 && tid < 50) {
+    const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
+#pragma unroll 8
+    for (int p = 0; p < 64; ++p) b2sum += dzo[p];
+  }
+  wave_group_sync(&s_grp[0], 8u);
+  stamp(dbg, 2);
+  for (int it = tid; it < 720; it += 512) {  // phase 3 (as below)
+    const int c = it / 144, p = it - c * 144;
+    const int y = p / 12, x = p - y * 12;
+    const float* base = dcol_s + c * 25 * F_DC + y * 8 + x;
+    bool colok[5];
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) colok[kw] = (x - kw >= 0) & (x - kw <= 7);
+    float da = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      float dr = 0.f;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const float v = base[kh * (5 * F_DC - 8) + kw * (F_DC - 1)];
+        dr += colok[kw] ? v : 0.f;
+      }
+      da += ((y - kh >= 0) & (y - kh <= 7)) ? dr : 0.f;
+    }
+    const float d = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
+    const int pidx = idx_s[it];
+    float* z = dz1_s + c * F_Z1 + (2 * y) * F_Z1R + 2 * x;
+    z[0] = pidx == 0 ? d : 0.f;
+    z[1] = pidx == 1 ? d : 0.f;
+    z[F_Z1R] = pidx == 2 ? d : 0.f;
+    z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
+  }
+  wave_group_sync(&s_grp[0], 16u);
+  stamp(dbg, 3);
+  {
+    constexpr int NPART = 24;
+    for (int it = tid; it < 600; it += 512) {  // phase 4 (as below)
+      const int c = it / 120, rem = it - c * 120;
+      const int y = rem / 5, kh = rem - y * 5;
+      const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
+      const float* xr = x_s + (y + kh) * F_XR;
+      float xw[28];
+#pragma unroll
+      for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
+      float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+      float bs = 0.f;
+#pragma unroll
+      for (int x = 0; x < 24; ++x) {
+        const float a = zr[x];
+        bs += a;
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
+      }
+      float* pr = red + y * F_RED1;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
+      if (kh == 0) pr[125 + c] = bs;
+    }
+    wave_group_sync(&s_grp[0], 24u);
+    stamp(dbg, 4);
+    float* rowb = slab + (size_t)b * stride;
+    if (tid < 130) {
+      float w1sum = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
+      if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;
+      else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
+    }
+    if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
+    stamp(dbg, 5);
+  }
+#else
 
   // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
   // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
@@ -1718,6 +1908,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
   stamp(dbg, 5);
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -19,3 +19,8 @@ for rep in 1 2; do for v in 4 5; do
   PTO_ATTN_DKDV=$v timeout -k 10 200 python tools/attn_bench.py --impl hip --json-out $O/attn_dkdv${v}_$rep.json > $O/attn_dkdv${v}_$rep.log 2>&1 || { tail -20 $O/attn_dkdv${v}_$rep.log; exit 1; }
   echo "dkdv $v rep $rep: $(tail -1 $O/attn_dkdv${v}_$rep.log)"
 done; done
+bash tools/gpu/ab_libs.sh $O/ab 2 || exit 1
+bash tools/gpu/profile.sh $O/prof 2050 python3 bench.py --steps 2000 --warmup 50 --job-latency 0 || exit 1
+bash tools/gpu/pmc.sh $O/pmc python3 bench.py --steps 200 --warmup 10 --mode eager --job-latency 0 || exit 1
+timeout -k 10 120 python tools/step_timeline.py --json $O/timeline.json > $O/timeline.txt 2>&1 || { cat $O/timeline.txt; exit 1; }
+grep -E "period|one step" $O/timeline.txt
