@@ -1165,160 +1165,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv2_kernel(
   store_rows_T(dka, scale, &qd[0][0] + w * 32 * CH, lane, dk + off, kvstride);
 }
 
-// ------------------------ backward pass 2, lean registers + chain-ahead operand reads (dK, dV)
-// attn_bwd_dkdv2_kernel's work split and staging; each MFMA chain's LDS operand reads are issued
-// before the previous chain's MFMAs instead of after them (one wave per SIMD has no sibling wave
-// to hide a read round trip under), and the softmax statistics are read under the dP chain.
-__global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv5_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
-    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B, int S, int Hq, int Hkv, float c, float scale,
-    int causal) {
-  __shared__ u32x4 qd[2][2 * QT * CH];               // [buf][Q | dO] (32 KB); dK/dV epilogue
-  __shared__ __align__(16) float stat[2][2 * QT];    // [buf][lse2 | delta]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-  const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
-  const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
-  const int k0w = kblk * BK + w * 32, kme = k0w + r;
-  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
-
-  bf16x8 kf[NDS], vf[NDS];
-  {
-    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
-#pragma unroll
-    for (int s = 0; s < NDS; ++s) {
-      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
-      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(v + off + 16 * s));
-    }
-  }
-  const int qt0 = causal ? (kblk * BK) / QT : 0;
-  const int nqt = S / QT - qt0;
-  const int ntiles = G * nqt;
-  const int wskip = causal ? __builtin_amdgcn_readfirstlane(w) : 0;  // first live tile: qt0 + w
-
-  auto fetch = [&](int t, int buf) {
-    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
-    const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
-    glds_tile<QT, NT>(q + off, qstride, qd[buf], tid);
-    glds_tile<QT, NT>(dout + off, qstride, qd[buf] + QT * CH, tid);
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
-      const size_t srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
-      const float* src = (lane < 32 ? lse2 : delta) + srow + (lane & 31);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)stat[buf], 4, 0, 0);
-    }
-  };
-  fetch(0, 0);
-  __syncthreads();
-
-  f32x16 dka[NDT], dva[NDT];
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) {
-    dka[dt] = zero16();
-    dva[dt] = zero16();
-  }
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < ntiles) fetch(t + 1, cur ^ 1);  // lands under this tile's MFMAs
-    const int qtl = t % nqt;
-    if (qtl >= wskip) {  // wave-uniform
-      int boff = cur * 2 * QT * CH;
-      asm volatile("" : "+s"(boff));  // one set of operand addresses for both buffers
-      const u32x4* Qs = &qd[0][0] + boff;
-      const u32x4* Ds = Qs + QT * CH;
-      const int q0 = (qt0 + qtl) * QT;
-      f32x16 sa, pa;
-      // every chain's LDS operands are read one chain ahead: the reads of chain n+1 are issued
-      // before chain n's MFMAs (sched barriers pin the order), so with one wave per SIMD the
-      // read latency of dP, dV and dK hides under the previous chain; only S waits on its reads
-      bf16x8 qa[NDS], da[NDS];
-#pragma unroll
-      for (int s = 0; s < NDS; ++s) qa[s] = row_frag(Qs, r, 2 * s + h);
-#pragma unroll
-      for (int s = 0; s < NDS; ++s) da[s] = row_frag(Ds, r, 2 * s + h);
-      __builtin_amdgcn_sched_barrier(0);
-      sa = zero16();
-#pragma unroll
-      for (int s = 0; s < NDS; ++s) sa = mfma(qa[s], kf[s], sa);
-      __builtin_amdgcn_sched_barrier(0);
-      const float* st = reinterpret_cast<const float*>(stat) + cur * 2 * QT;
-      float4 L4[4], D4[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        L4[g4] = *reinterpret_cast<const float4*>(st + 8 * g4 + 4 * h);
-        D4[g4] = *reinterpret_cast<const float4*>(st + QT + 8 * g4 + 4 * h);
-      }
-      bf16x8 td0[NDT];
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) td0[dt] = tr_frag(Ds, 0, dt * 32, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      pa = zero16();
-#pragma unroll
-      for (int s = 0; s < NDS; ++s) pa = mfma(da[s], vf[s], pa);
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 td1[NDT];
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) td1[dt] = tr_frag(Ds, 16, dt * 32, lane);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float Lv[4] = {L4[g4].x, L4[g4].y, L4[g4].z, L4[g4].w};
-        const float Dv[4] = {D4[g4].x, D4[g4].y, D4[g4].z, D4[g4].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          const float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
-          sa[i] = p;
-          pa[i] = p * (pa[i] - Dv[e]);
-        }
-      }
-      if (causal && qtl == wskip) {  // the diagonal tile: keys after the query are masked
-        const int lim = kme - q0 - 4 * h;  // key > query  <=>  (i&3) + 8(i>>2) < lim
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if ((i & 3) + 8 * (i >> 2) < lim) {
-            sa[i] = 0.f;
-            pa[i] = 0.f;
-          }
-      }
-      bf16x8 tq0[NDT];
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) tq0[dt] = tr_frag(Qs, 0, dt * 32, lane);
-      {
-        const bf16x8 pb = acc_frag(sa, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) dva[dt] = mfma(td0[dt], pb, dva[dt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      bf16x8 tq1[NDT];
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) tq1[dt] = tr_frag(Qs, 16, dt * 32, lane);
-      {
-        const bf16x8 pb = acc_frag(sa, 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) dva[dt] = mfma(td1[dt], pb, dva[dt]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      {
-        const bf16x8 db = acc_frag(pa, 0);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) dka[dt] = mfma(tq0[dt], db, dka[dt]);
-      }
-      {
-        const bf16x8 db = acc_frag(pa, 1);
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) dka[dt] = mfma(tq1[dt], db, dka[dt]);
-      }
-    }
-    __syncthreads();
-  }
-  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
-  store_rows_T(dva, 1.f, &qd[0][0] + w * 32 * CH, lane, dv + off, kvstride);
-  __syncthreads();
-  store_rows_T(dka, scale, &qd[0][0] + w * 32 * CH, lane, dk + off, kvstride);
-}
-
 // ----------------------------------------- backward pass 2, software-pipelined (dK, dV)
 // Same work split as attn_bwd_dkdv_kernel (one wave per SIMD: dK^T / dV^T of 32 keys, K and V
 // fragments in registers, 390 of the 512), with the free registers spent on a pipeline: the
@@ -1608,8 +1454,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 int g_fwd_variant = -1;
 // dK/dV pass: 4 = lean-register 4-wave with LDS-DMA staging (default), 1 = the plain 4-wave
 // one (equal within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-pipelined 4-wave
-// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower), 5 = variant 4 with
-// chain-ahead operand reads (round 4 A/B); PTO_ATTN_DKDV or
+// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
@@ -1640,7 +1485,7 @@ extern "C" {
 
 int pto_attn_set_dkdv_variant(int v) {
   const int old = dkdv_variant();
-  if (v >= 1 && v <= 5) g_dkdv_variant = v;
+  if (v >= 1 && v <= 4) g_dkdv_variant = v;
   return old;
 }
 
@@ -1694,8 +1539,7 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
                        (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
   else
-    hipLaunchKernelGGL(dkdv_variant() == 5   ? attn_bwd_dkdv5_kernel
-                       : dkdv_variant() == 4 ? attn_bwd_dkdv2_kernel
+    hipLaunchKernelGGL(dkdv_variant() == 4   ? attn_bwd_dkdv2_kernel
                        : dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel
                                              : attn_bwd_dkdv_kernel,
                        dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,

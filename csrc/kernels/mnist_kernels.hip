@@ -1413,88 +1413,18 @@ static_assert(G_LDS * 4 <= 160 * 1024, "conv_bwd4 LDS budget");
 static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
 
 
-// Phase 2 of conv_bwd4 for one wave, software-pipelined: the LDS operand reads of chunk c+1
-// are issued before the MFMAs of chunk c (sched_barrier groups; the compiler's counted
-// lgkmcnt waits then only wait for chunk c), so every wave keeps its MFMA chain and its next
-// reads in flight together instead of all 16 waves alternating read bursts and MFMA bursts.
-//   DO_A: 2a, dcolT tiles (jt0, jt0+1) x position tile pt, K = 52 co in chunks of 4 k-steps
-//   DO_B: 2b, dW_conv2 tile pair tp over K half kh2 (32 k-steps, chunks of 8)
-template <bool DO_A, bool DO_B>
-__device__ __forceinline__ void bwd4_phase2(const float* dzc_s, const float* w_s, float* dcol_s,
-                                            const float* a1c_s, int r, int wv, int lane, int jbase,
-                                            int c0, f32x4& gacc) {
-  const int i = lane & 15, g = lane >> 4;
-  const int pt = wv & 3, jt0 = (wv >> 2) * F_TPW;
-  const float* qa_b = dzc_s + r * G_DZN + g * G_DZS + pt * 16 + i;
-  const float* qa_a = w_s + g * F_WS + jt0 * 16 + i;
-  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1, kh2 = wv / 6;
-  const int jc = min(max(jbase + jt * 16 + i, 0), 124);  // clamped: unstored columns read finite data
-  const int ci = jc / 25, t = jc - ci * 25;
-  const float* qb_a = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
-  const float* qb_b = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
-  float xa[2][13], ya[13], xb[32], yb[32];
-  f32x4 a0 = zero4(), a1 = zero4(), e0 = zero4(), e1 = zero4();
-#define B4_RA(c)                                                  \
-  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s)   \
-    if (s < 13) {                                                 \
-      ya[s] = qa_b[4 * s * G_DZS];                                \
-      xa[0][s] = qa_a[4 * s * F_WS];                              \
-      xa[1][s] = qa_a[4 * s * F_WS + 16];                         \
-    }
-#define B4_MA(c)                                                  \
-  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s)   \
-    if (s < 13) {                                                 \
-      a0 = mfma16x16x4(xa[0][s], ya[s], a0);                      \
-      a1 = mfma16x16x4(xa[1][s], ya[s], a1);                      \
-    }
-#define B4_RB(c)                                                  \
-  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
-    const int s_ = u >> 4, uu = u & 15;                           \
-    xb[u] = qb_a[s_ * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];  \
-    yb[u] = qb_b[s_ * G_DZN + 4 * uu];                            \
-  }
-#define B4_MB(c)                                                  \
-  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
-    if (u & 1) e1 = mfma16x16x4(xb[u], yb[u], e1);                \
-    else e0 = mfma16x16x4(xb[u], yb[u], e0);                      \
-  }
-#define B4_SB __builtin_amdgcn_sched_barrier(0);
-  if constexpr (DO_A) {
-    B4_RA(0) B4_SB B4_RA(1) B4_SB B4_MA(0) B4_SB B4_RA(2) B4_SB B4_MA(1) B4_SB B4_RA(3) B4_SB B4_MA(2) B4_SB
-    if constexpr (DO_B) { B4_RB(0) B4_SB }
-    B4_MA(3) B4_SB
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      dcol_s[(jt0 * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = a0[rr];
-      dcol_s[((jt0 + 1) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = a1[rr];
-    }
-    if constexpr (DO_B) { B4_RB(1) B4_SB B4_MB(0) B4_SB B4_RB(2) B4_SB B4_MB(1) B4_SB B4_RB(3) B4_SB B4_MB(2) B4_SB B4_MB(3) }
-  } else {
-    B4_RB(0) B4_SB B4_RB(1) B4_SB B4_MB(0) B4_SB B4_RB(2) B4_SB B4_MB(1) B4_SB B4_RB(3) B4_SB B4_MB(2) B4_SB B4_MB(3)
-  }
-#undef B4_RA
-#undef B4_MA
-#undef B4_RB
-#undef B4_MB
-#undef B4_SB
-  if constexpr (DO_B) gacc = e0 + e1;
-}
-static_assert(F_TPW == 2, "bwd4_phase2 holds two 2a tiles per wave");
 
-#ifndef PTO_BWD4_SPLIT
-#define PTO_BWD4_SPLIT 0
-#endif
-// PTO_BWD4_SPLIT (round-4 A/B): after staging, waves 0-7 run 2a (four dcolT tiles each) and then
-// the VALU phases 3-4 + epilogue while waves 8-15 run all of 2b: the VALU work overlaps the 2b
-// MFMAs on the same SIMDs (waves w and w + 4 share one) instead of following them behind a
-// block barrier.  The two groups synchronise through LDS arrival counters.  Same per-tile
-// operation order as the barrier form: bit-identical.
+// conv_bwd4's two wave groups synchronise through LDS arrival counters (one lane per wave adds,
+// release; every lane polls, acquire)
 __device__ __forceinline__ void wave_group_sync(unsigned* ctr, unsigned target) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
 }
 
-// 2a for wave w of 8: dcolT tiles jt0 .. jt0 + 3 (jt0 = 4 (w >> 2)) x position tile w & 3
+// 2a for wave w of 8: dcolT tiles jt0 .. jt0 + 3 (jt0 = 4 (w >> 2)) x position tile w & 3.
+// Software-pipelined like 2b below: the LDS operand reads of k-chunk c + 1 are issued before
+// the MFMAs of chunk c (sched_barrier groups keep the compiler from sinking each read to its
+// use, which serialises one LDS round trip per MFMA pair).
 __device__ __forceinline__ void bwd4_2a4(const float* dzc_s, const float* w_s, float* dcol_s, int r, int w,
                                          int lane) {
   const int i = lane & 15, g = lane >> 4;
@@ -1502,24 +1432,31 @@ __device__ __forceinline__ void bwd4_2a4(const float* dzc_s, const float* w_s, f
   const float* qa_b = dzc_s + r * G_DZN + g * G_DZS + pt * 16 + i;
   const float* qa_a = w_s + g * F_WS + jt0 * 16 + i;
   float ya[13], xa[4][13];
-#pragma unroll
-  for (int s = 0; s < 13; ++s) {
-    ya[s] = qa_b[4 * s * G_DZS];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) xa[t][s] = qa_a[4 * s * F_WS + 16 * t];
-  }
   f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-#pragma unroll
-  for (int s = 0; s < 13; ++s)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = mfma16x16x4(xa[t][s], ya[s], acc[t]);
+#define A4_R(c)                                                 \
+  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s) \
+    if (s < 13) {                                               \
+      ya[s] = qa_b[4 * s * G_DZS];                              \
+      _Pragma("unroll") for (int t = 0; t < 4; ++t) xa[t][s] = qa_a[4 * s * F_WS + 16 * t]; \
+    }
+#define A4_M(c)                                                 \
+  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s) \
+    if (s < 13) {                                               \
+      _Pragma("unroll") for (int t = 0; t < 4; ++t) acc[t] = mfma16x16x4(xa[t][s], ya[s], acc[t]); \
+    }
+#define A4_SB __builtin_amdgcn_sched_barrier(0);
+  A4_R(0) A4_SB A4_R(1) A4_SB A4_M(0) A4_SB A4_R(2) A4_SB A4_M(1) A4_SB A4_R(3) A4_SB A4_M(2) A4_SB A4_M(3)
+#undef A4_R
+#undef A4_M
+#undef A4_SB
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) dcol_s[((jt0 + t) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[t][rr];
 }
 
-// 2b, one K half (samples 2 kh2, 2 kh2 + 1 of the chunk) of dW_conv2 tile pair tp
+// 2b, one K half (samples 2 kh2, 2 kh2 + 1 of the chunk) of dW_conv2 tile pair tp, in four
+// chunks of 8 k-steps, reads one chunk ahead of the MFMAs
 __device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s, int tp, int kh2, int lane,
                                          int jbase, int c0) {
   const int i = lane & 15, g = lane >> 4;
@@ -1529,18 +1466,23 @@ __device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s,
   const float* qb_a = a1c_s + 2 * kh2 * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5) + g;
   const float* qb_b = dzc_s + 2 * kh2 * G_DZN + (ct * 16 + i) * G_DZS + g;
   float xb[32], yb[32];
-#pragma unroll
-  for (int u = 0; u < 32; ++u) {
-    const int s_ = u >> 4, uu = u & 15;
-    xb[u] = qb_a[s_ * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];
-    yb[u] = qb_b[s_ * G_DZN + 4 * uu];
-  }
   f32x4 e0 = zero4(), e1 = zero4();
-#pragma unroll
-  for (int u = 0; u < 32; ++u) {
-    if (u & 1) e1 = mfma16x16x4(xb[u], yb[u], e1);
-    else e0 = mfma16x16x4(xb[u], yb[u], e0);
+#define B2_R(c)                                                   \
+  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
+    const int s_ = u >> 4, uu = u & 15;                           \
+    xb[u] = qb_a[s_ * G_A1S + (uu >> 1) * F_A1R + 4 * (uu & 1)];  \
+    yb[u] = qb_b[s_ * G_DZN + 4 * uu];                            \
   }
+#define B2_M(c)                                                   \
+  _Pragma("unroll") for (int u = 8 * (c); u < 8 * (c) + 8; ++u) { \
+    if (u & 1) e1 = mfma16x16x4(xb[u], yb[u], e1);                \
+    else e0 = mfma16x16x4(xb[u], yb[u], e0);                      \
+  }
+#define B2_SB __builtin_amdgcn_sched_barrier(0);
+  B2_R(0) B2_SB B2_R(1) B2_SB B2_M(0) B2_SB B2_R(2) B2_SB B2_M(1) B2_SB B2_R(3) B2_SB B2_M(2) B2_SB B2_M(3)
+#undef B2_R
+#undef B2_M
+#undef B2_SB
   return e0 + e1;
 }
 
@@ -1653,17 +1595,26 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     }
     if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv1;
   };
-#if PTO_BWD4_SPLIT
   __shared__ unsigned s_grp[2];  // group arrival counters (waves 0-7, waves 8-15)
   if (tid == 0) {
     s_grp[0] = 0u;
     s_grp[1] = 0u;
   }
-#endif
   stage_g2();
   __syncthreads();
   stamp(dbg, 1);
-#if PTO_BWD4_SPLIT
+
+  // ---- phases 2-4 in two wave groups (round-4 A/B, profiles/r4_bwd4_split_ab.txt: -0.6 us per
+  // step).  Waves w and w + 4 share a SIMD, so each SIMD runs two waves of each group:
+  //   group B (waves 8-15): all of 2b -- dW_conv2[co, jbase + jl] over the chunk's 4 samples
+  //     (K = 256 positions); waves 8-11 tile pairs 0-3 over both K halves, waves 12-15 tile
+  //     pairs 4-5 one K half each + co 48 / 49 (a fourth 16-row tile would be 7/8 padding) as
+  //     256 VALU dot products; then its slab rows.
+  //   group A (waves 0-7): 2a -- dcolT[j][pos] = W2 slice^T . dz2[b] (M = 128 j, N = 64 pos,
+  //     K = 52), four tiles per wave -- then col2im, dW_conv1 and the own sample's slab row:
+  //     its VALU phases overlap group B's MFMAs instead of following them behind a barrier.
+  // The groups synchronise through LDS arrival counters; per-tile operation order as the
+  // one-barrier form: bit-identical.
   if (wv >= 8) {  // ---- group B: all of 2b, then its slab rows
     const int w8 = wv - 8;
     const int tpb = w8 < 4 ? w8 : 4 + ((w8 - 4) >> 1), khb = (w8 - 4) & 1;
@@ -1782,133 +1733,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
     stamp(dbg, 5);
   }
-#else
-
-  // ---- phase 2a (own sample): dcolT[j][pos] = W2 slice^T . dz2[b]  (M = 128 j, N = 64 pos, K = 52)
-  // ---- phase 2b: dW_conv2[co, jbase + jl] over the chunk's 4 samples (K = 256 positions)
-  //   waves 0-11: tile pair tp = wv % 6 (co tile ct = tp / 2 of 0..47, column tile jt = tp % 2),
-  //   K half wv / 6 (samples {0,1} or {2,3}); A = im2col (rows = columns jl), B = dz (cols = co).
-  //   waves 12-15: co 48 and 49 (a fourth 16-row tile would be 7/8 padding) as 256 VALU dot
-  //   products, one sample each, summed in sample order after the barrier.
-  f32x4 gacc = zero4();
-  const int tp = wv % 6, ct = tp >> 1, jt = tp & 1;
-  if (wv < 12) {
-    if (own) bwd4_phase2<true, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
-    else bwd4_phase2<false, true>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
-    if (wv >= 6) pk_s[tp * 64 + lane] = gacc;
-  } else {
-    if (own) bwd4_phase2<true, false>(dzc_s, w_s, dcol_s, a1c_s, r, wv, lane, jbase, c0, gacc);
-    const int item = tid - 768;  // (sample s, co 48 + cr, column jl)
-    const int s = item >> 6, cr = (item >> 5) & 1, jl = item & 31;
-    const int jc = min(max(jbase + jl, 0), 124);
-    const int ci = jc / 25, t = jc - ci * 25;
-    const float* ar = a1c_s + s * G_A1S + (ci - c0) * F_A1C + (t / 5) * F_A1R + (t % 5);
-    const float* dr = dzc_s + s * G_DZN + (48 + cr) * G_DZS;
-    float accv = 0.f;
-#pragma unroll 16
-    for (int pos = 0; pos < 64; ++pos) accv = fmaf(dr[pos], ar[(pos >> 3) * F_A1R + (pos & 7)], accv);
-    pv_s[item] = accv;
-  }
-  float b2sum = 0.f;
-  if (own && cig == 0 && tid < 50) {
-    const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
-#pragma unroll 8
-    for (int p = 0; p < 64; ++p) b2sum += dzo[p];
-  }
-  __syncthreads();
-  stamp(dbg, 2);
-  {
-    float* rowq = slab + (size_t)q * stride + o_gw2 + cig * 125;
-    if (wv < 6) {
-      gacc += pk_s[tp * 64 + lane];  // K half 0 + K half 1
-      // lane (i, g) holds co = 16 ct + i, columns jbase + 16 jt + 4 g + [0, 4)
-      float* rp = rowq + (ct * 16 + i) * 500;
-      const int j0 = jbase + jt * 16 + 4 * g;
-      if (j0 >= 0 && j0 + 3 < 125) {
-        *reinterpret_cast<float4*>(rp + j0) = make_float4(gacc[0], gacc[1], gacc[2], gacc[3]);
-      } else {
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          if (j0 + rr >= 0 && j0 + rr < 125) rp[j0 + rr] = gacc[rr];
-      }
-    } else if (wv == 12) {
-      const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
-      const int j = jbase + (lane & 31);
-      if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
-    }
-  }
-  if (!own) return;  // block-uniform: padding blocks of the last chunk are done
-
-  // ---- phase 3: col2im + un-pool + ReLU mask -> dz1_s[5][24*24]  (as conv_bwd_kernel)
-  if (tid < 720) {
-    const int c = tid / 144, p = tid - c * 144;
-    const int y = p / 12, x = p - y * 12;
-    const float* base = dcol_s + c * 25 * F_DC + y * 8 + x;
-    bool colok[5];
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) colok[kw] = (x - kw >= 0) & (x - kw <= 7);
-    float da = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      float dr = 0.f;
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const float v = base[kh * (5 * F_DC - 8) + kw * (F_DC - 1)];
-        dr += colok[kw] ? v : 0.f;
-      }
-      da += ((y - kh >= 0) & (y - kh <= 7)) ? dr : 0.f;
-    }
-    const float d = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
-    const int pidx = idx_s[tid];
-    float* z = dz1_s + c * F_Z1 + (2 * y) * F_Z1R + 2 * x;
-    z[0] = pidx == 0 ? d : 0.f;
-    z[1] = pidx == 1 ? d : 0.f;
-    z[F_Z1R] = pidx == 2 ? d : 0.f;
-    z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
-  }
-  __syncthreads();
-  stamp(dbg, 3);
-  // ---- phase 4: dW_conv1 partial + db_conv1 on the VALU: 600 threads = (channel c, output row
-  // y, kernel row kh), each slides a 28-wide register window of input row y + kh across the
-  // 24 outputs of dz1 row y: 5 FMAs per LDS read of dz1; 24 row partials meet in LDS.
-  constexpr int NPART = 24;
-  if (tid < 600) {
-    const int c = tid / 120, rem = tid - c * 120;
-    const int y = rem / 5, kh = rem - y * 5;
-    const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
-    const float* xr = x_s + (y + kh) * F_XR;
-    float xw[28];
-#pragma unroll
-    for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    float bs = 0.f;
-#pragma unroll
-    for (int x = 0; x < 24; ++x) {
-      const float a = zr[x];
-      bs += a;
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
-    }
-    float* pr = red + y * F_RED1;
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
-    if (kh == 0) pr[125 + c] = bs;
-  }
-  static_assert(5 * F_Z1 + NPART * F_RED1 <= 52 * F_WS, "phase-4 partials alias the W2 slice");
-  __syncthreads();
-  stamp(dbg, 4);
-  // ---- epilogue: sample b's small partials into slab row b
-  float* rowb = slab + (size_t)b * stride;
-  if (tid < 130) {
-    float w1sum = 0.f;
-#pragma unroll
-    for (int qq = 0; qq < NPART; ++qq) w1sum += red[qq * F_RED1 + tid];
-    if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;  // tid = c * 25 + kh * 5 + kw
-    else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
-  }
-  if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
-  stamp(dbg, 5);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2106,6 +1930,52 @@ int set_max_lds(K kernel, int bytes, std::atomic<unsigned>& done) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// S: the learnable synthetic MNIST stand-in (data/synthetic.py's recipe) drawn on the device by
+// one launch of this library -- the worker's start-up path: torch's own kernels for the same
+// warps cost 0.4-0.8 s of first-use code-object loading there (profiles/r4_startup.md).  Image
+// n: label = class template picked by a counter hash; sample = the template under a random
+// isotropic scale (+-10 %) and shift (+-0.125 of the half-width) read bilinearly with zero
+// padding (affine_grid / grid_sample, align_corners = False), times a random contrast in
+// [0.6, 1), plus noise * u^3; clamped to [0, 1], rounded to uint8.  One thread per pixel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned hash3(unsigned a, unsigned b, unsigned c) {
+  unsigned h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float unif(unsigned h) { return (float)(h >> 8) * (1.f / 16777216.f); }
+
+__global__ __launch_bounds__(256) void synth_mnist_kernel(const float* __restrict__ tmpl, uint8_t* __restrict__ img,
+                                                          int* __restrict__ lab, int n, unsigned seed,
+                                                          float noise) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)n * 784) return;
+  const int im = (int)(idx / 784), px = (int)(idx - (long)im * 784);
+  const unsigned u = (unsigned)im;
+  const int c = (int)(hash3(seed, u, 0u) % 10u);
+  const float sc = 1.f + (unif(hash3(seed, u, 1u)) - 0.5f) * 0.2f;
+  const float tx = (unif(hash3(seed, u, 2u)) - 0.5f) * 0.25f, ty = (unif(hash3(seed, u, 3u)) - 0.5f) * 0.25f;
+  const float contrast = 0.6f + 0.4f * unif(hash3(seed, u, 4u));
+  const int y = px / 28, x = px - y * 28;
+  const float gx = sc * ((2 * x + 1) / 28.f - 1.f) + tx, gy = sc * ((2 * y + 1) / 28.f - 1.f) + ty;
+  const float ix = ((gx + 1.f) * 28.f - 1.f) * 0.5f, iy = ((gy + 1.f) * 28.f - 1.f) * 0.5f;
+  const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  const float fx = ix - x0, fy = iy - y0;
+  const float* t = tmpl + c * 784;
+  auto at = [&](int yy, int xx) { return (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? t[yy * 28 + xx] : 0.f; };
+  float v = (1.f - fy) * ((1.f - fx) * at(y0, x0) + fx * at(y0, x0 + 1)) +
+            fy * ((1.f - fx) * at(y0 + 1, x0) + fx * at(y0 + 1, x0 + 1));
+  const float un = unif(hash3(seed, u, 5u + (unsigned)px));
+  v = v * contrast + noise * un * un * un;
+  img[idx] = (uint8_t)__float2int_rn(fminf(fmaxf(v, 0.f), 1.f) * 255.f);
+  if (px == 0) lab[im] = c;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -2116,6 +1986,17 @@ int set_max_lds(K kernel, int bytes, std::atomic<unsigned>& done) {
 #define PTO_CHECK_B(B) do { if ((B) <= 0 || (B) > (1 << 20)) return -1; } while (0)
 
 extern "C" {
+
+// Synthetic MNIST: n images [n][784] uint8 + int32 labels from the 10 class templates
+// tmpl [10][28][28] fp32 (synth_mnist_kernel).
+int pto_mnist_synth(const float* tmpl, void* img, int* lab, int n, unsigned seed, float noise, void* stream) {
+  if (tmpl == nullptr || img == nullptr || lab == nullptr || n <= 0 || n > (1 << 24)) return -1;
+  const long total = (long)n * 784;
+  hipLaunchKernelGGL(synth_mnist_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     tmpl, (uint8_t*)img, lab, n, seed, noise);
+  return (int)hipGetLastError();
+}
+
 
 void pto_set_debug_buffer(void* p) {
   g_dbg = reinterpret_cast<u64*>(p);

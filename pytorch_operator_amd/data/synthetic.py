@@ -55,33 +55,38 @@ def make_synthetic_mnist(n: int = 60000, seed: int = 1, device: Optional[torch.d
                          noise: float = 0.35, on_device: bool = False) -> SyntheticMnist:
     """``n`` images + labels (+ the epoch-0 permutation), moved to ``device``.
 
-    ``on_device``: draw every random number and run the warps on ``device`` itself (a GPU
-    generator seeded with ``seed``): the same recipe in a few ms instead of ~1-2 s of
-    single-threaded CPU work -- the worker's start-up path (harness/mnist.py).  A different
-    random stream than the CPU recipe, so a different (equally learnable) dataset; every rank
-    with the same seed draws the same one.
+    ``on_device`` (a GPU ``device``): the same recipe drawn by one HIP kernel of this
+    framework (``ops.mnist.synth_mnist``: counter-hash random numbers, bilinear warp) in ~1 ms
+    instead of ~2 s of single-threaded CPU warps -- the worker's start-up path
+    (harness/mnist.py).  A different random stream than the CPU recipe, so a different (equally
+    learnable) dataset; every rank with the same seed draws the same one.
     """
-    dev = torch.device(device) if (on_device and device is not None) else torch.device("cpu")
-    gen = torch.Generator(device=dev).manual_seed(seed)
-    tmpl = _templates(torch.Generator(device="cpu").manual_seed(12345)).to(dev)
-    labels = torch.randint(0, 10, (n,), generator=gen, device=dev)
-    out = torch.empty(n, 784, dtype=torch.uint8, device=dev)
-    chunk = 8192 if dev.type == "cpu" else 65536
+    tmpl = _templates(torch.Generator(device="cpu").manual_seed(12345))
+    if on_device and device is not None and torch.device(device).type == "cuda":
+        from ..ops import mnist as K
+        images, labels = K.synth_mnist(tmpl.to(device), n, seed, noise)
+        ds = SyntheticMnist(images, labels, torch.empty(n, dtype=torch.int32, device=device), seed)
+        ds.reshuffle(0)
+        return ds
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    labels = torch.randint(0, 10, (n,), generator=gen)
+    out = torch.empty(n, 784, dtype=torch.uint8)
+    chunk = 8192
     for s in range(0, n, chunk):
         lab = labels[s:s + chunk]
         m = lab.numel()
         base = tmpl[lab].unsqueeze(1)  # [m,1,28,28]
-        theta = torch.zeros(m, 2, 3, device=dev)
-        scale = 1.0 + (torch.rand(m, generator=gen, device=dev) - 0.5) * 0.2
+        theta = torch.zeros(m, 2, 3)
+        scale = 1.0 + (torch.rand(m, generator=gen) - 0.5) * 0.2
         theta[:, 0, 0] = scale
         theta[:, 1, 1] = scale
-        theta[:, :, 2] = (torch.rand(m, 2, generator=gen, device=dev) - 0.5) * 0.25
+        theta[:, :, 2] = (torch.rand(m, 2, generator=gen) - 0.5) * 0.25
         grid = F.affine_grid(theta, (m, 1, 28, 28), align_corners=False)
         img = F.grid_sample(base, grid, align_corners=False).squeeze(1)
-        img = img * (0.6 + 0.4 * torch.rand(m, 1, 1, generator=gen, device=dev))
-        img = img + noise * torch.rand(m, 28, 28, generator=gen, device=dev) ** 3
+        img = img * (0.6 + 0.4 * torch.rand(m, 1, 1, generator=gen))
+        img = img + noise * torch.rand(m, 28, 28, generator=gen) ** 3
         out[s:s + chunk] = (img.clamp(0, 1) * 255).round().to(torch.uint8).view(m, 784)
-    ds = SyntheticMnist(out, labels.to(torch.int32), torch.empty(n, dtype=torch.int32, device=dev), seed)
+    ds = SyntheticMnist(out, labels.to(torch.int32), torch.empty(n, dtype=torch.int32), seed)
     ds.reshuffle(0)
     if device is not None:
         ds.images = ds.images.to(device)

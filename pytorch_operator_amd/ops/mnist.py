@@ -445,6 +445,20 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     _native.check(rc, "conv_bwd4")
 
 
+def synth_mnist(templates: torch.Tensor, n: int, seed: int, noise: float = 0.35):
+    """(images uint8 [n, 784], labels int32 [n]) of the synthetic MNIST recipe drawn on the
+    device by one kernel (``templates``: fp32 [10, 28, 28] on the device); see
+    data/synthetic.py."""
+    lib = _native.load()
+    _req(templates, (10, 28, 28), torch.float32, "templates")
+    img = torch.empty((n, 784), dtype=torch.uint8, device=templates.device)
+    lab = torch.empty((n,), dtype=torch.int32, device=templates.device)
+    rc = lib.pto_mnist_synth(templates.data_ptr(), img.data_ptr(), lab.data_ptr(), int(n),
+                             int(seed) & 0xFFFFFFFF, float(noise), _stream())
+    _native.check(rc, "synth_mnist")
+    return img, lab
+
+
 def conv_bwd4_rows(B: int, offsets: dict) -> tuple:
     """(rows, lo, hi): the slab columns conv_bwd4 writes per 4-sample chunk."""
     lo = int(offsets["conv2.weight"])

@@ -134,7 +134,7 @@ def test_flash_forward_variants_agree(fwd_variant, shape):
     assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
 
 
-@pytest.mark.parametrize("dkdv", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("dkdv", [1, 2, 3, 4])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_backward_dkdv_variants(dkdv, causal):
     """The dK/dV passes -- plain 4-wave, software-pipelined 4-wave (3-deep Q/dO ring: 1-5 tiles
