@@ -1414,9 +1414,6 @@ static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS 
 
 
 
-#ifndef PTO_BWD4_PRIO
-#define PTO_BWD4_PRIO 0  // A/B: s_setprio of conv_bwd4's wave group A (2a + VALU phases)
-#endif
 // conv_bwd4's two wave groups synchronise through LDS arrival counters (one lane per wave adds,
 // release; every lane polls, acquire)
 __device__ __forceinline__ void wave_group_sync(unsigned* ctr, unsigned target) {
@@ -1662,7 +1659,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   // ---- group A (waves 0-7): 2a, col2im, dW_conv1, the own sample's slab row
   if (!own) return;
-  if (PTO_BWD4_PRIO > 0) __builtin_amdgcn_s_setprio(PTO_BWD4_PRIO);
   bwd4_2a4(dzc_s, w_s, dcol_s, r, wv, lane);
   float b2sum = 0.f;
   if (cig == 0 && tid < 50) {
