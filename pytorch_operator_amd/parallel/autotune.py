@@ -87,11 +87,25 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
         skipped["rccl-graph"] = "eager race"
     elif dist.get_backend() != "nccl":
         skipped["rccl-graph"] = f"{dist.get_backend()} collectives are not capturable"
+    elif "rccl-graph" in os.environ.get("PTO_RACE_SKIP", "").split(","):
+        skipped["rccl-graph"] = "PTO_RACE_SKIP"
     else:
-        r = GraphedStep(tr, mode="graph-comm")
-        runners["rccl-graph"] = r
-        times["rccl-graph"] = _timed(r, trial, dev, "rccl-graph")
-        steps += r.internal_steps + trial
+        # a capture that fails does so on every rank (same code, same data): every rank then
+        # drops the candidate together (the flag all-reduce keeps the ranks' collectives paired)
+        err = None
+        try:
+            r = GraphedStep(tr, mode="graph-comm")
+        except Exception as e:  # noqa: BLE001 -- the race must survive a failed candidate
+            err, r = repr(e)[:200], None
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            runners["rccl-graph"] = r
+            times["rccl-graph"] = _timed(r, trial, dev, "rccl-graph")
+            steps += r.internal_steps + trial
+        else:
+            skipped["rccl-graph"] = f"capture failed: {err or 'on another rank'}"
+            torch.cuda.synchronize(dev)
     tr.grad_sync = xgmi_sync
     r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
     runners["xgmi"] = r
