@@ -25,13 +25,14 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     tot = sum(int(r["TotalDurationNs"]) for r in rows)
-    print(f"total kernel time {tot / 1e6:.1f} ms over {a.steps:g} steps = {tot / 1e6 / a.steps:.1f} ms/step\n")
+    steps = a.steps if a.steps > 0 else 1.0  # 0: no per-step division
+    print(f"total kernel time {tot / 1e6:.1f} ms over {a.steps:g} steps = {tot / 1e6 / steps:.1f} ms/step\n")
     print("| kernel | calls | mean us | ms/step | % time |")
     print("|---|---|---|---|---|")
     for r in rows[: a.top]:
         t = int(r["TotalDurationNs"])
         print(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
-              f"{t / 1e6 / a.steps:.2f} | {100 * t / tot:.2f} |")
+              f"{t / 1e6 / steps:.2f} | {100 * t / tot:.2f} |")
 
 
 if __name__ == "__main__":
