@@ -49,12 +49,6 @@ using namespace pto;
 // fc1 split-K factor of the training path: 256 workgroups of 5 waves (K = 800 = 2 x 400)
 constexpr int FC1_KS = 2;
 
-#ifndef PTO_FC2F
-#define PTO_FC2F 0
-#endif
-#ifndef PTO_BWD4_AFIRST
-#define PTO_BWD4_AFIRST 0
-#endif
 
 namespace {
 
@@ -872,26 +866,15 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
   // dispatched first onto idle CUs, ordered so the four sample tiles of one feature tile share an
   // XCD (round-robin placement: blocks b and b + 8 share one) and read that W1 column slab into
   // one L2; then [nJ2, nJ2 + nJ1) dW_fc1, then fc2 + staging
-  int pb = blk;  // physical position among the dz2 / dW_fc1 blocks
-  if (PTO_FC2F) {  // A/B: the fc2 + statistics blocks (the last job to finish) take ids 0 .. nJ3 - 1
-    if (pb < nJ3) {
-      blk = nJ1 + nJ2 + pb;
-      pb = -1;
-    } else if (pb < nJ3 + nJ2 + nJ1) {
-      pb -= nJ3;
-    } else {
-      pb = -1;
-    }
-  }
-  if (pb >= 0 && pb < nJ2) {
-    int t2x = pb;  // dz2 tile mt * 50 + kt
+  if (blk < nJ2) {
+    int t2x = blk;  // dz2 tile mt * 50 + kt
     if (nJ2 == 200) {
-      const int s = (pb & 7) * 25 + (pb >> 3);  // blocks grouped by XCD: 25 per XCD
-      t2x = (s & 3) * 50 + (s >> 2);            // 4 consecutive slots = the 4 mt of one kt
+      const int s = (blk & 7) * 25 + (blk >> 3);  // blocks grouped by XCD: 25 per XCD
+      t2x = (s & 3) * 50 + (s >> 2);              // 4 consecutive slots = the 4 mt of one kt
     }
     blk = nJ1 + t2x;
-  } else if (pb >= nJ2 && pb < nJ2 + nJ1) {
-    blk = pb - nJ2;
+  } else if (blk < nJ2 + nJ1) {
+    blk -= nJ2;
   }
   if (blk < nJ1) {
     const int tile = blk * E_NW + wv;
@@ -1473,40 +1456,6 @@ __device__ __forceinline__ void bwd4_2a4(const float* dzc_s, const float* w_s, f
     for (int rr = 0; rr < 4; ++rr) dcol_s[((jt0 + t) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[t][rr];
 }
 
-// 2a over all 16 waves (PTO_BWD4_AFIRST): wave w: tiles jt0, jt0 + 1 (jt0 = 2 (w >> 2)) x position
-// tile w & 3, the same chunked read-ahead as bwd4_2a4
-__device__ __forceinline__ void bwd4_2a2(const float* dzc_s, const float* w_s, float* dcol_s, int r, int w,
-                                         int lane) {
-  const int i = lane & 15, g = lane >> 4;
-  const int pt = w & 3, jt0 = (w >> 2) * 2;
-  const float* qa_b = dzc_s + r * G_DZN + g * G_DZS + pt * 16 + i;
-  const float* qa_a = w_s + g * F_WS + jt0 * 16 + i;
-  float ya[13], xa[2][13];
-  f32x4 acc[2] = {zero4(), zero4()};
-#define A2_R(c)                                                 \
-  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s) \
-    if (s < 13) {                                               \
-      ya[s] = qa_b[4 * s * G_DZS];                              \
-      xa[0][s] = qa_a[4 * s * F_WS];                            \
-      xa[1][s] = qa_a[4 * s * F_WS + 16];                       \
-    }
-#define A2_M(c)                                                 \
-  _Pragma("unroll") for (int s = 4 * (c); s < 4 * (c) + 4; ++s) \
-    if (s < 13) {                                               \
-      acc[0] = mfma16x16x4(xa[0][s], ya[s], acc[0]);            \
-      acc[1] = mfma16x16x4(xa[1][s], ya[s], acc[1]);            \
-    }
-#define A2_SB __builtin_amdgcn_sched_barrier(0);
-  A2_R(0) A2_SB A2_R(1) A2_SB A2_M(0) A2_SB A2_R(2) A2_SB A2_M(1) A2_SB A2_R(3) A2_SB A2_M(2) A2_SB A2_M(3)
-#undef A2_R
-#undef A2_M
-#undef A2_SB
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) dcol_s[((jt0 + t) * 16 + g * 4 + rr) * F_DC + pt * 16 + i] = acc[t][rr];
-}
-
 // 2b, one K half (samples 2 kh2, 2 kh2 + 1 of the chunk) of dW_conv2 tile pair tp, in four
 // chunks of 8 k-steps, reads one chunk ahead of the MFMAs
 __device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s, int tp, int kh2, int lane,
@@ -1655,10 +1604,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   stage_g2();
   __syncthreads();
   stamp(dbg, 1);
-  if (PTO_BWD4_AFIRST) {  // A/B: 2a on all 16 waves before the split (no 2b contention)
-    if (own) bwd4_2a2(dzc_s, w_s, dcol_s, r, wv, lane);
-    __syncthreads();
-  }
 
   // ---- phases 2-4 in two wave groups (round-4 A/B, profiles/r4_bwd4_split_ab.txt: -0.6 us per
   // step).  Waves w and w + 4 share a SIMD, so each SIMD runs two waves of each group:
@@ -1715,14 +1660,14 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   // ---- group A (waves 0-7): 2a, col2im, dW_conv1, the own sample's slab row
   if (!own) return;
-  if (!PTO_BWD4_AFIRST) bwd4_2a4(dzc_s, w_s, dcol_s, r, wv, lane);
+  bwd4_2a4(dzc_s, w_s, dcol_s, r, wv, lane);
   float b2sum = 0.f;
   if (cig == 0 && tid < 50) {
     const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
 #pragma unroll 8
     for (int p = 0; p < 64; ++p) b2sum += dzo[p];
   }
-  if (!PTO_BWD4_AFIRST) wave_group_sync(&s_grp[0], 8u);
+  wave_group_sync(&s_grp[0], 8u);
   stamp(dbg, 2);
   for (int it = tid; it < 720; it += 512) {  // phase 3 (as below)
     const int c = it / 144, p = it - c * 144;
@@ -1750,7 +1695,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     z[F_Z1R] = pidx == 2 ? d : 0.f;
     z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
   }
-  wave_group_sync(&s_grp[0], PTO_BWD4_AFIRST ? 8u : 16u);
+  wave_group_sync(&s_grp[0], 16u);
   stamp(dbg, 3);
   {
     constexpr int NPART = 24;
@@ -1776,7 +1721,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
       if (kh == 0) pr[125 + c] = bs;
     }
-    wave_group_sync(&s_grp[0], PTO_BWD4_AFIRST ? 16u : 24u);
+    wave_group_sync(&s_grp[0], 24u);
     stamp(dbg, 4);
     float* rowb = slab + (size_t)b * stride;
     if (tid < 130) {
