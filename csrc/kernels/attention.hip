@@ -1165,6 +1165,134 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv2_kernel(
   store_rows_T(dka, scale, &qd[0][0] + w * 32 * CH, lane, dk + off, kvstride);
 }
 
+// ------------------------------------- backward pass 2 split in two (dV pass, dK pass)
+// attn_bwd_dkdv2_kernel holds both 32-key x 128-d accumulators (128 registers) plus the K and V
+// fragments: 394 registers, one wave per SIMD, nothing to hide its LDS / exp2 latencies under.
+// Split, each pass holds one accumulator and fits 256 registers, so two workgroups share a CU
+// (two waves per SIMD):
+//   DK = false (dV pass): S = Q.K^T, P = exp2(S c - lse2), dV^T += dO^T.P
+//   DK = true  (dK pass): S, dP = dO.V^T, dS = P (dP - delta), dK^T += Q^T.dS
+// (S is computed twice: 40 MFMAs per tile instead of 32).  Same per-element operation order
+// as attn_bwd_dkdv2_kernel: bit-identical dK, dV.  Block order pairs key blocks so the two
+// resident on a CU sum to the same causal work: heavy ones first, then the light ones
+// lightest-first (block j and j + grid/2 land on one CU).
+template <bool DK>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkdv_split_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
+    bf16_t* __restrict__ dkv, int B, int S, int Hq, int Hkv, float c, float scale, int causal) {
+  __shared__ u32x4 qd[2][2 * QT * CH];               // [buf][Q | dO] (32 KB); epilogue staging
+  __shared__ __align__(16) float stat[2][2 * QT];    // [buf][lse2 | delta]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int per = B * Hkv, nkb = S / BK;
+  const int jb = (int)blockIdx.x / per, bh = (int)blockIdx.x % per;
+  const int kblk = !causal || jb < nkb / 2 ? jb : nkb - 1 - (jb - nkb / 2);
+  const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
+  const int k0w = kblk * BK + w * 32, kme = k0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 kf[NDS], vf[DK ? NDS : 1];
+  {
+    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
+      if constexpr (DK) vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(v + off + 16 * s));
+    }
+  }
+  const int qt0 = causal ? (kblk * BK) / QT : 0;
+  const int nqt = S / QT - qt0;
+  const int ntiles = G * nqt;
+  const int wskip = causal ? __builtin_amdgcn_readfirstlane(w) : 0;
+
+  auto fetch = [&](int t, int buf) {
+    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
+    const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
+    glds_tile<QT, NT>(q + off, qstride, qd[buf], tid);
+    glds_tile<QT, NT>(dout + off, qstride, qd[buf] + QT * CH, tid);
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+      const size_t srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
+      const float* src = (lane < 32 ? lse2 : delta) + srow + (lane & 31);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)stat[buf], 4, 0, 0);
+    }
+  };
+  fetch(0, 0);
+  __syncthreads();
+
+  f32x16 acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) acc[dt] = zero16();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) fetch(t + 1, cur ^ 1);  // lands under this tile's MFMAs
+    const int qtl = t % nqt;
+    if (qtl >= wskip) {  // wave-uniform
+      int boff = cur * 2 * QT * CH;
+      asm volatile("" : "+s"(boff));
+      const u32x4* Qs = &qd[0][0] + boff;
+      const u32x4* Ds = Qs + QT * CH;
+      const int q0 = (qt0 + qtl) * QT;
+      f32x16 sa, pa;
+      {
+        bf16x8 qa[NDS];
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) qa[s] = row_frag(Qs, r, 2 * s + h);
+        __builtin_amdgcn_sched_barrier(0);
+        sa = zero16();
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) sa = mfma(qa[s], kf[s], sa);
+      }
+      if constexpr (DK) {
+        bf16x8 da[NDS];
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) da[s] = row_frag(Ds, r, 2 * s + h);
+        __builtin_amdgcn_sched_barrier(0);
+        pa = zero16();
+#pragma unroll
+        for (int s = 0; s < NDS; ++s) pa = mfma(da[s], vf[s], pa);
+      }
+      const float* st = reinterpret_cast<const float*>(stat) + cur * 2 * QT;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 L4 = *reinterpret_cast<const float4*>(st + 8 * g4 + 4 * h);
+        const float Lv[4] = {L4.x, L4.y, L4.z, L4.w};
+        float Dv[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (DK) {
+          const float4 D4 = *reinterpret_cast<const float4*>(st + QT + 8 * g4 + 4 * h);
+          Dv[0] = D4.x; Dv[1] = D4.y; Dv[2] = D4.z; Dv[3] = D4.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
+          if constexpr (DK) pa[i] = p * (pa[i] - Dv[e]);
+          else sa[i] = p;
+        }
+      }
+      f32x16& op = DK ? pa : sa;
+      if (causal && qtl == wskip) {  // the diagonal tile: keys after the query are masked
+        const int lim = kme - q0 - 4 * h;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if ((i & 3) + 8 * (i >> 2) < lim) op[i] = 0.f;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 tf[NDT];
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) tf[dt] = tr_frag(DK ? Qs : Ds, 16 * s2, dt * 32, lane);
+        const bf16x8 ob = acc_frag(op, s2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) acc[dt] = mfma(tf[dt], ob, acc[dt]);
+      }
+    }
+    __syncthreads();
+  }
+  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+  store_rows_T(acc, DK ? scale : 1.f, &qd[0][0] + w * 32 * CH, lane, dkv + off, kvstride);
+}
+
 // ----------------------------------------- backward pass 2, software-pipelined (dK, dV)
 // Same work split as attn_bwd_dkdv_kernel (one wave per SIMD: dK^T / dV^T of 32 keys, K and V
 // fragments in registers, 390 of the 512), with the free registers spent on a pipeline: the
@@ -1454,7 +1582,8 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 int g_fwd_variant = -1;
 // dK/dV pass: 4 = lean-register 4-wave with LDS-DMA staging (default), 1 = the plain 4-wave
 // one (equal within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-pipelined 4-wave
-// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower); PTO_ATTN_DKDV or
+// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower), 6 = split into a dV
+// pass and a dK pass of two waves per SIMD each (round-4 A/B); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
@@ -1485,7 +1614,7 @@ extern "C" {
 
 int pto_attn_set_dkdv_variant(int v) {
   const int old = dkdv_variant();
-  if (v >= 1 && v <= 4) g_dkdv_variant = v;
+  if ((v >= 1 && v <= 4) || v == 6) g_dkdv_variant = v;
   return old;
 }
 
@@ -1538,7 +1667,16 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
     hipLaunchKernelGGL(attn_bwd_dkdv8_kernel, dim3((S / BK8) * B * Hkv), dim3(NT8), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2,
                        (const float*)delta, (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
-  else
+  else if (dkdv_variant() == 6) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<false>, dim3((S / BK) * B * Hkv), dim3(NT), 0,
+                       (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       (const bf16_t*)dout, lse2, (const float*)delta, (bf16_t*)dv, B, S, Hq, Hkv, c, scale,
+                       causal);
+    hipLaunchKernelGGL(attn_bwd_dkdv_split_kernel<true>, dim3((S / BK) * B * Hkv), dim3(NT), 0,
+                       (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                       (const bf16_t*)dout, lse2, (const float*)delta, (bf16_t*)dk, B, S, Hq, Hkv, c, scale,
+                       causal);
+  } else
     hipLaunchKernelGGL(dkdv_variant() == 4   ? attn_bwd_dkdv2_kernel
                        : dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel
                                              : attn_bwd_dkdv_kernel,
