@@ -25,184 +25,13 @@
 //     the Hq/Hkv query heads of its kv head and every query tile at or after its keys;
 //     S = Q.K^T, dP = dO.V^T, dV^T += dO^T.P, dK^T += Q^T.dS.  Deterministic, no atomics.
 //   Causal workgroups run heaviest-first (the block index is the slowest grid index).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
+#include "attention_common.h"
+
+extern "C" int pto_attn_dkdv_pipe(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                                  const float* delta, void* dk, void* dv, int B, int S, int Hq, int Hkv, float c,
+                                  float scale, int causal, int variant, void* stream);
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef uint16_t bf16_t;
-// native clang vectors (HIP's u32x4 is a struct: copies of it into arrays become memcpys that
-// keep the staging arrays in scratch)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-
-constexpr int D = 128;       // head dim (the 8B / 70B Llama-3 value)
-constexpr int NDS = D / 16;  // k-steps of a d-contraction
-constexpr int NDT = D / 32;  // 32-wide output tiles along d
-constexpr int BM = 128;      // query rows per forward / dQ workgroup (32 per wave)
-constexpr int BN = 64;       // keys per K/V tile
-constexpr int BK = 128;      // keys per dK/dV workgroup (32 per wave)
-constexpr int QT = 32;       // query rows per dK/dV tile
-constexpr int NT = 256;
-constexpr int CH = D / 8;    // 16-byte chunks per row (16)
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// XOR-swizzled image of a [rows][128] bf16 tile, in 16-byte units: chunk ch of row r.
-// Row reads of 16 consecutive rows at one chunk and transposed 4-row x 16-column reads both
-// hit 64 distinct banks.
-__device__ __forceinline__ int xo(int r, int ch) { return r * CH + (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))); }
-
-__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
-  uint32_t r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
-}
-
-// registers 8s..8s+7 of an accumulator as a bf16 MFMA operand (k-step s)
-__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
-  u32x4 u;
-  u.x = pk_bf16(a[8 * s + 0], a[8 * s + 1]);
-  u.y = pk_bf16(a[8 * s + 2], a[8 * s + 3]);
-  u.z = pk_bf16(a[8 * s + 4], a[8 * s + 5]);
-  u.w = pk_bf16(a[8 * s + 6], a[8 * s + 7]);
-  return __builtin_bit_cast(bf16x8, u);
-}
-
-// operand whose k runs along the tile's COLUMNS: element j <- [row][ch*8 + j]
-__device__ __forceinline__ bf16x8 row_frag(const u32x4* tile, int row, int ch) {
-  return __builtin_bit_cast(bf16x8, tile[xo(row, ch)]);
-}
-
-__device__ __forceinline__ s16x4 tr_read(const u32x4* tile, int row, int ch, int sub_bytes) {
-  const char* p = reinterpret_cast<const char*>(tile + xo(row, ch)) + sub_bytes;
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
-}
-
-// operand whose k runs along the tile's ROWS, in the accumulator-as-operand order: element j
-// of lane half h <- row rbase + 8*(j>>2) + 4h + (j&3), column cbase + (lane & 31).
-__device__ __forceinline__ bf16x8 tr_frag(const u32x4* tile, int rbase, int cbase, int lane) {
-  const int l16 = lane & 15, q = l16 >> 2, p = l16 & 3;
-  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * p;
-  const int r0 = rbase + 4 * (lane >> 5) + q;
-  const s16x4 lo = tr_read(tile, r0, col >> 3, (col & 7) * 2);
-  const s16x4 hi = tr_read(tile, r0 + 8, col >> 3, (col & 7) * 2);
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v;
-  v.lo = lo;
-  v.hi = hi;
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-__device__ __forceinline__ float max3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-// combine a lane's value with lane ^ 32's (v_permlane32_swap: one VALU op, no LDS round trip);
-// both halves get the same result (lower half's value first)
-__device__ __forceinline__ float half_max(float x) {
-  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return max3(__uint_as_float(s[0]), __uint_as_float(s[1]), __uint_as_float(s[1]));
-}
-__device__ __forceinline__ float half_sum(float x) {
-  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
-
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-
-// key/query row index of accumulator register i in lane half h (C/D map of 32x32x16)
-__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-
-__device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
-
-// Stage a [ROWS][128] bf16 tile (rows ROWS apart in global by `stride` elements) into the
-// XOR image: each thread moves ROWS*16/NT 16-byte chunks.
-template <int ROWS, int NTH = NT>
-struct Stage {
-  static constexpr int N = ROWS * CH / NTH;
-  u32x4 r[N];
-  __device__ __forceinline__ void load(const bf16_t* base, size_t stride, int tid) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int e = tid + NTH * i, row = e / CH, ch = e % CH;
-      r[i] = *reinterpret_cast<const u32x4*>(base + (size_t)row * stride + ch * 8);
-    }
-  }
-  __device__ __forceinline__ void store(u32x4* tile, int tid) const {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int e = tid + NTH * i, row = e / CH, ch = e % CH;
-      tile[xo(row, ch)] = r[i];
-    }
-  }
-};
-
-// The same XOR image filled by LDS-DMA (global_load_lds_dwordx4: no staging registers).  A
-// wave-instruction writes 64 consecutive 16-byte slots (wave-uniform base + 16 x lane), so the
-// swizzle moves to the per-lane SOURCE address: slot j of row R holds chunk j ^ swz(R).  Wave w
-// issues pieces w, w + NW, ...  The LDS writes count on vmcnt: __syncthreads() retires them.
-template <int ROWS, int NTH>
-__device__ __forceinline__ void glds_tile(const bf16_t* base, size_t stride, u32x4* tile, int tid) {
-  constexpr int NP = ROWS * CH / 64, NW = NTH / 64;
-  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  static_assert(NP % NW == 0, "whole pieces per wave");
-#pragma unroll
-  for (int i = 0; i < NP / NW; ++i) {
-    const int p = w + NW * i;
-    const int e = 64 * p + lane, row = e / CH, j = e % CH;
-    const int ch = j ^ (((row & 3) << 2) | ((row >> 2) & 3));
-    __builtin_amdgcn_global_load_lds(base + (size_t)row * stride + ch * 8,
-                                     (__attribute__((address_space(3))) void*)(tile + 64 * p), 16, 0, 0);
-  }
-}
-
-// Write a wave's 32 x 128 transposed accumulator (acc[dt] reg i = [d = dt*32 + acc_row(i,h)]
-// [col = lane & 31]) as rows [col][d] bf16 to global via the wave's LDS region (8 KB).
-__device__ __forceinline__ void store_rows_T(const f32x16 (&acc)[NDT], float scale, u32x4* stage, int lane,
-                                             bf16_t* out, size_t row_stride) {
-  const int c = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d0 = dt * 32 + 8 * g + 4 * h;
-      u32x2 w;
-      w.x = pk_bf16(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
-      w.y = pk_bf16(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
-      *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(stage + xo(c, d0 >> 3)) + (d0 & 7) * 2) = w;
-    }
-  __syncthreads();  // every wave calls this together (after its tile loop)
-#pragma unroll
-  for (int i = 0; i < 32 * CH / 64; ++i) {
-    const int e = lane + 64 * i, row = e / CH, ch = e % CH;
-    *reinterpret_cast<u32x4*>(out + (size_t)row * row_stride + ch * 8) = stage[xo(row, ch)];
-  }
-}
-
-// Forward / dQ workgroup -> (query block, batch, q head, kv head).  The query block is the
-// slowest index of the launch order, heaviest (last) block first under the causal mask, so
-// the light blocks fill in behind the heavy ones across the whole grid.
-__device__ __forceinline__ void block_coords(int S, int B, int Hq, int Hkv, int causal, int& qblk, int& b, int& hq,
-                                             int& hk) {
-  const int nqb = S / BM, qi = (int)blockIdx.x / (B * Hq), bh = (int)blockIdx.x % (B * Hq);
-  qblk = causal ? nqb - 1 - qi : qi;
-  b = bh / Hq;
-  hq = bh % Hq;
-  hk = hq / (Hq / Hkv);
-}
 
 // ------------------------------------------------------------------------------- forward
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
@@ -1037,6 +866,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(
 // Q / dO tiles arrive by LDS-DMA (no staging registers, no per-tile store address math), the
 // causal mask is a uniform branch taken on diagonal tiles only, and waves skip the query
 // tiles wholly above their keys.
+template <bool ASM_DMA>
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv2_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -1067,15 +897,22 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv2_kernel(
   auto fetch = [&](int t, int buf) {
     const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
     const size_t off = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
-    glds_tile<QT, NT>(q + off, qstride, qd[buf], tid);
-    glds_tile<QT, NT>(dout + off, qstride, qd[buf] + QT * CH, tid);
+    if constexpr (ASM_DMA) {
+      glds_tile_asm<QT, NT>(q + off, qstride, qd[buf], tid);
+      glds_tile_asm<QT, NT>(dout + off, qstride, qd[buf] + QT * CH, tid);
+    } else {
+      glds_tile<QT, NT>(q + off, qstride, qd[buf], tid);
+      glds_tile<QT, NT>(dout + off, qstride, qd[buf] + QT * CH, tid);
+    }
     if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
       const size_t srow = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
       const float* src = (lane < 32 ? lse2 : delta) + srow + (lane & 31);
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)stat[buf], 4, 0, 0);
+      if constexpr (ASM_DMA) glds_dword_asm(src, stat[buf]);
+      else __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)stat[buf], 4, 0, 0);
     }
   };
   fetch(0, 0);
+  if constexpr (ASM_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   f32x16 dka[NDT], dva[NDT];
@@ -1157,6 +994,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv2_kernel(
         for (int dt = 0; dt < NDT; ++dt) dka[dt] = mfma(tq[dt], db, dka[dt]);
       }
     }
+    if constexpr (ASM_DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1 landed
     __syncthreads();
   }
   const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
@@ -1580,16 +1418,19 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // with the ping-pong forward, 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
-// dK/dV pass: 4 = lean-register 4-wave with LDS-DMA staging (default), 1 = the plain 4-wave
-// one (equal within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-pipelined 4-wave
-// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower), 6 = split into a dV
-// pass and a dK pass of two waves per SIMD each (round-4 A/B); PTO_ATTN_DKDV or
-// pto_attn_set_dkdv_variant()
+// dK/dV pass: 7 = lean-register 4-wave with LDS-DMA staging issued from inline asm (default:
+// 429 vs 487 us, profiles/r4_attn_dkdv_asm_dma_ab.json), 4 = the same with the builtin DMA (the
+// compiler waits for the next tile's prefetch before each tile's first LDS read), 1 = the plain
+// 4-wave one (equal to 4 within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-
+// pipelined 4-wave (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower),
+// 6 = split into a dV pass and a dK pass of two waves per SIMD each (slower, round-4 A/B),
+// 8 = software-pipelined across query tiles with AGPR-pinned accumulators
+// (attention_bwd_pipe.hip); PTO_ATTN_DKDV or pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
   if (g_dkdv_variant < 0) {
     const char* e = getenv("PTO_ATTN_DKDV");
-    g_dkdv_variant = e != nullptr ? atoi(e) : 4;
+    g_dkdv_variant = e != nullptr ? atoi(e) : 7;
   }
   return g_dkdv_variant;
 }
@@ -1614,7 +1455,7 @@ extern "C" {
 
 int pto_attn_set_dkdv_variant(int v) {
   const int old = dkdv_variant();
-  if ((v >= 1 && v <= 4) || v == 6) g_dkdv_variant = v;
+  if ((v >= 1 && v <= 4) || (v >= 6 && v <= 8)) g_dkdv_variant = v;
   return old;
 }
 
@@ -1676,8 +1517,13 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
                        (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                        (const bf16_t*)dout, lse2, (const float*)delta, (bf16_t*)dk, B, S, Hq, Hkv, c, scale,
                        causal);
+  } else if (dkdv_variant() == 8) {
+    const int rc = pto_attn_dkdv_pipe(q, k, v, dout, lse2, delta, dk, dv, B, S, Hq, Hkv, c, scale, causal,
+                                      dkdv_variant(), stream);
+    if (rc != 0) return rc;
   } else
-    hipLaunchKernelGGL(dkdv_variant() == 4   ? attn_bwd_dkdv2_kernel
+    hipLaunchKernelGGL(dkdv_variant() == 7   ? attn_bwd_dkdv2_kernel<true>
+                       : dkdv_variant() == 4 ? attn_bwd_dkdv2_kernel<false>
                        : dkdv_variant() == 2 ? attn_bwd_dkdv_p_kernel
                                              : attn_bwd_dkdv_kernel,
                        dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,

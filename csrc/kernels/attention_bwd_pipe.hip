@@ -1,0 +1,307 @@
+// Flash-attention backward, dK/dV pass, software-pipelined across query tiles (dK/dV variant 8
+// of attention.hip's pto_attn_bwd).  Its own translation unit: its dK / dV accumulators are
+// pinned in AGPRs by hand-written MFMAs (below), and everything the compiler allocates fits the
+// 256 architectural VGPRs.
+#include "attention_common.h"
+
+namespace {
+
+// dK / dV accumulators pinned in AGPRs a0-a127 (dV^T tile dt in a[16dt..], dK^T tile dt in
+// a[64 + 16dt..]): only these asm MFMAs touch them, so the compiler neither copies them between
+// register files nor counts them against the 256 VGPRs its own values share.  Every statement
+// clobbers all 128 so nothing of the compiler's is kept there (checked in the ISA: no compiler
+// v_accvgpr_* in the kernel).  Hazards: the accumulate chains are MFMA -> MFMA (C = previous D:
+// none); a VALU-written operand is padded with `s_nop 1` where it can be fresh (PAD); the
+// epilogue waits out the last MFMA before reading (acc_read).
+#define PTO_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127"
+template <int A0, bool PAD>
+__device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
+  if constexpr (PAD)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
+                 :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
+                 :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
+}
+// tile `slot` (0-3 dV^T, 4-7 dK^T); a constant after unrolling, so the switch folds away
+__device__ __forceinline__ void mfma_acc_slot(int slot, const bf16x8& a, const bf16x8& b) {
+  switch (slot) {
+    case 0: mfma_acc<0, true>(a, b); break;
+    case 1: mfma_acc<16, false>(a, b); break;
+    case 2: mfma_acc<32, false>(a, b); break;
+    case 3: mfma_acc<48, false>(a, b); break;
+    case 4: mfma_acc<64, true>(a, b); break;
+    case 5: mfma_acc<80, false>(a, b); break;
+    case 6: mfma_acc<96, false>(a, b); break;
+    default: mfma_acc<112, false>(a, b); break;
+  }
+}
+__device__ __forceinline__ void acc_zero() {
+  asm volatile("v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\tv_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\tv_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\tv_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\tv_accvgpr_write_b32 a16, 0\n\tv_accvgpr_write_b32 a17, 0\n\tv_accvgpr_write_b32 a18, 0\n\tv_accvgpr_write_b32 a19, 0\n\tv_accvgpr_write_b32 a20, 0\n\tv_accvgpr_write_b32 a21, 0\n\tv_accvgpr_write_b32 a22, 0\n\tv_accvgpr_write_b32 a23, 0\n\tv_accvgpr_write_b32 a24, 0\n\tv_accvgpr_write_b32 a25, 0\n\tv_accvgpr_write_b32 a26, 0\n\tv_accvgpr_write_b32 a27, 0\n\tv_accvgpr_write_b32 a28, 0\n\tv_accvgpr_write_b32 a29, 0\n\tv_accvgpr_write_b32 a30, 0\n\tv_accvgpr_write_b32 a31, 0\n\tv_accvgpr_write_b32 a32, 0\n\tv_accvgpr_write_b32 a33, 0\n\tv_accvgpr_write_b32 a34, 0\n\tv_accvgpr_write_b32 a35, 0\n\tv_accvgpr_write_b32 a36, 0\n\tv_accvgpr_write_b32 a37, 0\n\tv_accvgpr_write_b32 a38, 0\n\tv_accvgpr_write_b32 a39, 0\n\tv_accvgpr_write_b32 a40, 0\n\tv_accvgpr_write_b32 a41, 0\n\tv_accvgpr_write_b32 a42, 0\n\tv_accvgpr_write_b32 a43, 0\n\tv_accvgpr_write_b32 a44, 0\n\tv_accvgpr_write_b32 a45, 0\n\tv_accvgpr_write_b32 a46, 0\n\tv_accvgpr_write_b32 a47, 0\n\tv_accvgpr_write_b32 a48, 0\n\tv_accvgpr_write_b32 a49, 0\n\tv_accvgpr_write_b32 a50, 0\n\tv_accvgpr_write_b32 a51, 0\n\tv_accvgpr_write_b32 a52, 0\n\tv_accvgpr_write_b32 a53, 0\n\tv_accvgpr_write_b32 a54, 0\n\tv_accvgpr_write_b32 a55, 0\n\tv_accvgpr_write_b32 a56, 0\n\tv_accvgpr_write_b32 a57, 0\n\tv_accvgpr_write_b32 a58, 0\n\tv_accvgpr_write_b32 a59, 0\n\tv_accvgpr_write_b32 a60, 0\n\tv_accvgpr_write_b32 a61, 0\n\tv_accvgpr_write_b32 a62, 0\n\tv_accvgpr_write_b32 a63, 0\n\tv_accvgpr_write_b32 a64, 0\n\tv_accvgpr_write_b32 a65, 0\n\tv_accvgpr_write_b32 a66, 0\n\tv_accvgpr_write_b32 a67, 0\n\tv_accvgpr_write_b32 a68, 0\n\tv_accvgpr_write_b32 a69, 0\n\tv_accvgpr_write_b32 a70, 0\n\tv_accvgpr_write_b32 a71, 0\n\tv_accvgpr_write_b32 a72, 0\n\tv_accvgpr_write_b32 a73, 0\n\tv_accvgpr_write_b32 a74, 0\n\tv_accvgpr_write_b32 a75, 0\n\tv_accvgpr_write_b32 a76, 0\n\tv_accvgpr_write_b32 a77, 0\n\tv_accvgpr_write_b32 a78, 0\n\tv_accvgpr_write_b32 a79, 0\n\tv_accvgpr_write_b32 a80, 0\n\tv_accvgpr_write_b32 a81, 0\n\tv_accvgpr_write_b32 a82, 0\n\tv_accvgpr_write_b32 a83, 0\n\tv_accvgpr_write_b32 a84, 0\n\tv_accvgpr_write_b32 a85, 0\n\tv_accvgpr_write_b32 a86, 0\n\tv_accvgpr_write_b32 a87, 0\n\tv_accvgpr_write_b32 a88, 0\n\tv_accvgpr_write_b32 a89, 0\n\tv_accvgpr_write_b32 a90, 0\n\tv_accvgpr_write_b32 a91, 0\n\tv_accvgpr_write_b32 a92, 0\n\tv_accvgpr_write_b32 a93, 0\n\tv_accvgpr_write_b32 a94, 0\n\tv_accvgpr_write_b32 a95, 0\n\tv_accvgpr_write_b32 a96, 0\n\tv_accvgpr_write_b32 a97, 0\n\tv_accvgpr_write_b32 a98, 0\n\tv_accvgpr_write_b32 a99, 0\n\tv_accvgpr_write_b32 a100, 0\n\tv_accvgpr_write_b32 a101, 0\n\tv_accvgpr_write_b32 a102, 0\n\tv_accvgpr_write_b32 a103, 0\n\tv_accvgpr_write_b32 a104, 0\n\tv_accvgpr_write_b32 a105, 0\n\tv_accvgpr_write_b32 a106, 0\n\tv_accvgpr_write_b32 a107, 0\n\tv_accvgpr_write_b32 a108, 0\n\tv_accvgpr_write_b32 a109, 0\n\tv_accvgpr_write_b32 a110, 0\n\tv_accvgpr_write_b32 a111, 0\n\tv_accvgpr_write_b32 a112, 0\n\tv_accvgpr_write_b32 a113, 0\n\tv_accvgpr_write_b32 a114, 0\n\tv_accvgpr_write_b32 a115, 0\n\tv_accvgpr_write_b32 a116, 0\n\tv_accvgpr_write_b32 a117, 0\n\tv_accvgpr_write_b32 a118, 0\n\tv_accvgpr_write_b32 a119, 0\n\tv_accvgpr_write_b32 a120, 0\n\tv_accvgpr_write_b32 a121, 0\n\tv_accvgpr_write_b32 a122, 0\n\tv_accvgpr_write_b32 a123, 0\n\tv_accvgpr_write_b32 a124, 0\n\tv_accvgpr_write_b32 a125, 0\n\tv_accvgpr_write_b32 a126, 0\n\tv_accvgpr_write_b32 a127, 0" ::: PTO_AGPR_CLOBBERS);
+}
+// accumulator tile A0 (16 AGPRs) -> registers, after the last MFMA into it has drained
+template <int A0>
+__device__ __forceinline__ f32x16 acc_read() {
+  f32x16 x;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float f;
+    asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(f) : "i"(A0 + i));
+    x[i] = f;
+  }
+  return x;
+}
+
+// ------------------------------------- backward pass 2, software-pipelined across query tiles
+// attn_bwd_dkdv2_kernel (attention.hip) runs one wave per SIMD and issues in order, so a tile's
+// phases serialize: S MFMAs, dP MFMAs, ~100 VALU instructions (exp2, dS, bf16 packing) with the
+// matrix pipe idle, then the dV / dK MFMAs -- and an MFMA chain holds the wave for its whole
+// length, so nothing placed after it overlaps it (26.5 % MFMA busy, profiles/r3_pmc_digest.md).
+// Here a tile is 32 MFMA gaps, each one MFMA plus about five independent fillers (at most one
+// v_exp; MI355X_MICROARCH.md, constants table), and the iteration also computes S for the next
+// tile (its Q tile is prefetched two ahead, three LDS buffers):
+//   gaps  0-7   dP_t          P_t = exp2(S_t c - lse2), one element per gap; dO_t rows 4-7
+//   gaps  8-15  S_{t+1}       the rest of P_t; Q_{t+1} rows read in gaps 4-7
+//   gaps 16-23  dV_t          dS_t = P_t (dP_t - delta); dO_t^T transposed reads (gaps 12-19)
+//   gaps 24-31  dK_t          Q_t^T reads (20-27); tile t+2's LDS-DMA (24-28); tile t+1's
+//                             dO rows 0-3, lse2 and causal lane masks
+// Every operand is read four gaps ahead of its MFMA; every gap ends in a sched_barrier.  The
+// loop is unrolled over the three buffers, so each LDS read is a per-lane offset plus an
+// immediate and S_t / S_{t+1} rotate through three register sets with no copies.  The
+// end-of-tile wait is counted (vmcnt(5): the tile needed next has landed, the one after may
+// still fly).  Per-element operations and their order match attn_bwd_dkdv2_kernel:
+// bit-identical dK, dV.
+__global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
+    bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
+  constexpr int NB = 3, TILE = 2 * QT * CH;
+  __shared__ u32x4 qd[NB * TILE];                   // [buf][Q | dO] (48 KB); dK/dV epilogue
+  __shared__ __align__(16) float stat[NB][2 * QT];  // [buf][lse2 | delta]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
+  const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
+  const int k0w = kblk * BK + w * 32, kme = k0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 kf[NDS], vf[NDS];
+  {
+    const size_t off = ((size_t)b * S + kme) * kvstride + (size_t)hk * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(k + off + 16 * s));
+      vf[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(v + off + 16 * s));
+    }
+  }
+  const int qt0 = causal ? (kblk * BK) / QT : 0;
+  const int nqt = S / QT - qt0;
+  const int ntiles = G * nqt;
+  const int wskip = causal ? wu : 0;  // first live tile of a head: qt0 + w
+
+  // LDS-DMA: piece k of a tile (k = 0, 1: Q rows; 2, 3: dO rows; 4: lse2 | delta).  Each wave
+  // moves pieces w and w + 4 of the 8 per [QT][D] tile; every wave also issues the statistics
+  // piece (the same 256 bytes), so all waves count the same five loads per tile.
+  uint32_t doff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = 64 * (w + 4 * i) + lane, row = e / CH, j = e % CH;
+    doff[i] = (uint32_t)(row * qstride) + 8 * (j ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  }
+  const float* sbase = (lane < 32 ? lse2 : delta) + (lane & 31);
+  auto tile_off = [&](int t, size_t& toff, size_t& soff) {  // scalar: tile t's Q/dO and stat offsets
+    t = t < ntiles ? t : ntiles - 1;  // past the end: refetch the last tile into a dead buffer
+    const int g = t / nqt, qt = qt0 + t % nqt, hq = hk * G + g;
+    toff = ((size_t)b * S + (size_t)qt * QT) * qstride + (size_t)hq * D;
+    soff = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
+  };
+  const unsigned lds_w = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(qd + 64 * wu));  // this wave's piece 0
+  auto dma = [&](int buf, int piece, size_t toff, size_t soff) {
+    if (piece < 4) {
+      const int i = piece & 1;
+      const bf16_t* src = (piece < 2 ? q : dout) + toff + doff[i];
+      const unsigned dst = lds_w + 16u * (buf * TILE + (piece < 2 ? 0 : QT * CH) + 64 * 4 * i);
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                   :: "s"(dst), "v"(src) : "memory", "m0");
+    } else {
+      glds_dword_asm(sbase + soff, stat[buf]);
+    }
+  };
+
+  // loop-carried: S of the current tile (one of three rotating sets), dO rows 0-3 and lse2 rows
+  // 0-3 of the current tile, and its causal mask as 16 lane masks (SGPR pairs; element i of a
+  // lane is masked where (i&3) + 8(i>>2) < lim: one v_cndmask per element, the compares in
+  // the previous tile's last gaps)
+  uint64_t mk[16];
+  f32x16 s0 = zero16(), s1 = zero16(), s2 = zero16();
+  bf16x8 da[NDS];
+  float4 L4[4], D4[4];
+
+  acc_zero();
+
+  // one tile in buffer CUR: consumes sin (S_t), produces sout (S_{t+1} from buffer CUR + 1),
+  // DMAs tile t + 2 into buffer CUR + 2
+  auto step = [&](auto curc, f32x16& sin, f32x16& sout, int lim_next, size_t toff2, size_t soff2) {
+    constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
+    const u32x4* Qs = qd + CUR * TILE;
+    const u32x4* Ds = Qs + QT * CH;
+    const u32x4* Qn = qd + NXT * TILE;
+    const u32x4* Dn = Qn + QT * CH;
+    const float* st = stat[CUR];
+    const float* stn = stat[NXT];
+    f32x16 pa = zero16();
+    sout = zero16();
+    bf16x8 qa[NDS], td[8], tq[8], pb[2], db[2];
+    uint32_t pw[8], dw[8];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      // ---- the gap's MFMA
+      if (j < 8) {
+        pa = mfma(da[j], vf[j], pa);
+      } else if (j < 16) {
+        sout = mfma(qa[j - 8], kf[j - 8], sout);
+      } else if (j < 24) {  // dV^T tile (j & 3) += dO^T . P
+        mfma_acc_slot(j & 3, td[j - 16], pb[(j - 16) >> 2]);
+      } else {               // dK^T tile (j & 3) += Q^T . dS
+        mfma_acc_slot(4 + (j & 3), tq[j - 24], db[(j - 24) >> 2]);
+      }
+      // ---- VALU: P_t (gaps 0-15), dS_t (16-23)
+      if (j < 16) {
+        const float4 l4 = L4[j >> 2];
+        const int e = j & 3;
+        const float Lv = e == 0 ? l4.x : e == 1 ? l4.y : e == 2 ? l4.z : l4.w;
+        float p = __builtin_amdgcn_exp2f(fmaf(sin[j], c, -Lv));
+        asm("v_cndmask_b32_e64 %0, %1, 0, %2" : "=v"(p) : "v"(p), "s"(mk[j]));  // key > query: 0
+        sin[j] = p;
+        if (j & 1) pw[j >> 1] = pk_bf16(sin[j - 1], sin[j]);
+        if (j == 7 || j == 15) {
+          const int s = j >> 3;
+          u32x4 u = {pw[4 * s], pw[4 * s + 1], pw[4 * s + 2], pw[4 * s + 3]};
+          pb[s] = __builtin_bit_cast(bf16x8, u);
+        }
+      } else if (j < 24) {
+        const int m = j - 16;
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const int i = 2 * m + e2, ei = i & 3;
+          const float4 d4 = D4[i >> 2];
+          const float Dv = ei == 0 ? d4.x : ei == 1 ? d4.y : ei == 2 ? d4.z : d4.w;
+          pa[i] = sin[i] * (pa[i] - Dv);
+        }
+        dw[m] = pk_bf16(pa[2 * m], pa[2 * m + 1]);
+        if (m == 3 || m == 7) {
+          const int s = m >> 2;
+          u32x4 u = {dw[4 * s], dw[4 * s + 1], dw[4 * s + 2], dw[4 * s + 3]};
+          db[s] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+      // ---- LDS reads, four gaps ahead of their consumer
+      if (j < 4) da[4 + j] = row_frag(Ds, r, 2 * (4 + j) + h);
+      if (j == 0 || j == 4 || j == 8) L4[(j >> 2) + 1] = *reinterpret_cast<const float4*>(st + 8 * ((j >> 2) + 1) + 4 * h);
+      if (j >= 4 && j < 8) {
+        qa[2 * (j - 4)] = row_frag(Qn, r, 4 * (j - 4) + h);
+        qa[2 * (j - 4) + 1] = row_frag(Qn, r, 4 * (j - 4) + 2 + h);
+      }
+      if (j >= 12 && j < 20) td[j - 12] = tr_frag(Ds, 16 * ((j - 12) >> 2), ((j - 12) & 3) * 32, lane);
+      if (j == 12 || j == 14 || j == 16 || j == 18)
+        D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + QT + 8 * ((j - 12) >> 1) + 4 * h);
+      if (j >= 20 && j < 28) tq[j - 20] = tr_frag(Qs, 16 * ((j - 20) >> 2), ((j - 20) & 3) * 32, lane);
+      if (j >= 28) {
+        da[j - 28] = row_frag(Dn, r, 2 * (j - 28) + h);
+        if (j == 28) L4[0] = *reinterpret_cast<const float4*>(stn + 4 * h);
+      }
+      // ---- tile t + 1's causal lane masks (this tile's were last read in gap 15)
+      if (j >= 24) {
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const int i = 2 * (j - 24) + e2;
+          mk[i] = __builtin_amdgcn_ballot_w64((i & 3) + 8 * (i >> 2) < lim_next);
+        }
+      }
+      // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier)
+      if (j >= 24 && j < 29) dma(NN, j - 24, toff2, soff2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  std::integral_constant<int, 0> B0;
+  std::integral_constant<int, 1> B1;
+  std::integral_constant<int, 2> B2;
+
+  // prologue: tiles 0 and 1 in flight, then S_0 and the loop-carried operands of tile 0
+  {
+    size_t toff, soff;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      tile_off(t, toff, soff);
+#pragma unroll
+      for (int pc = 0; pc < 5; ++pc) dma(t, pc, toff, soff);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const u32x4* Qs = qd;
+    bf16x8 qa[NDS];
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) qa[s] = row_frag(Qs, r, 2 * s + h);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) da[s] = row_frag(Qs + QT * CH, r, 2 * s + h);
+    L4[0] = *reinterpret_cast<const float4*>(stat[0] + 4 * h);
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) s0 = mfma(qa[s], kf[s], s0);
+  }
+  auto lim_of = [&](int t) {  // mask P where (i&3) + 8(i>>2) < lim
+    const int qtl = t % nqt;
+    return !causal || qtl > wskip ? 0 : qtl < wskip ? QT : kme - (qt0 + qtl) * QT - 4 * h;
+  };
+
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mk[i] = __builtin_amdgcn_ballot_w64((i & 3) + 8 * (i >> 2) < lim_of(0));
+  auto tile_end = [&]() {
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // tile t + 1 landed (t + 2 may fly)
+    __syncthreads();
+  };
+  for (int t = 0;;) {
+    size_t toff, soff;
+    tile_off(t + 2, toff, soff);
+    step(B0, s0, s1, lim_of(t + 1), toff, soff);
+    tile_end();
+    if (++t == ntiles) break;
+    tile_off(t + 2, toff, soff);
+    step(B1, s1, s2, lim_of(t + 1), toff, soff);
+    tile_end();
+    if (++t == ntiles) break;
+    tile_off(t + 2, toff, soff);
+    step(B2, s2, s0, lim_of(t + 1), toff, soff);
+    tile_end();
+    if (++t == ntiles) break;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped refetches, before the epilogue
+  __syncthreads();                                   // reuses buffers 0-1
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA drained
+  f32x16 acc[NDT];
+  acc[0] = acc_read<0>();
+  acc[1] = acc_read<16>();
+  acc[2] = acc_read<32>();
+  acc[3] = acc_read<48>();
+  const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+  store_rows_T(acc, 1.f, qd + w * 32 * CH, lane, dv + off, kvstride);
+  __syncthreads();
+  acc[0] = acc_read<64>();
+  acc[1] = acc_read<80>();
+  acc[2] = acc_read<96>();
+  acc[3] = acc_read<112>();
+  store_rows_T(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
+}
+
+}  // namespace
+
+extern "C" int pto_attn_dkdv_pipe(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
+                                  const float* delta, void* dk, void* dv, int B, int S, int Hq, int Hkv, float c,
+                                  float scale, int causal, int variant, void* stream) {
+  if (S % BK != 0 || S % QT != 0 || Hq % Hkv != 0) return -1;
+  (void)variant;
+  hipLaunchKernelGGL(attn_bwd_dkdv_pipe_kernel, dim3((S / BK) * B * Hkv), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse2, delta,
+                     (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

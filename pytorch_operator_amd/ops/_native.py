@@ -47,7 +47,10 @@ def _sources():
 # kernels need more than the 256 architectural VGPRs, and with the default (AGPR-form)
 # accumulators the compiler moved them between AGPRs and VGPRs every tile (298 v_accvgpr_read +
 # 261 v_accvgpr_write in the kernel against 31 + 22 with VGPR form).
-_FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# attention_bwd_pipe.hip: VGPR form as well; its dK/dV accumulators are pinned in AGPRs by its
+# own asm MFMAs, so the compiler's MFMAs (S, dP) write VGPRs that the VALU reads directly.
+_FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+               "attention_bwd_pipe.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _source_digest() -> str:

@@ -134,7 +134,7 @@ def test_flash_forward_variants_agree(fwd_variant, shape):
     assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
 
 
-@pytest.mark.parametrize("dkdv", [1, 2, 3, 4, 6])
+@pytest.mark.parametrize("dkdv", [1, 2, 3, 4, 6, 7, 8])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_backward_dkdv_variants(dkdv, causal):
     """The dK/dV passes -- plain 4-wave, software-pipelined 4-wave (3-deep Q/dO ring: 1-5 tiles
@@ -196,8 +196,9 @@ def test_flash_rejects_unsupported_shape_on_gpu():
 
 @pytest.mark.parametrize("causal", [True, False])
 def test_split_dkdv_passes_bit_identical(causal):
-    """Variant 6 (a dV pass and a dK pass, two waves per SIMD each) runs the lean dK/dV pass's
-    per-element operation order: dK and dV bit-identical to variant 4."""
+    """Variants 6 (a dV pass and a dK pass, two waves per SIMD each), 7 (the Q / dO prefetch issued
+    from inline asm) and 8 (software-pipelined across query tiles, its own translation unit) run
+    the lean dK/dV pass's per-element operation order: dK and dV bit-identical to variant 4."""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import flash_attention
     lib = _native.load()
@@ -207,12 +208,13 @@ def test_split_dkdv_passes_bit_identical(causal):
     outs = {}
     old = lib.pto_attn_set_dkdv_variant(4)
     try:
-        for var in (4, 6):
+        for var in (4, 6, 7, 8):
             lib.pto_attn_set_dkdv_variant(var)
             xs = [x.detach().clone().requires_grad_(True) for x in (q, k, v)]
             flash_attention(*xs, causal).backward(do)
             outs[var] = [x.grad for x in xs]
     finally:
         lib.pto_attn_set_dkdv_variant(old)
-    for a, b in zip(outs[4], outs[6]):
-        assert torch.equal(a, b)
+    for var in (6, 7, 8):
+        for a, b in zip(outs[4], outs[var]):
+            assert torch.equal(a, b), var
