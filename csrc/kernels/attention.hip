@@ -1418,19 +1418,20 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // with the ping-pong forward, 4 = the 4-wave ones;
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
-// dK/dV pass: 7 = lean-register 4-wave with LDS-DMA staging issued from inline asm (default:
-// 429 vs 487 us, profiles/r4_attn_dkdv_asm_dma_ab.json), 4 = the same with the builtin DMA (the
-// compiler waits for the next tile's prefetch before each tile's first LDS read), 1 = the plain
-// 4-wave one (equal to 4 within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-
-// pipelined 4-wave (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower),
-// 6 = split into a dV pass and a dK pass of two waves per SIMD each (slower, round-4 A/B),
-// 8 = software-pipelined across query tiles with AGPR-pinned accumulators
-// (attention_bwd_pipe.hip); PTO_ATTN_DKDV or pto_attn_set_dkdv_variant()
+// dK/dV pass: 8 = software-pipelined across query tiles with AGPR-pinned accumulators
+// (attention_bwd_pipe.hip; default: 314 vs 429 us, profiles/r4_attn_dkdv_pipe_ab.json),
+// 7 = lean-register 4-wave with LDS-DMA staging issued from inline asm (429 vs 487 us,
+// profiles/r4_attn_dkdv_asm_dma_ab.json), 4 = the same with the builtin DMA (the compiler waits
+// for the next tile's prefetch before each tile's first LDS read), 1 = the plain 4-wave one
+// (equal to 4 within noise, profiles/r3_attn_dkdv_vgpr_ab.json), 2 = software-pipelined 4-wave
+// (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower), 6 = split into a dV
+// pass and a dK pass of two waves per SIMD each (slower, round-4 A/B); PTO_ATTN_DKDV or
+// pto_attn_set_dkdv_variant()
 int g_dkdv_variant = -1;
 int dkdv_variant() {
   if (g_dkdv_variant < 0) {
     const char* e = getenv("PTO_ATTN_DKDV");
-    g_dkdv_variant = e != nullptr ? atoi(e) : 7;
+    g_dkdv_variant = e != nullptr ? atoi(e) : 8;
   }
   return g_dkdv_variant;
 }

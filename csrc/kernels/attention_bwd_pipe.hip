@@ -39,6 +39,13 @@ __device__ __forceinline__ void mfma_acc_slot(int slot, const bf16x8& a, const b
 __device__ __forceinline__ void acc_zero() {
   asm volatile("v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\tv_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\tv_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\tv_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\tv_accvgpr_write_b32 a16, 0\n\tv_accvgpr_write_b32 a17, 0\n\tv_accvgpr_write_b32 a18, 0\n\tv_accvgpr_write_b32 a19, 0\n\tv_accvgpr_write_b32 a20, 0\n\tv_accvgpr_write_b32 a21, 0\n\tv_accvgpr_write_b32 a22, 0\n\tv_accvgpr_write_b32 a23, 0\n\tv_accvgpr_write_b32 a24, 0\n\tv_accvgpr_write_b32 a25, 0\n\tv_accvgpr_write_b32 a26, 0\n\tv_accvgpr_write_b32 a27, 0\n\tv_accvgpr_write_b32 a28, 0\n\tv_accvgpr_write_b32 a29, 0\n\tv_accvgpr_write_b32 a30, 0\n\tv_accvgpr_write_b32 a31, 0\n\tv_accvgpr_write_b32 a32, 0\n\tv_accvgpr_write_b32 a33, 0\n\tv_accvgpr_write_b32 a34, 0\n\tv_accvgpr_write_b32 a35, 0\n\tv_accvgpr_write_b32 a36, 0\n\tv_accvgpr_write_b32 a37, 0\n\tv_accvgpr_write_b32 a38, 0\n\tv_accvgpr_write_b32 a39, 0\n\tv_accvgpr_write_b32 a40, 0\n\tv_accvgpr_write_b32 a41, 0\n\tv_accvgpr_write_b32 a42, 0\n\tv_accvgpr_write_b32 a43, 0\n\tv_accvgpr_write_b32 a44, 0\n\tv_accvgpr_write_b32 a45, 0\n\tv_accvgpr_write_b32 a46, 0\n\tv_accvgpr_write_b32 a47, 0\n\tv_accvgpr_write_b32 a48, 0\n\tv_accvgpr_write_b32 a49, 0\n\tv_accvgpr_write_b32 a50, 0\n\tv_accvgpr_write_b32 a51, 0\n\tv_accvgpr_write_b32 a52, 0\n\tv_accvgpr_write_b32 a53, 0\n\tv_accvgpr_write_b32 a54, 0\n\tv_accvgpr_write_b32 a55, 0\n\tv_accvgpr_write_b32 a56, 0\n\tv_accvgpr_write_b32 a57, 0\n\tv_accvgpr_write_b32 a58, 0\n\tv_accvgpr_write_b32 a59, 0\n\tv_accvgpr_write_b32 a60, 0\n\tv_accvgpr_write_b32 a61, 0\n\tv_accvgpr_write_b32 a62, 0\n\tv_accvgpr_write_b32 a63, 0\n\tv_accvgpr_write_b32 a64, 0\n\tv_accvgpr_write_b32 a65, 0\n\tv_accvgpr_write_b32 a66, 0\n\tv_accvgpr_write_b32 a67, 0\n\tv_accvgpr_write_b32 a68, 0\n\tv_accvgpr_write_b32 a69, 0\n\tv_accvgpr_write_b32 a70, 0\n\tv_accvgpr_write_b32 a71, 0\n\tv_accvgpr_write_b32 a72, 0\n\tv_accvgpr_write_b32 a73, 0\n\tv_accvgpr_write_b32 a74, 0\n\tv_accvgpr_write_b32 a75, 0\n\tv_accvgpr_write_b32 a76, 0\n\tv_accvgpr_write_b32 a77, 0\n\tv_accvgpr_write_b32 a78, 0\n\tv_accvgpr_write_b32 a79, 0\n\tv_accvgpr_write_b32 a80, 0\n\tv_accvgpr_write_b32 a81, 0\n\tv_accvgpr_write_b32 a82, 0\n\tv_accvgpr_write_b32 a83, 0\n\tv_accvgpr_write_b32 a84, 0\n\tv_accvgpr_write_b32 a85, 0\n\tv_accvgpr_write_b32 a86, 0\n\tv_accvgpr_write_b32 a87, 0\n\tv_accvgpr_write_b32 a88, 0\n\tv_accvgpr_write_b32 a89, 0\n\tv_accvgpr_write_b32 a90, 0\n\tv_accvgpr_write_b32 a91, 0\n\tv_accvgpr_write_b32 a92, 0\n\tv_accvgpr_write_b32 a93, 0\n\tv_accvgpr_write_b32 a94, 0\n\tv_accvgpr_write_b32 a95, 0\n\tv_accvgpr_write_b32 a96, 0\n\tv_accvgpr_write_b32 a97, 0\n\tv_accvgpr_write_b32 a98, 0\n\tv_accvgpr_write_b32 a99, 0\n\tv_accvgpr_write_b32 a100, 0\n\tv_accvgpr_write_b32 a101, 0\n\tv_accvgpr_write_b32 a102, 0\n\tv_accvgpr_write_b32 a103, 0\n\tv_accvgpr_write_b32 a104, 0\n\tv_accvgpr_write_b32 a105, 0\n\tv_accvgpr_write_b32 a106, 0\n\tv_accvgpr_write_b32 a107, 0\n\tv_accvgpr_write_b32 a108, 0\n\tv_accvgpr_write_b32 a109, 0\n\tv_accvgpr_write_b32 a110, 0\n\tv_accvgpr_write_b32 a111, 0\n\tv_accvgpr_write_b32 a112, 0\n\tv_accvgpr_write_b32 a113, 0\n\tv_accvgpr_write_b32 a114, 0\n\tv_accvgpr_write_b32 a115, 0\n\tv_accvgpr_write_b32 a116, 0\n\tv_accvgpr_write_b32 a117, 0\n\tv_accvgpr_write_b32 a118, 0\n\tv_accvgpr_write_b32 a119, 0\n\tv_accvgpr_write_b32 a120, 0\n\tv_accvgpr_write_b32 a121, 0\n\tv_accvgpr_write_b32 a122, 0\n\tv_accvgpr_write_b32 a123, 0\n\tv_accvgpr_write_b32 a124, 0\n\tv_accvgpr_write_b32 a125, 0\n\tv_accvgpr_write_b32 a126, 0\n\tv_accvgpr_write_b32 a127, 0" ::: PTO_AGPR_CLOBBERS);
 }
+// two floats -> packed bf16 (v_cvt_pk_bf16_f32, RNE; compiler-visible, so no inline-asm pads)
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
 // accumulator tile A0 (16 AGPRs) -> registers, after the last MFMA into it has drained
 template <int A0>
 __device__ __forceinline__ f32x16 acc_read() {
@@ -63,13 +70,12 @@ __device__ __forceinline__ f32x16 acc_read() {
 //   gaps  0-7   dP_t          P_t = exp2(S_t c - lse2), one element per gap; dO_t rows 4-7
 //   gaps  8-15  S_{t+1}       the rest of P_t; Q_{t+1} rows read in gaps 4-7
 //   gaps 16-23  dV_t          dS_t = P_t (dP_t - delta); dO_t^T transposed reads (gaps 12-19)
-//   gaps 24-31  dK_t          Q_t^T reads (20-27); tile t+2's LDS-DMA (24-28); tile t+1's
-//                             dO rows 0-3, lse2 and causal lane masks
+//   gaps 24-31  dK_t          Q_t^T reads (20-27); tile t+1's dO rows 0-3 and lse2
+// Tile t+2's LDS-DMA goes out in gaps 8-12: iteration t+1 reads it (its S_{t+2} operands), so
+// it has to land by this iteration's closing barrier.
 // Every operand is read four gaps ahead of its MFMA; every gap ends in a sched_barrier.  The
 // loop is unrolled over the three buffers, so each LDS read is a per-lane offset plus an
-// immediate and S_t / S_{t+1} rotate through three register sets with no copies.  The
-// end-of-tile wait is counted (vmcnt(5): the tile needed next has landed, the one after may
-// still fly).  Per-element operations and their order match attn_bwd_dkdv2_kernel:
+// immediate and S_t / S_{t+1} rotate through three register sets with no copies.  Per-element operations and their order match attn_bwd_dkdv2_kernel:
 // bit-identical dK, dV.
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
@@ -130,10 +136,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   };
 
   // loop-carried: S of the current tile (one of three rotating sets), dO rows 0-3 and lse2 rows
-  // 0-3 of the current tile, and its causal mask as 16 lane masks (SGPR pairs; element i of a
-  // lane is masked where (i&3) + 8(i>>2) < lim: one v_cndmask per element, the compares in
-  // the previous tile's last gaps)
-  uint64_t mk[16];
+  // 0-3 of the current tile
   f32x16 s0 = zero16(), s1 = zero16(), s2 = zero16();
   bf16x8 da[NDS];
   float4 L4[4], D4[4];
@@ -142,8 +145,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 
   // one tile in buffer CUR: consumes sin (S_t), produces sout (S_{t+1} from buffer CUR + 1),
   // DMAs tile t + 2 into buffer CUR + 2
-  auto step = [&](auto curc, f32x16& sin, f32x16& sout, int lim_next, size_t toff2, size_t soff2) {
+  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, size_t toff2, size_t soff2) {
     constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
+    constexpr bool MASK = decltype(maskc)::value;
     const u32x4* Qs = qd + CUR * TILE;
     const u32x4* Ds = Qs + QT * CH;
     const u32x4* Qn = qd + NXT * TILE;
@@ -172,9 +176,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         const int e = j & 3;
         const float Lv = e == 0 ? l4.x : e == 1 ? l4.y : e == 2 ? l4.z : l4.w;
         float p = __builtin_amdgcn_exp2f(fmaf(sin[j], c, -Lv));
-        asm("v_cndmask_b32_e64 %0, %1, 0, %2" : "=v"(p) : "v"(p), "s"(mk[j]));  // key > query: 0
+        if (MASK && (j & 3) + 8 * (j >> 2) < lim) p = 0.f;  // key > query
         sin[j] = p;
-        if (j & 1) pw[j >> 1] = pk_bf16(sin[j - 1], sin[j]);
+        if (j & 1) pw[j >> 1] = pk2(sin[j - 1], sin[j]);
         if (j == 7 || j == 15) {
           const int s = j >> 3;
           u32x4 u = {pw[4 * s], pw[4 * s + 1], pw[4 * s + 2], pw[4 * s + 3]};
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
           const float Dv = ei == 0 ? d4.x : ei == 1 ? d4.y : ei == 2 ? d4.z : d4.w;
           pa[i] = sin[i] * (pa[i] - Dv);
         }
-        dw[m] = pk_bf16(pa[2 * m], pa[2 * m + 1]);
+        dw[m] = pk2(pa[2 * m], pa[2 * m + 1]);
         if (m == 3 || m == 7) {
           const int s = m >> 2;
           u32x4 u = {dw[4 * s], dw[4 * s + 1], dw[4 * s + 2], dw[4 * s + 3]};
@@ -211,19 +215,14 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         da[j - 28] = row_frag(Dn, r, 2 * (j - 28) + h);
         if (j == 28) L4[0] = *reinterpret_cast<const float4*>(stn + 4 * h);
       }
-      // ---- tile t + 1's causal lane masks (this tile's were last read in gap 15)
-      if (j >= 24) {
-#pragma unroll
-        for (int e2 = 0; e2 < 2; ++e2) {
-          const int i = 2 * (j - 24) + e2;
-          mk[i] = __builtin_amdgcn_ballot_w64((i & 3) + 8 * (i >> 2) < lim_next);
-        }
-      }
-      // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier)
-      if (j >= 24 && j < 29) dma(NN, j - 24, toff2, soff2);
+      // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier); it must
+      // land by this tile's closing barrier (tile t + 1 reads it), so it goes out early
+      if (j >= 8 && j < 13) dma(NN, j - 8, toff2, soff2);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  std::integral_constant<bool, true> MK;
+  std::integral_constant<bool, false> NM;
   std::integral_constant<int, 0> B0;
   std::integral_constant<int, 1> B1;
   std::integral_constant<int, 2> B2;
@@ -249,29 +248,40 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 #pragma unroll
     for (int s = 0; s < NDS; ++s) s0 = mfma(qa[s], kf[s], s0);
   }
+  // causal: a wave's diagonal tile is masked per element, the tiles wholly above its keys
+  // (t % nqt < wskip) are masked whole (they add exact zeros; wave 0, which has none, sets the
+  // block's time); every other tile runs the unmasked step
+  auto masked_of = [&](int t) { return causal && t % nqt <= wskip; };  // wave-uniform
   auto lim_of = [&](int t) {  // mask P where (i&3) + 8(i>>2) < lim
     const int qtl = t % nqt;
     return !causal || qtl > wskip ? 0 : qtl < wskip ? QT : kme - (qt0 + qtl) * QT - 4 * h;
   };
 
-#pragma unroll
-  for (int i = 0; i < 16; ++i) mk[i] = __builtin_amdgcn_ballot_w64((i & 3) + 8 * (i >> 2) < lim_of(0));
   auto tile_end = [&]() {
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // tile t + 1 landed (t + 2 may fly)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 2 landed (read from tile t + 1 on)
     __syncthreads();
   };
   for (int t = 0;;) {
     size_t toff, soff;
     tile_off(t + 2, toff, soff);
-    step(B0, s0, s1, lim_of(t + 1), toff, soff);
+    if (masked_of(t))
+      step(B0, MK, s0, s1, lim_of(t), toff, soff);
+    else
+      step(B0, NM, s0, s1, 0, toff, soff);
     tile_end();
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
-    step(B1, s1, s2, lim_of(t + 1), toff, soff);
+    if (masked_of(t))
+      step(B1, MK, s1, s2, lim_of(t), toff, soff);
+    else
+      step(B1, NM, s1, s2, 0, toff, soff);
     tile_end();
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
-    step(B2, s2, s0, lim_of(t + 1), toff, soff);
+    if (masked_of(t))
+      step(B2, MK, s2, s0, lim_of(t), toff, soff);
+    else
+      step(B2, NM, s2, s0, 0, toff, soff);
     tile_end();
     if (++t == ntiles) break;
   }

@@ -47,10 +47,12 @@ def _sources():
 # kernels need more than the 256 architectural VGPRs, and with the default (AGPR-form)
 # accumulators the compiler moved them between AGPRs and VGPRs every tile (298 v_accvgpr_read +
 # 261 v_accvgpr_write in the kernel against 31 + 22 with VGPR form).
-# attention_bwd_pipe.hip: VGPR form as well; its dK/dV accumulators are pinned in AGPRs by its
-# own asm MFMAs, so the compiler's MFMAs (S, dP) write VGPRs that the VALU reads directly.
+# attention_bwd_pipe.hip: VGPR form as well (its dK/dV accumulators are pinned in AGPRs by its
+# own asm MFMAs, so the compiler's MFMAs (S, dP) write VGPRs that the VALU reads directly), and
+# no SLP vectorisation: packed f32 VALU beside MFMAs costs more issue time than two scalar ops
+# (MI355X_MICROARCH.md, constants table).
 _FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-               "attention_bwd_pipe.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+               "attention_bwd_pipe.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _source_digest() -> str:

@@ -13,6 +13,7 @@ pids=()
 for f in csrc/kernels/*.hip; do
   n=$(basename $f .hip); [ "$n" = mnist_kernels ] && continue
   extra=""; [ "$n" = attention ] && extra="${ATTN_FLAGS--mllvm -amdgpu-mfma-vgpr-form=1}"  # as ops/_native.py
+  [ "$n" = attention_bwd_pipe ] && extra="-mllvm -amdgpu-mfma-vgpr-form=1 -fno-slp-vectorize"
   [ $OBJ/$n.o -nt $f ] || { $HIPCC $FLAGS $extra -c $f -o $OBJ/$n.o & pids+=($!); }
 done
 while [ $# -ge 2 ]; do

@@ -13,3 +13,7 @@ for rep in 1 2 3; do for v in 7 8; do
   echo "dkdv $v rep $rep: $(tail -1 $O/attn_dkdv${v}_$rep.log)"
 done; done
 PTO_ATTN_DKDV=8 PROF_TIMEOUT=200 TOP=8 bash tools/gpu/profile.sh $O/prof8 0 python3 tools/attn_bench.py --impl hip --reps 10 || exit 1
+for v in 8 7; do
+  PTO_ATTN_DKDV=$v bash tools/gpu/pmc.sh gpurun_out/r4s15/pmc$v python3 tools/attn_bench.py --impl hip --reps 5 > gpurun_out/r4s15/pmc$v.log 2>&1 || { tail -20 gpurun_out/r4s15/pmc$v.log; exit 1; }
+done
+grep -A 12 "attn_bwd" gpurun_out/r4s15/pmc8/summary.txt | head -40
