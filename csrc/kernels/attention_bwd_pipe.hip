@@ -77,6 +77,19 @@ __device__ __forceinline__ f32x16 acc_read() {
 // loop is unrolled over the three buffers, so each LDS read is a per-lane offset plus an
 // immediate and S_t / S_{t+1} rotate through three register sets with no copies.  Per-element operations and their order match attn_bwd_dkdv2_kernel:
 // bit-identical dK, dV.
+#ifdef PTO_ATTN_STAMPS
+// diagnostic build only (tools/build_exp.sh ... "-DPTO_ATTN_STAMPS"): per wave, s_memtime at
+// kernel entry, loop entry, loop exit and kernel end, plus s_memrealtime at entry / end and the
+// tile count; read back with pto_attn_pipe_stamps()
+__device__ unsigned long long g_pipe_stamps[8192 * 8];
+#define PTO_STAMP(k) \
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#define PTO_RSTAMP(k) \
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PTO_STAMP(k)
+#define PTO_RSTAMP(k)
+#endif
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -91,6 +104,8 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   const int b = bh / Hkv, hk = bh % Hkv, G = Hq / Hkv;
   const int k0w = kblk * BK + w * 32, kme = k0w + r;
   const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+  PTO_STAMP(0);
+  PTO_RSTAMP(4);
 
   bf16x8 kf[NDS], vf[NDS];
   {
@@ -261,6 +276,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 2 landed (read from tile t + 1 on)
     __syncthreads();
   };
+  PTO_STAMP(1);
   for (int t = 0;;) {
     size_t toff, soff;
     tile_off(t + 2, toff, soff);
@@ -285,6 +301,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     tile_end();
     if (++t == ntiles) break;
   }
+  PTO_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped refetches, before the epilogue
   __syncthreads();                                   // reuses buffers 0-1
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA drained
@@ -301,6 +318,11 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   acc[2] = acc_read<96>();
   acc[3] = acc_read<112>();
   store_rows_T(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
+  PTO_STAMP(3);
+  PTO_RSTAMP(5);
+#ifdef PTO_ATTN_STAMPS
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + 6] = (unsigned long long)ntiles;
+#endif
 }
 
 }  // namespace
@@ -315,3 +337,9 @@ extern "C" int pto_attn_dkdv_pipe(const void* q, const void* k, const void* v, c
                      (bf16_t*)dk, (bf16_t*)dv, B, S, Hq, Hkv, c, scale, causal);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#ifdef PTO_ATTN_STAMPS
+extern "C" int pto_attn_pipe_stamps(void* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pipe_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
