@@ -14,9 +14,12 @@ namespace {
 // none); a VALU-written operand is padded with `s_nop 1` where it can be fresh (PAD); the
 // epilogue waits out the last MFMA before reading (acc_read).
 #define PTO_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127"
+#ifndef PTO_PIPE_PAD
+#define PTO_PIPE_PAD 1
+#endif
 template <int A0, bool PAD>
 __device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
-  if constexpr (PAD)
+  if constexpr (PAD && PTO_PIPE_PAD)
     asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
                  :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
   else
@@ -81,15 +84,20 @@ __device__ __forceinline__ f32x16 acc_read() {
 // diagnostic build only (tools/build_exp.sh ... "-DPTO_ATTN_STAMPS"): per wave, s_memtime at
 // kernel entry, loop entry, loop exit and kernel end, plus s_memrealtime at entry / end and the
 // tile count; read back with pto_attn_pipe_stamps()
-__device__ unsigned long long g_pipe_stamps[8192 * 8];
+// slots 8-15: s_memtime at gaps 0, 8, 16, 24 of tile 9 and after its closing barrier
+__device__ unsigned long long g_pipe_stamps[8192 * 16];
 #define PTO_STAMP(k) \
-  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + (k)] = __builtin_amdgcn_s_memtime()
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 16 + (k)] = __builtin_amdgcn_s_memtime()
 #define PTO_RSTAMP(k) \
-  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 16 + (k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define PTO_STAMP(k)
 #define PTO_RSTAMP(k)
 #endif
+#ifndef PTO_PIPE_TLEAD
+#define PTO_PIPE_TLEAD 4
+#endif
+constexpr int TLEAD = PTO_PIPE_TLEAD;  // gaps between a transposed operand read and its MFMA
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -160,7 +168,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 
   // one tile in buffer CUR: consumes sin (S_t), produces sout (S_{t+1} from buffer CUR + 1),
   // DMAs tile t + 2 into buffer CUR + 2
-  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, size_t toff2, size_t soff2) {
+  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, size_t toff2, size_t soff2, bool stamp) {
     constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
     constexpr bool MASK = decltype(maskc)::value;
     const u32x4* Qs = qd + CUR * TILE;
@@ -175,6 +183,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     uint32_t pw[8], dw[8];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
+#ifdef PTO_ATTN_STAMPS
+      if ((j & 7) == 0 && stamp) PTO_STAMP(8 + (j >> 3));
+#endif
       // ---- the gap's MFMA
       if (j < 8) {
         pa = mfma(da[j], vf[j], pa);
@@ -185,29 +196,50 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       } else {               // dK^T tile (j & 3) += Q^T . dS
         mfma_acc_slot(4 + (j & 3), tq[j - 24], db[(j - 24) >> 2]);
       }
-      // ---- VALU: P_t (gaps 0-15), dS_t (16-23)
+      // ---- VALU, skewed so that no filler waits on another in the same gap (in-order issue:
+      // a dependent VALU op stalls the wave, and the next MFMA with it):
+      //   P_t:  fma of element j in gap j, its exp2 in gap j + 1, the pair's bf16 pack in the
+      //         gap after the pair's second exp2 (gaps 0-17)
+      //   dS_t: dP - delta of elements 2m, 2m+1 in gap 16 + m, times P in gap 17 + m, the pack
+      //         in gap 18 + m (gaps 16-25)
       if (j < 16) {
         const float4 l4 = L4[j >> 2];
         const int e = j & 3;
         const float Lv = e == 0 ? l4.x : e == 1 ? l4.y : e == 2 ? l4.z : l4.w;
-        float p = __builtin_amdgcn_exp2f(fmaf(sin[j], c, -Lv));
-        if (MASK && (j & 3) + 8 * (j >> 2) < lim) p = 0.f;  // key > query
-        sin[j] = p;
-        if (j & 1) pw[j >> 1] = pk2(sin[j - 1], sin[j]);
-        if (j == 7 || j == 15) {
-          const int s = j >> 3;
+        sin[j] = fmaf(sin[j], c, -Lv);
+      }
+      if (j >= 1 && j <= 16) {
+        const int i = j - 1;
+        float p = __builtin_amdgcn_exp2f(sin[i]);
+        if (MASK && (i & 3) + 8 * (i >> 2) < lim) p = 0.f;  // key > query
+        sin[i] = p;
+      }
+      if (j >= 3 && j <= 17 && (j & 1)) {
+        const int k2 = (j - 3) >> 1;  // pair k2 = elements 2 k2, 2 k2 + 1
+        pw[k2] = pk2(sin[2 * k2], sin[2 * k2 + 1]);
+        if (k2 == 3 || k2 == 7) {
+          const int s = k2 >> 2;
           u32x4 u = {pw[4 * s], pw[4 * s + 1], pw[4 * s + 2], pw[4 * s + 3]};
           pb[s] = __builtin_bit_cast(bf16x8, u);
         }
-      } else if (j < 24) {
+      }
+      if (j >= 16 && j < 24) {
         const int m = j - 16;
 #pragma unroll
         for (int e2 = 0; e2 < 2; ++e2) {
           const int i = 2 * m + e2, ei = i & 3;
           const float4 d4 = D4[i >> 2];
           const float Dv = ei == 0 ? d4.x : ei == 1 ? d4.y : ei == 2 ? d4.z : d4.w;
-          pa[i] = sin[i] * (pa[i] - Dv);
+          pa[i] = pa[i] - Dv;
         }
+      }
+      if (j >= 17 && j < 25) {
+        const int m = j - 17;
+        pa[2 * m] = sin[2 * m] * pa[2 * m];
+        pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
+      }
+      if (j >= 18 && j < 26) {
+        const int m = j - 18;
         dw[m] = pk2(pa[2 * m], pa[2 * m + 1]);
         if (m == 3 || m == 7) {
           const int s = m >> 2;
@@ -222,10 +254,12 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         qa[2 * (j - 4)] = row_frag(Qn, r, 4 * (j - 4) + h);
         qa[2 * (j - 4) + 1] = row_frag(Qn, r, 4 * (j - 4) + 2 + h);
       }
-      if (j >= 12 && j < 20) td[j - 12] = tr_frag(Ds, 16 * ((j - 12) >> 2), ((j - 12) & 3) * 32, lane);
+      if (j >= 16 - TLEAD && j < 24 - TLEAD)
+        td[j - 16 + TLEAD] = tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
       if (j == 12 || j == 14 || j == 16 || j == 18)
         D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + QT + 8 * ((j - 12) >> 1) + 4 * h);
-      if (j >= 20 && j < 28) tq[j - 20] = tr_frag(Qs, 16 * ((j - 20) >> 2), ((j - 20) & 3) * 32, lane);
+      if (j >= 24 - TLEAD && j < 32 - TLEAD)
+        tq[j - 24 + TLEAD] = tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
       if (j >= 28) {
         da[j - 28] = row_frag(Dn, r, 2 * (j - 28) + h);
         if (j == 28) L4[0] = *reinterpret_cast<const float4*>(stn + 4 * h);
@@ -272,33 +306,40 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     return !causal || qtl > wskip ? 0 : qtl < wskip ? QT : kme - (qt0 + qtl) * QT - 4 * h;
   };
 
-  auto tile_end = [&]() {
+  auto tile_end = [&](int t) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 2 landed (read from tile t + 1 on)
+#ifdef PTO_ATTN_STAMPS
+    if (t == 9) PTO_STAMP(12);
+#endif
     __syncthreads();
+#ifdef PTO_ATTN_STAMPS
+    if (t == 9) PTO_STAMP(13);
+#endif
+    (void)t;
   };
   PTO_STAMP(1);
   for (int t = 0;;) {
     size_t toff, soff;
     tile_off(t + 2, toff, soff);
     if (masked_of(t))
-      step(B0, MK, s0, s1, lim_of(t), toff, soff);
+      step(B0, MK, s0, s1, lim_of(t), toff, soff, t == 9);
     else
-      step(B0, NM, s0, s1, 0, toff, soff);
-    tile_end();
+      step(B0, NM, s0, s1, 0, toff, soff, t == 9);
+    tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
     if (masked_of(t))
-      step(B1, MK, s1, s2, lim_of(t), toff, soff);
+      step(B1, MK, s1, s2, lim_of(t), toff, soff, t == 9);
     else
-      step(B1, NM, s1, s2, 0, toff, soff);
-    tile_end();
+      step(B1, NM, s1, s2, 0, toff, soff, t == 9);
+    tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
     if (masked_of(t))
-      step(B2, MK, s2, s0, lim_of(t), toff, soff);
+      step(B2, MK, s2, s0, lim_of(t), toff, soff, t == 9);
     else
-      step(B2, NM, s2, s0, 0, toff, soff);
-    tile_end();
+      step(B2, NM, s2, s0, 0, toff, soff, t == 9);
+    tile_end(t);
     if (++t == ntiles) break;
   }
   PTO_STAMP(2);
@@ -321,7 +362,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   PTO_STAMP(3);
   PTO_RSTAMP(5);
 #ifdef PTO_ATTN_STAMPS
-  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 8 + 6] = (unsigned long long)ntiles;
+  if (lane == 0 && blockIdx.x < 2048) g_pipe_stamps[((size_t)blockIdx.x * 4 + w) * 16 + 6] = (unsigned long long)ntiles;
 #endif
 }
 

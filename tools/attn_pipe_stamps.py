@@ -40,10 +40,10 @@ def main():
         flash_attention(q, k, v, True).backward(do)
     torch.cuda.synchronize()
     nblk = (a.S // 128) * a.B * a.Hkv
-    n = min(nblk, 2048) * 4 * 8
+    n = min(nblk, 2048) * 4 * 16
     buf = np.zeros(n, dtype=np.uint64)
     assert fn(buf.ctypes.data, n) == 0
-    st = buf.reshape(-1, 4, 8)[: min(nblk, 2048)].astype(np.float64)
+    st = buf.reshape(-1, 4, 16)[: min(nblk, 2048)].astype(np.float64)
     t0, t1, t2, t3, r0, r1, nt = (st[..., i] for i in range(7))
     clock_mhz = float(np.median((t3 - t0) / np.maximum(r1 - r0, 1) * 100.0))
     per_tile = (t2 - t1) / np.maximum(nt, 1)
@@ -60,6 +60,14 @@ def main():
         "busy_us_sum_over_blocks": round(float(((r1 - r0)[:, 0]).sum() / 100.0), 1),
         "mfma_bound_cycles_per_tile": 32 * 32,
     }
+    # tile 9 of every wave that has one: gaps 0-7 / 8-15 / 16-23 / 24-31, the closing wait
+    # (vmcnt for the next-but-one tile's DMA) and the barrier
+    ok = nt > 10
+    ph = st[..., 8:14]
+    names = ["gaps0_7", "gaps8_15", "gaps16_23", "gaps24_31+wait", "barrier"]
+    d = [ph[..., i + 1] - ph[..., i] for i in range(4)] + [ph[..., 5] - ph[..., 4]]
+    res["tile9_phase_cycles_p50"] = {nm: round(float(np.median(x[ok])), 1) for nm, x in zip(names, d)}
+    res["tile9_phase_cycles_p90"] = {nm: round(float(np.percentile(x[ok], 90)), 1) for nm, x in zip(names, d)}
     print(json.dumps(res, indent=1))
     if a.json:
         with open(a.json, "w") as f:
