@@ -27,6 +27,9 @@
 //   Causal workgroups run heaviest-first (the block index is the slowest grid index).
 #include "attention_common.h"
 
+extern "C" int pto_attn_dq_pipe(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                const float* lse2, float* delta, void* dq, int B, int S, int Hq, int Hkv, float c,
+                                float scale, int causal, void* stream);
 extern "C" int pto_attn_dkdv_pipe(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
                                   const float* delta, void* dk, void* dv, int B, int S, int Hq, int Hkv, float c,
                                   float scale, int causal, int variant, void* stream);
@@ -1427,6 +1430,18 @@ int g_fwd_variant = -1;
 // (slower: profiles/r3_attn_v2_ab.json), 3 = 8-wave (S % 256 == 0; slower), 6 = split into a dV
 // pass and a dK pass of two waves per SIMD each (slower, round-4 A/B); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
+// dQ pass: 9 = software-pipelined across key tiles with an AGPR-pinned accumulator
+// (attention_bwd_pipe.hip), 8 = the 8-wave two-waves-per-SIMD pass (default)
+// (attn_bwd_dq8_kernel; the 4-wave attn_bwd_dq_kernel when S % 256 != 0 or the forward
+// variant is below 8); PTO_ATTN_DQ or pto_attn_set_dq_variant()
+int g_dq_variant = -1;
+int dq_variant() {
+  if (g_dq_variant < 0) {
+    const char* e = getenv("PTO_ATTN_DQ");
+    g_dq_variant = e != nullptr ? atoi(e) : 8;
+  }
+  return g_dq_variant;
+}
 int g_dkdv_variant = -1;
 int dkdv_variant() {
   if (g_dkdv_variant < 0) {
@@ -1453,6 +1468,12 @@ int check_shapes(int B, int S, int Hq, int Hkv, int Dh) {
 }  // namespace
 
 extern "C" {
+
+int pto_attn_set_dq_variant(int v) {
+  const int old = dq_variant();
+  if (v == 8 || v == 9) g_dq_variant = v;
+  return old;
+}
 
 int pto_attn_set_dkdv_variant(int v) {
   const int old = dkdv_variant();
@@ -1497,7 +1518,10 @@ int pto_attn_bwd(const void* q, const void* k, const void* v, const void* o, con
   for (const void* p : ps)
     if (!aligned16(p)) return -2;
   const float c = scale * 1.4426950408889634f;
-  if (fwd_variant() >= 8 && S % BM8 == 0)
+  if (dq_variant() == 9) {
+    const int rc = pto_attn_dq_pipe(q, k, v, o, dout, lse2, delta, dq, B, S, Hq, Hkv, c, scale, causal, stream);
+    if (rc != 0) return rc;
+  } else if (fwd_variant() >= 8 && S % BM8 == 0)
     hipLaunchKernelGGL(attn_bwd_dq8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                        (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);

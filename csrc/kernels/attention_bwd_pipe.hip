@@ -11,11 +11,12 @@ namespace {
 // register files nor counts them against the 256 VGPRs its own values share.  Every statement
 // clobbers all 128 so nothing of the compiler's is kept there (checked in the ISA: no compiler
 // v_accvgpr_* in the kernel).  Hazards: the accumulate chains are MFMA -> MFMA (C = previous D:
-// none); a VALU-written operand is padded with `s_nop 1` where it can be fresh (PAD); the
-// epilogue waits out the last MFMA before reading (acc_read).
+// none); every VALU-written operand (the bf16-packed P and dS) is packed at least two gaps
+// before the MFMA that reads it (the schedule below), so no `s_nop` pad is needed (PAD keeps
+// one for A/B); the epilogue waits out the last MFMA before reading (acc_read).
 #define PTO_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127"
-#ifndef PTO_PIPE_PAD
-#define PTO_PIPE_PAD 1
+#ifndef PTO_PIPE_PAD  // 1: s_nop 1 before the first MFMA of each k-step (8 us slower, no effect on
+#define PTO_PIPE_PAD 0  // the results: profiles/r4_attn_dkdv_pipe_knobs_ab.json)
 #endif
 template <int A0, bool PAD>
 __device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
@@ -366,6 +367,209 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 #endif
 }
 
+// ---------------------------------- backward pass 1 (dQ), software-pipelined across key tiles
+// The dQ pass in the dK/dV pipeline's form (attn_bwd_dq8_kernel, attention.hip, is the
+// two-waves-per-SIMD form it replaces): one wave per SIMD, 4 waves x 32 queries (the query on
+// the lane), key tiles of KT = 32 keys (K | V, 16 KB) shared through three LDS buffers, the dQ^T
+// accumulator pinned in AGPRs a0-a63.  A tile is 24 MFMA gaps:
+//   gaps  0-7   dP^T_t = V_t . dO^T      P_t = exp2(S^T_t c - lse2): fma gap i, exp2 gap i + 1
+//   gaps  8-15  S^T_{t+1} = K_{t+1} . Q^T     dS_t = P (dP - delta): subtract gaps 9-16, multiply
+//                                              10-17, bf16 pack 11-18
+//   gaps 16-23  dQ^T += K_t^T . dS^T_t
+// LDS reads four gaps ahead: V_t rows (gaps 20-23 of the previous tile and 0-3), K_{t+1} rows
+// (4-11), K_t^T transposed (12-19).  Tile t+2's LDS-DMA goes out in gaps 4-7 and lands by the
+// closing barrier (tile t+1 computes S^T_{t+2} from it).  lse2 and delta are per-lane scalars.
+// Block order: kv head fastest (the G query heads sharing a K/V stream sit 8 blocks apart, on
+// one XCD), heaviest causal query block first.  Per-element operations and the key order of
+// the dQ accumulation match attn_bwd_dq8_kernel: bit-identical dQ and delta.
+constexpr int KT = 32;
+__global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
+    float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, float c, float scale,
+    int causal) {
+  constexpr int NB = 3, TILE = 2 * KT * CH;
+  __shared__ u32x4 kvs[NB * TILE];  // [buf][K | V] (48 KB); dQ epilogue
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int G = Hq / Hkv, nqb = S / BM;
+  int bi = (int)blockIdx.x;
+  const int hk = bi % Hkv;
+  bi /= Hkv;
+  const int hq = hk * G + bi % G;
+  bi /= G;
+  const int b = bi % B, qi = bi / B;
+  const int qblk = causal ? nqb - 1 - qi : qi;
+  const int q0w = qblk * BM + w * 32, qme = q0w + r;
+  const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
+
+  bf16x8 qf[NDS], df[NDS];
+  float dl;
+  {
+    const size_t off = ((size_t)b * S + qme) * qstride + (size_t)hq * D + 8 * h;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) {
+      const u32x4 qq = *reinterpret_cast<const u32x4*>(q + off + 16 * s);
+      const u32x4 dd = *reinterpret_cast<const u32x4*>(dout + off + 16 * s);
+      const u32x4 oo = *reinterpret_cast<const u32x4*>(o + off + 16 * s);
+      qf[s] = __builtin_bit_cast(bf16x8, qq);
+      df[s] = __builtin_bit_cast(bf16x8, dd);
+      const uint32_t dw[4] = {dd.x, dd.y, dd.z, dd.w}, ow[4] = {oo.x, oo.y, oo.z, oo.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        part = fmaf(bf2f(dw[e] & 0xffffu), bf2f(ow[e] & 0xffffu), part);
+        part = fmaf(bf2f(dw[e] >> 16), bf2f(ow[e] >> 16), part);
+      }
+    }
+    dl = half_sum(part);
+  }
+  const size_t srow = ((size_t)b * Hq + hq) * S + qme;
+  const float lq = lse2[srow];
+  if (h == 0) delta[srow] = dl;
+
+  const int ntiles = causal ? (qblk * BM + BM) / KT : S / KT;
+  const int tdiag = q0w / KT;  // causal: this wave's diagonal tile; later tiles are masked whole
+
+  // LDS-DMA: piece k of a tile (k = 0, 1: K rows; 2, 3: V rows), pieces w and w + 4 of the 8 per
+  // [KT][D] image for wave w
+  uint32_t doff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = 64 * (w + 4 * i) + lane, row = e / CH, j = e % CH;
+    doff[i] = (uint32_t)(row * kvstride) + 8 * (j ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  }
+  const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
+  const bf16_t* vb = v + (size_t)b * S * kvstride + (size_t)hk * D;
+  const unsigned lds_w = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(kvs + 64 * wu));
+  auto dma = [&](int buf, int piece, int t) {
+    t = t < ntiles ? t : ntiles - 1;  // past the end: refetch the last tile into a dead buffer
+    const int i = piece & 1;
+    const bf16_t* src = (piece < 2 ? kb : vb) + (size_t)t * KT * kvstride + doff[i];
+    const unsigned dst = lds_w + 16u * (buf * TILE + (piece < 2 ? 0 : KT * CH) + 64 * 4 * i);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                 :: "s"(dst), "v"(src) : "memory", "m0");
+  };
+
+  // loop-carried: S^T of the current tile (rotating sets) and V rows 0-3 of the current tile
+  f32x16 s0 = zero16(), s1 = zero16(), s2 = zero16();
+  bf16x8 va[NDS];
+  acc_zero();
+
+  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, int t2) {
+    constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
+    constexpr bool MASK = decltype(maskc)::value;
+    const u32x4* Ks = kvs + CUR * TILE;
+    const u32x4* Vs = Ks + KT * CH;
+    const u32x4* Kn = kvs + NXT * TILE;
+    const u32x4* Vn = Kn + KT * CH;
+    f32x16 pa = zero16();
+    sout = zero16();
+    bf16x8 ka[NDS], kt[8], db[2];
+    uint32_t dw[8];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      // ---- the gap's MFMA
+      if (j < 8) {
+        pa = mfma(va[j], df[j], pa);
+      } else if (j < 16) {
+        sout = mfma(ka[j - 8], qf[j - 8], sout);
+      } else {  // dQ^T tile (j & 3) += K^T . dS^T, k-step (j - 16) >> 2
+        mfma_acc_slot(j & 3, kt[j - 16], db[(j - 16) >> 2]);
+      }
+      // ---- VALU (no filler depends on another in the same gap)
+      if (j < 16) {  // (opaque first: lse2 is loop-invariant, and the compiler would otherwise
+                     // hoist all 16 fma into the tile's first gap)
+        asm volatile("" : "+v"(sin[j]));
+        sin[j] = fmaf(sin[j], c, -lq);
+      }
+      if (j >= 1 && j <= 16) {
+        const int i = j - 1;
+        float p = __builtin_amdgcn_exp2f(sin[i]);
+        if (MASK && (i & 3) + 8 * (i >> 2) > lim) p = 0.f;  // key > query
+        sin[i] = p;
+      }
+      if (j >= 9 && j < 17) {
+        const int m = j - 9;
+        pa[2 * m] = pa[2 * m] - dl;
+        pa[2 * m + 1] = pa[2 * m + 1] - dl;
+      }
+      if (j >= 10 && j < 18) {
+        const int m = j - 10;
+        pa[2 * m] = sin[2 * m] * pa[2 * m];
+        pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
+      }
+      if (j >= 11 && j < 19) {
+        const int m = j - 11;
+        dw[m] = pk2(pa[2 * m], pa[2 * m + 1]);
+        if (m == 3 || m == 7) {
+          const int s = m >> 2;
+          u32x4 u = {dw[4 * s], dw[4 * s + 1], dw[4 * s + 2], dw[4 * s + 3]};
+          db[s] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+      // ---- LDS reads, four gaps ahead of their MFMA
+      if (j < 4) va[4 + j] = row_frag(Vs, r, 2 * (4 + j) + h);
+      if (j >= 4 && j < 12) ka[j - 4] = row_frag(Kn, r, 2 * (j - 4) + h);
+      if (j >= 12 && j < 20) kt[j - 12] = tr_frag(Ks, 16 * ((j - 12) >> 2), ((j - 12) & 3) * 32, lane);
+      if (j >= 20) va[j - 20] = row_frag(Vn, r, 2 * (j - 20) + h);
+      // ---- tile t + 2 -> buffer NN
+      if (j >= 4 && j < 8) dma(NN, j - 4, t2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  std::integral_constant<bool, true> MK;
+  std::integral_constant<bool, false> NM;
+  std::integral_constant<int, 0> B0;
+  std::integral_constant<int, 1> B1;
+  std::integral_constant<int, 2> B2;
+
+  // prologue: tiles 0 and 1 in flight, then S^T_0 and V_0 rows 0-3
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) dma(t, pc, t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  {
+    bf16x8 ka[NDS];
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) ka[s] = row_frag(kvs, r, 2 * s + h);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) va[s] = row_frag(kvs + KT * CH, r, 2 * s + h);
+#pragma unroll
+    for (int s = 0; s < NDS; ++s) s0 = mfma(ka[s], qf[s], s0);
+  }
+  // causal: keys after the query are masked (the diagonal tile per element, later tiles whole)
+  auto masked_of = [&](int t) { return causal && t >= tdiag; };  // wave-uniform
+  auto lim_of = [&](int t) { return t > tdiag ? -1 : qme - t * KT - 4 * h; };
+  auto tile_end = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 2 landed
+    __syncthreads();
+  };
+  for (int t = 0;;) {
+    if (masked_of(t)) step(B0, MK, s0, s1, lim_of(t), t + 2);
+    else step(B0, NM, s0, s1, 0, t + 2);
+    tile_end();
+    if (++t == ntiles) break;
+    if (masked_of(t)) step(B1, MK, s1, s2, lim_of(t), t + 2);
+    else step(B1, NM, s1, s2, 0, t + 2);
+    tile_end();
+    if (++t == ntiles) break;
+    if (masked_of(t)) step(B2, MK, s2, s0, lim_of(t), t + 2);
+    else step(B2, NM, s2, s0, 0, t + 2);
+    tile_end();
+    if (++t == ntiles) break;
+  }
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");  // last MFMA drained
+  f32x16 acc[NDT];
+  acc[0] = acc_read<0>();
+  acc[1] = acc_read<16>();
+  acc[2] = acc_read<32>();
+  acc[3] = acc_read<48>();
+  store_rows_T(acc, scale, kvs + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+}
+
 }  // namespace
 
 extern "C" int pto_attn_dkdv_pipe(const void* q, const void* k, const void* v, const void* dout, const float* lse2,
@@ -384,3 +588,13 @@ extern "C" int pto_attn_pipe_stamps(void* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pipe_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" int pto_attn_dq_pipe(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                const float* lse2, float* delta, void* dq, int B, int S, int Hq, int Hkv, float c,
+                                float scale, int causal, void* stream) {
+  if (S % BM != 0 || Hq % Hkv != 0) return -1;
+  hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout,
+                     lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}

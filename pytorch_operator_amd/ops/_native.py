@@ -184,6 +184,7 @@ _SIGNATURES = {
     "pto_attn_bwd": [_VP] * 10 + [_I] * 5 + [_F, _I, _VP],
     "pto_attn_set_variant": [_I],
     "pto_attn_set_dkdv_variant": [_I],
+    "pto_attn_set_dq_variant": [_I],
     # pool.hip
     "pto_maxpool3s2_fwd": [_VP, _VP, _VP, _I, _I, _I, _I, _VP],
     "pto_maxpool3s2_bwd": [_VP, _VP, _VP, _I, _I, _I, _I, _VP],

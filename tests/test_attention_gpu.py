@@ -195,6 +195,32 @@ def test_flash_rejects_unsupported_shape_on_gpu():
 
 
 @pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 384, 4, 4), (3, 128, 2, 1)])
+def test_pipelined_dq_pass_bit_identical(causal, shape):
+    """The software-pipelined dQ pass (dQ variant 9, attention_bwd_pipe.hip) runs the 8-wave
+    pass's per-element operations in its key order: dQ, and the delta it writes for the dK/dV
+    pass, bit-identical to dQ variant 8 (S % 256 == 0) or the 4-wave pass it falls back to."""
+    from pytorch_operator_amd.ops import _native
+    from pytorch_operator_amd.ops.attention import flash_attention
+    lib = _native.load()
+    q, k, v = _inputs(*shape, seed=23)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    do = torch.randn(q.shape, device="cuda", generator=g).to(torch.bfloat16)
+    outs = {}
+    old = lib.pto_attn_set_dq_variant(9)
+    try:
+        for var in (8, 9):
+            lib.pto_attn_set_dq_variant(var)
+            xs = [x.detach().clone().requires_grad_(True) for x in (q, k, v)]
+            flash_attention(*xs, causal).backward(do)
+            outs[var] = [x.grad for x in xs]
+    finally:
+        lib.pto_attn_set_dq_variant(old)
+    for a, b in zip(outs[8], outs[9]):
+        assert torch.equal(a, b), shape
+
+
+@pytest.mark.parametrize("causal", [True, False])
 def test_split_dkdv_passes_bit_identical(causal):
     """Variants 6 (a dV pass and a dK pass, two waves per SIMD each), 7 (the Q / dO prefetch issued
     from inline asm) and 8 (software-pipelined across query tiles, its own translation unit) run
