@@ -18,6 +18,8 @@ namespace {
 #ifndef PTO_PIPE_PAD  // 1: s_nop 1 before the first MFMA of each k-step (8 us slower, no effect on
 #define PTO_PIPE_PAD 0  // the results: profiles/r4_attn_dkdv_pipe_knobs_ab.json)
 #endif
+#define PTO_AGPR_CLOBBERS_0_63 "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63"
+#define PTO_ZERO_0_63 "v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\tv_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\tv_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\tv_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\tv_accvgpr_write_b32 a16, 0\n\tv_accvgpr_write_b32 a17, 0\n\tv_accvgpr_write_b32 a18, 0\n\tv_accvgpr_write_b32 a19, 0\n\tv_accvgpr_write_b32 a20, 0\n\tv_accvgpr_write_b32 a21, 0\n\tv_accvgpr_write_b32 a22, 0\n\tv_accvgpr_write_b32 a23, 0\n\tv_accvgpr_write_b32 a24, 0\n\tv_accvgpr_write_b32 a25, 0\n\tv_accvgpr_write_b32 a26, 0\n\tv_accvgpr_write_b32 a27, 0\n\tv_accvgpr_write_b32 a28, 0\n\tv_accvgpr_write_b32 a29, 0\n\tv_accvgpr_write_b32 a30, 0\n\tv_accvgpr_write_b32 a31, 0\n\tv_accvgpr_write_b32 a32, 0\n\tv_accvgpr_write_b32 a33, 0\n\tv_accvgpr_write_b32 a34, 0\n\tv_accvgpr_write_b32 a35, 0\n\tv_accvgpr_write_b32 a36, 0\n\tv_accvgpr_write_b32 a37, 0\n\tv_accvgpr_write_b32 a38, 0\n\tv_accvgpr_write_b32 a39, 0\n\tv_accvgpr_write_b32 a40, 0\n\tv_accvgpr_write_b32 a41, 0\n\tv_accvgpr_write_b32 a42, 0\n\tv_accvgpr_write_b32 a43, 0\n\tv_accvgpr_write_b32 a44, 0\n\tv_accvgpr_write_b32 a45, 0\n\tv_accvgpr_write_b32 a46, 0\n\tv_accvgpr_write_b32 a47, 0\n\tv_accvgpr_write_b32 a48, 0\n\tv_accvgpr_write_b32 a49, 0\n\tv_accvgpr_write_b32 a50, 0\n\tv_accvgpr_write_b32 a51, 0\n\tv_accvgpr_write_b32 a52, 0\n\tv_accvgpr_write_b32 a53, 0\n\tv_accvgpr_write_b32 a54, 0\n\tv_accvgpr_write_b32 a55, 0\n\tv_accvgpr_write_b32 a56, 0\n\tv_accvgpr_write_b32 a57, 0\n\tv_accvgpr_write_b32 a58, 0\n\tv_accvgpr_write_b32 a59, 0\n\tv_accvgpr_write_b32 a60, 0\n\tv_accvgpr_write_b32 a61, 0\n\tv_accvgpr_write_b32 a62, 0\n\tv_accvgpr_write_b32 a63, 0"
 template <int A0, bool PAD>
 __device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
   if constexpr (PAD && PTO_PIPE_PAD)
@@ -383,16 +385,58 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 // one XCD), heaviest causal query block first.  Per-element operations and the key order of
 // the dQ accumulation match attn_bwd_dq8_kernel: bit-identical dQ and delta.
 constexpr int KT = 32;
-__global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
+// dQ^T accumulator tile `slot` (0-3) in a[16 slot..]: clobbers only a0-a63, so two waves per
+// SIMD fit (NW = 8: 184 VGPRs + 64 AGPRs of the 256 each)
+// qf / df (the MFMA B operands of S^T and dP^T, fixed per wave) in a64-a95 / a96-a127, so the
+// compiler's VGPRs stay within 128 (two waves per SIMD at NW = 8); every asm statement of this
+// kernel clobbers a0-a127 so the compiler keeps nothing of its own there
+#define PTO_AGPR_CLOBBERS_64 PTO_AGPR_CLOBBERS
+// acc (16 VGPRs) = A . a[B0..B0+3] (+ acc unless FIRST, which starts from 0).  The S^T / dP^T
+// chains are read by VALU only gaps later (>= 12 wait states after the chain's last MFMA).
+template <int B0, bool FIRST>
+__device__ __forceinline__ void mfma_vb(f32x16& acc, const bf16x8& a) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, a[%c2:%c3], 0" : "=v"(acc) : "v"(a), "i"(B0), "i"(B0 + 3)
+                 : PTO_AGPR_CLOBBERS_64);
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, a[%c2:%c3], %0" : "+v"(acc) : "v"(a), "i"(B0), "i"(B0 + 3)
+                 : PTO_AGPR_CLOBBERS_64);
+}
+// k-step s (a constant after unrolling) of the chain whose B operands start at BASE
+template <int BASE>
+__device__ __forceinline__ void mfma_vb_step(int s, f32x16& acc, const bf16x8& a) {
+  switch (s) {
+    case 0: mfma_vb<BASE, true>(acc, a); break;
+    case 1: mfma_vb<BASE + 4, false>(acc, a); break;
+    case 2: mfma_vb<BASE + 8, false>(acc, a); break;
+    case 3: mfma_vb<BASE + 12, false>(acc, a); break;
+    case 4: mfma_vb<BASE + 16, false>(acc, a); break;
+    case 5: mfma_vb<BASE + 20, false>(acc, a); break;
+    case 6: mfma_vb<BASE + 24, false>(acc, a); break;
+    default: mfma_vb<BASE + 28, false>(acc, a); break;
+  }
+}
+__device__ __forceinline__ void mfma_dq_slot(int slot, const bf16x8& a, const bf16x8& b) {
+  switch (slot) {
+    case 0: asm volatile("v_mfma_f32_32x32x16_bf16 a[0:15], %0, %1, a[0:15]" :: "v"(a), "v"(b) : PTO_AGPR_CLOBBERS_64); break;
+    case 1: asm volatile("v_mfma_f32_32x32x16_bf16 a[16:31], %0, %1, a[16:31]" :: "v"(a), "v"(b) : PTO_AGPR_CLOBBERS_64); break;
+    case 2: asm volatile("v_mfma_f32_32x32x16_bf16 a[32:47], %0, %1, a[32:47]" :: "v"(a), "v"(b) : PTO_AGPR_CLOBBERS_64); break;
+    default: asm volatile("v_mfma_f32_32x32x16_bf16 a[48:63], %0, %1, a[48:63]" :: "v"(a), "v"(b) : PTO_AGPR_CLOBBERS_64); break;
+  }
+}
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, const float* __restrict__ lse2,
     float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, float c, float scale,
     int causal) {
-  constexpr int NB = 3, TILE = 2 * KT * CH;
-  __shared__ u32x4 kvs[NB * TILE];  // [buf][K | V] (48 KB); dQ epilogue
+  constexpr int NB = 3, TILE = 2 * KT * CH, BMW = 32 * NW;  // BMW query rows per workgroup
+  constexpr int NPW = 8 / NW;  // pieces of one [KT][D] image per wave
+  constexpr int LEAD = NW == 8 ? 2 : 4;
+  __shared__ u32x4 kvs[NB * TILE > NW * 32 * CH ? NB * TILE : NW * 32 * CH];  // [buf][K | V]; dQ epilogue
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int G = Hq / Hkv, nqb = S / BM;
+  const int G = Hq / Hkv, nqb = S / BMW;
   int bi = (int)blockIdx.x;
   const int hk = bi % Hkv;
   bi /= Hkv;
@@ -400,7 +444,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
   bi /= G;
   const int b = bi % B, qi = bi / B;
   const int qblk = causal ? nqb - 1 - qi : qi;
-  const int q0w = qblk * BM + w * 32, qme = q0w + r;
+  const int q0w = qblk * BMW + w * 32, qme = q0w + r;
   const size_t qstride = (size_t)Hq * D, kvstride = (size_t)Hkv * D;
 
   bf16x8 qf[NDS], df[NDS];
@@ -424,19 +468,32 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
     }
     dl = half_sum(part);
   }
+#pragma unroll
+  for (int s = 0; s < NDS; ++s) {
+    const u32x4 qq = __builtin_bit_cast(u32x4, qf[s]), dd = __builtin_bit_cast(u32x4, df[s]);
+    asm volatile("v_accvgpr_write_b32 a[%c4], %0\n\tv_accvgpr_write_b32 a[%c5], %1\n\t"
+                 "v_accvgpr_write_b32 a[%c6], %2\n\tv_accvgpr_write_b32 a[%c7], %3"
+                 :: "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(qq.w), "i"(64 + 4 * s), "i"(65 + 4 * s), "i"(66 + 4 * s),
+                    "i"(67 + 4 * s) : PTO_AGPR_CLOBBERS_64);
+    asm volatile("v_accvgpr_write_b32 a[%c4], %0\n\tv_accvgpr_write_b32 a[%c5], %1\n\t"
+                 "v_accvgpr_write_b32 a[%c6], %2\n\tv_accvgpr_write_b32 a[%c7], %3"
+                 :: "v"(dd.x), "v"(dd.y), "v"(dd.z), "v"(dd.w), "i"(96 + 4 * s), "i"(97 + 4 * s), "i"(98 + 4 * s),
+                    "i"(99 + 4 * s) : PTO_AGPR_CLOBBERS_64);
+  }
+  asm volatile("s_nop 4" ::: "memory");  // AGPR writes before the first MFMA reading them
   const size_t srow = ((size_t)b * Hq + hq) * S + qme;
   const float lq = lse2[srow];
   if (h == 0) delta[srow] = dl;
 
-  const int ntiles = causal ? (qblk * BM + BM) / KT : S / KT;
+  const int ntiles = causal ? (qblk * BMW + BMW) / KT : S / KT;
   const int tdiag = q0w / KT;  // causal: this wave's diagonal tile; later tiles are masked whole
 
-  // LDS-DMA: piece k of a tile (k = 0, 1: K rows; 2, 3: V rows), pieces w and w + 4 of the 8 per
-  // [KT][D] image for wave w
-  uint32_t doff[2];
+  // LDS-DMA: piece k of a tile (k < NPW: K rows, then V rows); wave w moves pieces w + NW i of
+  // the 8 per [KT][D] image
+  uint32_t doff[NPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int e = 64 * (w + 4 * i) + lane, row = e / CH, j = e % CH;
+  for (int i = 0; i < NPW; ++i) {
+    const int e = 64 * (w + NW * i) + lane, row = e / CH, j = e % CH;
     doff[i] = (uint32_t)(row * kvstride) + 8 * (j ^ (((row & 3) << 2) | ((row >> 2) & 3)));
   }
   const bf16_t* kb = k + (size_t)b * S * kvstride + (size_t)hk * D;
@@ -444,9 +501,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
   const unsigned lds_w = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(kvs + 64 * wu));
   auto dma = [&](int buf, int piece, int t) {
     t = t < ntiles ? t : ntiles - 1;  // past the end: refetch the last tile into a dead buffer
-    const int i = piece & 1;
-    const bf16_t* src = (piece < 2 ? kb : vb) + (size_t)t * KT * kvstride + doff[i];
-    const unsigned dst = lds_w + 16u * (buf * TILE + (piece < 2 ? 0 : KT * CH) + 64 * 4 * i);
+    const int i = piece % NPW;
+    const bf16_t* src = (piece < NPW ? kb : vb) + (size_t)t * KT * kvstride + doff[i];
+    const unsigned dst = lds_w + 16u * (buf * TILE + (piece < NPW ? 0 : KT * CH) + 64 * NW * i);
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
                  :: "s"(dst), "v"(src) : "memory", "m0");
   };
@@ -454,7 +511,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
   // loop-carried: S^T of the current tile (rotating sets) and V rows 0-3 of the current tile
   f32x16 s0 = zero16(), s1 = zero16(), s2 = zero16();
   bf16x8 va[NDS];
-  acc_zero();
+  asm volatile(PTO_ZERO_0_63 ::: PTO_AGPR_CLOBBERS_64);
 
   auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, int t2) {
     constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
@@ -463,19 +520,18 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
     const u32x4* Vs = Ks + KT * CH;
     const u32x4* Kn = kvs + NXT * TILE;
     const u32x4* Vn = Kn + KT * CH;
-    f32x16 pa = zero16();
-    sout = zero16();
+    f32x16 pa;
     bf16x8 ka[NDS], kt[8], db[2];
     uint32_t dw[8];
 #pragma unroll
     for (int j = 0; j < 24; ++j) {
       // ---- the gap's MFMA
       if (j < 8) {
-        pa = mfma(va[j], df[j], pa);
+        mfma_vb_step<96>(j, pa, va[j]);  // dP^T = V . dO^T
       } else if (j < 16) {
-        sout = mfma(ka[j - 8], qf[j - 8], sout);
+        mfma_vb_step<64>(j - 8, sout, ka[j - 8]);  // S^T = K . Q^T
       } else {  // dQ^T tile (j & 3) += K^T . dS^T, k-step (j - 16) >> 2
-        mfma_acc_slot(j & 3, kt[j - 16], db[(j - 16) >> 2]);
+        mfma_dq_slot(j & 3, kt[j - 16], db[(j - 16) >> 2]);
       }
       // ---- VALU (no filler depends on another in the same gap)
       if (j < 16) {  // (opaque first: lse2 is loop-invariant, and the compiler would otherwise
@@ -508,13 +564,15 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
           db[s] = __builtin_bit_cast(bf16x8, u);
         }
       }
-      // ---- LDS reads, four gaps ahead of their MFMA
-      if (j < 4) va[4 + j] = row_frag(Vs, r, 2 * (4 + j) + h);
-      if (j >= 4 && j < 12) ka[j - 4] = row_frag(Kn, r, 2 * (j - 4) + h);
-      if (j >= 12 && j < 20) kt[j - 12] = tr_frag(Ks, 16 * ((j - 12) >> 2), ((j - 12) & 3) * 32, lane);
-      if (j >= 20) va[j - 20] = row_frag(Vn, r, 2 * (j - 20) + h);
+      // ---- LDS reads, LEAD gaps ahead of their MFMA (4 at one wave per SIMD; 2 at two, where
+      // the partner wave covers the latency and the registers are scarcer)
+      if (j < 8 - LEAD) va[LEAD + j] = row_frag(Vs, r, 2 * (LEAD + j) + h);
+      if (j >= 8 - LEAD && j < 16 - LEAD) ka[j - 8 + LEAD] = row_frag(Kn, r, 2 * (j - 8 + LEAD) + h);
+      if (j >= 16 - LEAD && j < 24 - LEAD)
+        kt[j - 16 + LEAD] = tr_frag(Ks, 16 * ((j - 16 + LEAD) >> 2), ((j - 16 + LEAD) & 3) * 32, lane);
+      if (j >= 24 - LEAD) va[j - 24 + LEAD] = row_frag(Vn, r, 2 * (j - 24 + LEAD) + h);
       // ---- tile t + 2 -> buffer NN
-      if (j >= 4 && j < 8) dma(NN, j - 4, t2);
+      if (j >= 4 && j < 4 + 2 * NPW) dma(NN, j - 4, t2);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -528,7 +586,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) dma(t, pc, t);
+    for (int pc = 0; pc < 2 * NPW; ++pc) dma(t, pc, t);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   {
@@ -536,27 +594,37 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dq_pipe_kernel(
 #pragma unroll
     for (int s = 0; s < NDS; ++s) ka[s] = row_frag(kvs, r, 2 * s + h);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) va[s] = row_frag(kvs + KT * CH, r, 2 * s + h);
+    for (int s = 0; s < LEAD; ++s) va[s] = row_frag(kvs + KT * CH, r, 2 * s + h);
 #pragma unroll
-    for (int s = 0; s < NDS; ++s) s0 = mfma(ka[s], qf[s], s0);
+    for (int s = 0; s < NDS; ++s) mfma_vb_step<64>(s, s0, ka[s]);
+    asm volatile("s_nop 15" ::: "memory");  // S^T_0 complete before the first tile's VALU reads it
   }
   // causal: keys after the query are masked (the diagonal tile per element, later tiles whole)
   auto masked_of = [&](int t) { return causal && t >= tdiag; };  // wave-uniform
-  auto lim_of = [&](int t) { return t > tdiag ? -1 : qme - t * KT - 4 * h; };
+  auto lim_of = [&](int t) { return qme - t * KT - 4 * h; };  // t <= tdiag
   auto tile_end = [&]() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 2 landed
     __syncthreads();
   };
+  // tiles after the wave's diagonal (causal) are all masked and come last: the wave only moves
+  // its DMA pieces and keeps the barriers (its partner wave on the SIMD runs unslowed)
+  auto idle = [&](int nn, int t2) {
+#pragma unroll
+    for (int pc = 0; pc < 2 * NPW; ++pc) dma(nn, pc, t2);
+  };
   for (int t = 0;;) {
-    if (masked_of(t)) step(B0, MK, s0, s1, lim_of(t), t + 2);
+    if (causal && t > tdiag) idle(2, t + 2);
+    else if (masked_of(t)) step(B0, MK, s0, s1, lim_of(t), t + 2);
     else step(B0, NM, s0, s1, 0, t + 2);
     tile_end();
     if (++t == ntiles) break;
-    if (masked_of(t)) step(B1, MK, s1, s2, lim_of(t), t + 2);
+    if (causal && t > tdiag) idle(0, t + 2);
+    else if (masked_of(t)) step(B1, MK, s1, s2, lim_of(t), t + 2);
     else step(B1, NM, s1, s2, 0, t + 2);
     tile_end();
     if (++t == ntiles) break;
-    if (masked_of(t)) step(B2, MK, s2, s0, lim_of(t), t + 2);
+    if (causal && t > tdiag) idle(1, t + 2);
+    else if (masked_of(t)) step(B2, MK, s2, s0, lim_of(t), t + 2);
     else step(B2, NM, s2, s0, 0, t + 2);
     tile_end();
     if (++t == ntiles) break;
@@ -593,8 +661,13 @@ extern "C" int pto_attn_dq_pipe(const void* q, const void* k, const void* v, con
                                 const float* lse2, float* delta, void* dq, int B, int S, int Hq, int Hkv, float c,
                                 float scale, int causal, void* stream) {
   if (S % BM != 0 || Hq % Hkv != 0) return -1;
-  hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel, dim3((S / BM) * B * Hq), dim3(NT), 0, (hipStream_t)stream,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout,
-                     lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  if (S % (2 * BM) == 0)  // 8 waves (256 query rows share each K/V tile), two per SIMD
+    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel<8>, dim3((S / (2 * BM)) * B * Hq), dim3(8 * 64), 0,
+                       (hipStream_t)stream, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
+                       (const bf16_t*)dout, lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
+  else
+    hipLaunchKernelGGL(attn_bwd_dq_pipe_kernel<4>, dim3((S / BM) * B * Hq), dim3(4 * 64), 0, (hipStream_t)stream,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o, (const bf16_t*)dout,
+                       lse2, delta, (bf16_t*)dq, B, S, Hq, Hkv, c, scale, causal);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
