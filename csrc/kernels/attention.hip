@@ -1431,14 +1431,15 @@ int g_fwd_variant = -1;
 // pass and a dK pass of two waves per SIMD each (slower, round-4 A/B); PTO_ATTN_DKDV or
 // pto_attn_set_dkdv_variant()
 // dQ pass: 9 = software-pipelined across key tiles with an AGPR-pinned accumulator
-// (attention_bwd_pipe.hip), 8 = the 8-wave two-waves-per-SIMD pass (default)
+// (attention_bwd_pipe.hip, default: 247 vs 274 us, profiles/r4_attn_dq_pipe_ab.json), 8 = the
+// 8-wave two-waves-per-SIMD compiler-scheduled pass
 // (attn_bwd_dq8_kernel; the 4-wave attn_bwd_dq_kernel when S % 256 != 0 or the forward
 // variant is below 8); PTO_ATTN_DQ or pto_attn_set_dq_variant()
 int g_dq_variant = -1;
 int dq_variant() {
   if (g_dq_variant < 0) {
     const char* e = getenv("PTO_ATTN_DQ");
-    g_dq_variant = e != nullptr ? atoi(e) : 8;
+    g_dq_variant = e != nullptr ? atoi(e) : 9;
   }
   return g_dq_variant;
 }

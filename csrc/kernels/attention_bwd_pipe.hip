@@ -370,20 +370,24 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 }
 
 // ---------------------------------- backward pass 1 (dQ), software-pipelined across key tiles
-// The dQ pass in the dK/dV pipeline's form (attn_bwd_dq8_kernel, attention.hip, is the
-// two-waves-per-SIMD form it replaces): one wave per SIMD, 4 waves x 32 queries (the query on
-// the lane), key tiles of KT = 32 keys (K | V, 16 KB) shared through three LDS buffers, the dQ^T
-// accumulator pinned in AGPRs a0-a63.  A tile is 24 MFMA gaps:
+// The dQ pass in the dK/dV pipeline's form.  NW waves x 32 queries per workgroup (the query on
+// the lane): NW = 8 (default, S % 256 == 0: 256 query rows share each K/V tile, two waves per
+// SIMD) or NW = 4 (one per SIMD).  Key tiles of KT = 32 keys (K | V, 16 KB) pass through three
+// LDS buffers; the dQ^T accumulator is pinned in AGPRs a0-a63 and the wave's Q / dO operands
+// (the B operands of S^T and dP^T) in a64-a127, so the compiler's VGPRs fit 128 (NW = 8).
+// A tile is 24 MFMA gaps:
 //   gaps  0-7   dP^T_t = V_t . dO^T      P_t = exp2(S^T_t c - lse2): fma gap i, exp2 gap i + 1
 //   gaps  8-15  S^T_{t+1} = K_{t+1} . Q^T     dS_t = P (dP - delta): subtract gaps 9-16, multiply
 //                                              10-17, bf16 pack 11-18
 //   gaps 16-23  dQ^T += K_t^T . dS^T_t
-// LDS reads four gaps ahead: V_t rows (gaps 20-23 of the previous tile and 0-3), K_{t+1} rows
-// (4-11), K_t^T transposed (12-19).  Tile t+2's LDS-DMA goes out in gaps 4-7 and lands by the
-// closing barrier (tile t+1 computes S^T_{t+2} from it).  lse2 and delta are per-lane scalars.
-// Block order: kv head fastest (the G query heads sharing a K/V stream sit 8 blocks apart, on
-// one XCD), heaviest causal query block first.  Per-element operations and the key order of
-// the dQ accumulation match attn_bwd_dq8_kernel: bit-identical dQ and delta.
+// LDS reads LEAD gaps ahead (4 at NW = 4, 2 at NW = 8): V_t rows, K_{t+1} rows, K_t^T
+// transposed.  Tile t+2's LDS-DMA goes out in gaps 4-7 and lands by the closing barrier (tile
+// t+1 computes S^T_{t+2} from it).  lse2 and delta are per-lane scalars.  A wave past its
+// causal diagonal only moves its DMA pieces.  Block order: kv head fastest (the G query heads
+// sharing a K/V stream sit 8 blocks apart, on one XCD), heaviest causal query block first.
+// Per-element operations and the key order of the dQ accumulation match attn_bwd_dq8_kernel:
+// bit-identical dQ and delta.  NW = 8: 247 vs 274 us on the 8B shape
+// (profiles/r4_attn_dq_pipe_ab.json); NW = 4 measured equal to attn_bwd_dq8_kernel.
 constexpr int KT = 32;
 // dQ^T accumulator tile `slot` (0-3) in a[16 slot..]: clobbers only a0-a63, so two waves per
 // SIMD fit (NW = 8: 184 VGPRs + 64 AGPRs of the 256 each)
