@@ -15,6 +15,12 @@ namespace {
 // before the MFMA that reads it (the schedule below), so no `s_nop` pad is needed (PAD keeps
 // one for A/B); the epilogue waits out the last MFMA before reading (acc_read).
 #define PTO_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127"
+// Diagnostic ablations of the dK/dV pipeline (wrong results, in-bounds accesses; A/B builds
+// only): 1 no dS arithmetic, 2 row reads in place of the transposed reads, 4 no per-tile DMA,
+// 8 no per-tile barrier, 16 no exp2
+#ifndef PTO_PIPE_ABL
+#define PTO_PIPE_ABL 0
+#endif
 #ifndef PTO_PIPE_PAD  // 1: s_nop 1 before the first MFMA of each k-step (8 us slower, no effect on
 #define PTO_PIPE_PAD 0  // the results: profiles/r4_attn_dkdv_pipe_knobs_ab.json)
 #endif
@@ -213,7 +219,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       }
       if (j >= 1 && j <= 16) {
         const int i = j - 1;
-        float p = __builtin_amdgcn_exp2f(sin[i]);
+        float p = (PTO_PIPE_ABL & 16) ? sin[i] : __builtin_amdgcn_exp2f(sin[i]);
         if (MASK && (i & 3) + 8 * (i >> 2) < lim) p = 0.f;  // key > query
         sin[i] = p;
       }
@@ -233,13 +239,15 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
           const int i = 2 * m + e2, ei = i & 3;
           const float4 d4 = D4[i >> 2];
           const float Dv = ei == 0 ? d4.x : ei == 1 ? d4.y : ei == 2 ? d4.z : d4.w;
-          pa[i] = pa[i] - Dv;
+          if (!(PTO_PIPE_ABL & 1)) pa[i] = pa[i] - Dv;
         }
       }
       if (j >= 17 && j < 25) {
         const int m = j - 17;
-        pa[2 * m] = sin[2 * m] * pa[2 * m];
-        pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
+        if (!(PTO_PIPE_ABL & 1)) {
+          pa[2 * m] = sin[2 * m] * pa[2 * m];
+          pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
+        }
       }
       if (j >= 18 && j < 26) {
         const int m = j - 18;
@@ -258,18 +266,20 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         qa[2 * (j - 4) + 1] = row_frag(Qn, r, 4 * (j - 4) + 2 + h);
       }
       if (j >= 16 - TLEAD && j < 24 - TLEAD)
-        td[j - 16 + TLEAD] = tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
+        td[j - 16 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Ds, (16 * ((j - 16 + TLEAD) >> 2) + r) & 31, (j - 16 + TLEAD) & 3)
+                                                : tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
       if (j == 12 || j == 14 || j == 16 || j == 18)
         D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + QT + 8 * ((j - 12) >> 1) + 4 * h);
       if (j >= 24 - TLEAD && j < 32 - TLEAD)
-        tq[j - 24 + TLEAD] = tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
+        tq[j - 24 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Qs, (16 * ((j - 24 + TLEAD) >> 2) + r) & 31, (j - 24 + TLEAD) & 3)
+                                                : tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
       if (j >= 28) {
         da[j - 28] = row_frag(Dn, r, 2 * (j - 28) + h);
         if (j == 28) L4[0] = *reinterpret_cast<const float4*>(stn + 4 * h);
       }
       // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier); it must
       // land by this tile's closing barrier (tile t + 1 reads it), so it goes out early
-      if (j >= 8 && j < 13) dma(NN, j - 8, toff2, soff2);
+      if (j >= 8 && j < 13 && !(PTO_PIPE_ABL & 4)) dma(NN, j - 8, toff2, soff2);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 #ifdef PTO_ATTN_STAMPS
     if (t == 9) PTO_STAMP(12);
 #endif
-    __syncthreads();
+    if (!(PTO_PIPE_ABL & 8)) __syncthreads();
 #ifdef PTO_ATTN_STAMPS
     if (t == 9) PTO_STAMP(13);
 #endif
