@@ -21,6 +21,12 @@ namespace {
 #ifndef PTO_PIPE_ABL
 #define PTO_PIPE_ABL 0
 #endif
+#ifndef PTO_PIPE_DMA0  // gap of the first of a tile's five LDS-DMA pieces, and the spacing
+#define PTO_PIPE_DMA0 8
+#endif
+#ifndef PTO_PIPE_DMAS
+#define PTO_PIPE_DMAS 1
+#endif
 #ifndef PTO_PIPE_PAD  // 1: s_nop 1 before the first MFMA of each k-step (8 us slower, no effect on
 #define PTO_PIPE_PAD 0  // the results: profiles/r4_attn_dkdv_pipe_knobs_ab.json)
 #endif
@@ -279,7 +285,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       }
       // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier); it must
       // land by this tile's closing barrier (tile t + 1 reads it), so it goes out early
-      if (j >= 8 && j < 13 && !(PTO_PIPE_ABL & 4)) dma(NN, j - 8, toff2, soff2);
+      if (j >= PTO_PIPE_DMA0 && (j - PTO_PIPE_DMA0) % PTO_PIPE_DMAS == 0 &&
+          (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS < 5 && !(PTO_PIPE_ABL & 4))
+        dma(NN, (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS, toff2, soff2);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
