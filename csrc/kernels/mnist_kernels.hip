@@ -54,6 +54,17 @@ namespace {
 
 typedef unsigned long long u64;
 
+// diagnostic builds only (-DPTO_MNIST_STAMPW): a stamp from the thread `who` of the block
+__device__ __forceinline__ void stamp_by(u64* dbg, int phase, int who) {
+#ifdef PTO_MNIST_STAMPW
+  if (dbg != nullptr && (int)threadIdx.x == who) {
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    dbg[blk * 16 + phase] = (u64)wall_clock64();
+  }
+#else
+  (void)dbg; (void)phase; (void)who;
+#endif
+}
 __device__ __forceinline__ void stamp(u64* dbg, int phase) {
   if (dbg != nullptr && threadIdx.x == 0) {
     const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
@@ -545,9 +556,13 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
-    conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+    stamp_by(dbg, 4, 0);             // wave 0: 3 MFMA tiles done
+    stamp_by(dbg, 5, AB_NT - 64);    // last wave: 2 MFMA tiles done, VALU windows next
+    stamp_by(dbg, 7, 4 * 64);        // wave 4: 2 MFMA tiles, no VALU windows
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
+    stamp_by(dbg, 6, AB_NT - 64);    // last wave: VALU windows done
   }
   __syncthreads();
   stamp(dbg, 2);

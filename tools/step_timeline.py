@@ -62,6 +62,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=5, help="timelines sampled (each after --steps steps)")
+    ap.add_argument("--conv1-waves", action="store_true",
+                    help="diagnostic build (-DPTO_MNIST_STAMPW): conv12_fwd's per-wave conv1 stamps")
     args = ap.parse_args(argv)
     dev = torch.device("cuda")
     ds = make_synthetic_mnist(60000, seed=1, device=dev)
@@ -88,6 +90,13 @@ def main(argv=None):
         g.replay_stream(args.steps // 2)
         torch.cuda.synchronize()
         samples.append(analyse(dbg, nk))
+        if args.conv1_waves:  # slot 0 = conv12_fwd: stamps 4-7 relative to stamp 1 (conv1 start)
+            d = dbg.view(-1, 16).cpu()[:1024].double()
+            d = d[d[:, 0] > 0]
+            rel = {k: float(((d[:, k] - d[:, 1]) / 100.0).mean()) for k in (4, 5, 6, 7, 2)}
+            print("conv1 per-wave (us after conv1 start): wave0 tiles done %.2f, wave4 tiles %.2f, "
+                  "last wave tiles %.2f, last wave VALU windows %.2f, barrier %.2f"
+                  % (rel[4], rel[7], rel[5], rel[6], rel[2]), flush=True)
     # per-kernel medians over the samples
     rows = []
     per = nk // 2
