@@ -131,7 +131,7 @@ def main(argv=None) -> int:
     # autotune hand-over in both directions keeps the replicas identical
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
     # Shared GPU at the one-GPU-per-rank geometry: the stream-launched runners pack both ranks'
-    # kernels back to back, and 2 of 5 rehearsals (tools/gpu/r4_s4.sh, check.sh) then timed
+    # kernels back to back, and 2 of 5 rehearsals (tools/gpu/sessions/r4_s4.sh, check.sh) then timed
     # out in the xGMI hand-over's run (both waits, error 3) while every graph-launched and eager
     # stage passed -- the co-residency squeeze the conv_chunk note above describes, which one
     # rank per GPU never has.  Graph launch (round 3's form) keeps the rehearsal to the protocol.
