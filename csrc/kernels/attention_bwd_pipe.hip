@@ -21,6 +21,9 @@ namespace {
 #ifndef PTO_PIPE_ABL
 #define PTO_PIPE_ABL 0
 #endif
+#ifndef PTO_PIPE_EPIW  // 1: the epilogue stages each wave's rows without block barriers
+#define PTO_PIPE_EPIW 1
+#endif
 #ifndef PTO_PIPE_DMA0  // gap of the first of a tile's five LDS-DMA pieces, and the spacing
 #define PTO_PIPE_DMA0 8
 #endif
@@ -373,6 +376,14 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   acc[2] = acc_read<32>();
   acc[3] = acc_read<48>();
   const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
+#if PTO_PIPE_EPIW  // wave-local staging: the loop's closing barrier already retired every tile read
+  store_rows_T_wave(acc, 1.f, qd + w * 32 * CH, lane, dv + off, kvstride);
+  acc[0] = acc_read<64>();
+  acc[1] = acc_read<80>();
+  acc[2] = acc_read<96>();
+  acc[3] = acc_read<112>();
+  store_rows_T_wave(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
+#else
   store_rows_T(acc, 1.f, qd + w * 32 * CH, lane, dv + off, kvstride);
   __syncthreads();
   acc[0] = acc_read<64>();
@@ -380,6 +391,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   acc[2] = acc_read<96>();
   acc[3] = acc_read<112>();
   store_rows_T(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
+#endif
   PTO_STAMP(3);
   PTO_RSTAMP(5);
 #ifdef PTO_ATTN_STAMPS
@@ -657,7 +669,12 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   acc[1] = acc_read<16>();
   acc[2] = acc_read<32>();
   acc[3] = acc_read<48>();
+#if PTO_PIPE_EPIW
+  store_rows_T_wave(acc, scale, kvs + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D,
+                    qstride);
+#else
   store_rows_T(acc, scale, kvs + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
+#endif
 }
 
 }  // namespace

@@ -198,6 +198,32 @@ __device__ __forceinline__ void store_rows_T(const f32x16 (&acc)[NDT], float sca
   }
 }
 
+// store_rows_T for a wave whose staging region no other wave touches any more (after the last
+// tile's barrier): the hand-off from this wave's LDS writes to its own reads needs no block
+// barrier (one wave's LDS operations complete in order)
+__device__ __forceinline__ void store_rows_T_wave(const f32x16 (&acc)[NDT], float scale, u32x4* stage, int lane,
+                                                  bf16_t* out, size_t row_stride) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = dt * 32 + 8 * g + 4 * h;
+      u32x2 w;
+      w.x = pk_bf16(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+      w.y = pk_bf16(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+      *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(stage + xo(c, d0 >> 3)) + (d0 & 7) * 2) = w;
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 32 * CH / 64; ++i) {
+    const int e = lane + 64 * i, row = e / CH, ch = e % CH;
+    *reinterpret_cast<u32x4*>(out + (size_t)row * row_stride + ch * 8) = stage[xo(row, ch)];
+  }
+}
+
 // Forward / dQ workgroup -> (query block, batch, q head, kv head).  The query block is the
 // slowest index of the launch order, heaviest (last) block first under the causal mask, so
 // the light blocks fill in behind the heavy ones across the whole grid.
