@@ -21,6 +21,9 @@ namespace {
 #ifndef PTO_PIPE_ABL
 #define PTO_PIPE_ABL 0
 #endif
+#ifndef PTO_PIPE_STAT4  // 1: lse2 / delta staged once per four query tiles
+#define PTO_PIPE_STAT4 0
+#endif
 #ifndef PTO_PIPE_EPIW  // 1: the epilogue stages each wave's rows without block barriers
 #define PTO_PIPE_EPIW 1
 #endif
@@ -123,7 +126,15 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     int causal) {
   constexpr int NB = 3, TILE = 2 * QT * CH;
   __shared__ u32x4 qd[NB * TILE];                   // [buf][Q | dO] (48 KB); dK/dV epilogue
+#if PTO_PIPE_STAT4
+  // lse2 / delta of four consecutive query tiles (one head) per slot, two slots: one 1 KiB
+  // LDS-DMA per four tiles instead of a 256-byte piece per tile from every wave
+  __shared__ __align__(16) float stat4[2][2][4 * QT];  // [slot][lse2 | delta][4 tiles x 32 rows]
+  constexpr int SDOFF = 4 * QT;                          // lse2 -> delta of the same rows
+#else
   __shared__ __align__(16) float stat[NB][2 * QT];  // [buf][lse2 | delta]
+  constexpr int SDOFF = QT;
+#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
@@ -164,6 +175,19 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     soff = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
   };
   const unsigned lds_w = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(qd + 64 * wu));  // this wave's piece 0
+#if PTO_PIPE_STAT4
+  // the statistics of the four tiles starting at tile t4 (a multiple of 4; nqt is one too, so the
+  // group stays in one head) into slot `slot`: lanes 0-31 lse2, 32-63 delta, 4 rows per lane
+  auto dma_stat4 = [&](int slot, int t4) {
+    t4 = t4 < ntiles ? t4 : ntiles - 4;
+    const int g = t4 / nqt, qt = qt0 + t4 % nqt, hq = hk * G + g;
+    const float* src = (lane < 32 ? lse2 : delta) + ((size_t)b * Hq + hq) * S + (size_t)qt * QT + 4 * (lane & 31);
+    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&stat4[slot][0][0]));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                 :: "s"(dst), "v"(src) : "memory", "m0");
+  };
+  auto stat_ptr = [&](int t) -> const float* { return &stat4[(t >> 2) & 1][0][(t & 3) * QT]; };
+#endif
   auto dma = [&](int buf, int piece, size_t toff, size_t soff) {
     if (piece < 4) {
       const int i = piece & 1;
@@ -172,7 +196,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
                    :: "s"(dst), "v"(src) : "memory", "m0");
     } else {
+#if !PTO_PIPE_STAT4
       glds_dword_asm(sbase + soff, stat[buf]);
+#endif
     }
   };
 
@@ -186,15 +212,22 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 
   // one tile in buffer CUR: consumes sin (S_t), produces sout (S_{t+1} from buffer CUR + 1),
   // DMAs tile t + 2 into buffer CUR + 2
-  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, size_t toff2, size_t soff2, bool stamp) {
+  auto step = [&](auto curc, auto maskc, f32x16& sin, f32x16& sout, int lim, size_t toff2, size_t soff2, bool stamp,
+                  int t) {
     constexpr int CUR = decltype(curc)::value, NXT = (CUR + 1) % NB, NN = (CUR + 2) % NB;
     constexpr bool MASK = decltype(maskc)::value;
     const u32x4* Qs = qd + CUR * TILE;
     const u32x4* Ds = Qs + QT * CH;
     const u32x4* Qn = qd + NXT * TILE;
     const u32x4* Dn = Qn + QT * CH;
+#if PTO_PIPE_STAT4
+    const float* st = stat_ptr(t);
+    const float* stn = stat_ptr(t + 1);
+#else
     const float* st = stat[CUR];
     const float* stn = stat[NXT];
+    (void)t;
+#endif
     f32x16 pa = zero16();
     sout = zero16();
     bf16x8 qa[NDS], td[8], tq[8], pb[2], db[2];
@@ -278,7 +311,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         td[j - 16 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Ds, (16 * ((j - 16 + TLEAD) >> 2) + r) & 31, (j - 16 + TLEAD) & 3)
                                                 : tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
       if (j == 12 || j == 14 || j == 16 || j == 18)
-        D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + QT + 8 * ((j - 12) >> 1) + 4 * h);
+        D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + SDOFF + 8 * ((j - 12) >> 1) + 4 * h);
       if (j >= 24 - TLEAD && j < 32 - TLEAD)
         tq[j - 24 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Qs, (16 * ((j - 24 + TLEAD) >> 2) + r) & 31, (j - 24 + TLEAD) & 3)
                                                 : tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
@@ -289,8 +322,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier); it must
       // land by this tile's closing barrier (tile t + 1 reads it), so it goes out early
       if (j >= PTO_PIPE_DMA0 && (j - PTO_PIPE_DMA0) % PTO_PIPE_DMAS == 0 &&
-          (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS < 5 && !(PTO_PIPE_ABL & 4))
+          (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS < (PTO_PIPE_STAT4 ? 4 : 5) && !(PTO_PIPE_ABL & 4))
         dma(NN, (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS, toff2, soff2);
+
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -308,6 +342,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       tile_off(t, toff, soff);
 #pragma unroll
       for (int pc = 0; pc < 5; ++pc) dma(t, pc, toff, soff);
+#if PTO_PIPE_STAT4
+      if (t == 0 && wu == 0) dma_stat4(0, 0);
+#endif
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -317,7 +354,11 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     for (int s = 0; s < NDS; ++s) qa[s] = row_frag(Qs, r, 2 * s + h);
 #pragma unroll
     for (int s = 0; s < 4; ++s) da[s] = row_frag(Qs + QT * CH, r, 2 * s + h);
+#if PTO_PIPE_STAT4
+    L4[0] = *reinterpret_cast<const float4*>(stat_ptr(0) + 4 * h);
+#else
     L4[0] = *reinterpret_cast<const float4*>(stat[0] + 4 * h);
+#endif
 #pragma unroll
     for (int s = 0; s < NDS; ++s) s0 = mfma(qa[s], kf[s], s0);
   }
@@ -345,24 +386,39 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   for (int t = 0;;) {
     size_t toff, soff;
     tile_off(t + 2, toff, soff);
+#if PTO_PIPE_STAT4
+    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
+    // tile's gaps; its slot was last read in the previous group's last tile
+    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
+#endif
     if (masked_of(t))
-      step(B0, MK, s0, s1, lim_of(t), toff, soff, t == 9);
+      step(B0, MK, s0, s1, lim_of(t), toff, soff, t == 9, t);
     else
-      step(B0, NM, s0, s1, 0, toff, soff, t == 9);
+      step(B0, NM, s0, s1, 0, toff, soff, t == 9, t);
     tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
+#if PTO_PIPE_STAT4
+    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
+    // tile's gaps; its slot was last read in the previous group's last tile
+    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
+#endif
     if (masked_of(t))
-      step(B1, MK, s1, s2, lim_of(t), toff, soff, t == 9);
+      step(B1, MK, s1, s2, lim_of(t), toff, soff, t == 9, t);
     else
-      step(B1, NM, s1, s2, 0, toff, soff, t == 9);
+      step(B1, NM, s1, s2, 0, toff, soff, t == 9, t);
     tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
+#if PTO_PIPE_STAT4
+    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
+    // tile's gaps; its slot was last read in the previous group's last tile
+    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
+#endif
     if (masked_of(t))
-      step(B2, MK, s2, s0, lim_of(t), toff, soff, t == 9);
+      step(B2, MK, s2, s0, lim_of(t), toff, soff, t == 9, t);
     else
-      step(B2, NM, s2, s0, 0, toff, soff, t == 9);
+      step(B2, NM, s2, s0, 0, toff, soff, t == 9, t);
     tile_end(t);
     if (++t == ntiles) break;
   }
