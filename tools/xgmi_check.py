@@ -128,17 +128,23 @@ def main(argv=None) -> int:
     res["graph_in_sync"] = bool(torch.equal(ref, ta.flat_params))
     res["error_after"]["graph"] = xar.error()
     res["finite"] = bool(torch.isfinite(ta.flat_params).all())
-    # autotune hand-over in both directions keeps the replicas identical
+    # autotune hand-over in both directions keeps the replicas identical.  Ranks sharing one GPU
+    # at the one-GPU-per-rank geometry (256 exchange workgroups each) run this stage on a second
+    # exchange at 128 workgroups: the race's trial runs pack both ranks' kernels back to back, and
+    # at 2 x 256 spinning workgroups the peer's compute kernels are not guaranteed a CU -- the
+    # stage timed out (both waits, error 3) in 2 of 5 stream-launched and 1 of 4 graph-launched
+    # rehearsals (tools/gpu/sessions/r4_s4.sh, r4_s31.sh) while every eager and graph stage above passed.
+    # One rank per GPU never has that squeeze; the hand-over logic does not depend on the geometry,
+    # and the 256-workgroup exchange itself is covered by the stages above.
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
-    # Shared GPU at the one-GPU-per-rank geometry: the stream-launched runners pack both ranks'
-    # kernels back to back, and 2 of 5 rehearsals (tools/gpu/sessions/r4_s4.sh, check.sh) then timed
-    # out in the xGMI hand-over's run (both waits, error 3) while every graph-launched and eager
-    # stage passed -- the co-residency squeeze the conv_chunk note above describes, which one
-    # rank per GPU never has.  Graph launch (round 3's form) keeps the rehearsal to the protocol.
-    launch = "graph" if shared_256 else "stream"
+    hx = XgmiAllReduce(L, device=dev, nblk=128) if shared_256 else xar
+    if hx is not xar:
+        res["handover_self_test"] = hx.self_test()
+    res["handover_nblk"] = hx.nblk
+    launch = "stream"
     res["handover_launch"] = launch
     for force in ("rccl", "xgmi"):
-        runner, path, times = choose_grad_sync(ta, FlatGradAllReduce(), XgmiGradSync(xar), spg=4,
+        runner, path, times = choose_grad_sync(ta, FlatGradAllReduce(), XgmiGradSync(hx), spg=4,
                                                trial_steps=8, force=force, launch=launch)
         runner.run(8)
         torch.cuda.synchronize(dev)
@@ -149,11 +155,11 @@ def main(argv=None) -> int:
         res[f"handover_{force}_in_sync"] = bool(torch.equal(ref, ta.flat_params)) and (
             force == "xgmi" or bool(torch.equal(mref, ta.flat_momentum)))
         res[f"handover_{force}_times"] = times
-        res["error_after"][f"handover_{force}"] = xar.error()
+        res["error_after"][f"handover_{force}"] = hx.error()
     if a.bench:
         res["exchange_us"] = _bench_exchange(xar, ta, dev)
-    res["kernel_error"] = xar.error()
-    ok = res["self_test"] and res["eager_match"] and res["push_bit_identical"] and res["graph_in_sync"] and res["finite"] \
+    res["kernel_error"] = xar.error() | (hx.error() if hx is not xar else 0)
+    ok = res.get("handover_self_test", True) and res["self_test"] and res["eager_match"] and res["push_bit_identical"] and res["graph_in_sync"] and res["finite"] \
         and res["kernel_error"] == 0 and res["handover_rccl_in_sync"] and res["handover_xgmi_in_sync"]
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -164,6 +170,8 @@ def main(argv=None) -> int:
         with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
             json.dump(res, f)
     dist.barrier()
+    if hx is not xar:
+        hx.close()
     xar.close()
     dist.destroy_process_group()
     return 0 if res["all_ok"] else 1
