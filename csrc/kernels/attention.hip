@@ -178,6 +178,7 @@ constexpr int NT8 = 512;
 constexpr int BM8 = 256;
 constexpr float DEFER = 8.f;
 
+template <bool DMA>
 __global__ __launch_bounds__(NT8, 1) void attn_fwd8_kernel(const bf16_t* __restrict__ q,
                                                           const bf16_t* __restrict__ k,
                                                           const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
@@ -209,11 +210,19 @@ __global__ __launch_bounds__(NT8, 1) void attn_fwd8_kernel(const bf16_t* __restr
   // tiles this wave needs: under the mask the ones starting at or before its last row
   const int wtiles = causal ? (q0w + 31) / BN + 1 : ntiles;
 
+  // K/V tiles: register-staged (DMA = false) or LDS-DMA issued from asm (variant 10: no staging
+  // registers, no store pass; the next tile lands under this tile's MFMAs)
   Stage<BN, NT8> ks, vs;
-  ks.load(kb, kvstride, tid);
-  vs.load(vb, kvstride, tid);
-  ks.store(smem, tid);
-  vs.store(smem + BN * CH, tid);
+  if constexpr (DMA) {
+    glds_tile_asm<BN, NT8>(kb, kvstride, smem, tid);
+    glds_tile_asm<BN, NT8>(vb, kvstride, smem + BN * CH, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    ks.load(kb, kvstride, tid);
+    vs.load(vb, kvstride, tid);
+    ks.store(smem, tid);
+    vs.store(smem + BN * CH, tid);
+  }
   __syncthreads();
 
   f32x16 oacc[NDT];
@@ -228,8 +237,14 @@ __global__ __launch_bounds__(NT8, 1) void attn_fwd8_kernel(const bf16_t* __restr
     const int kv0 = t * BN;
     const bool more = t + 1 < ntiles;
     if (more) {  // next tile's global loads fly under this tile's MFMAs
-      ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
-      vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      if constexpr (DMA) {  // into the buffer tile t-1 left (freed by the last barrier)
+        u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
+        glds_tile_asm<BN, NT8>(kb + (size_t)(t + 1) * BN * kvstride, kvstride, nk, tid);
+        glds_tile_asm<BN, NT8>(vb + (size_t)(t + 1) * BN * kvstride, kvstride, nk + BN * CH, tid);
+      } else {
+        ks.load(kb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+        vs.load(vb + (size_t)(t + 1) * BN * kvstride, kvstride, tid);
+      }
     }
     if (t < wtiles) {  // wave-uniform
       f32x16 sacc[2];
@@ -303,7 +318,9 @@ __global__ __launch_bounds__(NT8, 1) void attn_fwd8_kernel(const bf16_t* __restr
           for (int dt = 0; dt < NDT; ++dt) oacc[dt] = mfma(vv[s2][dt], pb[s2], oacc[dt]);
       }
     }
-    if (more) {
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1 landed
+    } else if (more) {
       u32x4* nk = smem + (cur ^ 1) * 2 * BN * CH;
       ks.store(nk, tid);
       vs.store(nk + BN * CH, tid);
@@ -1484,7 +1501,7 @@ int pto_attn_set_dkdv_variant(int v) {
 
 int pto_attn_set_variant(int fwd) {
   const int old = fwd_variant();
-  if (fwd == 4 || fwd == 8 || fwd == 9) g_fwd_variant = fwd;
+  if (fwd == 4 || fwd == 8 || fwd == 9 || fwd == 10) g_fwd_variant = fwd;
   return old;
 }
 
@@ -1500,7 +1517,8 @@ int pto_attn_fwd(const void* q, const void* k, const void* v, void* o, float* ls
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
                        causal);
   else if (fwd_variant() >= 8 && S % BM8 == 0)
-    hipLaunchKernelGGL(attn_fwd8_kernel, dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(fwd_variant() == 10 ? attn_fwd8_kernel<true> : attn_fwd8_kernel<false>,
+                       dim3((S / BM8) * B * Hq), dim3(NT8), 0, (hipStream_t)stream,
                        (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse2, B, S, Hq, Hkv, c,
                        causal);
   else

@@ -93,7 +93,7 @@ def _fwd(q, k, v, causal):
     return o, lse2
 
 
-@pytest.mark.parametrize("variant", [4, 8, 9])
+@pytest.mark.parametrize("variant", [4, 8, 9, 10])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal):
     """Both forward kernels on scores whose row maximum keeps growing along the keys (large,
@@ -126,12 +126,14 @@ def test_flash_forward_variants_agree(fwd_variant, shape):
     rounding; the two 8-wave kernels do the same per-row operations in the same order)."""
     q, k, v = _inputs(*shape, seed=5)
     outs = {}
-    for var in (4, 8, 9):
+    for var in (4, 8, 9, 10):
         fwd_variant(var)
         outs[var] = _fwd(q, k, v, True)
     assert _rel(outs[8][0], outs[4][0]) < 4e-3
     assert torch.allclose(outs[8][1], outs[4][1], atol=1e-3, rtol=1e-5)
     assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
+    # 10: the 8-wave forward with its K/V tiles staged by LDS-DMA (same LDS image, same math)
+    assert torch.equal(outs[10][0], outs[8][0]) and torch.equal(outs[10][1], outs[8][1])
 
 
 @pytest.mark.parametrize("dkdv", [1, 2, 3, 4, 6, 7, 8])
