@@ -1434,8 +1434,10 @@ __global__ __launch_bounds__(NT8, 1) void attn_bwd_dkdv8_kernel(
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// forward + dQ-pass variant: 8 = the 8-wave kernels where S % 256 == 0 (default), 9 = the same
-// with the ping-pong forward, 4 = the 4-wave ones;
+// forward + dQ-pass variant: 10 = the 8-wave forward with LDS-DMA K/V staging (default; 187 vs
+// 189 us, bit-identical, profiles/r4_attn_fwd_dma_ab.json), 8 = the 8-wave kernels where
+// S % 256 == 0 with register-staged K/V, 9 = the same with the ping-pong forward, 4 = the 4-wave
+// ones (the dQ-pass fallback of PTO_ATTN_DQ=8 follows: 8-wave for 8-10, 4-wave for 4);
 // PTO_ATTN_FWD in the environment or pto_attn_set_variant() (A/B runs, tests)
 int g_fwd_variant = -1;
 // dK/dV pass: 8 = software-pipelined across query tiles with AGPR-pinned accumulators
@@ -1471,7 +1473,7 @@ int dkdv_variant() {
 int fwd_variant() {
   if (g_fwd_variant < 0) {
     const char* e = getenv("PTO_ATTN_FWD");
-    g_fwd_variant = e != nullptr ? atoi(e) : 8;
+    g_fwd_variant = e != nullptr ? atoi(e) : 10;
   }
   return g_fwd_variant;
 }
