@@ -6,10 +6,11 @@ every rank builds the same Llama (tiny config), steps it with ``ZeroAdamW(reduce
 grad_view=True)`` and, from the same initial state, with ``grad_view=False``, on rank-dependent
 batches.  With grad_view the bf16 buckets hold the unscaled gradient sum and AdamW applies 1/W;
 the copy path scales each deposit by 1/W before the sum.  For a power-of-two W both are exact,
-so the gathered fp32 masters must be bit-identical; the process prints one JSON line
-per rank and exits 0 when they are.
+so the gathered fp32 masters must be bit-identical.  Each rank writes its result to
+``<out>/rank<r>.json`` (concurrent ranks share one stdout pipe, where their lines can interleave, so
+callers must read the files, not stdout); the process exits 0 when every rank agrees.
 
-    python -m torch.distributed.run --nproc-per-node 2 tools/zero_gv_check.py --backend gloo
+    python -m torch.distributed.run --nproc-per-node 2 tools/zero_gv_check.py --backend gloo --out DIR
 """
 import argparse
 import copy
@@ -27,6 +28,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--out", default=None, help="directory for rank<r>.json result files")
     a = ap.parse_args(argv)
     from pytorch_operator_amd.models.llama import CONFIGS, Llama
     from pytorch_operator_amd.ops.optim import to_bf16_matmul_weights
@@ -63,7 +65,12 @@ def main(argv=None):
     res = {"rank": rank, "world": world, "sinks": opts[0].sinks,
            "unscaled_buckets": sum(b.unscaled for b in opts[0].buckets),
            "masters_equal": d_view == d_copy, "weights_equal": weights_equal, "digest": d_view}
-    print(json.dumps(res), flush=True)
+    if a.out:
+        os.makedirs(a.out, exist_ok=True)
+        with open(os.path.join(a.out, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     ok = torch.tensor([1 if (res["masters_equal"] and weights_equal and res["sinks"] > 0) else 0], dtype=torch.int32)
     if a.backend == "nccl":
         ok = ok.to(dev)
