@@ -65,6 +65,11 @@ def parse_args(argv=None):
     p.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
                    help="DDP gradient path for world>1: xGMI peer-memory kernel fused with SGD "
                         "(self-tested at start-up, RCCL fallback) or RCCL all-reduce")
+    p.add_argument("--force-collectives", type=int,
+                   default=int(os.environ.get("PTO_FORCE_COLLECTIVES", "0") not in ("", "0")),
+                   help="world 1: still build a (single-rank) process group and issue the two bucket "
+                        "all-reduces every step, racing the RCCL step forms (their single-rank floor; "
+                        "not the headline configuration)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--job-latency", type=int, default=1,
                    help="after the timed region, run one PyTorchJob with one pod per GPU through "
@@ -92,7 +97,8 @@ def job_gpu_plan(world: int, job_gpus: str, job_backend: str):
     return gpus, backend
 
 
-def job_latency(world: int, rank: int, timeout: float, gpus=None, backend: str = "rccl") -> dict:
+def job_latency(world: int, rank: int, timeout: float, gpus=None, backend: str = "rccl",
+                extra_args=()) -> dict:
     """create->first-step / create->Succeeded of a real job (BASELINE's second metric):
     fake API server -> pytorch-operator binary -> kubelet emulator -> ``world`` worker pods,
     each pinned to one GPU (HIP_VISIBLE_DEVICES narrowed like the amd.com/gpu plugin).
@@ -105,7 +111,7 @@ def job_latency(world: int, rank: int, timeout: float, gpus=None, backend: str =
             sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "benchmarks"))
             from job_latency import measure
             r = measure(world, gpus=list(gpus) if gpus else list(range(world)), backend=backend,
-                        timeout=timeout)
+                        timeout=timeout, extra_args=tuple(extra_args))
             out = {"create_to_first_step_s": r["create_to_first_step_s"],
                    "create_to_running_s": r["create_to_running_s"],
                    "create_to_succeeded_s": r["create_to_succeeded_s"],
@@ -153,8 +159,10 @@ def main(argv=None):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from pytorch_operator_amd.parallel.dist import init_from_env
 
-    env = init_from_env(args.backend, use_gpu=True)
+    force = bool(args.force_collectives) and args.kernels == "hip"
+    env = init_from_env(args.backend, use_gpu=True, force_pg=force)
     world, rank, dev = env.world_size, env.rank, env.device
+    pg = dist.is_initialized()  # world > 1, or a forced single-rank group
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
@@ -172,12 +180,12 @@ def main(argv=None):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
         sync, xg, ar_path = None, None, "none"
-        if world > 1:
+        if world > 1 or force:
             from pytorch_operator_amd.models.mnist import flat_layout
             from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
             from pytorch_operator_amd.parallel.xgmi import try_xgmi
-            sync, ar_path = FlatGradAllReduce(), "rccl"
-            if args.allreduce != "rccl":
+            sync, ar_path = FlatGradAllReduce(force=force), "rccl"
+            if args.allreduce != "rccl" and world > 1:
                 xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
                               log=lambda m: print(m, file=sys.stderr) if rank == 0 else None)
         tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
@@ -190,8 +198,10 @@ def main(argv=None):
         spg = args.steps_per_graph if args.steps_per_graph > 0 else pick_steps_per_graph(args.steps, args.warmup)
         done_w = 0
         tune = None
-        if xg is not None and args.allreduce == "auto" and args.mode != "eager":
-            # measured choice between RCCL and the xGMI kernel (both trials are warm-up steps)
+        if (xg is not None or (force and sync is not None)) and args.allreduce == "auto" and \
+                args.mode != "eager":
+            # measured choice between the RCCL forms and the xGMI kernel (the trials are warm-up
+            # steps; forced at world 1 only the two RCCL forms race)
             from pytorch_operator_amd.parallel.autotune import choose_grad_sync
             tr.train_step()  # momentum initialisation + library load, outside any graph
             done_w = 1
@@ -242,13 +252,13 @@ def main(argv=None):
         xgmi_error = lambda: 0  # noqa: E731
 
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
@@ -271,7 +281,9 @@ def main(argv=None):
         dist.all_reduce(diff, op=dist.ReduceOp.MAX)
         in_sync = bool(float(diff.item()) == 0.0) and ar_err == 0
 
-    lat = job_latency(world, rank, args.job_timeout, *job_plan) if args.job_latency else {}
+    # a forced-collectives bench forces them in the job's pods too (their race lands in job.allreduce_trial)
+    lat = job_latency(world, rank, args.job_timeout, *job_plan,
+                      extra_args=("--force-collectives", "1") if force else ()) if args.job_latency else {}
 
     samples = steps * B * world
     value = samples / dt
@@ -301,8 +313,9 @@ def main(argv=None):
             "optimizer": "SGD(lr=0.01, momentum=0.5)",
             "kernels": args.kernels,
             "exec": mode_desc,
-            "backend": ("rccl" if env.backend == "nccl" else env.backend) if world > 1 else "none",
+            "backend": ("rccl" if env.backend == "nccl" else env.backend) if pg else "none",
             "grad_allreduce": ar_path,
+            "forced_collectives": force,
             "allreduce_trial": tune,
         },
     }
@@ -312,7 +325,7 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
     return 138 if ar_err else 0

@@ -73,6 +73,11 @@ def parse_args(argv=None):
                    help="HIP path, world>1: auto = time the xGMI peer-memory all-reduce fused with SGD "
                         "(self-tested) against RCCL at start-up and keep the faster (parallel/autotune.py); "
                         "xgmi / rccl force one")
+    p.add_argument("--force-collectives", type=int,
+                   default=int(os.environ.get("PTO_FORCE_COLLECTIVES", "0") not in ("", "0")),
+                   help="HIP path, world 1: build a single-rank process group anyway and issue the "
+                        "gradient all-reduces every step (--allreduce auto then races the RCCL step "
+                        "forms); env PTO_FORCE_COLLECTIVES")
     p.add_argument("--race-steps", type=int, default=40,
                    help="training steps each candidate of the --allreduce auto race runs (the state is "
                         "restored afterwards: the race does not change the trajectory)")
@@ -116,6 +121,9 @@ class _Emitter:
             elif event == "grad_allreduce":
                 self.info["grad_allreduce"] = kw.get("path", "")
                 self.wm.set("pto_worker_info", 1, replace=True, **self.info)
+                for k, v in (kw.get("trial") or {}).items():
+                    if k.endswith("_ms_per_step") and v is not None:
+                        self.wm.set("pto_worker_allreduce_trial_ms", v, candidate=k[:-len("_ms_per_step")])
             elif event == "xgmi_error":
                 self.wm.set("pto_worker_grad_exchange_errors", kw.get("code", 1))
             elif event == "train_done" and kw.get("accuracy") is not None:
@@ -200,7 +208,12 @@ def run(args, t_main_ns: Optional[int] = None) -> dict:
         torch.cuda.init()
         startup.mark("hip_init")
     torch.manual_seed(args.seed)
-    env = init_from_env(args.backend, use_gpu=use_cuda)
+    kernels = args.kernels
+    if kernels == "auto":
+        kernels = "hip" if use_cuda else "torch"
+    # forced collectives (HIP path): a single-rank group at world 1, all-reduces issued anyway
+    args.force_collectives = bool(args.force_collectives) and kernels == "hip"
+    env = init_from_env(args.backend, use_gpu=use_cuda, force_pg=args.force_collectives)
     rank, world, device = env.rank, env.world_size, env.device
     startup.mark("process_group")
     wm = None
@@ -213,9 +226,6 @@ def run(args, t_main_ns: Optional[int] = None) -> dict:
         emit("metrics_endpoint", port=port)
     if world > 1:
         print(f"Using distributed PyTorch with {args.backend} backend")
-    kernels = args.kernels
-    if kernels == "auto":
-        kernels = "hip" if use_cuda else "torch"
     if kernels == "hip" and not use_cuda:
         raise SystemExit("--kernels hip needs a GPU (drop --no-cuda or use --kernels torch)")
 
@@ -244,8 +254,8 @@ def run(args, t_main_ns: Optional[int] = None) -> dict:
         result = _train_torch(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, startup)
     writer.close()
     emit("train_done", **result)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     return result
@@ -380,14 +390,16 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, sta
     src = K.BatchSource(xtr, ytr, perm=perm, cursor=cursor)
     sync = xg = rccl = None
     race = False
-    if world > 1:
+    forced = bool(getattr(args, "force_collectives", False))
+    if world > 1 or forced:
         from ..models.mnist import flat_layout
         from ..parallel.xgmi import try_xgmi
-        rccl = FlatGradAllReduce()
+        rccl = FlatGradAllReduce(force=forced)
         xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
-                      timeout_s=args.xgmi_timeout) if args.allreduce != "rccl" else None
+                      timeout_s=args.xgmi_timeout) if args.allreduce != "rccl" and world > 1 else None
         sync = xg or rccl
-        race = xg is not None and args.allreduce == "auto" and not args.no_graph
+        # forced at world 1 there is no xGMI candidate: the two RCCL forms race
+        race = (xg is not None or forced) and args.allreduce == "auto" and not args.no_graph
         if not race:
             emit("grad_allreduce", path="xgmi" if xg is not None else "rccl")
         startup.mark("grad_sync")
@@ -453,7 +465,8 @@ def _train_hip(args, env, writer, emit, xtr, ytr, xte, yte, steps_per_epoch, sta
                 sync = runner.sync
                 emit("grad_allreduce", path=path, trial=trial)
             else:
-                whole = world == 1 or getattr(sync, "fused_sgd", False)  # one graph holds whole steps
+                # one graph holds whole steps unless RCCL collectives sit between the pieces
+                whole = sync is None or getattr(sync, "fused_sgd", False) or not getattr(sync, "active", True)
                 runner = GraphedStep(tr, mode="graph", steps_per_graph=log_iv if whole else 1, launch=args.launch)
             tr.flat_params.copy_(saved[0])
             tr.flat_momentum.copy_(saved[1])

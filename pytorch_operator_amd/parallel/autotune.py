@@ -10,7 +10,8 @@ The reference synchronises gradients with DDP's bucketed all-reduce
                 (``GraphedStep(mode="graph-comm")``; RCCL only -- gloo collectives are not
                 capturable, so with gloo this candidate is reported as skipped);
 ``xgmi``        the peer-memory exchange kernel fused with SGD (``parallel.xgmi``), one whole
-                step per kernel list.
+                step per kernel list.  ``xgmi_sync=None`` (no peer exchange: world 1 with forced
+                collectives, or a failed self-test) races the two RCCL forms alone.
 
 Whether the xGMI kernel beats RCCL for this 1.7 MB gradient is a property of the fabric the job
 lands on, so it is measured rather than assumed: every candidate runs ``trial_steps`` real DDP
@@ -60,7 +61,7 @@ def _timed(runner: GraphedStep, steps: int, device, name: str) -> float:
     return float(t.item())
 
 
-def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 10,
+def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: int = 10,
                      trial_steps: int = 60, force: Optional[str] = None,
                      launch: str = "stream") -> Tuple[GraphedStep, str, Dict]:
     """Returns (runner, path, record).  ``path`` is one of ``CANDIDATES``; ``record`` holds
@@ -77,7 +78,8 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
     steps = 0
     # the RCCL steps keep momentum for every parameter: make it whole if fused xGMI steps ran
     # before (a no-op when it already is)
-    xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+    if xgmi_sync is not None:
+        xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
     tr.grad_sync = rccl_sync
     r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=1, launch=launch)
     runners["rccl"] = r
@@ -106,12 +108,15 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
         else:
             skipped["rccl-graph"] = f"capture failed: {err or 'on another rank'}"
             torch.cuda.synchronize(dev)
-    tr.grad_sync = xgmi_sync
-    r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
-    runners["xgmi"] = r
-    t = _timed(r, trial, dev, "xgmi")
-    steps += r.internal_steps + trial
-    times["xgmi"] = float("inf") if xgmi_sync.xar.error() else t
+    if xgmi_sync is None:
+        skipped["xgmi"] = "no xGMI exchange (world 1 or self-test failed)"
+    else:
+        tr.grad_sync = xgmi_sync
+        r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
+        runners["xgmi"] = r
+        t = _timed(r, trial, dev, "xgmi")
+        steps += r.internal_steps + trial
+        times["xgmi"] = float("inf") if xgmi_sync.xar.error() else t
     if force is not None:
         if force not in runners:
             raise ValueError(f"force={force!r}: candidate not available ({skipped.get(force, 'unknown')})")
@@ -126,14 +131,15 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync, mode: str = "graph", spg: int = 1
     if int(lo.item()) != int(hi.item()):
         pick = "rccl"  # ranks disagree (cannot happen with shared numbers): the safe path
     if pick != "xgmi":
-        xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+        if xgmi_sync is not None:
+            xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
         tr.grad_sync = rccl_sync
     record = {f"{k.replace('-', '_')}_ms_per_step": (round(v / trial * 1e3, 4) if v != float("inf") else None)
               for k, v in times.items()}
     for k, why in skipped.items():
         record[f"{k.replace('-', '_')}_ms_per_step"] = None
         record[f"{k.replace('-', '_')}_skipped"] = why
-    if times["xgmi"] == float("inf"):
+    if times.get("xgmi") == float("inf"):
         record["xgmi_error"] = int(xgmi_sync.xar.error())
     record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,
                    "steps": steps})

@@ -14,6 +14,11 @@ the conv bucket (ready after the conv backward launch).  The fc all-reduce is
 issued on RCCL's stream while the conv backward kernel still runs; SGD waits for
 both (``finish``) and folds the 1/world average into its update.
 
+At world 1 the collectives are skipped unless ``force`` (or ``PTO_FORCE_COLLECTIVES=1``) is
+set: then both bucket all-reduces are really issued on the (single-rank) process group, so the
+RCCL step forms -- stream-launched pieces and the one-graph ``graph-comm`` step -- run under a
+real RCCL communicator on a one-GPU box (their single-rank floor; ``tools/rccl_w1_check.py``).
+
 ``BucketedDDP`` is the generic path for arbitrary ``nn.Module`` s (the ResNet /
 Llama configs, the CPU gloo plumbing): gradient hooks copy each parameter's grad
 into a flat bucket buffer in reverse-registration order and launch the bucket's
@@ -21,6 +26,7 @@ all-reduce the moment it fills, exactly one collective per bucket.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -28,19 +34,32 @@ import torch.distributed as dist
 import torch.nn as nn
 
 
+def forced_collectives() -> bool:
+    """``PTO_FORCE_COLLECTIVES=1``: issue the gradient collectives even at world 1."""
+    return os.environ.get("PTO_FORCE_COLLECTIVES", "0") not in ("", "0")
+
+
 class FlatGradAllReduce:
     """Two-bucket overlapped all-reduce hooks for ``FusedMnistTrainer``."""
 
-    def __init__(self, group=None, compress_bf16: bool = False):
+    def __init__(self, group=None, compress_bf16: bool = False, force: Optional[bool] = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.compress_bf16 = compress_bf16
+        if force is None:
+            force = forced_collectives()
+        if force and not dist.is_initialized():
+            raise RuntimeError("force=True needs an initialised process group (init_from_env(force_pg=True))")
+        # active: the bucket all-reduces are issued (always at world > 1; at world 1 only forced)
+        self.active = self.world > 1 or bool(force)
         self._works: List = []
         self._pending_copies: List = []
+        self.issued = 0  # bucket all-reduces issued from the host (a captured one counts once)
 
     def _launch(self, t: torch.Tensor) -> None:
-        if self.world == 1:
+        if not self.active:
             return
+        self.issued += 1
         if self.compress_bf16:
             tmp = t.to(torch.bfloat16)
             w = dist.all_reduce(tmp, group=self.group, async_op=True)

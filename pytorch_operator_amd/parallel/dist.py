@@ -61,9 +61,18 @@ def env_world_size() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def init_from_env(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
-                  timeout_s: float = 600.0) -> DistEnv:
-    """Initialise the default process group from the env contract (if WORLD_SIZE>1)."""
+                  timeout_s: float = 600.0, force_pg: bool = False) -> DistEnv:
+    """Initialise the default process group from the env contract (if WORLD_SIZE>1, or with
+    ``force_pg`` also at world 1: a single-rank group, e.g. to run RCCL collectives on one GPU;
+    a missing MASTER_ADDR/MASTER_PORT then defaults to 127.0.0.1 and a free port)."""
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     world = env_world_size()
@@ -82,9 +91,14 @@ def init_from_env(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
         device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
+    if force_pg and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("MASTER_PORT", "23456"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_pg) and not dist.is_initialized():
         kw = {}
         if b == "nccl" and use_gpu:
             kw["device_id"] = device

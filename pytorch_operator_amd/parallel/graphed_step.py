@@ -8,8 +8,8 @@ inside the SGD launch, so replays walk the dataset without host involvement.
 Modes
 -----
 ``eager``       plain launches (debugging / first step).
-``graph``       world == 1: one graph holding ``steps_per_graph`` whole steps.
-                world  > 1: three graphs per step -- G1 (forward + fc backward),
+``graph``       no collectives (world 1): one graph holding ``steps_per_graph`` whole steps.
+                RCCL collectives (world > 1, or forced at world 1): three graphs per step -- G1 (forward + fc backward),
                 G2 (conv backward), G3 (SGD) -- with the two bucket all-reduces
                 issued eagerly between them (the fc bucket's RCCL all-reduce
                 overlaps G2 on RCCL's own stream; G3 waits for both).  With
@@ -120,6 +120,9 @@ class GraphedStep:
         self.mode = mode
         self.steps_per_graph = max(1, int(steps_per_graph)) if mode != "eager" else 1
         self.world = trainer.grad_sync.world if trainer.grad_sync is not None else 1
+        # collectives issued per step: world > 1, or forced at world 1 (FlatGradAllReduce.active)
+        gs = trainer.grad_sync
+        self.collectives = gs is not None and bool(getattr(gs, "active", self.world > 1))
         self._graph = None   # timed graph: steps_per_graph whole steps
         self._warm = None    # one whole step (warm-up of any length)
         self._split = False  # RCCL three-graph step
@@ -132,7 +135,7 @@ class GraphedStep:
             tr.train_step()  # momentum initialisation happens outside any graph
             self.internal_steps += 1
         torch.cuda.synchronize(tr.device)
-        whole_step = self.world == 1 or getattr(tr.grad_sync, "fused_sgd", False)
+        whole_step = not self.collectives or getattr(tr.grad_sync, "fused_sgd", False)
         if not whole_step or mode == "graph-comm":
             # torch capture: RCCL collectives need torch's capture bookkeeping.  Warm the
             # allocator / RCCL on a side stream before capture (torch recommendation).

@@ -25,6 +25,7 @@ METRICS: Dict[str, Tuple[str, str]] = {
     "pto_worker_accuracy": ("gauge", "Test accuracy after the last epoch"),
     "pto_worker_first_step_unix_seconds": ("gauge", "Wall-clock time of this rank's first optimizer step"),
     "pto_worker_startup_phase_seconds": ("gauge", "Process start -> first step, per phase (label: phase)"),
+    "pto_worker_allreduce_trial_ms": ("gauge", "Start-up race: per-step ms of each DDP gradient-path candidate (label: candidate)"),
     "pto_worker_grad_exchange_errors": ("gauge", "Non-zero when the xGMI gradient exchange timed out (the worker then exits 138)"),
 }
 

@@ -570,3 +570,35 @@ def test_train_ckpt_resume_after_crash_keeps_the_fallback(tmp_path):
     assert sorted(os.listdir(d)) == ["meta.json", "step_5", "step_6"]
     with open(os.path.join(d, "meta.json")) as f:
         assert json.load(f)["complete"] == ["step_5", "step_6"]
+
+
+def test_flat_grad_allreduce_forced_at_world1_gloo():
+    """FlatGradAllReduce at world 1: inactive by default, all-reduces issued when forced on a
+    single-rank group (init_from_env(force_pg=True)); force without a group is an error."""
+    import torch
+    import torch.distributed as dist
+    from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
+    from pytorch_operator_amd.parallel.dist import init_from_env
+    assert not dist.is_initialized()
+    with pytest.raises(RuntimeError):
+        FlatGradAllReduce(force=True)
+    saved = {k: os.environ.pop(k, None) for k in ("WORLD_SIZE", "RANK", "MASTER_ADDR", "MASTER_PORT")}
+    try:
+        env = init_from_env("gloo", use_gpu=False, force_pg=True)
+        assert dist.is_initialized() and env.world_size == 1
+        off, on = FlatGradAllReduce(), FlatGradAllReduce(force=True)
+        assert not off.active and on.active
+        t = torch.arange(6, dtype=torch.float32)
+        for s in (off, on):
+            s.fc_ready(t[3:])
+            s.conv_ready(t[:3])
+            assert s.finish() == 1.0
+        assert off.issued == 0 and on.issued == 2
+        assert torch.equal(t, torch.arange(6, dtype=torch.float32))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v

@@ -49,9 +49,9 @@ def test_guide_worker_metrics_are_exported(tmp_path, capsys, monkeypatch):
     text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=10).read().decode()
     exported = _exported(text)
     # every series the training run could produce on a CPU world-1 job (no xGMI path, so no
-    # exchange-error series) is present; every metric is at least described
+    # exchange-error series; no gradient-path race, so no trial series) is present; every metric is at least described
     assert quoted - {"pto_worker_grad_exchange_errors", "pto_worker_samples_per_second",
-                     "pto_worker_step_seconds"} <= exported, quoted - exported
+                     "pto_worker_step_seconds", "pto_worker_allreduce_trial_ms"} <= exported, quoted - exported
     assert all(f"# TYPE {n} " in text for n in quoted)
     steps = float(re.search(r"^pto_worker_steps_total (\S+)$", text, re.M).group(1))
     assert steps == 10  # 640 / 64
