@@ -24,7 +24,9 @@
 //   F  conv_bwd        per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
 //                      dW_conv2 (MFMA + VALU rows), col2im + un-pool + ReLU mask ->
 //                      dz1 (LDS), dW_conv1 (VALU), per-sample slab rows
-//   G  slab_reduce_sgd deterministic slab reduction + SGD(momentum) on every parameter
+//   G  slab_reduce_sgd deterministic slab reduction + SGD(momentum) on every parameter; in the
+//                      world-1 step it also computes dW_fc1 / db_fc1 (fc1_bwd's job 1) and
+//                      applies their SGD straight from the MFMA accumulators
 // (A conv1_fwd_pool, B conv2_fwd_pool, conv_bwd (per-sample slab rows), sgd_momentum: the
 // unfused / eval / fallback building blocks.)
 //
@@ -1829,17 +1831,93 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(
 //   advances the device batch cursor.  Blocks past the reduction: plain SGD over a
 //   second, already-reduced range (p2/g2/buf2: the fc parameters).
 // ---------------------------------------------------------------------------
+// fc1.weight's gradient computed inside the tail (world-1 step, round 5): dW_fc1 = dh^T . a2
+// (K = B) tile by tile on MFMA -- the same tiles, lane mapping and summation order as
+// fc1_bwd's job 1, so the gradient bits are identical -- and SGD applied to the tile's float4s
+// straight from the accumulators.  fc1_bwd then runs only the dz2 / fc2 / staging jobs (its
+// span no longer waits for the dW_fc1 tiles), and the 1.6 MB gradient is neither stored by
+// fc1_bwd nor re-read here.  db_fc1 (the kt == 0 tiles' dh column sums) gets its SGD here too.
+struct TailW1 {
+  const float *dh, *a2;  // head's dh [B][500], conv12's a2 [B][800]
+  float *p, *m;          // fc1.weight then fc1.bias (p + 400000) params / momentum
+  float* g;              // optional: also store the gradient (fc1.weight, then fc1.bias)
+  int B, blocks;         // blocks: 400 (4 tiles of 16 x 16 per 256-thread block), 0 = off
+};
+constexpr int T_W1_BLOCKS = 1600 / 4;
+
+__device__ __forceinline__ void tail_w1_tile(const TailW1& tw, int tile, int lane, const SgdHyper& hy) {
+  const int i = lane & 15, g = lane >> 4;
+  const int B = tw.B;
+  const int nt = tile / 50, kt = tile - nt * 50;
+  const int n = nt * 16 + i, f = kt * 16 + i;
+  const bool nv = n < 500;
+  const int nc = nv ? n : 499;
+  // parameters + momentum of this lane's four outputs, in flight with the GEMM operand loads
+  const unsigned e4 = (unsigned)(nc * 200 + kt * 4 + g);
+  float4 pp = reinterpret_cast<const float4*>(tw.p)[e4];
+  float4 mm = reinterpret_cast<const float4*>(tw.m)[e4];
+  const bool bl = kt == 0 && g == 0;  // this lane also updates fc1.bias[n]
+  float bp = 0.f, bm = 0.f;
+  if (bl) { bp = tw.p[400000 + nc]; bm = tw.m[400000 + nc]; }
+  f32x4 c0 = zero4(), c1 = zero4();
+  float dbsum = 0.f;
+  for (int base = 0; base < B; base += 64) {
+    float av[16], fv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int bb = min(base + 4 * s + g, B - 1);
+      av[s] = tw.dh[(size_t)bb * 500 + nc];
+      fv[s] = tw.a2[(size_t)bb * 800 + f];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool bv = base + 4 * s + g < B;
+      const float x = (bv && nv) ? av[s] : 0.f;
+      dbsum += x;
+      const float fb = bv ? fv[s] : 0.f;
+      if (s & 1) c1 = mfma16x16x4(fb, x, c1);
+      else c0 = mfma16x16x4(fb, x, c0);
+    }
+  }
+  const f32x4 c = c0 + c1;
+  if (nv) {
+    const float4 gg = make_float4(c[0], c[1], c[2], c[3]);
+    if (tw.g != nullptr) reinterpret_cast<float4*>(tw.g)[e4] = gg;
+    sgd4(pp, mm, gg, hy);
+    reinterpret_cast<float4*>(tw.p)[e4] = pp;
+    reinterpret_cast<float4*>(tw.m)[e4] = mm;
+  }
+  if (kt == 0) {
+    dbsum = sum_lane_rows(dbsum);
+    if (bl && nv) {
+      if (tw.g != nullptr) tw.g[400000 + n] = dbsum;
+      sgd_elem(bp, bm, dbsum, hy);
+      tw.p[400000 + n] = bp;
+      tw.m[400000 + n] = bm;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     const float* __restrict__ P, SlabRows sr, int n, int stride, float* __restrict__ gout,
     float* __restrict__ p, float* __restrict__ buf, SgdHyper hy, int* __restrict__ step_counter,
     float* __restrict__ p2, const float* __restrict__ g2, float* __restrict__ buf2, int n2,
-    int red_blocks, u64* dbg) {
+    int red_blocks, TailW1 tw, u64* dbg) {
   __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
-  if ((int)blockIdx.x >= red_blocks) {
+  // block ids: [0, tw.blocks) the fc1.weight tiles (the longest blocks, dispatched first), then
+  // the slab reduction, then the plain SGD range
+  int blk = blockIdx.x;
+  if (blk < tw.blocks) {
+    tail_w1_tile(tw, blk * 4 + (tid >> 6), tid & 63, hy);
+    stamp(dbg, 1);
+    return;
+  }
+  blk -= tw.blocks;
+  if (blk >= red_blocks) {
     // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
-    const int v = (blockIdx.x - red_blocks) * 256 + tid;
+    const int v = (blk - red_blocks) * 256 + tid;
     if (v < (n2 >> 2)) {
       float4 pp = reinterpret_cast<float4*>(p2)[v];
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];
@@ -1851,7 +1929,7 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     stamp(dbg, 1);
     return;
   }
-  const int col = blockIdx.x * SR_COLS + (tid % SR_COLS);
+  const int col = blk * SR_COLS + (tid % SR_COLS);
   const int slice = tid / SR_COLS;
   const int n4 = n >> 2;
   const int cc = min(col, n4 - 1);
@@ -1872,7 +1950,7 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
     reinterpret_cast<float4*>(p)[col] = pp;
     reinterpret_cast<float4*>(buf)[col] = bb;
   }
-  if (step_counter != nullptr && blockIdx.x == 0 && tid == 0) atomicAdd(step_counter, 1);
+  if (step_counter != nullptr && blk == 0 && tid == 0) atomicAdd(step_counter, 1);
   stamp(dbg, 1);
 }
 
@@ -2159,17 +2237,18 @@ int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, con
   return fc1_bwd_launch(a, stream);
 }
 
-// fc1_bwd (every job) + next-batch staging blocks.
+// fc1_bwd (jobs: 7, or 6 when the tail computes dW_fc1) + next-batch staging blocks.
 int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                             const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                             float* gb2, float* dz2, const float* per_sample, float* stats,
                             float loss_scale, int B, const void* nx, const int* nlabels, const int* nperm,
-                            const int* ncursor, int n_total, int stage_adv, uint8_t* stage_x, int* stage_lab,
-                            int* stage_tag, void* stream) {
+                            const int* ncursor, int n_total, int stage_adv, int jobs, uint8_t* stage_x,
+                            int* stage_lab, int* stage_tag, void* stream) {
   Fc1Bwd a{};
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
-  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
+  a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = jobs; a.B = B;
+  if ((jobs & 6) != 6) return -1;  // staging rides with the dz2 and fc2 jobs
   if (stage_x == nullptr) return -1;
   a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
   a.stage_adv = stage_adv;
@@ -2247,8 +2326,38 @@ int pto_slab_reduce_sgd(const float* P, int B, int n, int stride, float* gout, f
   const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
   const int blocks = red_blocks + (n2 / 4 + 255) / 256;
   const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  const TailW1 tw{};
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
-                     sr, n, stride, gout, p, buf, hy, step_counter, p2, g2, buf2, n2, red_blocks, dbg_next());
+                     sr, n, stride, gout, p, buf, hy, step_counter, p2, g2, buf2, n2, red_blocks, tw, dbg_next());
+  return (int)hipGetLastError();
+}
+
+// The tail with fc1.weight's gradient computed in it (TailW1): as pto_slab_reduce_sgd, plus
+// dW_fc1 = dh^T . a2 (dh [B][500], a2 [B][800]) and SGD on w1p/w1m [400000 + 500: fc1.weight
+// then fc1.bias] (w1g: optional gradient output of the same layout).  The plain SGD range
+// p2/g2/buf2 then covers only the parameters after fc1.bias.
+int pto_slab_reduce_sgd_w1(const float* P, int B, int n, int stride, float* gout, float* p,
+                           float* buf, float lr, float momentum, float dampening, float wd,
+                           float grad_scale, int nesterov, int first_step, int* step_counter,
+                           float* p2, const float* g2, float* buf2, int n2, int rows_big, int big_lo,
+                           int big_hi, const float* dh, const float* a2, float* w1p, float* w1m, float* w1g,
+                           void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if (n2 < 0 || (n2 & 3) || (n2 > 0 && (p2 == nullptr || g2 == nullptr || buf2 == nullptr)))
+    return -1;
+  if (dh == nullptr || a2 == nullptr || w1p == nullptr || w1m == nullptr) return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) | ((uintptr_t)p2) |
+       ((uintptr_t)g2) | ((uintptr_t)buf2) | ((uintptr_t)w1p) | ((uintptr_t)w1m) | ((uintptr_t)w1g)) & 15)
+    return -2;
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
+  const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
+  const int blocks = T_W1_BLOCKS + red_blocks + (n2 / 4 + 255) / 256;
+  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  const TailW1 tw{dh, a2, w1p, w1m, w1g, B, T_W1_BLOCKS};
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
+                     sr, n, stride, gout, p, buf, hy, step_counter, p2, g2, buf2, n2, red_blocks, tw, dbg_next());
   return (int)hipGetLastError();
 }
 

@@ -12,6 +12,7 @@ pre-allocated workspaces, and a whole step can be captured into one hipGraph.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -150,6 +151,11 @@ class FusedMnistTrainer:
         self.fuse_conv12 = True
         self.conv_chunk = 4
         self.stage_batches = True
+        #   w1_tail: the single-process step computes dW_fc1 / db_fc1 in the tail launch and
+        #            applies SGD from the accumulators (fc1_bwd runs only dz2 + fc2 + staging);
+        #            materialize_fc1_grad: the tail also stores that gradient into flat_grads
+        self.w1_tail = os.environ.get("PTO_W1_TAIL", "1") != "0"
+        self.materialize_fc1_grad = False
 
     # ---------------------------------------------------------------- state
     @property
@@ -253,7 +259,8 @@ class FusedMnistTrainer:
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
-    def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None, xpush: Optional[tuple] = None) -> None:
+    def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None, xpush: Optional[tuple] = None,
+                 jobs: Optional[int] = None) -> None:
         """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv;
         with ``xpush``, also push dW_fc1 to its xGMI owners (ops.mnist.fc1_bwd)."""
         K, p, g = self.K, self._pv, self.grads
@@ -261,7 +268,8 @@ class FusedMnistTrainer:
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
                   dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
-                  loss_scale=1.0 / B, jobs=K.FC1_BWD_ALL, src=self.source if st is not None else None,
+                  loss_scale=1.0 / B, jobs=K.FC1_BWD_ALL if jobs is None else jobs,
+                  src=self.source if st is not None else None,
                   stage=st, stage_adv=stage_adv or 0, xpush=xpush)
 
     def _conv_bwd(self, B: int) -> None:
@@ -351,15 +359,20 @@ class FusedMnistTrainer:
         ce = self.layout.conv_end
         self.forward(source, B)
         self._head(B)
-        self._fc1_bwd(B, stage_adv=1 if advance_cursor else 0)
+        w1t = self.w1_tail
+        self._fc1_bwd(B, stage_adv=1 if advance_cursor else 0,
+                      jobs=(K.FC1_BWD_DGRAD | K.FC1_BWD_FC2) if w1t else None)
         self._conv_bwd(B)
+        e0 = self.layout.offsets["fc2.weight"] if w1t else ce  # the plain-SGD range
+        w1 = (self.dh[:B], self.a2[:B], self._fp[ce:e0], self._fm[ce:e0],
+              self.flat_grads[ce:e0] if self.materialize_fc1_grad else None) if w1t else None
         K.slab_reduce_sgd_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce],
                            self._fm[:ce], lr=self.lr, momentum=self.momentum,
                            dampening=self.dampening, weight_decay=self.weight_decay,
                            nesterov=self.nesterov, first_step=self._first_step,
                            step_counter=self.cursor if advance_cursor else None,
-                           extra=(self._fp[ce:], self.flat_grads[ce:], self._fm[ce:]),
-                           big=self._slab_big(B))
+                           extra=(self._fp[e0:], self.flat_grads[e0:], self._fm[e0:]),
+                           big=self._slab_big(B), w1=w1)
         self._first_step = False
 
     def loss(self) -> float:

@@ -137,7 +137,9 @@ _SIGNATURES = {
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_synth": [_VP, _VP, _VP, _I, ctypes.c_uint, _F, _VP],
     "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
-    "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP],
+    "pto_slab_reduce_sgd_w1": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
+                               _VP, _VP, _VP, _I, _I, _I, _I] + [_VP] * 6,
     "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     # xgmi_allreduce.hip

@@ -346,15 +346,15 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     if per_sample is not None:
         _req(per_sample, (B, 2), torch.float32, "per_sample")
     if stage is not None:
-        if jobs != FC1_BWD_ALL or src is None or not BatchStage.supported(src):
-            raise ValueError("staging needs jobs=FC1_BWD_ALL and a uint8 BatchSource with labels, perm, cursor")
+        if jobs not in (FC1_BWD_ALL, FC1_BWD_DGRAD | FC1_BWD_FC2) or src is None or not BatchStage.supported(src):
+            raise ValueError("staging needs jobs DGRAD|FC2 (+WGRAD) and a uint8 BatchSource with labels, perm, cursor")
         if stage.B < B or src.x.data_ptr() % 16:
             raise ValueError("stage too small or unaligned source")
         rc = lib.pto_mnist_fc1_bwd_stage(
             dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
             gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
             _ptr(stats), float(loss_scale), B, src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(),
-            src.cursor.data_ptr(), src.n_total, int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(),
+            src.cursor.data_ptr(), src.n_total, int(stage_adv), int(jobs), stage.x.data_ptr(), stage.lab.data_ptr(),
             stage.tag.data_ptr(), _stream())
         _native.check(rc, "fc1_bwd(stage)")
         return dz2
@@ -489,12 +489,17 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
                      dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
                      grad_scale: float = 1.0, first_step: bool = False,
                      step_counter: Optional[torch.Tensor] = None,
-                     extra: Optional[tuple] = None, big: Optional[tuple] = None) -> None:
+                     extra: Optional[tuple] = None, big: Optional[tuple] = None,
+                     w1: Optional[tuple] = None) -> None:
     """grads = sum_b slab[b, :n]; then SGD(momentum) on params/buf[:n] (one launch).
 
     ``extra=(params2, grads2, buf2)``: also apply the same SGD to a second,
     already-reduced range in the same launch (e.g. the fc parameters).
     ``big=(rows, lo, hi)``: columns [lo, hi) sum only their first ``rows`` rows.
+    ``w1=(dh, a2, params_w1, buf_w1, grads_w1 or None)``: also compute fc1's weight / bias
+    gradient (dh^T . a2 and dh's column sums, fc1_bwd's job 1, bit-identical) in this launch and
+    apply SGD to it (``params_w1`` = fc1.weight followed by fc1.bias); ``extra`` must then
+    exclude those two.
     """
     lib = _native.load()
     n = params.numel()
@@ -513,6 +518,21 @@ def slab_reduce_sgd_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: to
             if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n2:
                 raise ValueError(f"{nm} must be contiguous fp32 with {n2} elements")
     rb, lo, hi = big if big is not None else (B, 0, 0)
+    if w1 is not None:
+        dh, a2, w1p, w1m, w1g = w1
+        _req(dh, (B, 500), torch.float32, "dh")
+        _req(a2, (B, 800), torch.float32, "a2")
+        for t, nm in ((w1p, "fc1 params"), (w1m, "fc1 momentum")) + (((w1g, "fc1 grads"),) if w1g is not None else ()):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < 400500:
+                raise ValueError(f"{nm}: contiguous fp32 [fc1.weight (400000) | fc1.bias (500)] expected")
+        rc = lib.pto_slab_reduce_sgd_w1(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
+                                        params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
+                                        float(dampening), float(weight_decay), float(grad_scale),
+                                        int(nesterov), int(first_step), _ptr(step_counter), _ptr(p2),
+                                        _ptr(g2), _ptr(b2), n2, int(rb), int(lo), int(hi), dh.data_ptr(),
+                                        a2.data_ptr(), w1p.data_ptr(), w1m.data_ptr(), _ptr(w1g), _stream())
+        _native.check(rc, "slab_reduce_sgd(w1)")
+        return
     rc = lib.pto_slab_reduce_sgd(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(),
                                  params.data_ptr(), buf.data_ptr(), float(lr), float(momentum),
                                  float(dampening), float(weight_decay), float(grad_scale),

@@ -341,8 +341,8 @@ def test_round3_step_matches_round2_step(lib, B):
     n = 8 * B
     x, y = _data(n, seed=300 + B, n_total=n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(5)).to(torch.int32)
-    new = _stage_trainer(x, y, perm, B=B)
-    old = _stage_trainer(x, y, perm, B=B, conv_chunk=1, stage_batches=False)
+    new = _stage_trainer(x, y, perm, B=B, materialize_fc1_grad=True)
+    old = _stage_trainer(x, y, perm, B=B, conv_chunk=1, stage_batches=False, w1_tail=False)
     for _ in range(5):
         new.train_step()
         old.train_step()
@@ -371,3 +371,26 @@ def test_on_device_synthetic_dataset_is_deterministic_and_mnist_like(lib):
     assert abs(ma - mc) < 0.05 * mc, (ma, mc)
     counts = torch.bincount(a.labels.long().cpu(), minlength=10)
     assert int(counts.min()) > 1700 and sorted(a.perm.cpu().tolist()) == list(range(20000))
+
+
+@pytest.mark.parametrize("B", [64, 37])
+def test_w1_tail_is_bit_identical_to_fc1_bwd_wgrad(lib, B):
+    """Round 5: dW_fc1 / db_fc1 computed in the tail launch with SGD straight from the MFMA
+    accumulators (fc1_bwd runs only dz2 + fc2 + staging) trains bit-identically to fc1_bwd's
+    weight-gradient job + the tail's plain SGD, and the materialised gradient has the same bits."""
+    n = 12 * B
+    x, y = _data(n, seed=500 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(9)).to(torch.int32)
+    a = _stage_trainer(x, y, perm, B=B, w1_tail=True, materialize_fc1_grad=True)
+    b = _stage_trainer(x, y, perm, B=B, w1_tail=False)
+    for _ in range(10):
+        a.train_step()
+        b.train_step()
+    torch.cuda.synchronize()
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 10
+    assert torch.equal(a.flat_params, b.flat_params)
+    assert torch.equal(a.flat_momentum, b.flat_momentum)
+    assert torch.equal(a.stats, b.stats)
+    o1, o2 = a.layout.offsets["fc1.weight"], a.layout.offsets["fc1.bias"]
+    assert torch.equal(a.flat_grads[o1:o1 + 400000], b.flat_grads[o1:o1 + 400000])
+    assert torch.equal(a.flat_grads[o2:o2 + 500], b.flat_grads[o2:o2 + 500])
