@@ -1,5 +1,5 @@
-// Flash-attention backward, dK/dV pass, software-pipelined across query tiles (dK/dV variant 8
-// of attention.hip's pto_attn_bwd).  Its own translation unit: its dK / dV accumulators are
+// Flash-attention backward, dK/dV pass, software-pipelined across query tiles (the default dK/dV
+// pass of attention.hip's pto_attn_bwd), and the dQ pass in the same form.  Its own translation unit: its dK / dV accumulators are
 // pinned in AGPRs by hand-written MFMAs (below), and everything the compiler allocates fits the
 // 256 architectural VGPRs.
 #include "attention_common.h"
@@ -12,52 +12,34 @@ namespace {
 // clobbers all 128 so nothing of the compiler's is kept there (checked in the ISA: no compiler
 // v_accvgpr_* in the kernel).  Hazards: the accumulate chains are MFMA -> MFMA (C = previous D:
 // none); every VALU-written operand (the bf16-packed P and dS) is packed at least two gaps
-// before the MFMA that reads it (the schedule below), so no `s_nop` pad is needed (PAD keeps
-// one for A/B); the epilogue waits out the last MFMA before reading (acc_read).
+// before the MFMA that reads it (the schedule below), so no `s_nop` pad is needed
+// (tests/test_attention_isa.py checks the distance in the built code object); the epilogue
+// waits out the last MFMA before reading (acc_read).
 #define PTO_AGPR_CLOBBERS "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63","a64","a65","a66","a67","a68","a69","a70","a71","a72","a73","a74","a75","a76","a77","a78","a79","a80","a81","a82","a83","a84","a85","a86","a87","a88","a89","a90","a91","a92","a93","a94","a95","a96","a97","a98","a99","a100","a101","a102","a103","a104","a105","a106","a107","a108","a109","a110","a111","a112","a113","a114","a115","a116","a117","a118","a119","a120","a121","a122","a123","a124","a125","a126","a127"
-// Diagnostic ablations of the dK/dV pipeline (wrong results, in-bounds accesses; A/B builds
-// only): 1 no dS arithmetic, 2 row reads in place of the transposed reads, 4 no per-tile DMA,
-// 8 no per-tile barrier, 16 no exp2
-#ifndef PTO_PIPE_ABL
-#define PTO_PIPE_ABL 0
-#endif
-#ifndef PTO_PIPE_STAT4  // 1: lse2 / delta staged once per four query tiles
-#define PTO_PIPE_STAT4 0
-#endif
-#ifndef PTO_PIPE_EPIW  // 1: the epilogue stages each wave's rows without block barriers
-#define PTO_PIPE_EPIW 1
-#endif
-#ifndef PTO_PIPE_DMA0  // gap of the first of a tile's five LDS-DMA pieces, and the spacing
-#define PTO_PIPE_DMA0 8
-#endif
-#ifndef PTO_PIPE_DMAS
-#define PTO_PIPE_DMAS 1
-#endif
-#ifndef PTO_PIPE_PAD  // 1: s_nop 1 before the first MFMA of each k-step (8 us slower, no effect on
-#define PTO_PIPE_PAD 0  // the results: profiles/r4_attn_dkdv_pipe_knobs_ab.json)
-#endif
+// Round-4 ablation and placement knobs (no dS / exp2 / DMA / barrier; lse2 staged per four tiles;
+// DMA start gap and spacing; an s_nop pad before each k-step's first MFMA; barrier-staged
+// epilogue) were measured and are recorded in profiles/r4_attn_dkdv_pipe_ablations.md and
+// r4_attn_dkdv_pipe_knobs_ab.json; the source keeps only the chosen settings (git show 3eed2ef
+// for the knobbed form).
+constexpr int DMA0 = 8;  // gap of the first of a tile's five LDS-DMA pieces (one per gap after it)
 #define PTO_AGPR_CLOBBERS_0_63 "a0","a1","a2","a3","a4","a5","a6","a7","a8","a9","a10","a11","a12","a13","a14","a15","a16","a17","a18","a19","a20","a21","a22","a23","a24","a25","a26","a27","a28","a29","a30","a31","a32","a33","a34","a35","a36","a37","a38","a39","a40","a41","a42","a43","a44","a45","a46","a47","a48","a49","a50","a51","a52","a53","a54","a55","a56","a57","a58","a59","a60","a61","a62","a63"
 #define PTO_ZERO_0_63 "v_accvgpr_write_b32 a0, 0\n\tv_accvgpr_write_b32 a1, 0\n\tv_accvgpr_write_b32 a2, 0\n\tv_accvgpr_write_b32 a3, 0\n\tv_accvgpr_write_b32 a4, 0\n\tv_accvgpr_write_b32 a5, 0\n\tv_accvgpr_write_b32 a6, 0\n\tv_accvgpr_write_b32 a7, 0\n\tv_accvgpr_write_b32 a8, 0\n\tv_accvgpr_write_b32 a9, 0\n\tv_accvgpr_write_b32 a10, 0\n\tv_accvgpr_write_b32 a11, 0\n\tv_accvgpr_write_b32 a12, 0\n\tv_accvgpr_write_b32 a13, 0\n\tv_accvgpr_write_b32 a14, 0\n\tv_accvgpr_write_b32 a15, 0\n\tv_accvgpr_write_b32 a16, 0\n\tv_accvgpr_write_b32 a17, 0\n\tv_accvgpr_write_b32 a18, 0\n\tv_accvgpr_write_b32 a19, 0\n\tv_accvgpr_write_b32 a20, 0\n\tv_accvgpr_write_b32 a21, 0\n\tv_accvgpr_write_b32 a22, 0\n\tv_accvgpr_write_b32 a23, 0\n\tv_accvgpr_write_b32 a24, 0\n\tv_accvgpr_write_b32 a25, 0\n\tv_accvgpr_write_b32 a26, 0\n\tv_accvgpr_write_b32 a27, 0\n\tv_accvgpr_write_b32 a28, 0\n\tv_accvgpr_write_b32 a29, 0\n\tv_accvgpr_write_b32 a30, 0\n\tv_accvgpr_write_b32 a31, 0\n\tv_accvgpr_write_b32 a32, 0\n\tv_accvgpr_write_b32 a33, 0\n\tv_accvgpr_write_b32 a34, 0\n\tv_accvgpr_write_b32 a35, 0\n\tv_accvgpr_write_b32 a36, 0\n\tv_accvgpr_write_b32 a37, 0\n\tv_accvgpr_write_b32 a38, 0\n\tv_accvgpr_write_b32 a39, 0\n\tv_accvgpr_write_b32 a40, 0\n\tv_accvgpr_write_b32 a41, 0\n\tv_accvgpr_write_b32 a42, 0\n\tv_accvgpr_write_b32 a43, 0\n\tv_accvgpr_write_b32 a44, 0\n\tv_accvgpr_write_b32 a45, 0\n\tv_accvgpr_write_b32 a46, 0\n\tv_accvgpr_write_b32 a47, 0\n\tv_accvgpr_write_b32 a48, 0\n\tv_accvgpr_write_b32 a49, 0\n\tv_accvgpr_write_b32 a50, 0\n\tv_accvgpr_write_b32 a51, 0\n\tv_accvgpr_write_b32 a52, 0\n\tv_accvgpr_write_b32 a53, 0\n\tv_accvgpr_write_b32 a54, 0\n\tv_accvgpr_write_b32 a55, 0\n\tv_accvgpr_write_b32 a56, 0\n\tv_accvgpr_write_b32 a57, 0\n\tv_accvgpr_write_b32 a58, 0\n\tv_accvgpr_write_b32 a59, 0\n\tv_accvgpr_write_b32 a60, 0\n\tv_accvgpr_write_b32 a61, 0\n\tv_accvgpr_write_b32 a62, 0\n\tv_accvgpr_write_b32 a63, 0"
-template <int A0, bool PAD>
+template <int A0>
 __device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
-  if constexpr (PAD && PTO_PIPE_PAD)
-    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
-                 :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
-  else
-    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
-                 :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
+  asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
+               :: "v"(a), "v"(b), "i"(A0), "i"(A0 + 15) : PTO_AGPR_CLOBBERS);
 }
 // tile `slot` (0-3 dV^T, 4-7 dK^T); a constant after unrolling, so the switch folds away
 __device__ __forceinline__ void mfma_acc_slot(int slot, const bf16x8& a, const bf16x8& b) {
   switch (slot) {
-    case 0: mfma_acc<0, true>(a, b); break;
-    case 1: mfma_acc<16, false>(a, b); break;
-    case 2: mfma_acc<32, false>(a, b); break;
-    case 3: mfma_acc<48, false>(a, b); break;
-    case 4: mfma_acc<64, true>(a, b); break;
-    case 5: mfma_acc<80, false>(a, b); break;
-    case 6: mfma_acc<96, false>(a, b); break;
-    default: mfma_acc<112, false>(a, b); break;
+    case 0: mfma_acc<0>(a, b); break;
+    case 1: mfma_acc<16>(a, b); break;
+    case 2: mfma_acc<32>(a, b); break;
+    case 3: mfma_acc<48>(a, b); break;
+    case 4: mfma_acc<64>(a, b); break;
+    case 5: mfma_acc<80>(a, b); break;
+    case 6: mfma_acc<96>(a, b); break;
+    default: mfma_acc<112>(a, b); break;
   }
 }
 __device__ __forceinline__ void acc_zero() {
@@ -115,10 +97,7 @@ __device__ unsigned long long g_pipe_stamps[8192 * 16];
 #define PTO_STAMP(k)
 #define PTO_RSTAMP(k)
 #endif
-#ifndef PTO_PIPE_TLEAD
-#define PTO_PIPE_TLEAD 4
-#endif
-constexpr int TLEAD = PTO_PIPE_TLEAD;  // gaps between a transposed operand read and its MFMA
+constexpr int TLEAD = 4;  // gaps between a transposed operand read and its MFMA
 __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse2, const float* __restrict__ delta,
@@ -126,15 +105,8 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     int causal) {
   constexpr int NB = 3, TILE = 2 * QT * CH;
   __shared__ u32x4 qd[NB * TILE];                   // [buf][Q | dO] (48 KB); dK/dV epilogue
-#if PTO_PIPE_STAT4
-  // lse2 / delta of four consecutive query tiles (one head) per slot, two slots: one 1 KiB
-  // LDS-DMA per four tiles instead of a 256-byte piece per tile from every wave
-  __shared__ __align__(16) float stat4[2][2][4 * QT];  // [slot][lse2 | delta][4 tiles x 32 rows]
-  constexpr int SDOFF = 4 * QT;                          // lse2 -> delta of the same rows
-#else
   __shared__ __align__(16) float stat[NB][2 * QT];  // [buf][lse2 | delta]
   constexpr int SDOFF = QT;
-#endif
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int kblk = (int)blockIdx.x / (B * Hkv), bh = (int)blockIdx.x % (B * Hkv);
@@ -175,19 +147,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     soff = ((size_t)b * Hq + hq) * S + (size_t)qt * QT;
   };
   const unsigned lds_w = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(qd + 64 * wu));  // this wave's piece 0
-#if PTO_PIPE_STAT4
-  // the statistics of the four tiles starting at tile t4 (a multiple of 4; nqt is one too, so the
-  // group stays in one head) into slot `slot`: lanes 0-31 lse2, 32-63 delta, 4 rows per lane
-  auto dma_stat4 = [&](int slot, int t4) {
-    t4 = t4 < ntiles ? t4 : ntiles - 4;
-    const int g = t4 / nqt, qt = qt0 + t4 % nqt, hq = hk * G + g;
-    const float* src = (lane < 32 ? lse2 : delta) + ((size_t)b * Hq + hq) * S + (size_t)qt * QT + 4 * (lane & 31);
-    const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&stat4[slot][0][0]));
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                 :: "s"(dst), "v"(src) : "memory", "m0");
-  };
-  auto stat_ptr = [&](int t) -> const float* { return &stat4[(t >> 2) & 1][0][(t & 3) * QT]; };
-#endif
   auto dma = [&](int buf, int piece, size_t toff, size_t soff) {
     if (piece < 4) {
       const int i = piece & 1;
@@ -196,9 +155,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
                    :: "s"(dst), "v"(src) : "memory", "m0");
     } else {
-#if !PTO_PIPE_STAT4
       glds_dword_asm(sbase + soff, stat[buf]);
-#endif
     }
   };
 
@@ -220,14 +177,9 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     const u32x4* Ds = Qs + QT * CH;
     const u32x4* Qn = qd + NXT * TILE;
     const u32x4* Dn = Qn + QT * CH;
-#if PTO_PIPE_STAT4
-    const float* st = stat_ptr(t);
-    const float* stn = stat_ptr(t + 1);
-#else
     const float* st = stat[CUR];
     const float* stn = stat[NXT];
     (void)t;
-#endif
     f32x16 pa = zero16();
     sout = zero16();
     bf16x8 qa[NDS], td[8], tq[8], pb[2], db[2];
@@ -261,7 +213,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       }
       if (j >= 1 && j <= 16) {
         const int i = j - 1;
-        float p = (PTO_PIPE_ABL & 16) ? sin[i] : __builtin_amdgcn_exp2f(sin[i]);
+        float p = __builtin_amdgcn_exp2f(sin[i]);
         if (MASK && (i & 3) + 8 * (i >> 2) < lim) p = 0.f;  // key > query
         sin[i] = p;
       }
@@ -281,15 +233,13 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
           const int i = 2 * m + e2, ei = i & 3;
           const float4 d4 = D4[i >> 2];
           const float Dv = ei == 0 ? d4.x : ei == 1 ? d4.y : ei == 2 ? d4.z : d4.w;
-          if (!(PTO_PIPE_ABL & 1)) pa[i] = pa[i] - Dv;
+          pa[i] = pa[i] - Dv;
         }
       }
       if (j >= 17 && j < 25) {
         const int m = j - 17;
-        if (!(PTO_PIPE_ABL & 1)) {
-          pa[2 * m] = sin[2 * m] * pa[2 * m];
-          pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
-        }
+        pa[2 * m] = sin[2 * m] * pa[2 * m];
+        pa[2 * m + 1] = sin[2 * m + 1] * pa[2 * m + 1];
       }
       if (j >= 18 && j < 26) {
         const int m = j - 18;
@@ -308,22 +258,18 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
         qa[2 * (j - 4) + 1] = row_frag(Qn, r, 4 * (j - 4) + 2 + h);
       }
       if (j >= 16 - TLEAD && j < 24 - TLEAD)
-        td[j - 16 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Ds, (16 * ((j - 16 + TLEAD) >> 2) + r) & 31, (j - 16 + TLEAD) & 3)
-                                                : tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
+        td[j - 16 + TLEAD] = tr_frag(Ds, 16 * ((j - 16 + TLEAD) >> 2), ((j - 16 + TLEAD) & 3) * 32, lane);
       if (j == 12 || j == 14 || j == 16 || j == 18)
         D4[(j - 12) >> 1] = *reinterpret_cast<const float4*>(st + SDOFF + 8 * ((j - 12) >> 1) + 4 * h);
       if (j >= 24 - TLEAD && j < 32 - TLEAD)
-        tq[j - 24 + TLEAD] = (PTO_PIPE_ABL & 2) ? row_frag(Qs, (16 * ((j - 24 + TLEAD) >> 2) + r) & 31, (j - 24 + TLEAD) & 3)
-                                                : tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
+        tq[j - 24 + TLEAD] = tr_frag(Qs, 16 * ((j - 24 + TLEAD) >> 2), ((j - 24 + TLEAD) & 3) * 32, lane);
       if (j >= 28) {
         da[j - 28] = row_frag(Dn, r, 2 * (j - 28) + h);
         if (j == 28) L4[0] = *reinterpret_cast<const float4*>(stn + 4 * h);
       }
       // ---- tile t + 2 -> buffer NN (last read before this tile's opening barrier); it must
       // land by this tile's closing barrier (tile t + 1 reads it), so it goes out early
-      if (j >= PTO_PIPE_DMA0 && (j - PTO_PIPE_DMA0) % PTO_PIPE_DMAS == 0 &&
-          (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS < (PTO_PIPE_STAT4 ? 4 : 5) && !(PTO_PIPE_ABL & 4))
-        dma(NN, (j - PTO_PIPE_DMA0) / PTO_PIPE_DMAS, toff2, soff2);
+      if (j >= DMA0 && j < DMA0 + 5) dma(NN, j - DMA0, toff2, soff2);
 
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -342,9 +288,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
       tile_off(t, toff, soff);
 #pragma unroll
       for (int pc = 0; pc < 5; ++pc) dma(t, pc, toff, soff);
-#if PTO_PIPE_STAT4
-      if (t == 0 && wu == 0) dma_stat4(0, 0);
-#endif
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -354,11 +297,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     for (int s = 0; s < NDS; ++s) qa[s] = row_frag(Qs, r, 2 * s + h);
 #pragma unroll
     for (int s = 0; s < 4; ++s) da[s] = row_frag(Qs + QT * CH, r, 2 * s + h);
-#if PTO_PIPE_STAT4
-    L4[0] = *reinterpret_cast<const float4*>(stat_ptr(0) + 4 * h);
-#else
     L4[0] = *reinterpret_cast<const float4*>(stat[0] + 4 * h);
-#endif
 #pragma unroll
     for (int s = 0; s < NDS; ++s) s0 = mfma(qa[s], kf[s], s0);
   }
@@ -376,7 +315,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
 #ifdef PTO_ATTN_STAMPS
     if (t == 9) PTO_STAMP(12);
 #endif
-    if (!(PTO_PIPE_ABL & 8)) __syncthreads();
+    __syncthreads();
 #ifdef PTO_ATTN_STAMPS
     if (t == 9) PTO_STAMP(13);
 #endif
@@ -386,11 +325,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   for (int t = 0;;) {
     size_t toff, soff;
     tile_off(t + 2, toff, soff);
-#if PTO_PIPE_STAT4
-    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
-    // tile's gaps; its slot was last read in the previous group's last tile
-    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
-#endif
     if (masked_of(t))
       step(B0, MK, s0, s1, lim_of(t), toff, soff, t == 9, t);
     else
@@ -398,11 +332,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
-#if PTO_PIPE_STAT4
-    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
-    // tile's gaps; its slot was last read in the previous group's last tile
-    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
-#endif
     if (masked_of(t))
       step(B1, MK, s1, s2, lim_of(t), toff, soff, t == 9, t);
     else
@@ -410,11 +339,6 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
     tile_end(t);
     if (++t == ntiles) break;
     tile_off(t + 2, toff, soff);
-#if PTO_PIPE_STAT4
-    // the next group's statistics, once per four tiles, from one wave (rotating), ahead of the
-    // tile's gaps; its slot was last read in the previous group's last tile
-    if ((t & 3) == 0 && ((t >> 2) & 3) == wu) dma_stat4(((t >> 2) + 1) & 1, t + 4);
-#endif
     if (masked_of(t))
       step(B2, MK, s2, s0, lim_of(t), toff, soff, t == 9, t);
     else
@@ -432,22 +356,13 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_pipe_kernel(
   acc[2] = acc_read<32>();
   acc[3] = acc_read<48>();
   const size_t off = ((size_t)b * S + k0w) * kvstride + (size_t)hk * D;
-#if PTO_PIPE_EPIW  // wave-local staging: the loop's closing barrier already retired every tile read
+  // wave-local staging: the loop's closing barrier already retired every tile read
   store_rows_T_wave(acc, 1.f, qd + w * 32 * CH, lane, dv + off, kvstride);
   acc[0] = acc_read<64>();
   acc[1] = acc_read<80>();
   acc[2] = acc_read<96>();
   acc[3] = acc_read<112>();
   store_rows_T_wave(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
-#else
-  store_rows_T(acc, 1.f, qd + w * 32 * CH, lane, dv + off, kvstride);
-  __syncthreads();
-  acc[0] = acc_read<64>();
-  acc[1] = acc_read<80>();
-  acc[2] = acc_read<96>();
-  acc[3] = acc_read<112>();
-  store_rows_T(acc, scale, qd + w * 32 * CH, lane, dk + off, kvstride);
-#endif
   PTO_STAMP(3);
   PTO_RSTAMP(5);
 #ifdef PTO_ATTN_STAMPS
@@ -725,12 +640,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attn_bwd_dq_pipe_kernel(
   acc[1] = acc_read<16>();
   acc[2] = acc_read<32>();
   acc[3] = acc_read<48>();
-#if PTO_PIPE_EPIW
   store_rows_T_wave(acc, scale, kvs + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D,
                     qstride);
-#else
-  store_rows_T(acc, scale, kvs + w * 32 * CH, lane, dq + ((size_t)b * S + q0w) * qstride + (size_t)hq * D, qstride);
-#endif
 }
 
 }  // namespace

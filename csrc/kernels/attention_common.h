@@ -27,6 +27,9 @@ constexpr int BK = 128;      // keys per dK/dV workgroup (32 per wave)
 constexpr int QT = 32;       // query rows per dK/dV tile
 constexpr int NT = 256;
 constexpr int CH = D / 8;    // 16-byte chunks per row (16)
+constexpr int NT8 = 512;     // 8-wave workgroups (two waves per SIMD)
+constexpr int BM8 = 256;     // query rows per 8-wave forward / dQ workgroup
+constexpr float DEFER = 8.f; // deferred-rescale threshold of the 8-wave forward (log2 units)
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);

@@ -1906,18 +1906,20 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
   __shared__ float4 red[SR_SL][SR_COLS];
   stamp(dbg, 0);
   const int tid = threadIdx.x;
-  // block ids: [0, tw.blocks) the fc1.weight tiles (the longest blocks, dispatched first), then
-  // the slab reduction, then the plain SGD range
-  int blk = blockIdx.x;
-  if (blk < tw.blocks) {
-    tail_w1_tile(tw, blk * 4 + (tid >> 6), tid & 63, hy);
+  // logical block ids: [0, red_blocks) the slab reduction, [red_blocks, + tw.blocks) the
+  // fc1.weight tiles, then the plain SGD range.  Dispatch order: the fc1.weight tiles first
+  // (same-box A/B against reduction-first: 38.49-38.63 vs 38.60-38.77 us/step at K = 2000,
+  // profiles/r5_tail/ab.txt)
+  const int blk = (int)blockIdx.x < tw.blocks ? (int)blockIdx.x + red_blocks
+                  : (int)blockIdx.x < tw.blocks + red_blocks ? (int)blockIdx.x - tw.blocks : (int)blockIdx.x;
+  if (blk >= red_blocks && blk < red_blocks + tw.blocks) {
+    tail_w1_tile(tw, (blk - red_blocks) * 4 + (tid >> 6), tid & 63, hy);
     stamp(dbg, 1);
     return;
   }
-  blk -= tw.blocks;
   if (blk >= red_blocks) {
     // plain SGD over the second range (already-reduced grads, e.g. the fc bucket)
-    const int v = (blk - red_blocks) * 256 + tid;
+    const int v = (blk - red_blocks - tw.blocks) * 256 + tid;
     if (v < (n2 >> 2)) {
       float4 pp = reinterpret_cast<float4*>(p2)[v];
       const float4 gg = reinterpret_cast<const float4*>(g2)[v];

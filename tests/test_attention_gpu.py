@@ -93,7 +93,7 @@ def _fwd(q, k, v, causal):
     return o, lse2
 
 
-@pytest.mark.parametrize("variant", [4, 8, 9, 10])
+@pytest.mark.parametrize("variant", [4, 10])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal):
     """Both forward kernels on scores whose row maximum keeps growing along the keys (large,
@@ -122,27 +122,23 @@ def test_flash_forward_variants_with_growing_scores(fwd_variant, variant, causal
 
 @pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 768, 4, 4), (1, 256, 2, 1)])
 def test_flash_forward_variants_agree(fwd_variant, shape):
-    """8-wave (plain / ping-pong) vs 4-wave forward on the same inputs (bf16 outputs within
-    rounding; the two 8-wave kernels do the same per-row operations in the same order)."""
+    """The default 8-wave forward (LDS-DMA K/V staging, deferred rescale) vs the plain 4-wave
+    forward on the same inputs: bf16 outputs within rounding, the same log-sum-exp."""
     q, k, v = _inputs(*shape, seed=5)
     outs = {}
-    for var in (4, 8, 9, 10):
+    for var in (4, 10):
         fwd_variant(var)
         outs[var] = _fwd(q, k, v, True)
-    assert _rel(outs[8][0], outs[4][0]) < 4e-3
-    assert torch.allclose(outs[8][1], outs[4][1], atol=1e-3, rtol=1e-5)
-    assert torch.equal(outs[9][0], outs[8][0]) and torch.equal(outs[9][1], outs[8][1])
-    # 10: the 8-wave forward with its K/V tiles staged by LDS-DMA (same LDS image, same math)
-    assert torch.equal(outs[10][0], outs[8][0]) and torch.equal(outs[10][1], outs[8][1])
+    assert _rel(outs[10][0], outs[4][0]) < 4e-3
+    assert torch.allclose(outs[10][1], outs[4][1], atol=1e-3, rtol=1e-5)
 
 
-@pytest.mark.parametrize("dkdv", [1, 2, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("dkdv", [1, 8])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_backward_dkdv_variants(dkdv, causal):
-    """The dK/dV passes -- plain 4-wave, software-pipelined 4-wave (3-deep Q/dO ring: 1-5 tiles
-    per head cover its prologue/epilogue), 8-wave (S % 256 == 0; other S fall back), lean-register
-    4-wave with LDS-DMA staging and per-wave causal tile skip -- and the
-    8-wave dQ pass against the fp32 reference gradients."""
+    """The dK/dV passes -- plain 4-wave (the reference / fallback) and the default software-
+    pipelined pass (1-5 query tiles per head cover its prologue / epilogue) -- with the pipelined
+    dQ pass, against the fp32 reference gradients."""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import attention_reference, flash_attention, sdpa_bshd
     lib = _native.load()
@@ -199,9 +195,9 @@ def test_flash_rejects_unsupported_shape_on_gpu():
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("shape", [(2, 512, 8, 2), (1, 384, 4, 4), (3, 128, 2, 1)])
 def test_pipelined_dq_pass_bit_identical(causal, shape):
-    """The software-pipelined dQ pass (dQ variant 9, attention_bwd_pipe.hip) runs the 8-wave
+    """The software-pipelined dQ pass (dQ variant 9, attention_bwd_pipe.hip) runs the plain dQ
     pass's per-element operations in its key order: dQ, and the delta it writes for the dK/dV
-    pass, bit-identical to dQ variant 8 (S % 256 == 0) or the 4-wave pass it falls back to."""
+    pass, bit-identical to the 4-wave dQ pass (variant 4)."""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import flash_attention
     lib = _native.load()
@@ -211,22 +207,23 @@ def test_pipelined_dq_pass_bit_identical(causal, shape):
     outs = {}
     old = lib.pto_attn_set_dq_variant(9)
     try:
-        for var in (8, 9):
+        for var in (4, 9):
             lib.pto_attn_set_dq_variant(var)
             xs = [x.detach().clone().requires_grad_(True) for x in (q, k, v)]
             flash_attention(*xs, causal).backward(do)
             outs[var] = [x.grad for x in xs]
     finally:
         lib.pto_attn_set_dq_variant(old)
-    for a, b in zip(outs[8], outs[9]):
+    for a, b in zip(outs[4], outs[9]):
         assert torch.equal(a, b), shape
 
 
 @pytest.mark.parametrize("causal", [True, False])
-def test_split_dkdv_passes_bit_identical(causal):
-    """Variants 6 (a dV pass and a dK pass, two waves per SIMD each), 7 (the Q / dO prefetch issued
-    from inline asm) and 8 (software-pipelined across query tiles, its own translation unit) run
-    the lean dK/dV pass's per-element operation order: dK and dV bit-identical to variant 4."""
+def test_pipelined_dkdv_pass_bit_identical(causal):
+    """The default dK/dV pass (8: software-pipelined across query tiles, AGPR-pinned accumulators,
+    its own translation unit) runs the plain 4-wave pass's per-element operation order: dK and dV
+    bit-identical to variant 1.  (The rejected variants 2-7 live in csrc/kernels/experiments/:
+    tools/attn_variant_check.py.)"""
     from pytorch_operator_amd.ops import _native
     from pytorch_operator_amd.ops.attention import flash_attention
     lib = _native.load()
@@ -234,15 +231,28 @@ def test_split_dkdv_passes_bit_identical(causal):
     g = torch.Generator(device="cuda").manual_seed(5)
     do = torch.randn(q.shape, device="cuda", generator=g).to(torch.bfloat16)
     outs = {}
-    old = lib.pto_attn_set_dkdv_variant(4)
+    old = lib.pto_attn_set_dkdv_variant(1)
     try:
-        for var in (4, 6, 7, 8):
+        for var in (1, 8):
             lib.pto_attn_set_dkdv_variant(var)
             xs = [x.detach().clone().requires_grad_(True) for x in (q, k, v)]
             flash_attention(*xs, causal).backward(do)
             outs[var] = [x.grad for x in xs]
     finally:
         lib.pto_attn_set_dkdv_variant(old)
-    for var in (6, 7, 8):
-        for a, b in zip(outs[4], outs[var]):
-            assert torch.equal(a, b), var
+    for a, b in zip(outs[1], outs[8]):
+        assert torch.equal(a, b)
+
+
+def test_default_library_has_no_rejected_attention_variants():
+    """The default build links only the chosen passes and their plain references: asking for a
+    rejected variant leaves the selection unchanged."""
+    from pytorch_operator_amd.ops import _native
+    lib = _native.load()
+    for setter, dflt, bad in ((lib.pto_attn_set_variant, 10, (8, 9)), (lib.pto_attn_set_dq_variant, 9, (8,)),
+                              (lib.pto_attn_set_dkdv_variant, 8, (2, 3, 4, 6, 7))):
+        cur = setter(dflt)
+        for v in bad:
+            setter(v)
+            assert setter(dflt) == dflt, (v, "accepted by the default library")
+        setter(cur)

@@ -4,7 +4,8 @@
 #   tools/build_diag_attn.sh                       -> _lib/diag/attn_stamps.so (-DPTO_ATTN_STAMPS:
 #                                                     the dK/dV pipeline's s_memtime stamps,
 #                                                     read by tools/attn_pipe_stamps.py)
-#   tools/build_diag_attn.sh NAME "DEFS" [...]     -> _lib/diag/NAME.so per pair
+#   tools/build_diag_attn.sh NAME "DEFS" [...]     -> _lib/diag/NAME.so per pair (the round-4
+#                                                     ablation knobs were removed in round 5)
 # The default build never contains the stamps.
 set -e
 cd "$(dirname "$0")/.."
