@@ -831,11 +831,17 @@ __device__ __forceinline__ int batch_row_at(const BatchSrc& s, long long step, i
 // phase 1 no longer re-reads and re-sends 93.9 % of the gradient bytes.  Write-through system-
 // scope stores (visible over the fabric whatever the IPC mapping's cache type), drained by every
 // pushing wave before it ends; the exchange raises its flags in a later launch of this stream.
+// Write-after-read invariant the push relies on: the owner reduces its receive slot in the
+// exchange launch of step t and this launch (step t + 1) overwrites it; that is safe only because
+// the step-t exchange waited for every owner's flag2 before it ended, i.e. every owner finished
+// reading.  After a timed-out wait (the exchange's error word is set) that no longer holds, so a
+// degraded rank stops pushing (err != 0): its replicas have diverged and the worker exits 138.
 struct XPush {
   char* base[8];  // every rank's exchange buffer (IPC-mapped); null: no push
   int rank, world;
   long shard4;    // float4s per owner shard
   long w1_f4;     // flat float4 index of fc1.weight's first element
+  const int* err; // the exchange's error word (pto_xar_err_ptr); nullable
 };
 constexpr long kXarHdrBytes = 64 * 1024;  // xgmi_allreduce.hip kHdrBytes
 
@@ -922,11 +928,14 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
       }
     }
     const f32x4 c = c0 + c1;
+    // DDP over xGMI: push unless the exchange has flagged an error (wave-uniform)
+    const bool push = a.xp.base[0] != nullptr &&
+                      (a.xp.err == nullptr || __hip_atomic_load(a.xp.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0);
     if (nv) {
       const unsigned e4 = (unsigned)(n * 200 + kt * 4 + g);  // float4 index of (n, 16 kt + 4 g)
       const float4 v4 = make_float4(c[0], c[1], c[2], c[3]);
       reinterpret_cast<float4*>(a.gw1)[e4] = v4;
-      if (a.xp.base[0] != nullptr) {  // DDP over xGMI: also straight to the owner's receive buffer
+      if (push) {  // also straight to the owner's receive buffer
         const long v = a.xp.w1_f4 + (long)e4;
         const int q = (int)(v / a.xp.shard4);
         char* b = a.xp.base[0];
@@ -935,7 +944,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
         push_wt4(b + kXarHdrBytes + (((long)a.xp.rank * a.xp.shard4 + (v - (long)q * a.xp.shard4)) << 4), v4);
       }
     }
-    if (a.xp.base[0] != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (push) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (kt == 0) {
       dbsum = sum_lane_rows(dbsum);
       if (g == 0 && nv) a.gb1[n] = dbsum;
@@ -1056,6 +1065,272 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     if (j4 == 0 && tid == 0) a.stage_tag[0] = (int)step;
   }
   stamp(dbg, 1);
+}
+
+// ---------------------------------------------------------------------------
+// E': fc1 backward with the head fused in (the world-1 step, round 5).  Replaces the head launch
+// and its kernel boundary.  Every dz2 block (mt, kt) of fc1_bwd's layout recomputes the head of
+// its 16 samples on MFMA, then runs the dz2 job on that dh:
+//   h  = relu(p0 + p1 + b1)                      (the split-K fc1 partials; into LDS)
+//   logits = h . W2^T + b2                       (M 16 samples, N 16 (10), K 512 over 8 waves)
+//   log-softmax, NLL, d(logits) = (softmax - onehot) / B        (one thread per sample)
+//   dh = (d(logits) . W2) * (h > 0)             (M 16, N 512, K 16; each wave its own 64 k)
+//   dz2 = un-pool(relu'(a2) * (dh . W1))         (fc1_bwd's job 2, unchanged)
+// The 50 kt blocks of a sample tile recompute the same head -- a few MFMAs next to the dz2 GEMM,
+// against a launch + boundary -- and the kt == 0 block publishes h, dh, d(logits) and the
+// per-sample (loss, correct) for the tail (dW_fc1, dW_fc2, statistics).  Sums differ from
+// head_kernel's lane-tree order by fp32 rounding (the DDP paths keep head + fc1_bwd).
+struct Fc1BwdHead {
+  const float *hp0, *hp1, *b1;  // fc1 split-K partials [B][500] x 2, fc1.bias [500]
+  const float *w2, *b2;         // fc2.weight [10][500], fc2.bias [10]
+  const int* lab;               // [B]
+  const float* a2;              // [B][800]
+  const uint8_t* idx2;          // [B][800]
+  const float* w1;              // fc1.weight [500][800]
+  float* dz2;                   // [B][50][8][8]
+  float *h_out, *dh_out, *dlog_out, *per_sample;  // published by the kt == 0 blocks
+  float grad_scale;             // 1 / B
+  int B;
+  BatchSrc nsrc;                // next-batch staging (stage_x != null), as fc1_bwd
+  int stage_adv;
+  uint8_t* stage_x;
+  int* stage_lab;
+  int* stage_tag;
+};
+constexpr int H_RS = 514;  // hs / w2s row stride: lane rows 2 banks apart -> conflict-free b32 reads
+constexpr int H_DS = 516;  // dhs row stride: 16-byte aligned rows for the dz2 job's b128 reads
+
+__global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* dbg) {
+  __shared__ float hs[16 * H_RS];
+  __shared__ float w2s[16 * H_RS];
+  __shared__ __align__(16) float dhs[16 * H_DS];
+  __shared__ f32x4 red[E_NW][64];
+  __shared__ float dls[16][16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int B = a.B;
+  const int nmt = (B + 15) / 16;
+  const int nJ2 = nmt * 50;
+  stamp(dbg, 0);
+  if ((int)blockIdx.x >= nJ2) {  // next-batch staging (fc1_bwd's staging blocks)
+    const int j4 = blockIdx.x - nJ2;
+    const long long step = (long long)a.nsrc.cursor[0] + a.stage_adv;
+    if (tid < 196) {
+      const int s = tid / 49, c = tid - s * 49, smp = 4 * j4 + s;
+      if (smp < B) {
+        const int row = batch_row_at(a.nsrc, step, smp, B);
+        const uint4 v = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(a.nsrc.x) + (size_t)row * 784)[c];
+        reinterpret_cast<uint4*>(a.stage_x + (size_t)smp * 784)[c] = v;
+        if (c == 0) a.stage_lab[smp] = a.nsrc.labels[row];
+      }
+    }
+    if (j4 == 0 && tid == 0) a.stage_tag[0] = (int)step;
+    stamp(dbg, 1);
+    return;
+  }
+  int t2x = blockIdx.x;  // dz2 tile mt * 50 + kt; grouped by XCD as fc1_bwd (4 mt of one kt together)
+  if (nJ2 == 200) {
+    const int s = (t2x & 7) * 25 + (t2x >> 3);
+    t2x = (s & 3) * 50 + (s >> 2);
+  }
+  const int mt = t2x / 50, kt = t2x - mt * 50;
+  const bool pub = kt == 0;
+
+  // ---- loads, all issued before the first use: the 16 rows' fc1 partials and bias, W2, the W1
+  // column slice of the dz2 job, its epilogue operands, labels and b2
+  float4 hq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = min(tid + q * E_NT, 1999), row = e / 125, c4 = e - row * 125;
+    const size_t o = (size_t)min(mt * 16 + row, B - 1) * 500 + 4 * c4;
+    const float4 x0 = *reinterpret_cast<const float4*>(a.hp0 + o);
+    const float4 x1 = *reinterpret_cast<const float4*>(a.hp1 + o);
+    const float4 c = *reinterpret_cast<const float4*>(a.b1 + 4 * c4);
+    // head_kernel's h: relu((part0 + part1) + b1)
+    hq[q] = make_float4(fmaxf(x0.x + x1.x + c.x, 0.f), fmaxf(x0.y + x1.y + c.y, 0.f),
+                        fmaxf(x0.z + x1.z + c.z, 0.f), fmaxf(x0.w + x1.w + c.w, 0.f));
+  }
+  float4 wq[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) wq[q] = reinterpret_cast<const float4*>(a.w2)[min(tid + q * E_NT, 1249)];
+  const int kb = 64 * wv + 16 * g;  // the dz2 job's K range of this lane
+  float bv[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bv[s] = a.w1[(size_t)min(kb + s, 499) * 800 + kt * 16 + i];
+  const int l_e = (tid & 255) >> 2, r_e = tid & 3;
+  const int bs = mt * 16 + (l_e >> 4) * 4 + r_e;
+  const int ff = kt * 16 + (l_e & 15);
+  const size_t oe = (size_t)min(bs, B - 1) * 800 + ff;
+  float a2o = a.a2[oe];
+  int pidx = a.idx2[oe];
+  // softmax lanes (waves 0-3): sample 4 wv + (lane >> 4), class lane & 15
+  const int sm_s = 4 * wv + (lane >> 4), sm_j = lane & 15;
+  int lab_t = 0;
+  float b2v = 0.f;
+  if (tid < 256) {
+    lab_t = a.lab[min(mt * 16 + sm_s, B - 1)];
+    b2v = a.b2[min(sm_j, 9)];
+  }
+  // ---- h and W2 into LDS (zero rows / columns pad K to 512 and N to 16)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + q * E_NT;
+    if (e < 2000) {
+      const int row = e / 125, c4 = e - row * 125;
+      const bool rv = mt * 16 + row < B;
+      const float4 h4 = rv ? hq[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float2* d = reinterpret_cast<float2*>(hs + row * H_RS + 4 * c4);
+      d[0] = make_float2(h4.x, h4.y);
+      d[1] = make_float2(h4.z, h4.w);
+      if (pub && rv) reinterpret_cast<float4*>(a.h_out + (size_t)(mt * 16 + row) * 500)[c4] = h4;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int e = tid + q * E_NT;
+    if (e < 1250) {
+      const int row = e / 125, c4 = e - row * 125;
+      float2* d = reinterpret_cast<float2*>(w2s + row * H_RS + 4 * c4);
+      d[0] = make_float2(wq[q].x, wq[q].y);
+      d[1] = make_float2(wq[q].z, wq[q].w);
+    }
+  }
+  for (int e = tid; e < 16 * 12; e += E_NT) {  // columns 500..511 of every row
+    const int row = e / 12, c = 500 + e % 12;
+    hs[row * H_RS + c] = 0.f;
+    w2s[row * H_RS + c] = 0.f;
+  }
+  for (int e = tid; e < 6 * 512; e += E_NT) w2s[(10 + e / 512) * H_RS + (e & 511)] = 0.f;  // rows 10-15
+  __syncthreads();
+  stamp(dbg, 1);
+
+  // ---- logits partials: wave wv sums k in [64 wv, 64 wv + 64)
+  {
+    const float* ha = hs + i * H_RS + 64 * wv + g;
+    const float* wb = w2s + i * H_RS + 64 * wv + g;
+    float av[16], wvv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) { av[s] = ha[4 * s]; wvv[s] = wb[4 * s]; }
+    __builtin_amdgcn_sched_barrier(0);  // every operand read in flight before the first MFMA
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s & 1) c1 = mfma16x16x4(av[s], wvv[s], c1);
+      else c0 = mfma16x16x4(av[s], wvv[s], c0);
+    }
+    red[wv][lane] = c0 + c1;  // lane (i = j, g): logits of samples 4g + r
+  }
+  __syncthreads();
+  // ---- log-softmax / NLL / d(logits), one 16-lane row per sample (waves 0-3): max, sums and
+  // argmax over the row by quad / half-row / row-mirror DPP steps (every lane of the row ends
+  // with the same bits)
+  if (tid < 256) {
+    const int smp = mt * 16 + sm_s;
+    const bool jv = sm_j < 10, sv = smp < B;
+    float part[E_NW];
+#pragma unroll
+    for (int q = 0; q < E_NW; ++q) part[q] = red[q][16 * wv + sm_j][lane >> 4];
+    __builtin_amdgcn_sched_barrier(0);
+    float v = part[0];
+#pragma unroll
+    for (int q = 1; q < E_NW; ++q) v += part[q];
+    const float logit = v + b2v;
+    float mx = jv ? logit : -INFINITY;
+    mx = fmaxf(mx, dpp_f<0xB1>(mx));
+    mx = fmaxf(mx, dpp_f<0x4E>(mx));
+    mx = fmaxf(mx, dpp_f<0x141>(mx));
+    mx = fmaxf(mx, dpp_f<0x140>(mx));
+    float se = jv ? __expf(logit - mx) : 0.f;
+    float lt = sm_j == lab_t ? logit : 0.f;  // one non-zero term: exact
+    int pr = (jv && logit == mx) ? sm_j : 16;  // first maximum, as torch / head_kernel
+#define PTO_ROW_STEP(CTRL)                                                                      \
+    se += dpp_f<CTRL>(se);                                                                      \
+    lt += dpp_f<CTRL>(lt);                                                                      \
+    pr = min(pr, __builtin_amdgcn_mov_dpp(pr, CTRL, 0xF, 0xF, false));
+    PTO_ROW_STEP(0xB1) PTO_ROW_STEP(0x4E) PTO_ROW_STEP(0x141) PTO_ROW_STEP(0x140)
+#undef PTO_ROW_STEP
+    const float lse = mx + __logf(se);
+    const float dl = (jv && sv) ? (__expf(logit - lse) - (sm_j == lab_t ? 1.f : 0.f)) * a.grad_scale : 0.f;
+    dls[sm_s][sm_j] = dl;
+    if (pub && sv) {
+      if (jv) a.dlog_out[(size_t)smp * 10 + sm_j] = dl;
+      if (sm_j == 0) {
+        a.per_sample[2 * smp] = lse - lt;
+        a.per_sample[2 * smp + 1] = pr == lab_t ? 1.f : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(dbg, 2);
+  // ---- dh for this wave's 64 k (= its dz2 K range): four 16-column tiles, K = 16 (j)
+  {
+    float da[4], db[4][4], hm[4][4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      da[st] = dls[i][4 * st + g];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) db[t][st] = w2s[(4 * st + g) * H_RS + 64 * wv + 16 * t + i];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hm[t][r] = hs[(4 * g + r) * H_RS + 64 * wv + 16 * t + i];
+    __builtin_amdgcn_sched_barrier(0);  // operands and ReLU masks in registers first
+    float dv[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 c = zero4();
+#pragma unroll
+      for (int st = 0; st < 4; ++st) c = mfma16x16x4(da[st], db[t][st], c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dv[t][r] = hm[t][r] > 0.f ? c[r] : 0.f;
+        dhs[(4 * g + r) * H_DS + 64 * wv + 16 * t + i] = dv[t][r];
+      }
+    }
+    if (pub) {  // block-uniform
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 64 * wv + 16 * t + i, smp = mt * 16 + 4 * g + r;
+          if (k < 500 && smp < B) a.dh_out[(size_t)smp * 500 + k] = dv[t][r];
+        }
+    }
+  }
+  // ---- dz2 job (fc1_bwd's job 2): K = 500 split over the waves; this wave reads only the dh it wrote
+  {
+    const float4* dr = reinterpret_cast<const float4*>(dhs + i * H_DS + kb);
+    float av[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 d4 = dr[q];
+      av[4 * q] = d4.x; av[4 * q + 1] = d4.y; av[4 * q + 2] = d4.z; av[4 * q + 3] = d4.w;
+    }
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s & 1) c1 = mfma16x16x4(av[s], bv[s], c1);
+      else c0 = mfma16x16x4(av[s], bv[s], c0);
+    }
+    asm volatile("" : "+v"(a2o), "+v"(pidx));
+    red[wv][lane] = c0 + c1;  // (the logits partials in red were consumed before the last barrier)
+  }
+  __syncthreads();
+  float v = red[0][l_e][r_e];
+#pragma unroll
+  for (int q = 1; q < E_NW; ++q) v += red[q][l_e][r_e];
+  if (tid < 256 && bs < B) {
+    const float d = a2o > 0.f ? v : 0.f;
+    const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
+    float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+    z[0] = pidx == 0 ? d : 0.f;
+    z[1] = pidx == 1 ? d : 0.f;
+    z[8] = pidx == 2 ? d : 0.f;
+    z[9] = pidx == 3 ? d : 0.f;
+  }
+  stamp(dbg, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -1841,9 +2116,88 @@ struct TailW1 {
   const float *dh, *a2;  // head's dh [B][500], conv12's a2 [B][800]
   float *p, *m;          // fc1.weight then fc1.bias (p + 400000) params / momentum
   float* g;              // optional: also store the gradient (fc1.weight, then fc1.bias)
-  int B, blocks;         // blocks: 400 (4 tiles of 16 x 16 per 256-thread block), 0 = off
+  int B, blocks;         // blocks: 400 (4 tiles of 16 x 16 per 256-thread block), +8 with fc2; 0 = off
+  // fc2 (with the fused head, fc1_bwd's job 3 moves here too): dW_fc2 = d(logits)^T . h, db_fc2,
+  // their SGD, and the step's loss statistics; fc2 == 0: off
+  int fc2;
+  const float *dlog, *h, *per_sample;
+  float* stats;
+  float loss_scale;
+  float *p2, *m2, *g2;    // fc2.weight [10][500] params / momentum / optional gradient
+  float *pb2, *mb2, *gb2; // fc2.bias [10]
 };
 constexpr int T_W1_BLOCKS = 1600 / 4;
+constexpr int T_FC2_BLOCKS = 32 / 4;
+
+// fc1_bwd's job 3 as a tail tile (same tiles, operands and summation order: the same gradient
+// bits) with SGD applied from the accumulators
+__device__ __forceinline__ void tail_fc2_tile(const TailW1& tw, int nt, int lane, const SgdHyper& hy) {
+  const int i = lane & 15, g = lane >> 4;
+  const int B = tw.B;
+  const int jc = min(i, 9);
+  const int n = nt * 16 + i;
+  const int ncl = min(n, 499);
+  const bool do_stats = nt == 1 && tw.per_sample != nullptr && tw.stats != nullptr;
+  float ls = 0.f, cs = 0.f;
+  if (do_stats && lane < B) { ls = tw.per_sample[2 * lane]; cs = tw.per_sample[2 * lane + 1]; }
+  float pp[4], mm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = min(g * 4 + r, 9);
+    pp[r] = tw.p2[j * 500 + ncl];
+    mm[r] = tw.m2[j * 500 + ncl];
+  }
+  float bp = 0.f, bm = 0.f;
+  if (nt == 0 && g == 0) { bp = tw.pb2[jc]; bm = tw.mb2[jc]; }
+  f32x4 c0 = zero4(), c1 = zero4();
+  float dbsum = 0.f;
+  for (int base = 0; base < B; base += 64) {
+    float av[16], hv[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int bb = min(base + 4 * s + g, B - 1);
+      av[s] = tw.dlog[(size_t)bb * 10 + jc];
+      hv[s] = tw.h[(size_t)bb * 500 + ncl];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool bv = base + 4 * s + g < B;
+      const float x = (bv && i < 10) ? av[s] : 0.f;
+      dbsum += x;
+      const float hb = bv ? hv[s] : 0.f;
+      if (s & 1) c1 = mfma16x16x4(x, hb, c1);
+      else c0 = mfma16x16x4(x, hb, c0);
+    }
+  }
+  const f32x4 c = c0 + c1;
+  if (n < 500) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = g * 4 + r;
+      if (j < 10) {
+        if (tw.g2 != nullptr) tw.g2[j * 500 + n] = c[r];
+        sgd_elem(pp[r], mm[r], c[r], hy);
+        tw.p2[j * 500 + n] = pp[r];
+        tw.m2[j * 500 + n] = mm[r];
+      }
+    }
+  }
+  if (nt == 0) {
+    dbsum = sum_lane_rows(dbsum);
+    if (g == 0 && i < 10) {
+      if (tw.gb2 != nullptr) tw.gb2[i] = dbsum;
+      sgd_elem(bp, bm, dbsum, hy);
+      tw.pb2[i] = bp;
+      tw.mb2[i] = bm;
+    }
+  }
+  if (do_stats) {
+    for (int bb = lane + 64; bb < B; bb += 64) { ls += tw.per_sample[2 * bb]; cs += tw.per_sample[2 * bb + 1]; }
+    ls = wave_allsum_dpp(ls);
+    cs = wave_allsum_dpp(cs);
+    if (lane == 0) { tw.stats[0] = ls * tw.loss_scale; tw.stats[1] = cs; }
+  }
+}
 
 __device__ __forceinline__ void tail_w1_tile(const TailW1& tw, int tile, int lane, const SgdHyper& hy) {
   const int i = lane & 15, g = lane >> 4;
@@ -1913,7 +2267,9 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
   const int blk = (int)blockIdx.x < tw.blocks ? (int)blockIdx.x + red_blocks
                   : (int)blockIdx.x < tw.blocks + red_blocks ? (int)blockIdx.x - tw.blocks : (int)blockIdx.x;
   if (blk >= red_blocks && blk < red_blocks + tw.blocks) {
-    tail_w1_tile(tw, (blk - red_blocks) * 4 + (tid >> 6), tid & 63, hy);
+    const int tile = (blk - red_blocks) * 4 + (tid >> 6);
+    if (tile < 1600) tail_w1_tile(tw, tile, tid & 63, hy);
+    else tail_fc2_tile(tw, tile - 1600, tid & 63, hy);
     stamp(dbg, 1);
     return;
   }
@@ -2217,11 +2573,12 @@ int pto_mnist_fc1_bwd_push(const float* dh, const float* a2, const uint8_t* idx2
                            const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                            float* gb2, float* dz2, const float* per_sample, float* stats,
                            float loss_scale, int B, void* const* xp_bases, int xp_rank, int xp_world,
-                           long xp_shard4, long xp_w1_f4, void* stream) {
+                           long xp_shard4, long xp_w1_f4, const int* xp_err, void* stream) {
   Fc1Bwd a{};
   if (xp_bases == nullptr || xp_world < 2 || xp_world > 8) return -1;
   for (int q = 0; q < xp_world; ++q) a.xp.base[q] = static_cast<char*>(xp_bases[q]);
   a.xp.rank = xp_rank; a.xp.world = xp_world; a.xp.shard4 = xp_shard4; a.xp.w1_f4 = xp_w1_f4;
+  a.xp.err = xp_err;
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
   a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = 7; a.B = B;
@@ -2357,9 +2714,79 @@ int pto_slab_reduce_sgd_w1(const float* P, int B, int n, int stride, float* gout
   const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
   const int blocks = T_W1_BLOCKS + red_blocks + (n2 / 4 + 255) / 256;
   const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
-  const TailW1 tw{dh, a2, w1p, w1m, w1g, B, T_W1_BLOCKS};
+  TailW1 tw{};
+  tw.dh = dh; tw.a2 = a2; tw.p = w1p; tw.m = w1m; tw.g = w1g; tw.B = B; tw.blocks = T_W1_BLOCKS;
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
                      sr, n, stride, gout, p, buf, hy, step_counter, p2, g2, buf2, n2, red_blocks, tw, dbg_next());
+  return (int)hipGetLastError();
+}
+
+// The tail of the fused-head step: as pto_slab_reduce_sgd_w1 (no plain SGD range) plus fc1_bwd's
+// job 3 -- dW_fc2 = dlog^T . h, db_fc2 and their SGD on fc2.weight (p2w/m2w, [10][500]) and
+// fc2.bias (pb2/mb2), optional gradients g2w/gb2, and stats = (sum(loss) * loss_scale, #correct)
+// from per_sample.
+int pto_mnist_tail(const float* P, int B, int n, int stride, float* gout, float* p, float* buf, float lr,
+                   float momentum, float dampening, float wd, float grad_scale, int nesterov, int first_step,
+                   int* step_counter, int rows_big, int big_lo, int big_hi, const float* dh, const float* a2,
+                   float* w1p, float* w1m, float* w1g, const float* dlog, const float* h, const float* per_sample,
+                   float* stats, float loss_scale, float* p2w, float* m2w, float* g2w, float* pb2, float* mb2,
+                   float* gb2, void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if (dh == nullptr || a2 == nullptr || w1p == nullptr || w1m == nullptr || dlog == nullptr || h == nullptr ||
+      p2w == nullptr || m2w == nullptr || pb2 == nullptr || mb2 == nullptr || per_sample == nullptr || stats == nullptr)
+    return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)p) | ((uintptr_t)buf) | ((uintptr_t)w1p) |
+       ((uintptr_t)w1m) | ((uintptr_t)w1g)) & 15)
+    return -2;
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
+  const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
+  const int blocks = T_W1_BLOCKS + T_FC2_BLOCKS + red_blocks;
+  const SgdHyper hy{lr, momentum, dampening, wd, grad_scale, nesterov, first_step};
+  TailW1 tw{};
+  tw.dh = dh; tw.a2 = a2; tw.p = w1p; tw.m = w1m; tw.g = w1g; tw.B = B; tw.blocks = T_W1_BLOCKS + T_FC2_BLOCKS;
+  tw.fc2 = 1; tw.dlog = dlog; tw.h = h; tw.per_sample = per_sample; tw.stats = stats; tw.loss_scale = loss_scale;
+  tw.p2 = p2w; tw.m2 = m2w; tw.g2 = g2w; tw.pb2 = pb2; tw.mb2 = mb2; tw.gb2 = gb2;
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
+                     sr, n, stride, gout, p, buf, hy, step_counter, nullptr, nullptr, nullptr, 0, red_blocks, tw,
+                     dbg_next());
+  return (int)hipGetLastError();
+}
+
+// fc1_bwd with the head fused in (fc1_bwd_head_kernel): dz2 from the split-K fc1 partials hp0/hp1;
+// publishes h_out, dh_out [B][500], dlog_out [B][10], per_sample [B][2]; with stage_x, also the
+// next-batch staging blocks (as pto_mnist_fc1_bwd_stage).
+int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, const float* w2, const float* b2,
+                           const int* lab, const float* a2, const uint8_t* idx2, const float* w1, float* dz2,
+                           float* h_out, float* dh_out, float* dlog_out, float* per_sample, float grad_scale, int B,
+                           const void* nx, const int* nlabels, const int* nperm, const int* ncursor, int n_total,
+                           int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
+  PTO_CHECK_B(B);
+  if (hp0 == nullptr || hp1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || lab == nullptr ||
+      a2 == nullptr || idx2 == nullptr || w1 == nullptr || dz2 == nullptr || h_out == nullptr || dh_out == nullptr ||
+      dlog_out == nullptr || per_sample == nullptr)
+    return -1;
+  if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out)) & 15)
+    return -2;  // float4 rows
+  Fc1BwdHead a{};
+  a.hp0 = hp0; a.hp1 = hp1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.lab = lab; a.a2 = a2; a.idx2 = idx2; a.w1 = w1;
+  a.dz2 = dz2; a.h_out = h_out; a.dh_out = dh_out; a.dlog_out = dlog_out; a.per_sample = per_sample;
+  a.grad_scale = grad_scale; a.B = B;
+  int nst = 0;
+  if (stage_x != nullptr) {
+    if (nperm == nullptr || ncursor == nullptr || nlabels == nullptr || stage_lab == nullptr || stage_tag == nullptr ||
+        n_total <= 0 || ((((uintptr_t)nx) | ((uintptr_t)stage_x)) & 15))
+      return -1;
+    a.nsrc = make_src(nx, 1, nlabels, nperm, ncursor, 0, n_total, 1.f, 0.f);
+    a.stage_adv = stage_adv;
+    a.stage_x = stage_x;
+    a.stage_lab = stage_lab;
+    a.stage_tag = stage_tag;
+    nst = (B + 3) / 4;
+  }
+  const int blocks = ((B + 15) / 16) * 50 + nst;
+  hipLaunchKernelGGL(fc1_bwd_head_kernel, dim3(blocks), dim3(E_NT), 0, (hipStream_t)stream, a, dbg_next());
   return (int)hipGetLastError();
 }
 

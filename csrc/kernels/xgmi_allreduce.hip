@@ -581,6 +581,9 @@ int pto_xar_push_info(void* ctx, void** bases, int* rank, int* world, long* shar
   return 0;
 }
 long pto_xar_npad(void* ctx) { return static_cast<XarCtx*>(ctx)->npad; }
+// Device address of the exchange's error word (non-zero after a bounded wait timed out): a
+// producer that pushes into peers' receive buffers checks it and stops pushing (XPush::err).
+void* pto_xar_err_ptr(void* ctx) { return static_cast<XarCtx*>(ctx)->err; }
 
 // Map every peer's buffer (handles: world x 64 bytes, in rank order).
 int pto_xar_open(void* ctx, const void* handles) {

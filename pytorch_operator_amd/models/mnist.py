@@ -156,6 +156,9 @@ class FusedMnistTrainer:
         #            materialize_fc1_grad: the tail also stores that gradient into flat_grads
         self.w1_tail = os.environ.get("PTO_W1_TAIL", "1") != "0"
         self.materialize_fc1_grad = False
+        #   fuse_head (with w1_tail): fc1_bwd recomputes the head of its sample tile on MFMA (no
+        #             head launch); dW_fc2 / db_fc2 / statistics move to the tail with their SGD
+        self.fuse_head = os.environ.get("PTO_FUSE_HEAD", "1") != "0"
 
     # ---------------------------------------------------------------- state
     @property
@@ -272,6 +275,16 @@ class FusedMnistTrainer:
                   src=self.source if st is not None else None,
                   stage=st, stage_adv=stage_adv or 0, xpush=xpush)
 
+    def _fc1_bwd_head(self, B: int, stage_adv: int) -> None:
+        """fc1_bwd with the head fused in (ops.mnist.fc1_bwd_head)."""
+        K, p = self.K, self._pv
+        st = self._stage_for(None)
+        K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"], p["fc2.bias"],
+                       self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], dz2=self.dz2[:B],
+                       h_out=self.h1[:B], dh_out=self.dh[:B], dlog_out=self.dlogits[:B],
+                       per_sample=self.per_sample[:B], grad_scale=1.0 / B,
+                       src=self.source if st is not None else None, stage=st, stage_adv=stage_adv)
+
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self._pv
         if self.conv_chunk == 4:
@@ -339,7 +352,7 @@ class FusedMnistTrainer:
             push = getattr(self.grad_sync, "push_fc1", True)
             self.forward(source, B)
             self._head(B)
-            self._fc1_bwd(B, xpush=(*xar.push_info(), w1o) if push else None)
+            self._fc1_bwd(B, xpush=(*xar.push_info(), w1o, xar.err_ptr()) if push else None)
             self._conv_bwd(B)
             self.grad_sync.xar.allreduce_sgd_(
                 self.flat_grads, self._fp, self._fm, lr=self.lr,
@@ -354,9 +367,27 @@ class FusedMnistTrainer:
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return
-        # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
         K = self.K
         ce = self.layout.conv_end
+        if self.w1_tail and self.fuse_head and self.fc1_ks == 2:
+            # 5 launches: conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head -> conv_bwd4 -> tail
+            self.forward(source, B)
+            self._fc1_bwd_head(B, stage_adv=1 if advance_cursor else 0)
+            self._conv_bwd(B)
+            o2w, o2b = self.layout.offsets["fc2.weight"], self.layout.offsets["fc2.bias"]
+            mat = self.materialize_fc1_grad
+            K.tail_(self.conv_slab, B, self.conv_bucket(), self._fp[:ce], self._fm[:ce], lr=self.lr,
+                    momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
+                    nesterov=self.nesterov, first_step=self._first_step,
+                    step_counter=self.cursor if advance_cursor else None, big=self._slab_big(B),
+                    w1=(self.dh[:B], self.a2[:B], self._fp[ce:o2w], self._fm[ce:o2w],
+                        self.flat_grads[ce:o2w] if mat else None),
+                    fc2=(self.dlogits[:B], self.h1[:B], self.per_sample[:B], self.stats, 1.0 / B,
+                         self._fp[o2w:o2b], self._fm[o2w:o2b], self.flat_grads[o2w:o2b] if mat else None,
+                         self._fp[o2b:], self._fm[o2b:], self.flat_grads[o2b:] if mat else None))
+            self._first_step = False
+            return
+        # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
         self.forward(source, B)
         self._head(B)
         w1t = self.w1_tail

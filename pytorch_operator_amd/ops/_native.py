@@ -138,9 +138,12 @@ _SIGNATURES = {
     "pto_mnist_synth": [_VP, _VP, _VP, _I, ctypes.c_uint, _F, _VP],
     "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP],
+    "pto_mnist_tail": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _I, _I, _I]
+                      + [_VP] * 9 + [_F] + [_VP] * 7,
+    "pto_mnist_fc1_bwd_head": [_VP] * 14 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
     "pto_slab_reduce_sgd_w1": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                                _VP, _VP, _VP, _I, _I, _I, _I] + [_VP] * 6,
-    "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP],
+    "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     # xgmi_allreduce.hip
     "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],
@@ -202,6 +205,7 @@ _SIGNATURES = {
 _LONG_FNS = {"pto_xar_npad": [_VP], "pto_xar_emu_npad": [_VP], "pto_rmsnorm_bwd_parts": [_L, _I],
              "pto_graph_nodes": [_VP]}
 _VOID_FNS = {"pto_set_debug_buffer": [_VP], "pto_xar_emu_stamps": [_VP, _VP]}
+_PTR_FNS = {"pto_xar_err_ptr": [_VP]}
 
 
 def load(build_if_missing: bool = True):
@@ -220,7 +224,8 @@ def load(build_if_missing: bool = True):
             raise NativeLibraryError(f"{path} missing; run pytorch_operator_amd.ops.build()")
         lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         variant = path != _LIB_PATH  # an A/B build may predate entry points it never exercises
-        for table, restype in ((_SIGNATURES, ctypes.c_int), (_LONG_FNS, ctypes.c_long), (_VOID_FNS, None)):
+        for table, restype in ((_SIGNATURES, ctypes.c_int), (_LONG_FNS, ctypes.c_long), (_VOID_FNS, None),
+                               (_PTR_FNS, ctypes.c_void_p)):
             for name, argtypes in table.items():
                 try:
                     fn = getattr(lib, name)

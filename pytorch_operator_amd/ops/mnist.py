@@ -325,7 +325,7 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     ``stats[0] = sum(loss)*loss_scale`` and ``stats[1] = #correct``.
     With ``src`` + ``stage`` (all jobs), ceil(B/4) extra blocks stage the batch of step
     ``cursor + stage_adv`` for the next conv12_fwd.
-    ``xpush = (bases, rank, world, shard4, w1_offset)`` (DDP over xGMI, all jobs): dW_fc1 is also
+    ``xpush = (bases, rank, world, shard4, w1_offset[, err_ptr])`` (DDP over xGMI, all jobs): dW_fc1 is also
     pushed into the owning ranks' receive buffers (``XgmiAllReduce.push_info``; ``w1_offset`` =
     float offset of fc1.weight in the flat gradient); the exchange then skips that range.
     """
@@ -361,14 +361,15 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     if xpush is not None:
         if stage is not None or jobs != FC1_BWD_ALL:
             raise ValueError("xpush runs every job and no staging")
-        bases, rank, world, shard4, w1_off = xpush
+        bases, rank, world, shard4, w1_off = xpush[:5]
+        err = xpush[5] if len(xpush) > 5 else None  # the exchange's error word: no push once set
         if w1_off % 4:
             raise ValueError("fc1.weight must start on a float4 boundary of the flat gradient")
         rc = lib.pto_mnist_fc1_bwd_push(
             dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
             gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
             _ptr(stats), float(loss_scale), B, bases, int(rank), int(world), int(shard4), int(w1_off) // 4,
-            _stream())
+            err, _stream())
         _native.check(rc, "fc1_bwd(xpush)")
         return dz2
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
@@ -377,6 +378,84 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
                                _ptr(stats), float(loss_scale), int(jobs), B, _stream())
     _native.check(rc, "fc1_bwd")
     return dz2
+
+
+def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh_out, dlog_out, per_sample,
+                 grad_scale: float, src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None,
+                 stage_adv: int = 1) -> None:
+    """fc1 backward with the head fused in (one launch instead of head + fc1_bwd; the world-1
+    step).  ``h_parts``: the split-K fc1 pre-activation partials [2, B, 500].  Writes dz2 and
+    publishes h = relu(p0 + p1 + b1), dh, d(logits) and per-sample (loss, correct) for the
+    tail (``tail_``).  With ``src`` + ``stage`` it also stages the batch of step
+    ``cursor + stage_adv`` (as ``fc1_bwd``)."""
+    lib = _native.load()
+    B = a2.shape[0]
+    if h_parts.dim() != 3 or h_parts.shape[0] != 2 or tuple(h_parts.shape[1:]) != (B, 500) or \
+            h_parts.dtype != torch.float32 or not h_parts.is_contiguous():
+        raise ValueError("h_parts must be contiguous fp32 [2, B, 500]")
+    _req(fc1_bias, (500,), torch.float32, "fc1.bias")
+    _req(w2, (10, 500), torch.float32, "fc2.weight")
+    _req(b2, (10,), torch.float32, "fc2.bias")
+    _req(lab, (B,), torch.int32, "labels")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
+    _req(w1, (500, 800), torch.float32, "fc1.weight")
+    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    _req(h_out, (B, 500), torch.float32, "h")
+    _req(dh_out, (B, 500), torch.float32, "dh")
+    _req(dlog_out, (B, 10), torch.float32, "dlogits")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    st = (0, 0, 0, 0, 0, 0, 0, 0, 0)
+    if stage is not None:
+        if src is None or not BatchStage.supported(src) or stage.B < B or src.x.data_ptr() % 16:
+            raise ValueError("staging needs a uint8 BatchSource with labels, perm, cursor and a large enough stage")
+        st = (src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(), src.cursor.data_ptr(), src.n_total,
+              int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(), stage.tag.data_ptr())
+    rc = lib.pto_mnist_fc1_bwd_head(h_parts[0].data_ptr(), h_parts[1].data_ptr(), fc1_bias.data_ptr(), w2.data_ptr(),
+                                    b2.data_ptr(), lab.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
+                                    dz2.data_ptr(), h_out.data_ptr(), dh_out.data_ptr(), dlog_out.data_ptr(),
+                                    per_sample.data_ptr(), float(grad_scale), B, *st, _stream())
+    _native.check(rc, "fc1_bwd_head")
+
+
+def tail_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: torch.Tensor, buf: torch.Tensor, *,
+          lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+          nesterov: bool = False, grad_scale: float = 1.0, first_step: bool = False,
+          step_counter: Optional[torch.Tensor] = None, big: Optional[tuple] = None, w1: tuple, fc2: tuple) -> None:
+    """The fused-head step's tail: ``slab_reduce_sgd_(..., w1=w1)`` plus fc1_bwd's job 3 --
+    ``fc2=(dlogits, h, per_sample, stats, loss_scale, fc2.weight params, momentum, grads or None,
+    fc2.bias params, momentum, grads or None)`` -- with SGD applied from the accumulators."""
+    lib = _native.load()
+    n = params.numel()
+    for t, nm in ((grads, "grads"), (params, "params"), (buf, "momentum_buffer")):
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+            raise ValueError(f"{nm} must be contiguous fp32 CUDA with {n} elements")
+    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
+            slab.shape[1] < n or slab.shape[0] < B:
+        raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
+    dh, a2, w1p, w1m, w1g = w1
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    for t, nm in ((w1p, "fc1 params"), (w1m, "fc1 momentum")) + (((w1g, "fc1 grads"),) if w1g is not None else ()):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < 400500:
+            raise ValueError(f"{nm}: contiguous fp32 [fc1.weight (400000) | fc1.bias (500)] expected")
+    dlog, h, per_sample, stats, loss_scale, p2, m2, g2, pb, mb, gb = fc2
+    _req(dlog, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    for t, nm, k in ((p2, "fc2.weight", 5000), (m2, "fc2.weight momentum", 5000), (pb, "fc2.bias", 10),
+                     (mb, "fc2.bias momentum", 10)) + (((g2, "fc2.weight grads", 5000),) if g2 is not None else ()) + \
+            (((gb, "fc2.bias grads", 10),) if gb is not None else ()):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < k:
+            raise ValueError(f"{nm}: contiguous fp32 with >= {k} elements expected")
+    rb, lo, hi = big if big is not None else (B, 0, 0)
+    rc = lib.pto_mnist_tail(slab.data_ptr(), B, n, slab.shape[1], grads.data_ptr(), params.data_ptr(),
+                            buf.data_ptr(), float(lr), float(momentum), float(dampening), float(weight_decay),
+                            float(grad_scale), int(nesterov), int(first_step), _ptr(step_counter), int(rb), int(lo),
+                            int(hi), dh.data_ptr(), a2.data_ptr(), w1p.data_ptr(), w1m.data_ptr(), _ptr(w1g),
+                            dlog.data_ptr(), h.data_ptr(), per_sample.data_ptr(), stats.data_ptr(), float(loss_scale),
+                            p2.data_ptr(), m2.data_ptr(), _ptr(g2), pb.data_ptr(), mb.data_ptr(), _ptr(gb), _stream())
+    _native.check(rc, "tail")
 
 
 def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,

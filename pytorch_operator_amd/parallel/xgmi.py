@@ -137,6 +137,10 @@ class XgmiAllReduce:
             self._push_info = (bases, rank.value, world.value, shard4.value)
         return self._push_info
 
+    def err_ptr(self) -> int:
+        """Device address of the exchange's error word (a pushing producer stops once it is set)."""
+        return int(self.lib.pto_xar_err_ptr(self._ctx) or 0)
+
     def gather_sharded_(self, t: torch.Tensor) -> None:
         """Reassemble a tensor each rank only kept for its own shard (e.g. the momentum
         buffer after fused steps) so every rank holds the full, identical copy."""

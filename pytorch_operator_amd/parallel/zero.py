@@ -298,6 +298,10 @@ class ZeroAdamW:
                 if id(p) not in skipped:
                     t = self.pstep[id(p)] = self.pstep.get(id(p), self.t - 1) + 1
                     groups.setdefault(t, []).append(p)
+            if self.world > 1 and len(groups) > 1:
+                # _save_ranges / _restore_ranges index bucket-absolute offsets, valid only when the
+                # shard is the whole bucket (world 1); at world > 1 every parameter steps together
+                raise RuntimeError("ZeroAdamW: parameters of one bucket diverged in step count at world > 1")
             for t, members in groups.items():
                 ids = {id(p) for p in members}
                 keep = self._save_ranges(b, [(b.slot[id(p)], p.numel()) for p in b.params if id(p) not in ids])

@@ -381,7 +381,7 @@ def test_w1_tail_is_bit_identical_to_fc1_bwd_wgrad(lib, B):
     n = 12 * B
     x, y = _data(n, seed=500 + B, n_total=n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(9)).to(torch.int32)
-    a = _stage_trainer(x, y, perm, B=B, w1_tail=True, materialize_fc1_grad=True)
+    a = _stage_trainer(x, y, perm, B=B, w1_tail=True, fuse_head=False, materialize_fc1_grad=True)
     b = _stage_trainer(x, y, perm, B=B, w1_tail=False)
     for _ in range(10):
         a.train_step()
@@ -394,3 +394,37 @@ def test_w1_tail_is_bit_identical_to_fc1_bwd_wgrad(lib, B):
     o1, o2 = a.layout.offsets["fc1.weight"], a.layout.offsets["fc1.bias"]
     assert torch.equal(a.flat_grads[o1:o1 + 400000], b.flat_grads[o1:o1 + 400000])
     assert torch.equal(a.flat_grads[o2:o2 + 500], b.flat_grads[o2:o2 + 500])
+
+
+@pytest.mark.parametrize("B", [64, 37])
+def test_fused_head_step_matches_head_kernel_step(lib, B):
+    """Round 5: fc1_bwd with the head recomputed per sample tile on MFMA (no head launch; dW_fc2,
+    db_fc2 and the statistics in the tail) against the head-kernel step: h bit-identical (same
+    formula), logits-derived tensors equal up to fp32 summation order, and the same training
+    trajectory over 10 steps."""
+    n = 12 * B
+    x, y = _data(n, seed=700 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(2)).to(torch.int32)
+    a = _stage_trainer(x, y, perm, B=B, fuse_head=True, materialize_fc1_grad=True)
+    b = _stage_trainer(x, y, perm, B=B, fuse_head=False, materialize_fc1_grad=True)
+    a.train_step()
+    b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.h1[:B], b.h1[:B])
+    assert _rel(a.dlogits[:B], b.dlogits[:B]) < 1e-5
+    assert _rel(a.dh[:B], b.dh[:B]) < 1e-5
+    assert _rel(a.dz2[:B], b.dz2[:B]) < 1e-5
+    assert torch.equal(a.per_sample[:B, 1], b.per_sample[:B, 1])
+    assert _rel(a.per_sample[:B, 0], b.per_sample[:B, 0]) < 1e-5
+    assert abs(float(a.stats[0]) - float(b.stats[0])) < 1e-5 * max(1.0, abs(float(b.stats[0])))
+    assert float(a.stats[1]) == float(b.stats[1])
+    for name in ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "conv2.weight", "conv1.weight"):
+        assert _rel(a.grads[name], b.grads[name]) < 1e-5, name
+    for _ in range(9):
+        a.train_step()
+        b.train_step()
+    torch.cuda.synchronize()
+    assert int(a.cursor.item()) == int(b.cursor.item()) == 10
+    # rounding differences of one step grow along the trajectory (lr 0.05): 1e-5 after 10 steps
+    assert _rel(a.flat_params, b.flat_params) < 1e-4
+    assert _rel(a.flat_momentum, b.flat_momentum) < 1e-4

@@ -43,6 +43,7 @@ def test_rccl_forms_bit_identical_at_world1(tmp_path):
     for k in ("eager", "rccl", "rccl_graph"):
         assert res[f"{k}_vs_split_equal"], (k, res)
     assert res["split_vs_six_equal"], res
+    assert res["fused_head_max_rel_diff_vs_six"] < 1e-5, res
     race = res["race"]
     assert race["rccl_ms_per_step"] > 0 and race["rccl_graph_ms_per_step"] > 0, race
     assert race["xgmi_ms_per_step"] is None and "world 1" in race["xgmi_skipped"], race

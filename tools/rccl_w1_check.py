@@ -12,7 +12,8 @@ are issued every step.  This runs, on one GPU, the forms the start-up race
 
 Each trainer takes N steps from the same initial state; at world 1 the all-reduce is an exact
 identity, so params and momentum must equal (``torch.equal``) the split step without collectives
-and the six-kernel single-GPU step.  Then the RCCL race runs (``choose_grad_sync`` without an xGMI
+and the six-kernel single-GPU step (head launch; the default five-launch step recomputes the head
+in fc1_bwd with another fp32 summation order and is reported as a relative difference).  Then the RCCL race runs (``choose_grad_sync`` without an xGMI
 candidate) beside a timed six-kernel run of the same length: RCCL's single-rank floor.
 
     python tools/rccl_w1_check.py --out DIR      (writes DIR/rank0.json, exit 0 iff all equal)
@@ -57,10 +58,12 @@ def main(argv=None) -> int:
                                  grad_sync=sync)
 
     N = a.steps
-    six = trainer(None)                              # the single-GPU six-kernel step
+    six = trainer(None)                              # the single-GPU six-kernel step (head launch)
+    six.fuse_head = False
+    fused = trainer(None)                            # the five-launch step (head fused into fc1_bwd)
     split = trainer(FlatGradAllReduce(force=False))  # same split kernels, collectives skipped
     eager = trainer(FlatGradAllReduce(force=True))
-    for tr in (six, split, eager):
+    for tr in (six, fused, split, eager):
         for _ in range(N):
             tr.train_step()
     forms = {"eager": eager}
@@ -78,6 +81,8 @@ def main(argv=None) -> int:
     def same(x, y):
         return bool(torch.equal(x.flat_params, y.flat_params) and torch.equal(x.flat_momentum, y.flat_momentum))
     res["split_vs_six_equal"] = same(split, six)
+    res["fused_head_max_rel_diff_vs_six"] = float((fused.flat_params - six.flat_params).abs().max() /
+                                                 six.flat_params.abs().max())
     for k, t in forms.items():
         res[f"{k}_vs_split_equal"] = same(t, split)
         res[f"{k}_vs_six_equal"] = same(t, six)

@@ -31,11 +31,16 @@ from pytorch_operator_amd.parallel.graphed_step import NativeGraph  # noqa: E402
 
 SLOT_U64 = 1024 * 16  # mnist_kernels.hip kDbgSlotU64
 NAMES = ["conv12_fwd", "fc1_fwd", "head", "fc1_bwd", "conv_bwd4", "tail"]
+if os.environ.get("PTO_FUSE_HEAD", "1") != "0" and os.environ.get("PTO_W1_TAIL", "1") != "0":
+    NAMES = ["conv12_fwd", "fc1_fwd", "fc1_bwd_head", "conv_bwd4", "tail"]
 # block ranges of the launches that run several jobs (B = 64): name -> [(first, end, job)]
 # (fc1_bwd: the dz2 job takes the first ids, mnist_kernels.hip fc1_bwd_kernel's block layout)
 # (round 5 default, w1_tail: fc1_bwd has no dW_fc1 job; the tail's first 400 blocks are the dW_fc1
 # tiles + their SGD; PTO_W1_TAIL=0 restores the round-4 layout)
-if os.environ.get("PTO_W1_TAIL", "1") != "0":
+if os.environ.get("PTO_W1_TAIL", "1") != "0" and os.environ.get("PTO_FUSE_HEAD", "1") != "0":
+    GROUPS = {"fc1_bwd_head": [(0, 200, "head+dz2"), (200, 216, "stage")],
+              "tail": [(0, 400, "dW_fc1+sgd"), (400, 408, "fc2+sgd+stats"), (408, 609, "conv reduce+sgd")]}
+elif os.environ.get("PTO_W1_TAIL", "1") != "0":
     GROUPS = {"fc1_bwd": [(0, 200, "dz2"), (200, 204, "fc2+stats"), (204, 220, "stage")],
               "tail": [(0, 400, "dW_fc1+sgd"), (400, 601, "conv reduce+sgd"), (601, 606, "fc2 sgd")]}
 else:
