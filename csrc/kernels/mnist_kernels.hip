@@ -361,21 +361,27 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
 //   the cg == 0 block publishes a1/idx1 (for the backward), xn and lab.
 //   conv2 then runs exactly as conv2_fwd_pool_kernel.
 // ---------------------------------------------------------------------------
-// conv1 channels 0-15 on MFMA: position tiles t0, t0 + 16, .. (NU of them; tile = conv
-// rows {2py, 2py+1} x cols 8px..8px+7) as NU independent accumulator chains, then bias +
-// ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1 if pub).  Channels 16-19
-// would fill only a quarter of a second 16-wide channel tile: conv1_valu_window does them.
+// conv1 channels 0-15 on MFMA: position tiles t0, t0 + 16, .. (NU of them) as NU independent
+// accumulator chains, then bias + ReLU + 2x2 max-pool into the conv2 im2col image (and a1/idx1
+// if pub).  Tile t = pooled row py = t / 3, pooled columns 4 (t % 3) .. + 3; its 16 MFMA rows are
+// those 4 pooling windows x their 4 elements (row 4 w + e, e = 2 di + dj), so a lane's four
+// accumulator registers ARE one window: the pool is a max over registers (round 5: the
+// rows x columns tile needed four v_permlane32_swap pairings per tile and ~2x the epilogue VALU
+// work, which the conv1 phase is issue-bound on).  Same taps in the same MFMA K order per output:
+// bit-identical.  Channels 16-19 would fill only a quarter of a second 16-wide channel tile:
+// conv1_valu_window does them.
 template <int NU, int TS = 16>
 __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int (&toff)[7],
                                             const float (&bw)[7], float bc, float* in_s,
                                             bool pub, float* a1, uint8_t* idx1, int b, int i, int g) {
   f32x4 acc[NU];
   const float* ibs[NU];
+  const int wi = i >> 2, e = i & 3;  // A row i: window wi, element e
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int pt1 = t0 + TS * u;
-    const int py = pt1 / 3, px = pt1 - py * 3;
-    ibs[u] = img + (2 * py + (i >> 3)) * AB_IRS + 8 * px + (i & 7);
+    const int py = pt1 / 3, pq = pt1 - py * 3;
+    ibs[u] = img + (2 * py + (e >> 1)) * AB_IRS + 8 * pq + 2 * wi + (e & 1);
     acc[u] = zero4();
   }
   // every LDS operand read is issued before the first MFMA (the scheduler would otherwise
@@ -392,30 +398,22 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     for (int u = 0; u < NU; ++u) acc[u] = mfma16x16x4(av[u][s], bw[s], acc[u]);
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
+    // lane (channel i, g): window g of tile pt1 -- pooled (py, 4 pq + g) -- elements in acc[u][0..3]
     const int pt1 = t0 + TS * u;
-    const int py = pt1 / 3, px = pt1 - py * 3;
-    const int c = i;
-    const float v0 = acc[u][0] + bc, v1 = acc[u][1] + bc, v2 = acc[u][2] + bc, v3 = acc[u][3] + bc;
-    float mA = v0; int aA = 0;
-    if (v1 > mA) { mA = v1; aA = 1; }
-    float mB = v2; int aB = 0;
-    if (v3 > mB) { mB = v3; aB = 1; }
-    const float pA = from_upper_half(mA);
-    const int paA = from_upper_half(aA);
-    const float pB = from_upper_half(mB);
-    const int paB = from_upper_half(aB);
-    if (g < 2) {
-      if (pA > mA) { mA = pA; aA = 2 + paA; }
-      if (pB > mB) { mB = pB; aB = 2 + paB; }
-      const int pw = 4 * px + 2 * (g & 1);
-      const float va = fmaxf(mA, 0.f), vb = fmaxf(mB, 0.f);
-      // pw is even: one 8-byte LDS / global store per pair
-      *reinterpret_cast<float2*>(in_s + c * C2_CS + py * C2_RS + pw) = make_float2(va, vb);
-      if (pub) {
-        const size_t o = (size_t)b * 2880 + c * 144 + py * 12 + pw;
-        *reinterpret_cast<float2*>(a1 + o) = make_float2(va, vb);
-        *reinterpret_cast<uchar2*>(idx1 + o) = make_uchar2((uint8_t)aA, (uint8_t)aB);
-      }
+    const int py = pt1 / 3, px = 4 * (pt1 - py * 3) + g;
+    const float o00 = acc[u][0] + bc, o01 = acc[u][1] + bc, o10 = acc[u][2] + bc, o11 = acc[u][3] + bc;
+    // torch max_pool2d scans (0,0),(0,1),(1,0),(1,1) and keeps the first maximum
+    float m = o00;
+    int am = 0;
+    if (o01 > m) { m = o01; am = 1; }
+    if (o10 > m) { m = o10; am = 2; }
+    if (o11 > m) { m = o11; am = 3; }
+    const float v = fmaxf(m, 0.f);
+    in_s[i * C2_CS + py * C2_RS + px] = v;
+    if (pub) {
+      const size_t o = (size_t)b * 2880 + i * 144 + py * 12 + px;
+      a1[o] = v;
+      idx1[o] = (uint8_t)am;
     }
   }
 }
@@ -538,10 +536,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   __syncthreads();
   stamp(dbg, 1);
   // conv1 + bias + ReLU + 2x2 max-pool.  Channels 0-15: implicit GEMM on MFMA, 36
-  // position tiles (conv rows {2py,2py+1} x cols 8px..8px+7) x 7 K-steps (25 taps,
+  // position tiles (4 pooling windows each, see conv1_tasks) x 7 K-steps (25 taps,
   // zero-padded to 28 through the weight fragments); wave w takes tiles w, w+16 (+ w+32
-  // for w < 4): 9 tiles per SIMD.  The pool epilogue is the same register/lane^32
-  // pairing as conv2's.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
+  // for w < 4): 9 tiles per SIMD.  The pool is a max over each lane's four accumulator
+  // registers.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
   // (Measured: giving the MFMA tiles and the VALU windows to disjoint waves was no faster.)
   {
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -563,6 +561,8 @@ conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     stamp_by(dbg, 4, 0);             // wave 0: 3 MFMA tiles done
     stamp_by(dbg, 5, AB_NT - 64);    // last wave: 2 MFMA tiles done, VALU windows next
     stamp_by(dbg, 7, 4 * 64);        // wave 4: 2 MFMA tiles, no VALU windows
+    // (round 5: the same windows as 25-step v_mfma_f32_4x4x1_16b_f32 chains on waves 7-15 --
+    // bit-identical -- measured 0.1 us/step slower, profiles/r5_c1/ab.txt)
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
     stamp_by(dbg, 6, AB_NT - 64);    // last wave: VALU windows done
   }

@@ -62,9 +62,15 @@ def analyse(dbg: torch.Tensor, nslots: int):
         dph = (w[:, 1:] - w[:, :-1]) * both
         phases = (dph.sum(0) / both.sum(0).clamp_min(1) / 100.0).tolist()
         nph = int(both.any(0).sum())
+        # effective shader clock per phase: clock64 ticks (stamps 8-15) / wall_clock64 (100 MHz)
+        c = d[used][:, 8:].double()
+        cv = (c[:, 1:] > 0) & (c[:, :-1] > 0) & both
+        dc = (c[:, 1:] - c[:, :-1]) * cv
+        dw = (w[:, 1:] - w[:, :-1]) * cv
+        ghz = (dc.sum(0) / dw.sum(0).clamp_min(1) / 10.0).tolist()  # ticks per 10 ns -> GHz
         out.append({"blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
                     "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist())),
-                    "phases": phases[:nph]})
+                    "phases": phases[:nph], "ghz": ghz[:nph]})
     return out
 
 
@@ -122,7 +128,9 @@ def main(argv=None):
                      "p50_block_end_us": round(med["p50end"] - med["start"], 2),
                      "gap_from_prev_us": round(gaps[len(gaps) // 2], 2),
                      "phase_means_us": [round(sum(x["phases"][j] for x in (s_[k] for s_ in samples)) / len(samples), 2)
-                                        for j in range(len(samples[0][k]["phases"]))]})
+                                        for j in range(len(samples[0][k]["phases"]))],
+                     "phase_ghz": [round(sum(x["ghz"][j] for x in (s_[k] for s_ in samples)) / len(samples), 2)
+                                   for j in range(len(samples[0][k]["ghz"]))]})
     for r, k in zip(rows, range(nk)):
         if r["kernel"] in GROUPS:
             r["jobs"] = {}
@@ -144,6 +152,8 @@ def main(argv=None):
     print(f"one step: sum of spans {res['sum_span_us']} us + sum of gaps {res['sum_gap_us']} us")
     print("mean block phase times (us, stamp k -> k+1): " +
           "; ".join(f"{r['kernel']} {r['phase_means_us']}" for r in rows[per:]))
+    print("effective shader clock per phase (GHz, clock64 / wall_clock64): " +
+          "; ".join(f"{r['kernel']} {r['phase_ghz']}" for r in rows[per:]))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
