@@ -418,6 +418,88 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
   }
 }
 
+// Waves 7-15: two channel 0-15 tiles (as conv1_tasks<2>) and one channel 16-19 group -- 16 pooled
+// positions p = 16 G + lane / 4 on v_mfma_f32_4x4x1_16b_f32: block lane / 4 is one pooled position,
+// its 4 rows the 2x2 window (row 2 di + dj), its 4 columns the channels; the 25 taps are 25 K = 1
+// steps in tap order from zero, the fmaf chain of conv1_valu_window / conv1_fwd_pool_kernel
+// (bit-identical).  The group's dependent chain is interleaved with the tiles' MFMAs (3-4 after
+// every tile k-step) so each chain's latency hides behind the others, on the matrix pipe instead
+// of ~140 VALU instructions per lane.  D of the group: lane 4 b + j, register i = window element
+// i of channel 16 + j.
+__device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* img, const float* w1s,
+                                                   const int (&toff)[7], const float (&bw)[7], float bc,
+                                                   float* in_s, bool pub, float* a1, uint8_t* idx1, int b,
+                                                   int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int wi = i >> 2, e = i & 3;
+  const float* ibs[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int pt1 = t0 + 16 * u;
+    const int py = pt1 / 3, pq = pt1 - py * 3;
+    ibs[u] = img + (2 * py + (e >> 1)) * AB_IRS + 8 * pq + 2 * wi + (e & 1);
+  }
+  const int q = lane & 3;
+  const int p4 = 16 * G + (lane >> 2);  // G < 9: p4 < 144
+  const int ph4 = p4 / 12, pw4 = p4 - ph4 * 12;
+  const float* ia = img + (2 * ph4 + (q >> 1)) * AB_IRS + 2 * pw4 + (q & 1);
+  const float* wb = w1s + (16 + q) * 25;
+  float av[2][7], av4[25], bv4[25];
+#pragma unroll
+  for (int st = 0; st < 7; ++st)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) av[u][st] = ibs[u][toff[st]];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) {
+    av4[k] = ia[(k / 5) * AB_IRS + k % 5];
+    bv4[k] = wb[k];
+  }
+  const float bc4 = w1s[500 + 16 + q];
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc[2] = {zero4(), zero4()}, acc4 = zero4();
+#pragma unroll
+  for (int st = 0; st < 7; ++st) {
+    acc[0] = mfma16x16x4(av[0][st], bw[st], acc[0]);
+    acc[1] = mfma16x16x4(av[1][st], bw[st], acc[1]);
+    const int k0 = st < 4 ? 4 * st : 16 + 3 * (st - 4), nk = st < 4 ? 4 : 3;  // 4 x 4 + 3 x 3 = 25
+#pragma unroll
+    for (int k = k0; k < k0 + nk; ++k) acc4 = __builtin_amdgcn_mfma_f32_4x4x1f32(av4[k], bv4[k], acc4, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // the tiles' epilogue (conv1_tasks)
+    const int pt1 = t0 + 16 * u;
+    const int py = pt1 / 3, px = 4 * (pt1 - py * 3) + g;
+    const float o00 = acc[u][0] + bc, o01 = acc[u][1] + bc, o10 = acc[u][2] + bc, o11 = acc[u][3] + bc;
+    float m = o00;
+    int am = 0;
+    if (o01 > m) { m = o01; am = 1; }
+    if (o10 > m) { m = o10; am = 2; }
+    if (o11 > m) { m = o11; am = 3; }
+    const float v = fmaxf(m, 0.f);
+    in_s[i * C2_CS + py * C2_RS + px] = v;
+    if (pub) {
+      const size_t o = (size_t)b * 2880 + i * 144 + py * 12 + px;
+      a1[o] = v;
+      idx1[o] = (uint8_t)am;
+    }
+  }
+  {  // the group's epilogue
+    const float o00 = acc4[0] + bc4, o01 = acc4[1] + bc4, o10 = acc4[2] + bc4, o11 = acc4[3] + bc4;
+    float m = o00;
+    int am = 0;
+    if (o01 > m) { m = o01; am = 1; }
+    if (o10 > m) { m = o10; am = 2; }
+    if (o11 > m) { m = o11; am = 3; }
+    const float v = fmaxf(m, 0.f);
+    in_s[(16 + q) * C2_CS + ph4 * C2_RS + pw4] = v;
+    if (pub) {
+      const size_t o = (size_t)b * 2880 + (16 + q) * 144 + p4;
+      a1[o] = v;
+      idx1[o] = (uint8_t)am;
+    }
+  }
+}
+
 // conv1 channels 16-19 on the VALU (f32 FMA runs at the f32 MFMA rate): one pooled output
 // per thread, item = pooled position * 4 + (c - 16): the four channels of a position share
 // the image reads (broadcast), so a 32-lane half reads 8 windows at stride 2 -- with the
@@ -556,14 +638,22 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
-conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+#ifdef PTO_CONV1_VALUWIN  // A/B: channels 16-19 as 576 VALU windows after the tiles (round 4)
+    conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+#else
+    if (wv >= 7) conv1_tiles2_group(wv, wv - 7, img, w1s, toff, bw, bc, in_s, pub, a1, idx1, b, lane);
+    else conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+#endif
     if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
     stamp_by(dbg, 4, 0);             // wave 0: 3 MFMA tiles done
     stamp_by(dbg, 5, AB_NT - 64);    // last wave: 2 MFMA tiles done, VALU windows next
     stamp_by(dbg, 7, 4 * 64);        // wave 4: 2 MFMA tiles, no VALU windows
     // (round 5: the same windows as 25-step v_mfma_f32_4x4x1_16b_f32 chains on waves 7-15 --
-    // bit-identical -- measured 0.1 us/step slower, profiles/r5_c1/ab.txt)
+    // bit-identical -- measured no faster, before and after the register pool: profiles/r5_c1,
+    // r5_mfma4)
+#ifdef PTO_CONV1_VALUWIN
     if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
+#endif
     stamp_by(dbg, 6, AB_NT - 64);    // last wave: VALU windows done
   }
   __syncthreads();
