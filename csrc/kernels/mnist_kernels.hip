@@ -947,6 +947,7 @@ struct Fc1Bwd {
   const uint8_t* idx2;
   const float *w1, *dlog, *h;
   float *gw1, *gb1, *gw2, *gb2, *dz2;
+  float* dpool;  // non-null: the dz2 job writes d(a2) pooled [B][800] here instead of dense dz2
   const float* per_sample;
   float* stats;
   float loss_scale;
@@ -1084,12 +1085,16 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
     for (int q = 1; q < E_NW; ++q) v += red[q][l][r];
     if (tid < 256 && bs < B) {
       const float d = a2o > 0.f ? v : 0.f;
-      const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
-      float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
-      z[0] = p == 0 ? d : 0.f;
-      z[1] = p == 1 ? d : 0.f;
-      z[8] = p == 2 ? d : 0.f;
-      z[9] = p == 3 ? d : 0.f;
+      if (a.dpool != nullptr) {
+        a.dpool[(size_t)bs * 800 + ff] = d;
+      } else {
+        const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
+        float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+        z[0] = p == 0 ? d : 0.f;
+        z[1] = p == 1 ? d : 0.f;
+        z[8] = p == 2 ? d : 0.f;
+        z[9] = p == 3 ? d : 0.f;
+      }
     }
   } else if (blk < nJ1 + nJ2 + nJ3) {
     // dW_fc2[10,500] = dlogits^T . h : M = 10 (16), N = 500 (32 tiles), K = B
@@ -1177,7 +1182,8 @@ struct Fc1BwdHead {
   const float* a2;              // [B][800]
   const uint8_t* idx2;          // [B][800]
   const float* w1;              // fc1.weight [500][800]
-  float* dz2;                   // [B][50][8][8]
+  float* dz2;                   // [B][50][8][8] (dense), or
+  float* dpool;                 // [B][800] pooled d(a2) (conv_bwd4 un-pools it through idx2)
   float *h_out, *dh_out, *dlog_out, *per_sample;  // published by the kt == 0 blocks
   float grad_scale;             // 1 / B
   int B;
@@ -1413,12 +1419,16 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   for (int q = 1; q < E_NW; ++q) v += red[q][l_e][r_e];
   if (tid < 256 && bs < B) {
     const float d = a2o > 0.f ? v : 0.f;
-    const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
-    float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
-    z[0] = pidx == 0 ? d : 0.f;
-    z[1] = pidx == 1 ? d : 0.f;
-    z[8] = pidx == 2 ? d : 0.f;
-    z[9] = pidx == 3 ? d : 0.f;
+    if (a.dpool != nullptr) {
+      a.dpool[(size_t)bs * 800 + ff] = d;
+    } else {
+      const int co = ff >> 4, ph = (ff >> 2) & 3, pw = ff & 3;
+      float* z = a.dz2 + (size_t)bs * 3200 + co * 64 + (2 * ph) * 8 + 2 * pw;
+      z[0] = pidx == 0 ? d : 0.f;
+      z[1] = pidx == 1 ? d : 0.f;
+      z[8] = pidx == 2 ? d : 0.f;
+      z[9] = pidx == 3 ? d : 0.f;
+    }
   }
   stamp(dbg, 3);
 }
@@ -1870,7 +1880,8 @@ __device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s,
 }
 
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
-    const float* __restrict__ dz2, const float* __restrict__ w2, const float* __restrict__ a1,
+    const float* __restrict__ dz2, const float* __restrict__ dp, const uint8_t* __restrict__ ip,
+    const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
     int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, u64* dbg) {
   extern __shared__ float lds[];
@@ -1902,12 +1913,29 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   // other three samples, the 2b im2col source, the own a1 / idx1 / xn (measured: keeping group
   // 2 in flight through phase 2a behind a second barrier was slower).  Every load independent
   // and unpredicated (clamped addresses + selects).
+  // dp != null (round 5): dz2 arrives pooled -- d(a2) [B][800] (ReLU-masked) and conv12's pool
+  // argmax idx2 [B][800] -- and is un-pooled here into the LDS image: 4 KB per sample instead of
+  // 12.8 KB (3 of every 4 dz2 values are zeros), 16 instead of 51 KB of this block's staging loads
+  const bool pooled = dp != nullptr;  // kernel-uniform
   float4 dv2[3];
+  float pd[4];
+  uint8_t pi[4];
   float cv[2], av1;
   uint8_t iv1;
   float xv1;
   {
-    const float4 dv1 = reinterpret_cast<const float4*>(dz2 + (size_t)bo * 3200)[min(tid, 799)];
+    float4 dv1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (pooled) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = min(tid + k * F_NT, 3199), sq = e / 800, f = e - sq * 800;
+        const size_t o = (size_t)min(4 * q + sq, B - 1) * 800 + f;
+        pd[k] = dp[o];
+        pi[k] = ip[o];
+      }
+    } else {
+      dv1 = reinterpret_cast<const float4*>(dz2 + (size_t)bo * 3200)[min(tid, 799)];
+    }
     float wv_[F_NW2];
 #pragma unroll
     for (int k = 0; k < F_NW2; ++k) {
@@ -1916,11 +1944,13 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
     }
     // group 2
+    if (!pooled) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = min(tid + k * F_NT, 2399);
-      const int o = e / 800, s = o < r ? o : o + 1;  // the chunk's other samples
-      dv2[k] = reinterpret_cast<const float4*>(dz2 + (size_t)min(4 * q + s, B - 1) * 3200)[e - o * 800];
+      for (int k = 0; k < 3; ++k) {
+        const int e = min(tid + k * F_NT, 2399);
+        const int o = e / 800, s = o < r ? o : o + 1;  // the chunk's other samples
+        dv2[k] = reinterpret_cast<const float4*>(dz2 + (size_t)min(4 * q + s, B - 1) * 3200)[e - o * 800];
+      }
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -1933,7 +1963,21 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     iv1 = idx1[(size_t)bo * 2880 + cig * 720 + ec];
     xv1 = xn[(size_t)bo * 784 + min(tid, 783)];
     // group 1 -> LDS
-    if (tid < 800) {
+    if (pooled) {  // every sample of the chunk, un-pooled (samples >= B as 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + k * F_NT;
+        if (e < 3200) {
+          const int sq = e / 800, f = e - sq * 800, co = f >> 4, ph = (f >> 2) & 3, pw = f & 3;
+          const float v = 4 * q + sq < B ? pd[k] : 0.f;
+          float* z = dzc_s + sq * G_DZN + co * G_DZS + (2 * ph) * 8 + 2 * pw;
+          z[0] = pi[k] == 0 ? v : 0.f;
+          z[1] = pi[k] == 1 ? v : 0.f;
+          z[8] = pi[k] == 2 ? v : 0.f;
+          z[9] = pi[k] == 3 ? v : 0.f;
+        }
+      }
+    } else if (tid < 800) {
       const int co = tid >> 4, c4 = tid & 15;
       const float4 v = own ? dv1 : make_float4(0.f, 0.f, 0.f, 0.f);
       float2* d = reinterpret_cast<float2*>(dzc_s + r * G_DZN + co * G_DZS + 4 * c4);
@@ -1955,7 +1999,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int e = tid + k * F_NT;
-      if (e < 2400) {
+      if (!pooled && e < 2400) {
         const int o = e / 800, s = o < r ? o : o + 1, rem = e - o * 800, co = rem >> 4, c4 = rem & 15;
         const float4 v = 4 * q + s < B ? dv2[k] : make_float4(0.f, 0.f, 0.f, 0.f);
         float2* d = reinterpret_cast<float2*>(dzc_s + s * G_DZN + co * G_DZS + 4 * c4);
@@ -2635,6 +2679,7 @@ static int fc1_bwd_launch(const Fc1Bwd& a, void* stream) {
   PTO_CHECK_B(B);
   if (a.jobs <= 0 || a.jobs > 7) return -1;
   if (a.gw1 == nullptr || a.gb1 == nullptr || a.gw2 == nullptr || a.gb2 == nullptr) return -1;
+  if ((a.jobs & 2) && a.dz2 == nullptr && a.dpool == nullptr) return -1;  // job 2 writes one of them
   if ((((uintptr_t)a.dh) | ((uintptr_t)a.gw1)) & 15) return -2;  // float4 dh rows (job 2), dW_fc1 stores
   if (a.xp.base[0] != nullptr) {
     if (a.xp.world < 2 || a.xp.world > 8 || a.xp.rank < 0 || a.xp.rank >= a.xp.world || a.xp.shard4 <= 0 ||
@@ -2663,8 +2708,9 @@ int pto_mnist_fc1_bwd_push(const float* dh, const float* a2, const uint8_t* idx2
                            const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                            float* gb2, float* dz2, const float* per_sample, float* stats,
                            float loss_scale, int B, void* const* xp_bases, int xp_rank, int xp_world,
-                           long xp_shard4, long xp_w1_f4, const int* xp_err, void* stream) {
+                           long xp_shard4, long xp_w1_f4, const int* xp_err, float* dpool, void* stream) {
   Fc1Bwd a{};
+  a.dpool = dpool;
   if (xp_bases == nullptr || xp_world < 2 || xp_world > 8) return -1;
   for (int q = 0; q < xp_world; ++q) a.xp.base[q] = static_cast<char*>(xp_bases[q]);
   a.xp.rank = xp_rank; a.xp.world = xp_world; a.xp.shard4 = xp_shard4; a.xp.w1_f4 = xp_w1_f4;
@@ -2678,8 +2724,9 @@ int pto_mnist_fc1_bwd_push(const float* dh, const float* a2, const uint8_t* idx2
 int pto_mnist_fc1_bwd(const float* dh, const float* a2, const uint8_t* idx2, const float* w1,
                       const float* dlog, const float* h, float* gw1, float* gb1, float* gw2,
                       float* gb2, float* dz2, const float* per_sample, float* stats,
-                      float loss_scale, int jobs, int B, void* stream) {
+                      float loss_scale, int jobs, int B, float* dpool, void* stream) {
   Fc1Bwd a{};
+  a.dpool = dpool;
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
   a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = jobs; a.B = B;
@@ -2692,8 +2739,9 @@ int pto_mnist_fc1_bwd_stage(const float* dh, const float* a2, const uint8_t* idx
                             float* gb2, float* dz2, const float* per_sample, float* stats,
                             float loss_scale, int B, const void* nx, const int* nlabels, const int* nperm,
                             const int* ncursor, int n_total, int stage_adv, int jobs, uint8_t* stage_x,
-                            int* stage_lab, int* stage_tag, void* stream) {
+                            int* stage_lab, int* stage_tag, float* dpool, void* stream) {
   Fc1Bwd a{};
+  a.dpool = dpool;
   a.dh = dh; a.a2 = a2; a.idx2 = idx2; a.w1 = w1; a.dlog = dlog; a.h = h;
   a.gw1 = gw1; a.gb1 = gb1; a.gw2 = gw2; a.gb2 = gb2; a.dz2 = dz2;
   a.per_sample = per_sample; a.stats = stats; a.loss_scale = loss_scale; a.jobs = jobs; a.B = B;
@@ -2851,17 +2899,18 @@ int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, 
                            const int* lab, const float* a2, const uint8_t* idx2, const float* w1, float* dz2,
                            float* h_out, float* dh_out, float* dlog_out, float* per_sample, float grad_scale, int B,
                            const void* nx, const int* nlabels, const int* nperm, const int* ncursor, int n_total,
-                           int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, void* stream) {
+                           int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, float* dpool,
+                           void* stream) {
   PTO_CHECK_B(B);
   if (hp0 == nullptr || hp1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || lab == nullptr ||
-      a2 == nullptr || idx2 == nullptr || w1 == nullptr || dz2 == nullptr || h_out == nullptr || dh_out == nullptr ||
-      dlog_out == nullptr || per_sample == nullptr)
+      a2 == nullptr || idx2 == nullptr || w1 == nullptr || (dz2 == nullptr && dpool == nullptr) ||
+      h_out == nullptr || dh_out == nullptr || dlog_out == nullptr || per_sample == nullptr)
     return -1;
   if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out)) & 15)
     return -2;  // float4 rows
   Fc1BwdHead a{};
   a.hp0 = hp0; a.hp1 = hp1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.lab = lab; a.a2 = a2; a.idx2 = idx2; a.w1 = w1;
-  a.dz2 = dz2; a.h_out = h_out; a.dh_out = dh_out; a.dlog_out = dlog_out; a.per_sample = per_sample;
+  a.dz2 = dz2; a.dpool = dpool; a.h_out = h_out; a.dh_out = dh_out; a.dlog_out = dlog_out; a.per_sample = per_sample;
   a.grad_scale = grad_scale; a.B = B;
   int nst = 0;
   if (stage_x != nullptr) {
@@ -2885,9 +2934,10 @@ int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, 
 // conv1.weight / conv1.bias / conv2.bias partials at o_gw1 / o_gb1 / o_gb2.
 int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
                         const float* xn, float* slab, int stride, int o_gw2, int o_gb2, int o_gw1,
-                        int o_gb1, int B, void* stream) {
+                        int o_gb1, int B, const float* dpool, const uint8_t* idx2, void* stream) {
   PTO_CHECK_B(B);
   if (4 * ((B + 3) / 4) > 65535) return -1;  // grid y
+  if ((dz2 == nullptr) == (dpool == nullptr) || (dpool != nullptr && idx2 == nullptr)) return -1;  // one form
   if ((stride & 3) || (o_gw2 & 3) || (((uintptr_t)slab) & 15) || (((uintptr_t)dz2) & 15)) return -2;
   if (o_gw2 < 0 || o_gb2 < 0 || o_gw1 < 0 || o_gb1 < 0 || o_gw2 + 25000 > stride || o_gb2 + 50 > stride ||
       o_gw1 + 500 > stride || o_gb1 + 20 > stride)
@@ -2897,7 +2947,7 @@ int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, cons
   if (rc != 0) return rc;
   const int nb = 4 * ((B + 3) / 4);
   hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
-                     dz2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
+                     dz2, dpool, idx2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
   return (int)hipGetLastError();
 }
 

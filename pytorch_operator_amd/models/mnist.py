@@ -159,6 +159,9 @@ class FusedMnistTrainer:
         #   fuse_head (with w1_tail): fc1_bwd recomputes the head of its sample tile on MFMA (no
         #             head launch); dW_fc2 / db_fc2 / statistics move to the tail with their SGD
         self.fuse_head = os.environ.get("PTO_FUSE_HEAD", "1") != "0"
+        #   pooled_dz2 (conv_chunk 4): fc1_bwd hands d(a2) over still pooled ([B, 800], 3.2 KB per
+        #             sample instead of the 12.8 KB dense dz2); conv_bwd4 un-pools it via idx2
+        self.pooled_dz2 = os.environ.get("PTO_POOLED_DZ2", "1") != "0"
 
     # ---------------------------------------------------------------- state
     @property
@@ -183,6 +186,7 @@ class FusedMnistTrainer:
         self.dlogits = torch.empty((B, 10), device=dev)
         self.dh = torch.empty((B, 500), device=dev)
         self.dz2 = torch.empty((B, 50, 8, 8), device=dev)
+        self.dpool = torch.empty((B, 800), device=dev)
         self.xn = torch.empty((B, 784), device=dev)
         self.lab = torch.empty((B,), device=dev, dtype=torch.int32)
         self.per_sample = torch.empty((B, 2), device=dev)
@@ -262,6 +266,12 @@ class FusedMnistTrainer:
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
+    def _dz2_out(self, B: int) -> dict:
+        """Where the input-gradient job writes: pooled d(a2) (conv_bwd4 un-pools it) or dense dz2."""
+        if self.pooled_dz2 and self.conv_chunk == 4:
+            return {"dz2": None, "dpool": self.dpool[:B]}
+        return {"dz2": self.dz2[:B], "dpool": None}
+
     def _fc1_bwd(self, B: int, stage_adv: Optional[int] = None, xpush: Optional[tuple] = None,
                  jobs: Optional[int] = None) -> None:
         """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv;
@@ -270,7 +280,7 @@ class FusedMnistTrainer:
         st = self._stage_for(None) if stage_adv is not None and xpush is None else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
-                  dz2=self.dz2[:B], per_sample=self.per_sample[:B], stats=self.stats,
+                  **self._dz2_out(B), per_sample=self.per_sample[:B], stats=self.stats,
                   loss_scale=1.0 / B, jobs=K.FC1_BWD_ALL if jobs is None else jobs,
                   src=self.source if st is not None else None,
                   stage=st, stage_adv=stage_adv or 0, xpush=xpush)
@@ -280,7 +290,7 @@ class FusedMnistTrainer:
         K, p = self.K, self._pv
         st = self._stage_for(None)
         K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"], p["fc2.bias"],
-                       self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], dz2=self.dz2[:B],
+                       self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], **self._dz2_out(B),
                        h_out=self.h1[:B], dh_out=self.dh[:B], dlog_out=self.dlogits[:B],
                        per_sample=self.per_sample[:B], grad_scale=1.0 / B,
                        src=self.source if st is not None else None, stage=st, stage_adv=stage_adv)
@@ -288,8 +298,10 @@ class FusedMnistTrainer:
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self._pv
         if self.conv_chunk == 4:
-            K.conv_bwd4(self.dz2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
-                        self.conv_slab, self.layout.offsets, B)
+            d = self._dz2_out(B)
+            K.conv_bwd4(d["dz2"], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
+                        self.conv_slab, self.layout.offsets, B, dpool=d["dpool"],
+                        idx2=self.idx2[:B] if d["dpool"] is not None else None)
             self._last_big = K.conv_bwd4_rows(B, self.layout.offsets)
             return
         self._last_big = None

@@ -132,18 +132,18 @@ _SIGNATURES = {
     "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_ks": [],
-    "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP],
+    "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_synth": [_VP, _VP, _VP, _I, ctypes.c_uint, _F, _VP],
-    "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP],
-    "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP],
+    "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP, _VP, _VP],
+    "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_tail": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _I, _I, _I]
                       + [_VP] * 9 + [_F] + [_VP] * 7,
-    "pto_mnist_fc1_bwd_head": [_VP] * 14 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd_head": [_VP] * 14 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_slab_reduce_sgd_w1": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                                _VP, _VP, _VP, _I, _I, _I, _I] + [_VP] * 6,
-    "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP, _VP],
+    "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP, _VP, _VP],
     "pto_sgd_momentum": [_VP, _VP, _VP, _L, _F, _F, _F, _F, _F, _I, _I, _VP, _VP],
     # xgmi_allreduce.hip
     "pto_xar_create": [_I, _I, _L, _I, ctypes.c_double, ctypes.POINTER(_VP), _VP],

@@ -316,8 +316,11 @@ FC1_BWD_ALL = 7
 def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_sample=None,
             stats=None, loss_scale: float = 1.0, jobs: int = FC1_BWD_ALL,
             src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None, stage_adv: int = 1,
-            xpush: Optional[tuple] = None):
+            xpush: Optional[tuple] = None, dpool: Optional[torch.Tensor] = None):
     """fc1/fc2 weight+bias grads and dz2 [B,50,8,8] (un-pooled, ReLU-masked).
+
+    With ``dpool`` ([B, 800] fp32) the input-gradient job writes d(a2) there, still pooled and
+    ReLU-masked, instead of dz2 (``conv_bwd4(..., dpool=, idx2=)`` un-pools it); returns dpool.
 
     ``jobs`` selects which of the three independent parts to launch (so the weight
     gradients can run on a side stream concurrently with the input gradient).
@@ -341,8 +344,14 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     _req(gb1, (500,), torch.float32, "grad fc1.bias")
     _req(gw2, (10, 500), torch.float32, "grad fc2.weight")
     _req(gb2, (10,), torch.float32, "grad fc2.bias")
-    dz2 = torch.empty((B, 50, 8, 8), device=dh.device) if dz2 is None else dz2
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    if dpool is not None:
+        _req(dpool, (B, 800), torch.float32, "dpool")
+        if dz2 is not None:
+            raise ValueError("dz2 and dpool are exclusive")
+    else:
+        dz2 = torch.empty((B, 50, 8, 8), device=dh.device) if dz2 is None else dz2
+        _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    out = dpool if dpool is not None else dz2
     if per_sample is not None:
         _req(per_sample, (B, 2), torch.float32, "per_sample")
     if stage is not None:
@@ -352,12 +361,12 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
             raise ValueError("stage too small or unaligned source")
         rc = lib.pto_mnist_fc1_bwd_stage(
             dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
-            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
+            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), _ptr(dz2), _ptr(per_sample),
             _ptr(stats), float(loss_scale), B, src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(),
             src.cursor.data_ptr(), src.n_total, int(stage_adv), int(jobs), stage.x.data_ptr(), stage.lab.data_ptr(),
-            stage.tag.data_ptr(), _stream())
+            stage.tag.data_ptr(), _ptr(dpool), _stream())
         _native.check(rc, "fc1_bwd(stage)")
-        return dz2
+        return out
     if xpush is not None:
         if stage is not None or jobs != FC1_BWD_ALL:
             raise ValueError("xpush runs every job and no staging")
@@ -367,24 +376,25 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
             raise ValueError("fc1.weight must start on a float4 boundary of the flat gradient")
         rc = lib.pto_mnist_fc1_bwd_push(
             dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(), dlogits.data_ptr(), h.data_ptr(),
-            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
+            gw1.data_ptr(), gb1.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), _ptr(dz2), _ptr(per_sample),
             _ptr(stats), float(loss_scale), B, bases, int(rank), int(world), int(shard4), int(w1_off) // 4,
-            err, _stream())
+            err, _ptr(dpool), _stream())
         _native.check(rc, "fc1_bwd(xpush)")
-        return dz2
+        return out
     rc = lib.pto_mnist_fc1_bwd(dh.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                dlogits.data_ptr(), h.data_ptr(), gw1.data_ptr(), gb1.data_ptr(),
-                               gw2.data_ptr(), gb2.data_ptr(), dz2.data_ptr(), _ptr(per_sample),
-                               _ptr(stats), float(loss_scale), int(jobs), B, _stream())
+                               gw2.data_ptr(), gb2.data_ptr(), _ptr(dz2), _ptr(per_sample),
+                               _ptr(stats), float(loss_scale), int(jobs), B, _ptr(dpool), _stream())
     _native.check(rc, "fc1_bwd")
-    return dz2
+    return out
 
 
 def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh_out, dlog_out, per_sample,
                  grad_scale: float, src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None,
-                 stage_adv: int = 1) -> None:
+                 stage_adv: int = 1, dpool: Optional[torch.Tensor] = None) -> None:
     """fc1 backward with the head fused in (one launch instead of head + fc1_bwd; the world-1
-    step).  ``h_parts``: the split-K fc1 pre-activation partials [2, B, 500].  Writes dz2 and
+    step).  ``h_parts``: the split-K fc1 pre-activation partials [2, B, 500].  Writes dz2 (or,
+    with ``dz2=None`` and ``dpool`` [B, 800], the pooled d(a2) -- see ``fc1_bwd``) and
     publishes h = relu(p0 + p1 + b1), dh, d(logits) and per-sample (loss, correct) for the
     tail (``tail_``).  With ``src`` + ``stage`` it also stages the batch of step
     ``cursor + stage_adv`` (as ``fc1_bwd``)."""
@@ -400,7 +410,12 @@ def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh
     _req(a2, (B, 800), torch.float32, "a2")
     _req(idx2, (B, 800), torch.uint8, "idx2")
     _req(w1, (500, 800), torch.float32, "fc1.weight")
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    if (dz2 is None) == (dpool is None):
+        raise ValueError("exactly one of dz2 / dpool")
+    if dz2 is not None:
+        _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    else:
+        _req(dpool, (B, 800), torch.float32, "dpool")
     _req(h_out, (B, 500), torch.float32, "h")
     _req(dh_out, (B, 500), torch.float32, "dh")
     _req(dlog_out, (B, 10), torch.float32, "dlogits")
@@ -413,8 +428,8 @@ def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh
               int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(), stage.tag.data_ptr())
     rc = lib.pto_mnist_fc1_bwd_head(h_parts[0].data_ptr(), h_parts[1].data_ptr(), fc1_bias.data_ptr(), w2.data_ptr(),
                                     b2.data_ptr(), lab.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
-                                    dz2.data_ptr(), h_out.data_ptr(), dh_out.data_ptr(), dlog_out.data_ptr(),
-                                    per_sample.data_ptr(), float(grad_scale), B, *st, _stream())
+                                    _ptr(dz2), h_out.data_ptr(), dh_out.data_ptr(), dlog_out.data_ptr(),
+                                    per_sample.data_ptr(), float(grad_scale), B, *st, _ptr(dpool), _stream())
     _native.check(rc, "fc1_bwd_head")
 
 
@@ -500,8 +515,12 @@ def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
 CONV2_W = (50, 20, 5, 5)
 
 
-def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optional[int] = None):
+def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optional[int] = None, *,
+              dpool: Optional[torch.Tensor] = None, idx2: Optional[torch.Tensor] = None):
     """conv backward with dW_conv2 summed over 4-sample chunks (deterministic, no atomics).
+
+    ``dz2`` [B,50,8,8], or ``dz2=None`` with ``dpool`` [B,800] (pooled, ReLU-masked d(a2)) and
+    ``idx2`` [B,800] uint8 (conv12_fwd's pool argmax): the kernel un-pools it while staging.
 
     ``slab``: contiguous fp32 [>= B, S]; ``offsets``: the row offsets (floats) of
     ``conv2.weight`` / ``conv2.bias`` / ``conv1.weight`` / ``conv1.bias`` inside a row (the
@@ -510,8 +529,14 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     ``slab_reduce(..., big=conv_bwd4_rows(B, offsets))``.
     """
     lib = _native.load()
-    B = dz2.shape[0] if B is None else B
-    _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    if (dz2 is None) == (dpool is None) or (dpool is None) != (idx2 is None):
+        raise ValueError("conv_bwd4 takes dz2, or dpool with idx2")
+    B = (dz2 if dz2 is not None else dpool).shape[0] if B is None else B
+    if dz2 is not None:
+        _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
+    else:
+        _req(dpool, (B, 800), torch.float32, "dpool")
+        _req(idx2, (B, 800), torch.uint8, "idx2")
     _req(w2, CONV2_W, torch.float32, "conv2.weight")
     _req(a1, (B, 20, 12, 12), torch.float32, "a1")
     _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
@@ -519,8 +544,8 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
         raise ValueError("slab must be contiguous fp32 [>=B, S]")
     o = [int(offsets[k]) for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
-    rc = lib.pto_mnist_conv_bwd4(dz2.data_ptr(), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
-                                 slab.data_ptr(), slab.shape[1], *o, B, _stream())
+    rc = lib.pto_mnist_conv_bwd4(_ptr(dz2), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
+                                 slab.data_ptr(), slab.shape[1], *o, B, _ptr(dpool), _ptr(idx2), _stream())
     _native.check(rc, "conv_bwd4")
 
 

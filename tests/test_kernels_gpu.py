@@ -396,6 +396,34 @@ def test_w1_tail_is_bit_identical_to_fc1_bwd_wgrad(lib, B):
     assert torch.equal(a.flat_grads[o2:o2 + 500], b.flat_grads[o2:o2 + 500])
 
 
+@pytest.mark.parametrize("fuse_head", [True, False])
+@pytest.mark.parametrize("B", [64, 37])
+def test_pooled_dz2_handoff_is_bit_identical(lib, B, fuse_head):
+    """Round 5: the input-gradient job hands d(a2) to conv_bwd4 still pooled ([B, 800]) and
+    conv_bwd4 un-pools it through idx2 while staging; the dense dz2 hand-off ([B, 50, 8, 8])
+    carries the same values, so 10 steps train bit-identically.  Also: the un-pooled image of
+    dpool is the dense dz2."""
+    n = 12 * B
+    x, y = _data(n, seed=800 + B, n_total=n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    a = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head, pooled_dz2=True)
+    b = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head, pooled_dz2=False)
+    a.train_step()
+    b.train_step()
+    torch.cuda.synchronize()
+    idx = a.idx2[:B].long()
+    dense = torch.zeros(B, 800, 4, device=idx.device).scatter_(2, idx[..., None], a.dpool[:B, :, None])
+    dense = dense.view(B, 50, 4, 4, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, 50, 8, 8)
+    assert torch.equal(dense, b.dz2[:B])
+    for _ in range(9):
+        a.train_step()
+        b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.flat_params, b.flat_params)
+    assert torch.equal(a.flat_momentum, b.flat_momentum)
+    assert torch.equal(a.stats, b.stats)
+
+
 @pytest.mark.parametrize("B", [64, 37])
 def test_fused_head_step_matches_head_kernel_step(lib, B):
     """Round 5: fc1_bwd with the head recomputed per sample tile on MFMA (no head launch; dW_fc2,
@@ -413,7 +441,8 @@ def test_fused_head_step_matches_head_kernel_step(lib, B):
     assert torch.equal(a.h1[:B], b.h1[:B])
     assert _rel(a.dlogits[:B], b.dlogits[:B]) < 1e-5
     assert _rel(a.dh[:B], b.dh[:B]) < 1e-5
-    assert _rel(a.dz2[:B], b.dz2[:B]) < 1e-5
+    da, db = (next(t for t in tr._dz2_out(B).values() if t is not None) for tr in (a, b))
+    assert _rel(da, db) < 1e-5  # the input-gradient hand-off (pooled or dense)
     assert torch.equal(a.per_sample[:B, 1], b.per_sample[:B, 1])
     assert _rel(a.per_sample[:B, 0], b.per_sample[:B, 0]) < 1e-5
     assert abs(float(a.stats[0]) - float(b.stats[0])) < 1e-5 * max(1.0, abs(float(b.stats[0])))
