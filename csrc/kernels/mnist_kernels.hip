@@ -1880,7 +1880,7 @@ __device__ __forceinline__ f32x4 bwd4_2b(const float* dzc_s, const float* a1c_s,
 }
 
 __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
-    const float* __restrict__ dz2, const float* __restrict__ dp, const uint8_t* __restrict__ ip,
+    const float* __restrict__ dp, const uint8_t* __restrict__ ip,
     const float* __restrict__ w2, const float* __restrict__ a1,
     const uint8_t* __restrict__ idx1, const float* __restrict__ xn, float* __restrict__ slab,
     int stride, int o_gw2, int o_gb2, int o_gw1, int o_gb1, int B, u64* dbg) {
@@ -1909,125 +1909,95 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   const int c0 = max(jbase, 0) / 25;  // first of the <= 2 input channels those columns touch
   stamp(dbg, 0);
 
-  // ---- phase 1: stage.  Group 1: the own sample's dz2 and the W2 slice; group 2: the chunk's
-  // other three samples, the 2b im2col source, the own a1 / idx1 / xn (measured: keeping group
-  // 2 in flight through phase 2a behind a second barrier was slower).  Every load independent
-  // and unpredicated (clamped addresses + selects).
-  // dp != null (round 5): dz2 arrives pooled -- d(a2) [B][800] (ReLU-masked) and conv12's pool
-  // argmax idx2 [B][800] -- and is un-pooled here into the LDS image: 4 KB per sample instead of
-  // 12.8 KB (3 of every 4 dz2 values are zeros), 16 instead of 51 KB of this block's staging loads
-  const bool pooled = dp != nullptr;  // kernel-uniform
-  float4 dv2[3];
-  float pd[4];
-  uint8_t pi[4];
-  float cv[2], av1;
-  uint8_t iv1;
-  float xv1;
-  {
-    float4 dv1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (pooled) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = min(tid + k * F_NT, 3199), sq = e / 800, f = e - sq * 800;
-        const size_t o = (size_t)min(4 * q + sq, B - 1) * 800 + f;
-        pd[k] = dp[o];
-        pi[k] = ip[o];
-      }
-    } else {
-      dv1 = reinterpret_cast<const float4*>(dz2 + (size_t)bo * 3200)[min(tid, 799)];
-    }
-    float wv_[F_NW2];
-#pragma unroll
-    for (int k = 0; k < F_NW2; ++k) {
-      const int e = tid + k * F_NT;
-      const int co = min(e >> 7, 49), j = min(e & 127, 124);
-      wv_[k] = w2[(size_t)co * 500 + cig * 125 + j];
-    }
-    // group 2
-    if (!pooled) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int e = min(tid + k * F_NT, 2399);
-        const int o = e / 800, s = o < r ? o : o + 1;  // the chunk's other samples
-        dv2[k] = reinterpret_cast<const float4*>(dz2 + (size_t)min(4 * q + s, B - 1) * 3200)[e - o * 800];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = min(tid + k * F_NT, 1151);
-      const int s = e / 288, rem = e - s * 288, c = rem / 144, p = rem - c * 144;
-      cv[k] = a1[(size_t)min(4 * q + s, B - 1) * 2880 + (cig * 5 + c0 + c) * 144 + p];
-    }
-    const int ec = min(tid, 719);
-    av1 = a1[(size_t)bo * 2880 + cig * 720 + ec];
-    iv1 = idx1[(size_t)bo * 2880 + cig * 720 + ec];
-    xv1 = xn[(size_t)bo * 784 + min(tid, 783)];
-    // group 1 -> LDS
-    if (pooled) {  // every sample of the chunk, un-pooled (samples >= B as 0)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = tid + k * F_NT;
-        if (e < 3200) {
-          const int sq = e / 800, f = e - sq * 800, co = f >> 4, ph = (f >> 2) & 3, pw = f & 3;
-          const float v = 4 * q + sq < B ? pd[k] : 0.f;
-          float* z = dzc_s + sq * G_DZN + co * G_DZS + (2 * ph) * 8 + 2 * pw;
-          z[0] = pi[k] == 0 ? v : 0.f;
-          z[1] = pi[k] == 1 ? v : 0.f;
-          z[8] = pi[k] == 2 ? v : 0.f;
-          z[9] = pi[k] == 3 ? v : 0.f;
-        }
-      }
-    } else if (tid < 800) {
-      const int co = tid >> 4, c4 = tid & 15;
-      const float4 v = own ? dv1 : make_float4(0.f, 0.f, 0.f, 0.f);
-      float2* d = reinterpret_cast<float2*>(dzc_s + r * G_DZN + co * G_DZS + 4 * c4);
-      d[0] = make_float2(v.x, v.y);
-      d[1] = make_float2(v.z, v.w);
-    }
-    if (tid < 512) {  // zero rows 50, 51 of every sample (2a reads co up to 51)
-      const int s = tid >> 7, rr = 50 + ((tid >> 6) & 1);
-      dzc_s[s * G_DZN + rr * G_DZS + (tid & 63)] = 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < F_NW2; ++k) {
-      const int e = tid + k * F_NT;
-      if (e < 6656) w_s[(e >> 7) * F_WS + (e & 127)] = ((e >> 7) >= 50 || (e & 127) >= 125) ? 0.f : wv_[k];
-    }
+  // ---- phase 1: stage.  dz2 arrives pooled -- d(a2) [B][800] (ReLU-masked) + conv12's pool
+  // argmax idx2 [B][800] -- and is un-pooled into the LDS image of the chunk's 4 samples (3.2 KB
+  // per sample instead of the 12.8 KB dense dz2); with it the W2 slice, the 2b im2col source, the
+  // own a1 / idx1 / xn.  Every load is a 16-byte vector (4-byte for idx2), spread over the
+  // waves (<= 6 per wave instead of 20 scalar ones), all issued before the first LDS write.
+  // The W2 slice is staged as the aligned float4 window w2[co][124 cig .. 124 cig + 128) and read
+  // at j + cig (2a's rows j >= 125 are garbage-in, never read by col2im).
+  float4 pdv = make_float4(0.f, 0.f, 0.f, 0.f), wq1 = pdv, cvv = pdv, avv = pdv, xvv = pdv;
+  uint32_t piv = 0u;
+  uint4 ivv = make_uint4(0u, 0u, 0u, 0u);
+  const int e_cv = tid - 736, e_av = tid - 640, e_x = tid - 800;  // 288 / 180 / 196 lanes
+  if (tid < 800) {
+    const int sq = tid / 200;
+    const size_t o = (size_t)min(4 * q + sq, B - 1) * 200 + (tid - sq * 200);
+    pdv = reinterpret_cast<const float4*>(dp)[o];
+    piv = reinterpret_cast<const uint32_t*>(ip)[o];
   }
-  // group 2 -> LDS (samples >= B of the chunk read as 0)
-  auto stage_g2 = [&]() {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = tid + k * F_NT;
-      if (!pooled && e < 2400) {
-        const int o = e / 800, s = o < r ? o : o + 1, rem = e - o * 800, co = rem >> 4, c4 = rem & 15;
-        const float4 v = 4 * q + s < B ? dv2[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-        float2* d = reinterpret_cast<float2*>(dzc_s + s * G_DZN + co * G_DZS + 4 * c4);
-        d[0] = make_float2(v.x, v.y);
-        d[1] = make_float2(v.z, v.w);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int e = tid + k * F_NT;
-      if (e < 1152) {
-        const int s = e / 288, rem = e - s * 288, c = rem / 144, p = rem - c * 144, y = p / 12;
-        a1c_s[s * G_A1S + c * F_A1C + y * F_A1R + (p - y * 12)] = 4 * q + s < B ? cv[k] : 0.f;
-      }
-    }
-    if (tid < 720) {
-      const int c = tid / 144, pp = tid - c * 144, yy = pp / 12;
-      a1_s[c * F_A1C + yy * F_A1R + (pp - yy * 12)] = av1;
-      idx_s[tid] = iv1;
-    }
-    if (tid < 784) x_s[(tid / 28) * F_XR + tid % 28] = xv1;
-  };
+  const float4* w24 = reinterpret_cast<const float4*>(w2) + cig * 31;
+  const float4 wq0 = w24[(tid >> 5) * 125 + (tid & 31)];
+  if (tid < 640) wq1 = w24[min((tid + 1024) >> 5, 49) * 125 + (tid & 31)];
+  if (e_cv >= 0) {
+    const int s = e_cv / 72, rem = e_cv - s * 72, c = rem / 36;
+    cvv = reinterpret_cast<const float4*>(a1)[(size_t)min(4 * q + s, B - 1) * 720 + (cig * 5 + c0 + c) * 36 +
+                                              (rem - c * 36)];
+  }
+  if (e_av >= 0 && e_av < 180) avv = reinterpret_cast<const float4*>(a1)[(size_t)bo * 720 + cig * 180 + e_av];
+  if (e_x >= 0 && e_x < 196) xvv = reinterpret_cast<const float4*>(xn)[(size_t)bo * 196 + e_x];
+  if (tid < 45) ivv = reinterpret_cast<const uint4*>(idx1)[(size_t)bo * 180 + cig * 45 + tid];
   __shared__ unsigned s_grp[2];  // group arrival counters (waves 0-7, waves 8-15)
   if (tid == 0) {
     s_grp[0] = 0u;
     s_grp[1] = 0u;
   }
-  stage_g2();
+  if (tid < 800) {  // the lane's 4 pooled values (one co, pooled row ph, pw 0..3) -> 2 rows x 8
+    const int sq = tid / 200, f4 = tid - sq * 200, co = f4 >> 2, ph = f4 & 3;
+    const bool ok = 4 * q + sq < B;  // samples >= B of the chunk as 0
+    const float v[4] = {pdv.x, pdv.y, pdv.z, pdv.w};
+    float2* z0 = reinterpret_cast<float2*>(dzc_s + sq * G_DZN + co * G_DZS + 16 * ph);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned pu = (piv >> (8 * u)) & 0xffu;
+      const float vv = ok ? v[u] : 0.f;
+      z0[u] = make_float2(pu == 0u ? vv : 0.f, pu == 1u ? vv : 0.f);
+      z0[4 + u] = make_float2(pu == 2u ? vv : 0.f, pu == 3u ? vv : 0.f);
+    }
+  }
+  if (tid < 512) {  // zero rows 50, 51 of every sample (2a reads co up to 51)
+    const int s = tid >> 7, rr = 50 + ((tid >> 6) & 1);
+    dzc_s[s * G_DZN + rr * G_DZS + (tid & 63)] = 0.f;
+  }
+  reinterpret_cast<float4*>(w_s + (tid >> 5) * F_WS)[tid & 31] = wq0;
+  if (tid < 640) {
+    const int co = (tid + 1024) >> 5;
+    reinterpret_cast<float4*>(w_s + co * F_WS)[tid & 31] = co < 50 ? wq1 : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (tid >= 960 && tid < 1012)  // window tail (j + cig reads up to m = 130)
+    reinterpret_cast<float4*>(w_s + (tid - 960) * F_WS)[32] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e_cv >= 0) {
+    const int s = e_cv / 72, rem = e_cv - s * 72, c = rem / 36, p4 = rem - c * 36, y = p4 / 3;
+    const bool ok = 4 * q + s < B;
+    float* d = a1c_s + s * G_A1S + c * F_A1C + y * F_A1R + 4 * (p4 - 3 * y);
+    d[0] = ok ? cvv.x : 0.f;
+    d[1] = ok ? cvv.y : 0.f;
+    d[2] = ok ? cvv.z : 0.f;
+    d[3] = ok ? cvv.w : 0.f;
+  }
+  if (e_av >= 0 && e_av < 180) {
+    const int c = e_av / 36, p4 = e_av - c * 36, y = p4 / 3;
+    float* d = a1_s + c * F_A1C + y * F_A1R + 4 * (p4 - 3 * y);
+    d[0] = avv.x;
+    d[1] = avv.y;
+    d[2] = avv.z;
+    d[3] = avv.w;
+  }
+  if (e_x >= 0 && e_x < 196) {
+    const int y = e_x / 7;
+    float* d = x_s + y * F_XR + 4 * (e_x - 7 * y);
+    d[0] = xvv.x;
+    d[1] = xvv.y;
+    d[2] = xvv.z;
+    d[3] = xvv.w;
+  }
+  if (tid < 45) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(idx_s) + 4 * tid;
+    d[0] = ivv.x;
+    d[1] = ivv.y;
+    d[2] = ivv.z;
+    d[3] = ivv.w;
+  }
   __syncthreads();
   stamp(dbg, 1);
 
@@ -2086,7 +2056,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   // ---- group A (waves 0-7): 2a, col2im, dW_conv1, the own sample's slab row
   if (!own) return;
-  bwd4_2a4(dzc_s, w_s, dcol_s, r, wv, lane);
+  bwd4_2a4(dzc_s, w_s + cig, dcol_s, r, wv, lane);
   float b2sum = 0.f;
   if (cig == 0 && tid < 50) {
     const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
@@ -2932,13 +2902,17 @@ int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, 
 // conv backward, dW_conv2 over 4-sample chunks (conv_bwd4_kernel): slab rows 0..ceil(B/4)-1
 // get the chunk partials of conv2.weight at row offset o_gw2; rows 0..B-1 the per-sample
 // conv1.weight / conv1.bias / conv2.bias partials at o_gw1 / o_gb1 / o_gb2.
-int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, const uint8_t* idx1,
-                        const float* xn, float* slab, int stride, int o_gw2, int o_gb2, int o_gw1,
-                        int o_gb1, int B, const float* dpool, const uint8_t* idx2, void* stream) {
+int pto_mnist_conv_bwd4(const float* dpool, const uint8_t* idx2, const float* w2, const float* a1,
+                        const uint8_t* idx1, const float* xn, float* slab, int stride, int o_gw2, int o_gb2,
+                        int o_gw1, int o_gb1, int B, void* stream) {
   PTO_CHECK_B(B);
   if (4 * ((B + 3) / 4) > 65535) return -1;  // grid y
-  if ((dz2 == nullptr) == (dpool == nullptr) || (dpool != nullptr && idx2 == nullptr)) return -1;  // one form
-  if ((stride & 3) || (o_gw2 & 3) || (((uintptr_t)slab) & 15) || (((uintptr_t)dz2) & 15)) return -2;
+  if (dpool == nullptr || idx2 == nullptr || w2 == nullptr || a1 == nullptr || idx1 == nullptr || xn == nullptr)
+    return -1;
+  // 16-byte staging loads (idx2: 4-byte)
+  if ((stride & 3) || (o_gw2 & 3) || ((((uintptr_t)slab) | ((uintptr_t)dpool) | ((uintptr_t)w2) | ((uintptr_t)a1) |
+                                       ((uintptr_t)idx1) | ((uintptr_t)xn)) & 15) || (((uintptr_t)idx2) & 3))
+    return -2;
   if (o_gw2 < 0 || o_gb2 < 0 || o_gw1 < 0 || o_gb1 < 0 || o_gw2 + 25000 > stride || o_gb2 + 50 > stride ||
       o_gw1 + 500 > stride || o_gb1 + 20 > stride)
     return -1;
@@ -2947,7 +2921,7 @@ int pto_mnist_conv_bwd4(const float* dz2, const float* w2, const float* a1, cons
   if (rc != 0) return rc;
   const int nb = 4 * ((B + 3) / 4);
   hipLaunchKernelGGL(conv_bwd4_kernel, dim3(4, nb), dim3(F_NT), G_LDS * sizeof(float), (hipStream_t)stream,
-                     dz2, dpool, idx2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
+                     dpool, idx2, w2, a1, idx1, xn, slab, stride, o_gw2, o_gb2, o_gw1, o_gb1, B, dbg_next());
   return (int)hipGetLastError();
 }
 

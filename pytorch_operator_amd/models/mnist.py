@@ -159,9 +159,6 @@ class FusedMnistTrainer:
         #   fuse_head (with w1_tail): fc1_bwd recomputes the head of its sample tile on MFMA (no
         #             head launch); dW_fc2 / db_fc2 / statistics move to the tail with their SGD
         self.fuse_head = os.environ.get("PTO_FUSE_HEAD", "1") != "0"
-        #   pooled_dz2 (conv_chunk 4): fc1_bwd hands d(a2) over still pooled ([B, 800], 3.2 KB per
-        #             sample instead of the 12.8 KB dense dz2); conv_bwd4 un-pools it via idx2
-        self.pooled_dz2 = os.environ.get("PTO_POOLED_DZ2", "1") != "0"
 
     # ---------------------------------------------------------------- state
     @property
@@ -267,8 +264,10 @@ class FusedMnistTrainer:
                h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
 
     def _dz2_out(self, B: int) -> dict:
-        """Where the input-gradient job writes: pooled d(a2) (conv_bwd4 un-pools it) or dense dz2."""
-        if self.pooled_dz2 and self.conv_chunk == 4:
+        """Where the input-gradient job writes: d(a2) still pooled ([B, 800], 3.2 KB per sample; conv_bwd4
+        un-pools it through idx2 -- round 5: -0.5 us per step, profiles/r5_dpool/ab.txt) or, for the
+        per-sample conv_bwd, the dense dz2."""
+        if self.conv_chunk == 4:
             return {"dz2": None, "dpool": self.dpool[:B]}
         return {"dz2": self.dz2[:B], "dpool": None}
 
@@ -298,10 +297,8 @@ class FusedMnistTrainer:
     def _conv_bwd(self, B: int) -> None:
         K, p = self.K, self._pv
         if self.conv_chunk == 4:
-            d = self._dz2_out(B)
-            K.conv_bwd4(d["dz2"], p["conv2.weight"], self.a1[:B], self.idx1[:B], self.xn[:B],
-                        self.conv_slab, self.layout.offsets, B, dpool=d["dpool"],
-                        idx2=self.idx2[:B] if d["dpool"] is not None else None)
+            K.conv_bwd4(self.dpool[:B], self.idx2[:B], p["conv2.weight"], self.a1[:B], self.idx1[:B],
+                        self.xn[:B], self.conv_slab, self.layout.offsets, B)
             self._last_big = K.conv_bwd4_rows(B, self.layout.offsets)
             return
         self._last_big = None

@@ -136,7 +136,7 @@ _SIGNATURES = {
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
     "pto_slab_reduce": [_VP, _I, _I, _I, _VP, _I, _I, _I, _VP],
     "pto_mnist_synth": [_VP, _VP, _VP, _I, ctypes.c_uint, _F, _VP],
-    "pto_mnist_conv_bwd4": [_VP] * 6 + [_I] * 6 + [_VP, _VP, _VP],
+    "pto_mnist_conv_bwd4": [_VP] * 7 + [_I] * 6 + [_VP],
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_tail": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _I, _I, _I]
                       + [_VP] * 9 + [_F] + [_VP] * 7,

@@ -515,13 +515,12 @@ def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
 CONV2_W = (50, 20, 5, 5)
 
 
-def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optional[int] = None, *,
-              dpool: Optional[torch.Tensor] = None, idx2: Optional[torch.Tensor] = None):
+def conv_bwd4(dpool, idx2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optional[int] = None):
     """conv backward with dW_conv2 summed over 4-sample chunks (deterministic, no atomics).
 
-    ``dz2`` [B,50,8,8], or ``dz2=None`` with ``dpool`` [B,800] (pooled, ReLU-masked d(a2)) and
-    ``idx2`` [B,800] uint8 (conv12_fwd's pool argmax): the kernel un-pools it while staging.
-
+    ``dpool`` [B, 800]: d(a2), pooled and ReLU-masked (``fc1_bwd(..., dpool=)`` /
+    ``fc1_bwd_head(..., dpool=)``); ``idx2`` [B, 800] uint8: conv12_fwd's pool argmax -- the
+    kernel un-pools dz2 while staging.
     ``slab``: contiguous fp32 [>= B, S]; ``offsets``: the row offsets (floats) of
     ``conv2.weight`` / ``conv2.bias`` / ``conv1.weight`` / ``conv1.bias`` inside a row (the
     flat conv-segment layout).  Rows 0..ceil(B/4)-1 receive the chunk partials of
@@ -529,14 +528,9 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     ``slab_reduce(..., big=conv_bwd4_rows(B, offsets))``.
     """
     lib = _native.load()
-    if (dz2 is None) == (dpool is None) or (dpool is None) != (idx2 is None):
-        raise ValueError("conv_bwd4 takes dz2, or dpool with idx2")
-    B = (dz2 if dz2 is not None else dpool).shape[0] if B is None else B
-    if dz2 is not None:
-        _req(dz2, (B, 50, 8, 8), torch.float32, "dz2")
-    else:
-        _req(dpool, (B, 800), torch.float32, "dpool")
-        _req(idx2, (B, 800), torch.uint8, "idx2")
+    B = dpool.shape[0] if B is None else B
+    _req(dpool, (B, 800), torch.float32, "dpool")
+    _req(idx2, (B, 800), torch.uint8, "idx2")
     _req(w2, CONV2_W, torch.float32, "conv2.weight")
     _req(a1, (B, 20, 12, 12), torch.float32, "a1")
     _req(idx1, (B, 20, 12, 12), torch.uint8, "idx1")
@@ -544,8 +538,8 @@ def conv_bwd4(dz2, w2, a1, idx1, xn, slab: torch.Tensor, offsets: dict, B: Optio
     if slab.dim() != 2 or slab.shape[0] < B or not slab.is_contiguous() or slab.dtype != torch.float32:
         raise ValueError("slab must be contiguous fp32 [>=B, S]")
     o = [int(offsets[k]) for k in ("conv2.weight", "conv2.bias", "conv1.weight", "conv1.bias")]
-    rc = lib.pto_mnist_conv_bwd4(_ptr(dz2), w2.data_ptr(), a1.data_ptr(), idx1.data_ptr(), xn.data_ptr(),
-                                 slab.data_ptr(), slab.shape[1], *o, B, _ptr(dpool), _ptr(idx2), _stream())
+    rc = lib.pto_mnist_conv_bwd4(dpool.data_ptr(), idx2.data_ptr(), w2.data_ptr(), a1.data_ptr(),
+                                 idx1.data_ptr(), xn.data_ptr(), slab.data_ptr(), slab.shape[1], *o, B, _stream())
     _native.check(rc, "conv_bwd4")
 
 

@@ -272,7 +272,11 @@ def test_conv_bwd4_chunked_slab_matches_autograd(lib, B):
     ce = lay.conv_end
     slab = torch.full((B, ce), float("nan"), device=dev)
     slab.zero_()
-    K.conv_bwd4(dz2, p["conv2.weight"], a1, idx1, xnk, slab, lay.offsets, B)
+    # conv_bwd4 takes dz2 pooled: d at each window's argmax + the argmax code (dy * 2 + dx)
+    _, ind = F.max_pool2d(F.relu(z2.detach()), 2, 2, return_indices=True)  # [B, 50, 4, 4] into 8 x 8
+    dpool = z2.grad.flatten(2).gather(2, ind.flatten(2)).reshape(B, 800).contiguous().to(dev)
+    idx2 = (((ind // 8) % 2) * 2 + ind % 2).reshape(B, 800).to(torch.uint8).contiguous().to(dev)
+    K.conv_bwd4(dpool, idx2, p["conv2.weight"], a1, idx1, xnk, slab, lay.offsets, B)
     got = torch.empty(ce, device=dev)
     K.slab_reduce(slab, B, got, big=K.conv_bwd4_rows(B, lay.offsets))
     # per-sample path
@@ -291,7 +295,7 @@ def test_conv_bwd4_chunked_slab_matches_autograd(lib, B):
         assert _rel(got[o:o + n], ref1[o:o + n]) < 1e-5, name
     # the per-sample small partials and chunk rows are deterministic: a second launch is bit-identical
     slab2 = torch.zeros_like(slab)
-    K.conv_bwd4(dz2, p["conv2.weight"], a1, idx1, xnk, slab2, lay.offsets, B)
+    K.conv_bwd4(dpool, idx2, p["conv2.weight"], a1, idx1, xnk, slab2, lay.offsets, B)
     got2 = torch.empty(ce, device=dev)
     K.slab_reduce(slab2, B, got2, big=K.conv_bwd4_rows(B, lay.offsets))
     torch.cuda.synchronize()
@@ -398,16 +402,15 @@ def test_w1_tail_is_bit_identical_to_fc1_bwd_wgrad(lib, B):
 
 @pytest.mark.parametrize("fuse_head", [True, False])
 @pytest.mark.parametrize("B", [64, 37])
-def test_pooled_dz2_handoff_is_bit_identical(lib, B, fuse_head):
-    """Round 5: the input-gradient job hands d(a2) to conv_bwd4 still pooled ([B, 800]) and
-    conv_bwd4 un-pools it through idx2 while staging; the dense dz2 hand-off ([B, 50, 8, 8])
-    carries the same values, so 10 steps train bit-identically.  Also: the un-pooled image of
-    dpool is the dense dz2."""
+def test_pooled_dz2_unpools_to_the_dense_dz2(lib, B, fuse_head):
+    """Round 5: with conv_bwd4 the input-gradient job hands d(a2) over still pooled ([B, 800]) and
+    conv_bwd4 un-pools it through idx2 while staging.  Its un-pooled image is bit-identical to
+    the dense dz2 ([B, 50, 8, 8]) the same job writes for the per-sample conv_bwd (conv_chunk 1)."""
     n = 12 * B
     x, y = _data(n, seed=800 + B, n_total=n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32)
-    a = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head, pooled_dz2=True)
-    b = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head, pooled_dz2=False)
+    a = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head)
+    b = _stage_trainer(x, y, perm, B=B, fuse_head=fuse_head, conv_chunk=1)
     a.train_step()
     b.train_step()
     torch.cuda.synchronize()
@@ -415,13 +418,7 @@ def test_pooled_dz2_handoff_is_bit_identical(lib, B, fuse_head):
     dense = torch.zeros(B, 800, 4, device=idx.device).scatter_(2, idx[..., None], a.dpool[:B, :, None])
     dense = dense.view(B, 50, 4, 4, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, 50, 8, 8)
     assert torch.equal(dense, b.dz2[:B])
-    for _ in range(9):
-        a.train_step()
-        b.train_step()
-    torch.cuda.synchronize()
-    assert torch.equal(a.flat_params, b.flat_params)
-    assert torch.equal(a.flat_momentum, b.flat_momentum)
-    assert torch.equal(a.stats, b.stats)
+    assert _rel(a.flat_params, b.flat_params) < 1e-6
 
 
 @pytest.mark.parametrize("B", [64, 37])

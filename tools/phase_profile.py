@@ -50,7 +50,7 @@ def main():
                                         tr.slab_views["conv2.weight"], tr.slab_views["conv2.bias"],
                                         tr.slab_views["conv1.weight"], tr.slab_views["conv1.bias"],
                                         slab=tr.conv_slab)),
-        ("conv_bwd4", lambda: K.conv_bwd4(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn, tr.conv_slab,
+        ("conv_bwd4", lambda: K.conv_bwd4(tr.dpool, tr.idx2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn, tr.conv_slab,
                                           lay.offsets, B)),
         ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
                                                     tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
