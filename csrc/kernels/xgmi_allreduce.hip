@@ -86,6 +86,11 @@ struct XarArgs {
   int* err;
   long long timeout_ticks;  // wall_clock64 ticks (100 MHz)
   unsigned long long* stamps;  // optional: 4 wall_clock64 stamps per (rank, block)
+  // stamp_ring > 0 (the one-rank-per-process exchange, diagnostics): stamps is a ring of
+  // stamp_ring launches x nblk records of 8 words -- step, block start, flag1 raised, flag2
+  // raised, end, error word at the end, first pending flag1 index (q * nblk + j) + 1 at a
+  // phase-2 timeout; a launch that starts degraded writes none (the failing one is kept)
+  int stamp_ring;
   int light_fence;  // exchange buffers are uncached: no L2 writeback / invalidate needed
 };
 
@@ -282,7 +287,19 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   const unsigned s = s_step;
   const bool degraded = s_degraded;
   const long long deadline = (long long)wall_clock64() + a.timeout_ticks;
-  unsigned long long* st = a.stamps != nullptr ? a.stamps + ((long)a.rank * a.nblk + b) * 4 : nullptr;
+  unsigned long long* st = nullptr;
+  if (a.stamps != nullptr) {
+    if (a.stamp_ring == 0) {
+      st = a.stamps + ((long)a.rank * a.nblk + b) * 4;
+    } else if (!degraded) {
+      unsigned long long* r = a.stamps + ((long)(s % (unsigned)a.stamp_ring) * a.nblk + b) * 8;
+      if (tid == 0) {
+        r[0] = s;
+        for (int k = 2; k < 8; ++k) r[k] = 0ull;
+      }
+      st = r + 1;
+    }
+  }
   if (st != nullptr && tid == 0) st[0] = wall_clock64();
   const f4 zero4 = f4{0.f, 0.f, 0.f, 0.f};
 
@@ -388,8 +405,15 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     // pre-push start as soon as the matching sender block is in its exchange
     int src_lo[3], src_hi[3];
     push_sources(a, b, src_lo, src_hi);
-    wait_flag_ranges<NT>(reinterpret_cast<const unsigned*>(mine), a.nblk, a.world, src_lo, src_hi, s, deadline,
-                         a.err, kErrPushWait);
+    const bool got = wait_flag_ranges<NT>(reinterpret_cast<const unsigned*>(mine), a.nblk, a.world, src_lo,
+                                          src_hi, s, deadline, a.err, kErrPushWait);
+    if (!got && st != nullptr && a.stamp_ring > 0) {  // which sender block was missing
+      const unsigned* f = reinterpret_cast<const unsigned*>(mine);
+      for (int k = 0; k < 3; ++k)
+        for (int j = src_lo[k] + tid; j < src_hi[k]; j += NT)
+          for (int q = 0; q < a.world; ++q)
+            if (load_sys(f + q * a.nblk + j) < s) atomicCAS(&st[5], 0ull, (unsigned long long)(q * a.nblk + j + 1));
+    }
     acquire_fence(a);
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
       // every sender's contribution in flight at once (clamped addresses, no predicated
@@ -470,7 +494,10 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   }
   if (a.step_counter != nullptr && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
   if (tid == 0) store_sys(stepc(mine, a.nblk, b), s);
-  if (st != nullptr && tid == 0) st[3] = wall_clock64();
+  if (st != nullptr && tid == 0) {
+    st[3] = wall_clock64();
+    if (a.stamp_ring > 0) st[4] = (unsigned long long)__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body<kThreads>(a, blockIdx.x); }
@@ -503,6 +530,8 @@ struct XarCtx {
   char* base[kMaxWorld];
   int* err;
   long long timeout_ticks;
+  unsigned long long* stamps;  // optional diagnostics ring (pto_xar_stamps)
+  int stamp_ring;
 };
 
 long round_up(long x, long m) { return (x + m - 1) / m * m; }
@@ -585,6 +614,17 @@ long pto_xar_npad(void* ctx) { return static_cast<XarCtx*>(ctx)->npad; }
 // producer that pushes into peers' receive buffers checks it and stops pushing (XPush::err).
 void* pto_xar_err_ptr(void* ctx) { return static_cast<XarCtx*>(ctx)->err; }
 
+// Diagnostics: per-block phase stamps of the last `ring` launches into buf (ring x nblk x 8
+// uint64, see XarArgs::stamp_ring; wall_clock64 at 100 MHz, shared by every process on the GPU).
+// Null buf turns them off.  Applies to launches made (or captured) afterwards.
+int pto_xar_stamps(void* ctx, unsigned long long* buf, int ring) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  if (buf != nullptr && ring < 1) return -1;
+  c->stamps = buf;
+  c->stamp_ring = buf != nullptr ? ring : 0;
+  return 0;
+}
+
 // Map every peer's buffer (handles: world x 64 bytes, in rank order).
 int pto_xar_open(void* ctx, const void* handles) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
@@ -618,6 +658,8 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.chunk4 = a.shard4 / c->nblk;
   a.err = c->err;
   a.timeout_ticks = c->timeout_ticks;
+  a.stamps = c->stamps;
+  a.stamp_ring = c->stamp_ring;
   a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
   hipLaunchKernelGGL(xar_kernel, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);

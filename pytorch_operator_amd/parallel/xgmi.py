@@ -155,6 +155,18 @@ class XgmiAllReduce:
     def error(self) -> int:
         return int(self.lib.pto_xar_error(self._ctx))
 
+    def enable_stamps(self, ring: int = 16) -> torch.Tensor:
+        """Diagnostics: every later (or later-captured) launch records, per workgroup, its step,
+        wall_clock64 stamps (100 MHz, one clock for every process on the GPU) at start / flag1
+        raised / flag2 raised / end, the error word at the end and, after a phase-2 timeout, the
+        first sender flag still missing (q * nblk + j + 1) -- into a ring of the last ``ring``
+        launches, [ring, nblk, 8] int64.  A launch that starts degraded writes nothing, so the
+        record of the launch that timed out survives."""
+        self.stamps = torch.zeros((ring, self.nblk, 8), dtype=torch.int64, device=self.device)
+        _native.check(self.lib.pto_xar_stamps(self._ctx, ctypes.c_void_p(self.stamps.data_ptr()), int(ring)),
+                      "pto_xar_stamps")
+        return self.stamps
+
     def _check(self, t: torch.Tensor) -> None:
         if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == self.n):
             raise ValueError(f"expected contiguous fp32 CUDA tensor of {self.n} elements")

@@ -26,8 +26,9 @@ def _port():
 @pytest.mark.parametrize("world,nblk", [(2, 0), (4, 0), (2, 256)])
 def test_xgmi_allreduce_ranks(tmp_path, world, nblk):
     """nblk=0 picks 128 workgroups per rank here (ranks share the box's GPU); nblk=256 runs the
-    geometry a one-GPU-per-rank job uses (eager and graph stages; the autotune hand-over stage runs
-    on a 128-workgroup exchange there, tools/xgmi_check.py)."""
+    geometry a one-GPU-per-rank job uses, every stage including the autotune hand-over, with the
+    step's kernels that fit beside a spinning exchange workgroup (tools/xgmi_check.py,
+    tests/test_kernel_resources.py)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
            "--backend", "gloo", "--out", str(tmp_path), "--nblk", str(nblk)]

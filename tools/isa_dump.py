@@ -19,6 +19,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
 _MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -52,6 +53,36 @@ def disassemble(lib: Path, arch: str = "gfx950") -> str:
             r = subprocess.run([OBJDUMP, "-d", f"--mcpu={arch}", f.name], capture_output=True, text=True, check=True)
             texts.append(r.stdout)
     return "\n".join(texts)
+
+
+def kernel_resources(lib: Path, arch: str = "gfx950") -> dict:
+    """{kernel name: {vgpr, agpr, sgpr, lds (static bytes), max_wg, spills}} from the AMDGPU metadata
+    note of every code object (``llvm-readelf --notes``)."""
+    import yaml
+    out = {}
+    for _, b in ((t, b) for t, b in code_objects(lib) if arch in t):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(b)
+            f.flush()
+            r = subprocess.run([READELF, "--notes", f.name], capture_output=True, text=True, check=True)
+        text = r.stdout
+        i = text.find("---")
+        j = text.find("\n...", i)
+        meta = yaml.safe_load(text[i:j if j > 0 else None])
+        for k in meta.get("amdhsa.kernels", []):
+            out[k[".name"]] = {"vgpr": k.get(".vgpr_count", 0), "agpr": k.get(".agpr_count", 0),
+                               "sgpr": k.get(".sgpr_count", 0), "lds": k.get(".group_segment_fixed_size", 0),
+                               "max_wg": k.get(".max_flat_workgroup_size", 0),
+                               "spills": k.get(".vgpr_spill_count", 0)}
+    return out
+
+
+def vgpr_alloc(res: dict) -> int:
+    """VGPRs one wave of the kernel takes from its SIMD's 512 (arch VGPRs 4-aligned, then the
+    AGPRs, in granules of 8)."""
+    v, a = res["vgpr"], res["agpr"]
+    t = ((v + 3) // 4 * 4 + a) if a else v
+    return (t + 7) // 8 * 8
 
 
 def kernel_bodies(disasm: str, name_substr: str) -> dict:

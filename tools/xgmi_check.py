@@ -57,6 +57,14 @@ def main(argv=None) -> int:
     ap.add_argument("--nblk", type=int, default=0,
                     help="workgroups per rank (0 = auto: 256 when every rank owns its GPU, 128 "
                          "when ranks share one; 256 on a shared GPU runs the cross-device geometry)")
+    ap.add_argument("--handover-nblk", type=int, default=0,
+                    help="workgroups of the hand-over stage's exchange (0 = the main exchange's)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="record the hand-over exchange's per-workgroup phase stamps (XgmiAllReduce."
+                         "enable_stamps) and write <out>/rank<r>_stamps.json (tools/xgmi_stamps.py reads them)")
+    ap.add_argument("--fuse-conv12", type=int, default=-1,
+                    help="1/0: force the fused conv12 forward on/off (default: off when ranks share a GPU at "
+                         "256 workgroups, see below; 1 there reproduces the starvation)")
     ap.add_argument("--bench", action="store_true",
                     help="time the fused exchange alone (graph of back-to-back launches)")
     a = ap.parse_args(argv)
@@ -77,21 +85,27 @@ def main(argv=None) -> int:
     xar = XgmiAllReduce(L, device=dev, nblk=a.nblk)
     res["nblk"] = xar.nblk
     res["alloc_kind"] = xar.alloc_kind
+    stamps_main = xar.enable_stamps(64) if a.stamps else None
     res["self_test"] = xar.self_test()
     res["self_test_report"] = xar.last_report[:4]
 
     ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
-    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each):
-    # a rank's exchange blocks spin on every CU until its peer reaches the same step, so the
-    # peer's conv backward must fit on a CU NEXT to them.  The 4-sample-chunk conv_bwd4 block
-    # (152 KB of LDS, 16 waves) does not fit beside two ranks' exchange blocks and the shared-GPU
-    # rehearsal then times out (the job topology never has this: one rank per GPU runs its own
-    # kernels in stream order); the per-sample conv_bwd block (105 KB) does.  The chunked slab
-    # path of the exchange is covered by the auto-geometry runs (128 workgroups per rank).
+    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each): a
+    # rank's exchange workgroups spin on every CU until its peer reaches the same step, so every
+    # kernel of the peer's step must fit on a CU beside one of them (one wave per SIMD, 112 VGPRs):
+    # <= 512 VGPRs per SIMD.  The fused conv12 forward (4 waves x 104) and the 4-sample-chunk
+    # conv_bwd4 (152 KB of LDS) do not: their workgroups waited until the peer's exchange timed
+    # out -- the exchange's stamps show the peer's exchange starting 5 s late, just after the
+    # waiter's deadline released the CUs (profiles/r5_xgmi_handover.md).  So that rehearsal runs
+    # the split conv1 / conv2 forward and the per-sample conv_bwd (tests/test_kernel_resources.py
+    # keeps them within the budget).  The job topology never has this: one rank per GPU runs its
+    # own kernels in stream order.  The chunked paths are covered by the auto-geometry runs (128
+    # workgroups per rank).
     peers = [None] * world
     dist.all_gather_object(peers, dev.index)
     shared_256 = len(set(peers)) < world and xar.nblk >= 256
     res["conv_chunk"] = 1 if shared_256 else 4
+    res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not shared_256
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -99,6 +113,7 @@ def main(argv=None) -> int:
         tr = FusedMnistTrainer(batch_size=64, source=src, lr=0.01, momentum=0.5, device=dev, seed=1,
                                grad_sync=sync)
         tr.conv_chunk = res["conv_chunk"]
+        tr.fuse_conv12 = res["fuse_conv12"]
         dist.broadcast(tr.flat_params, 0)
         return tr
 
@@ -128,16 +143,13 @@ def main(argv=None) -> int:
     res["graph_in_sync"] = bool(torch.equal(ref, ta.flat_params))
     res["error_after"]["graph"] = xar.error()
     res["finite"] = bool(torch.isfinite(ta.flat_params).all())
-    # autotune hand-over in both directions keeps the replicas identical.  Ranks sharing one GPU
-    # at the one-GPU-per-rank geometry (256 exchange workgroups each) run this stage on a second
-    # exchange at 128 workgroups: the race's trial runs pack both ranks' kernels back to back, and
-    # at 2 x 256 spinning workgroups the peer's compute kernels are not guaranteed a CU -- the
-    # stage timed out (both waits, error 3) in 2 of 5 stream-launched and 1 of 4 graph-launched
-    # rehearsals (tools/gpu/sessions/r4_s4.sh, r4_s31.sh) while every eager and graph stage above passed.
-    # One rank per GPU never has that squeeze; the hand-over logic does not depend on the geometry,
-    # and the 256-workgroup exchange itself is covered by the stages above.
+    # autotune hand-over in both directions keeps the replicas identical (on the main exchange's
+    # geometry; round 4 ran it at 128 workgroups when ranks shared a GPU at 256 -- the timeouts
+    # that prompted it were the co-residency starvation above, not the hand-over)
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
-    hx = XgmiAllReduce(L, device=dev, nblk=128) if shared_256 else xar
+    hnb = a.handover_nblk or xar.nblk
+    hx = XgmiAllReduce(L, device=dev, nblk=hnb) if hnb != xar.nblk else xar
+    stamps_hx = hx.enable_stamps(64) if a.stamps and hx is not xar else None
     if hx is not xar:
         res["handover_self_test"] = hx.self_test()
     res["handover_nblk"] = hx.nblk
@@ -159,6 +171,19 @@ def main(argv=None) -> int:
     if a.bench:
         res["exchange_us"] = _bench_exchange(xar, ta, dev)
     res["kernel_error"] = xar.error() | (hx.error() if hx is not xar else 0)
+    if a.stamps and a.out:
+        torch.cuda.synchronize(dev)
+        res["stamp_rows"] = {}
+        for tag, xx, st in (("main", xar, stamps_main), ("handover", hx, stamps_hx)):
+            if st is None:
+                continue
+            rows = [[i % xx.nblk] + r[:7] for i, r in enumerate(st.view(-1, 8).cpu().tolist()) if r[0] > 0]
+            os.makedirs(os.path.join(a.out, f"stamps_{tag}"), exist_ok=True)
+            with open(os.path.join(a.out, f"stamps_{tag}", f"rank{rank}_stamps.json"), "w") as f:
+                json.dump({"rank": rank, "world": world, "nblk": xx.nblk, "error": xx.error(), "timeout_s": 5.0,
+                           "fields": ["block", "step", "start", "flag1", "flag2", "end", "err", "missing"],
+                           "rows": rows}, f)
+            res["stamp_rows"][tag] = len(rows)
     ok = res.get("handover_self_test", True) and res["self_test"] and res["eager_match"] and res["push_bit_identical"] and res["graph_in_sync"] and res["finite"] \
         and res["kernel_error"] == 0 and res["handover_rccl_in_sync"] and res["handover_xgmi_in_sync"]
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
