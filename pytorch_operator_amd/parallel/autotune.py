@@ -47,18 +47,52 @@ def _delay_ms(name: str) -> float:
     return 0.0
 
 
+def _sync(device) -> None:
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def _timed(runner: GraphedStep, steps: int, device, name: str) -> float:
-    torch.cuda.synchronize(device)
+    _sync(device)
     dist.barrier()
     t0 = time.perf_counter()
     runner.warm(steps)
     delay = _delay_ms(name)
     if delay > 0:
         time.sleep(delay * steps / 1e3)
-    torch.cuda.synchronize(device)
+    _sync(device)
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def graph_comm_precheck(tr) -> Optional[str]:
+    """Why this rank cannot capture the step with its collectives (None: it can).  Local checks
+    only -- no collective is issued -- so every rank can agree on the answer before any rank
+    enters the candidate's warm-up collectives (a rank raising inside them while the
+    others wait in an all-reduce would hang the job)."""
+    if dist.get_backend() != "nccl":
+        return f"{dist.get_backend()} collectives are not capturable"
+    if "rccl-graph" in os.environ.get("PTO_RACE_SKIP", "").split(","):
+        return "PTO_RACE_SKIP"
+    try:
+        ver = torch.cuda.nccl.version()
+    except Exception as e:  # noqa: BLE001
+        return f"RCCL version unknown: {e!r}"[:120]
+    if tuple(ver[:2]) < (2, 9):
+        return f"RCCL {ver} predates collective stream capture"
+    gs = tr.grad_sync
+    if gs is None or not bool(getattr(gs, "active", True)) or getattr(gs, "fused_sgd", False):
+        return "the step issues no RCCL collective"
+    if os.environ.get("PTO_FAULT_GRAPH_COMM_PRECHECK") == str(dist.get_rank()):
+        return "fault injection"  # tests: one rank says no
+    return None
+
+
+def _agree(flag: bool, dev) -> bool:
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
 
 
 def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: int = 10,
@@ -85,31 +119,44 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     runners["rccl"] = r
     times["rccl"] = _timed(r, trial, dev, "rccl")
     steps += r.internal_steps + trial
-    if eager:
-        skipped["rccl-graph"] = "eager race"
-    elif dist.get_backend() != "nccl":
-        skipped["rccl-graph"] = f"{dist.get_backend()} collectives are not capturable"
-    elif "rccl-graph" in os.environ.get("PTO_RACE_SKIP", "").split(","):
-        skipped["rccl-graph"] = "PTO_RACE_SKIP"
+    why = "eager race" if eager else graph_comm_precheck(tr)
+    # every rank agrees on the pre-check before any rank issues the candidate's collectives
+    if not _agree(why is None, dev):
+        skipped["rccl-graph"] = why or "pre-check failed on another rank"
     else:
-        # a capture that fails does so on every rank (same code, same data): every rank then
-        # drops the candidate together (the flag all-reduce keeps the ranks' collectives paired)
+        # past the pre-check, the candidate's eager warm-up steps are the rccl trial's (which just
+        # ran on every rank); what can still fail is the capture itself, which issues no
+        # collective -- so a failing rank reaches the agreement below like the others
         err = None
         try:
             r = GraphedStep(tr, mode="graph-comm")
         except Exception as e:  # noqa: BLE001 -- the race must survive a failed candidate
             err, r = repr(e)[:200], None
-        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 1:
+            steps += int(getattr(e, "internal_steps", 0))
+        if _agree(err is None, dev):
             runners["rccl-graph"] = r
             times["rccl-graph"] = _timed(r, trial, dev, "rccl-graph")
             steps += r.internal_steps + trial
         else:
+            if r is not None:
+                steps += r.internal_steps
             skipped["rccl-graph"] = f"capture failed: {err or 'on another rank'}"
-            torch.cuda.synchronize(dev)
+            # leave no half-captured work behind, then prove the stream and the communicator
+            # still work (one all-reduce every rank issues); if they do not, no further trials
+            _sync(dev)
+            try:
+                probe = torch.ones(1, device=dev)
+                dist.all_reduce(probe)
+                _sync(dev)
+                healthy = int(probe.item()) == dist.get_world_size()
+            except Exception:  # noqa: BLE001
+                healthy = False
+            if not healthy:
+                skipped["xgmi"] = "communicator unhealthy after a failed capture"
+                xgmi_sync = None
+                skipped.setdefault("rccl-graph", "capture failed")
     if xgmi_sync is None:
-        skipped["xgmi"] = "no xGMI exchange (world 1 or self-test failed)"
+        skipped.setdefault("xgmi", "no xGMI exchange (world 1 or self-test failed)")
     else:
         tr.grad_sync = xgmi_sync
         r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)

@@ -130,7 +130,14 @@ class GraphedStep:
         self.launch = "graph"
         if mode == "eager":
             return
-        tr = trainer
+        try:
+            self._prepare(native, launch)
+        except Exception as e:
+            e.internal_steps = self.internal_steps  # steps taken before the failure (autotune counts them)
+            raise
+
+    def _prepare(self, native: bool, launch: str) -> None:
+        tr, mode = self.tr, self.mode
         if tr._first_step:
             tr.train_step()  # momentum initialisation happens outside any graph
             self.internal_steps += 1

@@ -1,0 +1,97 @@
+"""The DDP gradient-path race survives a candidate that fails on some ranks only:
+every rank agrees on the one-graph RCCL candidate's pre-check before any rank issues its
+collectives, a capture failure on one rank drops the candidate on all of them (no hang), the
+steps taken before the failure are counted, and the communicator is probed before the race
+goes on.  Two gloo ranks on the CPU with a stand-in step runner (no GPU)."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+import torch
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, scenario, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pytorch_operator_amd.parallel.autotune as at
+
+    class Tr:
+        device = torch.device("cpu")
+        grad_sync = None
+        log = []
+
+    class FakeStep:
+        def __init__(self, tr, mode="graph", steps_per_graph=1, launch="graph", **kw):
+            self.internal_steps, self.launch = 1, launch
+            if mode == "graph-comm":
+                tr.log.append("graph-comm built")
+                if scenario == "capture_fails" and rank == 1:
+                    e = RuntimeError("stream capture failed")
+                    e.internal_steps = 2
+                    raise e
+
+        def warm(self, n):
+            pass
+
+    at.GraphedStep = FakeStep
+    at.graph_comm_precheck = lambda tr: "no capture here" if scenario == "precheck_fails" and rank == 1 else None
+    tr = Tr()
+    try:
+        _, pick, rec = at.choose_grad_sync(tr, object(), None, trial_steps=2)
+        q.put((rank, pick, rec, list(tr.log)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _race(scenario):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, scenario, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        rank, pick, rec, log = q.get(timeout=120)
+        out[rank] = (pick, rec, log)
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.timeout(180)
+def test_precheck_disagreement_skips_the_candidate_everywhere_before_its_collectives():
+    out = _race("precheck_fails")
+    for rank, (pick, rec, log) in out.items():
+        assert pick == "rccl" and rec["rccl_graph_ms_per_step"] is None
+        assert log == []  # no rank built (entered the warm-up collectives of) the candidate
+    assert out[1][1]["rccl_graph_skipped"] == "no capture here"
+    assert out[0][1]["rccl_graph_skipped"] == "pre-check failed on another rank"
+
+
+@pytest.mark.timeout(180)
+def test_capture_failure_on_one_rank_drops_the_candidate_on_all():
+    out = _race("capture_fails")
+    for rank, (pick, rec, log) in out.items():
+        assert pick == "rccl" and rec["rccl_graph_ms_per_step"] is None
+        assert rec["rccl_graph_skipped"].startswith("capture failed")
+        assert rec["xgmi_skipped"].startswith("no xGMI")  # the communicator probe passed
+    assert "stream capture failed" in out[1][1]["rccl_graph_skipped"]
+    # rccl trial: 1 internal + 2 timed; the failed candidate: 2 (rank 1) / 1 (rank 0) internal
+    assert out[1][1]["steps"] == 5 and out[0][1]["steps"] == 4
+
+
+@pytest.mark.timeout(180)
+def test_candidate_runs_when_every_rank_can_capture():
+    out = _race("ok")
+    for rank, (pick, rec, log) in out.items():
+        assert rec["rccl_graph_ms_per_step"] is not None and log == ["graph-comm built"]
