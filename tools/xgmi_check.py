@@ -90,9 +90,9 @@ def main(argv=None) -> int:
     res["self_test_report"] = xar.last_report[:4]
 
     ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
-    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each): a
-    # rank's exchange workgroups spin on every CU until its peer reaches the same step, so every
-    # kernel of the peer's step must fit on a CU beside one of them (one wave per SIMD, 112 VGPRs):
+    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each; or 4
+    # ranks at 128): a rank's exchange workgroups spin on every CU until its peer reaches the same
+    # step, so every kernel of the peer's step must fit on a CU beside one of them (one wave per SIMD, 112 VGPRs):
     # <= 512 VGPRs per SIMD.  The fused conv12 forward (4 waves x 104) and the 4-sample-chunk
     # conv_bwd4 (152 KB of LDS) do not: their workgroups waited until the peer's exchange timed
     # out -- the exchange's stamps show the peer's exchange starting 5 s late, just after the
@@ -103,9 +103,14 @@ def main(argv=None) -> int:
     # workgroups per rank).
     peers = [None] * world
     dist.all_gather_object(peers, dev.index)
-    shared_256 = len(set(peers)) < world and xar.nblk >= 256
-    res["conv_chunk"] = 1 if shared_256 else 4
-    res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not shared_256
+    # crowded: while one rank computes, the other ranks on its GPU may all be spinning in their
+    # exchanges -- (ranks on the GPU - 1) x nblk workgroups, enough to sit on every one of the 256
+    # CUs (2 ranks x 256, 4 ranks x 128, ...)
+    on_gpu = sum(1 for p in peers if p == dev.index)
+    crowded = on_gpu > 1 and (on_gpu - 1) * xar.nblk >= 256
+    res["crowded"] = crowded
+    res["conv_chunk"] = 1 if crowded else 4
+    res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not crowded
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
