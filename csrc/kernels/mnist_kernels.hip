@@ -67,8 +67,8 @@ __device__ __forceinline__ void stamp_by(u64* dbg, int phase, int who) {
   (void)dbg; (void)phase; (void)who;
 #endif
 }
-__device__ __forceinline__ void stamp(u64* dbg, int phase) {
-  if (dbg != nullptr && threadIdx.x == 0) {
+__device__ __forceinline__ void stamp(u64* dbg, int phase, int thread = 0) {
+  if (dbg != nullptr && (int)threadIdx.x == thread) {
     const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
     dbg[blk * 16 + phase] = (u64)wall_clock64();
     dbg[blk * 16 + 8 + phase] = (u64)clock64();  // shader clock -> effective GHz per phase
@@ -1814,6 +1814,31 @@ __device__ __forceinline__ void wave_group_sync(unsigned* ctr, unsigned target) 
   while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
 }
 
+// conv_bwd4 phase 4, one item: the dW_conv1 / db_conv1 partials of channel c, dz1 row y, tap row kh
+// (sliding window over the row's 24 positions); red[y][c * 25 + kh * 5 + kw], red[y][125 + c]
+__device__ __forceinline__ void bwd4_dw1_item(int it, const float* dz1_s, const float* x_s, float* red) {
+  const int c = it / 120, rem = it - c * 120;
+  const int y = rem / 5, kh = rem - y * 5;
+  const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
+  const float* xr = x_s + (y + kh) * F_XR;
+  float xw[28];
+#pragma unroll
+  for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float bs = 0.f;
+#pragma unroll
+  for (int x = 0; x < 24; ++x) {
+    const float a = zr[x];
+    bs += a;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
+  }
+  float* pr = red + y * F_RED1;
+#pragma unroll
+  for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
+  if (kh == 0) pr[125 + c] = bs;
+}
+
 // 2a for wave w of 8: dcolT tiles jt0 .. jt0 + 3 (jt0 = 4 (w >> 2)) x position tile w & 3.
 // Software-pipelined like 2b below: the LDS operand reads of k-chunk c + 1 are issued before
 // the MFMAs of chunk c (sched_barrier groups keep the compiler from sinking each read to its
@@ -2034,6 +2059,8 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       pv_s[item] = accv;
     }
     wave_group_sync(&s_grp[1], 8u);
+    stamp(dbg, 7, 512);  // diagnostics: 2b done (group B), read by tools/step_timeline.py (round 5:
+                         // 4.66 us after the stage, when group A has just finished col2im)
     float* rowq = slab + (size_t)q * stride + o_gw2 + cig * 125;
     if (w8 < 4 || khb == 0) {
       if (w8 >= 4) gacc += pk_s[tpb * 64 + lane];
@@ -2095,28 +2122,10 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   stamp(dbg, 3);
   {
     constexpr int NPART = 24;
-    for (int it = tid; it < 600; it += 512) {  // phase 4 (as below)
-      const int c = it / 120, rem = it - c * 120;
-      const int y = rem / 5, kh = rem - y * 5;
-      const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
-      const float* xr = x_s + (y + kh) * F_XR;
-      float xw[28];
-#pragma unroll
-      for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
-      float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-      float bs = 0.f;
-#pragma unroll
-      for (int x = 0; x < 24; ++x) {
-        const float a = zr[x];
-        bs += a;
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
-      }
-      float* pr = red + y * F_RED1;
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
-      if (kh == 0) pr[125 + c] = bs;
-    }
+    // phase 4: 600 items over group A's 512 threads (round 5: handing items 512..599 to group B's
+    // waves 8, 9, idle after 2b, measured no faster -- profiles/r5_dw1/ab.txt)
+    bwd4_dw1_item(tid, dz1_s, x_s, red);
+    if (tid < 88) bwd4_dw1_item(tid + 512, dz1_s, x_s, red);
     wave_group_sync(&s_grp[0], 24u);
     stamp(dbg, 4);
     float* rowb = slab + (size_t)b * stride;

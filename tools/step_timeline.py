@@ -68,7 +68,12 @@ def analyse(dbg: torch.Tensor, nslots: int):
         dc = (c[:, 1:] - c[:, :-1]) * cv
         dw = (w[:, 1:] - w[:, :-1]) * cv
         ghz = (dc.sum(0) / dw.sum(0).clamp_min(1) / 10.0).tolist()  # ticks per 10 ns -> GHz
-        out.append({"blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
+        # stamp 7 written by another wave than stamps 0-5 (conv_bwd4: group B's 2b done): us after stamp 1
+        aux = None
+        if nph < 6 and bool((w[:, 7] > 0).any()):
+            ok = (w[:, 7] > 0) & (w[:, 1] > 0)
+            aux = float(((w[:, 7] - w[:, 1]) * ok).sum() / ok.sum().clamp_min(1) / 100.0)
+        out.append({"aux71": aux, "blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
                     "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist())),
                     "phases": phases[:nph], "ghz": ghz[:nph]})
     return out
@@ -152,6 +157,11 @@ def main(argv=None):
     print(f"one step: sum of spans {res['sum_span_us']} us + sum of gaps {res['sum_gap_us']} us")
     print("mean block phase times (us, stamp k -> k+1): " +
           "; ".join(f"{r['kernel']} {r['phase_means_us']}" for r in rows[per:]))
+    aux = [(r["kernel"], round(sum(s_[k]["aux71"] for s_ in samples) / len(samples), 2))
+           for r, k in zip(rows[per:], range(per, nk)) if samples[0][k]["aux71"] is not None]
+    if aux:
+        print("second-group stamp 7 (us after stamp 1; conv_bwd4: 2b done): " +
+              "; ".join(f"{n} {v}" for n, v in aux))
     print("effective shader clock per phase (GHz, clock64 / wall_clock64): " +
           "; ".join(f"{r['kernel']} {r['phase_ghz']}" for r in rows[per:]))
     if args.json:
