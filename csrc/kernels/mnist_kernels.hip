@@ -1814,26 +1814,35 @@ __device__ __forceinline__ void wave_group_sync(unsigned* ctr, unsigned target) 
   while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
 }
 
-// conv_bwd4 phase 4, one item: the dW_conv1 / db_conv1 partials of channel c, dz1 row y, tap row kh
-// (sliding window over the row's 24 positions); red[y][c * 25 + kh * 5 + kw], red[y][125 + c]
-__device__ __forceinline__ void bwd4_dw1_item(int it, const float* dz1_s, const float* x_s, float* red) {
-  const int c = it / 120, rem = it - c * 120;
-  const int y = rem / 5, kh = rem - y * 5;
-  const float* zr = dz1_s + c * F_Z1 + y * F_Z1R;
-  const float* xr = x_s + (y + kh) * F_XR;
-  float xw[28];
+// conv_bwd4 phase 4 on the pooled dz1 (round 5), one item: channel c, pooled row py, tap row kh.
+// dz1 is non-zero only at each pooling window's argmax (dy, dx) = idx1 (row-major 2 x 2), so
+//   dW_conv1[c][kh][kw] += d[c][py][px] * x[2 py + dy + kh][2 px + dx + kw],  db_conv1[c] += d
+// -- half the FMAs of the dense sliding window and one item per thread; partial rows red[py].
+__device__ __forceinline__ void bwd4_dw1_item_pooled(int it, const float* dp1_s, const uint8_t* idx_s,
+                                                     const float* x_s, float* red) {
+  const int c = it / 60, rem = it - c * 60;
+  const int py = rem / 5, kh = rem - py * 5;
+  const float* dr = dp1_s + c * 144 + py * 12;
+  const uint8_t* ir = idx_s + c * 144 + py * 12;
+  float dv[12];
+  int iv[12];
 #pragma unroll
-  for (int qq = 0; qq < 28; ++qq) xw[qq] = xr[qq];
+  for (int k = 0; k < 12; ++k) {
+    dv[k] = dr[k];
+    iv[k] = ir[k];
+  }
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   float bs = 0.f;
 #pragma unroll
-  for (int x = 0; x < 24; ++x) {
-    const float a = zr[x];
+  for (int px = 0; px < 12; ++px) {
+    const int p = iv[px];
+    const float* xr = x_s + (2 * py + (p >> 1) + kh) * F_XR + 2 * px + (p & 1);
+    const float a = dv[px];
     bs += a;
 #pragma unroll
-    for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xw[x + kw], acc[kw]);
+    for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(a, xr[kw], acc[kw]);
   }
-  float* pr = red + y * F_RED1;
+  float* pr = red + py * F_RED1;
 #pragma unroll
   for (int kw = 0; kw < 5; ++kw) pr[c * 25 + kh * 5 + kw] = acc[kw];
   if (kh == 0) pr[125 + c] = bs;
@@ -1919,7 +1928,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   uint8_t* idx_s = reinterpret_cast<uint8_t*>(lds + G_OFF_IDX);
   f32x4* pk_s = reinterpret_cast<f32x4*>(lds + G_OFF_PK);
   float* pv_s = lds + G_OFF_PV;
-  float* dz1_s = lds + G_OFF_DZ1;
+  float* dp1_s = lds + G_OFF_DZ1;  // pooled d(a1) [5][144]
   float* red = lds + G_OFF_RED;
 
   const int cig = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -2110,22 +2119,16 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       }
       da += ((y - kh >= 0) & (y - kh <= 7)) ? dr : 0.f;
     }
-    const float d = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
-    const int pidx = idx_s[it];
-    float* z = dz1_s + c * F_Z1 + (2 * y) * F_Z1R + 2 * x;
-    z[0] = pidx == 0 ? d : 0.f;
-    z[1] = pidx == 1 ? d : 0.f;
-    z[F_Z1R] = pidx == 2 ? d : 0.f;
-    z[F_Z1R + 1] = pidx == 3 ? d : 0.f;
+    // the pooled d(a1), ReLU-masked: dz1 stays pooled (its un-pooled image is 3/4 zeros; phase 4
+    // places each value through idx1)
+    dp1_s[it] = a1_s[c * F_A1C + y * F_A1R + x] > 0.f ? da : 0.f;
   }
   wave_group_sync(&s_grp[0], 16u);
   stamp(dbg, 3);
   {
-    constexpr int NPART = 24;
-    // phase 4: 600 items over group A's 512 threads (round 5: handing items 512..599 to group B's
-    // waves 8, 9, idle after 2b, measured no faster -- profiles/r5_dw1/ab.txt)
-    bwd4_dw1_item(tid, dz1_s, x_s, red);
-    if (tid < 88) bwd4_dw1_item(tid + 512, dz1_s, x_s, red);
+    constexpr int NPART = 12;
+    // phase 4 on the pooled dz1: 300 items (c, pooled row py, tap row kh), one per thread
+    if (tid < 300) bwd4_dw1_item_pooled(tid, dp1_s, idx_s, x_s, red);
     wave_group_sync(&s_grp[0], 24u);
     stamp(dbg, 4);
     float* rowb = slab + (size_t)b * stride;
