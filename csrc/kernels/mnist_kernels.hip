@@ -262,7 +262,7 @@ __device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb)
 
 constexpr int AB_NT = 1024;  // conv forward blocks: 16 waves, 4 per SIMD keep the matrix pipe fed
 // conv12's LDS image row stride: with 44 (== 12 mod 32) the conv1 MFMA operand reads (lane
-// rows {r, r+1} x 8 columns, lane groups one tap apart) and the VALU windows touch 32
+// rows {r, r+1} x 8 columns, lane groups one tap apart) touch 32
 // distinct banks per half-wave; the dense 28 gave 2-way conflicts (bank model: profiles/
 // r2_lds_banks.md)
 constexpr int AB_IRS = 44;
@@ -358,7 +358,8 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
 //   channel groups, B samples), 16 waves.  Every block recomputes conv1 + ReLU +
 //   pool for its sample on MFMA straight into the conv2 im2col image in LDS
 //   (4x redundant, ~1 us, cheaper than a launch boundary + an HBM round trip);
-//   the cg == 0 block publishes a1/idx1 (for the backward), xn and lab.
+//   block cg publishes a1/idx1 channels [5 cg, 5 cg + 5) (for the backward), cg == 0 also xn
+//   and lab.
 //   conv2 then runs exactly as conv2_fwd_pool_kernel.
 // ---------------------------------------------------------------------------
 // conv1 channels 0-15 on MFMA: position tiles t0, t0 + 16, .. (NU of them) as NU independent
@@ -369,11 +370,11 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
 // rows x columns tile needed four v_permlane32_swap pairings per tile and ~2x the epilogue VALU
 // work, which the conv1 phase is issue-bound on).  Same taps in the same MFMA K order per output:
 // bit-identical.  Channels 16-19 would fill only a quarter of a second 16-wide channel tile:
-// conv1_valu_window does them.
+// conv1_tiles2_group does them as 4x4x1 MFMA chains.
 template <int NU, int TS = 16>
 __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int (&toff)[7],
-                                            const float (&bw)[7], float bc, float* in_s,
-                                            bool pub, float* a1, uint8_t* idx1, int b, int i, int g) {
+                                            const float (&bw)[7], float bc, float* in_s, uint8_t* id1_s,
+                                            int i, int g) {
   f32x4 acc[NU];
   const float* ibs[NU];
   const int wi = i >> 2, e = i & 3;  // A row i: window wi, element e
@@ -410,26 +411,21 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
     in_s[i * C2_CS + py * C2_RS + px] = v;
-    if (pub) {
-      const size_t o = (size_t)b * 2880 + i * 144 + py * 12 + px;
-      a1[o] = v;
-      idx1[o] = (uint8_t)am;
-    }
+    id1_s[i * 144 + py * 12 + px] = (uint8_t)am;
   }
 }
 
 // Waves 7-15: two channel 0-15 tiles (as conv1_tasks<2>) and one channel 16-19 group -- 16 pooled
 // positions p = 16 G + lane / 4 on v_mfma_f32_4x4x1_16b_f32: block lane / 4 is one pooled position,
 // its 4 rows the 2x2 window (row 2 di + dj), its 4 columns the channels; the 25 taps are 25 K = 1
-// steps in tap order from zero, the fmaf chain of conv1_valu_window / conv1_fwd_pool_kernel
+// steps in tap order from zero, the fmaf chain of conv1_fwd_pool_kernel
 // (bit-identical).  The group's dependent chain is interleaved with the tiles' MFMAs (3-4 after
 // every tile k-step) so each chain's latency hides behind the others, on the matrix pipe instead
 // of ~140 VALU instructions per lane.  D of the group: lane 4 b + j, register i = window element
 // i of channel 16 + j.
 __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* img, const float* w1s,
                                                    const int (&toff)[7], const float (&bw)[7], float bc,
-                                                   float* in_s, bool pub, float* a1, uint8_t* idx1, int b,
-                                                   int lane) {
+                                                   float* in_s, uint8_t* id1_s, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int wi = i >> 2, e = i & 3;
   const float* ibs[2];
@@ -477,11 +473,7 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
     in_s[i * C2_CS + py * C2_RS + px] = v;
-    if (pub) {
-      const size_t o = (size_t)b * 2880 + i * 144 + py * 12 + px;
-      a1[o] = v;
-      idx1[o] = (uint8_t)am;
-    }
+    id1_s[i * 144 + py * 12 + px] = (uint8_t)am;
   }
   {  // the group's epilogue
     const float o00 = acc4[0] + bc4, o01 = acc4[1] + bc4, o10 = acc4[2] + bc4, o11 = acc4[3] + bc4;
@@ -492,54 +484,7 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
     in_s[(16 + q) * C2_CS + ph4 * C2_RS + pw4] = v;
-    if (pub) {
-      const size_t o = (size_t)b * 2880 + (16 + q) * 144 + p4;
-      a1[o] = v;
-      idx1[o] = (uint8_t)am;
-    }
-  }
-}
-
-// conv1 channels 16-19 on the VALU (f32 FMA runs at the f32 MFMA rate): one pooled output
-// per thread, item = pooled position * 4 + (c - 16): the four channels of a position share
-// the image reads (broadcast), so a 32-lane half reads 8 windows at stride 2 -- with the
-// AB_IRS row stride every read is conflict-free.  Same tap order as the MFMA chain and the
-// standalone conv1 kernel (bit-identical results).
-__device__ __forceinline__ void conv1_valu_window(int item, const float* img, const float* w1s,
-                                                  float* in_s, bool pub, float* a1, uint8_t* idx1,
-                                                  int b) {
-  const int c = 16 + (item & 3), p = item >> 2;
-  const int ph = p / 12, pw = p - ph * 12;
-  const float* im = img + (2 * ph) * AB_IRS + 2 * pw;
-  const float* wc = w1s + c * 25;
-  float patch[6][6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) patch[r][q] = im[r * AB_IRS + q];
-  float o00 = 0.f, o01 = 0.f, o10 = 0.f, o11 = 0.f;
-#pragma unroll
-  for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      const float wv = wc[kh * 5 + kw];
-      o00 = fmaf(patch[kh][kw], wv, o00);
-      o01 = fmaf(patch[kh][kw + 1], wv, o01);
-      o10 = fmaf(patch[kh + 1][kw], wv, o10);
-      o11 = fmaf(patch[kh + 1][kw + 1], wv, o11);
-    }
-  const float bc = w1s[500 + c];
-  o00 += bc; o01 += bc; o10 += bc; o11 += bc;
-  float m = o00; int am = 0;
-  if (o01 > m) { m = o01; am = 1; }
-  if (o10 > m) { m = o10; am = 2; }
-  if (o11 > m) { m = o11; am = 3; }
-  const float v = fmaxf(m, 0.f);
-  in_s[c * C2_CS + ph * C2_RS + pw] = v;
-  if (pub) {
-    const size_t o = (size_t)b * 2880 + c * 144 + p;
-    a1[o] = v;
-    idx1[o] = (uint8_t)am;
+    id1_s[(16 + q) * 144 + p4] = (uint8_t)am;
   }
 }
 
@@ -570,9 +515,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   __shared__ __align__(16) float in_s[20 * C2_CS];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
+  __shared__ __align__(16) uint8_t id1_s[20 * 144];  // conv1 pool argmax (published per channel group)
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   stamp(dbg, 0);
-  const bool pub = cg == 0;
+  const bool pub = cg == 0;  // xn and lab
   // conv2 epilogue bias, loaded with the staging loads (no round trip after the last barrier)
   const int co_pre = cg * 16 + (tid & 15);
   const float bco = co_pre < 50 ? bias[co_pre] : 0.f;
@@ -621,8 +567,8 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   // position tiles (4 pooling windows each, see conv1_tasks) x 7 K-steps (25 taps,
   // zero-padded to 28 through the weight fragments); wave w takes tiles w, w+16 (+ w+32
   // for w < 4): 9 tiles per SIMD.  The pool is a max over each lane's four accumulator
-  // registers.  Channels 16-19: 576 pooled outputs on the VALU of waves 7-15.
-  // (Measured: giving the MFMA tiles and the VALU windows to disjoint waves was no faster.)
+  // registers.  Channels 16-19: 4x4x1 MFMA chains interleaved with the tiles on waves 7-15
+  // (conv1_tiles2_group; the round-4 VALU windows: profiles/r5_c1g/ab.txt).
   {
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
@@ -638,26 +584,26 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     }
     const float bc = w1s[500 + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
-#ifdef PTO_CONV1_VALUWIN  // A/B: channels 16-19 as 576 VALU windows after the tiles (round 4)
-    conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
-#else
-    if (wv >= 7) conv1_tiles2_group(wv, wv - 7, img, w1s, toff, bw, bc, in_s, pub, a1, idx1, b, lane);
-    else conv1_tasks<2>(wv, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
-#endif
-    if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, pub, a1, idx1, b, i, g);
+    if (wv >= 7) conv1_tiles2_group(wv, wv - 7, img, w1s, toff, bw, bc, in_s, id1_s, lane);
+    else conv1_tasks<2>(wv, img, toff, bw, bc, in_s, id1_s, i, g);
+    if (wv < 4) conv1_tasks<1>(wv + 32, img, toff, bw, bc, in_s, id1_s, i, g);
     stamp_by(dbg, 4, 0);             // wave 0: 3 MFMA tiles done
-    stamp_by(dbg, 5, AB_NT - 64);    // last wave: 2 MFMA tiles done, VALU windows next
-    stamp_by(dbg, 7, 4 * 64);        // wave 4: 2 MFMA tiles, no VALU windows
-    // (round 5: the same windows as 25-step v_mfma_f32_4x4x1_16b_f32 chains on waves 7-15 --
-    // bit-identical -- measured no faster, before and after the register pool: profiles/r5_c1,
-    // r5_mfma4)
-#ifdef PTO_CONV1_VALUWIN
-    if (tid >= AB_NT - 576) conv1_valu_window(tid - (AB_NT - 576), img, w1s, in_s, pub, a1, idx1, b);
-#endif
-    stamp_by(dbg, 6, AB_NT - 64);    // last wave: VALU windows done
+    stamp_by(dbg, 5, AB_NT - 64);    // last wave: 2 MFMA tiles + the 4x4x1 group done
+    stamp_by(dbg, 7, 4 * 64);        // wave 4: 2 MFMA tiles
   }
   __syncthreads();
   stamp(dbg, 2);
+  // a1 / idx1 for the backward: block cg publishes channels [5 cg, 5 cg + 5) -- conv_bwd4's
+  // block (cg, b) reads exactly that slice, on the same XCD; coalesced stores from the LDS images
+  // instead of scattered 4- and 1-byte stores in the conv1 epilogues of one block per sample
+  if (tid < 720) {
+    const int c = 5 * cg + tid / 144, p = tid - (tid / 144) * 144, py = p / 12;
+    a1[(size_t)b * 2880 + c * 144 + p] = in_s[c * C2_CS + py * C2_RS + (p - py * 12)];
+  } else if (tid < 900) {
+    const int e = tid - 720;
+    reinterpret_cast<uint32_t*>(idx1 + (size_t)b * 2880 + 720 * cg)[e] =
+        reinterpret_cast<const uint32_t*>(id1_s + 720 * cg)[e];
+  }
 
   const int lane = tid & 63, wv = tid >> 6;
   const int pt = wv & 3, i = lane & 15, g = lane >> 4;
@@ -1803,7 +1749,7 @@ constexpr int G_LDS = G_OFF_PV + 4 * 64;
 constexpr int G_OFF_DZ1 = G_OFF_W;            // aliases of the W2 slice (dead after phase 2a)
 constexpr int G_OFF_RED = G_OFF_W + 5 * F_Z1;
 static_assert(G_LDS * 4 <= 160 * 1024, "conv_bwd4 LDS budget");
-static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
+static_assert(G_OFF_PK % 4 == 0 && G_OFF_DZ1 % 4 == 0 && G_OFF_DZ % 2 == 0 && G_DZN % 2 == 0 && G_DZS % 2 == 0, "LDS alignment");
 
 
 
@@ -2604,7 +2550,7 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
   if (B > 65535) return -1;  // grid y
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
-  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 1)) return -2;
+  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 3)) return -2;  // idx1: 4-byte stores
   // staged batches exist only for uint8 sources walked by a device cursor
   if (stg_x != nullptr && (stg_lab == nullptr || stg_tag == nullptr || cursor == nullptr || perm == nullptr ||
                            !is_u8 || labels == nullptr))
