@@ -345,11 +345,9 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
   if (g < 2 && co < 50) {  // top row of the window; partner lane holds the bottom row
     if (pA > mA) { mA = pA; aA = 2 + paA; }
     if (pB > mB) { mB = pB; aB = 2 + paB; }
-    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);
-    a2[o] = fmaxf(mA, 0.f);
-    a2[o + 1] = fmaxf(mB, 0.f);
-    idx2[o] = (uint8_t)aA;
-    idx2[o + 1] = (uint8_t)aB;
+    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);  // even: one 8-B / 2-B store each
+    *reinterpret_cast<float2*>(a2 + o) = make_float2(fmaxf(mA, 0.f), fmaxf(mB, 0.f));
+    *reinterpret_cast<uint16_t*>(idx2 + o) = (uint16_t)(aA | (aB << 8));
   }
 }
 
@@ -623,11 +621,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   if (g < 2 && co < 50) {
     if (pA > mA) { mA = pA; aA = 2 + paA; }
     if (pB > mB) { mB = pB; aB = 2 + paB; }
-    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);
-    a2[o] = fmaxf(mA, 0.f);
-    a2[o + 1] = fmaxf(mB, 0.f);
-    idx2[o] = (uint8_t)aA;
-    idx2[o + 1] = (uint8_t)aB;
+    const size_t o = (size_t)b * 800 + co * 16 + pt * 4 + 2 * (g & 1);  // even: one 8-B / 2-B store each
+    *reinterpret_cast<float2*>(a2 + o) = make_float2(fmaxf(mA, 0.f), fmaxf(mB, 0.f));
+    *reinterpret_cast<uint16_t*>(idx2 + o) = (uint16_t)(aA | (aB << 8));
   }
 }
 
@@ -1331,7 +1327,8 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
         dhs[(4 * g + r) * H_DS + 64 * wv + 16 * t + i] = dv[t][r];
       }
     }
-    if (pub) {  // block-uniform
+    if (pub) {  // block-uniform (round 5: spreading h / dh over the 50 kt blocks was no faster,
+                // profiles/r5_hpub/ab.txt)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -2535,6 +2532,7 @@ int pto_mnist_conv1_fwd(const void* x, int is_u8, const int* labels, const int* 
 int pto_mnist_conv2_fwd(const float* a1, const float* w, const float* bias, float* a2,
                         uint8_t* idx2, int B, void* stream) {
   PTO_CHECK_B(B);
+  if ((((uintptr_t)a2) & 7) || (((uintptr_t)idx2) & 1)) return -2;  // 8-byte / 2-byte pair stores
   hipLaunchKernelGGL(conv2_fwd_pool_kernel, dim3(4, B), dim3(AB_NT), 0, (hipStream_t)stream,
                      a1, w, bias, a2, idx2, B, dbg_next());
   return (int)hipGetLastError();
@@ -2550,7 +2548,9 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
   if (B > 65535) return -1;  // grid y
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
-  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 3)) return -2;  // idx1: 4-byte stores
+  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 3) || (((uintptr_t)a2) & 7) ||
+      (((uintptr_t)idx2) & 1))
+    return -2;  // idx1: 4-byte, a2: 8-byte, idx2: 2-byte stores
   // staged batches exist only for uint8 sources walked by a device cursor
   if (stg_x != nullptr && (stg_lab == nullptr || stg_tag == nullptr || cursor == nullptr || perm == nullptr ||
                            !is_u8 || labels == nullptr))
