@@ -244,6 +244,21 @@ def library_path() -> Path:
     return Path(os.environ["PTO_HIP_LIB"]) if os.environ.get("PTO_HIP_LIB") else _LIB_PATH
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def current_stream_ptr(device=None) -> int:
+    """The current HIP stream of ``device`` (default: the current device) as an integer handle.
+    Uses torch's raw-pointer accessor (no ``torch.cuda.Stream`` object per call: a few us less
+    host time before every launch -- the first launch of a timed region included)."""
+    if _raw_stream is not None:
+        idx = torch.cuda.current_device() if device is None else (
+            device.index if isinstance(device, torch.device) and device.index is not None else
+            (torch.cuda.current_device() if isinstance(device, torch.device) else int(device)))
+        return int(_raw_stream(idx))
+    return torch.cuda.current_stream(device).cuda_stream
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         raise NativeLibraryError(f"{what} failed with code {rc}")

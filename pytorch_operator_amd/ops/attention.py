@@ -26,7 +26,7 @@ SEQ_MULTIPLE = 128
 
 
 def _stream(t: torch.Tensor):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return ctypes.c_void_p(_native.current_stream_ptr(t.device))
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:

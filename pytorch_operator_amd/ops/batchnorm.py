@@ -40,7 +40,7 @@ MASK_BITS = True  # residual+ReLU backward masks from the forward's bit image (F
 
 
 def _stream(t: torch.Tensor):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return ctypes.c_void_p(_native.current_stream_ptr(t.device))
 
 
 def supported(x: torch.Tensor) -> bool:

@@ -20,7 +20,7 @@ _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
 def _stream(t: torch.Tensor):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return ctypes.c_void_p(_native.current_stream_ptr(t.device))
 
 
 def _aligned(t: torch.Tensor) -> torch.Tensor:

@@ -27,7 +27,7 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream_ptr()
 
 
 def _req(t: torch.Tensor, shape, dtype, name: str) -> None:

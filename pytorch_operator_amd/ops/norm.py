@@ -23,7 +23,7 @@ _ROWS_PER_BLOCK = 8  # tools/llm_kernel_bench.py sweep at 8192x4096: 4/8/16/32 -
 
 
 def _stream(t: torch.Tensor):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    return ctypes.c_void_p(_native.current_stream_ptr(t.device))
 
 
 def rms_norm_reference(x: torch.Tensor, w: torch.Tensor, eps: float, out_dtype=None) -> torch.Tensor:

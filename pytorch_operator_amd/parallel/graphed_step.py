@@ -82,13 +82,13 @@ class NativeGraph:
 
     def replay(self, n: int = 1) -> None:
         _native.check(self._lib.pto_graph_launch(
-            self._h, torch.cuda.current_stream(self.device).cuda_stream, int(n)), "hipGraphLaunch")
+            self._h, _native.current_stream_ptr(self.device), int(n)), "hipGraphLaunch")
 
     def replay_stream(self, n: int = 1) -> None:
         """The captured kernels launched directly on the current stream, ``n`` times over
         (same kernels and arguments as ``replay``; no per-replay graph-launch cost)."""
         _native.check(self._lib.pto_graph_launch_stream(
-            self._h, torch.cuda.current_stream(self.device).cuda_stream, int(n)), "graph stream replay")
+            self._h, _native.current_stream_ptr(self.device), int(n)), "graph stream replay")
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
