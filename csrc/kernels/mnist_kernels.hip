@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   __shared__ float w2s[16 * H_RS];
   __shared__ __align__(16) float dhs[16 * H_DS];
   __shared__ f32x4 red[E_NW][64];
-  __shared__ float dls[16][16];
+  __shared__ float dls[16][17];  // +1: the dh operand reads (8 sample rows per half-wave) hit 8 banks
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, g = lane >> 4;
@@ -1301,14 +1301,18 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   }
   __syncthreads();
   stamp(dbg, 2);
-  // ---- dh for this wave's 64 k (= its dz2 K range): four 16-column tiles, K = 16 (j)
+  // ---- dh for this wave's 64 k (= its dz2 K range): four 16-column tiles, K = the 10 classes
+  // exactly, as 10 K = 1 steps of v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4: block lane / 4 =
+  // samples 4 (lane / 16) .. + 3 x columns 16 t + 4 ((lane / 4) % 4) .. + 3) -- the same D layout
+  // as a 16x16x4 tile (lane (g, i): samples 4 g + r, column 16 t + i) without its 6 zero classes,
+  // 80 instead of 128 matrix-pipe cycles per tile; the same k-ordered fmaf chain
   {
-    float da[4], db[4][4], hm[4][4];
+    float da[10], db[4][10], hm[4][4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      da[st] = dls[i][4 * st + g];
+    for (int c = 0; c < 10; ++c) {
+      da[c] = dls[4 * g + (lane & 3)][c];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) db[t][st] = w2s[(4 * st + g) * H_RS + 64 * wv + 16 * t + i];
+      for (int t = 0; t < 4; ++t) db[t][c] = w2s[c * H_RS + 64 * wv + 16 * t + i];
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -1320,7 +1324,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
     for (int t = 0; t < 4; ++t) {
       f32x4 c = zero4();
 #pragma unroll
-      for (int st = 0; st < 4; ++st) c = mfma16x16x4(da[st], db[t][st], c);
+      for (int k = 0; k < 10; ++k) c = __builtin_amdgcn_mfma_f32_4x4x1f32(da[k], db[t][k], c, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dv[t][r] = hm[t][r] > 0.f ? c[r] : 0.f;

@@ -42,6 +42,29 @@ def test_xgmi_allreduce_ranks(tmp_path, world, nblk):
         assert res["nblk"] == nblk or (nblk == 0 and res["nblk"] in (128, 256)), res
 
 
+def test_xgmi_exchange_stamps_record_every_launch(tmp_path):
+    """The exchange's per-workgroup stamp ring (XgmiAllReduce.enable_stamps, the diagnostics behind
+    profiles/r5_xgmi_handover.md): a passing 2-rank rehearsal records its launches on both ranks, in
+    phase order, and tools/xgmi_stamps.py finds no timed-out wait."""
+    import importlib.util
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
+           "--backend", "gloo", "--out", str(tmp_path), "--stamps"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=dict(os.environ, PYTHONPATH=str(ROOT)))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    spec = importlib.util.spec_from_file_location("xgmi_stamps", ROOT / "tools" / "xgmi_stamps.py")
+    xs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(xs)
+    ranks = xs.load(str(tmp_path / "stamps_main"))
+    assert sorted(ranks) == [0, 1]
+    for rec in ranks.values():
+        assert rec["error"] == 0 and len(rec["rows"]) >= rec["nblk"]
+        for blk, step, t0, f1, f2, t1, err, missing in rec["rows"]:
+            assert 0 < t0 <= f1 <= f2 <= t1 and err == 0 and missing == 0
+    assert xs.analyse(ranks)["failures"] == []
+
+
 def test_xgmi_stall_makes_every_rank_exit_retryable(tmp_path):
     """A rank that stalls past the exchange's bounded wait must not leave the job running
     rank-local: every rank's worker notices the kernel's error word at its next
