@@ -591,23 +591,26 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
   }
   __syncthreads();
   stamp(dbg, 2);
-  // a1 / idx1 for the backward: block cg publishes channels [5 cg, 5 cg + 5) -- conv_bwd4's
-  // block (cg, b) reads exactly that slice, on the same XCD; coalesced stores from the LDS images
-  // instead of scattered 4- and 1-byte stores in the conv1 epilogues of one block per sample
-  if (tid < 720) {
-    const int c = 5 * cg + tid / 144, p = tid - (tid / 144) * 144, py = p / 12;
-    a1[(size_t)b * 2880 + c * 144 + p] = in_s[c * C2_CS + py * C2_RS + (p - py * 12)];
-  } else if (tid < 900) {
-    const int e = tid - 720;
-    reinterpret_cast<uint32_t*>(idx1 + (size_t)b * 2880 + 720 * cg)[e] =
-        reinterpret_cast<const uint32_t*>(id1_s + 720 * cg)[e];
-  }
-
   const int lane = tid & 63, wv = tid >> 6;
   const int pt = wv & 3, i = lane & 15, g = lane >> 4;
   f32x4 acc = conv2_block(in_s, w_s, red, wv, lane);
   stamp(dbg, 3);
-  if (wv >= 4) return;
+  if (wv >= 4) {
+    // a1 / idx1 for the backward, by the waves the conv2 epilogue does not need: block cg publishes
+    // channels [5 cg, 5 cg + 5) (conv_bwd4's block (cg, b) reads exactly that slice) with 16-byte
+    // stores from the LDS images -- instead of scattered 4- and 1-byte stores in the conv1
+    // epilogues of one block per sample (round 5)
+    const int e = tid - 256;
+    if (e < 180) {  // 5 channels x 12 rows x 3 float4
+      const int c = 5 * cg + e / 36, rem = e - (e / 36) * 36, py = rem / 3, k = rem - py * 3;
+      *reinterpret_cast<float4*>(a1 + (size_t)b * 2880 + c * 144 + py * 12 + 4 * k) =
+          *reinterpret_cast<const float4*>(in_s + c * C2_CS + py * C2_RS + 4 * k);
+    } else if (e < 225) {
+      reinterpret_cast<uint4*>(idx1 + (size_t)b * 2880 + 720 * cg)[e - 180] =
+          reinterpret_cast<const uint4*>(id1_s + 720 * cg)[e - 180];
+    }
+    return;
+  }
   const int co = cg * 16 + i;
   const float v0 = acc[0] + bco, v1 = acc[1] + bco, v2 = acc[2] + bco, v3 = acc[3] + bco;
   float mA = v0; int aA = 0;
@@ -2552,9 +2555,9 @@ int pto_mnist_conv12_fwd(const void* x, int is_u8, const int* labels, const int*
   if (B > 65535) return -1;  // grid y
   if (perm != nullptr && n_total <= 0) return -1;
   if (lab_out != nullptr && labels == nullptr) return -1;
-  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 7) || (((uintptr_t)idx1) & 3) || (((uintptr_t)a2) & 7) ||
+  if ((((uintptr_t)w2) & 15) || (((uintptr_t)a1) & 15) || (((uintptr_t)idx1) & 15) || (((uintptr_t)a2) & 7) ||
       (((uintptr_t)idx2) & 1))
-    return -2;  // idx1: 4-byte, a2: 8-byte, idx2: 2-byte stores
+    return -2;  // a1 / idx1: 16-byte, a2: 8-byte, idx2: 2-byte stores
   // staged batches exist only for uint8 sources walked by a device cursor
   if (stg_x != nullptr && (stg_lab == nullptr || stg_tag == nullptr || cursor == nullptr || perm == nullptr ||
                            !is_u8 || labels == nullptr))
