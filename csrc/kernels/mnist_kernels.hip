@@ -1334,16 +1334,6 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
         dhs[(4 * g + r) * H_DS + 64 * wv + 16 * t + i] = dv[t][r];
       }
     }
-    if (pub) {  // block-uniform (round 5: spreading h / dh over the 50 kt blocks was no faster,
-                // profiles/r5_hpub/ab.txt)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 64 * wv + 16 * t + i, smp = mt * 16 + 4 * g + r;
-          if (k < 500 && smp < B) a.dh_out[(size_t)smp * 500 + k] = dv[t][r];
-        }
-    }
   }
   // ---- dz2 job (fc1_bwd's job 2): K = 500 split over the waves; this wave reads only the dh it wrote
   {
@@ -1378,6 +1368,15 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
       z[1] = pidx == 1 ? d : 0.f;
       z[8] = pidx == 2 ? d : 0.f;
       z[9] = pidx == 3 ? d : 0.f;
+    }
+  }
+  if (pub) {  // block-uniform: dh for the tail, copied from LDS with 16-byte stores after the block's
+              // own output (spreading h / dh over the 50 kt blocks was no faster, profiles/r5_hpub)
+    for (int e = tid; e < 16 * 125; e += E_NT) {
+      const int row = e / 125, c4 = e - row * 125;
+      if (mt * 16 + row < B)
+        reinterpret_cast<float4*>(a.dh_out + (size_t)(mt * 16 + row) * 500)[c4] =
+            *reinterpret_cast<const float4*>(dhs + row * H_DS + 4 * c4);
     }
   }
   stamp(dbg, 3);
@@ -2841,7 +2840,7 @@ int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, 
       a2 == nullptr || idx2 == nullptr || w1 == nullptr || (dz2 == nullptr && dpool == nullptr) ||
       h_out == nullptr || dh_out == nullptr || dlog_out == nullptr || per_sample == nullptr)
     return -1;
-  if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out)) & 15)
+  if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out) | ((uintptr_t)dh_out)) & 15)
     return -2;  // float4 rows
   Fc1BwdHead a{};
   a.hp0 = hp0; a.hp1 = hp1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.lab = lab; a.a2 = a2; a.idx2 = idx2; a.w1 = w1;
