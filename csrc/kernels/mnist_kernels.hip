@@ -4,31 +4,30 @@
 //   conv1(1->20,k5) -> ReLU -> maxpool2 -> conv2(20->50,k5) -> ReLU -> maxpool2
 //   -> fc1(800->500) -> ReLU -> fc2(500->10) -> log_softmax -> nll_loss(mean)
 //
-// The training step is 6 launches (world_size > 1: the tail launch is the xGMI
-// exchange of xgmi_allreduce.hip, or RCCL buckets).  At B=64 the step is ~0.84
-// GFLOP: it is latency-bound, so every kernel is shaped to (a) issue all of its
-// global loads up front (no load -> use -> load chains, no predicated loads, at most
-// the 63 loads vmcnt can track), (b) keep its MFMA chains short by splitting K
-// across the waves of a workgroup, and (c) keep the launch count low so a hipGraph
-// replays the step back to back (docs/kernels.md has the measured design log):
+// The single-GPU training step is 5 launches (round 5; world_size > 1: 6, the head and fc1_bwd
+// separate and the tail launch the xGMI exchange of xgmi_allreduce.hip, or RCCL buckets).  At B=64
+// the step is ~0.84 GFLOP: it is latency-bound, so every kernel is shaped to (a) issue all of its
+// global loads up front (no load -> use -> load chains, no predicated loads, at most the 63 loads
+// vmcnt can track), (b) keep its MFMA chains short by splitting K across the waves of a workgroup,
+// (c) keep the launch count low, and (d) keep bulk stores off the critical waves and out of the
+// kernel's last moments (docs/kernels.md has the measured design log):
 //
-//   AB conv12_fwd      uint8 gather + Normalize; conv1 channels 0-15 on MFMA, 16-19 on
-//                      the VALU; bias + ReLU + 2x2 max-pool (argmax) into an LDS
-//                      im2col image; conv2 as an implicit GEMM on
-//                      v_mfma_f32_16x16x4_f32, bias + ReLU + pool in the epilogue
+//   AB conv12_fwd      uint8 batch (staged by the previous step) + Normalize; conv1 channels 0-15
+//                      on MFMA with the 2x2 pool in the accumulator registers, 16-19 as 4x4x1 MFMA
+//                      chains; bias + ReLU + pool (argmax) into an LDS im2col image; conv2 as an
+//                      implicit GEMM on v_mfma_f32_16x16x4_f32, bias + ReLU + pool in the epilogue;
+//                      a1 / idx1 published per channel group by the waves conv2's epilogue idles
 //   C  fc1_fwd<2>      split-K MFMA GEMM (256 workgroups), pre-activation halves
-//   D  head            relu(half0 + half1 + b1), fc2 + log_softmax + NLL +
-//                      d(logits) + fc2^T GEMV + ReLU mask
-//   E  fc1_bwd         dW_fc1 / db_fc1 (MFMA), dX_fc1 (MFMA) with un-pool + ReLU
-//                      mask epilogue, dW_fc2 / db_fc2, loss statistics
-//   F  conv_bwd        per (sample, 5-channel group): dcol = W2^T dz2 (MFMA),
-//                      dW_conv2 (MFMA + VALU rows), col2im + un-pool + ReLU mask ->
-//                      dz1 (LDS), dW_conv1 (VALU), per-sample slab rows
-//   G  slab_reduce_sgd deterministic slab reduction + SGD(momentum) on every parameter; in the
-//                      world-1 step it also computes dW_fc1 / db_fc1 (fc1_bwd's job 1) and
-//                      applies their SGD straight from the MFMA accumulators
-// (A conv1_fwd_pool, B conv2_fwd_pool, conv_bwd (per-sample slab rows), sgd_momentum: the
-// unfused / eval / fallback building blocks.)
+//   E' fc1_bwd_head    per (16-sample, 16-feature) tile: the head recomputed on MFMA (h, logits,
+//                      DPP log-softmax / NLL, d(logits), dh on 4x4x1 chains), then d(a2) =
+//                      relu'(a2) . (dh W1) written pooled; next-batch staging blocks
+//   F' conv_bwd4       per (4-sample chunk, 5-channel group): d(a2) un-pooled in LDS, dcol = W2^T
+//                      dz2 (MFMA) -> col2im + ReLU mask (dz1 kept pooled) -> dW_conv1 through idx1
+//                      on waves 0-7, dW_conv2 over the chunk (MFMA + VALU rows) on waves 8-15
+//   G  slab_reduce_sgd the tail: dW_fc1 / db_fc1 and dW_fc2 / db_fc2 tiles (MFMA) with SGD from the
+//                      accumulators, the deterministic conv-slab reduction + SGD(momentum), stats
+// (D head + E fc1_bwd: the world > 1 / fallback form of E'; A conv1_fwd_pool, B conv2_fwd_pool,
+// conv_bwd (per-sample slab rows), sgd_momentum: the unfused / eval / fallback building blocks.)
 //
 // All arithmetic is fp32 (the reference's dtype); matrix work uses the exact-fp32
 // MFMA (one rounding per product, same as an fmaf chain).

@@ -216,11 +216,14 @@ class FusedMnistTrainer:
 
     # ---------------------------------------------------------------- step
     #
-    # One single-process step is six launches (one hipGraph, or the captured kernel list
-    # launched from C++ -- parallel/graphed_step.py):
+    # One single-process step is five launches (round 5; one hipGraph, or the captured kernel
+    # list launched from C++ -- parallel/graphed_step.py):
     #
-    #   conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd (+ next-batch staging) -> conv_bwd4
-    #   -> slab_reduce_sgd (conv slab reduction + SGD of every parameter + cursor advance)
+    #   conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head (head recomputed per tile + d(a2) pooled +
+    #   next-batch staging) -> conv_bwd4 -> tail (dW_fc1 / dW_fc2 tiles with SGD, conv slab
+    #   reduction + SGD, cursor advance)
+    #
+    # (fuse_head / w1_tail off, or world > 1: the six-launch form with head + fc1_bwd.)
     #
     # Fusing a pair across an in-launch hand-off (last-arriving workgroups continue, write-through
     # stores + an arrival counter) measured slower than the launch boundary it removes: fc1 + head
