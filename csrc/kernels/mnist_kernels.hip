@@ -1352,6 +1352,16 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
     asm volatile("" : "+v"(a2o), "+v"(pidx));
     red[wv][lane] = c0 + c1;  // (the logits partials in red were consumed before the last barrier)
   }
+  if (pub) {  // dh for the tail: this wave's 64 columns of the 16 rows, 16-byte stores from its own
+              // LDS writes (one block-end copy of all 500 columns was 0.15 us/step slower, profiles/r5_dhw)
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int e = lane + 64 * it, row = e >> 4, col = 64 * wv + 4 * (e & 15);
+      if (col < 500 && mt * 16 + row < B)
+        *reinterpret_cast<float4*>(a.dh_out + (size_t)(mt * 16 + row) * 500 + col) =
+            *reinterpret_cast<const float4*>(dhs + row * H_DS + col);
+    }
+  }
   __syncthreads();
   float v = red[0][l_e][r_e];
 #pragma unroll
@@ -1367,15 +1377,6 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
       z[1] = pidx == 1 ? d : 0.f;
       z[8] = pidx == 2 ? d : 0.f;
       z[9] = pidx == 3 ? d : 0.f;
-    }
-  }
-  if (pub) {  // block-uniform: dh for the tail, copied from LDS with 16-byte stores after the block's
-              // own output (spreading h / dh over the 50 kt blocks was no faster, profiles/r5_hpub)
-    for (int e = tid; e < 16 * 125; e += E_NT) {
-      const int row = e / 125, c4 = e - row * 125;
-      if (mt * 16 + row < B)
-        reinterpret_cast<float4*>(a.dh_out + (size_t)(mt * 16 + row) * 500)[c4] =
-            *reinterpret_cast<const float4*>(dhs + row * H_DS + 4 * c4);
     }
   }
   stamp(dbg, 3);
