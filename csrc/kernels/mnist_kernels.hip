@@ -2036,18 +2036,19 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       const float v = ((pv_s[lane] + pv_s[64 + lane]) + pv_s[128 + lane]) + pv_s[192 + lane];
       const int j = jbase + (lane & 31);
       if (j >= 0 && j < 125) rowq[(48 + (lane >> 5)) * 500 + j] = v;
+    } else if (cig == 0 && own && lane < 50) {  // wave 15: db_conv2 of the own sample, off group A's
+      // critical path (on wave 0 of group A it made the cig == 0 blocks 0.5 us slower, profiles/r5_b2)
+      const float* dzo = dzc_s + r * G_DZN + lane * G_DZS;
+      float b2sum = 0.f;
+#pragma unroll 8
+      for (int p = 0; p < 64; ++p) b2sum += dzo[p];
+      slab[(size_t)b * stride + o_gb2 + lane] = b2sum;
     }
     return;
   }
   // ---- group A (waves 0-7): 2a, col2im, dW_conv1, the own sample's slab row
   if (!own) return;
   bwd4_2a4(dzc_s, w_s + cig, dcol_s, r, wv, lane);
-  float b2sum = 0.f;
-  if (cig == 0 && tid < 50) {
-    const float* dzo = dzc_s + r * G_DZN + tid * G_DZS;
-#pragma unroll 8
-    for (int p = 0; p < 64; ++p) b2sum += dzo[p];
-  }
   wave_group_sync(&s_grp[0], 8u);
   stamp(dbg, 2);
   for (int it = tid; it < 720; it += 512) {  // phase 3 (as below)
@@ -2088,7 +2089,6 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
       if (tid < 125) rowb[o_gw1 + cig * 125 + tid] = w1sum;
       else rowb[o_gb1 + cig * 5 + (tid - 125)] = w1sum;
     }
-    if (cig == 0 && tid < 50) rowb[o_gb2 + tid] = b2sum;
     stamp(dbg, 5);
   }
 }

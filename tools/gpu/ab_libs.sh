@@ -4,7 +4,7 @@
 # variant named in AB_ENVS ("tag:VAR=VAL[,VAR=VAL]" entries, space-separated; run on the
 # in-tree library).  Per variant: the kernel tests, the in-situ step timeline
 # (tools/step_timeline.py), then REPS rounds of bench K=2000 x3 and K=20 x2.
-#   AB_ENVS="tag:VAR=VAL" bash tools/gpu/ab_libs.sh OUT_DIR [REPS]
+#   AB_ENVS="tag:VAR=VAL" TL_ARGS="--by-mod conv_bwd4:4" bash tools/gpu/ab_libs.sh OUT_DIR [REPS]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -22,7 +22,7 @@ for v in $variants; do
   IFS='|' read -r tag L E <<< "$v"
   run "$L" "$E" timeout -k 10 200 python -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
     -k "fused or round3 or staged or stream_launch" > $O/pytest_$tag.log 2>&1 || { tail -30 $O/pytest_$tag.log; exit 1; }
-  run "$L" "$E" timeout -k 10 120 python tools/step_timeline.py --json $O/timeline_$tag.json > $O/timeline_$tag.txt 2>&1 || { cat $O/timeline_$tag.txt; exit 1; }
+  run "$L" "$E" timeout -k 10 120 python tools/step_timeline.py $TL_ARGS --json $O/timeline_$tag.json > $O/timeline_$tag.txt 2>&1 || { cat $O/timeline_$tag.txt; exit 1; }
   echo "== $tag"; grep -E "period|one step" $O/timeline_$tag.txt
 done
 for rep in $(seq 1 $REPS); do

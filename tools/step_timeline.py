@@ -75,7 +75,8 @@ def analyse(dbg: torch.Tensor, nslots: int):
             aux = float(((w[:, 7] - w[:, 1]) * ok).sum() / ok.sum().clamp_min(1) / 100.0)
         out.append({"aux71": aux, "blocks": int(used.sum()), "start": float(w[:, 0].min()), "end": float(last.max()),
                     "p50end": float(last.median()), "block_end": dict(zip(idx.tolist(), last.tolist())),
-                    "phases": phases[:nph], "ghz": ghz[:nph]})
+                    "phases": phases[:nph], "ghz": ghz[:nph],
+                    "block_rows": {"idx": idx, "w": w, "valid": valid}})
     return out
 
 
@@ -84,6 +85,9 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--json", default=None)
     ap.add_argument("--reps", type=int, default=5, help="timelines sampled (each after --steps steps)")
+    ap.add_argument("--by-mod", action="append", default=[], metavar="KERNEL:N",
+                    help="per-block breakdown of KERNEL (second step) grouped by block id %% N: start, "
+                         "phase times and end relative to the kernel's first stamp, plus the latest blocks")
     ap.add_argument("--conv1-waves", action="store_true",
                     help="diagnostic build (-DPTO_MNIST_STAMPW): conv12_fwd's per-wave conv1 stamps")
     args = ap.parse_args(argv)
@@ -164,9 +168,45 @@ def main(argv=None):
               "; ".join(f"{n} {v}" for n, v in aux))
     print("effective shader clock per phase (GHz, clock64 / wall_clock64): " +
           "; ".join(f"{r['kernel']} {r['phase_ghz']}" for r in rows[per:]))
+    for spec in args.by_mod:
+        kname, mod = spec.split(":")
+        res.setdefault("by_mod", {})[spec] = by_mod(samples, names, per, kname, int(mod))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
+
+
+def by_mod(samples, names, per, kname, mod):
+    """Mean start / phase times / end of the blocks of KERNEL (second step) grouped by block id % mod,
+    over every sample, and the ten latest-ending blocks of the last sample."""
+    k = per + names.index(kname)
+    acc = {}
+    for s in samples:
+        br = s[k]["block_rows"]
+        t0 = s[k]["start"]
+        for row, blk in enumerate(br["idx"].tolist()):
+            w, v = br["w"][row], br["valid"][row]
+            stamps = [float(w[j]) for j in range(8) if v[j]]
+            a = acc.setdefault(blk % mod, {"n": 0, "start": 0.0, "end": 0.0, "ph": [0.0] * 7, "phn": [0] * 7})
+            a["n"] += 1
+            a["start"] += (float(w[0]) - t0) / 100.0
+            a["end"] += (max(stamps) - t0) / 100.0
+            for j in range(6):
+                if v[j] and v[j + 1]:
+                    a["ph"][j] += float(w[j + 1] - w[j]) / 100.0
+                    a["phn"][j] += 1
+    out = {}
+    print(f"{kname} blocks by id % {mod}: start / phases / end (us after the kernel's first stamp)")
+    for g in sorted(acc):
+        a = acc[g]
+        ph = [round(a["ph"][j] / a["phn"][j], 2) for j in range(6) if a["phn"][j]]
+        out[g] = {"blocks": a["n"] // len(samples), "start": round(a["start"] / a["n"], 2), "phases": ph,
+                  "end": round(a["end"] / a["n"], 2)}
+        print(f"  {g}: {out[g]}")
+    s = samples[-1]
+    ends = sorted(((e - s[k]["start"]) / 100.0, b) for b, e in s[k]["block_end"].items())[-10:]
+    print("  latest blocks (end us, block id): " + ", ".join(f"{e:.2f} #{b}" for e, b in ends))
+    return out
 
 
 if __name__ == "__main__":
