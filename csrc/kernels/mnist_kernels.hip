@@ -1116,8 +1116,9 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
 //   dh = (d(logits) . W2) * (h > 0)             (M 16, N 512, K 16; each wave its own 64 k)
 //   dz2 = un-pool(relu'(a2) * (dh . W1))         (fc1_bwd's job 2, unchanged)
 // The 50 kt blocks of a sample tile recompute the same head -- a few MFMAs next to the dz2 GEMM,
-// against a launch + boundary -- and the kt == 0 block publishes h, dh, d(logits) and the
-// per-sample (loss, correct) for the tail (dW_fc1, dW_fc2, statistics).  Sums differ from
+// against a launch + boundary -- and the kt == 0 block publishes h, d(logits) and the
+// per-sample (loss, correct), the kt = 1..8 blocks one wave's dh columns each, for the tail
+// (dW_fc1, dW_fc2, statistics).  Sums differ from
 // head_kernel's lane-tree order by fp32 rounding (the DDP paths keep head + fc1_bwd).
 struct Fc1BwdHead {
   const float *hp0, *hp1, *b1;  // fc1 split-K partials [B][500] x 2, fc1.bias [500]
@@ -1128,7 +1129,7 @@ struct Fc1BwdHead {
   const float* w1;              // fc1.weight [500][800]
   float* dz2;                   // [B][50][8][8] (dense), or
   float* dpool;                 // [B][800] pooled d(a2) (conv_bwd4 un-pools it through idx2)
-  float *h_out, *dh_out, *dlog_out, *per_sample;  // published by the kt == 0 blocks
+  float *h_out, *dh_out, *dlog_out, *per_sample;  // published by the kt == 0 (dh: 1..8) blocks
   float grad_scale;             // 1 / B
   int B;
   BatchSrc nsrc;                // next-batch staging (stage_x != null), as fc1_bwd
@@ -1352,8 +1353,11 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
     asm volatile("" : "+v"(a2o), "+v"(pidx));
     red[wv][lane] = c0 + c1;  // (the logits partials in red were consumed before the last barrier)
   }
-  if (pub) {  // dh for the tail: this wave's 64 columns of the 16 rows, 16-byte stores from its own
-              // LDS writes (one block-end copy of all 500 columns was 0.15 us/step slower, profiles/r5_dhw)
+  if (kt == 1 + wv) {  // dh for the tail: wave wv of tile kt = 1 + wv publishes its 64 columns of the
+                       // 16 rows (every tile of the row block computes the same dh), 16-byte stores
+                       // from its own LDS writes -- not all on the kt == 0 tiles, which then ended
+                       // the kernel 0.3 us after the others (profiles/r5_dhs); one block-end copy of
+                       // all 500 columns was slower still (profiles/r5_dhw)
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int e = lane + 64 * it, row = e >> 4, col = 64 * wv + 4 * (e & 15);
