@@ -75,3 +75,26 @@ def test_bench_forced_collectives_world1_through_operator(tmp_path):
     assert job.get("result") == "Succeeded" and job["backend"] == "rccl", job
     jt = job["allreduce_trial"]
     assert jt is not None and jt["rccl_ms_per_step"] > 0 and jt["rccl_graph_ms_per_step"] > 0, job
+
+
+@pytest.mark.timeout(300)
+def test_rccl_tune_candidates_run_under_rccl(tmp_path):
+    """tools/rccl_tune.py: every RCCL env candidate initialises a real RCCL communicator and
+    all-reduces the two gradient buckets correctly (one rank: the protocol choice itself needs
+    >= 2 GPUs, see the tool's docstring)."""
+    out = tmp_path / "tune.json"
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "rccl_tune.py"), "--nproc", "1", "--candidates",
+                        "default,proto-LL,proto-Simple,algo-Ring", "--iters", "50", "--reps", "3",
+                        "--timeout", "120", "--out", str(out)],
+                       capture_output=True, text=True, timeout=290, cwd=ROOT, env=_env())
+    assert out.exists(), r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    rec = os.environ.get("PTO_TEST_RECORD_DIR")
+    if rec:
+        Path(rec).mkdir(parents=True, exist_ok=True)
+        (Path(rec) / "rccl_tune_w1.json").write_text(json.dumps(res, indent=1))
+    assert r.returncode == 0, r.stderr[-3000:]
+    for c in res["candidates"]:
+        assert "error" not in c, c
+        assert c["correct"] and c["backend"] == "nccl" and c["device"] == "cuda" and c["step_us"] > 0
+    assert "HSA_ENABLE_IPC_MODE_LEGACY=0" in res["winner"]["operator_flags"]
