@@ -1,6 +1,7 @@
 #include "pto/options.hpp"
 
 #include <cstdlib>
+#include <fstream>
 #include <functional>
 #include <map>
 
@@ -68,6 +69,8 @@ std::string usage() {
          "  -inject-rccl-env          Inject LOCAL_RANK and the RCCL env set into pytorch containers\n"
          "  -rccl-env KEY=VALUE       Replace the injected RCCL env set (repeatable; default\n"
          "                            HSA_ENABLE_IPC_MODE_LEGACY=0)\n"
+         "  -rccl-env-file path       As -rccl-env, one KEY=VALUE per line (# comments): the\n"
+         "                            measured set tools/rccl_tune.py --env-out writes\n"
          "  -xgmi-pod-topology        GPU pods: hostPID/hostIPC, NCCL_HOSTID=<node>, one-node affinity\n"
          "  -init-container-template-file  (default /etc/config/initContainer.yaml)\n"
          "  -log-level string         debug|info|warning|error (default info)\n";
@@ -136,6 +139,25 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
          auto eq = v.find('=');
          if (eq == std::string::npos || eq == 0) return std::string("expected KEY=VALUE, got \"") + v + "\"";
          o->rccl_env.emplace_back(v.substr(0, eq), v.substr(eq + 1));
+         o->rccl_env_set = true;
+         return std::string();
+       }}},
+      {"rccl-env-file", Flag{false, [o](const std::string& path) {
+         std::ifstream f(path);
+         if (!f) return std::string("cannot read \"") + path + "\"";
+         std::string line;
+         int n = 0;
+         while (std::getline(f, line)) {
+           ++n;
+           const auto b = line.find_first_not_of(" \t\r");
+           if (b == std::string::npos || line[b] == '#') continue;
+           const auto e = line.find_last_not_of(" \t\r");
+           const std::string kv = line.substr(b, e - b + 1);
+           const auto eq = kv.find('=');
+           if (eq == std::string::npos || eq == 0)
+             return path + ":" + std::to_string(n) + ": expected KEY=VALUE, got \"" + kv + "\"";
+           o->rccl_env.emplace_back(kv.substr(0, eq), kv.substr(eq + 1));
+         }
          o->rccl_env_set = true;
          return std::string();
        }}},

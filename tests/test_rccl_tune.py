@@ -43,3 +43,28 @@ def test_unknown_candidate_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_tune.py"), "--candidates", "nope"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "unknown candidates" in r.stderr
+
+
+def test_env_file_reaches_the_operator(tmp_path):
+    """--env-out writes the winner as KEY=VALUE lines; pytorch-operator --rccl-env-file reads them
+    (comments and blank lines skipped, a malformed line refused with its line number)."""
+    from pytorch_operator_amd.cluster.local import operator_binary
+    out, env = tmp_path / "tune.json", tmp_path / "rccl.env"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_tune.py"), "--nproc", "1", "--backend",
+                        "gloo", "--device", "cpu", "--candidates", "proto-LL", "--iters", "2", "--reps", "1",
+                        "--warmup", "1", "--out", str(out), "--env-out", str(env)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in env.read_text().splitlines() if ln and not ln.startswith("#")]
+    assert lines == ["HSA_ENABLE_IPC_MODE_LEGACY=0", "NCCL_PROTO=LL"]
+    bin_ = operator_binary()
+    r = subprocess.run([bin_, "--inject-rccl-env", "--rccl-env-file", str(env), "--version"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    bad = tmp_path / "bad.env"
+    bad.write_text("# ok\n\nNCCL_ALGO=Ring\nNOVALUE\n")
+    r = subprocess.run([bin_, "--rccl-env-file", str(bad), "--version"], capture_output=True, text=True)
+    assert r.returncode != 0 and "bad.env:4" in (r.stderr + r.stdout)
+    r = subprocess.run([bin_, "--rccl-env-file", str(tmp_path / "missing.env"), "--version"],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "cannot read" in (r.stderr + r.stdout)

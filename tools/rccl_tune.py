@@ -9,7 +9,8 @@ rank timing ``all_reduce`` of the fc bucket (fc1 + fc2, 1.61 MB fp32) and of the
 timed repetitions).  The winner comes out as the operator's ``--rccl-env`` flags (they replace
 the injected set, so ``HSA_ENABLE_IPC_MODE_LEGACY=0`` is kept in them).
 
-    python tools/rccl_tune.py --nproc 8 --out rccl_tune.json            # on the 8-GPU node
+    python tools/rccl_tune.py --nproc 8 --out rccl_tune.json --env-out rccl.env   # the 8-GPU node
+    pytorch-operator --inject-rccl-env --rccl-env-file rccl.env ...
     python tools/rccl_tune.py --nproc 2 --backend gloo --device cpu ...  # plumbing (CPU test)
 
 At one rank RCCL's all-reduce is a local copy: the race then only checks that every candidate
@@ -182,6 +183,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--timeout", type=float, default=180.0, help="seconds per candidate job")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--env-out", default=None,
+                    help="also write the winner's env as KEY=VALUE lines (pytorch-operator --rccl-env-file)")
     args = ap.parse_args(argv)
     if args.worker:
         return worker(args)
@@ -193,6 +196,12 @@ def main(argv=None) -> int:
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
+    if args.env_out and "winner" in res:
+        w = res["winner"]
+        with open(args.env_out, "w") as f:
+            f.write(f"# tools/rccl_tune.py winner {w['name']} ({w['step_us']} us per step, {res['nproc']} ranks)\n")
+            for k, v in sorted({**BASE_ENV, **w["env"]}.items()):
+                f.write(f"{k}={v}\n")
     print(json.dumps(res.get("winner", {"error": "no candidate ran"})))
     return 0 if "winner" in res else 1
 
