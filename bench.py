@@ -29,6 +29,11 @@ import time
 
 BASELINE_PER_RANK = 210.0
 
+# Kernel arguments in device memory -- this image's default; with them in host memory every
+# dependent launch of the step waits on the host read: 43.61-43.83 instead of 35.30-35.37 us/step
+# at K=2000 (profiles/r5_env/ab.txt).  Set before HIP initialises, unless the caller chose.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 
 def pick_steps_per_graph(steps: int, warmup: int = 0, cap: int = 250) -> int:
     """Whole training steps per hipGraph replay of the timed region: a divisor of ``steps``
