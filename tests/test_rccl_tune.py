@@ -68,3 +68,15 @@ def test_env_file_reaches_the_operator(tmp_path):
     r = subprocess.run([bin_, "--rccl-env-file", str(tmp_path / "missing.env"), "--version"],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "cannot read" in (r.stderr + r.stdout)
+
+
+def test_candidate_timeout_kills_its_job(tmp_path):
+    """A candidate job over --timeout is killed with its process group and reported; with no
+    candidate left the tool exits 1 and names no winner."""
+    out = tmp_path / "tune.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_tune.py"), "--nproc", "2", "--backend",
+                        "gloo", "--device", "cpu", "--candidates", "default", "--timeout", "0.5", "--out", str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert "winner" not in res and res["candidates"][0]["error"].startswith("timeout")

@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -141,13 +142,18 @@ def race(names, nproc: int, backend: str, device: str, iters: int, reps: int, wa
                    "--worker", "--out", out, "--backend", backend, "--device", device, "--iters", str(iters),
                    "--reps", str(reps), "--warmup", str(warmup)]
             row = {"name": name, "env": CANDIDATES[name]}
+            # own process group: a candidate that hangs is killed with its torchrun workers
+            p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                 start_new_session=True)
             try:
-                r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
-                if r.returncode == 0 and os.path.exists(out):
+                so, se = p.communicate(timeout=timeout)
+                if p.returncode == 0 and os.path.exists(out):
                     row.update(json.load(open(out)))
                 else:
-                    row["error"] = f"rc={r.returncode}: {(r.stderr or r.stdout)[-400:]}"
+                    row["error"] = f"rc={p.returncode}: {(se or so)[-400:]}"
             except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.communicate()
                 row["error"] = f"timeout after {timeout} s"
             rows.append(row)
             print(json.dumps({k: row.get(k) for k in ("name", "step_us", "fc_us", "conv_us", "correct", "error")}),
