@@ -14,8 +14,16 @@ random-init (torch.manual_seed + the reference's default init).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--kernels hip|torch]
     torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
 
+``python bench.py --gpus N`` with N > 1 and no launcher (no ``WORLD_SIZE`` in the env) starts
+the N ranks itself: before importing torch or touching HIP it runs ``torch.distributed.run
+--nproc-per-node N`` as a CHILD process (never an exec), relays rank 0's line and exits with
+the child's code.  A realised world size that differs from ``--gpus`` is an error (exit 2),
+never a warning.
+
 Rank 0 prints ONE JSON line.  ``value`` is the whole-job samples/s (sum over
 ranks), timed as the MAX over ranks of K steps bracketed by barrier+synchronize.
+``world_size`` is the process group's size and ``rccl_nranks`` the rank count RCCL's own
+communicator reports (``ncclCommCount``; null unless the group runs on RCCL).
 ``vs_baseline`` divides by 210 samples/s/rank x N: the reference's derived
 per-rank throughput (>= 210 samples/s/rank, 420 aggregate at 2 ranks).
 """
@@ -24,6 +32,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
 import time
 
@@ -92,6 +102,123 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+SELF_LAUNCH_ENV = "PTO_BENCH_LAUNCHER"
+
+
+def needs_self_launch(gpus: int, environ=None) -> bool:
+    """True when this process must start the ``gpus`` ranks itself: more than one GPU asked
+    for and no launcher (torchrun or the operator's pods) has set up a rank environment."""
+    environ = os.environ if environ is None else environ
+    return gpus > 1 and "WORLD_SIZE" not in environ
+
+
+def launch_command(argv, gpus: int, port: int, script: str = None):
+    """The ``torch.distributed.run`` command line of a self-launched N-rank bench: one process
+    per GPU on this node, rendezvous on 127.0.0.1, the same bench arguments."""
+    script = script or os.path.abspath(__file__)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), script, *argv]
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpu_count(timeout: float = 300.0) -> int:
+    """GPUs this node exposes, counted in a child interpreter so that the launching process
+    itself never loads HIP (``torch.cuda.device_count()`` does not initialise the device)."""
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=timeout)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def check_line(line: dict, gpus: int):
+    """None if rank 0's line describes a ``gpus``-rank run, else the reason it does not."""
+    if line.get("n_gpus") != gpus or line.get("world_size") != gpus:
+        return (f"asked for {gpus} ranks, the run reports n_gpus={line.get('n_gpus')} "
+                f"world_size={line.get('world_size')}")
+    if line.get("rccl_nranks") not in (None, gpus):
+        return f"RCCL communicator has {line.get('rccl_nranks')} ranks, expected {gpus}"
+    return None
+
+
+def self_launch(args, argv, script: str = None) -> int:
+    """Run the N-rank bench as a child ``torch.distributed.run`` job and relay its output.
+
+    The parent never imports torch (the GPU count comes from a child interpreter), so no HIP
+    state exists here when the ranks start.  Exit code: the job's, or 2 when RCCL is asked
+    for more ranks than visible GPUs / the realised world differs from ``--gpus`` / rank 0
+    printed no line."""
+    if args.backend in ("nccl", "rccl"):
+        n = visible_gpu_count()
+        if n < args.gpus:
+            print(f"error: --gpus {args.gpus} with --backend {args.backend} needs one GPU per rank; "
+                  f"{n} visible (use --backend gloo to rehearse ranks sharing a GPU)", file=sys.stderr)
+            return 2
+    env = dict(os.environ, **{SELF_LAUNCH_ENV: "bench.py->torch.distributed.run"})
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = launch_command(argv, args.gpus, _free_port(), script)
+    print("launching: " + " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+
+    def _forward(signum, _frame):  # a timeout on the parent ends the ranks too
+        child.send_signal(signum)
+    prev = {s: signal.signal(s, _forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    line = None
+    try:
+        for raw in child.stdout:
+            sys.stdout.write(raw)
+            sys.stdout.flush()
+            if raw.startswith('{"metric"'):
+                line = json.loads(raw)
+        rc = child.wait()
+    finally:
+        for s, h in prev.items():
+            signal.signal(s, h)
+    if rc != 0:
+        return rc
+    if line is None:
+        print("error: rank 0 printed no result line", file=sys.stderr)
+        return 2
+    why = check_line(line, args.gpus)
+    if why:
+        print(f"error: {why}", file=sys.stderr)
+        return 2
+    return 0
+
+
+def rccl_nranks():
+    """Rank count of the default group's RCCL communicator (``ncclCommCount`` on the comm
+    torch's ProcessGroupNCCL holds), from the librccl this process has loaded; None when the
+    group is not on RCCL or the communicator is not exposed."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_backend() != "nccl":
+        return None
+    try:
+        ptr = int(dist.group.WORLD._get_backend(torch.device("cuda"))._comm_ptr())
+        path = None
+        with open("/proc/self/maps") as f:
+            for ln in f:
+                if "librccl.so" in ln:
+                    path = ln.split()[-1]
+                    break
+        if not ptr or path is None:
+            return None
+        lib = ctypes.CDLL(path)
+        n = ctypes.c_int(-1)
+        return int(n.value) if lib.ncclCommCount(ctypes.c_void_p(ptr), ctypes.byref(n)) == 0 else None
+    except Exception:  # noqa: BLE001 -- a missing accessor leaves the field null
+        return None
+
+
 def job_gpu_plan(world: int, job_gpus: str, job_backend: str):
     """(node GPU ids, backend) of the bench's PyTorchJob: one pod per GPU over RCCL unless
     ``job_gpus`` repeats an id (pods sharing a device need gloo: RCCL wants one GPU per rank)."""
@@ -157,7 +284,15 @@ def prewarm(ms: int, dev) -> None:
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse_args(argv)
+    if needs_self_launch(args.gpus):
+        return self_launch(args, argv)
+    launcher_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if launcher_world != args.gpus:  # decided before any process group or GPU work
+        print(f"error: --gpus {args.gpus} but the launcher's WORLD_SIZE is {launcher_world}",
+              file=sys.stderr)
+        return 2
     import torch
     import torch.distributed as dist
 
@@ -168,10 +303,10 @@ def main(argv=None):
     env = init_from_env(args.backend, use_gpu=True, force_pg=force)
     world, rank, dev = env.world_size, env.rank, env.device
     pg = dist.is_initialized()  # world > 1, or a forced single-rank group
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}",
-                  file=sys.stderr)
+    pg_world = dist.get_world_size() if pg else 1
+    if pg_world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the process group has {pg_world} ranks", file=sys.stderr)
+        return 2
     B = args.batch_size
     job_plan = job_gpu_plan(world, args.job_gpus, args.job_backend)  # validated before any work
 
@@ -285,6 +420,7 @@ def main(argv=None):
         diff = (flat - ref).abs().max().reshape(1)
         dist.all_reduce(diff, op=dist.ReduceOp.MAX)
         in_sync = bool(float(diff.item()) == 0.0) and ar_err == 0
+    nranks = rccl_nranks()
 
     # a forced-collectives bench forces them in the job's pods too (their race lands in job.allreduce_trial)
     lat = job_latency(world, rank, args.job_timeout, *job_plan,
@@ -303,6 +439,9 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (BASELINE_PER_RANK * world), 1),
+        "world_size": pg_world,
+        "rccl_nranks": nranks,
+        "launcher": os.environ.get(SELF_LAUNCH_ENV) or ("external" if "WORLD_SIZE" in os.environ else "none"),
         "replicas_in_sync": in_sync,
         "grad_allreduce_error": ar_err,
         "device_prewarm_ms": args.prewarm_ms,

@@ -1335,6 +1335,13 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
       }
     }
   }
+  // The dz2 job and the dh publication below read dhs columns [64 wv, 64 wv + 64) that OTHER lanes
+  // of this wave just wrote.  LDS operations of one wave execute in order, so no s_barrier is
+  // needed; the wave barrier and the wavefront-scope fences make that hand-off explicit to the
+  // compiler (no LDS read may be scheduled above the stores) without emitting a wait.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // ---- dz2 job (fc1_bwd's job 2): K = 500 split over the waves; this wave reads only the dh it wrote
   {
     const float4* dr = reinterpret_cast<const float4*>(dhs + i * H_DS + kb);

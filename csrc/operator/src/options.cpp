@@ -146,7 +146,7 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
          std::ifstream f(path);
          if (!f) return std::string("cannot read \"") + path + "\"";
          std::string line;
-         int n = 0;
+         int n = 0, pairs = 0;
          while (std::getline(f, line)) {
            ++n;
            const auto b = line.find_first_not_of(" \t\r");
@@ -157,7 +157,11 @@ std::string parse_flags(int argc, char** argv, ServerOption* o) {
            if (eq == std::string::npos || eq == 0)
              return path + ":" + std::to_string(n) + ": expected KEY=VALUE, got \"" + kv + "\"";
            o->rccl_env.emplace_back(kv.substr(0, eq), kv.substr(eq + 1));
+           ++pairs;
          }
+         // an empty (or comments-only) file would replace the default injected set with
+         // nothing and silently drop HSA_ENABLE_IPC_MODE_LEGACY=0 from every pod
+         if (pairs == 0) return path + ": no KEY=VALUE lines";
          o->rccl_env_set = true;
          return std::string();
        }}},

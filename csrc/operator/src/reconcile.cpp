@@ -143,6 +143,10 @@ static void inject_rccl_env(Json& tmpl, const ControllerConfig& cfg) {
       env.push_back(e);
     };
     add("LOCAL_RANK", "0");  // one amd.com/gpu per pod: the pod sees its GPU as device 0
+    // kernel arguments in device memory: with host-memory kernargs every dependent launch of
+    // the MNIST step waits on a host read, +8.3 us/step (profiles/r5_env/ab.txt).  Pinned here
+    // so a node image with another default cannot slow the job down behind the bench's back.
+    add("HIP_FORCE_DEV_KERNARG", "1");
     for (const auto& kv : cfg.rccl_env) add(kv.first, kv.second);
   }
 }

@@ -40,6 +40,11 @@ from typing import Optional
 
 _T_MODULE = time.time_ns()  # worker entry when run as ``python -m pytorch_operator_amd.harness.mnist``
 
+# Kernel arguments in device memory, pinned before anything can initialise HIP (the same pin as
+# bench.py; host-memory kernargs cost +8.3 us per MNIST step, profiles/r5_env/ab.txt).  The
+# operator also injects it into the pod (--inject-rccl-env); a value the environment sets wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description="PyTorch MNIST Example (MI355X-native worker)")

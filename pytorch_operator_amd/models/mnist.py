@@ -42,6 +42,44 @@ class Net(nn.Module):
         return F.log_softmax(x, dim=1)
 
 
+def _pool_at(r: torch.Tensor, code: torch.Tensor) -> torch.Tensor:
+    """2x2/stride-2 pooling of ``r`` [B, C, H, W] that takes, per window, the element whose
+    in-window code (dy * 2 + dx, the kernels' idx1 / idx2 convention) is ``code``."""
+    B, C, H, W = r.shape
+    win = r.view(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+    return win.gather(4, code.view(B, C, H // 2, W // 2, 1).long()).squeeze(4)
+
+
+class ArgmaxAlignedNet(Net):
+    """``Net`` whose two max-pools take their argmax from given codes (the HIP kernels' idx1 /
+    idx2 of the same step); every other op -- convs, ReLU, linears, log-softmax, and through the
+    caller NLL, DDP averaging and SGD -- is torch's own fp32.
+
+    Why: a pool window whose two largest values lie within fp32 rounding of each other has no
+    stable argmax.  The HIP convs sum in a different order than torch's, so such a window may
+    route its gradient to the other element -- a legitimate max, but a different trajectory
+    (tools/dbg/grad_diag.py found one per few dozen synthetic batches, moving conv grads by
+    ~5e-3).  ``forward`` also records in ``self.pool_gap`` the largest amount by which torch's
+    own window maximum exceeds the value at the given argmax (relative to the layer's
+    magnitude): ~1e-6 means every given argmax IS a maximum up to rounding."""
+
+    def forward(self, x, idx1=None, idx2=None):
+        if idx1 is None:
+            return super().forward(x)
+        r1 = F.relu(self.conv1(x))
+        p1 = _pool_at(r1, idx1)
+        r2 = F.relu(self.conv2(p1))
+        p2 = _pool_at(r2, idx2.view(-1, 50, 4, 4))
+        with torch.no_grad():
+            gap = 0.0
+            for r, p in ((r1, p1), (r2, p2)):
+                m = F.max_pool2d(r, 2, 2)
+                gap = max(gap, float((m - p).max() / m.abs().max().clamp_min(1e-30)))
+            self.pool_gap = max(getattr(self, "pool_gap", 0.0), gap)
+        h = F.relu(self.fc1(p2.reshape(-1, 800)))
+        return F.log_softmax(self.fc2(h), dim=1)
+
+
 PARAM_SPECS: List[Tuple[str, Tuple[int, ...]]] = [
     ("conv1.weight", (20, 1, 5, 5)),
     ("conv1.bias", (20,)),
@@ -53,6 +91,8 @@ PARAM_SPECS: List[Tuple[str, Tuple[int, ...]]] = [
     ("fc2.bias", (10,)),
 ]
 NUM_PARAMS = sum(int(torch.Size(s).numel()) for _, s in PARAM_SPECS)  # 431080
+_CONV_NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")
+_FC_NAMES = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
 _ALIGN = 16  # floats (64 B) per segment start
 
 
@@ -123,13 +163,17 @@ class FusedMnistTrainer:
         L = self.layout.total
         dev = self.device
         self._fp = torch.zeros(L, device=dev)
-        # grads are fully overwritten every step (no zeroing): fc grads by fc1_bwd, conv
-        # grads by the deterministic slab reduction; stats = (loss, #correct) of the step
+        # grads are overwritten (never accumulated, so never zeroed) by the launches that
+        # produce them -- but not every step form stores every gradient: the default world-1
+        # step applies SGD to fc1/fc2 straight from the MFMA accumulators and the xGMI step
+        # reduces conv grads in the exchange.  ``grads`` therefore raises for the segments the
+        # last step did not store (``_stale``); stats = (loss, #correct) of the step
         self.flat_grads = torch.zeros(L, device=dev)
         self.stats = torch.zeros(16, device=dev)
         self._fm = torch.zeros(L, device=dev)
         self._pv = _views(self._fp, self.layout)
-        self.grads = _views(self.flat_grads, self.layout)
+        self._gv = _views(self.flat_grads, self.layout)
+        self._stale: Tuple[str, ...] = ()
         # device batch cursor: advanced by the SGD launch, read by conv12_fwd / fc1_bwd's staging
         self.cursor = source.cursor if (source is not None and source.cursor is not None) \
             else torch.zeros(1, device=dev, dtype=torch.int32)
@@ -172,6 +216,19 @@ class FusedMnistTrainer:
     @property
     def params(self) -> Dict[str, torch.Tensor]:
         return self._pv
+
+    @property
+    def grads(self) -> Dict[str, torch.Tensor]:
+        """Per-parameter gradient views of ``flat_grads`` as the last step stored them.
+
+        Raises if that step did not store some of them (their buffer then holds an older
+        step's values): the default single-process step keeps the fc gradients in registers
+        (set ``materialize_fc1_grad = True`` to also store them), the xGMI step the conv and
+        dW_fc1 gradients.  ``forward_backward()`` stores all of them."""
+        if self._stale:
+            raise RuntimeError(f"gradients {list(self._stale)} were not stored by the last step "
+                               "(materialize_fc1_grad=True, or forward_backward(), stores them)")
+        return self._gv
 
     def _alloc(self, B: int):
         dev = self.device
@@ -278,7 +335,7 @@ class FusedMnistTrainer:
                  jobs: Optional[int] = None) -> None:
         """fc1_bwd; with ``stage_adv`` (and staging on), also stage the batch of cursor + stage_adv;
         with ``xpush``, also push dW_fc1 to its xGMI owners (ops.mnist.fc1_bwd)."""
-        K, p, g = self.K, self._pv, self.grads
+        K, p, g = self.K, self._pv, self._gv
         st = self._stage_for(None) if stage_adv is not None and xpush is None else None
         K.fc1_bwd(self.dh[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], self.dlogits[:B],
                   self.h1[:B], g["fc1.weight"], g["fc1.bias"], g["fc2.weight"], g["fc2.bias"],
@@ -343,6 +400,7 @@ class FusedMnistTrainer:
         self.backward_conv(source, B)
         if self.grad_sync is not None:
             self.grad_sync.conv_ready(self.conv_bucket())
+        self._stale = ()
 
     def optimizer_step(self, advance_cursor: bool = True, grad_scale: Optional[float] = None) -> None:
         if grad_scale is None:
@@ -374,6 +432,7 @@ class FusedMnistTrainer:
                 slab=self.conv_slab, slab_rows=B, conv_n=self.layout.conv_end,
                 slab_big=self._slab_big(B), skip=(w1o, w1o + 400000) if push else None)
             self._first_step = False
+            self._stale = _CONV_NAMES + (("fc1.weight",) if push else ())
             return
         if self.grad_sync is not None:
             self.forward_backward(source, B)
@@ -398,6 +457,7 @@ class FusedMnistTrainer:
                          self._fp[o2w:o2b], self._fm[o2w:o2b], self.flat_grads[o2w:o2b] if mat else None,
                          self._fp[o2b:], self._fm[o2b:], self.flat_grads[o2b:] if mat else None))
             self._first_step = False
+            self._stale = () if mat else _FC_NAMES
             return
         # 6 launches: conv12_fwd -> fc1_fwd<2> -> head -> fc1_bwd -> conv_bwd4 -> tail
         self.forward(source, B)
@@ -417,6 +477,7 @@ class FusedMnistTrainer:
                            extra=(self._fp[e0:], self.flat_grads[e0:], self._fm[e0:]),
                            big=self._slab_big(B), w1=w1)
         self._first_step = False
+        self._stale = ("fc1.weight", "fc1.bias") if w1t and not self.materialize_fc1_grad else ()
 
     def loss(self) -> float:
         return float(self.stats[0].item())

@@ -26,6 +26,45 @@ def _port():
         return s.getsockname()[1]
 
 
+@pytest.mark.timeout(300)
+def test_bench_self_launch(tmp_path):
+    """The driver's bare command ``python3 bench.py --gpus 2 ...`` (no torchrun, no WORLD_SIZE):
+    bench.py starts the two ranks itself and rank 0's line reports a two-rank run."""
+    out = tmp_path / "bench.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(ROOT)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "20",
+           "--warmup", "5", "--job-latency", "0", "--json-out", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line == json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["steps"] == 20, line
+    assert line["replicas_in_sync"] is True and line["grad_allreduce_error"] == 0, line
+    assert line["launcher"] == "bench.py->torch.distributed.run", line
+    assert line["rccl_nranks"] is None and line["config"]["backend"] == "gloo", line
+    rec = os.environ.get("PTO_TEST_RECORD_DIR")
+    if rec:
+        Path(rec).mkdir(parents=True, exist_ok=True)
+        (Path(rec) / "bench_self_launch_w2.json").write_text(json.dumps(line))
+
+
+@pytest.mark.timeout(200)
+def test_bench_rccl_nranks_world1(tmp_path):
+    """Forced single-rank RCCL group: the line carries the communicator's own rank count."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONPATH"] = str(ROOT)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--backend", "nccl", "--force-collectives", "1",
+           "--steps", "20", "--warmup", "5", "--job-latency", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric"')][0])
+    assert line["world_size"] == 1 and line["rccl_nranks"] == 1, line
+    assert line["config"]["backend"] == "rccl", line
+
+
 @pytest.mark.timeout(400)
 @pytest.mark.parametrize("allreduce", ["xgmi", "auto", "auto-slow-xgmi"])
 def test_bench_two_ranks_one_gpu(tmp_path, allreduce):

@@ -602,3 +602,21 @@ def test_flat_grad_allreduce_forced_at_world1_gloo():
             os.environ.pop(k, None)
             if v is not None:
                 os.environ[k] = v
+
+
+def test_worker_pins_device_kernel_arguments():
+    """The operator-deployed worker pins device-memory kernel arguments before HIP can start
+    (bench.py pins the same; profiles/r5_env/ab.txt), unless the pod's env chose otherwise."""
+    import subprocess
+    import sys
+    code = ("import os, sys; import pytorch_operator_amd.harness.mnist; "
+            "print(os.environ.get('HIP_FORCE_DEV_KERNARG'), 'torch.cuda' in sys.modules and "
+            "__import__('torch').cuda.is_initialized())")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "HIP_FORCE_DEV_KERNARG"}
+    env["PYTHONPATH"] = root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and r.stdout.split() == ["1", "False"], r.stdout + r.stderr
+    env["HIP_FORCE_DEV_KERNARG"] = "0"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.stdout.split()[0] == "0", r.stdout + r.stderr

@@ -412,6 +412,9 @@ def test_rccl_env_injection_extension():
     pod = json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, json.dumps({"injectRcclEnv": True})))
     env = env_of(pod)
     assert env["LOCAL_RANK"] == "0" and env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # device-memory kernel arguments pinned in the pod (bench.py pins the same; +8.3 us/step
+    # with host-memory kernargs, profiles/r5_env/ab.txt)
+    assert env["HIP_FORCE_DEV_KERNARG"] == "1"
     assert "NCCL_MIN_NCHANNELS" not in env  # unmeasured tuning is not injected by default
     pod = json.loads(opcore().build_pod(json.dumps(job), "Worker", 0))
     assert "LOCAL_RANK" not in env_of(pod)
@@ -422,6 +425,12 @@ def test_rccl_env_injection_extension():
     env = env_of(json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, json.dumps(cfg))))
     assert env["NCCL_PROTO"] == "Simple" and env["NCCL_ALGO"] == "Ring"
     assert "HSA_ENABLE_IPC_MODE_LEGACY" not in env
+    assert env["HIP_FORCE_DEV_KERNARG"] == "1"  # not part of the replaceable RCCL set
+    # a template that chooses host-memory kernel arguments keeps its choice
+    job["spec"]["pytorchReplicaSpecs"]["Worker"]["template"]["spec"]["containers"][0]["env"] = [
+        {"name": "HIP_FORCE_DEV_KERNARG", "value": "0"}]
+    env = env_of(json.loads(opcore().build_pod(json.dumps(job), "Worker", 0, json.dumps(cfg))))
+    assert env["HIP_FORCE_DEV_KERNARG"] == "0"
 
 
 def _gpu_job(n_workers):

@@ -50,12 +50,17 @@ def test_env_file_reaches_the_operator(tmp_path):
     (comments and blank lines skipped, a malformed line refused with its line number)."""
     from pytorch_operator_amd.cluster.local import operator_binary
     out, env = tmp_path / "tune.json", tmp_path / "rccl.env"
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_tune.py"), "--nproc", "1", "--backend",
-                        "gloo", "--device", "cpu", "--candidates", "proto-LL", "--iters", "2", "--reps", "1",
-                        "--warmup", "1", "--out", str(out), "--env-out", str(env)],
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in env.read_text().splitlines() if ln and not ln.startswith("#")]
+    def tune(nproc):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_tune.py"), "--nproc", str(nproc),
+                            "--backend", "gloo", "--device", "cpu", "--candidates", "proto-LL", "--iters", "2",
+                            "--reps", "1", "--warmup", "1", "--out", str(out), "--env-out", str(env)],
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return r, [ln for ln in env.read_text().splitlines() if ln and not ln.startswith("#")]
+    # one rank: the ranking is noise, so no protocol is pinned -- only the base environment
+    r, lines = tune(1)
+    assert lines == ["HSA_ENABLE_IPC_MODE_LEGACY=0"] and "--nproc < 2" in r.stderr
+    r, lines = tune(2)
     assert lines == ["HSA_ENABLE_IPC_MODE_LEGACY=0", "NCCL_PROTO=LL"]
     bin_ = operator_binary()
     r = subprocess.run([bin_, "--inject-rccl-env", "--rccl-env-file", str(env), "--version"],
@@ -68,6 +73,13 @@ def test_env_file_reaches_the_operator(tmp_path):
     r = subprocess.run([bin_, "--rccl-env-file", str(tmp_path / "missing.env"), "--version"],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "cannot read" in (r.stderr + r.stdout)
+    # empty / comments-only: refused (it would drop HSA_ENABLE_IPC_MODE_LEGACY=0 from every pod)
+    for body in ("", "# nothing measured\n\n"):
+        empty = tmp_path / "empty.env"
+        empty.write_text(body)
+        r = subprocess.run([bin_, "--inject-rccl-env", "--rccl-env-file", str(empty), "--version"],
+                           capture_output=True, text=True)
+        assert r.returncode != 0 and "no KEY=VALUE" in (r.stderr + r.stdout), (body, r.stderr)
 
 
 def test_candidate_timeout_kills_its_job(tmp_path):

@@ -205,8 +205,17 @@ def main(argv=None) -> int:
     if args.env_out and "winner" in res:
         w = res["winner"]
         with open(args.env_out, "w") as f:
-            f.write(f"# tools/rccl_tune.py winner {w['name']} ({w['step_us']} us per step, {res['nproc']} ranks)\n")
-            for k, v in sorted({**BASE_ENV, **w["env"]}.items()):
+            if args.nproc < 2:
+                # one rank: the all-reduce is a local copy, so the ranking is noise -- such a file
+                # must not pin NCCL_PROTO/NCCL_ALGO for multi-GPU jobs; only the base set is written
+                print("rccl_tune: --nproc < 2, the winner is not a measurement; --env-out gets the "
+                      "base environment only", file=sys.stderr)
+                f.write(f"# tools/rccl_tune.py at {res['nproc']} rank: no protocol measured, base environment only\n")
+                env = dict(BASE_ENV)
+            else:
+                f.write(f"# tools/rccl_tune.py winner {w['name']} ({w['step_us']} us per step, {res['nproc']} ranks)\n")
+                env = {**BASE_ENV, **w["env"]}
+            for k, v in sorted(env.items()):
                 f.write(f"{k}={v}\n")
     print(json.dumps(res.get("winner", {"error": "no candidate ran"})))
     return 0 if "winner" in res else 1
