@@ -50,33 +50,50 @@ def _pool_at(r: torch.Tensor, code: torch.Tensor) -> torch.Tensor:
     return win.gather(4, code.view(B, C, H // 2, W // 2, 1).long()).squeeze(4)
 
 
-class ArgmaxAlignedNet(Net):
-    """``Net`` whose two max-pools take their argmax from given codes (the HIP kernels' idx1 /
-    idx2 of the same step); every other op -- convs, ReLU, linears, log-softmax, and through the
-    caller NLL, DDP averaging and SGD -- is torch's own fp32.
+class DecisionAlignedNet(Net):
+    """``Net`` whose discontinuous decisions -- the two max-pool argmaxes and the three ReLU
+    masks -- are taken from the HIP step that ran on the same batch (its idx1 / idx2 codes and
+    the signs of its a1, a2 and h); every value is torch's own fp32 arithmetic (convs, linears,
+    log-softmax, and through the caller NLL, DDP averaging and SGD).
 
-    Why: a pool window whose two largest values lie within fp32 rounding of each other has no
-    stable argmax.  The HIP convs sum in a different order than torch's, so such a window may
-    route its gradient to the other element -- a legitimate max, but a different trajectory
-    (tools/dbg/grad_diag.py found one per few dozen synthetic batches, moving conv grads by
-    ~5e-3).  ``forward`` also records in ``self.pool_gap`` the largest amount by which torch's
-    own window maximum exceeds the value at the given argmax (relative to the layer's
-    magnitude): ~1e-6 means every given argmax IS a maximum up to rounding."""
+    Why: an argmax between two values within fp32 rounding of each other, or a ReLU input within
+    rounding of 0, has no stable decision.  The HIP kernels sum in another order than torch, so
+    such a point may go either way -- a different but equally valid gradient, and from then on a
+    different trajectory (tools/dbg/grad_diag.py: one flipped conv2 pool window moved the conv
+    grads of a batch by 6e-3; fc1 ReLU flips move dW_fc1 rows by O(1/B)).
 
-    def forward(self, x, idx1=None, idx2=None):
+    ``forward`` records in ``self.decision_gap`` how far torch's own numbers are from every
+    decision it was given (relative to the layer's magnitude): torch's window maximum minus its
+    value at the given argmax, and |pre-activation| wherever the given ReLU mask disagrees with
+    torch's sign.  ~1e-6 means every given decision is torch's own up to rounding."""
+
+    def forward(self, x, idx1=None, idx2=None, m1=None, m2=None, mh=None):
         if idx1 is None:
             return super().forward(x)
-        r1 = F.relu(self.conv1(x))
-        p1 = _pool_at(r1, idx1)
-        r2 = F.relu(self.conv2(p1))
-        p2 = _pool_at(r2, idx2.view(-1, 50, 4, 4))
+        B = x.shape[0]
+        z1 = self.conv1(x)
+        q1 = _pool_at(z1, idx1)                     # pre-activation at the chosen element
+        p1 = q1 * m1.view_as(q1) if m1 is not None else F.relu(q1)
+        z2 = self.conv2(p1)
+        q2 = _pool_at(z2, idx2.view(B, 50, 4, 4))
+        p2 = q2 * m2.view_as(q2) if m2 is not None else F.relu(q2)
+        zh = self.fc1(p2.reshape(B, 800))
+        h = zh * mh if mh is not None else F.relu(zh)
         with torch.no_grad():
             gap = 0.0
-            for r, p in ((r1, p1), (r2, p2)):
-                m = F.max_pool2d(r, 2, 2)
-                gap = max(gap, float((m - p).max() / m.abs().max().clamp_min(1e-30)))
-            self.pool_gap = max(getattr(self, "pool_gap", 0.0), gap)
-        h = F.relu(self.fc1(p2.reshape(-1, 800)))
+            for z, q, m in ((z1, q1, m1), (z2, q2, m2)):
+                mx = F.max_pool2d(z, 2, 2)  # relu and max commute: the window max pre-activation
+                scale = float(mx.abs().max().clamp_min(1e-30))
+                g = float((F.relu(mx) - F.relu(q)).max()) / scale
+                if m is not None:
+                    bad = (q > 0) != m.view_as(q).bool()
+                    g = max(g, float(q[bad].abs().max()) / scale if bad.any() else 0.0)
+                gap = max(gap, g)
+            if mh is not None:
+                bad = (zh > 0) != mh.bool()
+                if bad.any():
+                    gap = max(gap, float(zh[bad].abs().max() / zh.abs().max().clamp_min(1e-30)))
+            self.decision_gap = max(getattr(self, "decision_gap", 0.0), gap)
         return F.log_softmax(self.fc2(h), dim=1)
 
 

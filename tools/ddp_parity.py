@@ -7,11 +7,12 @@ Every rank builds three replicas of the reference MNIST job on the same per-rank
 
 * ``torch``: ``DistributedDataParallel(Net())`` + ``torch.optim.SGD(lr=0.01, momentum=0.5)`` in
   fp32 on the CPU -- the reference's wrapper and optimiser (examples/mnist/mnist.py:135-140),
-  whose constructor broadcasts rank 0's parameters.  The net is ``ArgmaxAlignedNet``: each
-  max-pool takes the argmax the HIP step chose for that window (a window whose top two values
-  are within fp32 rounding has no stable argmax, and a flipped choice sends a different
-  trajectory); ``pool_gap`` proves every such choice is torch's window maximum up to rounding,
-  and ``param_rel_torch_own_argmax`` reports the unaligned comparison as well;
+  whose constructor broadcasts rank 0's parameters.  The net is ``DecisionAlignedNet``: its two
+  max-pool argmaxes and three ReLU masks are the ones the HIP step took on that batch (a window
+  whose top two values, or a ReLU input within fp32 rounding of 0, has no stable decision, and a
+  flipped one sends a different trajectory); ``decision_gap`` proves every given decision is
+  torch's own up to rounding, and ``param_rel_torch_own_decisions`` reports the unaligned
+  comparison as well;
 * ``rccl``: ``FusedMnistTrainer`` + ``FlatGradAllReduce`` (two bucket all-reduces), run by the
   bench's runner (``GraphedStep(launch="stream")``);
 * ``xgmi``: ``FusedMnistTrainer`` + ``XgmiGradSync`` (the peer-memory exchange fused with SGD).
@@ -44,13 +45,13 @@ def main(argv=None) -> int:
     ap.add_argument("--tol", type=float, default=1e-4)
     ap.add_argument("--paths", default="rccl,xgmi")
     ap.add_argument("--gap-tol", type=float, default=1e-5,
-                    help="largest torch window max above the value at the HIP argmax (relative)")
+                    help="largest distance of torch's own numbers from a HIP decision (relative)")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
     import torch.nn.functional as F
     from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
-    from pytorch_operator_amd.models.mnist import ArgmaxAlignedNet, FusedMnistTrainer, _views, flat_layout
+    from pytorch_operator_amd.models.mnist import DecisionAlignedNet, FusedMnistTrainer, _views, flat_layout
     from pytorch_operator_amd.ops import mnist as K
     from pytorch_operator_amd.parallel.ddp import FlatGradAllReduce
     from pytorch_operator_amd.parallel.dist import init_from_env
@@ -83,14 +84,15 @@ def main(argv=None) -> int:
             raise SystemExit(f"unknown path {path}")
         runner = GraphedStep(tr, mode="graph", launch="stream")
         # one step at a time (the same recorded kernels as the bench's run(n)), keeping each
-        # step's pool argmax codes for the torch side
+        # step's decisions (pool argmax codes, ReLU masks) for the torch side
         codes = []
         if runner.internal_steps > 1:
-            raise SystemExit("more than one untimed preparation step: its argmax codes are lost")
+            raise SystemExit("more than one untimed preparation step: its decisions are lost")
 
         def keep():
             torch.cuda.synchronize(dev)
-            codes.append((tr.idx1[:B].cpu(), tr.idx2[:B].cpu()))
+            codes.append((tr.idx1[:B].cpu(), tr.idx2[:B].cpu(), (tr.a1[:B] > 0).cpu(), (tr.a2[:B] > 0).cpu(),
+                          (tr.h1[:B] > 0).cpu()))
         if runner.internal_steps:
             keep()
         while len(codes) < a.steps:
@@ -102,14 +104,14 @@ def main(argv=None) -> int:
         trained[path] = (tr, steps, runner.launch, getattr(tr.grad_sync, "xar", None), codes)
 
     # torch's DDP on the same per-rank batches (cursor t -> perm[t*B : (t+1)*B], wrapping):
-    # argmax-aligned (ArgmaxAlignedNet: each pool takes the HIP step's argmax, whose torch value is
-    # checked to be the window maximum up to rounding), and torch's own argmax for reference
+    # decision-aligned (DecisionAlignedNet: HIP's pool argmaxes and ReLU masks, each checked to be
+    # torch's own up to rounding), and torch's own decisions for reference
     xf, lab, perm = ds.float_images().cpu(), ds.labels.long().cpu(), ds.perm.long().cpu()
     n = perm.numel()
 
     def torch_ddp(codes, steps):
         torch.manual_seed(1 + rank)  # this rank's own init: only DDP's broadcast aligns the ranks
-        net = ArgmaxAlignedNet()
+        net = DecisionAlignedNet()
         ddp = torch.nn.parallel.DistributedDataParallel(net)
         opt = torch.optim.SGD(ddp.parameters(), lr=0.01, momentum=0.5)
         for t in range(steps):
@@ -119,23 +121,23 @@ def main(argv=None) -> int:
             F.nll_loss(ddp(*args), lab[idx]).backward()
             opt.step()
         return (dict(net.named_parameters()), {k: opt.state[q]["momentum_buffer"] for k, q in net.named_parameters()},
-                getattr(net, "pool_gap", 0.0))
+                getattr(net, "decision_gap", 0.0))
 
     worst = {}
     for path, (tr, steps, launch, xar, codes) in trained.items():
         ref_p, ref_m, gap = torch_ddp(codes, steps)
         own_p, _, _ = torch_ddp(None, steps)
-        row = {"steps": steps, "launch": launch, "argmax_aligned": True,
+        row = {"steps": steps, "launch": launch, "decisions_aligned": True,
                "param_rel": max(_rel(tr.params[k], ref_p[k]) for k in ref_p),
-               "pool_gap": gap,
-               "param_rel_torch_own_argmax": max(_rel(tr.params[k], own_p[k]) for k in own_p)}
+               "decision_gap": gap,
+               "param_rel_torch_own_decisions": max(_rel(tr.params[k], own_p[k]) for k in own_p)}
         if path == "rccl":  # the xGMI step keeps momentum only for the rank's own shard
             mv = _views(tr.flat_momentum, tr.layout)
             row["momentum_rel"] = max(_rel(mv[k], ref_m[k]) for k in ref_m)
         if xar is not None:
             row["kernel_error"] = int(xar.error())
         res[path] = row
-        for key in ("param_rel", "momentum_rel", "pool_gap"):
+        for key in ("param_rel", "momentum_rel", "decision_gap"):
             if key in row:
                 worst[f"{path}_{key}"] = row[key]
     # worst over ranks
@@ -145,7 +147,7 @@ def main(argv=None) -> int:
     res["worst_over_ranks"] = dict(zip(keys, [float(x) for x in v]))
     errs = torch.tensor([res[p].get("kernel_error", 0) for p in trained], dtype=torch.int64)
     dist.all_reduce(errs, op=dist.ReduceOp.MAX)
-    ok = all(x <= (a.gap_tol if k.endswith("pool_gap") else a.tol) for k, x in zip(keys, v.tolist())) and \
+    ok = all(x <= (a.gap_tol if k.endswith("decision_gap") else a.tol) for k, x in zip(keys, v.tolist())) and \
         int(errs.max()) == 0 and all(t[1] >= 10 for t in trained.values())
     res["all_ok"] = bool(ok)
     if rank == 0:

@@ -26,6 +26,11 @@ def main():
     src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cur)
     B = int(os.environ.get("B", "64"))
     tr = FusedMnistTrainer(batch_size=B, source=src)
+    # one per-sample-conv_bwd step first, so tr.dz2 holds a real dense dz2 for the conv_bwd row
+    # (the default conv_chunk 4 step writes the pooled d(a2) into tr.dpool instead)
+    tr.conv_chunk = 1
+    tr.train_step()
+    tr.conv_chunk = 4
     for _ in range(20):
         tr.train_step()
     torch.cuda.synchronize()
@@ -33,6 +38,15 @@ def main():
     p = tr.params
     lay = tr.layout
     ce = lay.conv_end
+    o2w, o2b = lay.offsets["fc2.weight"], lay.offsets["fc2.bias"]
+    fp, fm = tr.flat_params, tr.flat_momentum
+
+    def tail():  # as FusedMnistTrainer.train_step's tail_ call, lr 0 (parameters stay put)
+        K.tail_(tr.conv_slab, B, tr.conv_bucket(), fp[:ce], fm[:ce], lr=0.0, momentum=tr.momentum,
+                big=K.conv_bwd4_rows(B, lay.offsets),
+                w1=(tr.dh[:B], tr.a2[:B], fp[ce:o2w], fm[ce:o2w], None),
+                fc2=(tr.dlogits[:B], tr.h1[:B], tr.per_sample[:B], tr.stats, 1.0 / B,
+                     fp[o2w:o2b], fm[o2w:o2b], None, fp[o2b:], fm[o2b:], None))
     launches = [
         ("conv12_fwd", lambda: K.conv12_fwd(src, p["conv1.weight"], p["conv1.bias"],
                                             p["conv2.weight"], p["conv2.bias"], B, a1=tr.a1,
@@ -46,6 +60,7 @@ def main():
                                               out=tr.h_parts[:2 * B * 500].view(2, B, 500))),
         ("head_parts", lambda: tr._head(B)),
         ("fc1_bwd", lambda: tr._fc1_bwd(B, stage_adv=0)),
+        ("fc1_bwd_head", lambda: tr._fc1_bwd_head(B, stage_adv=0)),  # the default step's launch 3
         ("conv_bwd", lambda: K.conv_bwd(tr.dz2, p["conv2.weight"], tr.a1, tr.idx1, tr.xn,
                                         tr.slab_views["conv2.weight"], tr.slab_views["conv2.bias"],
                                         tr.slab_views["conv1.weight"], tr.slab_views["conv1.bias"],
@@ -55,11 +70,12 @@ def main():
         ("slab_red_sgd", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
                                                     tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
                                                     big=K.conv_bwd4_rows(B, lay.offsets))),
-        ("tail", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
-                                            tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
-                                            big=K.conv_bwd4_rows(B, lay.offsets),
-                                            extra=(tr.flat_params[ce:], tr.flat_grads[ce:],
-                                                   tr.flat_momentum[ce:]))),
+        ("slab_red_sgd_x", lambda: K.slab_reduce_sgd_(tr.conv_slab, B, tr.conv_bucket(), tr.flat_params[:ce],
+                                                      tr.flat_momentum[:ce], lr=0.0, momentum=0.5,
+                                                      big=K.conv_bwd4_rows(B, lay.offsets),
+                                                      extra=(tr.flat_params[ce:], tr.flat_grads[ce:],
+                                                             tr.flat_momentum[ce:]))),
+        ("tail", tail),  # the default step's launch 5, with the trainer's own arguments
     ]
     reps = 20
     for name, fn in launches:
