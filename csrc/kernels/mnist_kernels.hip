@@ -241,6 +241,13 @@ __device__ __forceinline__ void sgd4(float4& p, float4& m, const float4& g, cons
 constexpr int C2_RS = 16;
 constexpr int C2_CS = 200;
 constexpr int C2_WS = 514;
+// conv2 im2col image: channel c starts at c * C2_CS + 2 (c >> 2) (round 6).  C2_CS == 8 (mod 32)
+// puts the two channels of a conv2 A-operand read 8 banks apart (their 16 positions are two 8-wide
+// runs 16 apart); the extra 2 (c >> 2) spreads the conv1 epilogue's 16 channels x 2 columns over 32
+// distinct banks (with C2_CS alone: 4 channels per bank, 4-way store conflicts).  Model:
+// tools/lds_banks_fwd.py.
+constexpr int C2_IMG = 20 * C2_CS + 8;
+__device__ __forceinline__ constexpr int c2_ch(int c) { return c * C2_CS + 2 * (c >> 2); }
 
 template <int Q0, int Q1>
 __device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb) {
@@ -250,7 +257,7 @@ __device__ __forceinline__ f32x4 conv2_k_range(const float* Ab, const float* Bb)
     const int cj = q / 5, kh = q % 5;
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
-      const float av = Ab[cj * 4 * C2_CS + kh * C2_RS + kw];
+      const float av = Ab[cj * (4 * C2_CS + 2) + kh * C2_RS + kw];  // channel 4 cj + g: c2_ch
       const float bv = Bb[cj * 100 + kh * 5 + kw];
       if (kw & 1) acc1 = mfma16x16x4(av, bv, acc1);
       else acc0 = mfma16x16x4(av, bv, acc0);
@@ -265,6 +272,11 @@ constexpr int AB_NT = 1024;  // conv forward blocks: 16 waves, 4 per SIMD keep t
 // distinct banks per half-wave; the dense 28 gave 2-way conflicts (bank model: profiles/
 // r2_lds_banks.md)
 constexpr int AB_IRS = 44;
+// conv1 weights in LDS: 20 rows of 25 taps, W1R floats apart (26 == 26 mod 32: a weight-fragment read's
+// 16 channels x 2 taps on 32 distinct banks; the dense 25 gave 2-way conflicts), the 20 biases at W1B
+constexpr int W1R = 26;
+constexpr int W1B = 20 * W1R;
+static_assert(W1R == 26, "the conv1 weight staging store computes row * W1R + tap as tid + tid / 25");
 
 // conv2 implicit GEMM of one block: 4 position tiles x 4 K quarters (the 25
 // (ci-group, kh) rows split 6/7/6/6) over 16 waves; the quarters meet in LDS in a fixed
@@ -291,7 +303,7 @@ __device__ __forceinline__ f32x4 conv2_block(const float* in_s, const float* w_s
 __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
     const float* __restrict__ a1, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, u64* dbg) {
-  __shared__ float in_s[20 * C2_CS];
+  __shared__ float in_s[C2_IMG];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
   const int cg = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -306,7 +318,7 @@ __global__ __launch_bounds__(AB_NT) void conv2_fwd_pool_kernel(
     if (e < 2880) {
       const int c = e / 144, p = e - c * 144;
       const int y = p / 12, x = p - y * 12;
-      in_s[c * C2_CS + y * C2_RS + x] = src[e];
+      in_s[c2_ch(c) + y * C2_RS + x] = src[e];
     }
   }
 #pragma unroll
@@ -407,13 +419,13 @@ __device__ __forceinline__ void conv1_tasks(int t0, const float* img, const int 
     if (o10 > m) { m = o10; am = 2; }
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
-    in_s[i * C2_CS + py * C2_RS + px] = v;
+    in_s[c2_ch(i) + py * C2_RS + px] = v;
     id1_s[i * 144 + py * 12 + px] = (uint8_t)am;
   }
 }
 
 // Waves 7-15: two channel 0-15 tiles (as conv1_tasks<2>) and one channel 16-19 group -- 16 pooled
-// positions p = 16 G + lane / 4 on v_mfma_f32_4x4x1_16b_f32: block lane / 4 is one pooled position,
+// positions (two blocks of 4 rows x 2 columns, see below) on v_mfma_f32_4x4x1_16b_f32: block lane / 4 is one pooled position,
 // its 4 rows the 2x2 window (row 2 di + dj), its 4 columns the channels; the 25 taps are 25 K = 1
 // steps in tap order from zero, the fmaf chain of conv1_fwd_pool_kernel
 // (bit-identical).  The group's dependent chain is interleaved with the tiles' MFMAs (3-4 after
@@ -433,10 +445,14 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     ibs[u] = img + (2 * py + (e >> 1)) * AB_IRS + 8 * pq + 2 * wi + (e & 1);
   }
   const int q = lane & 3;
-  const int p4 = 16 * G + (lane >> 2);  // G < 9: p4 < 144
-  const int ph4 = p4 / 12, pw4 = p4 - ph4 * 12;
+  // the 8 pooled positions of a half-wave: one block of 4 pooled rows x 2 columns (18 blocks = the
+  // 12 x 12 positions; b = 2 G + half): their image windows then fall on 8 disjoint 4-bank runs for
+  // every tap (round 6; a run of 8 consecutive positions put rows 2 py and 2 py + 1 of
+  // neighbouring positions on the same banks -- 2-way conflicts on all 25 operand reads)
+  const int blk_ = 2 * G + (lane >> 5), pp = (lane >> 2) & 7;
+  const int ph4 = 4 * (blk_ / 6) + (pp >> 1), pw4 = 2 * (blk_ % 6) + (pp & 1);
   const float* ia = img + (2 * ph4 + (q >> 1)) * AB_IRS + 2 * pw4 + (q & 1);
-  const float* wb = w1s + (16 + q) * 25;
+  const float* wb = w1s + (16 + q) * W1R;
   float av[2][7], av4[25], bv4[25];
 #pragma unroll
   for (int st = 0; st < 7; ++st)
@@ -447,7 +463,7 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     av4[k] = ia[(k / 5) * AB_IRS + k % 5];
     bv4[k] = wb[k];
   }
-  const float bc4 = w1s[500 + 16 + q];
+  const float bc4 = w1s[W1B + 16 + q];
   __builtin_amdgcn_sched_barrier(0);
   f32x4 acc[2] = {zero4(), zero4()}, acc4 = zero4();
 #pragma unroll
@@ -469,7 +485,7 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     if (o10 > m) { m = o10; am = 2; }
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
-    in_s[i * C2_CS + py * C2_RS + px] = v;
+    in_s[c2_ch(i) + py * C2_RS + px] = v;
     id1_s[i * 144 + py * 12 + px] = (uint8_t)am;
   }
   {  // the group's epilogue
@@ -480,8 +496,8 @@ __device__ __forceinline__ void conv1_tiles2_group(int t0, int G, const float* i
     if (o10 > m) { m = o10; am = 2; }
     if (o11 > m) { m = o11; am = 3; }
     const float v = fmaxf(m, 0.f);
-    in_s[(16 + q) * C2_CS + ph4 * C2_RS + pw4] = v;
-    id1_s[(16 + q) * 144 + p4] = (uint8_t)am;
+    in_s[c2_ch(16 + q) + ph4 * C2_RS + pw4] = v;
+    id1_s[(16 + q) * 144 + ph4 * 12 + pw4] = (uint8_t)am;
   }
 }
 
@@ -494,9 +510,13 @@ __device__ __forceinline__ void conv12_store_w2(float* w_s, const float4 (&wq)[2
       const int j = e / 125, q = e - j * 125;
       float4 v = wq[k];
       if (cg * 16 + j >= 50) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      // lanes 8-15 of every 16 store their upper pair first: each ds_write_b64 of the 16 lanes then
+      // covers 32 distinct banks (dwords 4q, 4q + 1 of lanes 0-7 and 4q + 2, 4q + 3 of lanes 8-15)
       float2* d = reinterpret_cast<float2*>(w_s + j * C2_WS + q * 4);
-      d[0] = make_float2(v.x, v.y);
-      d[1] = make_float2(v.z, v.w);
+      const int sw = (tid >> 3) & 1;
+      const float2 lo = make_float2(v.x, v.y), hi = make_float2(v.z, v.w);
+      d[sw] = sw ? hi : lo;
+      d[sw ^ 1] = sw ? lo : hi;
     }
   }
 }
@@ -508,8 +528,8 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     float* __restrict__ a2, uint8_t* __restrict__ idx2, int B, const uint8_t* __restrict__ stg_x,
     const int* __restrict__ stg_lab, const int* __restrict__ stg_tag, u64* dbg) {
   __shared__ float img[28 * AB_IRS];
-  __shared__ float w1s[520];
-  __shared__ __align__(16) float in_s[20 * C2_CS];
+  __shared__ float w1s[W1B + 20];
+  __shared__ __align__(16) float in_s[C2_IMG];
   __shared__ float w_s[16 * C2_WS];
   __shared__ f32x4 red[3][4][64];
   __shared__ __align__(16) uint8_t id1_s[20 * 144];  // conv1 pool argmax (published per channel group)
@@ -550,8 +570,8 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
       wq[k] = reinterpret_cast<const float4*>(w + (size_t)co * 500)[q];
     }
     if (tid < 784) img[(tid / 28) * AB_IRS + tid % 28] = x0;
-    if (tid < 500) w1s[tid] = wv;
-    if (tid < 20) w1s[500 + tid] = bv1;
+    if (tid < 500) w1s[tid + tid / 25] = wv;  // (tid / 25) * W1R + tid % 25 with W1R = 26
+    if (tid < 20) w1s[W1B + tid] = bv1;
     conv12_store_w2(w_s, wq, cg, tid);
     if (pub && tid < 784) {
       xn_out[(size_t)b * 784 + tid] = x0;
@@ -576,10 +596,10 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
       const int tap = 4 * s + g;
       const int tc = tap < 25 ? tap : 24;
       toff[s] = (tc / 5) * AB_IRS + (tc % 5);
-      const float wv_ = w1s[i * 25 + tc];
+      const float wv_ = w1s[i * W1R + tc];
       bw[s] = tap < 25 ? wv_ : 0.f;
     }
-    const float bc = w1s[500 + i];
+    const float bc = w1s[W1B + i];
     __builtin_amdgcn_sched_barrier(0);  // weight fragments in registers before the tasks
     if (wv >= 7) conv1_tiles2_group(wv, wv - 7, img, w1s, toff, bw, bc, in_s, id1_s, lane);
     else conv1_tasks<2>(wv, img, toff, bw, bc, in_s, id1_s, i, g);
@@ -602,8 +622,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
     const int e = tid - 256;
     if (e < 180) {  // 5 channels x 12 rows x 3 float4
       const int c = 5 * cg + e / 36, rem = e - (e / 36) * 36, py = rem / 3, k = rem - py * 3;
-      *reinterpret_cast<float4*>(a1 + (size_t)b * 2880 + c * 144 + py * 12 + 4 * k) =
-          *reinterpret_cast<const float4*>(in_s + c * C2_CS + py * C2_RS + 4 * k);
+      const float2* s2 = reinterpret_cast<const float2*>(in_s + c2_ch(c) + py * C2_RS + 4 * k);  // 8-B aligned
+      const float2 u0 = s2[0], u1 = s2[1];
+      *reinterpret_cast<float4*>(a1 + (size_t)b * 2880 + c * 144 + py * 12 + 4 * k) = make_float4(u0.x, u0.y, u1.x, u1.y);
     } else if (e < 225) {
       reinterpret_cast<uint4*>(idx1 + (size_t)b * 2880 + 720 * cg)[e - 180] =
           reinterpret_cast<const uint4*>(id1_s + 720 * cg)[e - 180];
@@ -1138,12 +1159,28 @@ struct Fc1BwdHead {
   int* stage_lab;
   int* stage_tag;
 };
-constexpr int H_RS = 514;  // hs / w2s row stride: lane rows 2 banks apart -> conflict-free b32 reads
-constexpr int H_DS = 516;  // dhs row stride: 16-byte aligned rows for the dz2 job's b128 reads
+// LDS layouts (round 6; bank model and the round-5 layouts' conflicts: tools/lds_banks_fwd.py):
+//   hs / w2s  row r at r * H_RS, column c stored at c ^ (2 [r >= 8]).  H_RS == 4 (mod 32) puts rows
+//             4 apart 16 banks apart (the ReLU-mask reads: 4 sample rows x 16 columns per half-wave)
+//             and the XOR moves rows 8-15 two banks over (the logits operand reads: 16 rows x 2
+//             adjacent columns); 16-byte rows: one ds_write_b128 per staged float4 (the XOR swaps its
+//             halves).  Round 5 (514, no XOR): 2-way on the mask reads and the float2 stores.
+//   dhs       row r at r * H_DS (16-byte rows).  The dz2 job's ds_read_b128 (lanes (i, g): row i,
+//             chunks 16 wv + 4 g + q) stay 2-way (16 cycles per wave): no plain stride or row order
+//             avoids it.  Measured and rejected (profiles/r6_banks/ab.md): the 16-byte chunk XOR the
+//             row (conflict-free; per-lane address VALU on the 16 dh stores, +0.34 us in the phase)
+//             and K chunks 64 columns apart per wave (conflict-free; +26 LDS instructions per wave
+//             from lost read2/offset folding, +0.1 us).
+constexpr int H_RS = 516;
+constexpr int H_DS = 516;
+__device__ __forceinline__ int hsx(int row, int col) { return row * H_RS + (col ^ ((row >> 3) << 1)); }
+__device__ __forceinline__ int dsx(int row, int col) { return row * H_DS + col; }
+// float4 entry of staging pass q (0-3) for thread tid: rows 0-7 in passes 0-1, rows 8-15 in 2-3
+__device__ __forceinline__ int stage_e(int q, int tid) { return q < 2 ? tid + q * E_NT : 1000 + tid + (q - 2) * E_NT; }
 
 __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* dbg) {
-  __shared__ float hs[16 * H_RS];
-  __shared__ float w2s[16 * H_RS];
+  __shared__ __align__(16) float hs[16 * H_RS];
+  __shared__ __align__(16) float w2s[16 * H_RS];
   __shared__ __align__(16) float dhs[16 * H_DS];
   __shared__ f32x4 red[E_NW][64];
   __shared__ float dls[16][17];  // +1: the dh operand reads (8 sample rows per half-wave) hit 8 banks
@@ -1180,10 +1217,13 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
 
   // ---- loads, all issued before the first use: the 16 rows' fc1 partials and bias, W2, the W1
   // column slice of the dz2 job, its epilogue operands, labels and b2
+  // staged float4 entries e of the 16 h rows / 10 W2 rows (125 per row): passes 0-1 take rows 0-7
+  // (e < 1000), passes 2-3 rows 8-15, so hsx's swap of the float4 halves in rows 8-15 is a
+  // compile-time choice per pass (no per-lane select)
   float4 hq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int e = min(tid + q * E_NT, 1999), row = e / 125, c4 = e - row * 125;
+    const int e = min(stage_e(q, tid), 1999), row = e / 125, c4 = e - row * 125;
     const size_t o = (size_t)min(mt * 16 + row, B - 1) * 500 + 4 * c4;
     const float4 x0 = *reinterpret_cast<const float4*>(a.hp0 + o);
     const float4 x1 = *reinterpret_cast<const float4*>(a.hp1 + o);
@@ -1194,7 +1234,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   }
   float4 wq[3];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) wq[q] = reinterpret_cast<const float4*>(a.w2)[min(tid + q * E_NT, 1249)];
+  for (int q = 0; q < 3; ++q) wq[q] = reinterpret_cast<const float4*>(a.w2)[min(stage_e(q, tid), 1249)];
   const int kb = 64 * wv + 16 * g;  // the dz2 job's K range of this lane
   float bv[16];
 #pragma unroll
@@ -1216,28 +1256,27 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   // ---- h and W2 into LDS (zero rows / columns pad K to 512 and N to 16)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int e = tid + q * E_NT;
-    if (e < 2000) {
+    const int e = stage_e(q, tid);
+    if (e < (q < 2 ? 1000 : 2000)) {
       const int row = e / 125, c4 = e - row * 125;
       const bool rv = mt * 16 + row < B;
       const float4 h4 = rv ? hq[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float2* d = reinterpret_cast<float2*>(hs + row * H_RS + 4 * c4);
-      d[0] = make_float2(h4.x, h4.y);
-      d[1] = make_float2(h4.z, h4.w);
+      *reinterpret_cast<float4*>(hs + row * H_RS + 4 * c4) =
+          q >= 2 ? make_float4(h4.z, h4.w, h4.x, h4.y) : h4;  // hsx: columns ^ 2 in rows 8-15
       if (pub && rv) reinterpret_cast<float4*>(a.h_out + (size_t)(mt * 16 + row) * 500)[c4] = h4;
     }
   }
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const int e = tid + q * E_NT;
-    if (e < 1250) {
+    const int e = stage_e(q, tid);
+    if (e < (q < 2 ? 1000 : 1250)) {
       const int row = e / 125, c4 = e - row * 125;
-      float2* d = reinterpret_cast<float2*>(w2s + row * H_RS + 4 * c4);
-      d[0] = make_float2(wq[q].x, wq[q].y);
-      d[1] = make_float2(wq[q].z, wq[q].w);
+      const float4 w4 = wq[q];
+      *reinterpret_cast<float4*>(w2s + row * H_RS + 4 * c4) =
+          q >= 2 ? make_float4(w4.z, w4.w, w4.x, w4.y) : w4;
     }
   }
-  for (int e = tid; e < 16 * 12; e += E_NT) {  // columns 500..511 of every row
+  for (int e = tid; e < 16 * 12; e += E_NT) {  // columns 500..511 of every row (a set closed under the XOR)
     const int row = e / 12, c = 500 + e % 12;
     hs[row * H_RS + c] = 0.f;
     w2s[row * H_RS + c] = 0.f;
@@ -1248,8 +1287,8 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
 
   // ---- logits partials: wave wv sums k in [64 wv, 64 wv + 64)
   {
-    const float* ha = hs + i * H_RS + 64 * wv + g;
-    const float* wb = w2s + i * H_RS + 64 * wv + g;
+    const float* ha = hs + hsx(i, 64 * wv + g);   // + 4 s: the XOR touches only column bit 1
+    const float* wb = w2s + hsx(i, 64 * wv + g);
     float av[16], wvv[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) { av[s] = ha[4 * s]; wvv[s] = wb[4 * s]; }
@@ -1315,12 +1354,12 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
     for (int c = 0; c < 10; ++c) {
       da[c] = dls[4 * g + (lane & 3)][c];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) db[t][c] = w2s[c * H_RS + 64 * wv + 16 * t + i];
+      for (int t = 0; t < 4; ++t) db[t][c] = w2s[hsx(c, 64 * wv + 16 * t + i)];
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hm[t][r] = hs[(4 * g + r) * H_RS + 64 * wv + 16 * t + i];
+      for (int r = 0; r < 4; ++r) hm[t][r] = hs[hsx(4 * g + r, 64 * wv + 16 * t + i)];
     __builtin_amdgcn_sched_barrier(0);  // operands and ReLU masks in registers first
     float dv[4][4];
 #pragma unroll
@@ -1331,7 +1370,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dv[t][r] = hm[t][r] > 0.f ? c[r] : 0.f;
-        dhs[(4 * g + r) * H_DS + 64 * wv + 16 * t + i] = dv[t][r];
+        dhs[dsx(4 * g + r, 64 * wv + 16 * t + i)] = dv[t][r];
       }
     }
   }
@@ -1344,11 +1383,10 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // ---- dz2 job (fc1_bwd's job 2): K = 500 split over the waves; this wave reads only the dh it wrote
   {
-    const float4* dr = reinterpret_cast<const float4*>(dhs + i * H_DS + kb);
     float av[16];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 d4 = dr[q];
+      const float4 d4 = *reinterpret_cast<const float4*>(dhs + dsx(i, kb + 4 * q));
       av[4 * q] = d4.x; av[4 * q + 1] = d4.y; av[4 * q + 2] = d4.z; av[4 * q + 3] = d4.w;
     }
     f32x4 c0 = zero4(), c1 = zero4();
@@ -1370,7 +1408,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
       const int e = lane + 64 * it, row = e >> 4, col = 64 * wv + 4 * (e & 15);
       if (col < 500 && mt * 16 + row < B)
         *reinterpret_cast<float4*>(a.dh_out + (size_t)(mt * 16 + row) * 500 + col) =
-            *reinterpret_cast<const float4*>(dhs + row * H_DS + col);
+            *reinterpret_cast<const float4*>(dhs + dsx(row, col));
     }
   }
   __syncthreads();
