@@ -44,6 +44,7 @@
 #include <atomic>
 
 #include "pto_common.h"
+#include "mnist_fc_grads.h"
 
 using namespace pto;
 
@@ -170,40 +171,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_pool_kernel(
 //   The two K halves meet in LDS; the 2x2 pool window = 2 registers of this
 //   lane x 2 registers of lane^32.
 // ---------------------------------------------------------------------------
-// Sum over the 64 lanes, every lane the same bits: quad xor 1 and 2 and the row half-mirror /
-// mirror (DPP on the add), then v_permlane16_swap / v_permlane32_swap pairs (each step adds
-// two equal-size partial sums, a + b == b + a, so all lanes round identically).
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float wave_allsum_dpp(float x) {
-  x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
-  x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
-  x += dpp_f<0x141>(x);  // row_half_mirror
-  x += dpp_f<0x140>(x);  // row_mirror
-  {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
-  }
-  {
-    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
-  }
-  return x;
-}
-
-// Sum over the four 16-lane rows at this lane's row position (= x + shfl_xor 16, then + shfl_xor
-// 32, bit for bit): v_permlane16_swap / v_permlane32_swap pair sums instead of two ds_bpermute
-// round trips.
-__device__ __forceinline__ float sum_lane_rows(float x) {
-  {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    x = __uint_as_float(s[0]) + __uint_as_float(s[1]);
-  }
-  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
-}
+// wave_allsum_dpp / sum_lane_rows: mnist_fc_grads.h
 
 // Value of lane l + 32 for lanes l < 32 (v_permlane32_swap: one VALU op; __shfl_xor(v, 32)
 // lowers to an LDS ds_bpermute round trip).  Lanes >= 32 get an unspecified value.
@@ -2239,6 +2207,10 @@ struct TailW1 {
   float loss_scale;
   float *p2, *m2, *g2;    // fc2.weight [10][500] params / momentum / optional gradient
   float *pb2, *mb2, *gb2; // fc2.bias [10]
+  // grad_only (the DDP step over RCCL, round 6): store every gradient (g, g2, gb2, the slab
+  // reduction's gout) and touch no parameter or momentum -- the all-reduced buckets then feed
+  // one SGD launch
+  int grad_only;
 };
 constexpr int T_W1_BLOCKS = 1600 / 4;
 constexpr int T_FC2_BLOCKS = 32 / 4;
@@ -2252,47 +2224,33 @@ __device__ __forceinline__ void tail_fc2_tile(const TailW1& tw, int nt, int lane
   const int n = nt * 16 + i;
   const int ncl = min(n, 499);
   const bool do_stats = nt == 1 && tw.per_sample != nullptr && tw.stats != nullptr;
-  float ls = 0.f, cs = 0.f;
-  if (do_stats && lane < B) { ls = tw.per_sample[2 * lane]; cs = tw.per_sample[2 * lane + 1]; }
-  float pp[4], mm[4];
+  float ls = 0.f, cs = 0.f;  // the first 64 samples' statistics, in flight with the GEMM loads
+  if (do_stats) loss_stats_load(tw.per_sample, B, lane, ls, cs);
+  const bool upd = !tw.grad_only;
+  float pp[4] = {0.f, 0.f, 0.f, 0.f}, mm[4] = {0.f, 0.f, 0.f, 0.f};
+  if (upd) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = min(g * 4 + r, 9);
-    pp[r] = tw.p2[j * 500 + ncl];
-    mm[r] = tw.m2[j * 500 + ncl];
+    for (int r = 0; r < 4; ++r) {
+      const int j = min(g * 4 + r, 9);
+      pp[r] = tw.p2[j * 500 + ncl];
+      mm[r] = tw.m2[j * 500 + ncl];
+    }
   }
   float bp = 0.f, bm = 0.f;
-  if (nt == 0 && g == 0) { bp = tw.pb2[jc]; bm = tw.mb2[jc]; }
-  f32x4 c0 = zero4(), c1 = zero4();
-  float dbsum = 0.f;
-  for (int base = 0; base < B; base += 64) {
-    float av[16], hv[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int bb = min(base + 4 * s + g, B - 1);
-      av[s] = tw.dlog[(size_t)bb * 10 + jc];
-      hv[s] = tw.h[(size_t)bb * 500 + ncl];
-    }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const bool bv = base + 4 * s + g < B;
-      const float x = (bv && i < 10) ? av[s] : 0.f;
-      dbsum += x;
-      const float hb = bv ? hv[s] : 0.f;
-      if (s & 1) c1 = mfma16x16x4(x, hb, c1);
-      else c0 = mfma16x16x4(x, hb, c0);
-    }
-  }
-  const f32x4 c = c0 + c1;
+  if (upd && nt == 0 && g == 0) { bp = tw.pb2[jc]; bm = tw.mb2[jc]; }
+  float dbsum;
+  const f32x4 c = fc2_wgrad_tile(tw.dlog, tw.h, B, nt, lane, dbsum);
   if (n < 500) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = g * 4 + r;
       if (j < 10) {
         if (tw.g2 != nullptr) tw.g2[j * 500 + n] = c[r];
-        sgd_elem(pp[r], mm[r], c[r], hy);
-        tw.p2[j * 500 + n] = pp[r];
-        tw.m2[j * 500 + n] = mm[r];
+        if (upd) {
+          sgd_elem(pp[r], mm[r], c[r], hy);
+          tw.p2[j * 500 + n] = pp[r];
+          tw.m2[j * 500 + n] = mm[r];
+        }
       }
     }
   }
@@ -2300,68 +2258,56 @@ __device__ __forceinline__ void tail_fc2_tile(const TailW1& tw, int nt, int lane
     dbsum = sum_lane_rows(dbsum);
     if (g == 0 && i < 10) {
       if (tw.gb2 != nullptr) tw.gb2[i] = dbsum;
-      sgd_elem(bp, bm, dbsum, hy);
-      tw.pb2[i] = bp;
-      tw.mb2[i] = bm;
+      if (upd) {
+        sgd_elem(bp, bm, dbsum, hy);
+        tw.pb2[i] = bp;
+        tw.mb2[i] = bm;
+      }
     }
   }
   if (do_stats) {
-    for (int bb = lane + 64; bb < B; bb += 64) { ls += tw.per_sample[2 * bb]; cs += tw.per_sample[2 * bb + 1]; }
-    ls = wave_allsum_dpp(ls);
-    cs = wave_allsum_dpp(cs);
+    loss_stats_finish(tw.per_sample, B, lane, ls, cs);
     if (lane == 0) { tw.stats[0] = ls * tw.loss_scale; tw.stats[1] = cs; }
   }
 }
 
 __device__ __forceinline__ void tail_w1_tile(const TailW1& tw, int tile, int lane, const SgdHyper& hy) {
   const int i = lane & 15, g = lane >> 4;
-  const int B = tw.B;
   const int nt = tile / 50, kt = tile - nt * 50;
-  const int n = nt * 16 + i, f = kt * 16 + i;
+  const int n = nt * 16 + i;
   const bool nv = n < 500;
   const int nc = nv ? n : 499;
   // parameters + momentum of this lane's four outputs, in flight with the GEMM operand loads
   const unsigned e4 = (unsigned)(nc * 200 + kt * 4 + g);
-  float4 pp = reinterpret_cast<const float4*>(tw.p)[e4];
-  float4 mm = reinterpret_cast<const float4*>(tw.m)[e4];
+  const bool upd = !tw.grad_only;
+  float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), mm = pp;
+  if (upd) {
+    pp = reinterpret_cast<const float4*>(tw.p)[e4];
+    mm = reinterpret_cast<const float4*>(tw.m)[e4];
+  }
   const bool bl = kt == 0 && g == 0;  // this lane also updates fc1.bias[n]
   float bp = 0.f, bm = 0.f;
-  if (bl) { bp = tw.p[400000 + nc]; bm = tw.m[400000 + nc]; }
-  f32x4 c0 = zero4(), c1 = zero4();
-  float dbsum = 0.f;
-  for (int base = 0; base < B; base += 64) {
-    float av[16], fv[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int bb = min(base + 4 * s + g, B - 1);
-      av[s] = tw.dh[(size_t)bb * 500 + nc];
-      fv[s] = tw.a2[(size_t)bb * 800 + f];
-    }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const bool bv = base + 4 * s + g < B;
-      const float x = (bv && nv) ? av[s] : 0.f;
-      dbsum += x;
-      const float fb = bv ? fv[s] : 0.f;
-      if (s & 1) c1 = mfma16x16x4(fb, x, c1);
-      else c0 = mfma16x16x4(fb, x, c0);
-    }
-  }
-  const f32x4 c = c0 + c1;
+  if (upd && bl) { bp = tw.p[400000 + nc]; bm = tw.m[400000 + nc]; }
+  float dbsum;
+  const f32x4 c = fc1_wgrad_tile(tw.dh, tw.a2, tw.B, nt, kt, lane, dbsum);
   if (nv) {
     const float4 gg = make_float4(c[0], c[1], c[2], c[3]);
     if (tw.g != nullptr) reinterpret_cast<float4*>(tw.g)[e4] = gg;
-    sgd4(pp, mm, gg, hy);
-    reinterpret_cast<float4*>(tw.p)[e4] = pp;
-    reinterpret_cast<float4*>(tw.m)[e4] = mm;
+    if (upd) {
+      sgd4(pp, mm, gg, hy);
+      reinterpret_cast<float4*>(tw.p)[e4] = pp;
+      reinterpret_cast<float4*>(tw.m)[e4] = mm;
+    }
   }
   if (kt == 0) {
     dbsum = sum_lane_rows(dbsum);
     if (bl && nv) {
       if (tw.g != nullptr) tw.g[400000 + n] = dbsum;
-      sgd_elem(bp, bm, dbsum, hy);
-      tw.p[400000 + n] = bp;
-      tw.m[400000 + n] = bm;
+      if (upd) {
+        sgd_elem(bp, bm, dbsum, hy);
+        tw.p[400000 + n] = bp;
+        tw.m[400000 + n] = bm;
+      }
     }
   }
 }
@@ -2406,7 +2352,7 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
   const int n4 = n >> 2;
   const int cc = min(col, n4 - 1);
   float4 pp = make_float4(0.f, 0.f, 0.f, 0.f), bb = pp;
-  if (tid < SR_COLS) {  // prefetch the parameters + momentum this column updates
+  if (tid < SR_COLS && !tw.grad_only) {  // prefetch the parameters + momentum this column updates
     pp = reinterpret_cast<const float4*>(p)[cc];
     bb = reinterpret_cast<const float4*>(buf)[cc];
   }
@@ -2418,9 +2364,11 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
 #pragma unroll
     for (int q = 1; q < SR_SL; ++q) add4(r, red[q][tid]);
     if (gout != nullptr) reinterpret_cast<float4*>(gout)[col] = r;
-    sgd4(pp, bb, r, hy);
-    reinterpret_cast<float4*>(p)[col] = pp;
-    reinterpret_cast<float4*>(buf)[col] = bb;
+    if (!tw.grad_only) {
+      sgd4(pp, bb, r, hy);
+      reinterpret_cast<float4*>(p)[col] = pp;
+      reinterpret_cast<float4*>(buf)[col] = bb;
+    }
   }
   if (step_counter != nullptr && blk == 0 && tid == 0) atomicAdd(step_counter, 1);
   stamp(dbg, 1);
@@ -2871,6 +2819,35 @@ int pto_mnist_tail(const float* P, int B, int n, int stride, float* gout, float*
   tw.p2 = p2w; tw.m2 = m2w; tw.g2 = g2w; tw.pb2 = pb2; tw.mb2 = mb2; tw.gb2 = gb2;
   hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
                      sr, n, stride, gout, p, buf, hy, step_counter, nullptr, nullptr, nullptr, 0, red_blocks, tw,
+                     dbg_next());
+  return (int)hipGetLastError();
+}
+
+// The fused-head step's gradients for DDP over RCCL (round 6): pto_mnist_tail's tiles and slab
+// reduction with every gradient stored and no parameter touched -- gout [n] (the conv bucket,
+// reduced from the slab), w1g [400000 + 500] (fc1.weight, fc1.bias), g2w [10][500], gb2 [10] (fc2)
+// and the loss statistics.  The step counter is left to the SGD launch after the all-reduces.
+int pto_mnist_tail_grads(const float* P, int B, int n, int stride, float* gout, int rows_big, int big_lo,
+                         int big_hi, const float* dh, const float* a2, float* w1g, const float* dlog,
+                         const float* h, const float* per_sample, float* stats, float loss_scale, float* g2w,
+                         float* gb2, void* stream) {
+  PTO_CHECK_B(B);
+  if (n <= 0 || (n & 3) || (stride & 3) || stride < n) return -1;
+  if (gout == nullptr || dh == nullptr || a2 == nullptr || w1g == nullptr || dlog == nullptr || h == nullptr ||
+      per_sample == nullptr || stats == nullptr || g2w == nullptr || gb2 == nullptr)
+    return -1;
+  if ((((uintptr_t)P) | ((uintptr_t)gout) | ((uintptr_t)w1g)) & 15) return -2;
+  SlabRows sr;
+  if (!slab_rows_ok(B, n, rows_big, big_lo, big_hi, sr)) return -1;
+  const int red_blocks = (n / 4 + SR_COLS - 1) / SR_COLS;
+  const int blocks = T_W1_BLOCKS + T_FC2_BLOCKS + red_blocks;
+  const SgdHyper hy{};
+  TailW1 tw{};
+  tw.dh = dh; tw.a2 = a2; tw.g = w1g; tw.B = B; tw.blocks = T_W1_BLOCKS + T_FC2_BLOCKS;
+  tw.fc2 = 1; tw.dlog = dlog; tw.h = h; tw.per_sample = per_sample; tw.stats = stats; tw.loss_scale = loss_scale;
+  tw.g2 = g2w; tw.gb2 = gb2; tw.grad_only = 1;
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, P,
+                     sr, n, stride, gout, nullptr, nullptr, hy, nullptr, nullptr, nullptr, nullptr, 0, red_blocks, tw,
                      dbg_next());
   return (int)hipGetLastError();
 }

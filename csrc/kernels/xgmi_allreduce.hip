@@ -48,6 +48,8 @@
 
 #include <cstring>
 
+#include "mnist_fc_grads.h"
+
 namespace {
 
 // clang vector type: element-wise arithmetic stays in VGPRs (HIP's f4 wrapper makes
@@ -92,6 +94,18 @@ struct XarArgs {
   // phase-2 timeout; a launch that starts degraded writes none (the failing one is kept)
   int stamp_ring;
   int light_fence;  // exchange buffers are uncached: no L2 writeback / invalidate needed
+  // fc_tiles (the fused DDP step, round 6): phase 1 also computes the fully connected layers'
+  // gradients on MFMA from the step's activations (mnist_fc_grads.h: dW_fc1 / db_fc1 from dh and
+  // a2, dW_fc2 / db_fc2 from d(logits) and h) and deposits them straight with their owners, and
+  // writes the step's loss statistics -- no producer launch stores or pushes them.  The fc range is
+  // the skip range [skip_lo4, n4); fc_*4: float4 offsets of fc1.weight / fc1.bias / fc2.weight /
+  // fc2.bias in the flat gradient.  An owner then waits for every sender block (the tiles of a
+  // chunk come from any block).
+  int fc_tiles, fc_B;
+  const float *fc_dh, *fc_a2, *fc_dlog, *fc_h, *fc_per_sample;
+  float* fc_stats;
+  float fc_loss_scale;
+  long fc_w1_4, fc_b1_4, fc_w2_4, fc_b2_4;
 };
 
 // Release before raising a flag / acquire after seeing one.  The exchange buffers are
@@ -240,6 +254,12 @@ __device__ bool wait_flag_ranges(const unsigned* f, int nblk, int world, const i
 // range needs no phase-1 data; it waits on sender block b's flag alone, which proves that
 // sender's exchange launch began, so its producer launch (and its pre-push) had finished.
 __device__ __forceinline__ void push_sources(const XarArgs& a, int b, int (&lo)[3], int (&hi)[3]) {
+  if (a.fc_tiles) {  // in-launch fc tiles: any sender block may feed any chunk
+    lo[0] = 0;
+    hi[0] = a.nblk;
+    lo[1] = hi[1] = lo[2] = hi[2] = 0;
+    return;
+  }
   const long c4 = a.slab != nullptr ? a.conv4 : 0;
   const long skip = a.skip_hi4 - a.skip_lo4;
   const long rest = a.npad4 - c4 - skip;
@@ -265,6 +285,68 @@ __device__ __forceinline__ void push_sources(const XarArgs& a, int b, int (&lo)[
   if (lo[0] == hi[0] && lo[1] == hi[1] && lo[2] == hi[2]) {
     lo[0] = b;
     hi[0] = b + 1;
+  }
+}
+
+// Phase 1's fc gradient tiles (XarArgs::fc_tiles): tile t of the 1600 dW_fc1 tiles (row tile t / 50,
+// column tile t % 50) then the 32 dW_fc2 tiles, one wave each, dealt round-robin over every wave of
+// every block.  Each lane deposits its 16-byte run of dW_fc1 as computed; db_fc1, dW_fc2 and db_fc2
+// run along rows whose four consecutive elements sit in lanes i .. i + 3, so lane i (i % 4 == 0)
+// gathers them (ds_bpermute) and deposits one float4.
+template <int NT>
+__device__ __forceinline__ void fc_tiles_phase1(const XarArgs& a, int b, bool degraded) {
+  constexpr int kWpb = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  if (b == a.nblk - 1) {
+    // the padding float4s inside the fc range (between / after the four tensors): zero, deposited
+    // like the rest -- an owner's receive slot keeps whatever was last written to it (the start-up
+    // self-test's data), and the padding would otherwise take SGD steps with that
+    const long gaps[4][2] = {{a.fc_w1_4 + 100000, a.fc_b1_4}, {a.fc_b1_4 + 125, a.fc_w2_4},
+                             {a.fc_w2_4 + 1250, a.fc_b2_4}, {a.fc_b2_4 + 3, a.n4}};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      for (long v = gaps[k][0] + tid; v < gaps[k][1]; v += NT) deposit(a, v, f4{0.f, 0.f, 0.f, 0.f}, degraded);
+  }
+  for (int t = b * kWpb + wv; t < 1632; t += a.nblk * kWpb) {  // wave-uniform
+    float dbsum;
+    if (t < 1600) {
+      const int nt = t / 50, kt = t - nt * 50;
+      const f4 c = pto::fc1_wgrad_tile(a.fc_dh, a.fc_a2, a.fc_B, nt, kt, lane, dbsum);
+      const int n = nt * 16 + i;
+      if (n < 500) deposit(a, a.fc_w1_4 + (long)(n * 200 + kt * 4 + g), c, degraded);
+      if (kt == 0) {
+        dbsum = pto::sum_lane_rows(dbsum);
+        const float d1 = __shfl_down(dbsum, 1, 64), d2 = __shfl_down(dbsum, 2, 64), d3 = __shfl_down(dbsum, 3, 64);
+        if (g == 0 && (i & 3) == 0 && n < 500) deposit(a, a.fc_b1_4 + n / 4, f4{dbsum, d1, d2, d3}, degraded);
+      }
+    } else {
+      const int nt = t - 1600;
+      const bool do_stats = nt == 1 && a.fc_stats != nullptr;
+      float ls = 0.f, cs = 0.f;
+      if (do_stats) pto::loss_stats_load(a.fc_per_sample, a.fc_B, lane, ls, cs);
+      const f4 c = pto::fc2_wgrad_tile(a.fc_dlog, a.fc_h, a.fc_B, nt, lane, dbsum);
+      const int n = nt * 16 + i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = c[r];
+        const float v1 = __shfl_down(v, 1, 64), v2 = __shfl_down(v, 2, 64), v3 = __shfl_down(v, 3, 64);
+        const int j = 4 * g + r;
+        if (j < 10 && (i & 3) == 0 && n < 500) deposit(a, a.fc_w2_4 + (long)(j * 500 + n) / 4, f4{v, v1, v2, v3}, degraded);
+      }
+      if (nt == 0) {
+        dbsum = pto::sum_lane_rows(dbsum);  // zero for classes >= 10: the padding float4 stays zero
+        const float d1 = __shfl_down(dbsum, 1, 64), d2 = __shfl_down(dbsum, 2, 64), d3 = __shfl_down(dbsum, 3, 64);
+        if (g == 0 && (i & 3) == 0 && i < 12) deposit(a, a.fc_b2_4 + i / 4, f4{dbsum, d1, d2, d3}, degraded);
+      }
+      if (do_stats) {
+        pto::loss_stats_finish(a.fc_per_sample, a.fc_B, lane, ls, cs);
+        if (lane == 0) {
+          a.fc_stats[0] = ls * a.fc_loss_scale;
+          a.fc_stats[1] = cs;
+        }
+      }
+    }
   }
 }
 
@@ -334,6 +416,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       g3 = ld(v0 + 3 * kThreads);
     };
     load_batch(lo4 + tid);
+    if (a.fc_tiles) fc_tiles_phase1<NT>(a, b, degraded);
     if (c4 > 0) {
       // conv segment: columns [b*per_c, (b+1)*per_c) reduced over the slab rows, split in
       // nsplit row groups (fixed order -> deterministic)
@@ -367,7 +450,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       if (v0 + 2 * kThreads < hi4) deposit(a, vmap(v0 + 2 * kThreads), g2, degraded);
       if (v0 + 3 * kThreads < hi4) deposit(a, vmap(v0 + 3 * kThreads), g3, degraded);
     }
-    if (degraded && skip > 0) {
+    if (degraded && skip > 0 && !a.fc_tiles) {
       // rank-local fallback: the pre-pushed range still needs its local SGD step (the
       // pushing launch also stored it to `in`); block b takes its share of it
       const long sper = (skip + a.nblk - 1) / a.nblk;
@@ -677,14 +760,10 @@ int pto_xar_allreduce(void* ctx, const float* in, float* out, float scale, void*
   return launch(c, a, stream);
 }
 
-// p, mbuf <- SGD(p, mean over ranks of grads) -- each rank updates its shard, then all gather.
-int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
-                          float dampening, float wd, float scale, int nesterov, int first_step,
-                          int* step_counter, const float* slab, int slab_rows, long slab_stride,
-                          long conv_n, int slab_rows_big, long big_lo, long big_hi, long skip_lo, long skip_hi,
-                          void* stream) {
-  XarCtx* c = static_cast<XarCtx*>(ctx);
-  XarArgs a{};
+static int prep_sgd(XarCtx* c, XarArgs& a, const float* grads, float* p, float* mbuf, float lr, float momentum,
+                    float dampening, float wd, float scale, int nesterov, int first_step, int* step_counter,
+                    const float* slab, int slab_rows, long slab_stride, long conv_n, int slab_rows_big, long big_lo,
+                    long big_hi, long skip_lo, long skip_hi) {
   a.mode = 1;
   if (skip_lo < 0 || skip_hi < skip_lo || skip_hi > c->n || (skip_lo & 3) || (skip_hi & 3) ||
       (skip_hi > skip_lo && skip_lo < (slab != nullptr ? conv_n : 0)))
@@ -718,6 +797,55 @@ int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, 
     a.conv4 = conv_n >> 2;
     if ((a.conv4 + c->nblk - 1) / c->nblk > kThreads) return -1;  // one column per thread
   }
+  return 0;
+}
+
+// p, mbuf <- SGD(p, mean over ranks of grads) -- each rank updates its shard, then all gather.
+int pto_xar_allreduce_sgd(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
+                          float dampening, float wd, float scale, int nesterov, int first_step,
+                          int* step_counter, const float* slab, int slab_rows, long slab_stride,
+                          long conv_n, int slab_rows_big, long big_lo, long big_hi, long skip_lo, long skip_hi,
+                          void* stream) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  XarArgs a{};
+  const int rc = prep_sgd(c, a, grads, p, mbuf, lr, momentum, dampening, wd, scale, nesterov, first_step, step_counter,
+                          slab, slab_rows, slab_stride, conv_n, slab_rows_big, big_lo, big_hi, skip_lo, skip_hi);
+  return rc != 0 ? rc : launch(c, a, stream);
+}
+
+// The fused DDP step's exchange (round 6): as pto_xar_allreduce_sgd with the conv slab, plus the
+// fully connected layers' gradients computed in phase 1 (XarArgs::fc_tiles) from dh [B][500], a2
+// [B][800], dlog [B][10], h [B][500] and the loss statistics from per_sample [B][2] into stats.
+// w1_off / b1_off / w2_off / b2_off: float offsets of fc1.weight, fc1.bias, fc2.weight, fc2.bias in the
+// flat gradient (multiples of 4; [w1_off, n) is the fc range, nothing of it is read from grads).
+int pto_xar_allreduce_sgd_fc(void* ctx, const float* grads, float* p, float* mbuf, float lr, float momentum,
+                             float dampening, float wd, float scale, int nesterov, int first_step, int* step_counter,
+                             const float* slab, int slab_rows, long slab_stride, long conv_n, int slab_rows_big,
+                             long big_lo, long big_hi, const float* dh, const float* a2, const float* dlog,
+                             const float* h, const float* per_sample, float* stats, float loss_scale, int B,
+                             long w1_off, long b1_off, long w2_off, long b2_off, void* stream) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  if (slab == nullptr || dh == nullptr || a2 == nullptr || dlog == nullptr || h == nullptr || B < 1 ||
+      ((w1_off | b1_off | w2_off | b2_off) & 3) || w1_off < conv_n || b1_off < w1_off + 400000 ||
+      w2_off < b1_off + 500 || b2_off < w2_off + 5000 || b2_off + 12 > c->n)
+    return -1;
+  XarArgs a{};
+  const int rc = prep_sgd(c, a, grads, p, mbuf, lr, momentum, dampening, wd, scale, nesterov, first_step, step_counter,
+                          slab, slab_rows, slab_stride, conv_n, slab_rows_big, big_lo, big_hi, w1_off, c->n);
+  if (rc != 0) return rc;
+  a.fc_tiles = 1;
+  a.fc_B = B;
+  a.fc_dh = dh;
+  a.fc_a2 = a2;
+  a.fc_dlog = dlog;
+  a.fc_h = h;
+  a.fc_per_sample = per_sample;
+  a.fc_stats = stats;
+  a.fc_loss_scale = loss_scale;
+  a.fc_w1_4 = w1_off >> 2;
+  a.fc_b1_4 = b1_off >> 2;
+  a.fc_w2_4 = w2_off >> 2;
+  a.fc_b2_4 = b2_off >> 2;
   return launch(c, a, stream);
 }
 

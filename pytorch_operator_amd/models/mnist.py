@@ -220,6 +220,11 @@ class FusedMnistTrainer:
         #   fuse_head (with w1_tail): fc1_bwd recomputes the head of its sample tile on MFMA (no
         #             head launch); dW_fc2 / db_fc2 / statistics move to the tail with their SGD
         self.fuse_head = os.environ.get("PTO_FUSE_HEAD", "1") != "0"
+        #   ddp_fused (world > 1, round 6): the DDP step on the same four forward/backward launches
+        #             plus a gradient tail (forward_backward_fused) -- over RCCL one all-reduce of
+        #             the whole flat gradient and one SGD launch; over xGMI the exchange computes the
+        #             fc gradients itself (five launches).  0: the round-5 forms (head + fc1_bwd)
+        self.ddp_fused = os.environ.get("PTO_DDP_FUSED", "1") != "0"
 
     # ---------------------------------------------------------------- state
     @property
@@ -409,6 +414,27 @@ class FusedMnistTrainer:
         self._conv_bwd(B)
         self.K.slab_reduce(self.conv_slab, B, self.conv_bucket(), big=self._slab_big(B))
 
+    def fused_ok(self) -> bool:
+        """The fused-head DDP forms apply (fc1 split-K 2: fc1_bwd_head's partial layout)."""
+        return self.ddp_fused and self.fc1_ks == 2
+
+    def forward_backward_fused(self, source=None, B: Optional[int] = None, stage_adv: int = 1) -> None:
+        """The DDP step's forward and backward on the world-1 step's kernels, every gradient stored
+        (five launches): conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head (+ staging of the batch of cursor +
+        ``stage_adv``) -> conv_bwd4 -> tail_grads (dW_fc1 / db_fc1 / dW_fc2 / db_fc2 tiles, the conv
+        slab reduction, the loss statistics).  Both buckets are complete when it returns."""
+        B = self.B if B is None else B
+        K, ce = self.K, self.layout.conv_end
+        o2w, o2b = self.layout.offsets["fc2.weight"], self.layout.offsets["fc2.bias"]
+        self.forward(source, B)
+        self._fc1_bwd_head(B, stage_adv=stage_adv)
+        self._conv_bwd(B)
+        K.tail_grads_(self.conv_slab, B, self.conv_bucket(), big=self._slab_big(B), dh=self.dh[:B], a2=self.a2[:B],
+                      fc1_grads=self.flat_grads[ce:o2w], dlogits=self.dlogits[:B], h=self.h1[:B],
+                      per_sample=self.per_sample[:B], stats=self.stats, loss_scale=1.0 / B,
+                      fc2w_grads=self.flat_grads[o2w:o2b], fc2b_grads=self.flat_grads[o2b:])
+        self._stale = ()
+
     def forward_backward(self, source=None, B: Optional[int] = None) -> None:
         """All fwd/bwd launches for one batch; grads land in flat_grads (DDP hooks fire)."""
         self.forward_backward_fc(source, B)
@@ -428,6 +454,27 @@ class FusedMnistTrainer:
     def train_step(self, source=None, B: Optional[int] = None, advance_cursor: bool = True):
         """One full training step (forward, backward, [all-reduce], SGD)."""
         B = self.B if B is None else B
+        if getattr(self.grad_sync, "fused_sgd", False) and self.fused_ok():
+            # xGMI, fused (five launches): conv12_fwd -> fc1_fwd<2> -> fc1_bwd_head -> conv_bwd4 ->
+            # the exchange, which computes dW_fc1 / db_fc1 / dW_fc2 / db_fc2 (and the loss
+            # statistics) itself, deposits them and the slab-reduced conv gradient with their
+            # owners, applies SGD to this rank's shard and all-gathers the parameters.  flat_grads
+            # is not written.
+            xar = self.grad_sync.xar
+            o = self.layout.offsets
+            self.forward(source, B)
+            self._fc1_bwd_head(B, stage_adv=1 if advance_cursor else 0)
+            self._conv_bwd(B)
+            xar.allreduce_sgd_fc_(
+                self.flat_grads, self._fp, self._fm, lr=self.lr, momentum=self.momentum,
+                dampening=self.dampening, weight_decay=self.weight_decay, nesterov=self.nesterov,
+                first_step=self._first_step, step_counter=self.cursor if advance_cursor else None,
+                slab=self.conv_slab, slab_rows=B, conv_n=self.layout.conv_end, slab_big=self._slab_big(B),
+                fc=(self.dh[:B], self.a2[:B], self.dlogits[:B], self.h1[:B], self.per_sample[:B], self.stats,
+                    1.0 / B, (o["fc1.weight"], o["fc1.bias"], o["fc2.weight"], o["fc2.bias"])))
+            self._first_step = False
+            self._stale = _CONV_NAMES + _FC_NAMES
+            return
         if getattr(self.grad_sync, "fused_sgd", False):
             # xGMI path: one kernel reduces the per-sample conv-grad slabs, does the
             # cross-GPU reduce-scatter, SGD on this rank's shard and the all-gather of the
@@ -452,6 +499,13 @@ class FusedMnistTrainer:
             self._stale = _CONV_NAMES + (("fc1.weight",) if push else ())
             return
         if self.grad_sync is not None:
+            if self.fused_ok():
+                # six launches + ONE all-reduce of the whole flat gradient (both buckets are complete
+                # at the same time, so one collective instead of two)
+                self.forward_backward_fused(source, B, stage_adv=1 if advance_cursor else 0)
+                self.grad_sync.all_ready(self.flat_grads)
+                self.optimizer_step(advance_cursor)
+                return
             self.forward_backward(source, B)
             self.optimizer_step(advance_cursor)
             return

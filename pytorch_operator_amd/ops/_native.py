@@ -140,6 +140,7 @@ _SIGNATURES = {
     "pto_mnist_fc1_bwd_stage": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_mnist_tail": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _I, _I, _I]
                       + [_VP] * 9 + [_F] + [_VP] * 7,
+    "pto_mnist_tail_grads": [_VP, _I, _I, _I, _VP, _I, _I, _I] + [_VP] * 7 + [_F, _VP, _VP, _VP],
     "pto_mnist_fc1_bwd_head": [_VP] * 14 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_slab_reduce_sgd_w1": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                                _VP, _VP, _VP, _I, _I, _I, _I] + [_VP] * 6,
@@ -154,6 +155,8 @@ _SIGNATURES = {
     "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],
     "pto_xar_allreduce_sgd": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _I, _L, _L,
                               _I, _L, _L, _L, _L, _VP],
+    "pto_xar_allreduce_sgd_fc": [_VP, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _VP, _I, _L, _L,
+                                 _I, _L, _L] + [_VP] * 6 + [_F, _I, _L, _L, _L, _L, _VP],
     "pto_xar_push_info": [_VP, ctypes.POINTER(_VP), ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_L)],
     "pto_xar_destroy": [_VP],
     "pto_xar_emu_create": [_I, _L, _I, ctypes.c_double, _I, _I, ctypes.POINTER(_VP)],

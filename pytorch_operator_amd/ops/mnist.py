@@ -473,6 +473,37 @@ def tail_(slab: torch.Tensor, B: int, grads: torch.Tensor, params: torch.Tensor,
     _native.check(rc, "tail")
 
 
+def tail_grads_(slab: torch.Tensor, B: int, conv_grads: torch.Tensor, *, big: Optional[tuple], dh, a2,
+                fc1_grads: torch.Tensor, dlogits, h, per_sample, stats, loss_scale: float,
+                fc2w_grads: torch.Tensor, fc2b_grads: torch.Tensor) -> None:
+    """The fused-head step's gradients, stored (DDP over RCCL): ``tail_``'s dW_fc1 / db_fc1 and
+    dW_fc2 / db_fc2 tiles and its slab reduction into ``conv_grads``, the loss statistics -- no
+    parameter or momentum touched, no cursor advance (the SGD launch after the all-reduces does
+    both).  ``fc1_grads``: fc1.weight (400000) then fc1.bias (500), contiguous."""
+    lib = _native.load()
+    n = conv_grads.numel()
+    if conv_grads.dtype != torch.float32 or not conv_grads.is_contiguous():
+        raise ValueError("conv_grads must be contiguous fp32")
+    if slab.dtype != torch.float32 or not slab.is_contiguous() or slab.dim() != 2 or \
+            slab.shape[1] < n or slab.shape[0] < B:
+        raise ValueError("slab must be contiguous fp32 [>=B, >=n]")
+    _req(dh, (B, 500), torch.float32, "dh")
+    _req(a2, (B, 800), torch.float32, "a2")
+    _req(dlogits, (B, 10), torch.float32, "dlogits")
+    _req(h, (B, 500), torch.float32, "h")
+    _req(per_sample, (B, 2), torch.float32, "per_sample")
+    for t, nm, k in ((fc1_grads, "fc1 grads", 400500), (fc2w_grads, "fc2.weight grads", 5000),
+                     (fc2b_grads, "fc2.bias grads", 10), (stats, "stats", 2)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < k:
+            raise ValueError(f"{nm}: contiguous fp32 with >= {k} elements expected")
+    rb, lo, hi = big if big is not None else (B, 0, 0)
+    rc = lib.pto_mnist_tail_grads(slab.data_ptr(), B, n, slab.shape[1], conv_grads.data_ptr(), int(rb), int(lo),
+                                  int(hi), dh.data_ptr(), a2.data_ptr(), fc1_grads.data_ptr(), dlogits.data_ptr(),
+                                  h.data_ptr(), per_sample.data_ptr(), stats.data_ptr(), float(loss_scale),
+                                  fc2w_grads.data_ptr(), fc2b_grads.data_ptr(), _stream())
+    _native.check(rc, "tail_grads")
+
+
 def conv_bwd(dz2, w2, a1, idx1, xn, gw2, gb2, gw1, gb1, want_dz1=False,
              slab: Optional[torch.Tensor] = None):
     """conv2 weight/bias grads, dz1 (internal), conv1 weight/bias grads.

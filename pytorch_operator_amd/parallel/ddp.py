@@ -74,6 +74,11 @@ class FlatGradAllReduce:
     def conv_ready(self, t: torch.Tensor) -> None:
         self._launch(t)
 
+    def all_ready(self, t: torch.Tensor) -> None:
+        """The whole flat gradient at once (the fused step completes both buckets together): one
+        all-reduce instead of two."""
+        self._launch(t)
+
     def finish(self) -> float:
         for w in self._works:
             w.wait()

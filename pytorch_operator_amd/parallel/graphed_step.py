@@ -125,7 +125,8 @@ class GraphedStep:
         self.collectives = gs is not None and bool(getattr(gs, "active", self.world > 1))
         self._graph = None   # timed graph: steps_per_graph whole steps
         self._warm = None    # one whole step (warm-up of any length)
-        self._split = False  # RCCL three-graph step
+        self._split = False  # RCCL step in pieces with the collectives issued between them
+        self._fused = False  # the fused form's two pieces (trainer.fused_ok()) instead of three
         self.internal_steps = 0  # untimed steps taken while preparing the graphs
         self.launch = "graph"
         if mode == "eager":
@@ -182,8 +183,15 @@ class GraphedStep:
             inv = 1.0 / self.world
             self._split = True
             self.steps_per_graph = 1
-            pieces = (lambda: tr.forward_backward_fc(), lambda: tr.backward_conv(),
-                      lambda: tr.optimizer_step(grad_scale=inv))
+            if tr.fused_ok():
+                # fused form: one piece up to the complete gradient (five launches), ONE all-reduce
+                # of the whole flat gradient, the SGD launch
+                self._fused = True
+                pieces = (lambda: tr.forward_backward_fused(stage_adv=1),
+                          lambda: tr.optimizer_step(grad_scale=inv))
+            else:
+                pieces = (lambda: tr.forward_backward_fc(), lambda: tr.backward_conv(),
+                          lambda: tr.optimizer_step(grad_scale=inv))
             if native and launch == "stream":
                 # the three pieces launch only this library's kernels: record them natively
                 # and launch their kernel lists straight onto the stream (no ~8.6 us
@@ -191,22 +199,31 @@ class GraphedStep:
                 gs = [NativeGraph(f, tr.device) for f in pieces]
                 if all(g.stream_ok for g in gs):
                     self.launch = "stream"
-                    self._g1, self._g2, self._g3 = gs
+                    self._gs = gs
             if self.launch != "stream":
-                self._g1, self._g2, self._g3 = (_TorchGraph(_capture(f, tr.device)) for f in pieces)
+                self._gs = [_TorchGraph(_capture(f, tr.device)) for f in pieces]
         torch.cuda.synchronize(tr.device)
 
     def _split_steps(self, n: int) -> None:
         tr = self.tr
         sync = tr.grad_sync
         go = (lambda g: g.replay_stream(1)) if self.launch == "stream" else (lambda g: g.replay(1))
+        if self._fused:
+            g1, g3 = self._gs
+            for _ in range(n):
+                go(g1)
+                sync.all_ready(tr.flat_grads)
+                sync.finish()
+                go(g3)
+            return
+        g1, g2, g3 = self._gs
         for _ in range(n):
-            go(self._g1)
+            go(g1)
             sync.fc_ready(tr.fc_bucket())
-            go(self._g2)
+            go(g2)
             sync.conv_ready(tr.conv_bucket())
             sync.finish()
-            go(self._g3)
+            go(g3)
 
     def warm(self, n_steps: int) -> None:
         """``n_steps`` untimed steps of any count: whole replays of the timed graph first (a

@@ -126,6 +126,37 @@ class XgmiAllReduce:
             sp, int(slab_rows), int(stride), int(conv_n), int(big_rows), int(big_lo), int(big_hi),
             int(skip[0]) if skip else 0, int(skip[1]) if skip else 0, self._stream()), "pto_xar_allreduce_sgd")
 
+    def allreduce_sgd_fc_(self, grads: torch.Tensor, params: torch.Tensor, momentum_buf: torch.Tensor, *,
+                          lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
+                          nesterov: bool = False, first_step: bool = False,
+                          step_counter: Optional[torch.Tensor] = None, slab: torch.Tensor, slab_rows: int,
+                          conv_n: int, slab_big: Optional[tuple], fc: tuple) -> None:
+        """The fused DDP step's exchange: ``allreduce_sgd_`` with the conv slab, and the fully
+        connected layers' gradients computed inside the exchange from the step's activations --
+        ``fc = (dh [B,500], a2 [B,800], dlogits [B,10], h [B,500], per_sample [B,2], stats, loss_scale,
+        (fc1.weight, fc1.bias, fc2.weight, fc2.bias float offsets in the flat gradient))`` -- and
+        deposited straight with their owners; the loss statistics land in ``stats``.  Nothing of
+        the fc range is read from ``grads``."""
+        for t in (grads, params, momentum_buf):
+            self._check(t)
+        if not (slab.is_cuda and slab.dtype == torch.float32 and slab.is_contiguous() and slab.dim() == 2
+                and slab_rows <= slab.shape[0] and conv_n <= slab.shape[1]):
+            raise ValueError("slab must be a contiguous fp32 CUDA [rows, stride] tensor")
+        dh, a2, dlog, h, per_sample, stats, loss_scale, offs = fc
+        B = int(dh.shape[0])
+        for t, shape in ((dh, (B, 500)), (a2, (B, 800)), (dlog, (B, 10)), (h, (B, 500)), (per_sample, (B, 2))):
+            if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+                raise ValueError(f"fc operand must be contiguous fp32 CUDA {shape}")
+        sc = step_counter.data_ptr() if step_counter is not None else None
+        big_rows, big_lo, big_hi = slab_big if slab_big is not None else (max(1, slab_rows), 0, 0)
+        _native.check(self.lib.pto_xar_allreduce_sgd_fc(
+            self._ctx, grads.data_ptr(), params.data_ptr(), momentum_buf.data_ptr(), lr, momentum,
+            dampening, weight_decay, 1.0 / self.world, int(nesterov), int(first_step), sc,
+            slab.data_ptr(), int(slab_rows), int(slab.shape[1]), int(conv_n), int(big_rows), int(big_lo),
+            int(big_hi), dh.data_ptr(), a2.data_ptr(), dlog.data_ptr(), h.data_ptr(), per_sample.data_ptr(),
+            stats.data_ptr(), float(loss_scale), B, *[int(o) for o in offs], self._stream()),
+            "pto_xar_allreduce_sgd_fc")
+
     def push_info(self):
         """(bases, rank, world, shard4) for a producer kernel that pushes gradient float4s into
         their owners' receive buffers itself (``ops.mnist.fc1_bwd(xpush=...)``)."""
@@ -328,6 +359,9 @@ class XgmiGradSync:
         pass
 
     def conv_ready(self, t):
+        pass
+
+    def all_ready(self, t):
         pass
 
     def finish(self) -> float:

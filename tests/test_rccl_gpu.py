@@ -42,7 +42,10 @@ def test_rccl_forms_bit_identical_at_world1(tmp_path):
     assert all(v > 0 for v in res["issued"].values()), res
     for k in ("eager", "rccl", "rccl_graph"):
         assert res[f"{k}_vs_split_equal"], (k, res)
-    assert res["split_vs_six_equal"], res
+    # the default (fused) DDP form is the single-GPU five-launch step's kernels: bit-identical to it;
+    # the round-5 form (head launch + fc1_bwd) to the six-kernel step
+    assert res["ddp_form"] == "fused" and res["split_vs_fused_equal"], res
+    assert res["split_r5_vs_six_equal"], res
     assert res["fused_head_max_rel_diff_vs_six"] < 1e-5, res
     race = res["race"]
     assert race["rccl_ms_per_step"] > 0 and race["rccl_graph_ms_per_step"] > 0, race

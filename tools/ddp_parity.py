@@ -37,6 +37,23 @@ def _rel(a, b) -> float:
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
+def _run_path(entry, upto: int, B: int, dev) -> None:
+    """Step one replica to ``upto`` steps, one ``run(1)`` at a time (the same recorded kernels as the
+    bench's run(n)), keeping each step's decisions (pool argmax codes, ReLU masks) for the torch side."""
+    import torch
+    tr, runner, codes = entry
+
+    def keep():
+        torch.cuda.synchronize(dev)
+        codes.append((tr.idx1[:B].cpu(), tr.idx2[:B].cpu(), (tr.a1[:B] > 0).cpu(), (tr.a2[:B] > 0).cpu(),
+                      (tr.h1[:B] > 0).cpu()))
+    if not codes and runner.internal_steps:
+        keep()
+    while len(codes) < upto:
+        runner.run(1)
+        keep()
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
@@ -44,6 +61,8 @@ def main(argv=None) -> int:
     ap.add_argument("--dataset", type=int, default=2048)
     ap.add_argument("--tol", type=float, default=1e-4)
     ap.add_argument("--paths", default="rccl,xgmi")
+    ap.add_argument("--eager", action="store_true", help="eager train_step() calls instead of the bench's runner")
+    ap.add_argument("--interleave", action="store_true", help="(with --eager) step the paths' trainers in turn")
     ap.add_argument("--gap-tol", type=float, default=1e-5,
                     help="largest distance of torch's own numbers from a HIP decision (relative)")
     a = ap.parse_args(argv)
@@ -72,7 +91,7 @@ def main(argv=None) -> int:
         dist.broadcast(tr.flat_params, 0)  # DDP constructor semantics, as bench.py
         return tr
 
-    trained = {}
+    trained, runners = {}, {}
     for path in [p for p in a.paths.split(",") if p]:
         if path == "rccl":
             tr = hip_replica(FlatGradAllReduce())
@@ -82,22 +101,17 @@ def main(argv=None) -> int:
             tr = hip_replica(xg)
         else:
             raise SystemExit(f"unknown path {path}")
-        runner = GraphedStep(tr, mode="graph", launch="stream")
-        # one step at a time (the same recorded kernels as the bench's run(n)), keeping each
-        # step's decisions (pool argmax codes, ReLU masks) for the torch side
-        codes = []
+        runner = GraphedStep(tr, mode="eager" if a.eager else "graph", launch="stream")
         if runner.internal_steps > 1:
             raise SystemExit("more than one untimed preparation step: its decisions are lost")
-
-        def keep():
-            torch.cuda.synchronize(dev)
-            codes.append((tr.idx1[:B].cpu(), tr.idx2[:B].cpu(), (tr.a1[:B] > 0).cpu(), (tr.a2[:B] > 0).cpu(),
-                          (tr.h1[:B] > 0).cpu()))
-        if runner.internal_steps:
-            keep()
-        while len(codes) < a.steps:
-            runner.run(1)
-            keep()
+        runners[path] = (tr, runner, [])
+        if not a.interleave:
+            _run_path(runners[path], a.steps, B, dev)
+    if a.interleave:
+        for _ in range(a.steps):
+            for v in runners.values():
+                _run_path(v, len(v[2]) + 1, B, dev)
+    for path, (tr, runner, codes) in runners.items():
         steps = int(tr.cursor.item())
         if steps != len(codes):
             raise SystemExit(f"cursor {steps} != steps taken {len(codes)}")

@@ -11,9 +11,11 @@ are issued every step.  This runs, on one GPU, the forms the start-up race
 * eager steps with the collectives.
 
 Each trainer takes N steps from the same initial state; at world 1 the all-reduce is an exact
-identity, so params and momentum must equal (``torch.equal``) the split step without collectives
-and the six-kernel single-GPU step (head launch; the default five-launch step recomputes the head
-in fc1_bwd with another fp32 summation order and is reported as a relative difference).  Then the RCCL race runs (``choose_grad_sync`` without an xGMI
+identity, so params and momentum must equal (``torch.equal``) the split step without collectives,
+and that must equal the single-GPU step it is built from: the default (round 6) DDP form is the
+five-launch step's kernels plus a gradient tail and one SGD launch, bit-identical to the
+five-launch single-GPU step; the round-5 form (``ddp_fused`` off: head launch + fc1_bwd) is
+bit-identical to the six-kernel single-GPU step (head launch).  Then the RCCL race runs (``choose_grad_sync`` without an xGMI
 candidate) beside a timed six-kernel run of the same length: RCCL's single-rank floor.
 
     python tools/rccl_w1_check.py --out DIR      (writes DIR/rank0.json, exit 0 iff all equal)
@@ -61,9 +63,11 @@ def main(argv=None) -> int:
     six = trainer(None)                              # the single-GPU six-kernel step (head launch)
     six.fuse_head = False
     fused = trainer(None)                            # the five-launch step (head fused into fc1_bwd)
-    split = trainer(FlatGradAllReduce(force=False))  # same split kernels, collectives skipped
+    split = trainer(FlatGradAllReduce(force=False))  # the DDP step's kernels, collectives skipped
+    split_r5 = trainer(FlatGradAllReduce(force=False))
+    split_r5.ddp_fused = False                       # the round-5 DDP form: head + fc1_bwd, 7 launches
     eager = trainer(FlatGradAllReduce(force=True))
-    for tr in (six, fused, split, eager):
+    for tr in (six, fused, split, split_r5, eager):
         for _ in range(N):
             tr.train_step()
     forms = {"eager": eager}
@@ -75,11 +79,15 @@ def main(argv=None) -> int:
         forms[name] = tr
     torch.cuda.synchronize(dev)
     res["steps"] = N
-    res["cursors"] = {k: int(t.cursor.item()) for k, t in [("six", six), ("split", split), *forms.items()]}
+    res["cursors"] = {k: int(t.cursor.item()) for k, t in [("six", six), ("fused", fused), ("split", split),
+                                                           ("split_r5", split_r5), *forms.items()]}
+    res["ddp_form"] = "fused" if split.fused_ok() else "r5"
     res["issued"] = {k: t.grad_sync.issued for k, t in forms.items()}
 
     def same(x, y):
         return bool(torch.equal(x.flat_params, y.flat_params) and torch.equal(x.flat_momentum, y.flat_momentum))
+    res["split_vs_fused_equal"] = same(split, fused)
+    res["split_r5_vs_six_equal"] = same(split_r5, six)
     res["split_vs_six_equal"] = same(split, six)
     res["fused_head_max_rel_diff_vs_six"] = float((fused.flat_params - six.flat_params).abs().max() /
                                                  six.flat_params.abs().max())
@@ -99,7 +107,8 @@ def main(argv=None) -> int:
     rec["six_kernel_ms_per_step"] = round(t_six / a.trial_steps * 1e3, 4)
     res["race"] = rec
     res["picked"] = pick
-    ok = all(res["cursors"][k] == N for k in res["cursors"]) and res["split_vs_six_equal"] and all(
+    ok = all(res["cursors"][k] == N for k in res["cursors"]) and res["split_vs_fused_equal"] and \
+        res["split_r5_vs_six_equal"] and all(
         res[f"{k}_vs_split_equal"] for k in forms) and all(v > 0 for v in res["issued"].values()) and (
         rec.get("rccl_ms_per_step") is not None and rec.get("rccl_graph_ms_per_step") is not None)
     res["all_ok"] = bool(ok)
