@@ -353,7 +353,11 @@ __device__ __forceinline__ void fc_tiles_phase1(const XarArgs& a, int b, bool de
 constexpr int kP2 = 2;  // phase-2 elements per thread per batch
 constexpr int kP3 = 4;  // phase-3 float4s per thread per batch
 
-template <int NT>
+// FC: the fused DDP step's exchange (XarArgs::fc_tiles), a separate instantiation so the round-5
+// exchange keeps its register allocation (the tiles' operands raise it from 112 to 152 VGPRs --
+// what decides whether the step's kernels fit beside a spinning exchange when ranks share a GPU,
+// tests/test_kernel_resources.py)
+template <int NT, bool FC = false>
 __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   constexpr int kThreads = NT;
   __shared__ unsigned s_step;
@@ -416,7 +420,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       g3 = ld(v0 + 3 * kThreads);
     };
     load_batch(lo4 + tid);
-    if (a.fc_tiles) fc_tiles_phase1<NT>(a, b, degraded);
+    if constexpr (FC) fc_tiles_phase1<NT>(a, b, degraded);
     if (c4 > 0) {
       // conv segment: columns [b*per_c, (b+1)*per_c) reduced over the slab rows, split in
       // nsplit row groups (fixed order -> deterministic)
@@ -450,7 +454,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
       if (v0 + 2 * kThreads < hi4) deposit(a, vmap(v0 + 2 * kThreads), g2, degraded);
       if (v0 + 3 * kThreads < hi4) deposit(a, vmap(v0 + 3 * kThreads), g3, degraded);
     }
-    if (degraded && skip > 0 && !a.fc_tiles) {
+    if (degraded && skip > 0 && !FC) {
       // rank-local fallback: the pre-pushed range still needs its local SGD step (the
       // pushing launch also stored it to `in`); block b takes its share of it
       const long sper = (skip + a.nblk - 1) / a.nblk;
@@ -584,6 +588,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
 }
 
 __global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body<kThreads>(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel_fc(XarArgs a) { xar_body<kThreads, true>(a, blockIdx.x); }
 
 // Emulation of `world` ranks on ONE device in one launch (blockIdx.y = rank): all blocks
 // of all ranks are co-resident, so the protocol (and its latency floor over local HBM)
@@ -745,7 +750,10 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.stamp_ring = c->stamp_ring;
   a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
-  hipLaunchKernelGGL(xar_kernel, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
+  if (a.fc_tiles)
+    hipLaunchKernelGGL(xar_kernel_fc, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(xar_kernel, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -13,6 +13,14 @@ The reference synchronises gradients with DDP's bucketed all-reduce
                 step per kernel list.  ``xgmi_sync=None`` (no peer exchange: world 1 with forced
                 collectives, or a failed self-test) races the two RCCL forms alone.
 
+Each of ``rccl`` / ``rccl-graph`` / ``xgmi`` runs the round-6 fused DDP step (the single-GPU step's
+kernels with the gradient tail: 6 launches + one all-reduce over RCCL, 5 launches over xGMI with
+the fc gradients computed in the exchange).  ``rccl-r5`` and ``xgmi-r5`` race the round-5 forms
+beside them (head launch + fc1_bwd: the fc bucket's all-reduce overlaps the conv backward over
+RCCL; dW_fc1 pushed by fc1_bwd over xGMI): which one wins depends on the fabric's all-reduce
+latency and on whether ranks share CUs, so it is measured (``PTO_RACE_SKIP`` names candidates to
+leave out).
+
 Whether the xGMI kernel beats RCCL for this 1.7 MB gradient is a property of the fabric the job
 lands on, so it is measured rather than assumed: every candidate runs ``trial_steps`` real DDP
 steps (replicas stay identical), each trial is timed as the MAX over ranks, and every rank adopts
@@ -34,15 +42,21 @@ import torch.distributed as dist
 
 from .graphed_step import GraphedStep
 
-CANDIDATES = ("rccl", "rccl-graph", "xgmi")
+CANDIDATES = ("rccl", "rccl-graph", "xgmi", "rccl-r5", "xgmi-r5")
+
+
+def _skip_listed(name: str) -> bool:
+    return name in os.environ.get("PTO_RACE_SKIP", "").split(",")
 
 
 def _delay_ms(name: str) -> float:
+    """The fault-injection delay of candidate ``name``: an entry for ``k`` applies to ``k`` and to its
+    round-5 form ``k-r5`` (``xgmi:5`` slows both xGMI candidates, not ``rccl-graph``)."""
     spec = os.environ.get("PTO_RACE_DELAY_MS", "")
     for part in spec.split(","):
         if ":" in part:
             k, v = part.split(":", 1)
-            if k.strip() == name:
+            if name in (k.strip(), k.strip() + "-r5"):
                 return float(v)
     return 0.0
 
@@ -115,10 +129,28 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     if xgmi_sync is not None:
         xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
     tr.grad_sync = rccl_sync
+    fused = bool(getattr(tr, "fused_ok", lambda: False)())  # candidates without -r5: the fused form
+    forms = {k: (k.endswith("-r5") or not fused) for k in CANDIDATES}  # True: the round-5 form
+
+    def set_form(name):
+        tr.ddp_fused = not forms[name]
+
+    set_form("rccl")
     r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=1, launch=launch)
     runners["rccl"] = r
     times["rccl"] = _timed(r, trial, dev, "rccl")
     steps += r.internal_steps + trial
+    if not fused:
+        skipped["rccl-r5"] = "the trainer runs the round-5 form already (ddp_fused off)"
+    elif _skip_listed("rccl-r5"):
+        skipped["rccl-r5"] = "PTO_RACE_SKIP"
+    else:
+        set_form("rccl-r5")
+        r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=1, launch=launch)
+        runners["rccl-r5"] = r
+        times["rccl-r5"] = _timed(r, trial, dev, "rccl-r5")
+        steps += r.internal_steps + trial
+    set_form("rccl-graph")
     why = "eager race" if eager else graph_comm_precheck(tr)
     # every rank agrees on the pre-check before any rank issues the candidate's collectives
     if not _agree(why is None, dev):
@@ -157,13 +189,22 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
                 skipped.setdefault("rccl-graph", "capture failed")
     if xgmi_sync is None:
         skipped.setdefault("xgmi", "no xGMI exchange (world 1 or self-test failed)")
+        skipped.setdefault("xgmi-r5", skipped["xgmi"])
     else:
         tr.grad_sync = xgmi_sync
-        r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
-        runners["xgmi"] = r
-        t = _timed(r, trial, dev, "xgmi")
-        steps += r.internal_steps + trial
-        times["xgmi"] = float("inf") if xgmi_sync.xar.error() else t
+        for name in ("xgmi", "xgmi-r5"):
+            if name == "xgmi-r5" and not fused:
+                skipped[name] = "the trainer runs the round-5 form already (ddp_fused off)"
+                continue
+            if name == "xgmi-r5" and _skip_listed(name):
+                skipped[name] = "PTO_RACE_SKIP"
+                continue
+            set_form(name)
+            r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
+            runners[name] = r
+            t = _timed(r, trial, dev, name)
+            steps += r.internal_steps + trial
+            times[name] = float("inf") if xgmi_sync.xar.error() else t
     if force is not None:
         if force not in runners:
             raise ValueError(f"force={force!r}: candidate not available ({skipped.get(force, 'unknown')})")
@@ -177,17 +218,20 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
     if int(lo.item()) != int(hi.item()):
         pick = "rccl"  # ranks disagree (cannot happen with shared numbers): the safe path
-    if pick != "xgmi":
+    if not pick.startswith("xgmi"):
         if xgmi_sync is not None:
             xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
         tr.grad_sync = rccl_sync
+    else:
+        tr.grad_sync = xgmi_sync
+    set_form(pick)  # later eager steps of the trainer take the picked form too
     record = {f"{k.replace('-', '_')}_ms_per_step": (round(v / trial * 1e3, 4) if v != float("inf") else None)
               for k, v in times.items()}
     for k, why in skipped.items():
         record[f"{k.replace('-', '_')}_ms_per_step"] = None
         record[f"{k.replace('-', '_')}_skipped"] = why
-    if times.get("xgmi") == float("inf"):
+    if times.get("xgmi") == float("inf") or times.get("xgmi-r5") == float("inf"):
         record["xgmi_error"] = int(xgmi_sync.xar.error())
     record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,
-                   "steps": steps})
+                   "steps": steps, "ddp_form": "r5" if forms[pick] else "fused"})
     return runners[pick], pick, record

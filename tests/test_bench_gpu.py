@@ -100,8 +100,12 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
         assert trial["rccl_ms_per_step"] > 0 and trial["xgmi_ms_per_step"] > 0, trial
         assert trial["rccl_graph_ms_per_step"] is None and "gloo" in trial["rccl_graph_skipped"], trial
         assert line["config"]["grad_allreduce"] == trial["picked"], line
+        # both DDP forms of each path raced (round 6: fused, and the round-5 form as "-r5")
+        assert trial["rccl_r5_ms_per_step"] > 0 and trial["xgmi_r5_ms_per_step"] > 0, trial
+        assert trial["ddp_form"] == ("r5" if trial["picked"].endswith("-r5") else "fused"), trial
         if slow_xgmi:
-            assert trial["picked"] == "rccl" and trial["xgmi_ms_per_step"] > trial["rccl_ms_per_step"], trial
+            assert trial["picked"] in ("rccl", "rccl-r5"), trial
+            assert trial["xgmi_ms_per_step"] > trial["rccl_ms_per_step"], trial
             assert "launch=stream" in line["config"]["exec"], line
         # the operator-deployed pods ran the same race
         assert line["job"]["allreduce_trial"] is not None, line["job"]

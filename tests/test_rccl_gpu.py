@@ -50,7 +50,8 @@ def test_rccl_forms_bit_identical_at_world1(tmp_path):
     race = res["race"]
     assert race["rccl_ms_per_step"] > 0 and race["rccl_graph_ms_per_step"] > 0, race
     assert race["xgmi_ms_per_step"] is None and "world 1" in race["xgmi_skipped"], race
-    assert race["picked"] in ("rccl", "rccl-graph") and race["six_kernel_ms_per_step"] > 0, race
+    assert race["picked"] in ("rccl", "rccl-graph", "rccl-r5") and race["six_kernel_ms_per_step"] > 0, race
+    assert race["rccl_r5_ms_per_step"] > 0, race  # the round-5 form raced beside the fused one
     assert r.returncode == 0 and res["all_ok"], res
 
 

@@ -65,6 +65,8 @@ def main(argv=None) -> int:
     ap.add_argument("--fuse-conv12", type=int, default=-1,
                     help="1/0: force the fused conv12 forward on/off (default: off when ranks share a GPU at "
                          "256 workgroups, see below; 1 there reproduces the starvation)")
+    ap.add_argument("--ddp-form", default="auto", choices=["auto", "fused", "r5"],
+                    help="DDP step form (auto: fused unless the geometry is crowded, see below)")
     ap.add_argument("--bench", action="store_true",
                     help="time the fused exchange alone (graph of back-to-back launches)")
     a = ap.parse_args(argv)
@@ -111,6 +113,11 @@ def main(argv=None) -> int:
     res["crowded"] = crowded
     res["conv_chunk"] = 1 if crowded else 4
     res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not crowded
+    # crowded, the round-5 DDP form (head + fc1_bwd pushing dW_fc1, the 112-VGPR exchange): the fused
+    # form's exchange computes the fc tiles itself (152 VGPRs) and every owner waits for every sender
+    # block, so ranks whose exchanges spin on the CUs another rank's step needs time out (W = 4 at
+    # 128 workgroups each, profiles/r6_xgmi_geometry.md).  The job topology never shares CUs.
+    res["ddp_form"] = "r5" if (crowded if a.ddp_form == "auto" else a.ddp_form == "r5") else "fused"
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -119,6 +126,7 @@ def main(argv=None) -> int:
                                grad_sync=sync)
         tr.conv_chunk = res["conv_chunk"]
         tr.fuse_conv12 = res["fuse_conv12"]
+        tr.ddp_fused = res["ddp_form"] == "fused"
         dist.broadcast(tr.flat_params, 0)
         return tr
 
