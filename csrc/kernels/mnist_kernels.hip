@@ -2574,6 +2574,8 @@ int pto_mnist_fc1_fwd(const float* x, const float* w, const float* bias, float* 
 }
 
 int pto_mnist_fc1_ks() { return FC1_KS; }
+// conv_bwd4's dynamic LDS (bytes): not in the code object's metadata (tests/test_kernel_resources.py)
+int pto_mnist_conv_bwd4_lds() { return G_LDS * (int)sizeof(float); }
 
 // Split-K fc1: pre-activation partials to parts[KS][B][500] (head_kernel finishes h).
 int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, void* stream) {

@@ -350,14 +350,17 @@ __device__ __forceinline__ void fc_tiles_phase1(const XarArgs& a, int b, bool de
   }
 }
 
-constexpr int kP2 = 2;  // phase-2 elements per thread per batch
+constexpr int kP2 = 2;  // phase-2 elements per thread per batch (chunk4 > kThreads: xar_kernel_p2)
 constexpr int kP3 = 4;  // phase-3 float4s per thread per batch
 
 // FC: the fused DDP step's exchange (XarArgs::fc_tiles), a separate instantiation so the round-5
 // exchange keeps its register allocation (the tiles' operands raise it from 112 to 152 VGPRs --
 // what decides whether the step's kernels fit beside a spinning exchange when ranks share a GPU,
-// tests/test_kernel_resources.py)
-template <int NT, bool FC = false>
+// tests/test_kernel_resources.py).  P2: phase-2 float4s per thread per batch.  A chunk of at most
+// NT float4s (every chunk at 256 workgroups and world >= 2: 53 at world 8) needs one, and the
+// 8 senders' operands of a second batch are what held the exchange at 112 VGPRs: P2 = 1 brings it
+// under 96, so even the 4-wave fused conv12 forward (4 x 104) fits beside a spinning exchange wave.
+template <int NT, bool FC = false, int P2 = kP2>
 __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   constexpr int kThreads = NT;
   __shared__ unsigned s_step;
@@ -476,10 +479,10 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   {
     const long base4 = (long)a.rank * a.shard4 + (long)b * a.chunk4;
     const f4* rv = recv_buf(mine) + (long)b * a.chunk4;
-    f4 pp[kP2], bb[kP2];
+    f4 pp[P2], bb[P2];
     auto load_pb = [&](long i0) {  // parameters / momentum: independent of the peers
 #pragma unroll
-      for (int k = 0; k < kP2; ++k) {
+      for (int k = 0; k < P2; ++k) {
         const long i = i0 + (long)k * kThreads, v = base4 + i;
         const bool in = a.mode == 1 && i < a.chunk4 && v < a.n4;
         pp[k] = in ? reinterpret_cast<const f4*>(a.p)[v] : zero4;
@@ -505,23 +508,23 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
     for (long i0 = tid;;) {  // no barrier inside: threads may leave at different times
       // every sender's contribution in flight at once (clamped addresses, no predicated
       // load: a runtime-bounded loop here waited a full memory round trip per sender)
-      f4 rq[kP2][kMaxWorld];
+      f4 rq[P2][kMaxWorld];
 #pragma unroll
-      for (int k = 0; k < kP2; ++k) {
+      for (int k = 0; k < P2; ++k) {
         const long i = min(i0 + (long)k * kThreads, a.chunk4 - 1);
 #pragma unroll
         for (int q = 0; q < kMaxWorld; ++q) rq[k][q] = rv[(long)min(q, a.world - 1) * a.shard4 + i];
       }
-      f4 acc[kP2];
+      f4 acc[P2];
 #pragma unroll
-      for (int k = 0; k < kP2; ++k) {
+      for (int k = 0; k < P2; ++k) {
         acc[k] = rq[k][0];
 #pragma unroll
         for (int q = 1; q < kMaxWorld; ++q)
           if (q < a.world) acc[k] += rq[k][q];  // rank order (deterministic)
       }
 #pragma unroll
-      for (int k = 0; k < kP2; ++k) {
+      for (int k = 0; k < P2; ++k) {
         const long i = i0 + (long)k * kThreads, v = base4 + i;
         if (i >= a.chunk4) continue;
         f4 res;
@@ -543,7 +546,7 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
           push4(gath_buf(peer(a, q), a.npad4) + v, res);
         }
       }
-      i0 += (long)kP2 * kThreads;
+      i0 += (long)P2 * kThreads;
       if (i0 >= a.chunk4) break;
       load_pb(i0);
     }
@@ -587,8 +590,10 @@ __device__ __forceinline__ void xar_body(const XarArgs& a, const int b) {
   }
 }
 
-__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body<kThreads>(a, blockIdx.x); }
-__global__ __launch_bounds__(kThreads) void xar_kernel_fc(XarArgs a) { xar_body<kThreads, true>(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel(XarArgs a) { xar_body<kThreads, false, 1>(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel_p2(XarArgs a) { xar_body<kThreads, false, 2>(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel_fc(XarArgs a) { xar_body<kThreads, true, 1>(a, blockIdx.x); }
+__global__ __launch_bounds__(kThreads) void xar_kernel_fc_p2(XarArgs a) { xar_body<kThreads, true, 2>(a, blockIdx.x); }
 
 // Emulation of `world` ranks on ONE device in one launch (blockIdx.y = rank): all blocks
 // of all ranks are co-resident, so the protocol (and its latency floor over local HBM)
@@ -750,10 +755,9 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.stamp_ring = c->stamp_ring;
   a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
-  if (a.fc_tiles)
-    hipLaunchKernelGGL(xar_kernel_fc, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(xar_kernel, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
+  const bool one = a.chunk4 <= kThreads;  // phase 2 in one batch per thread
+  auto* k = a.fc_tiles ? (one ? xar_kernel_fc : xar_kernel_fc_p2) : (one ? xar_kernel : xar_kernel_p2);
+  hipLaunchKernelGGL(k, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -63,8 +63,10 @@ def main(argv=None) -> int:
                     help="record the hand-over exchange's per-workgroup phase stamps (XgmiAllReduce."
                          "enable_stamps) and write <out>/rank<r>_stamps.json (tools/xgmi_stamps.py reads them)")
     ap.add_argument("--fuse-conv12", type=int, default=-1,
-                    help="1/0: force the fused conv12 forward on/off (default: off when ranks share a GPU at "
-                         "256 workgroups, see below; 1 there reproduces the starvation)")
+                    help="1/0: force the fused conv12 forward on/off (default: off when the other ranks on "
+                         "this GPU can hold two exchange waves per SIMD, see below)")
+    ap.add_argument("--conv-chunk", type=int, default=0,
+                    help="conv backward samples per chunk (0 = auto: 1 where conv12 is split, else 4)")
     ap.add_argument("--ddp-form", default="auto", choices=["auto", "fused", "r5"],
                     help="DDP step form (auto: fused unless the geometry is crowded, see below)")
     ap.add_argument("--bench", action="store_true",
@@ -92,31 +94,30 @@ def main(argv=None) -> int:
     res["self_test_report"] = xar.last_report[:4]
 
     ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
-    # Ranks sharing one GPU with the one-GPU-per-rank geometry (256 exchange workgroups each; or 4
-    # ranks at 128): a rank's exchange workgroups spin on every CU until its peer reaches the same
-    # step, so every kernel of the peer's step must fit on a CU beside one of them (one wave per SIMD, 112 VGPRs):
-    # <= 512 VGPRs per SIMD.  The fused conv12 forward (4 waves x 104) and the 4-sample-chunk
-    # conv_bwd4 (152 KB of LDS) do not: their workgroups waited until the peer's exchange timed
-    # out -- the exchange's stamps show the peer's exchange starting 5 s late, just after the
-    # waiter's deadline released the CUs (profiles/r5_xgmi_handover.md).  So that rehearsal runs
-    # the split conv1 / conv2 forward and the per-sample conv_bwd (tests/test_kernel_resources.py
-    # keeps them within the budget).  The job topology never has this: one rank per GPU runs its
-    # own kernels in stream order.  The chunked paths are covered by the auto-geometry runs (128
-    # workgroups per rank).
+    # Ranks sharing one GPU: a rank's exchange workgroups spin on the CUs until its peers reach the
+    # same step, so every kernel of a peer's step must fit on a CU beside them -- its waves per
+    # SIMD x VGPR allocation + the spinning exchange waves' <= 512, and its LDS beside theirs.
+    # exch_waves = exchange waves per SIMD the other ranks on this GPU can hold: (on_gpu - 1) x nblk
+    # workgroups of one wave per SIMD over 256 CUs.  Round 5 found the fused conv12 forward (4 waves x
+    # 104 VGPRs) waiting out the peer's deadline beside the 112-VGPR exchange (profiles/
+    # r5_xgmi_handover.md).  Round 6 (profiles/r6_xgmi_geometry.md): the exchange with one phase-2
+    # batch per thread (every chunk at 256 workgroups) allocates 96 VGPRs, so at ONE exchange wave per
+    # SIMD -- 2 ranks x 256, the cross-device geometry -- the production kernels all fit (fused conv12,
+    # conv_bwd4's 152 KB of LDS beside the exchange's 4.3 KB) and run here; at two (4 ranks x 128) the
+    # rehearsal keeps the split conv1 / conv2 forward and the per-sample conv backward.  Both run the
+    # round-5 DDP form: the fused form's exchange (it also computes the fc tiles) allocates 144 VGPRs.
+    # tests/test_kernel_resources.py keeps each of these budgets.  The job topology never shares CUs:
+    # one rank per GPU runs its own kernels in stream order.
     peers = [None] * world
     dist.all_gather_object(peers, dev.index)
-    # crowded: while one rank computes, the other ranks on its GPU may all be spinning in their
-    # exchanges -- (ranks on the GPU - 1) x nblk workgroups, enough to sit on every one of the 256
-    # CUs (2 ranks x 256, 4 ranks x 128, ...)
     on_gpu = sum(1 for p in peers if p == dev.index)
-    crowded = on_gpu > 1 and (on_gpu - 1) * xar.nblk >= 256
+    exch_waves = -(-(on_gpu - 1) * xar.nblk // 256) if on_gpu > 1 else 0
+    crowded = on_gpu > 1 and (on_gpu - 1) * xar.nblk >= 256  # every CU can hold a spinning exchange
     res["crowded"] = crowded
-    res["conv_chunk"] = 1 if crowded else 4
-    res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not crowded
-    # crowded, the round-5 DDP form (head + fc1_bwd pushing dW_fc1, the 112-VGPR exchange): the fused
-    # form's exchange computes the fc tiles itself (152 VGPRs) and every owner waits for every sender
-    # block, so ranks whose exchanges spin on the CUs another rank's step needs time out (W = 4 at
-    # 128 workgroups each, profiles/r6_xgmi_geometry.md).  The job topology never shares CUs.
+    res["exchange_waves_per_simd"] = exch_waves
+    split = crowded and exch_waves >= 2
+    res["conv_chunk"] = a.conv_chunk if a.conv_chunk > 0 else (1 if split else 4)
+    res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not split
     res["ddp_form"] = "r5" if (crowded if a.ddp_form == "auto" else a.ddp_form == "r5") else "fused"
 
     def trainer(sync):
