@@ -96,3 +96,43 @@ def test_checker_catches_an_unbacked_figure():
     assert not _backed(37.5, "µs", False, [38.0, 0.0391])
     assert _backed(37.5, "µs", False, [0.0375])
     assert _backed(1.62, "samples/s", True, [0.03951])  # 64 samples / 39.51 us
+
+
+def _status_section(text: str) -> str:
+    i = text.index("## Status and limits")
+    j = text.find("\n## ", i + 1)
+    return text[i:] if j < 0 else text[i:j]
+
+
+def _bench_us(rec: Path) -> float:
+    import json
+    d = json.loads(rec.read_text())
+    line = d.get("parsed") or d
+    return float(line["ms_per_step"]) * 1e3
+
+
+def test_status_headline_is_a_driver_record():
+    """README's status section opens with the driver's record -- its first µs
+    figure sits in a bullet naming a ``BENCH_r0N.json`` that exists, and equals that record's
+    ms_per_step -- and the latest BENCH record is the one quoted (builder-box ranges are context)."""
+    status = _status_section((ROOT / "README.md").read_text())
+    m = next(f for f in _FIG.finditer(status) if f.group(4) in ("µs", "us"))
+    bullet_start = status.rfind("\n* ", 0, m.start())
+    bullet_end = status.find("\n* ", m.end())
+    bullet = status[bullet_start: bullet_end if bullet_end > 0 else len(status)]
+    recs = [r.group(0) for r in _REC.finditer(bullet) if r.group(0).startswith("BENCH")]
+    assert recs, f"first µs figure '{m.group(0)}' cites no BENCH record: {bullet[:200]}"
+    rec = ROOT / recs[0]
+    assert rec.is_file(), rec
+    latest = sorted(ROOT.glob("BENCH_r[0-9][0-9].json"))[-1]
+    assert rec.name == latest.name, (rec.name, latest.name)
+    assert abs(_val(m.group(1)) - _bench_us(rec)) <= 0.006 * _bench_us(rec), (m.group(0), _bench_us(rec))
+
+
+def test_perf_model_headline_is_a_driver_record():
+    text = (ROOT / "docs" / "perf_model.md").read_text()
+    first = next(b for b in _blocks(text) if _FIG.search(b))
+    latest = sorted(ROOT.glob("BENCH_r[0-9][0-9].json"))[-1]
+    assert latest.name in first, first[:300]
+    m = next(f for f in _FIG.finditer(first) if f.group(4) in ("µs", "us"))
+    assert abs(_val(m.group(1)) - _bench_us(latest)) <= 0.006 * _bench_us(latest), m.group(0)

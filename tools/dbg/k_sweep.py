@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Fixed vs per-step cost of bench.py's timed region: t(K) = a + b K.
+
+Builds the bench's world-1 runner (stream-launched one-step kernel list) and times K steps
+bracketed by ``torch.cuda.synchronize()`` exactly as bench.py does, for several K, several
+repeats each, interleaved.  Also times the floor of the bracket itself: an idle synchronize, and
+one empty kernel launch + synchronize.  Prints one JSON line.
+
+    python tools/dbg/k_sweep.py [--ks 1,2,5,10,20,50,200,2000] [--reps 7]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ks", default="1,2,5,10,20,50,200,2000")
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--prewarm-ms", type=int, default=40)
+    a = ap.parse_args()
+    import torch
+    from bench import prewarm
+    from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
+    from pytorch_operator_amd.models.mnist import FusedMnistTrainer
+    from pytorch_operator_amd.ops import mnist as K
+    from pytorch_operator_amd.parallel.graphed_step import GraphedStep
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    ds = make_synthetic_mnist(60000, seed=1, device=dev)
+    cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+    src = K.BatchSource(ds.images, ds.labels, perm=ds.perm, cursor=cursor)
+    tr = FusedMnistTrainer(batch_size=64, source=src, lr=0.01, momentum=0.5, device=dev, seed=1)
+    runner = GraphedStep(tr, mode="graph", steps_per_graph=1, launch="stream")
+    prewarm(a.prewarm_ms, dev)
+    runner.warm(50)
+    torch.cuda.synchronize(dev)
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    ks = [int(x) for x in a.ks.split(",")]
+    res = {k: [] for k in ks}
+    sink = torch.zeros(1, device=dev)
+    floor_idle, floor_one = [], []
+    for _ in range(a.reps):
+        for k in ks:
+            runner.warm(5)
+            res[k].append(timed(lambda: runner.run(k)))
+        floor_idle.append(timed(lambda: None))
+        floor_one.append(timed(lambda: sink.add_(1.0)))
+    med = {k: statistics.median(v) for k, v in res.items()}
+    mn = {k: min(v) for k, v in res.items()}
+    # least squares on the medians
+    xs, ys = ks, [med[k] for k in ks]
+    xb, yb = sum(xs) / len(xs), sum(ys) / len(ys)
+    b = sum((x - xb) * (y - yb) for x, y in zip(xs, ys)) / sum((x - xb) ** 2 for x in xs)
+    out = {
+        "us_per_step_median": {k: round(med[k] / k * 1e6, 3) for k in ks},
+        "us_per_step_min": {k: round(mn[k] / k * 1e6, 3) for k in ks},
+        "fit_us": {"fixed": round((yb - b * xb) * 1e6, 2), "per_step": round(b * 1e6, 3)},
+        "floor_idle_sync_us": round(statistics.median(floor_idle) * 1e6, 2),
+        "floor_one_kernel_us": round(statistics.median(floor_one) * 1e6, 2),
+        "reps": a.reps,
+    }
+    print(json.dumps(out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
