@@ -29,7 +29,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from pytorch_operator_amd.cluster.local import LocalCluster  # noqa: E402
-from pytorch_operator_amd.cluster.rest import PODS, PYTORCHJOBS  # noqa: E402
+from kubeflow.pytorchjob.rest import PODS, PYTORCHJOBS  # noqa: E402
 
 
 def _replica(n, args, gpu):

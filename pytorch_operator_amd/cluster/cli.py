@@ -22,7 +22,7 @@ import os
 import sys
 import time
 
-from .rest import PODS, PYTORCHJOBS, SERVICES, ApiException, KubeRest, load_kube_config
+from kubeflow.pytorchjob.rest import PODS, PYTORCHJOBS, SERVICES, ApiException, KubeRest, load_kube_config
 
 _KINDS = {"pytorchjob": PYTORCHJOBS, "pytorchjobs": PYTORCHJOBS, "ptj": PYTORCHJOBS,
           "pod": PODS, "pods": PODS, "service": SERVICES, "services": SERVICES, "svc": SERVICES}

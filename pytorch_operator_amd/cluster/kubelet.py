@@ -56,7 +56,7 @@ import threading
 import time
 from typing import Dict, List, Optional
 
-from .rest import PODS, SERVICES, ApiException, KubeRest
+from kubeflow.pytorchjob.rest import PODS, SERVICES, ApiException, KubeRest
 
 REPO_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 

@@ -21,7 +21,7 @@ from typing import Dict, List, Optional
 
 from .fake_apiserver import FakeApiServer
 from .kubelet import LocalKubelet
-from .rest import Configuration, KubeRest
+from kubeflow.pytorchjob.rest import Configuration, KubeRest
 
 _LIB = os.path.join(os.path.dirname(__file__), "..", "_lib")
 

@@ -5,7 +5,7 @@ import time
 import pytest
 
 from pytorch_operator_amd.cluster.fake_apiserver import FakeApiServer, label_selector_matches
-from pytorch_operator_amd.cluster.rest import (PODS, PYTORCHJOBS, SERVICES, ApiException, Configuration,
+from kubeflow.pytorchjob.rest import (PODS, PYTORCHJOBS, SERVICES, ApiException, Configuration,
                                                KubeRest)
 
 
@@ -173,7 +173,7 @@ def test_pod_logs_endpoint(api, tmp_path):
 
 
 def test_kubeconfig_roundtrip(api, tmp_path):
-    from pytorch_operator_amd.cluster.rest import load_kube_config
+    from kubeflow.pytorchjob.rest import load_kube_config
     srv, _ = api
     path = srv.write_kubeconfig(str(tmp_path / "kc.json"), namespace="team")
     cfg = load_kube_config(path)

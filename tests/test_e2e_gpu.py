@@ -10,7 +10,7 @@ import time
 import pytest
 
 from pytorch_operator_amd.cluster.local import LocalCluster
-from pytorch_operator_amd.cluster.rest import PODS, PYTORCHJOBS
+from kubeflow.pytorchjob.rest import PODS, PYTORCHJOBS
 
 pytestmark = pytest.mark.gpu
 

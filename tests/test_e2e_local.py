@@ -16,7 +16,7 @@ import time
 import pytest
 
 from pytorch_operator_amd.cluster.local import LocalCluster
-from pytorch_operator_amd.cluster.rest import EVENTS, PODGROUPS, PODS, PYTORCHJOBS, SERVICES, ApiException
+from kubeflow.pytorchjob.rest import EVENTS, PODGROUPS, PODS, PYTORCHJOBS, SERVICES, ApiException
 from pytorch_operator_amd.utils import pformat, rand_string
 
 NS = "default"
@@ -251,7 +251,7 @@ def test_gang_scheduling_creates_and_deletes_podgroup(tmp_path, api):
     """--enable-gang-scheduling with either PodGroup API: the PodGroup (minMember = all
     replicas) exists before the pods run, every pod names it and the gang scheduler, and it is
     deleted when the job finishes.  The other API's resource is never touched."""
-    from pytorch_operator_amd.cluster.rest import VOLCANO_PODGROUPS
+    from kubeflow.pytorchjob.rest import VOLCANO_PODGROUPS
     gvr, other = (VOLCANO_PODGROUPS, PODGROUPS) if api == "volcano" else (PODGROUPS, VOLCANO_PODGROUPS)
     with LocalCluster(workdir=str(tmp_path / "g"),
                       operator_args=["--enable-gang-scheduling", f"--gang-podgroup-api={api}"]) as c:

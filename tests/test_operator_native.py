@@ -87,7 +87,7 @@ def test_json_log_format(operator_bin):
 def test_sanitized_operator_runs_a_job(tmp_path, san):
     """Sanitizer builds of the operator drive a full job (informers, workqueue, HTTP, leader election)."""
     from pytorch_operator_amd.cluster.local import LocalCluster
-    from pytorch_operator_amd.cluster.rest import PYTORCHJOBS
+    from kubeflow.pytorchjob.rest import PYTORCHJOBS
     exe = nb.build_operator(sanitize=san)
     env = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1",
            "TSAN_OPTIONS": "halt_on_error=1"}
@@ -157,7 +157,7 @@ def test_sanitized_operator_concurrent_jobs_with_churn(tmp_path, san):
     terminal condition and the sanitizer must stay silent (no data race, no memory error,
     no leak at exit)."""
     from pytorch_operator_amd.cluster.local import LocalCluster
-    from pytorch_operator_amd.cluster.rest import PYTORCHJOBS
+    from kubeflow.pytorchjob.rest import PYTORCHJOBS
     exe = nb.build_operator(sanitize=san)
     env = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1",
            "TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}

@@ -20,7 +20,7 @@ import pytest
 
 from pytorch_operator_amd.cluster.fake_apiserver import FakeApiServer
 from pytorch_operator_amd.cluster.local import free_port, operator_binary
-from pytorch_operator_amd.cluster.rest import PYTORCHJOBS, ApiException, KubeRest, load_kube_config
+from kubeflow.pytorchjob.rest import PYTORCHJOBS, ApiException, KubeRest, load_kube_config
 
 TOKEN = "s3cret-operator-token"
 
