@@ -135,6 +135,18 @@ __device__ __forceinline__ unsigned* flag2(char* b, int nblk, int q, int blk) {
 __device__ __forceinline__ unsigned* stepc(char* b, int nblk, int blk) {
   return reinterpret_cast<unsigned*>(b) + 2 * kMaxWorld * nblk + blk;
 }
+// Pre-exchange rank barrier (XarCtx::prebarrier): pb_flag(b, q) = the last barrier step rank q
+// arrived at, in rank b's buffer; pb_step = this rank's own barrier count.  Fixed offsets past the
+// largest flag1 / flag2 / stepc layout (kMaxBlocks), inside the 64 KB header.
+constexpr int kPbWord = 2 * kMaxWorld * kMaxBlocks + kMaxBlocks + 64;
+__device__ __forceinline__ unsigned* pb_flag(char* b, int q) {
+  return reinterpret_cast<unsigned*>(b) + kPbWord + q;
+}
+__device__ __forceinline__ unsigned* pb_step(char* b) {
+  return reinterpret_cast<unsigned*>(b) + kPbWord + kMaxWorld;
+}
+static_assert((kPbWord + kMaxWorld + 1) * 4 <= (int)kHdrBytes, "pre-barrier words inside the header");
+
 __device__ __forceinline__ f4* recv_buf(char* b) {
   return reinterpret_cast<f4*>(b + kHdrBytes);
 }
@@ -170,6 +182,7 @@ __device__ __forceinline__ void store_sys(unsigned* p, unsigned v) {
 // Error word bits: which bounded wait timed out first (host reads it with pto_xar_error)
 constexpr int kErrPushWait = 1;    // phase 2: the senders' flag1 (their pushes to this owner)
 constexpr int kErrGatherWait = 2;  // phase 3: an owner's flag2 (its updated shard)
+constexpr int kErrPreBarrier = 4;  // the pre-exchange rank barrier
 
 // Poll one local flag until >= target; false (error flagged) on timeout.
 __device__ bool wait_flag(const unsigned* p, unsigned target, long long deadline, int* err, int code) {
@@ -595,6 +608,34 @@ __global__ __launch_bounds__(kThreads) void xar_kernel_p2(XarArgs a) { xar_body<
 __global__ __launch_bounds__(kThreads) void xar_kernel_fc(XarArgs a) { xar_body<kThreads, true, 1>(a, blockIdx.x); }
 __global__ __launch_bounds__(kThreads) void xar_kernel_fc_p2(XarArgs a) { xar_body<kThreads, true, 2>(a, blockIdx.x); }
 
+// Pre-exchange rank barrier (XarCtx::prebarrier; ranks sharing one GPU, the rehearsal of the
+// one-GPU-per-rank geometry): ONE wave, no LDS, launched before the exchange on the same stream.
+// An exchange's workgroups spin on the CUs until every peer's exchange joins; a peer still running
+// its step kernels must then find room beside them -- and LDS / VGPR fragmentation around a
+// spinning workgroup can leave none (conv_bwd4's 152 KB of LDS needs one contiguous range), which
+// the exchange stamps showed as a peer starting only after the waiter's deadline.  With this
+// barrier no rank's exchange starts before every rank has finished its step kernels: then only
+// exchanges (and this one wave) share the CUs.  Bounded wait like the exchange's; a degraded
+// exchange (error word set) skips it.
+__global__ __launch_bounds__(64) void xar_prebarrier_kernel(XarArgs a) {
+  const int lane = threadIdx.x;
+  char* mine = peer(a, a.rank);
+  if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // wave-uniform
+  const unsigned s = load_sys(pb_step(mine)) + 1u;  // one writer (lane 0, below): every lane reads the same
+  if (lane < a.world) store_sys(pb_flag(peer(a, lane), a.rank), s);
+  const long long deadline = (long long)wall_clock64() + a.timeout_ticks;
+  bool pending = lane < a.world;
+  while (__any(pending)) {
+    if (pending) pending = load_sys(pb_flag(mine, lane)) < s;
+    if ((long long)wall_clock64() > deadline) {
+      if (lane == 0) atomicOr(a.err, kErrPreBarrier);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (lane == 0) store_sys(pb_step(mine), s);
+}
+
 // Emulation of `world` ranks on ONE device in one launch (blockIdx.y = rank): all blocks
 // of all ranks are co-resident, so the protocol (and its latency floor over local HBM)
 // can be tested at any world size on a single GPU.  NT = kEmuThreads when the emulated
@@ -625,6 +666,7 @@ struct XarCtx {
   long long timeout_ticks;
   unsigned long long* stamps;  // optional diagnostics ring (pto_xar_stamps)
   int stamp_ring;
+  int prebarrier;  // launch xar_prebarrier_kernel before every exchange (pto_xar_prebarrier)
 };
 
 long round_up(long x, long m) { return (x + m - 1) / m * m; }
@@ -718,6 +760,13 @@ int pto_xar_stamps(void* ctx, unsigned long long* buf, int ring) {
   return 0;
 }
 
+// Ranks sharing one GPU: a one-wave rank barrier before every later (or later-captured) exchange
+// launch (xar_prebarrier_kernel).  Off by default: one rank per GPU never needs it.
+int pto_xar_prebarrier(void* ctx, int on) {
+  static_cast<XarCtx*>(ctx)->prebarrier = on != 0;
+  return 0;
+}
+
 // Map every peer's buffer (handles: world x 64 bytes, in rank order).
 int pto_xar_open(void* ctx, const void* handles) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
@@ -755,6 +804,11 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.stamp_ring = c->stamp_ring;
   a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
+  if (c->prebarrier) {
+    hipLaunchKernelGGL(xar_prebarrier_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
   const bool one = a.chunk4 <= kThreads;  // phase 2 in one batch per thread
   auto* k = a.fc_tiles ? (one ? xar_kernel_fc : xar_kernel_fc_p2) : (one ? xar_kernel : xar_kernel_p2);
   hipLaunchKernelGGL(k, dim3(c->nblk), dim3(kThreads), 0, (hipStream_t)stream, a);

@@ -28,6 +28,13 @@ the lowest time (identical numbers on every rank, so an identical choice; an all
 it).  The same procedure runs in ``bench.py`` and in the operator-deployed worker
 (``harness/mnist.py --allreduce auto``).
 
+Before an xGMI candidate is timed, one step of it is checked against one step over RCCL from the
+same state (parameters, momentum, batch cursor): parameters and momentum must agree to fp32
+summation-order noise on every rank, or the candidate is dropped (``xgmi_crosscheck`` in the
+record).  The start-up self-test exercises the exchange alone; this pins the whole DDP step it
+takes part in -- producer pushes, the fc tiles of the fused form, the slab reduction, the sharded
+momentum -- at the job's own world size and geometry.
+
 ``PTO_RACE_DELAY_MS="<candidate>:<ms>"`` (fault injection for tests) adds ``ms`` per step of host
 sleep inside that candidate's timed trial.
 """
@@ -103,6 +110,45 @@ def graph_comm_precheck(tr) -> Optional[str]:
     return None
 
 
+def crosscheck_step(tr, rccl_sync, xgmi_sync, dev, rtol: float = 1e-4) -> Dict:
+    """One step over xGMI vs one step over RCCL from the same state (the trainer's current form).
+
+    Leaves the trainer one step further (the xGMI step's state, momentum gathered whole).  Returns
+    ``{"ok", "param_err", "mom_err"}``; ``ok`` is agreed over ranks.  Errors are max |difference|
+    relative to max |reference| (parameters) and max |momentum| (momentum)."""
+    # an xGMI step before this one left the momentum sharded (each rank updates the shard it
+    # owns): make it whole first, or the RCCL reference steps from stale momentum
+    xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+    snap = (tr.flat_params.clone(), tr.flat_momentum.clone(), tr.cursor.clone())
+    tr.grad_sync = rccl_sync
+    tr.train_step()
+    p_ref, m_ref = tr.flat_params.clone(), tr.flat_momentum.clone()
+    tr.flat_params.copy_(snap[0])
+    tr.flat_momentum.copy_(snap[1])
+    tr.cursor.copy_(snap[2])
+    if hasattr(tr, "invalidate_stage"):
+        tr.invalidate_stage()  # the staged batch is the NEXT step's: stage again from the cursor
+    tr.grad_sync = xgmi_sync
+    ok = True
+    # every rank's GPU idle before any rank's exchange spins: work a rank still has queued (the
+    # host collectives' copies) must not wait for CUs held by a peer's exchange on a shared GPU
+    _sync(dev)
+    dist.barrier()
+    try:
+        tr.train_step()
+        xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+        _sync(dev)
+        pe = float((tr.flat_params - p_ref).abs().max() / p_ref.abs().max().clamp_min(1e-30))
+        me = float((tr.flat_momentum - m_ref).abs().max() / m_ref.abs().max().clamp_min(1e-30))
+        err = int(xgmi_sync.xar.error())
+        ok = pe <= rtol and me <= rtol and not err
+    except Exception as e:  # noqa: BLE001 -- a failing candidate is dropped, not fatal
+        pe = me = float("inf")
+        ok, err = False, -1
+        tr.last_crosscheck_error = repr(e)[:200]
+    return {"ok": _agree(ok, dev), "param_err": pe, "mom_err": me, "xgmi_error": err}
+
+
 def _agree(flag: bool, dev) -> bool:
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -123,6 +169,7 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     times: Dict[str, Optional[float]] = {}
     runners: Dict[str, GraphedStep] = {}
     skipped: Dict[str, str] = {}
+    crosscheck: Dict[str, Dict] = {}
     steps = 0
     # the RCCL steps keep momentum for every parameter: make it whole if fused xGMI steps ran
     # before (a no-op when it already is)
@@ -200,6 +247,15 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
                 skipped[name] = "PTO_RACE_SKIP"
                 continue
             set_form(name)
+            if os.environ.get("PTO_RACE_CROSSCHECK", "1") != "0":
+                chk = crosscheck_step(tr, rccl_sync, xgmi_sync, dev)
+                steps += 1
+                crosscheck[name] = {k: (round(v, 9) if isinstance(v, float) else v) for k, v in chk.items()}
+                tr.grad_sync = xgmi_sync
+                if not chk["ok"]:
+                    skipped[name] = (f"cross-check vs RCCL failed (param {chk['param_err']:.2e}, "
+                                     f"momentum {chk['mom_err']:.2e}, exchange error {chk['xgmi_error']})")
+                    continue
             r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
             runners[name] = r
             t = _timed(r, trial, dev, name)
@@ -225,11 +281,15 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     else:
         tr.grad_sync = xgmi_sync
     set_form(pick)  # later eager steps of the trainer take the picked form too
+    _sync(dev)
+    dist.barrier()  # the agreement's copies done on every rank before the picked runner's first step
     record = {f"{k.replace('-', '_')}_ms_per_step": (round(v / trial * 1e3, 4) if v != float("inf") else None)
               for k, v in times.items()}
     for k, why in skipped.items():
         record[f"{k.replace('-', '_')}_ms_per_step"] = None
         record[f"{k.replace('-', '_')}_skipped"] = why
+    if crosscheck:
+        record["xgmi_crosscheck"] = crosscheck
     if times.get("xgmi") == float("inf") or times.get("xgmi-r5") == float("inf"):
         record["xgmi_error"] = int(xgmi_sync.xar.error())
     record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,

@@ -54,6 +54,7 @@ class XgmiAllReduce:
             raise ValueError("n must be a multiple of 4")
         self.n = int(n)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.prebarrier = False
         if nblk <= 0:
             # one workgroup per CU when every rank owns its GPU (the kernel's phase 1 reduces
             # the conv backward's slab -- 1.6 MB of 4-sample chunk rows + per-sample rows of the
@@ -185,6 +186,14 @@ class XgmiAllReduce:
 
     def error(self) -> int:
         return int(self.lib.pto_xar_error(self._ctx))
+
+    def set_prebarrier(self, on: bool = True) -> None:
+        """Ranks sharing one GPU: a one-wave rank barrier before every later (or later-captured)
+        exchange launch, so no rank's exchange spins on the CUs while a peer still runs its step
+        kernels (csrc/kernels/xgmi_allreduce.hip ``xar_prebarrier_kernel``).  One rank per GPU
+        never needs it."""
+        _native.check(self.lib.pto_xar_prebarrier(self._ctx, 1 if on else 0), "pto_xar_prebarrier")
+        self.prebarrier = bool(on)
 
     def enable_stamps(self, ring: int = 16) -> torch.Tensor:
         """Diagnostics: every later (or later-captured) launch records, per workgroup, its step,

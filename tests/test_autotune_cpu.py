@@ -95,3 +95,104 @@ def test_candidate_runs_when_every_rank_can_capture():
     out = _race("ok")
     for rank, (pick, rec, log) in out.items():
         assert rec["rccl_graph_ms_per_step"] is not None and log == ["graph-comm built"]
+
+
+def _xc_worker(rank, world, port, scenario, q):
+    """The xGMI candidates' step cross-check: a stand-in trainer whose step adds its gradient path's
+    update; the xGMI stand-in is right, or off by 1e-3 on one rank (a broken exchange)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import pytorch_operator_amd.parallel.autotune as at
+
+    class Sync:
+        def __init__(self, scale):
+            self.scale = scale
+
+    class Xar:
+        def gather_sharded_(self, m):
+            pass
+
+        def error(self):
+            return 0
+
+    class XSync(Sync):
+        xar = Xar()
+
+    class Tr:
+        device = torch.device("cpu")
+        grad_sync = None
+        ddp_fused = True
+
+        def __init__(self):
+            self.flat_params = torch.linspace(-1, 1, 100)
+            self.flat_momentum = torch.zeros(100)
+            self.cursor = torch.zeros(1, dtype=torch.int32)
+            self.staged = 0
+
+        def fused_ok(self):
+            return True
+
+        def invalidate_stage(self):
+            self.staged += 1
+
+        def train_step(self):
+            g = torch.sin(self.flat_params + self.cursor.float()) * self.grad_sync.scale
+            self.flat_momentum.mul_(0.5).add_(g)
+            self.flat_params.sub_(0.01 * self.flat_momentum)
+            self.cursor += 1
+
+    class FakeStep:
+        def __init__(self, tr, mode="graph", steps_per_graph=1, launch="graph", **kw):
+            self.internal_steps, self.launch = 0, launch
+
+        def warm(self, n):
+            pass
+
+    at.GraphedStep = FakeStep
+    at.graph_comm_precheck = lambda tr: "no capture here"
+    tr = Tr()
+    bad = scenario == "wrong" and rank == 1
+    try:
+        _, pick, rec = at.choose_grad_sync(tr, Sync(1.0), XSync(1.001 if bad else 1.0), trial_steps=2)
+        q.put((rank, pick, rec, int(tr.cursor.item()), tr.staged))
+    finally:
+        dist.destroy_process_group()
+
+
+def _xc_race(scenario):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_xc_worker, args=(r, 2, port, scenario, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in ps:
+        rank, pick, rec, cursor, staged = q.get(timeout=120)
+        out[rank] = (pick, rec, cursor, staged)
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.timeout(180)
+def test_xgmi_candidates_pass_the_step_crosscheck():
+    for rank, (pick, rec, cursor, staged) in _xc_race("right").items():
+        cc = rec["xgmi_crosscheck"]
+        assert set(cc) == {"xgmi", "xgmi-r5"} and all(v["ok"] for v in cc.values()), cc
+        assert all(v["param_err"] < 1e-6 for v in cc.values()), cc
+        assert rec["xgmi_ms_per_step"] is not None and rec["xgmi_r5_ms_per_step"] is not None, rec
+        assert rec["steps"] == 2 + 2 + 2 * (1 + 2), rec  # rccl, rccl-r5 trials; per xGMI form 1 checked + 2 timed
+        assert staged == 2  # the staged batch dropped after each restore
+        assert cursor == 2  # the stand-in runners take no steps: the two checks' net steps
+
+
+@pytest.mark.timeout(180)
+def test_a_wrong_xgmi_step_on_one_rank_drops_the_candidates_everywhere():
+    for rank, (pick, rec, cursor, staged) in _xc_race("wrong").items():
+        assert pick.startswith("rccl"), (pick, rec)
+        assert rec["xgmi_ms_per_step"] is None and rec["xgmi_skipped"].startswith("cross-check vs RCCL failed")
+        assert rec["xgmi_r5_skipped"].startswith("cross-check vs RCCL failed")
+        assert not rec["xgmi_crosscheck"]["xgmi"]["ok"]

@@ -103,6 +103,9 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
         # both DDP forms of each path raced (round 6: fused, and the round-5 form as "-r5")
         assert trial["rccl_r5_ms_per_step"] > 0 and trial["xgmi_r5_ms_per_step"] > 0, trial
         assert trial["ddp_form"] == ("r5" if trial["picked"].endswith("-r5") else "fused"), trial
+        # each xGMI form was checked against a step over the other path before it was timed
+        cc = trial["xgmi_crosscheck"]
+        assert set(cc) == {"xgmi", "xgmi-r5"} and all(v["ok"] for v in cc.values()), cc
         if slow_xgmi:
             assert trial["picked"] in ("rccl", "rccl-r5"), trial
             assert trial["xgmi_ms_per_step"] > trial["rccl_ms_per_step"], trial

@@ -15,8 +15,11 @@ form fits -- fused conv12, conv_bwd4 with its 152 KB of dynamic LDS -- and tools
 runs them there.  At two (4 ranks x 128) the split conv1 / conv2 forward and the per-sample conv
 backward run.  The fused DDP form's exchange (``xar_kernel_fc``, which also computes the fc
 gradient tiles) allocates more; its kernels fit beside one of its waves except conv12, so crowded
-rehearsals run the round-5 form.  Reads the AMDGPU metadata of the built library
-(tools/isa_dump.py) and one size query, no GPU needed.
+rehearsals run the round-5 form when the budget is all they rely on (``--prebarrier 0``).  The
+budget is necessary, not sufficient: LDS / VGPR fragmentation around a spinning workgroup still
+starved a peer now and then, so crowded rehearsals now run a one-wave rank barrier before each
+exchange (profiles/r6_xgmi_geometry.md) and these rows document the static fit.  Reads the AMDGPU
+metadata of the built library (tools/isa_dump.py) and one size query, no GPU needed.
 """
 import ctypes
 import sys

@@ -28,8 +28,8 @@ def test_xgmi_allreduce_ranks(tmp_path, world, nblk):
     """nblk=0 picks 128 workgroups per rank here (ranks share the box's GPU); nblk=256 runs the
     geometry a one-GPU-per-rank job uses, every stage including the autotune hand-over, with the
     step's kernels that fit beside a spinning exchange workgroup (tools/xgmi_check.py,
-    tests/test_kernel_resources.py): at one exchange wave per SIMD (2 x 256) the production
-    kernels -- fused conv12 forward, conv_bwd4 -- in the round-5 DDP form."""
+    tests/test_kernel_resources.py): the production kernels -- fused conv12 forward, conv_bwd4 --
+    in the fused DDP form, behind the pre-exchange rank barrier where ranks crowd the CUs."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "tools" / "xgmi_check.py"),
            "--backend", "gloo", "--out", str(tmp_path), "--nblk", str(nblk)]
@@ -42,12 +42,10 @@ def test_xgmi_allreduce_ranks(tmp_path, world, nblk):
         assert res["all_ok"], res
         assert res["nblk"] == nblk or (nblk == 0 and res["nblk"] in (128, 256)), res
         # which production kernels ran beside the spinning exchange (profiles/r6_xgmi_geometry.md)
-        waves = res["exchange_waves_per_simd"]
-        if res["crowded"]:
-            assert res["ddp_form"] == "r5", res
-            assert (res["fuse_conv12"], res["conv_chunk"]) == ((True, 4) if waves == 1 else (False, 1)), res
-        else:
-            assert res["ddp_form"] == "fused" and res["fuse_conv12"] and res["conv_chunk"] == 4, res
+        # every geometry runs the production step in the fused DDP form; crowded ones (every CU can
+        # hold a spinning exchange) behind the pre-exchange rank barrier
+        assert res["ddp_form"] == "fused" and res["fuse_conv12"] and res["conv_chunk"] == 4, res
+        assert res["prebarrier"] == res["crowded"], res
     rec = os.environ.get("PTO_TEST_RECORD_DIR")
     if rec:
         Path(rec).mkdir(parents=True, exist_ok=True)

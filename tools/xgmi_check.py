@@ -63,12 +63,14 @@ def main(argv=None) -> int:
                     help="record the hand-over exchange's per-workgroup phase stamps (XgmiAllReduce."
                          "enable_stamps) and write <out>/rank<r>_stamps.json (tools/xgmi_stamps.py reads them)")
     ap.add_argument("--fuse-conv12", type=int, default=-1,
-                    help="1/0: force the fused conv12 forward on/off (default: off when the other ranks on "
-                         "this GPU can hold two exchange waves per SIMD, see below)")
+                    help="1/0: force the fused conv12 forward on/off (default: on, off only under "
+                         "--prebarrier 0 at two exchange waves per SIMD, see below)")
+    ap.add_argument("--prebarrier", type=int, default=-1,
+                    help="1/0: rank barrier before each exchange (default: on when crowded)")
     ap.add_argument("--conv-chunk", type=int, default=0,
                     help="conv backward samples per chunk (0 = auto: 1 where conv12 is split, else 4)")
     ap.add_argument("--ddp-form", default="auto", choices=["auto", "fused", "r5"],
-                    help="DDP step form (auto: fused unless the geometry is crowded, see below)")
+                    help="DDP step form (auto: fused, round-5 only under --prebarrier 0 when crowded)")
     ap.add_argument("--bench", action="store_true",
                     help="time the fused exchange alone (graph of back-to-back launches)")
     a = ap.parse_args(argv)
@@ -95,19 +97,19 @@ def main(argv=None) -> int:
 
     ds = make_synthetic_mnist(4096, seed=11 + rank, device=dev)
     # Ranks sharing one GPU: a rank's exchange workgroups spin on the CUs until its peers reach the
-    # same step, so every kernel of a peer's step must fit on a CU beside them -- its waves per
-    # SIMD x VGPR allocation + the spinning exchange waves' <= 512, and its LDS beside theirs.
-    # exch_waves = exchange waves per SIMD the other ranks on this GPU can hold: (on_gpu - 1) x nblk
-    # workgroups of one wave per SIMD over 256 CUs.  Round 5 found the fused conv12 forward (4 waves x
-    # 104 VGPRs) waiting out the peer's deadline beside the 112-VGPR exchange (profiles/
-    # r5_xgmi_handover.md).  Round 6 (profiles/r6_xgmi_geometry.md): the exchange with one phase-2
-    # batch per thread (every chunk at 256 workgroups) allocates 96 VGPRs, so at ONE exchange wave per
-    # SIMD -- 2 ranks x 256, the cross-device geometry -- the production kernels all fit (fused conv12,
-    # conv_bwd4's 152 KB of LDS beside the exchange's 4.3 KB) and run here; at two (4 ranks x 128) the
-    # rehearsal keeps the split conv1 / conv2 forward and the per-sample conv backward.  Both run the
-    # round-5 DDP form: the fused form's exchange (it also computes the fc tiles) allocates 144 VGPRs.
-    # tests/test_kernel_resources.py keeps each of these budgets.  The job topology never shares CUs:
-    # one rank per GPU runs its own kernels in stream order.
+    # same step.  A peer still running its step kernels must then find room beside them: its waves
+    # per SIMD x VGPR allocation + the spinning exchange waves' <= 512, and its LDS in ONE free
+    # range.  Round 5 found the fused conv12 forward waiting out the peer's deadline beside the
+    # 112-VGPR exchange (profiles/r5_xgmi_handover.md); round 6 brought the exchange to 96 VGPRs, so
+    # every production kernel fits the budget beside one exchange wave per SIMD
+    # (tests/test_kernel_resources.py) -- and still saw the same starvation now and then: LDS / VGPR
+    # fragmentation around a spinning workgroup (an exchange workgroup's 4.3 KB placed mid-LDS leaves
+    # no 152 KB range for conv_bwd4).  The fix is the ordering, not the budget: when crowded, a
+    # one-wave rank barrier runs before every exchange (XgmiAllReduce.set_prebarrier), so no rank's
+    # exchange starts before every rank has finished its step kernels, and the rehearsal runs the
+    # production step in the fused DDP form (profiles/r6_xgmi_geometry.md).  --prebarrier 0 keeps the
+    # budget-only policy: the round-5 form, split conv kernels at two exchange waves per SIMD.  The
+    # job topology never shares CUs: one rank per GPU runs its own kernels in stream order.
     peers = [None] * world
     dist.all_gather_object(peers, dev.index)
     on_gpu = sum(1 for p in peers if p == dev.index)
@@ -115,10 +117,14 @@ def main(argv=None) -> int:
     crowded = on_gpu > 1 and (on_gpu - 1) * xar.nblk >= 256  # every CU can hold a spinning exchange
     res["crowded"] = crowded
     res["exchange_waves_per_simd"] = exch_waves
-    split = crowded and exch_waves >= 2
+    res["prebarrier"] = crowded if a.prebarrier < 0 else bool(a.prebarrier)
+    budget_only = crowded and not res["prebarrier"]
+    split = budget_only and exch_waves >= 2
     res["conv_chunk"] = a.conv_chunk if a.conv_chunk > 0 else (1 if split else 4)
     res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not split
-    res["ddp_form"] = "r5" if (crowded if a.ddp_form == "auto" else a.ddp_form == "r5") else "fused"
+    res["ddp_form"] = "r5" if (budget_only if a.ddp_form == "auto" else a.ddp_form == "r5") else "fused"
+    if res["prebarrier"]:
+        xar.set_prebarrier(True)
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -150,6 +156,8 @@ def main(argv=None) -> int:
     res["error_after"] = {"eager": xar.error()}
 
     runner = GraphedStep(ta, mode="graph", steps_per_graph=4)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
     runner.run(8)
     torch.cuda.synchronize(dev)
     ref = ta.flat_params.clone()
@@ -163,6 +171,8 @@ def main(argv=None) -> int:
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
     hnb = a.handover_nblk or xar.nblk
     hx = XgmiAllReduce(L, device=dev, nblk=hnb) if hnb != xar.nblk else xar
+    if hx is not xar and res["prebarrier"]:
+        hx.set_prebarrier(True)
     stamps_hx = hx.enable_stamps(64) if a.stamps and hx is not xar else None
     if hx is not xar:
         res["handover_self_test"] = hx.self_test()
@@ -170,8 +180,14 @@ def main(argv=None) -> int:
     launch = "stream"
     res["handover_launch"] = launch
     for force in ("rccl", "xgmi"):
-        runner, path, times = choose_grad_sync(ta, FlatGradAllReduce(), XgmiGradSync(hx), spg=4,
-                                               trial_steps=8, force=force, launch=launch)
+        try:
+            runner, path, times = choose_grad_sync(ta, FlatGradAllReduce(), XgmiGradSync(hx), spg=4,
+                                                   trial_steps=8, force=force, launch=launch)
+        except ValueError as e:  # the forced candidate was dropped (its step cross-check failed)
+            res[f"handover_{force}_in_sync"] = False
+            res[f"handover_{force}_error"] = str(e)[:300]
+            res["error_after"][f"handover_{force}"] = hx.error()
+            continue
         runner.run(8)
         torch.cuda.synchronize(dev)
         ref = ta.flat_params.clone()
