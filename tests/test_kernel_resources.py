@@ -105,3 +105,11 @@ def test_fused_form_beside_its_exchange(res):
     assert not _fits(isa, r, dyn, "conv12_fwd_kernel", "xar_kernel_fcENS", 1)
     # nor fc1_bwd_head (2 x 120) beside two of them (W = 4 x 128)
     assert not _fits(isa, r, dyn, "fc1_bwd_head_kernel", "xar_kernel_fcENS", 2)
+
+
+def test_prebarrier_kernel_holds_next_to_nothing(res):
+    """The pre-exchange rank barrier spins beside a peer's step kernels: one wave, no LDS (any LDS
+    allocation can split a CU's 160 KB below conv_bwd4's 152 KB range), a few VGPRs."""
+    isa, r, _ = res
+    k = _find(r, "xar_prebarrier_kernel")
+    assert k["lds"] == 0 and k["max_wg"] == 64 and isa.vgpr_alloc(k) <= 16 and k["spills"] == 0, k
