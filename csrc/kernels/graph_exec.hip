@@ -142,6 +142,40 @@ int pto_graph_launch_stream(void* handle, void* stream, int n) {
   return 0;
 }
 
+// Probe (tools/dbg/twostream_probe.py): the price of a two-stream step structure with no work
+// moved.  The recorded kernels replay on s1 as pto_graph_launch_stream does; after kernel rec_after
+// of each step an event is recorded on s1, s2 waits for it, runs a no-op kernel of side_blocks
+// workgroups (0: none) and records a second event, which s1 waits for before kernel wait_before of
+// the NEXT step (-1: no wait).  rec_after = -1: plain replay.
+__global__ void pto_noop_kernel(int* p) {
+  if (p != nullptr && blockIdx.x == 0 && threadIdx.x == 0) p[0] = 0;
+}
+
+int pto_graph_launch_stream_probe(void* handle, void* s1, void* s2, int n, int rec_after, int wait_before,
+                                  int side_blocks) {
+  auto* h = static_cast<PtoGraph*>(handle);
+  if (h == nullptr || n < 0) return -1;
+  if (h->launches.empty()) return -2;
+  static hipEvent_t e1 = nullptr, e2 = nullptr;
+  if (e1 == nullptr && (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess ||
+                        hipEventCreateWithFlags(&e2, hipEventDisableTiming) != hipSuccess))
+    return -3;
+  for (int i = 0; i < n; ++i)
+    for (size_t k = 0; k < h->launches.size(); ++k) {
+      const hipKernelNodeParams& p = h->launches[k];
+      if ((int)k == wait_before && i > 0 && hipStreamWaitEvent((hipStream_t)s1, e2, 0) != hipSuccess) return -4;
+      hipError_t e = hipLaunchKernel(p.func, p.gridDim, p.blockDim, p.kernelParams, p.sharedMemBytes, (hipStream_t)s1);
+      if (e != hipSuccess) return (int)e;
+      if ((int)k == rec_after) {
+        if (hipEventRecord(e1, (hipStream_t)s1) != hipSuccess) return -5;
+        if (hipStreamWaitEvent((hipStream_t)s2, e1, 0) != hipSuccess) return -6;
+        if (side_blocks > 0) hipLaunchKernelGGL(pto_noop_kernel, dim3(side_blocks), dim3(64), 0, (hipStream_t)s2, nullptr);
+        if (hipEventRecord(e2, (hipStream_t)s2) != hipSuccess) return -7;
+      }
+    }
+  return 0;
+}
+
 long pto_graph_nodes(void* handle) {
   auto* h = static_cast<PtoGraph*>(handle);
   return h == nullptr ? -1 : (long)h->nodes;

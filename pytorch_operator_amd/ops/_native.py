@@ -204,6 +204,7 @@ _SIGNATURES = {
     "pto_graph_upload": [_VP, _VP],
     "pto_graph_launch": [_VP, _VP, _I],
     "pto_graph_launch_stream": [_VP, _VP, _I],
+    "pto_graph_launch_stream_probe": [_VP, _VP, _VP, _I, _I, _I, _I],
     "pto_graph_destroy": [_VP],
     "pto_device_prewarm": [_I, _VP, _VP],
 }
