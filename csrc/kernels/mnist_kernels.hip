@@ -1762,7 +1762,11 @@ constexpr int G_OFF_DCOL = G_OFF_W + 52 * F_WS;
 constexpr int G_OFF_A1 = G_OFF_DCOL + 128 * F_DC;
 constexpr int G_OFF_A1C = G_OFF_A1 + 4 * F_A1C + 12 * F_A1R;
 constexpr int G_OFF_X = G_OFF_A1C + 4 * G_A1S;
-constexpr int G_OFF_IDX = G_OFF_X + 28 * F_XR;
+// xn row stride of conv_bwd4 (round 6): phase 4 reads each lane's row 2 py + dy + kh at its own
+// pooling argmax, so a half-wave touches ~17 rows x 2 column parities; 30 (== -2 mod 32) halves
+// the conflicts of 29 (tools/lds_banks_fwd.py --only conv_bwd4: 99 -> 48 cycles per active wave)
+constexpr int G_XR = 30;
+constexpr int G_OFF_IDX = G_OFF_X + 28 * G_XR;
 constexpr int G_OFF_PK = G_OFF_IDX + 180;     // 2b K-half-1 partial tiles: 6 x 64 lanes x f32x4
 constexpr int G_OFF_PV = G_OFF_PK + 6 * 256;  // co 48/49 per-sample partials: 4 x 64
 constexpr int G_LDS = G_OFF_PV + 4 * 64;
@@ -1802,7 +1806,7 @@ __device__ __forceinline__ void bwd4_dw1_item_pooled(int it, const float* dp1_s,
 #pragma unroll
   for (int px = 0; px < 12; ++px) {
     const int p = iv[px];
-    const float* xr = x_s + (2 * py + (p >> 1) + kh) * F_XR + 2 * px + (p & 1);
+    const float* xr = x_s + (2 * py + (p >> 1) + kh) * G_XR + 2 * px + (p & 1);
     const float a = dv[px];
     bs += a;
 #pragma unroll
@@ -1947,12 +1951,18 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
     const bool ok = 4 * q + sq < B;  // samples >= B of the chunk as 0
     const float v[4] = {pdv.x, pdv.y, pdv.z, pdv.w};
     float2* z0 = reinterpret_cast<float2*>(dzc_s + sq * G_DZN + co * G_DZS + 16 * ph);
+    // lanes with ph 2, 3 store their second row first (round 6): their rows sit 32 floats after
+    // ph 0, 1's, i.e. on the same banks, and each 16-lane group of the float2 stores is 2-way
+    // otherwise (tools/lds_banks_fwd.py --only conv_bwd4: 25 -> 0 conflict cycles per wave)
+    const int sw = (ph & 2) ? 4 : 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const unsigned pu = (piv >> (8 * u)) & 0xffu;
       const float vv = ok ? v[u] : 0.f;
-      z0[u] = make_float2(pu == 0u ? vv : 0.f, pu == 1u ? vv : 0.f);
-      z0[4 + u] = make_float2(pu == 2u ? vv : 0.f, pu == 3u ? vv : 0.f);
+      const float2 ra = make_float2(pu == 0u ? vv : 0.f, pu == 1u ? vv : 0.f);
+      const float2 rb = make_float2(pu == 2u ? vv : 0.f, pu == 3u ? vv : 0.f);
+      z0[u + sw] = sw ? rb : ra;
+      z0[u + 4 - sw] = sw ? ra : rb;
     }
   }
   if (tid < 512) {  // zero rows 50, 51 of every sample (2a reads co up to 51)
@@ -1985,7 +1995,7 @@ __global__ __launch_bounds__(F_NT) void conv_bwd4_kernel(
   }
   if (e_x >= 0 && e_x < 196) {
     const int y = e_x / 7;
-    float* d = x_s + y * F_XR + 4 * (e_x - 7 * y);
+    float* d = x_s + y * G_XR + 4 * (e_x - 7 * y);
     d[0] = xvv.x;
     d[1] = xvv.y;
     d[2] = xvv.z;

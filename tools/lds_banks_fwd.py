@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""LDS bank-conflict model of conv12_fwd_kernel and fc1_bwd_head_kernel (round 6).
+"""LDS bank-conflict model of conv12_fwd_kernel, fc1_bwd_head_kernel and conv_bwd4_kernel (round 6).
 
 Banking rules (MI355X_MICROARCH.md §LDS): a wave64 LDS instruction is serviced in fixed lane
 groups, one cycle per group when conflict-free; within a group each bank serves one distinct dword
@@ -204,6 +204,180 @@ def conv12_fwd(a) -> float:
     return t.report(f"conv12_fwd ({a.layout}: AB_IRS {IRS}, C2_CS {CS}, C2_RS {RS}, C2_WS {WS}, w1s row {W1R})", 16)
 
 
+def conv_bwd4(a) -> float:
+    """conv_bwd4_kernel: every LDS access of one block per (cig, r), averaged over the 16 blocks of a
+    4-sample chunk (idx1-dependent phase-4 reads: random pooling argmax)."""
+    import random
+    rnd = random.Random(7)
+    DZS, DZR, WS, DC, A1R, A1C, XR, RED1 = a.g_dzs, 52, 144, 68, 13, 160, a.g_xr, 132
+    DZN = DZR * DZS
+    A1S = 2 * A1C
+    OFF_W = 4 * DZN
+    OFF_DCOL = OFF_W + 52 * WS
+    OFF_A1 = OFF_DCOL + 128 * DC
+    OFF_A1C = OFF_A1 + 4 * A1C + 12 * A1R
+    OFF_X = OFF_A1C + 4 * A1S
+    OFF_IDX = OFF_X + 28 * XR
+    OFF_PK = OFF_IDX + 180
+    OFF_PV = OFF_PK + 6 * 256
+    OFF_DZ1 = OFF_W
+    OFF_RED = OFF_W + 5 * 628
+    t = Tally()
+    nblk = 0
+    for cig in range(4):
+        for r in range(4):
+            nblk += 1
+            jbase = 32 * r - cig
+            c0 = max(jbase, 0) // 25
+            for wv in range(16):
+                tids = [64 * wv + ln for ln in range(64)]
+                # ---- phase 1 stores
+                for u in range(8):
+                    ad = []
+                    for tid in tids:
+                        if tid < 800:
+                            sq, f4 = tid // 200, tid % 200
+                            co, ph = f4 >> 2, f4 & 3
+                            uu = u if not (a.g_swz and ph & 2) else (u + 4) % 8  # rows swapped for ph 2, 3
+                            ad.append(sq * DZN + co * DZS + 16 * ph + (2 * uu if uu < 4 else 8 + 2 * (uu - 4)))
+                        else:
+                            ad.append(None)
+                    if any(x is not None for x in ad):
+                        t.add("1 dz2 un-pool float2 stores", "w64", ad)
+                ad = [(tid >> 7) * DZN + (50 + ((tid >> 6) & 1)) * DZS + (tid & 63) if tid < 512 else None for tid in tids]
+                if any(x is not None for x in ad):
+                    t.add("1 dz2 zero rows", "w32", ad)
+                t.add("1 w2 slice float4 stores", "w128", [OFF_W + (tid >> 5) * WS + 4 * (tid & 31) for tid in tids])
+                ad = [OFF_W + ((tid + 1024) >> 5) * WS + 4 * (tid & 31) if tid < 640 else None for tid in tids]
+                if any(x is not None for x in ad):
+                    t.add("1 w2 slice float4 stores", "w128", ad)
+                for k in range(4):
+                    ad = []
+                    for tid in tids:
+                        e = tid - 736
+                        if e >= 0:
+                            sm, rem = e // 72, e % 72
+                            c = rem // 36
+                            p4 = rem - c * 36
+                            y = p4 // 3
+                            ad.append(OFF_A1C + sm * A1S + c * A1C + y * A1R + 4 * (p4 - 3 * y) + k)
+                        else:
+                            ad.append(None)
+                    if any(x is not None for x in ad):
+                        t.add("1 a1 chunk image stores", "w32", ad)
+                    ad = []
+                    for tid in tids:
+                        e = tid - 640
+                        if 0 <= e < 180:
+                            c, p4 = e // 36, e % 36
+                            y = p4 // 3
+                            ad.append(OFF_A1 + c * A1C + y * A1R + 4 * (p4 - 3 * y) + k)
+                        else:
+                            ad.append(None)
+                    if any(x is not None for x in ad):
+                        t.add("1 own a1 stores", "w32", ad)
+                    ad = []
+                    for tid in tids:
+                        e = tid - 800
+                        ad.append(OFF_X + (e // 7) * XR + 4 * (e % 7) + k if 0 <= e < 196 else None)
+                    if any(x is not None for x in ad):
+                        t.add("1 xn stores", "w32", ad)
+                lanes = range(64)
+                if wv < 8:
+                    # ---- 2a
+                    pt, jt0 = wv & 3, (wv >> 2) * 4
+                    for sstep in range(13):
+                        t.add("2a dz2 operand reads", "r32",
+                              [r * DZN + (lane >> 4) * DZS + pt * 16 + (lane & 15) + 4 * sstep * DZS for lane in lanes])
+                        for tt in range(4):
+                            t.add("2a W2 operand reads", "r32",
+                                  [OFF_W + cig + (lane >> 4) * WS + jt0 * 16 + (lane & 15) + 4 * sstep * WS + 16 * tt
+                                   for lane in lanes])
+                    for tt in range(4):
+                        for rr in range(4):
+                            t.add("2a dcol stores", "w32",
+                                  [OFF_DCOL + ((jt0 + tt) * 16 + (lane >> 4) * 4 + rr) * DC + pt * 16 + (lane & 15)
+                                   for lane in lanes])
+                    # ---- 3: col2im (items tid, tid + 512)
+                    for base_it in (0, 512):
+                        its = [tid + base_it for tid in tids]
+                        for kh in range(5):
+                            for kw in range(5):
+                                ad = []
+                                for it in its:
+                                    if it >= 720:
+                                        ad.append(None)
+                                        continue
+                                    c, p = it // 144, it % 144
+                                    y, x = p // 12, p % 12
+                                    ad.append(OFF_DCOL + c * 25 * DC + y * 8 + x + kh * (5 * DC - 8) + kw * (DC - 1))
+                                if any(v is not None for v in ad):
+                                    t.add("3 col2im dcol reads", "r32", ad)
+                        ad = []
+                        for it in its:
+                            if it >= 720:
+                                ad.append(None)
+                                continue
+                            c, p = it // 144, it % 144
+                            ad.append(OFF_A1 + c * A1C + (p // 12) * A1R + p % 12)
+                        if any(v is not None for v in ad):
+                            t.add("3 ReLU-mask a1 reads", "r32", ad)
+                    # ---- 4: pooled dW_conv1 items (tid < 300)
+                    its = [tid if tid < 300 else None for tid in tids]
+                    if any(v is not None for v in its):
+                        pidx = {it: [rnd.randrange(4) for _ in range(12)] for it in its if it is not None}
+                        for k in range(12):
+                            t.add("4 pooled dz1 reads", "r32",
+                                  [OFF_DZ1 + (it // 60) * 144 + ((it % 60) // 5) * 12 + k if it is not None else None
+                                   for it in its])
+                        for px in range(12):
+                            for kw in range(5):
+                                ad = []
+                                for it in its:
+                                    if it is None:
+                                        ad.append(None)
+                                        continue
+                                    rem = it % 60
+                                    py, kh = rem // 5, rem % 5
+                                    pp = pidx[it][px]
+                                    ad.append(OFF_X + (2 * py + (pp >> 1) + kh) * XR + 2 * px + (pp & 1) + kw)
+                                t.add("4 xn window reads", "r32", ad)
+                        for kw in range(5):
+                            t.add("4 partial stores", "w32",
+                                  [OFF_RED + ((it % 60) // 5) * RED1 + (it // 60) * 25 + (it % 5) * 5 + kw
+                                   if it is not None else None for it in its])
+                else:
+                    # ---- 2b
+                    w8 = wv - 8
+                    calls = [(w8, 0), (w8, 1)] if w8 < 4 else [(4 + ((w8 - 4) >> 1), (w8 - 4) & 1)]
+                    for tp, kh2 in calls:
+                        ct, jt = tp >> 1, tp & 1
+                        for u in range(32):
+                            s_, uu = u >> 4, u & 15
+                            ad_a, ad_b = [], []
+                            for lane in lanes:
+                                i, g = lane & 15, lane >> 4
+                                jc = min(max(jbase + jt * 16 + i, 0), 124)
+                                ci, tt = jc // 25, jc % 25
+                                ad_a.append(OFF_A1C + 2 * kh2 * A1S + (ci - c0) * A1C + (tt // 5) * A1R + tt % 5 + g +
+                                            s_ * A1S + (uu >> 1) * A1R + 4 * (uu & 1))
+                                ad_b.append(2 * kh2 * DZN + (ct * 16 + i) * DZS + g + s_ * DZN + 4 * uu)
+                            t.add("2b a1 im2col operand reads", "r32", ad_a)
+                            t.add("2b dz2 operand reads", "r32", ad_b)
+                    if w8 >= 4:
+                        items = [64 * wv + ln - 768 for ln in lanes]
+                        for pos in range(64):
+                            ad = []
+                            for item in items:
+                                sm, jl = item >> 6, item & 31
+                                jc = min(max(jbase + jl, 0), 124)
+                                ci, tt = jc // 25, jc % 25
+                                ad.append(OFF_A1C + sm * A1S + (ci - c0) * A1C + (tt // 5) * A1R + tt % 5 +
+                                          (pos >> 3) * A1R + (pos & 7))
+                            t.add("2b co 48/49 VALU a1 reads", "r32", ad)
+    return t.report(f"conv_bwd4 (G_DZS {DZS}, G_XR {XR}, un-pool store swizzle {a.g_swz})", nblk * 16)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layout", default="r6", choices=["r5", "r6"])
@@ -216,11 +390,16 @@ def main():
     ap.add_argument("--c2-cs", type=int, default=200)
     ap.add_argument("--c2-rs", type=int, default=16)
     ap.add_argument("--c2-ws", type=int, default=514)
+    ap.add_argument("--g-dzs", type=int, default=82)
+    ap.add_argument("--g-xr", type=int, default=29, help="conv_bwd4's xn row stride (round 6: 30)")
+    ap.add_argument("--g-swz", type=int, default=0, help="1: conv_bwd4's un-pool float2 stores row-swapped for ph 2, 3")
+    ap.add_argument("--only", default="", help="fc1_bwd_head / conv12_fwd / conv_bwd4: one kernel")
     a = ap.parse_args()
     a.h_rs = a.h_rs or (516 if a.layout == "r6" else 514)
     a.h_ds = a.h_ds or (520 if a.dhs_xor else 516)
-    fc1_bwd_head(a)
-    conv12_fwd(a)
+    for name, fn in (("fc1_bwd_head", fc1_bwd_head), ("conv12_fwd", conv12_fwd), ("conv_bwd4", conv_bwd4)):
+        if not a.only or a.only == name:
+            fn(a)
 
 
 if __name__ == "__main__":
