@@ -55,6 +55,10 @@ class XgmiAllReduce:
         self.n = int(n)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.prebarrier = False
+        where = (socket.gethostname(), self.device.index)
+        peers = [None] * self.world
+        dist.all_gather_object(peers, where, group=group)
+        self.ranks_on_device = sum(1 for p in peers if p == where)
         if nblk <= 0:
             # one workgroup per CU when every rank owns its GPU (the kernel's phase 1 reduces
             # the conv backward's slab -- 1.6 MB of 4-sample chunk rows + per-sample rows of the
@@ -62,11 +66,11 @@ class XgmiAllReduce:
             # 128 on the emulated W=2 exchange, 16.7 vs 18.2 us/launch, when the slab was the
             # round-2 6.5 MB per-sample form); 128 when ranks share a device (1-GPU
             # rehearsals), where every rank's blocks must be resident at once
-            where = (socket.gethostname(), self.device.index)
-            peers = [None] * self.world
-            dist.all_gather_object(peers, where, group=group)
             nblk = 256 if len(set(peers)) == self.world else 128
         self.nblk = int(nblk)
+        # the other ranks on this GPU can hold a spinning exchange workgroup on every CU: order every
+        # exchange behind a rank barrier (set_prebarrier; never on one rank per GPU)
+        self.crowded = (self.ranks_on_device - 1) * self.nblk >= 256
         self.lib = _native.load()
         self._ctx = ctypes.c_void_p()
         handle = ctypes.create_string_buffer(64)
@@ -85,6 +89,8 @@ class XgmiAllReduce:
             raise XgmiUnavailable(f"hipIpcOpenMemHandle failed: {flags}")
         self.alloc_kind = int(self.lib.pto_xar_alloc_kind(self._ctx))
         self.npad = int(self.lib.pto_xar_npad(self._ctx))
+        if self.crowded:
+            self.set_prebarrier(True)
 
     # ------------------------------------------------------------------ ops
     def _stream(self):

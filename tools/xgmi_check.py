@@ -123,8 +123,7 @@ def main(argv=None) -> int:
     res["conv_chunk"] = a.conv_chunk if a.conv_chunk > 0 else (1 if split else 4)
     res["fuse_conv12"] = bool(a.fuse_conv12) if a.fuse_conv12 >= 0 else not split
     res["ddp_form"] = "r5" if (budget_only if a.ddp_form == "auto" else a.ddp_form == "r5") else "fused"
-    if res["prebarrier"]:
-        xar.set_prebarrier(True)
+    xar.set_prebarrier(res["prebarrier"])  # XgmiAllReduce turns it on by itself when crowded
 
     def trainer(sync):
         cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -171,8 +170,8 @@ def main(argv=None) -> int:
     from pytorch_operator_amd.parallel.autotune import choose_grad_sync
     hnb = a.handover_nblk or xar.nblk
     hx = XgmiAllReduce(L, device=dev, nblk=hnb) if hnb != xar.nblk else xar
-    if hx is not xar and res["prebarrier"]:
-        hx.set_prebarrier(True)
+    if hx is not xar:
+        hx.set_prebarrier(res["prebarrier"])
     stamps_hx = hx.enable_stamps(64) if a.stamps and hx is not xar else None
     if hx is not xar:
         res["handover_self_test"] = hx.self_test()
