@@ -641,9 +641,10 @@ __global__ __launch_bounds__(64) void xar_prebarrier_kernel(XarArgs a) {
 // can be tested at any world size on a single GPU.  NT = kEmuThreads when the emulated
 // grid (W x nblk workgroups) would not fit the device with 256-thread workgroups (W = 8 x
 // 256: the production geometry); same chunking, flags and phases, fewer lanes per chunk.
-template <int NT>
+// FC: the fused DDP step's exchange (xar_kernel_fc), e.g. at the W = 8 x 256 production geometry.
+template <int NT, bool FC>
 __global__ __launch_bounds__(NT) void xar_kernel_emu(const XarArgs* __restrict__ all) {
-  xar_body<NT>(all[blockIdx.y], blockIdx.x);
+  xar_body<NT, FC>(all[blockIdx.y], blockIdx.x);
 }
 
 // Emulated producer push (what fc1_bwd does with XPush): every emulated rank (blockIdx.y)
@@ -916,8 +917,11 @@ int pto_xar_allreduce_sgd_fc(void* ctx, const float* grads, float* p, float* mbu
 }
 
 // ---- single-device emulation of `world` ranks (tests / latency floor) -------------------
-// Emulated workgroup size: 256 threads while W x nblk <= 1024 (4 per CU), else one wave.
-static int emu_threads(int world, int nblk) { return world * nblk <= 1024 ? kThreads : kEmuThreads; }
+// Emulated workgroup size: 256 threads while W x nblk <= 1024 (4 per CU: 4 waves of 104 VGPRs per
+// SIMD), else one wave.  The fc form's 160-VGPR waves fit 3 per SIMD: 256 threads up to 768.
+static int emu_threads(int world, int nblk, bool fc = false) {
+  return world * nblk <= (fc ? 768 : 1024) ? kThreads : kEmuThreads;
+}
 
 struct XarEmu {
   int world, nblk;
@@ -925,6 +929,7 @@ struct XarEmu {
   char* base[kMaxWorld];
   int* err;         // one word per emulated rank
   XarArgs* d_args;  // device copy of the per-rank arguments
+  XarArgs h_args[kMaxWorld];  // host copy (pto_xar_emu_set_fc amends it)
   long long timeout_ticks;
   unsigned long long* stamps;
   int light_fence;
@@ -1026,23 +1031,58 @@ int pto_xar_emu_set(void* ctx, int mode, const long long* in, const long long* d
     a.light_fence = e->light_fence;
     h[r] = a;
   }
+  for (int r = 0; r < e->world; ++r) e->h_args[r] = h[r];
   if (hipMemcpy(e->d_args, h, e->world * sizeof(XarArgs), hipMemcpyHostToDevice) != hipSuccess) return -2;
+  return 0;
+}
+
+// The fused DDP step's exchange on top of the last pto_xar_emu_set (mode 1, skip = [w1_off, n) as
+// pto_xar_allreduce_sgd_fc sets it): per emulated rank the step's activations, from which phase 1
+// computes the fc gradients (XarArgs::fc_tiles).  Arrays of `world` device addresses.
+int pto_xar_emu_set_fc(void* ctx, const long long* dh, const long long* a2, const long long* dlog,
+                       const long long* hh, const long long* per_sample, const long long* stats, int B,
+                       float loss_scale, long w1_off, long b1_off, long w2_off, long b2_off) {
+  XarEmu* e = static_cast<XarEmu*>(ctx);
+  if (B < 1 || ((w1_off | b1_off | w2_off | b2_off) & 3) || b1_off < w1_off + 400000 || w2_off < b1_off + 500 ||
+      b2_off < w2_off + 5000 || b2_off + 12 > e->n)
+    return -1;
+  for (int r = 0; r < e->world; ++r) {
+    XarArgs& a = e->h_args[r];
+    if (a.mode != 1 || a.skip_lo4 != (w1_off >> 2) || a.skip_hi4 != (e->n >> 2) ||
+        w1_off < (a.slab != nullptr ? a.conv4 * 4 : 0) ||
+        (a.slab != nullptr && (a.conv4 + e->nblk - 1) / e->nblk > emu_threads(e->world, e->nblk, true)))
+      return -1;
+    a.fc_tiles = 1;
+    a.fc_B = B;
+    a.fc_dh = reinterpret_cast<const float*>(dh[r]);
+    a.fc_a2 = reinterpret_cast<const float*>(a2[r]);
+    a.fc_dlog = reinterpret_cast<const float*>(dlog[r]);
+    a.fc_h = reinterpret_cast<const float*>(hh[r]);
+    a.fc_per_sample = per_sample != nullptr ? reinterpret_cast<const float*>(per_sample[r]) : nullptr;
+    a.fc_stats = stats != nullptr ? reinterpret_cast<float*>(stats[r]) : nullptr;
+    a.fc_loss_scale = loss_scale;
+    a.fc_w1_4 = w1_off >> 2;
+    a.fc_b1_4 = b1_off >> 2;
+    a.fc_w2_4 = w2_off >> 2;
+    a.fc_b2_4 = b2_off >> 2;
+  }
+  if (hipMemcpy(e->d_args, e->h_args, e->world * sizeof(XarArgs), hipMemcpyHostToDevice) != hipSuccess) return -2;
   return 0;
 }
 
 int pto_xar_emu_threads(void* ctx) {
   XarEmu* e = static_cast<XarEmu*>(ctx);
-  return emu_threads(e->world, e->nblk);
+  return emu_threads(e->world, e->nblk, e->h_args[0].fc_tiles != 0);
 }
 
 int pto_xar_emu_launch(void* ctx, void* stream) {
   XarEmu* e = static_cast<XarEmu*>(ctx);
-  if (emu_threads(e->world, e->nblk) == kThreads)
-    hipLaunchKernelGGL(xar_kernel_emu<kThreads>, dim3(e->nblk, e->world), dim3(kThreads), 0, (hipStream_t)stream,
-                       e->d_args);
-  else
-    hipLaunchKernelGGL(xar_kernel_emu<kEmuThreads>, dim3(e->nblk, e->world), dim3(kEmuThreads), 0,
-                       (hipStream_t)stream, e->d_args);
+  const bool fc = e->h_args[0].fc_tiles != 0;
+  const bool wide = emu_threads(e->world, e->nblk, fc) == kThreads;
+  void (*k)(const XarArgs*) = wide ? (fc ? xar_kernel_emu<kThreads, true> : xar_kernel_emu<kThreads, false>)
+                                   : (fc ? xar_kernel_emu<kEmuThreads, true> : xar_kernel_emu<kEmuThreads, false>);
+  hipLaunchKernelGGL(k, dim3(e->nblk, e->world), dim3(wide ? kThreads : kEmuThreads), 0, (hipStream_t)stream,
+                     e->d_args);
   return (int)hipGetLastError();
 }
 

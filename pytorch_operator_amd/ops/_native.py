@@ -162,6 +162,7 @@ _SIGNATURES = {
     "pto_xar_destroy": [_VP],
     "pto_xar_emu_create": [_I, _L, _I, ctypes.c_double, _I, _I, ctypes.POINTER(_VP)],
     "pto_xar_emu_set": [_VP, _I, _VP, _VP, _VP, _VP, _I, _L, _L, _I, _L, _L, _F, _F, _F, _F, _I, _I, _L, _L],
+    "pto_xar_emu_set_fc": [_VP] + [_VP] * 6 + [_I, _F, _L, _L, _L, _L],
     "pto_xar_emu_prepush": [_VP, _VP],
     "pto_xar_emu_launch": [_VP, _VP],
     "pto_xar_emu_error": [_VP],

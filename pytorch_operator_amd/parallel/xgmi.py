@@ -334,6 +334,18 @@ class XgmiEmulation:
             dampening, weight_decay, int(nesterov), int(first_step), int(skip[0]) if skip else 0,
             int(skip[1]) if skip else 0), "pto_xar_emu_set")
 
+    def configure_fc(self, dh, a2, dlog, h, per_sample, stats, B: int, loss_scale: float, offsets) -> None:
+        """The fused DDP step's exchange on top of ``configure(mode=1, skip=(fc1.weight offset, n))``:
+        per emulated rank the step's activations (lists of ``world`` tensors), from which the
+        exchange computes dW_fc1 / db_fc1 / dW_fc2 / db_fc2 and the loss statistics itself.
+        ``offsets``: flat-layout offsets of fc1.weight, fc1.bias, fc2.weight, fc2.bias."""
+        w1, b1, w2, b2 = (int(o) for o in offsets)
+        self._keep_fc = (dh, a2, dlog, h, per_sample, stats)
+        _native.check(self.lib.pto_xar_emu_set_fc(
+            self._ctx, self._ptrs(dh), self._ptrs(a2), self._ptrs(dlog), self._ptrs(h), self._ptrs(per_sample),
+            self._ptrs(stats), int(B), float(loss_scale), w1, b1, w2, b2), "pto_xar_emu_set_fc")
+        self.threads = int(self.lib.pto_xar_emu_threads(self._ctx))
+
     def prepush(self) -> None:
         _native.check(self.lib.pto_xar_emu_prepush(
             self._ctx, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "pto_xar_emu_prepush")
