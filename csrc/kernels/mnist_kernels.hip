@@ -628,7 +628,9 @@ __global__ __launch_bounds__(AB_NT) void conv12_fwd_kernel(
 // ---------------------------------------------------------------------------
 // KS = 2 (training path): K split over two blocks (blockIdx.z) of 5 waves each, 256
 // blocks on the 256 CUs with half the operand bytes per CU; each writes its pre-activation
-// partial to h + z * B * 500 and head_kernel adds the halves, bias and ReLU.
+// partial to h + z * B * 500, the z == 0 half with the bias added (round 6: the consumers --
+// fc1_bwd_head's 216 tiles, head_kernel -- then form relu(part0 + part1) without reloading b1:
+// 4 of every tile's 12 float4 staging loads), and the consumer adds the halves and the ReLU.
 template <int KS>
 __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
@@ -651,7 +653,7 @@ __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
   // epilogue operands of thread tid < 256, in flight with the GEMM loads
   const int l_e = tid >> 2, r_e = tid & 3;
   const int orow = mt * 16 + (l_e >> 4) * 4 + r_e, ocol = nt * 16 + (l_e & 15);
-  const float bo = (tid < 256 && ocol < 500) ? bias[ocol] : 0.f;
+  const float bo = (bias != nullptr && tid < 256 && ocol < 500) ? bias[ocol] : 0.f;
   f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
   for (int s = 0; s < 5; ++s) {
@@ -674,7 +676,7 @@ __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
     for (int q = 0; q < NW; ++q) s += red[q][l_e][r_e];
     if (orow < B && ocol < 500) {
       if (KS == 1) h[(size_t)orow * 500 + ocol] = fmaxf(s + bo, 0.f);
-      else h[((size_t)kz * B + orow) * 500 + ocol] = s;
+      else h[((size_t)kz * B + orow) * 500 + ocol] = kz == 0 ? s + bo : s;
     }
   }
 }
@@ -690,15 +692,15 @@ __global__ __launch_bounds__(640 / KS) void fc1_fwd_kernel(
 // 20 KB W2 stream of each sample lands on its own CU (4 waves per block put 80 KB of
 // L2 traffic on each of 16 CUs); the eval path (B = 1000) keeps 4 to cut the atomics.
 // ---------------------------------------------------------------------------
-// With hp2 (the split-K fc1 path): h = relu(h + hp2 + b1) is formed here and written to
-// h_out for the backward.
+// With hp2 (the split-K fc1 path, the bias folded into the first partial h): h = relu(h + hp2)
+// is formed here and written to h_out for the backward.
 template <int WPB>
 __global__ __launch_bounds__(64 * WPB) void head_kernel(
     const float* __restrict__ h, const float* __restrict__ w2, const float* __restrict__ b2,
     const int* __restrict__ lab, int B, float grad_scale, float loss_scale,
     float* __restrict__ dlogits, float* __restrict__ dh, float* __restrict__ logp_out,
     float* __restrict__ per_sample, float* __restrict__ stats, const float* __restrict__ hp2,
-    const float* __restrict__ b1, float* __restrict__ h_out, u64* dbg) {
+    float* __restrict__ h_out, u64* dbg) {
   __shared__ float red[2][WPB];
   const int tid = threadIdx.x, lane = tid & 63, wq = tid >> 6;
   stamp(dbg, 0);
@@ -716,15 +718,13 @@ __global__ __launch_bounds__(64 * WPB) void head_kernel(
     float4 h0 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o0);
     float4 h1 = *reinterpret_cast<const float4*>(h + (size_t)bc * 500 + o1);
     if (hp2 != nullptr) {
-      // the second split-K fc1 partial
+      // the second split-K fc1 partial (the first holds the bias)
       const float4 q0 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o0);
       const float4 q1 = *reinterpret_cast<const float4*>(hp2 + (size_t)bc * 500 + o1);
-      const float4 c0 = *reinterpret_cast<const float4*>(b1 + o0);
-      const float4 c1 = *reinterpret_cast<const float4*>(b1 + o1);
-      h0 = make_float4(fmaxf(h0.x + q0.x + c0.x, 0.f), fmaxf(h0.y + q0.y + c0.y, 0.f),
-                       fmaxf(h0.z + q0.z + c0.z, 0.f), fmaxf(h0.w + q0.w + c0.w, 0.f));
-      h1 = make_float4(fmaxf(h1.x + q1.x + c1.x, 0.f), fmaxf(h1.y + q1.y + c1.y, 0.f),
-                       fmaxf(h1.z + q1.z + c1.z, 0.f), fmaxf(h1.w + q1.w + c1.w, 0.f));
+      h0 = make_float4(fmaxf(h0.x + q0.x, 0.f), fmaxf(h0.y + q0.y, 0.f), fmaxf(h0.z + q0.z, 0.f),
+                       fmaxf(h0.w + q0.w, 0.f));
+      h1 = make_float4(fmaxf(h1.x + q1.x, 0.f), fmaxf(h1.y + q1.y, 0.f), fmaxf(h1.z + q1.z, 0.f),
+                       fmaxf(h1.w + q1.w, 0.f));
       if (bvalid) {
         float4* ho = reinterpret_cast<float4*>(h_out + (size_t)b * 500);
         if (v0) ho[k0 >> 2] = h0;
@@ -1099,7 +1099,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
 // E': fc1 backward with the head fused in (the world-1 step, round 5).  Replaces the head launch
 // and its kernel boundary.  Every dz2 block (mt, kt) of fc1_bwd's layout recomputes the head of
 // its 16 samples on MFMA, then runs the dz2 job on that dh:
-//   h  = relu(p0 + p1 + b1)                      (the split-K fc1 partials; into LDS)
+//   h  = relu(p0 + p1)                           (the split-K fc1 partials, p0 with the bias; into LDS)
 //   logits = h . W2^T + b2                       (M 16 samples, N 16 (10), K 512 over 8 waves)
 //   log-softmax, NLL, d(logits) = (softmax - onehot) / B        (one thread per sample)
 //   dh = (d(logits) . W2) * (h > 0)             (M 16, N 512, K 16; each wave its own 64 k)
@@ -1110,7 +1110,7 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_kernel(Fc1Bwd a, u64* dbg) {
 // (dW_fc1, dW_fc2, statistics).  Sums differ from
 // head_kernel's lane-tree order by fp32 rounding (the DDP paths keep head + fc1_bwd).
 struct Fc1BwdHead {
-  const float *hp0, *hp1, *b1;  // fc1 split-K partials [B][500] x 2, fc1.bias [500]
+  const float *hp0, *hp1;       // fc1 split-K partials [B][500] x 2 (hp0 includes fc1.bias)
   const float *w2, *b2;         // fc2.weight [10][500], fc2.bias [10]
   const int* lab;               // [B]
   const float* a2;              // [B][800]
@@ -1195,10 +1195,9 @@ __global__ __launch_bounds__(E_NT) void fc1_bwd_head_kernel(Fc1BwdHead a, u64* d
     const size_t o = (size_t)min(mt * 16 + row, B - 1) * 500 + 4 * c4;
     const float4 x0 = *reinterpret_cast<const float4*>(a.hp0 + o);
     const float4 x1 = *reinterpret_cast<const float4*>(a.hp1 + o);
-    const float4 c = *reinterpret_cast<const float4*>(a.b1 + 4 * c4);
-    // head_kernel's h: relu((part0 + part1) + b1)
-    hq[q] = make_float4(fmaxf(x0.x + x1.x + c.x, 0.f), fmaxf(x0.y + x1.y + c.y, 0.f),
-                        fmaxf(x0.z + x1.z + c.z, 0.f), fmaxf(x0.w + x1.w + c.w, 0.f));
+    // head_kernel's h: relu(part0 + part1), the bias folded into part0 by fc1_fwd
+    hq[q] = make_float4(fmaxf(x0.x + x1.x, 0.f), fmaxf(x0.y + x1.y, 0.f), fmaxf(x0.z + x1.z, 0.f),
+                        fmaxf(x0.w + x1.w, 0.f));
   }
   float4 wq[3];
 #pragma unroll
@@ -2587,33 +2586,32 @@ int pto_mnist_fc1_ks() { return FC1_KS; }
 // conv_bwd4's dynamic LDS (bytes): not in the code object's metadata (tests/test_kernel_resources.py)
 int pto_mnist_conv_bwd4_lds() { return G_LDS * (int)sizeof(float); }
 
-// Split-K fc1: pre-activation partials to parts[KS][B][500] (head_kernel finishes h).
-int pto_mnist_fc1_fwd_parts(const float* x, const float* w, float* parts, int B, void* stream) {
+// Split-K fc1: pre-activation partials to parts[KS][B][500], the bias (may be null) added to
+// parts[0] (head_kernel / fc1_bwd_head finish h = relu(parts[0] + parts[1])).
+int pto_mnist_fc1_fwd_parts(const float* x, const float* w, const float* bias, float* parts, int B, void* stream) {
   PTO_CHECK_B(B);
   if ((((uintptr_t)x) | ((uintptr_t)w) | ((uintptr_t)parts)) & 15) return -2;
   hipLaunchKernelGGL(fc1_fwd_kernel<FC1_KS>, dim3(32, (B + 15) / 16, FC1_KS), dim3(640 / FC1_KS), 0,
-                     (hipStream_t)stream, x, w, nullptr, parts, B, dbg_next());
+                     (hipStream_t)stream, x, w, bias, parts, B, dbg_next());
   return (int)hipGetLastError();
 }
 
 int pto_mnist_head(const float* h, const float* w2, const float* b2, const int* lab, int B,
                    float grad_scale, float loss_scale, float* dlogits, float* dh, float* logp,
-                   float* per_sample, float* stats, const float* hp2, const float* b1, float* h_out,
-                   void* stream) {
+                   float* per_sample, float* stats, const float* hp2, float* h_out, void* stream) {
   PTO_CHECK_B(B);
   if (lab == nullptr) return -1;
-  if (hp2 != nullptr && (b1 == nullptr || h_out == nullptr)) return -1;
-  if ((((uintptr_t)h) | ((uintptr_t)w2) | ((uintptr_t)dh) | ((uintptr_t)hp2) | ((uintptr_t)b1) |
-       ((uintptr_t)h_out)) & 15)
+  if (hp2 != nullptr && h_out == nullptr) return -1;
+  if ((((uintptr_t)h) | ((uintptr_t)w2) | ((uintptr_t)dh) | ((uintptr_t)hp2) | ((uintptr_t)h_out)) & 15)
     return -2;  // float4 rows
   if (stats == nullptr)
     hipLaunchKernelGGL(head_kernel<1>, dim3(B), dim3(64), 0, (hipStream_t)stream, h, w2, b2, lab,
-                       B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, hp2, b1,
+                       B, grad_scale, loss_scale, dlogits, dh, logp, per_sample, stats, hp2,
                        h_out, dbg_next());
   else
     hipLaunchKernelGGL(head_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, h,
                        w2, b2, lab, B, grad_scale, loss_scale, dlogits, dh, logp, per_sample,
-                       stats, hp2, b1, h_out, dbg_next());
+                       stats, hp2, h_out, dbg_next());
   return (int)hipGetLastError();
 }
 
@@ -2867,21 +2865,21 @@ int pto_mnist_tail_grads(const float* P, int B, int n, int stride, float* gout, 
 // fc1_bwd with the head fused in (fc1_bwd_head_kernel): dz2 from the split-K fc1 partials hp0/hp1;
 // publishes h_out, dh_out [B][500], dlog_out [B][10], per_sample [B][2]; with stage_x, also the
 // next-batch staging blocks (as pto_mnist_fc1_bwd_stage).
-int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* b1, const float* w2, const float* b2,
+int pto_mnist_fc1_bwd_head(const float* hp0, const float* hp1, const float* w2, const float* b2,
                            const int* lab, const float* a2, const uint8_t* idx2, const float* w1, float* dz2,
                            float* h_out, float* dh_out, float* dlog_out, float* per_sample, float grad_scale, int B,
                            const void* nx, const int* nlabels, const int* nperm, const int* ncursor, int n_total,
                            int stage_adv, uint8_t* stage_x, int* stage_lab, int* stage_tag, float* dpool,
                            void* stream) {
   PTO_CHECK_B(B);
-  if (hp0 == nullptr || hp1 == nullptr || b1 == nullptr || w2 == nullptr || b2 == nullptr || lab == nullptr ||
+  if (hp0 == nullptr || hp1 == nullptr || w2 == nullptr || b2 == nullptr || lab == nullptr ||
       a2 == nullptr || idx2 == nullptr || w1 == nullptr || (dz2 == nullptr && dpool == nullptr) ||
       h_out == nullptr || dh_out == nullptr || dlog_out == nullptr || per_sample == nullptr)
     return -1;
-  if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)b1) | ((uintptr_t)w2) | ((uintptr_t)h_out) | ((uintptr_t)dh_out)) & 15)
+  if ((((uintptr_t)hp0) | ((uintptr_t)hp1) | ((uintptr_t)w2) | ((uintptr_t)h_out) | ((uintptr_t)dh_out)) & 15)
     return -2;  // float4 rows
   Fc1BwdHead a{};
-  a.hp0 = hp0; a.hp1 = hp1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.lab = lab; a.a2 = a2; a.idx2 = idx2; a.w1 = w1;
+  a.hp0 = hp0; a.hp1 = hp1; a.w2 = w2; a.b2 = b2; a.lab = lab; a.a2 = a2; a.idx2 = idx2; a.w1 = w1;
   a.dz2 = dz2; a.dpool = dpool; a.h_out = h_out; a.dh_out = dh_out; a.dlog_out = dlog_out; a.per_sample = per_sample;
   a.grad_scale = grad_scale; a.B = B;
   int nst = 0;

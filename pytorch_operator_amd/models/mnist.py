@@ -335,15 +335,16 @@ class FusedMnistTrainer:
             K.conv2_fwd(self.a1[:B], p["conv2.weight"], p["conv2.bias"], out=self.a2[:B],
                         idx=self.idx2[:B])
         ks = self.fc1_ks
-        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], out=self.h_parts[:ks * B * 500].view(ks, B, 500))
+        K.fc1_fwd_parts(self.a2[:B], p["fc1.weight"], p["fc1.bias"],
+                        out=self.h_parts[:ks * B * 500].view(ks, B, 500))
 
     def _head(self, B: int) -> None:
-        """h = relu(part0 + part1 + b1), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
+        """h = relu(part0 + part1) (part0 holds the bias), fc2, log-softmax, NLL, d(logits), dh (one launch)."""
         K, p = self.K, self._pv
         hp = self.h_parts[:self.fc1_ks * B * 500].view(self.fc1_ks, B, 500)
         K.head(hp[0], p["fc2.weight"], p["fc2.bias"], self.lab[:B], grad_scale=1.0 / B,
                per_sample=self.per_sample[:B], dlogits=self.dlogits[:B], dh=self.dh[:B],
-               h_second=hp[1], fc1_bias=p["fc1.bias"], h_out=self.h1[:B])
+               h_second=hp[1], h_out=self.h1[:B])
 
     def _dz2_out(self, B: int) -> dict:
         """Where the input-gradient job writes: d(a2) still pooled ([B, 800], 3.2 KB per sample; conv_bwd4
@@ -370,7 +371,7 @@ class FusedMnistTrainer:
         """fc1_bwd with the head fused in (ops.mnist.fc1_bwd_head)."""
         K, p = self.K, self._pv
         st = self._stage_for(None)
-        K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc1.bias"], p["fc2.weight"], p["fc2.bias"],
+        K.fc1_bwd_head(self.h_parts[:2 * B * 500].view(2, B, 500), p["fc2.weight"], p["fc2.bias"],
                        self.lab[:B], self.a2[:B], self.idx2[:B], p["fc1.weight"], **self._dz2_out(B),
                        h_out=self.h1[:B], dh_out=self.dh[:B], dlog_out=self.dlogits[:B],
                        per_sample=self.per_sample[:B], grad_scale=1.0 / B,

@@ -129,8 +129,8 @@ _SIGNATURES = {
     "pto_slab_reduce_sgd": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                             _VP, _VP, _VP, _I, _I, _I, _I, _VP],
     "pto_mnist_fc1_fwd": [_VP, _VP, _VP, _VP, _I, _VP],
-    "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
-    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _I, _VP],
+    "pto_mnist_head": [_VP, _VP, _VP, _VP, _I, _F, _F, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_fwd_parts": [_VP, _VP, _VP, _VP, _I, _VP],
     "pto_mnist_fc1_ks": [],
     "pto_mnist_fc1_bwd": [_VP] * 13 + [_F, _I, _I, _VP, _VP],
     "pto_mnist_conv_bwd": [_VP] * 10 + [_I, _I, _VP],
@@ -141,7 +141,7 @@ _SIGNATURES = {
     "pto_mnist_tail": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP, _I, _I, _I]
                       + [_VP] * 9 + [_F] + [_VP] * 7,
     "pto_mnist_tail_grads": [_VP, _I, _I, _I, _VP, _I, _I, _I] + [_VP] * 7 + [_F, _VP, _VP, _VP],
-    "pto_mnist_fc1_bwd_head": [_VP] * 14 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP, _VP],
+    "pto_mnist_fc1_bwd_head": [_VP] * 13 + [_F, _I] + [_VP] * 4 + [_I, _I, _VP, _VP, _VP, _VP, _VP],
     "pto_slab_reduce_sgd_w1": [_VP, _I, _I, _I, _VP, _VP, _VP, _F, _F, _F, _F, _F, _I, _I, _VP,
                                _VP, _VP, _VP, _I, _I, _I, _I] + [_VP] * 6,
     "pto_mnist_fc1_bwd_push": [_VP] * 13 + [_F, _I, _VP, _I, _I, _L, _L, _VP, _VP, _VP],

@@ -238,19 +238,22 @@ def fc1_split() -> int:
     return FC1_KS
 
 
-def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def fc1_fwd_parts(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Split-K fc1 forward: the pre-activation partials ``out[z] = x[:, Kz] @ w[:, Kz].T`` over
-    2 K slices (2 x 400) as fp32 [2, B, 500]; ``head(..., h_second=out[1], fc1_bias=b,
-    h_out=h)`` finishes ``h = relu(out[0] + out[1] + b)``.  256 workgroups instead of 128: half
-    the operand bytes per CU on the latency-bound load phase."""
+    2 K slices (2 x 400) as fp32 [2, B, 500], ``bias`` added to ``out[0]``; ``head(...,
+    h_second=out[1], h_out=h)`` and ``fc1_bwd_head`` finish ``h = relu(out[0] + out[1])``.  256
+    workgroups instead of 128: half the operand bytes per CU on the latency-bound load phase."""
     lib = _native.load()
     B = x.shape[0]
     ks = fc1_split()
     _req(x, (B, 800), torch.float32, "x")
     _req(w, (500, 800), torch.float32, "fc1.weight")
+    if bias is not None:
+        _req(bias, (500,), torch.float32, "fc1.bias")
     out = torch.empty((ks, B, 500), device=x.device) if out is None else out
     _req(out, (ks, B, 500), torch.float32, "fc1 partials")
-    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, _stream())
+    rc = lib.pto_mnist_fc1_fwd_parts(x.data_ptr(), w.data_ptr(), _ptr(bias), out.data_ptr(), B, _stream())
     _native.check(rc, "fc1_fwd_parts")
     return out
 
@@ -260,24 +263,22 @@ def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *
          want_logp: bool = False, stats: Optional[torch.Tensor] = None,
          per_sample: Optional[torch.Tensor] = None, dlogits: Optional[torch.Tensor] = None,
          dh: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None,
-         h_second: Optional[torch.Tensor] = None, fc1_bias: Optional[torch.Tensor] = None,
-         h_out: Optional[torch.Tensor] = None):
+         h_second: Optional[torch.Tensor] = None, h_out: Optional[torch.Tensor] = None):
     """fc2 + log_softmax + nll (+ d(logits), dh with the fc1 ReLU mask).
 
     ``lab``: int32 [B] targets (``conv1_fwd`` gathers them).  ``per_sample`` (fp32
     [B,2]) receives (loss, correct) per sample; ``stats`` (fp32 [>=2]) accumulates
     ``sum(loss)*loss_scale`` and the correct count atomically.  With ``h_second``
     (``fc1_fwd_parts``), ``h`` is the first split-K half: the kernel forms
-    ``relu(h + h_second + fc1_bias)`` and writes it to ``h_out``.
+    ``relu(h + h_second)`` (``h`` holds the bias) and writes it to ``h_out``.
     """
     lib = _native.load()
     B = h.shape[0]
     _req(h, (B, 500), torch.float32, "h1")
     if h_second is not None:
         _req(h_second, (B, 500), torch.float32, "h_second")
-        if fc1_bias is None or h_out is None:
-            raise ValueError("h_second needs fc1_bias and h_out")
-        _req(fc1_bias, (500,), torch.float32, "fc1.bias")
+        if h_out is None:
+            raise ValueError("h_second needs h_out")
         _req(h_out, (B, 500), torch.float32, "h_out")
     _req(w, (10, 500), torch.float32, "fc2.weight")
     _req(b, (10,), torch.float32, "fc2.bias")
@@ -302,7 +303,7 @@ def head(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, lab: torch.Tensor, *
     rc = lib.pto_mnist_head(h.data_ptr(), w.data_ptr(), b.data_ptr(), lab.data_ptr(), B,
                             float(grad_scale), float(loss_scale), _ptr(dlogits), _ptr(dh),
                             _ptr(logp), _ptr(per_sample), _ptr(stats), _ptr(h_second),
-                            _ptr(fc1_bias), _ptr(h_out), _stream())
+                            _ptr(h_out), _stream())
     _native.check(rc, "head")
     return dlogits, dh, logp
 
@@ -389,13 +390,13 @@ def fc1_bwd(dh, a2, idx2, w1, dlogits, h, gw1, gb1, gw2, gb2, dz2=None, per_samp
     return out
 
 
-def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh_out, dlog_out, per_sample,
+def fc1_bwd_head(h_parts, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh_out, dlog_out, per_sample,
                  grad_scale: float, src: Optional[BatchSource] = None, stage: Optional["BatchStage"] = None,
                  stage_adv: int = 1, dpool: Optional[torch.Tensor] = None) -> None:
     """fc1 backward with the head fused in (one launch instead of head + fc1_bwd; the world-1
-    step).  ``h_parts``: the split-K fc1 pre-activation partials [2, B, 500].  Writes dz2 (or,
-    with ``dz2=None`` and ``dpool`` [B, 800], the pooled d(a2) -- see ``fc1_bwd``) and
-    publishes h = relu(p0 + p1 + b1), dh, d(logits) and per-sample (loss, correct) for the
+    step).  ``h_parts``: the split-K fc1 pre-activation partials [2, B, 500], the bias in
+    ``h_parts[0]`` (``fc1_fwd_parts(..., bias)``).  Writes dz2 (or, with ``dz2=None`` and ``dpool``
+    [B, 800], the pooled d(a2) -- see ``fc1_bwd``) and publishes h = relu(p0 + p1), dh, d(logits) and per-sample (loss, correct) for the
     tail (``tail_``).  With ``src`` + ``stage`` it also stages the batch of step
     ``cursor + stage_adv`` (as ``fc1_bwd``)."""
     lib = _native.load()
@@ -403,7 +404,6 @@ def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh
     if h_parts.dim() != 3 or h_parts.shape[0] != 2 or tuple(h_parts.shape[1:]) != (B, 500) or \
             h_parts.dtype != torch.float32 or not h_parts.is_contiguous():
         raise ValueError("h_parts must be contiguous fp32 [2, B, 500]")
-    _req(fc1_bias, (500,), torch.float32, "fc1.bias")
     _req(w2, (10, 500), torch.float32, "fc2.weight")
     _req(b2, (10,), torch.float32, "fc2.bias")
     _req(lab, (B,), torch.int32, "labels")
@@ -426,7 +426,7 @@ def fc1_bwd_head(h_parts, fc1_bias, w2, b2, lab, a2, idx2, w1, *, dz2, h_out, dh
             raise ValueError("staging needs a uint8 BatchSource with labels, perm, cursor and a large enough stage")
         st = (src.x.data_ptr(), src.labels.data_ptr(), src.perm.data_ptr(), src.cursor.data_ptr(), src.n_total,
               int(stage_adv), stage.x.data_ptr(), stage.lab.data_ptr(), stage.tag.data_ptr())
-    rc = lib.pto_mnist_fc1_bwd_head(h_parts[0].data_ptr(), h_parts[1].data_ptr(), fc1_bias.data_ptr(), w2.data_ptr(),
+    rc = lib.pto_mnist_fc1_bwd_head(h_parts[0].data_ptr(), h_parts[1].data_ptr(), w2.data_ptr(),
                                     b2.data_ptr(), lab.data_ptr(), a2.data_ptr(), idx2.data_ptr(), w1.data_ptr(),
                                     _ptr(dz2), h_out.data_ptr(), dh_out.data_ptr(), dlog_out.data_ptr(),
                                     per_sample.data_ptr(), float(grad_scale), B, *st, _ptr(dpool), _stream())

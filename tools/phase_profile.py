@@ -56,7 +56,7 @@ def main():
                                                p["conv2.bias"], B, a1=tr.a1, idx1=tr.idx1, xn=tr.xn, lab=tr.lab,
                                                a2=tr.a2, idx2=tr.idx2, stage=tr.stage)),
         ("fc1_fwd", lambda: K.fc1_fwd(tr.a2, p["fc1.weight"], p["fc1.bias"], out=tr.h1)),
-        ("fc1_parts", lambda: K.fc1_fwd_parts(tr.a2, p["fc1.weight"],
+        ("fc1_parts", lambda: K.fc1_fwd_parts(tr.a2, p["fc1.weight"], p["fc1.bias"],
                                               out=tr.h_parts[:2 * B * 500].view(2, B, 500))),
         ("head_parts", lambda: tr._head(B)),
         ("fc1_bwd", lambda: tr._fc1_bwd(B, stage_adv=0)),
