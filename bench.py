@@ -398,9 +398,9 @@ def main(argv=None):
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize(dev)
-    if pg:
+    if pg:  # every rank's GPU work done, then the barrier, then this rank's device once more
         dist.barrier()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
