@@ -394,8 +394,9 @@ def main(argv=None):
 
     # no garbage-collector pass inside the timed region (as timeit does): after torch's imports an
     # automatic generation-0 / -1 collection stalls the host 0.2 / 1.5 ms (measured on the CPU),
-    # 10-75 us per step at the driver's K = 20 once the GPU drains the queued launches
-    gc.collect()
+    # 10-75 us per step at the driver's K = 20 once the GPU drains the queued launches.  No explicit
+    # collection here: its ~90 ms of GPU idle right before the region lets the clocks drop (K = 20
+    # measured 39.5-40.0 instead of 35.9-36.1 us, profiles/r6_twostream/gc_collect_k20.txt)
     gc.disable()
     torch.cuda.synchronize(dev)
     if pg:
