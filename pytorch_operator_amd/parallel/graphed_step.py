@@ -9,12 +9,15 @@ Modes
 -----
 ``eager``       plain launches (debugging / first step).
 ``graph``       no collectives (world 1): one graph holding ``steps_per_graph`` whole steps.
-                RCCL collectives (world > 1, or forced at world 1): three graphs per step -- G1 (forward + fc backward),
-                G2 (conv backward), G3 (SGD) -- with the two bucket all-reduces
-                issued eagerly between them (the fc bucket's RCCL all-reduce
-                overlaps G2 on RCCL's own stream; G3 waits for both).  With
-                ``launch="stream"`` the three pieces are native recordings whose
-                kernel lists are launched directly on the stream.
+                RCCL collectives (world > 1, or forced at world 1), the round-6 fused form
+                (``trainer.fused_ok()``): two pieces per step -- the five launches up to the
+                complete flat gradient (``forward_backward_fused``), then the SGD launch -- with
+                ONE all-reduce of the whole gradient issued eagerly between them.  The round-5
+                form (``ddp_fused`` off): three pieces -- G1 (forward + fc backward), G2 (conv
+                backward), G3 (SGD) -- with the two bucket all-reduces between them (the fc
+                bucket's overlaps G2 on RCCL's own stream; G3 waits for both).  With
+                ``launch="stream"`` the pieces are native recordings whose kernel lists are
+                launched directly on the stream.
 ``graph-comm``  the all-reduces are captured too: one graph per step (RCCL
                 collectives support stream capture).  Fewest host calls.
 
