@@ -4,8 +4,11 @@
 //   conv1(1->20,k5) -> ReLU -> maxpool2 -> conv2(20->50,k5) -> ReLU -> maxpool2
 //   -> fc1(800->500) -> ReLU -> fc2(500->10) -> log_softmax -> nll_loss(mean)
 //
-// The single-GPU training step is 5 launches (round 5; world_size > 1: 6, the head and fc1_bwd
-// separate and the tail launch the xGMI exchange of xgmi_allreduce.hip, or RCCL buckets).  At B=64
+// The single-GPU training step is 5 launches (round 5).  World size > 1 (round 6) keeps the first
+// four: over xGMI the exchange of xgmi_allreduce.hip replaces the tail and computes the fc
+// gradient tiles itself (mnist_fc_grads.h, shared with the tail), over RCCL the tail runs
+// gradient-only (pto_mnist_tail_grads) before ONE all-reduce and the SGD launch; the round-5
+// forms (head + fc1_bwd, 6 launches) stay as start-up race candidates.  At B=64
 // the step is ~0.84 GFLOP: it is latency-bound, so every kernel is shaped to (a) issue all of its
 // global loads up front (no load -> use -> load chains, no predicated loads, at most the 63 loads
 // vmcnt can track), (b) keep its MFMA chains short by splitting K across the waves of a workgroup,
@@ -17,7 +20,7 @@
 //                      chains; bias + ReLU + pool (argmax) into an LDS im2col image; conv2 as an
 //                      implicit GEMM on v_mfma_f32_16x16x4_f32, bias + ReLU + pool in the epilogue;
 //                      a1 / idx1 published per channel group by the waves conv2's epilogue idles
-//   C  fc1_fwd<2>      split-K MFMA GEMM (256 workgroups), pre-activation halves
+//   C  fc1_fwd<2>      split-K MFMA GEMM (256 workgroups), pre-activation halves (bias in the first)
 //   E' fc1_bwd_head    per (16-sample, 16-feature) tile: the head recomputed on MFMA (h, logits,
 //                      DPP log-softmax / NLL, d(logits), dh on 4x4x1 chains), then d(a2) =
 //                      relu'(a2) . (dh W1) written pooled; next-batch staging blocks
