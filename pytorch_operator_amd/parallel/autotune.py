@@ -122,7 +122,7 @@ def crosscheck_step(tr, rccl_sync, xgmi_sync, dev, rtol: float = 1e-4) -> Dict:
     snap = (tr.flat_params.clone(), tr.flat_momentum.clone(), tr.cursor.clone())
     tr.grad_sync = rccl_sync
     tr.train_step()
-    p_ref, m_ref = tr.flat_params.clone(), tr.flat_momentum.clone()
+    p_ref, m_ref, c_ref = tr.flat_params.clone(), tr.flat_momentum.clone(), tr.cursor.clone()
     tr.flat_params.copy_(snap[0])
     tr.flat_momentum.copy_(snap[1])
     tr.cursor.copy_(snap[2])
@@ -146,7 +146,17 @@ def crosscheck_step(tr, rccl_sync, xgmi_sync, dev, rtol: float = 1e-4) -> Dict:
         pe = me = float("inf")
         ok, err = False, -1
         tr.last_crosscheck_error = repr(e)[:200]
-    return {"ok": _agree(ok, dev), "param_err": pe, "mom_err": me, "xgmi_error": err}
+    ok = _agree(ok, dev)
+    if not ok:
+        # the dropped candidate's step may have left anything behind (a timed-out exchange stops
+        # half-way): continue from the RCCL step's state, which every rank holds
+        tr.flat_params.copy_(p_ref)
+        tr.flat_momentum.copy_(m_ref)
+        tr.cursor.copy_(c_ref)
+        if hasattr(tr, "invalidate_stage"):
+            tr.invalidate_stage()
+        _sync(dev)
+    return {"ok": ok, "param_err": pe, "mom_err": me, "xgmi_error": err}
 
 
 def _agree(flag: bool, dev) -> bool:

@@ -155,7 +155,7 @@ def _xc_worker(rank, world, port, scenario, q):
     bad = scenario == "wrong" and rank == 1
     try:
         _, pick, rec = at.choose_grad_sync(tr, Sync(1.0), XSync(1.001 if bad else 1.0), trial_steps=2)
-        q.put((rank, pick, rec, int(tr.cursor.item()), tr.staged))
+        q.put((rank, pick, rec, int(tr.cursor.item()), tr.staged, tr.flat_params.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -169,8 +169,8 @@ def _xc_race(scenario):
         p.start()
     out = {}
     for _ in ps:
-        rank, pick, rec, cursor, staged = q.get(timeout=120)
-        out[rank] = (pick, rec, cursor, staged)
+        rank, pick, rec, cursor, staged, params = q.get(timeout=120)
+        out[rank] = (pick, rec, cursor, staged, params)
     for p in ps:
         p.join(30)
         assert p.exitcode == 0
@@ -179,7 +179,7 @@ def _xc_race(scenario):
 
 @pytest.mark.timeout(180)
 def test_xgmi_candidates_pass_the_step_crosscheck():
-    for rank, (pick, rec, cursor, staged) in _xc_race("right").items():
+    for rank, (pick, rec, cursor, staged, _) in _xc_race("right").items():
         cc = rec["xgmi_crosscheck"]
         assert set(cc) == {"xgmi", "xgmi-r5"} and all(v["ok"] for v in cc.values()), cc
         assert all(v["param_err"] < 1e-6 for v in cc.values()), cc
@@ -191,8 +191,17 @@ def test_xgmi_candidates_pass_the_step_crosscheck():
 
 @pytest.mark.timeout(180)
 def test_a_wrong_xgmi_step_on_one_rank_drops_the_candidates_everywhere():
-    for rank, (pick, rec, cursor, staged) in _xc_race("wrong").items():
+    out = _xc_race("wrong")
+    # the RCCL trajectory: two steps (one per dropped candidate's check), gradient scale 1
+    p, m = torch.linspace(-1, 1, 100), torch.zeros(100)
+    for c in range(2):
+        m = m.mul(0.5).add(torch.sin(p + c))
+        p = p - 0.01 * m
+    for rank, (pick, rec, cursor, staged, params) in out.items():
         assert pick.startswith("rccl"), (pick, rec)
         assert rec["xgmi_ms_per_step"] is None and rec["xgmi_skipped"].startswith("cross-check vs RCCL failed")
         assert rec["xgmi_r5_skipped"].startswith("cross-check vs RCCL failed")
         assert not rec["xgmi_crosscheck"]["xgmi"]["ok"]
+        # a dropped candidate's step is undone: every rank continues from the RCCL step's state
+        assert cursor == 2 and staged == 4
+        assert torch.equal(torch.tensor(params), p), rank
