@@ -271,6 +271,21 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
             t = _timed(r, trial, dev, name)
             steps += r.internal_steps + trial
             times[name] = float("inf") if xgmi_sync.xar.error() else t
+    resynced = False
+    if xgmi_sync is not None:
+        # an exchange that timed out mid-trial may have stopped half-way on some ranks only: agree
+        # on it, drop both xGMI forms everywhere, and restart every replica from rank 0's state
+        bad = {n for n in ("xgmi", "xgmi-r5") if times.get(n) == float("inf")}
+        if not _agree(not bad, dev):
+            for n in ("xgmi", "xgmi-r5"):
+                if n in times:
+                    times[n] = float("inf")
+            xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+            _sync(dev)
+            dist.broadcast(tr.flat_params, 0)
+            dist.broadcast(tr.flat_momentum, 0)
+            _sync(dev)
+            resynced = True
     if force is not None:
         if force not in runners:
             raise ValueError(f"force={force!r}: candidate not available ({skipped.get(force, 'unknown')})")
@@ -302,6 +317,7 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
         record["xgmi_crosscheck"] = crosscheck
     if times.get("xgmi") == float("inf") or times.get("xgmi-r5") == float("inf"):
         record["xgmi_error"] = int(xgmi_sync.xar.error())
+        record["xgmi_resynced_from_rank0"] = resynced
     record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,
                    "steps": steps, "ddp_form": "r5" if forms[pick] else "fused"})
     return runners[pick], pick, record

@@ -110,11 +110,13 @@ def _xc_worker(rank, world, port, scenario, q):
             self.scale = scale
 
     class Xar:
+        err = 0
+
         def gather_sharded_(self, m):
             pass
 
         def error(self):
-            return 0
+            return self.err
 
     class XSync(Sync):
         xar = Xar()
@@ -144,10 +146,12 @@ def _xc_worker(rank, world, port, scenario, q):
 
     class FakeStep:
         def __init__(self, tr, mode="graph", steps_per_graph=1, launch="graph", **kw):
-            self.internal_steps, self.launch = 0, launch
+            self.internal_steps, self.launch, self.tr = 0, launch, tr
 
         def warm(self, n):
-            pass
+            if scenario == "timeout" and rank == 1 and isinstance(self.tr.grad_sync, XSync):
+                self.tr.flat_params.add_(1.0)  # an exchange that stopped half-way
+                XSync.xar.err = 4
 
     at.GraphedStep = FakeStep
     at.graph_comm_precheck = lambda tr: "no capture here"
@@ -205,3 +209,13 @@ def test_a_wrong_xgmi_step_on_one_rank_drops_the_candidates_everywhere():
         # a dropped candidate's step is undone: every rank continues from the RCCL step's state
         assert cursor == 2 and staged == 4
         assert torch.equal(torch.tensor(params), p), rank
+
+
+@pytest.mark.timeout(180)
+def test_an_exchange_error_on_one_rank_resyncs_every_replica():
+    out = _xc_race("timeout")
+    for rank, (pick, rec, cursor, staged, params) in out.items():
+        assert pick.startswith("rccl"), (pick, rec)
+        assert rec["xgmi_ms_per_step"] is None and rec["xgmi_r5_ms_per_step"] is None, rec
+        assert rec["xgmi_resynced_from_rank0"] is True, rec
+    assert out[0][4] == out[1][4]  # the replicas agree again (rank 0's state)
