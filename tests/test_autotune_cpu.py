@@ -164,11 +164,11 @@ def _xc_worker(rank, world, port, scenario, q):
         dist.destroy_process_group()
 
 
-def _xc_race(scenario):
+def _xc_race(scenario, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_xc_worker, args=(r, 2, port, scenario, q)) for r in range(2)]
+    ps = [ctx.Process(target=_xc_worker, args=(r, world, port, scenario, q)) for r in range(world)]
     for p in ps:
         p.start()
     out = {}
@@ -211,11 +211,13 @@ def test_a_wrong_xgmi_step_on_one_rank_drops_the_candidates_everywhere():
         assert torch.equal(torch.tensor(params), p), rank
 
 
-@pytest.mark.timeout(180)
-def test_an_exchange_error_on_one_rank_resyncs_every_replica():
-    out = _xc_race("timeout")
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world", [2, 4])
+def test_an_exchange_error_on_one_rank_resyncs_every_replica(world):
+    out = _xc_race("timeout", world)
+    assert len(out) == world
     for rank, (pick, rec, cursor, staged, params) in out.items():
         assert pick.startswith("rccl"), (pick, rec)
         assert rec["xgmi_ms_per_step"] is None and rec["xgmi_r5_ms_per_step"] is None, rec
         assert rec["xgmi_resynced_from_rank0"] is True, rec
-    assert out[0][4] == out[1][4]  # the replicas agree again (rank 0's state)
+        assert params == out[0][4], rank  # the replicas agree again (rank 0's state)
