@@ -36,7 +36,9 @@ takes part in -- producer pushes, the fc tiles of the fused form, the slab reduc
 momentum -- at the job's own world size and geometry.
 
 ``PTO_RACE_DELAY_MS="<candidate>:<ms>"`` (fault injection for tests) adds ``ms`` per step of host
-sleep inside that candidate's timed trial.
+sleep inside that candidate's timed trial.  ``PTO_RACE_STALL="<candidate>:<rank>:<seconds>"`` makes
+that rank sleep before the candidate's timed trial, after its peers have started theirs (an xGMI
+candidate's peers then time out in the exchange: the resync path).
 """
 from __future__ import annotations
 
@@ -73,9 +75,18 @@ def _sync(device) -> None:
         torch.cuda.synchronize(device)
 
 
+def _stall(name: str) -> None:
+    spec = os.environ.get("PTO_RACE_STALL", "")
+    if spec.count(":") == 2:
+        k, r, sec = spec.split(":")
+        if k.strip() == name and int(r) == dist.get_rank():
+            time.sleep(float(sec))
+
+
 def _timed(runner: GraphedStep, steps: int, device, name: str) -> float:
     _sync(device)
     dist.barrier()
+    _stall(name)
     t0 = time.perf_counter()
     runner.warm(steps)
     delay = _delay_ms(name)

@@ -66,18 +66,24 @@ def test_bench_rccl_nranks_world1(tmp_path):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("allreduce", ["xgmi", "auto", "auto-slow-xgmi"])
+@pytest.mark.parametrize("allreduce", ["xgmi", "auto", "auto-slow-xgmi", "auto-xgmi-stall"])
 def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
     """``auto-slow-xgmi``: PTO_RACE_DELAY_MS makes the xGMI candidate slow, so the race must
-    pick RCCL, and the timed runner must then be the stream-launched RCCL step."""
+    pick RCCL, and the timed runner must then be the stream-launched RCCL step.
+    ``auto-xgmi-stall``: rank 1 sleeps past the exchange's 5 s wait before the xGMI trial, so
+    the exchange fails: both xGMI forms are dropped, the replicas resync from rank 0, the timed
+    steps run over RCCL in sync."""
     out = tmp_path / "bench.json"
     env = dict(os.environ, PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1")
+    slow_xgmi = stall = False
     if allreduce == "auto-slow-xgmi":
         env["PTO_RACE_DELAY_MS"] = "xgmi:5"
         allreduce = "auto"
         slow_xgmi = True
-    else:
-        slow_xgmi = False
+    elif allreduce == "auto-xgmi-stall":
+        env["PTO_RACE_STALL"] = "xgmi:1:6"
+        allreduce = "auto"
+        stall = True
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
            "--gpus", "2", "--backend", "gloo", "--allreduce", allreduce, "--steps", "20", "--warmup", "5",
@@ -97,6 +103,13 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
         # every candidate reported: RCCL stream-launched (not the 3-hipGraph form), xGMI timed,
         # the captured one-graph RCCL step skipped on gloo (its collectives are not capturable)
         assert trial["rccl_launch"] == "stream", trial
+        if stall:
+            assert trial["xgmi_crosscheck"]["xgmi"]["ok"], trial  # the stall comes after the check
+            assert trial["xgmi_ms_per_step"] is None and trial["xgmi_r5_ms_per_step"] is None, trial
+            assert trial["xgmi_resynced_from_rank0"] is True and trial["xgmi_error"] != 0, trial
+            assert trial["picked"] in ("rccl", "rccl-r5"), trial
+            assert line["job"]["result"] == "Succeeded", line["job"]
+            return
         assert trial["rccl_ms_per_step"] > 0 and trial["xgmi_ms_per_step"] > 0, trial
         assert trial["rccl_graph_ms_per_step"] is None and "gloo" in trial["rccl_graph_skipped"], trial
         assert line["config"]["grad_allreduce"] == trial["picked"], line
