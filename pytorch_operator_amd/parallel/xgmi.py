@@ -38,6 +38,20 @@ class XgmiUnavailable(RuntimeError):
     pass
 
 
+def physical_gpu(device: torch.device) -> tuple:
+    """The GPU behind ``device``, independent of the process's visible-device list: its PCI
+    (domain, bus, device) ids.  Pods that each see one GPU as ``cuda:0`` (the kubelet emulator's
+    ``HIP_VISIBLE_DEVICES``) then count as sharing a GPU only when they really do."""
+    try:
+        p = torch.cuda.get_device_properties(device)
+        bus = getattr(p, "pci_bus_id", None)
+        if bus is not None:
+            return ("pci", int(getattr(p, "pci_domain_id", 0)), int(bus), int(getattr(p, "pci_device_id", 0)))
+    except (RuntimeError, AssertionError, AttributeError):
+        pass
+    return ("index", device.index)
+
+
 class XgmiAllReduce:
     """Rank-local handle on the shared exchange buffers (world 2..8, one GPU per rank)."""
 
@@ -55,7 +69,7 @@ class XgmiAllReduce:
         self.n = int(n)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.prebarrier = False
-        where = (socket.gethostname(), self.device.index)
+        where = (socket.gethostname(),) + physical_gpu(self.device)
         peers = [None] * self.world
         dist.all_gather_object(peers, where, group=group)
         self.ranks_on_device = sum(1 for p in peers if p == where)

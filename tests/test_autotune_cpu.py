@@ -221,3 +221,8 @@ def test_an_exchange_error_on_one_rank_resyncs_every_replica(world):
         assert rec["xgmi_ms_per_step"] is None and rec["xgmi_r5_ms_per_step"] is None, rec
         assert rec["xgmi_resynced_from_rank0"] is True, rec
         assert params == out[0][4], rank  # the replicas agree again (rank 0's state)
+
+
+def test_physical_gpu_falls_back_to_the_index_without_a_gpu():
+    from pytorch_operator_amd.parallel.xgmi import physical_gpu
+    assert physical_gpu(torch.device("cuda", 3)) == ("index", 3)

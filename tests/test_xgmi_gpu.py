@@ -103,3 +103,19 @@ def test_xgmi_stall_makes_every_rank_exit_retryable(tmp_path):
     assert codes == [138, 138], "\n----\n".join(o[-2500:] for o in outs)
     for o in outs:
         assert '"event": "xgmi_error"' in o and '"path": "xgmi"' in o
+
+
+def test_physical_gpu_ignores_the_visible_device_list():
+    """Ranks decide whether they share a GPU by its PCI ids, not by their cuda index: a process
+    that sees the GPU through HIP_VISIBLE_DEVICES (an emulated pod's cuda:0) names the same GPU."""
+    import torch
+
+    from pytorch_operator_amd.parallel.xgmi import physical_gpu
+    here = physical_gpu(torch.device("cuda", 0))
+    assert here[0] == "pci", here
+    code = ("import json, torch; from pytorch_operator_amd.parallel.xgmi import physical_gpu; "
+            "print(json.dumps(physical_gpu(torch.device('cuda', 0))))")
+    env = dict(os.environ, PYTHONPATH=str(ROOT), HIP_VISIBLE_DEVICES="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert tuple(json.loads(r.stdout.strip().splitlines()[-1])) == here
