@@ -143,3 +143,31 @@ def test_bench_two_ranks_one_gpu(tmp_path, allreduce):
         (Path(rec) / f"bench_w2_{'slow-xgmi' if slow_xgmi else allreduce}.json").write_text(json.dumps(line))
     print(json.dumps({"world2_shared_gpu": {"create_to_first_step_s": line.get("create_to_first_step_s"),
                                              "startup_breakdown": bd, "allreduce": allreduce}}))
+
+
+@pytest.mark.timeout(300)
+def test_bench_four_ranks_one_gpu(tmp_path):
+    """The self-launched bench at world 4 on the box's one GPU, racing every candidate with the
+    step cross-check at four ranks.  One hardware queue per process: with HIP's default four, the
+    16 queues of four processes oversubscribe the GPU's scheduler, which then time-slices them
+    and an xGMI step waits milliseconds for a descheduled peer (45.6 vs 0.135 ms per step,
+    profiles/r6_w4/).  On the node every rank owns its GPU."""
+    out = tmp_path / "bench.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1", GPU_MAX_HW_QUEUES="1")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--backend", "gloo", "--steps", "20",
+           "--warmup", "5", "--job-latency", "0", "--json-out", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=ROOT, env=env)
+    assert r.returncode == 0 and out.exists(), r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 4 and line["world_size"] == 4, line
+    assert line["replicas_in_sync"] is True and line["grad_allreduce_error"] == 0, line
+    trial = line["config"]["allreduce_trial"]
+    cc = trial["xgmi_crosscheck"]
+    assert set(cc) == {"xgmi", "xgmi-r5"} and all(v["ok"] for v in cc.values()), cc
+    assert trial["xgmi_ms_per_step"] > 0 and trial["xgmi_r5_ms_per_step"] > 0, trial
+    assert line["config"]["grad_allreduce"] == trial["picked"], line
+    rec = os.environ.get("PTO_TEST_RECORD_DIR")
+    if rec:
+        Path(rec).mkdir(parents=True, exist_ok=True)
+        (Path(rec) / "bench_w4_one_gpu.json").write_text(json.dumps(line))
