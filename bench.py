@@ -417,7 +417,7 @@ def main(argv=None):
 
     # a bounded wait that timed out inside the xGMI kernel means the replicas went rank-local:
     # the number above is then not a DDP result (reported, and the exit code is 138)
-    ar_err = int(xgmi_error()) if ar_path == "xgmi" else 0
+    ar_err = int(xgmi_error()) if ar_path.startswith("xgmi") else 0  # both DDP forms (xgmi, xgmi-r5)
     in_sync = None
     if world > 1:
         # DDP invariant (checked after the timed region): every replica holds rank 0's weights

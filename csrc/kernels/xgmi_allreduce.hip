@@ -783,6 +783,33 @@ int pto_xar_open(void* ctx, const void* handles) {
   return 0;
 }
 
+// Restart the protocol after a failed exchange: zero this rank's header (flags, step counters,
+// pre-barrier words) and error word.  Collective: every rank calls it with no exchange in flight
+// on any rank (its caller synchronises and barriers before and after), so every rank's next
+// exchange starts from step 1 against peers that also do.
+int pto_xar_reset(void* ctx) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemset(c->base[c->rank], 0, kHdrBytes) != hipSuccess || hipMemset(c->err, 0, sizeof(int)) != hipSuccess)
+    return -2;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -2;
+}
+
+// Workgroups of this rank's exchange kernel (the fused-form one with fc != 0) that the device holds
+// at once, by the occupancy calculator: ranks sharing one GPU can only finish an exchange when
+// all of their exchange workgroups are resident together.
+int pto_xar_resident_blocks(void* ctx, int fc) {
+  XarCtx* c = static_cast<XarCtx*>(ctx);
+  const long shard4 = (c->npad >> 2) / c->world;
+  const bool one = shard4 / c->nblk <= kThreads;
+  const void* k = fc ? (one ? (const void*)xar_kernel_fc : (const void*)xar_kernel_fc_p2)
+                     : (one ? (const void*)xar_kernel : (const void*)xar_kernel_p2);
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) return -1;
+  return per_cu * cus;
+}
+
 int pto_xar_error(void* ctx) {
   XarCtx* c = static_cast<XarCtx*>(ctx);
   int v = 0;

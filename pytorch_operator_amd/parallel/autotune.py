@@ -170,6 +170,20 @@ def crosscheck_step(tr, rccl_sync, xgmi_sync, dev, rtol: float = 1e-4) -> Dict:
     return {"ok": ok, "param_err": pe, "mom_err": me, "xgmi_error": err}
 
 
+def _restart_exchange(tr, xgmi_sync, dev) -> None:
+    """After an xGMI exchange failed on any rank: zero every rank's protocol state, so the next
+    candidate gets a clean start, and restart all replicas from rank 0's parameters and momentum
+    (a timed-out exchange falls back to a rank-local SGD step, and the replicas drift apart)."""
+    _sync(dev)
+    dist.barrier()  # no exchange in flight on any rank
+    xgmi_sync.xar.reset()
+    xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
+    dist.broadcast(tr.flat_params, 0)
+    dist.broadcast(tr.flat_momentum, 0)
+    _sync(dev)
+    dist.barrier()  # every rank's protocol state zeroed before any rank's next exchange
+
+
 def _agree(flag: bool, dev) -> bool:
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -191,6 +205,8 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
     runners: Dict[str, GraphedStep] = {}
     skipped: Dict[str, str] = {}
     crosscheck: Dict[str, Dict] = {}
+    errors: Dict[str, int] = {}
+    resynced = False
     steps = 0
     # the RCCL steps keep momentum for every parameter: make it whole if fused xGMI steps ran
     # before (a no-op when it already is)
@@ -267,6 +283,11 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
             if name == "xgmi-r5" and _skip_listed(name):
                 skipped[name] = "PTO_RACE_SKIP"
                 continue
+            # ranks sharing one GPU finish an exchange only when all of their exchange workgroups
+            # are resident together (the one-GPU rehearsals; one rank per GPU always fits)
+            if not _agree(xgmi_sync.xar.fits_shared_gpu(fc=not forms[name]), dev):
+                skipped[name] = "its exchange workgroups of every rank sharing the GPU cannot be resident at once"
+                continue
             set_form(name)
             if os.environ.get("PTO_RACE_CROSSCHECK", "1") != "0":
                 chk = crosscheck_step(tr, rccl_sync, xgmi_sync, dev)
@@ -276,27 +297,22 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
                 if not chk["ok"]:
                     skipped[name] = (f"cross-check vs RCCL failed (param {chk['param_err']:.2e}, "
                                      f"momentum {chk['mom_err']:.2e}, exchange error {chk['xgmi_error']})")
+                    if not _agree(chk["xgmi_error"] == 0, dev):
+                        _restart_exchange(tr, xgmi_sync, dev)
                     continue
             r = GraphedStep(tr, mode="eager" if eager else "graph", steps_per_graph=spg, launch=launch)
             runners[name] = r
             t = _timed(r, trial, dev, name)
             steps += r.internal_steps + trial
-            times[name] = float("inf") if xgmi_sync.xar.error() else t
-    resynced = False
-    if xgmi_sync is not None:
-        # an exchange that timed out mid-trial may have stopped half-way on some ranks only: agree
-        # on it, drop both xGMI forms everywhere, and restart every replica from rank 0's state
-        bad = {n for n in ("xgmi", "xgmi-r5") if times.get(n) == float("inf")}
-        if not _agree(not bad, dev):
-            for n in ("xgmi", "xgmi-r5"):
-                if n in times:
-                    times[n] = float("inf")
-            xgmi_sync.xar.gather_sharded_(tr.flat_momentum)
-            _sync(dev)
-            dist.broadcast(tr.flat_params, 0)
-            dist.broadcast(tr.flat_momentum, 0)
-            _sync(dev)
-            resynced = True
+            # an exchange that timed out mid-trial may have stopped half-way on some ranks only:
+            # agree on it, drop the candidate everywhere, restart the protocol and the replicas
+            err = int(xgmi_sync.xar.error())
+            times[name] = t
+            if not _agree(err == 0, dev):
+                times[name] = float("inf")
+                errors[name] = err
+                _restart_exchange(tr, xgmi_sync, dev)
+                resynced = True
     if force is not None:
         if force not in runners:
             raise ValueError(f"force={force!r}: candidate not available ({skipped.get(force, 'unknown')})")
@@ -326,8 +342,8 @@ def choose_grad_sync(tr, rccl_sync, xgmi_sync=None, mode: str = "graph", spg: in
         record[f"{k.replace('-', '_')}_skipped"] = why
     if crosscheck:
         record["xgmi_crosscheck"] = crosscheck
-    if times.get("xgmi") == float("inf") or times.get("xgmi-r5") == float("inf"):
-        record["xgmi_error"] = int(xgmi_sync.xar.error())
+    if errors:
+        record["xgmi_error"] = errors  # this rank's error word per failed candidate (0: a peer's failed)
         record["xgmi_resynced_from_rank0"] = resynced
     record.update({"picked": pick, "rccl_launch": runners["rccl"].launch, "trial_steps": trial,
                    "steps": steps, "ddp_form": "r5" if forms[pick] else "fused"})

@@ -207,6 +207,21 @@ class XgmiAllReduce:
     def error(self) -> int:
         return int(self.lib.pto_xar_error(self._ctx))
 
+    def reset(self) -> None:
+        """Restart the protocol after a failed exchange: this rank's flags, step counters and error
+        word back to zero.  Collective -- every rank calls it while no exchange is in flight on
+        any rank (synchronise and barrier before and after; ``autotune._restart_exchange``)."""
+        _native.check(self.lib.pto_xar_reset(self._ctx), "pto_xar_reset")
+
+    def fits_shared_gpu(self, fc: bool) -> bool:
+        """Whether the exchange workgroups of every rank on this GPU can be resident at once (the
+        fused form's kernel with ``fc``).  Ranks sharing a GPU finish an exchange only then; one
+        rank per GPU always fits."""
+        if self.ranks_on_device <= 1:
+            return True
+        resident = int(self.lib.pto_xar_resident_blocks(self._ctx, 1 if fc else 0))
+        return resident >= self.ranks_on_device * self.nblk
+
     def set_prebarrier(self, on: bool = True) -> None:
         """Ranks sharing one GPU: a one-wave rank barrier before every later (or later-captured)
         exchange launch, so no rank's exchange spins on the CUs while a peer still runs its step

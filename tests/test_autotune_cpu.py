@@ -118,6 +118,12 @@ def _xc_worker(rank, world, port, scenario, q):
         def error(self):
             return self.err
 
+        def reset(self):
+            XSync.xar.err = 0
+
+        def fits_shared_gpu(self, fc):
+            return not (scenario == "nofit" and fc)
+
     class XSync(Sync):
         xar = Xar()
 
@@ -226,3 +232,12 @@ def test_an_exchange_error_on_one_rank_resyncs_every_replica(world):
 def test_physical_gpu_falls_back_to_the_index_without_a_gpu():
     from pytorch_operator_amd.parallel.xgmi import physical_gpu
     assert physical_gpu(torch.device("cuda", 3)) == ("index", 3)
+
+
+@pytest.mark.timeout(180)
+def test_a_fused_exchange_that_cannot_be_resident_is_skipped():
+    """Ranks sharing a GPU whose fused-form exchange workgroups cannot all be resident at once:
+    that form is skipped everywhere (it could only time out); the round-5 form still races."""
+    for rank, (pick, rec, cursor, staged, params) in _xc_race("nofit").items():
+        assert rec["xgmi_ms_per_step"] is None and "resident" in rec["xgmi_skipped"], rec
+        assert rec["xgmi_r5_ms_per_step"] is not None and set(rec["xgmi_crosscheck"]) == {"xgmi-r5"}, rec
