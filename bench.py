@@ -314,6 +314,7 @@ def main(argv=None):
     from pytorch_operator_amd.data.synthetic import make_synthetic_mnist
     ds = make_synthetic_mnist(args.dataset_size, seed=1 + rank, device=dev)
 
+    xgmi_note = []  # why the xGMI gradient path is not used (try_xgmi's log), for the JSON line
     if args.kernels == "hip":
         from pytorch_operator_amd.models.mnist import FusedMnistTrainer
         from pytorch_operator_amd.ops import mnist as K
@@ -327,8 +328,11 @@ def main(argv=None):
             from pytorch_operator_amd.parallel.xgmi import try_xgmi
             sync, ar_path = FlatGradAllReduce(force=force), "rccl"
             if args.allreduce != "rccl" and world > 1:
-                xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi",
-                              log=lambda m: print(m, file=sys.stderr) if rank == 0 else None)
+                def xgmi_log(m):  # why the xGMI path is not used, kept for the JSON line too
+                    xgmi_note.append(str(m)[:300])
+                    if rank == 0:
+                        print(m, file=sys.stderr)
+                xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi", log=xgmi_log)
         tr = FusedMnistTrainer(batch_size=B, source=src, lr=0.01, momentum=0.5, device=dev,
                                seed=1, grad_sync=sync)
         tr.fuse_conv12 = bool(args.fuse_conv12)
@@ -469,6 +473,7 @@ def main(argv=None):
             "grad_allreduce": ar_path,
             "forced_collectives": force,
             "allreduce_trial": tune,
+            "xgmi_note": "; ".join(xgmi_note) or None,
         },
     }
     if rank == 0:

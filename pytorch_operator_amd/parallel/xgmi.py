@@ -433,6 +433,9 @@ def try_xgmi(n: int, device, required: bool = False, log=print,
     latter keeps the start-up race against the gloo bucket path, ``--allreduce auto``)."""
     if not required and dist.get_backend() != "nccl" and os.environ.get("PTO_XGMI_ANY_BACKEND") != "1":
         return None
+    # PTO_XGMI_TIMEOUT_S: the exchange's bounded wait (crowded one-GPU rehearsals, where a rank
+    # sharing the host's CPUs with many others can arrive seconds late)
+    timeout_s = float(os.environ.get("PTO_XGMI_TIMEOUT_S", timeout_s))
     try:
         xar = XgmiAllReduce(n, device=device, timeout_s=timeout_s)
     except XgmiUnavailable as e:

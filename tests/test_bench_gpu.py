@@ -160,7 +160,10 @@ def test_bench_many_ranks_one_gpu(tmp_path, world):
     node every rank owns its GPU."""
     out = tmp_path / "bench.json"
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env.update(PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1", GPU_MAX_HW_QUEUES="1")
+    # two host threads per rank: the box's OMP_NUM_THREADS (16) in each of eight ranks oversubscribes
+    # its CPU share, and a descheduled rank can miss its peers' bounded exchange wait
+    env.update(PYTHONPATH=str(ROOT), PTO_XGMI_ANY_BACKEND="1", GPU_MAX_HW_QUEUES="1", OMP_NUM_THREADS="2",
+               PTO_XGMI_TIMEOUT_S="20")
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--backend", "gloo", "--steps", "20",
            "--warmup", "5", "--job-latency", "0", "--json-out", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=ROOT, env=env)
@@ -169,6 +172,7 @@ def test_bench_many_ranks_one_gpu(tmp_path, world):
     assert line["n_gpus"] == world and line["world_size"] == world, line
     assert line["replicas_in_sync"] is True and line["grad_allreduce_error"] == 0, line
     trial = line["config"]["allreduce_trial"]
+    assert trial is not None, (line["config"]["xgmi_note"], r.stderr[-3000:])
     cc = trial["xgmi_crosscheck"]
     assert all(v["ok"] for v in cc.values()) and trial["xgmi_r5_ms_per_step"] > 0, trial
     if world == 4:
