@@ -668,6 +668,7 @@ struct XarCtx {
   unsigned long long* stamps;  // optional diagnostics ring (pto_xar_stamps)
   int stamp_ring;
   int prebarrier;  // launch xar_prebarrier_kernel before every exchange (pto_xar_prebarrier)
+  int fence;       // -1: light fences iff the buffer is uncached; 0 / 1: forced (pto_xar_fence)
 };
 
 long round_up(long x, long m) { return (x + m - 1) / m * m; }
@@ -683,6 +684,7 @@ int pto_xar_create(int rank, int world, long n, int nblk, double timeout_s, void
       nblk < 1 || nblk > kMaxBlocks || n > (1L << 32))
     return -1;
   XarCtx* c = new XarCtx{};
+  c->fence = -1;
   c->rank = rank;
   c->world = world;
   c->nblk = nblk;
@@ -761,6 +763,15 @@ int pto_xar_stamps(void* ctx, unsigned long long* buf, int ring) {
   return 0;
 }
 
+// Diagnostics: force the release / acquire fences light (1: s_waitcnt + workgroup fence) or full
+// (0: system-scope fences with L2 writeback / invalidate); -1 restores the default (light iff the
+// buffer is uncached).  Applies to launches made (or captured) afterwards.
+int pto_xar_fence(void* ctx, int light) {
+  if (light < -1 || light > 1) return -1;
+  static_cast<XarCtx*>(ctx)->fence = light;
+  return 0;
+}
+
 // Ranks sharing one GPU: a one-wave rank barrier before every later (or later-captured) exchange
 // launch (xar_prebarrier_kernel).  Off by default: one rank per GPU never needs it.
 int pto_xar_prebarrier(void* ctx, int on) {
@@ -830,7 +841,7 @@ static int launch(XarCtx* c, XarArgs& a, void* stream) {
   a.timeout_ticks = c->timeout_ticks;
   a.stamps = c->stamps;
   a.stamp_ring = c->stamp_ring;
-  a.light_fence = c->alloc_kind == (int)hipDeviceMallocUncached;
+  a.light_fence = c->fence >= 0 ? c->fence : c->alloc_kind == (int)hipDeviceMallocUncached;
   if ((((uintptr_t)a.in) | ((uintptr_t)a.out) | ((uintptr_t)a.p) | ((uintptr_t)a.mbuf)) & 15) return -2;
   if (c->prebarrier) {
     hipLaunchKernelGGL(xar_prebarrier_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);

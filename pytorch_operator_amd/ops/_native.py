@@ -153,6 +153,7 @@ _SIGNATURES = {
     "pto_xar_stamps": [_VP, _VP, _I],
     "pto_xar_prebarrier": [_VP, _I],
     "pto_xar_reset": [_VP],
+    "pto_xar_fence": [_VP, _I],
     "pto_xar_resident_blocks": [_VP, _I],
     "pto_xar_alloc_kind": [_VP],
     "pto_xar_allreduce": [_VP, _VP, _VP, _F, _VP],

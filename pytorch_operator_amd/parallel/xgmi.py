@@ -105,6 +105,10 @@ class XgmiAllReduce:
         self.npad = int(self.lib.pto_xar_npad(self._ctx))
         if self.crowded:
             self.set_prebarrier(True)
+        # PTO_XAR_FENCE=full|light (diagnostics): force the exchange's fence flavour
+        fence = {"full": 0, "light": 1}.get(os.environ.get("PTO_XAR_FENCE", ""), -1)
+        if fence >= 0:
+            _native.check(self.lib.pto_xar_fence(self._ctx, fence), "pto_xar_fence")
 
     # ------------------------------------------------------------------ ops
     def _stream(self):
