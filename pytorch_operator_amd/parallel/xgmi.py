@@ -259,10 +259,16 @@ class XgmiAllReduce:
         report = []
         g = torch.Generator(device="cpu").manual_seed(seed + self.rank)
         for i in range(steps):
-            x = torch.randn(self.n, generator=g).to(self.device)
+            xc = torch.randn(self.n, generator=g)
+            x = xc.to(self.device)
             ref = x.clone()
             dist.all_reduce(ref, group=self.group)  # collectives first: never skipped by a failure
             ref /= self.world
+            # every rank's input, to tell which side is off when a check fails: host tensors over
+            # gloo (not its GPU-tensor path, which the reference above takes), device ones otherwise
+            host = dist.get_backend(self.group) == "gloo"
+            xs = [torch.empty(self.n) if host else torch.empty_like(x) for _ in range(self.world)]
+            dist.all_gather(xs, xc if host else x, group=self.group)
             try:
                 out = torch.empty_like(x)
                 self.allreduce_mean(x, out)
@@ -279,10 +285,13 @@ class XgmiAllReduce:
                 errs = {"mean": float((out - ref).abs().max()), "param": float((p - p_ref).abs().max()),
                         "momentum": float((buf[lo:hi] - ref[lo:hi]).abs().max()) if hi > lo else 0.0}
                 bad = {k: v for k, v in errs.items() if not v <= 1e-5}
-                if bad:
+                if bad:  # both sides against the float64 mean of every rank's input
+                    truth = torch.stack([t.cpu() for t in xs]).double().mean(0).float()
                     ok = False
                     idx = int((out - ref).abs().argmax())
-                    report.append({"step": i, **bad, "argmax_mean": idx})
+                    report.append({"step": i, **bad, "argmax_mean": idx,
+                                   "xgmi_vs_host_mean": float((out.cpu() - truth).abs().max()),
+                                   "gloo_vs_host_mean": float((ref.cpu() - truth).abs().max())})
             except Exception as e:  # noqa: BLE001 -- any failure means "do not use this path"
                 ok = False
                 report.append({"step": i, "exception": repr(e)})

@@ -21,6 +21,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--n", type=int, default=431080)
+    ap.add_argument("--discriminate", action="store_true",
+                    help="check the exchange and gloo's GPU-tensor all_reduce separately against a host float64 mean")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -32,8 +34,31 @@ def main() -> int:
     n = a.n - a.n % 4
     xar = XgmiAllReduce(n, device=dev, timeout_s=float(os.environ.get("PTO_XGMI_TIMEOUT_S", "20")))
     t0 = time.perf_counter()
-    ok = xar.self_test(steps=a.steps)
-    rep = xar.last_report
+    if a.discriminate:
+        # per step: the exchange's mean and gloo's all_reduce of the GPU tensor, each against the
+        # float64 mean of every rank's input gathered on the host (CPU tensors through gloo)
+        g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+        rep = []
+        for i in range(a.steps):
+            xc = torch.randn(n, generator=g)
+            x = xc.to(dev)
+            xs = [torch.empty(n) for _ in range(world)]
+            dist.all_gather(xs, xc)
+            truth = torch.stack(xs).double().mean(0).float()
+            ref = x.clone()
+            dist.all_reduce(ref)
+            ref /= world
+            out = torch.empty_like(x)
+            xar.allreduce_mean(x, out)
+            torch.cuda.synchronize(dev)
+            e_x = float((out.cpu() - truth).abs().max())
+            e_ref = float((ref.cpu() - truth).abs().max())
+            if e_x > 1e-5 or e_ref > 1e-5:
+                rep.append({"step": i, "xgmi_err": e_x, "gloo_err": e_ref})
+        ok = not rep
+    else:
+        ok = xar.self_test(steps=a.steps)
+        rep = xar.last_report
     print(json.dumps({"rank": rank, "world": world, "ok": ok, "failed_steps": [r.get("step") for r in rep][:40],
                       "first": rep[:2], "error": xar.error(), "alloc_kind": xar.alloc_kind,
                       "fence": os.environ.get("PTO_XAR_FENCE", "default"), "prebarrier": xar.prebarrier,
