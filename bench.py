@@ -329,7 +329,7 @@ def main(argv=None):
             sync, ar_path = FlatGradAllReduce(force=force), "rccl"
             if args.allreduce != "rccl" and world > 1:
                 def xgmi_log(m):  # why the xGMI path is not used, kept for the JSON line too
-                    xgmi_note.append(str(m)[:300])
+                    xgmi_note.append(str(m)[:1200])
                     if rank == 0:
                         print(m, file=sys.stderr)
                 xg = try_xgmi(flat_layout().total, dev, required=args.allreduce == "xgmi", log=xgmi_log)
