@@ -24,6 +24,7 @@ falls back to RCCL (``FlatGradAllReduce``).
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 import socket
 from typing import Optional
@@ -258,6 +259,11 @@ class XgmiAllReduce:
         ok = True
         report = []
         g = torch.Generator(device="cpu").manual_seed(seed + self.rank)
+        # diagnostics: PTO_XAR_SELFTEST_STAMPS=<dir> keeps every launch's per-block stamps (step,
+        # wall-clock phases, error word) and writes them there as rank<r>.json after the test
+        stamp_dir = os.environ.get("PTO_XAR_SELFTEST_STAMPS")
+        if stamp_dir:
+            self.enable_stamps(ring=2 * steps)
         for i in range(steps):
             xc = torch.randn(self.n, generator=g)
             x = xc.to(self.device)
@@ -303,6 +309,10 @@ class XgmiAllReduce:
             ok = False
             report.append({"exception": repr(e)})
         self.last_report = report
+        if stamp_dir:
+            os.makedirs(stamp_dir, exist_ok=True)
+            with open(os.path.join(stamp_dir, f"rank{self.rank}.json"), "w") as f:
+                json.dump({"rank": self.rank, "report": report, "stamps": self.stamps.cpu().tolist()}, f)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item())
@@ -458,7 +468,8 @@ def try_xgmi(n: int, device, required: bool = False, log=print,
         return None
     if xar.self_test():
         return XgmiGradSync(xar)
-    log(f"xgmi all-reduce self-test failed ({xar.last_report[:2]}); using RCCL")
+    errs = [r for r in xar.last_report if "kernel_error" in r or "exception" in r]
+    log(f"xgmi all-reduce self-test failed ({errs + xar.last_report[:2]}); using RCCL")
     xar.close()
     if required:
         raise XgmiUnavailable("xgmi path requested but its self-test failed")
