@@ -625,8 +625,9 @@ __global__ __launch_bounds__(64) void xar_prebarrier_kernel(XarArgs a) {
   if (lane < a.world) store_sys(pb_flag(peer(a, lane), a.rank), s);
   const long long deadline = (long long)wall_clock64() + a.timeout_ticks;
   bool pending = lane < a.world;
-  while (__any(pending)) {
+  for (;;) {
     if (pending) pending = load_sys(pb_flag(mine, lane)) < s;
+    if (!__any(pending)) break;  // before the deadline check: a barrier met as it expires is met
     if ((long long)wall_clock64() > deadline) {
       if (lane == 0) atomicOr(a.err, kErrPreBarrier);
       break;
